@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Headline benchmark: batched qEI forward (q x restarts x MC evals/s) on MI355X.
+
+Workload (BASELINE.json metric, SURVEY.md section 8 config C3 at N=1):
+SingleTaskGP on Hartmann6, n=4096, d=6, fp64, Standardize; qExpectedImprovement
+with q=16, 512 restarts (t-batches) per GPU, 512 Sobol-QMC samples.  A "step" is
+one acquisition forward over the whole batch: fused kernel-row build + R = K*x
+L^{-T} GEMM + R R^T epilogue (post_partials), then per-t-batch finalisation,
+jittered q x q Cholesky, reparameterised sampling and the MC reduction
+(qmc_finalize), then the cross-rank argmax (one all-reduce).  Model caches
+(Cholesky, L^{-T}) are built once before timing, as the reference builds them
+on the first eval-mode call.
+
+Multi-GPU: one process per GPU (torchrun), each rank evaluates its own 512
+restarts (weak scaling, no data-path collective); the step ends with one
+all-reduce(MAX) of the best acquisition value (the argmax/gather of
+optimize_acqf, botorch/optim/optimize.py:384-387).
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+N_TRAIN, D, Q, RESTARTS, MC = 4096, 6, 16, 512, 512
+# Fixed hyperparameters for acquisition timing (the BoTorch defaults' modes:
+# lengthscale LogNormal mode 0.5016 at d=6, noise exp(-5)) -- see DESIGN.md.
+LENGTHSCALE, NOISE, CONSTANT = 0.5016, 6.737947e-3, 0.0
+
+
+def _dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def flops_post_partials(B, q, n, nrows_pad, nC):
+    """Algorithmic flops of one post_partials launch:
+    triangular R = K*x L^{-T}: (B q) n^2; R R^T diagonal blocks: 2 B q^2 n;
+    R beta: 2 B q n; kernel rows: B q n (3 d + 3)."""
+    return B * q * n * n + 2 * B * q * q * n + 2 * B * q * n + B * q * n * (3 * D + 3)
+
+
+def cpu_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except Exception:
+        return os.cpu_count()
+
+
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return platform.processor()
+
+
+def build_problem(device, restarts, seed_offset=0):
+    from botorch_amd.test_functions import Hartmann
+    from botorch_amd.utils_sampling import draw_sobol_samples
+    lo = torch.zeros(D, dtype=torch.float64)
+    hi = torch.ones(D, dtype=torch.float64)
+    Xtr = draw_sobol_samples(torch.stack([lo, hi]), N_TRAIN, 1, seed=0).squeeze(1)
+    Ytr = Hartmann(dim=6, negate=True)(Xtr).unsqueeze(-1)
+    Xc = draw_sobol_samples(torch.stack([lo, hi]), restarts, Q, seed=1 + seed_offset)
+    return Xtr, Ytr, Xc
+
+
+def cpu_baseline(Xtr, Ytr, Xc, best_f, budget_s=20.0):
+    """The reference-equivalent CPU restatement (oracle/, torch fp64 on the host
+    cores) timed on a bounded sample of the same workload."""
+    from oracle.acquisition import qei
+    from oracle.gp import ExactGPOracle, GPHyper
+    from oracle.sampling import draw_sobol_normal_samples
+    torch.set_num_threads(cpu_cores())
+    h = GPHyper(torch.full((D,), LENGTHSCALE, dtype=torch.float64), NOISE, CONSTANT)
+    model = ExactGPOracle(Xtr, Ytr, h)
+    Z = draw_sobol_normal_samples(Q, MC, 0)
+    b = 64
+    Xs = Xc[:b]
+    qei(model, Xs, Z, best_f)  # warm-up
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < 5 or (time.perf_counter() - t_start < budget_s and len(times) < 50):
+        t0 = time.perf_counter()
+        qei(model, Xs, Z, best_f)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s and len(times) >= 2:
+            break
+    times.sort()
+    med = times[len(times) // 2]
+    return {
+        "value": b * Q * MC / med,
+        "unit": "acq-evals/s",
+        "cores": torch.get_num_threads(),
+        "kind": "port",
+        "sample": f"qEI forward, {b} of the {RESTARTS} restarts (q={Q}, S={MC}, n={N_TRAIN}, "
+                  f"fp64), median of {len(times)} runs; torch fp64 CPU restatement (oracle/), "
+                  f"{cpu_model()}",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    ws, rank, local = _dist_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if ws > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from botorch_amd import _lib, kernels
+    from botorch_amd.models import SingleTaskGP
+
+    Xtr, Ytr, Xc = build_problem(dev, RESTARTS, seed_offset=rank)
+    best_f = Ytr.max().item()
+    model = SingleTaskGP(Xtr.to(dev), Ytr.to(dev))
+    model.covar_module.lengthscale = torch.full((1, D), LENGTHSCALE, dtype=torch.float64)
+    model.likelihood.noise = torch.tensor([NOISE], dtype=torch.float64)
+    model.mean_module.constant = torch.tensor(CONSTANT, dtype=torch.float64)
+    model.eval()
+    cache = model.prediction_cache()
+    ymean, ystd = model.outcome_stats()
+    Z = kernels.sobol_normal(Q, MC, 0, dev)
+    Xd = Xc.to(dev)
+
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    best = torch.empty(1, dtype=torch.float64, device=dev)
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        pp = kernels.post_partials(cache, Xd)
+        if i is not None:
+            ev[i][1].record(stream)
+        out = kernels.qmc_finalize(cache, pp, _lib.QMC_QEI, ymean, ystd, Z=Z, best_f=best_f,
+                                   want_mean=False, want_cov=False)
+        torch.max(out["acq"], dim=0, out=(best, torch.empty(1, dtype=torch.int64, device=dev).squeeze(0)))
+        if dist is not None:
+            dist.all_reduce(best, op=dist.ReduceOp.MAX)
+        return out, pp
+
+    for _ in range(args.warmup):
+        out, pp = step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out, pp = step(i)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms_step = 1e3 * elapsed / args.steps
+    evals_per_step = Q * RESTARTS * MC * ws
+    value = evals_per_step * args.steps / elapsed
+
+    kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
+    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    fl = flops_post_partials(RESTARTS, Q, N_TRAIN, pp.nrows_pad, pp.nC)
+    achieved = fl / (kern_avg_ms * 1e-3) / 1e12
+    peak = 78.6  # MI355X dense FP64 matrix TFLOP/s (MI355X_MICROARCH.md / SURVEY.md 8(d))
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and ws == 1:
+            cpu = cpu_baseline(Xtr, Ytr, Xc, best_f)
+        line = {
+            "metric": "acq-evals/sec (q x restarts x MC), qEI forward",
+            "value": value,
+            "unit": "acq-evals/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: Hartmann6 on Sobol(seed 0) training inputs, Sobol(seed 1+rank) candidates",
+            "config": {"workload": "C3 qEI forward: SingleTaskGP n=4096 d=6, q=16, "
+                                   "512 restarts/GPU, 512 Sobol MC samples",
+                       "n": N_TRAIN, "d": D, "q": Q, "restarts_per_gpu": RESTARTS, "mc": MC,
+                       "parallelism": f"restart-sharded x{ws}"},
+            "roofline": {"bound": "mfma", "kernel": "post_partials_kernel",
+                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": None,
+                         "kernel_ms": kern_avg_ms, "flops_per_launch": fl},
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["speedup_vs_cpu"] = value / cpu["value"]
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

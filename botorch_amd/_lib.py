@@ -1,0 +1,93 @@
+"""ctypes binding of the C ABI in ``include/botorch_amd.h``.
+
+This is the "reference-side FFI" of the drop-in boundary: plain pointers and
+sizes go in, status codes come out.  The library is built in-tree
+(``make`` -> ``botorch_amd/libbotorch_amd.so``) and there is deliberately no
+fallback: if it is missing, every GPU entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_int, c_int64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libbotorch_amd.so")
+
+BO_OK, BO_ERR_ARG, BO_ERR_HIP, BO_ERR_NOT_PSD, BO_ERR_NAN = 0, 1, 2, 3, 4
+RBF, MATERN52 = 0, 1
+GEMM_LOWER_C, GEMM_A_LOWER, GEMM_B_UPPER, GEMM_A_UPPER, GEMM_B_LOWER = 1, 2, 4, 8, 16
+QMC_POSTERIOR, QMC_QEI, QMC_QNEI, QMC_CHOL = 0, 1, 2, 3
+
+_P = c_void_p  # device pointers travel as void*
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "bo_last_error": (ctypes.c_char_p, []),
+    "bo_version": (c_int, []),
+    "bo_probe_mfma_f64_layout": (c_int, [_P, _P]),
+    "bo_gemm_f64": (c_int, [c_int, c_int, c_int, c_int, c_int, c_double, _P, c_int64, c_int64,
+                            _P, c_int64, c_int64, c_double, _P, c_int64, c_int64, c_int, c_int,
+                            _P]),
+    "bo_covar_matrix": (c_int, [c_int, _P, c_int64, _P, c_int64, c_int, _P, c_double, c_double,
+                                c_int, _P, c_int64, c_int64, c_int64, _P]),
+    "bo_padded_order": (c_int64, [c_int64]),
+    "bo_cholesky_inverse": (c_int, [_P, _P, _P, c_int64, _P, _P]),
+    "bo_transpose": (c_int, [_P, _P, c_int64, c_int64, _P]),
+    "bo_gemv": (c_int, [_P, c_int64, c_int64, _P, c_double, _P, _P]),
+    "bo_scale_inputs": (c_int, [_P, c_int64, c_int, _P, _P, c_int, _P, _P]),
+    "bo_gp_cache_build": (c_int, [c_int, _P, c_int64, c_int, _P, c_double, c_double, c_double,
+                                  _P, _P, _P, _P, _P, _P, c_int, c_double, POINTER(c_double),
+                                  _P, _P]),
+    "bo_post_geometry": (c_int, [c_int64, c_int, c_int64, POINTER(c_int), POINTER(c_int),
+                                 POINTER(c_int)]),
+    "bo_prepare_rows": (c_int, [_P, c_int, c_int, c_int, _P, _P, _P]),
+    "bo_post_partials": (c_int, [c_int, _P, c_int, c_int, _P, c_int64, _P, c_int64, _P,
+                                 c_double, _P, _P, _P]),
+    "bo_qmc_finalize": (c_int, [c_int, c_int, c_int, c_int, _P, _P, _P, c_int64, c_double,
+                                c_double, c_double, c_double, _P, c_int, c_double, _P, c_int,
+                                c_double, _P, _P, _P, _P, _P, _P, _P]),
+    "bo_sobol_normal": (c_int, [_P, _P, c_int, c_int64, c_int64, _P, _P]),
+}
+
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the native library; raise loudly if absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryMissing(
+                f"{LIB_PATH} not found: build it with `make` (or __graft_entry__.build()). "
+                "botorch_amd has no CPU fallback.")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGNATURES)
+
+
+def check(status: int, what: str = "") -> None:
+    """Map a C-ABI status to the reference's exception taxonomy."""
+    if status == BO_OK:
+        return
+    from .exceptions import NanError, NotPSDError
+    msg = lib().bo_last_error().decode(errors="replace")
+    if status == BO_ERR_NOT_PSD:
+        raise NotPSDError(msg)
+    if status == BO_ERR_NAN:
+        raise NanError(msg)
+    if status == BO_ERR_ARG:
+        raise ValueError(f"{what}: {msg}")
+    raise RuntimeError(f"{what}: HIP error: {msg}")

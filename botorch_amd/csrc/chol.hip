@@ -1,0 +1,330 @@
+// Exact-GP training caches on gfx950: kernel matrix, blocked Cholesky with the
+// reference's jitter ladder, explicit triangular inverse, and the two solves.
+//
+// Replaces, for the exact-prediction path of SingleTaskGP
+// (botorch/models/gpytorch.py:446 -> [G] DefaultPredictionStrategy):
+//   L          = psd_safe_cholesky(K + s2 I)         (jitter 1e-8 * 10^i, 6 tries,
+//                                                     botorch/__init__.py:47)
+//   covar_cache = L^{-T}                               (root_inv_decomposition,
+//                                                     fast_covar_root_decomposition
+//                                                     off, botorch/__init__.py:44)
+//   mean_cache  = (K + s2 I)^{-1} (y - c)
+// The mean is later formed as R beta with beta = L^{-1}(y - c)  (K*x alpha =
+// K*x L^{-T} L^{-1} (y - c) = R beta), so beta is cached beside alpha.
+//
+// Layout in HBM: every n x n cache is stored row-major at the padded order
+// np = roundup(n, 128) with an identity pad, so the 64-wide diagonal blocks of
+// the right-looking factorisation never straddle the edge.
+#include <cstdarg>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+#include "gemm.h"
+
+namespace {
+
+constexpr int NB = 32;   // diagonal block (one wave factors it, fully unrolled)
+constexpr int NBO = 128; // outer panel: the trailing SYRK runs once per 128 columns
+
+// K[i][j] = outputscale * k(x_i, x_j) (+ diag_add on i == j), row-major with
+// leading dimension ldk, over a `rows x cols` padded extent (identity pad).
+// mode bit 1: zero the strict upper triangle (Cholesky input).
+template <int KIND>
+__global__ __launch_bounds__(256) void covar_matrix_kernel(
+    const double* __restrict__ X1, int64_t n1, const double* __restrict__ X2, int64_t n2,
+    int d, const double* __restrict__ ls, double outputscale, double diag_add, int mode,
+    double* __restrict__ K, int64_t ldk, int64_t rows, int64_t cols) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (j >= cols || i >= rows) return;
+  double v;
+  if (i >= n1 || j >= n2) {
+    v = (i == j) ? 1.0 : 0.0;
+  } else if ((mode & 1) && j > i) {
+    v = 0.0;
+  } else {
+    double d2 = 0.0;
+    for (int t = 0; t < d; ++t) {
+      const double diff = (X1[i * d + t] - X2[j * d + t]) / ls[t];
+      d2 = fma(diff, diff, d2);
+    }
+    v = outputscale * kernel_from_d2<KIND>(d2);
+    if (i == j) v += diag_add;
+  }
+  K[i * ldk + j] = v;
+}
+
+// Factor the NB x NB diagonal block at (k0, k0) of the lower-stored matrix A
+// in place (one wave, one row per lane, column j broadcast through LDS) and
+// write its inverse into the same block of Linv.  A non-positive or NaN pivot
+// records info = k0 + j + 1 (1-based order of the failing leading minor, as
+// torch.linalg.cholesky_ex) for the first failing panel.
+// Launched with NB threads (half a wave; the upper lanes stay masked off).
+__global__ __launch_bounds__(NB) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
+                                                         int64_t k0, double* __restrict__ Linv,
+                                                         int64_t ldi, int* __restrict__ info) {
+  __shared__ double col[NB];
+  __shared__ double Ls[NB][NB + 1];
+  const int i = threadIdx.x;
+  double a[NB];
+  const double* row = A + (k0 + i) * lda + k0;
+#pragma unroll
+  for (int l = 0; l < NB; ++l) a[l] = (l <= i) ? row[l] : 0.0;
+
+  int fail = 0;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const double ajj = __shfl(a[j], j);
+    if (!(ajj > 0.0) && fail == 0) fail = j + 1;
+    const double djj = sqrt(ajj);
+    double lij = a[j] / djj;
+    if (i == j) lij = djj;
+    if (i < j) lij = 0.0;
+    a[j] = lij;
+    col[i] = lij;
+    __syncthreads();
+#pragma unroll
+    for (int l = j + 1; l < NB; ++l) a[l] = fma(-lij, col[l], a[l]);
+    __syncthreads();
+  }
+  if (fail && i == 0) atomicCAS(info, 0, (int)(k0 + fail));
+
+  double* out = A + (k0 + i) * lda + k0;
+#pragma unroll
+  for (int l = 0; l < NB; ++l) {
+    const double v = (l <= i) ? a[l] : 0.0;
+    out[l] = v;
+    Ls[i][l] = v;
+  }
+  __syncthreads();
+  // Column c = lane of X = L^{-1}: forward substitution, L rows broadcast from LDS.
+  const int c = i;
+  double x[NB];
+#pragma unroll
+  for (int r = 0; r < NB; ++r) {
+    double s = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < r; ++k) s = fma(-Ls[r][k], x[k], s);
+    x[r] = s / Ls[r][r];
+  }
+#pragma unroll
+  for (int r = 0; r < NB; ++r) Linv[(k0 + r) * ldi + k0 + c] = (r >= c) ? x[r] : 0.0;
+}
+
+__global__ void transpose_kernel(const double* __restrict__ A, double* __restrict__ B,
+                                 int64_t n, int64_t ld) {
+  __shared__ double tile[32][33];
+  const int64_t bx = blockIdx.x * 32, by = blockIdx.y * 32;
+  const int tx = threadIdx.x, ty = threadIdx.y;  // 32 x 8
+  for (int r = ty; r < 32; r += 8) {
+    const int64_t gi = by + r, gj = bx + tx;
+    tile[r][tx] = (gi < n && gj < n) ? A[gi * ld + gj] : 0.0;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int64_t gi = bx + r, gj = by + tx;
+    if (gi < n && gj < n) B[gi * ld + gj] = tile[tx][r];
+  }
+}
+
+// y = op(M) x (+ shift), one wave per output row.  trans: use M^T.
+__global__ __launch_bounds__(256) void gemv_kernel(const double* __restrict__ M, int64_t ld,
+                                                   int64_t n, const double* __restrict__ x,
+                                                   double xshift, double* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  double s = 0.0;
+  for (int64_t k = lane; k < n; k += 64) s = fma(M[row * ld + k], x[k] - xshift, s);
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) y[row] = s;
+}
+
+__global__ void scale_inputs_kernel(const double* __restrict__ X, int64_t n, int d,
+                                    const double* __restrict__ ls, const double* __restrict__ center,
+                                    int dp, double* __restrict__ Xs) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * dp) return;
+  const int64_t i = idx / dp;
+  const int t = (int)(idx % dp);
+  Xs[idx] = (t < d) ? (X[i * d + t] - (center ? center[t] : 0.0)) / ls[t] : 0.0;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+thread_local char g_err[512];
+void bo_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+extern "C" {
+
+const char* bo_last_error(void) { return g_err; }
+
+int bo_version(void) { return BO_ABI_VERSION; }
+
+// 128 = the fused posterior kernel's column tile (post.hip), a multiple of NB.
+int64_t bo_padded_order(int64_t n) { return ceil_div(n, 128) * 128; }
+
+int bo_covar_matrix(int kind, const double* X1, int64_t n1, const double* X2, int64_t n2,
+                    int d, const double* lengthscale, double outputscale, double diag_add,
+                    int mode, double* K, int64_t ldk, int64_t rows, int64_t cols, void* stream) {
+  BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bo_covar_matrix: bad kind %d", kind);
+  BO_CHECK_ARG(d > 0 && ldk >= cols && rows >= n1 && cols >= n2, "bo_covar_matrix: bad shape");
+  if (rows == 0 || cols == 0) return BO_OK;
+  dim3 grid((unsigned)ceil_div(cols, 256), (unsigned)rows);
+  hipStream_t st = as_stream(stream);
+  if (kind == BO_RBF)
+    covar_matrix_kernel<BO_RBF><<<grid, 256, 0, st>>>(X1, n1, X2, n2, d, lengthscale, outputscale, diag_add, mode, K, ldk, rows, cols);
+  else
+    covar_matrix_kernel<BO_MATERN52><<<grid, 256, 0, st>>>(X1, n1, X2, n2, d, lengthscale, outputscale, diag_add, mode, K, ldk, rows, cols);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+int bo_gemm_f64(int ta, int tb, int M, int N, int K, double alpha, const double* A, int64_t lda,
+                int64_t sA, const double* B, int64_t ldb, int64_t sB, double beta, double* C,
+                int64_t ldc, int64_t sC, int batch, int flags, void* stream) {
+  return bo_gemm_f64_impl(ta, tb, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
+                          batch, flags, as_stream(stream));
+}
+
+int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* info,
+                        void* stream) {
+  BO_CHECK_ARG(np > 0 && np % NB == 0, "bo_cholesky_inverse: order %lld not a multiple of %d",
+               (long long)np, NB);
+  hipStream_t st = as_stream(stream);
+  BO_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
+  BO_HIP(hipMemsetAsync(Linv, 0, sizeof(double) * np * np, st));
+  // Two-level right-looking factorisation.  Inside each 128-column outer
+  // panel: factor a 32 x 32 diagonal block (one wave), solve the rows below
+  // it as a GEMM against the block's inverse, and update only the rest of
+  // the outer panel; then one lower-triangle SYRK (K = 128) updates the
+  // trailing matrix, so the trailing matrix streams through HBM np/128
+  // times instead of np/32.
+  for (int64_t K0 = 0; K0 < np; K0 += NBO) {
+    const int64_t Kend = K0 + NBO < np ? K0 + NBO : np;
+    for (int64_t k0 = K0; k0 < Kend; k0 += NB) {
+      potrf_diag_kernel<<<1, NB, 0, st>>>(A, np, k0, Linv, np, info);
+      BO_LAUNCH_CHECK();
+      const int64_t rem = np - k0 - NB;
+      if (rem <= 0) break;
+      double* P = A + (k0 + NB) * np + k0;       // rem x NB panel
+      const double* Dinv = Linv + k0 * np + k0;  // NB x NB lower
+      // P <- P * Dinv^T  (in place: each workgroup reads its rows fully first)
+      int s = bo_gemm_f64_impl(0, 1, (int)rem, NB, NB, 1.0, P, np, 0, Dinv, np, 0, 0.0, P, np,
+                               0, 1, BO_GEMM_B_UPPER, st);
+      if (s) return s;
+      const int64_t inner = Kend - (k0 + NB);  // columns left in this outer panel
+      if (inner > 0) {
+        double* Ain = A + (k0 + NB) * np + (k0 + NB);
+        s = bo_gemm_f64_impl(0, 1, (int)rem, (int)inner, NB, -1.0, P, np, 0, P, np, 0, 1.0, Ain,
+                             np, 0, 1, BO_GEMM_LOWER_C, st);
+        if (s) return s;
+      }
+    }
+    const int64_t rem = np - Kend;
+    if (rem <= 0) break;
+    double* Pb = A + Kend * np + K0;  // rem x 128
+    double* A22 = A + Kend * np + Kend;
+    int s = bo_gemm_f64_impl(0, 1, (int)rem, (int)rem, (int)(Kend - K0), -1.0, Pb, np, 0, Pb, np,
+                             0, 1.0, A22, np, 0, 1, BO_GEMM_LOWER_C, st);
+    if (s) return s;
+  }
+  // Triangular inverse by recursive doubling over the inverted diagonal
+  // blocks:  [L11 0; L21 L22]^{-1} = [X11 0; -X22 L21 X11  X22].
+  for (int64_t sz = NB; sz < np; sz *= 2) {
+    const int64_t stride = 2 * sz;
+    const int64_t full = np / stride;          // pairs with a full-size second block
+    const int64_t tail_r2 = full * stride + sz;  // second block start of a ragged pair
+    for (int pass = 0; pass < 2; ++pass) {
+      int64_t npairs, r1, t;
+      if (pass == 0) { npairs = full; r1 = 0; t = sz; }
+      else {
+        if (tail_r2 >= np) break;
+        npairs = 1; r1 = full * stride; t = np - tail_r2;
+      }
+      if (npairs == 0) continue;
+      const int64_t r2 = r1 + sz;
+      const int64_t sBlk = stride * (np + 1);  // diagonal step between pairs
+      // T = L21 * X11     (t x sz)
+      int s = bo_gemm_f64_impl(0, 0, (int)t, (int)sz, (int)sz, 1.0, A + r2 * np + r1, np, sBlk,
+                               Linv + r1 * np + r1, np, sBlk, 0.0, work, sz, t * sz, (int)npairs,
+                               BO_GEMM_B_LOWER, st);
+      if (s) return s;
+      // X21 = -X22 * T     (t x sz)
+      s = bo_gemm_f64_impl(0, 0, (int)t, (int)sz, (int)t, -1.0, Linv + r2 * np + r2, np, sBlk,
+                           work, sz, t * sz, 0.0, Linv + r2 * np + r1, np, sBlk, (int)npairs,
+                           BO_GEMM_A_LOWER, st);
+      if (s) return s;
+    }
+  }
+  return BO_OK;
+}
+
+int bo_transpose(const double* A, double* B, int64_t n, int64_t ld, void* stream) {
+  dim3 grid((unsigned)ceil_div(n, 32), (unsigned)ceil_div(n, 32));
+  transpose_kernel<<<grid, dim3(32, 8), 0, as_stream(stream)>>>(A, B, n, ld);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+int bo_gemv(const double* M, int64_t ld, int64_t n, const double* x, double xshift, double* y,
+            void* stream) {
+  if (n <= 0) return BO_OK;
+  gemv_kernel<<<(unsigned)ceil_div(n, 4), 256, 0, as_stream(stream)>>>(M, ld, n, x, xshift, y);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+int bo_scale_inputs(const double* X, int64_t n, int d, const double* lengthscale,
+                    const double* center, int dp, double* Xs, void* stream) {
+  BO_CHECK_ARG(dp >= d, "bo_scale_inputs: dp < d");
+  const int64_t tot = n * dp;
+  if (tot == 0) return BO_OK;
+  scale_inputs_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, as_stream(stream)>>>(
+      X, n, d, lengthscale, center, dp, Xs);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+int bo_gp_cache_build(int kind, const double* Xt, int64_t n, int d, const double* lengthscale,
+                      double outputscale, double noise, double constant, const double* y,
+                      double* L, double* Linv, double* U, double* beta, double* alpha,
+                      int max_tries, double jitter0, double* jitter_used, int* info_dev,
+                      void* stream) {
+  BO_CHECK_ARG(n > 0 && d > 0, "bo_gp_cache_build: empty training set");
+  hipStream_t st = as_stream(stream);
+  const int64_t np = bo_padded_order(n);
+  double jitter = 0.0;
+  int info_h = 0;
+  for (int attempt = 0; attempt <= max_tries; ++attempt) {
+    if (attempt > 0) jitter = jitter0 * std::pow(10.0, (double)(attempt - 1));
+    int s = bo_covar_matrix(kind, Xt, n, Xt, n, d, lengthscale, outputscale, noise + jitter, 1,
+                            L, np, np, np, stream);
+    if (s) return s;
+    s = bo_cholesky_inverse(L, Linv, U, np, info_dev, stream);
+    if (s) return s;
+    BO_HIP(hipMemcpyAsync(&info_h, info_dev, sizeof(int), hipMemcpyDeviceToHost, st));
+    BO_HIP(hipStreamSynchronize(st));
+    if (info_h == 0) break;
+  }
+  if (jitter_used) *jitter_used = jitter;
+  if (info_h != 0) {
+    bo_set_error("Matrix not positive definite after repeatedly adding jitter up to %.1e "
+                 "(info %d)", jitter, info_h);
+    return BO_ERR_NOT_PSD;
+  }
+  int s = bo_transpose(Linv, U, np, np, stream);  // U = L^{-T}
+  if (s) return s;
+  s = bo_gemv(Linv, np, n, y, constant, beta, stream);  // beta = L^{-1} (y - c)
+  if (s) return s;
+  return bo_gemv(U, np, n, beta, 0.0, alpha, stream);   // alpha = L^{-T} beta
+}
+
+}  // extern "C"

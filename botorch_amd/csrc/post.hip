@@ -1,0 +1,230 @@
+// Batched exact-GP posterior over q-batches of candidates, fused with the
+// kernel-row builder, on the gfx950 fp64 matrix cores.
+//
+// Reference path (botorch/models/gpytorch.py:405-466 -> [G] exact prediction
+// under fast_pred_var, botorch/models/utils/assorted.py:286-298):
+//   K*x = k(X*, X_tr)          (b q) x n
+//   R   = K*x L^{-T}           (b q) x n      <- the dominant dense contraction
+//   mu  = c + K*x alpha = c + R beta,   beta = L^{-1}(y - c)
+//   Sigma_b = K**_b - R_b R_b^T         q x q per t-batch b
+//
+// post_partials_kernel computes R^T tile by tile as an MFMA GEMM
+//   R^T[c][i] = sum_k U[k][c] K*x[i][k],   U = L^{-T} (upper triangular)
+// with the K*x tile generated on the fly from the lengthscale-scaled inputs
+// (never written to HBM) and U streamed from HBM/L2.  Because the R^T tile's
+// MFMA accumulators have the test row on the lane and the training column on
+// (lane>>4, register), the same accumulator register is simultaneously a
+// valid A and B operand of a second MFMA, so  R_b R_b^T  over the tile's 128
+// columns is accumulated with 4 MFMAs per 16x16 accumulator and no data
+// movement.  Each workgroup writes its 16x16 partial blocks and its partial
+// R beta; post_finalize sums them over the column tiles.  R itself is never
+// materialised (C3: 268 MB saved per forward).
+//
+// Test rows are laid out per t-batch: row b*Qp + a, a < q, Qp = q rounded up
+// to a power of two <= 16, so every t-batch sits inside one 16-row MFMA tile.
+#include "common.h"
+
+namespace {
+
+constexpr int PC = 128;   // training columns c per workgroup
+constexpr int PI = 128;   // test rows i per workgroup
+constexpr int PK = 16;    // k-step
+constexpr int PLD = 144;  // LDS row pitch (doubles): 2 x 144 dwords = 32 mod 64 banks
+constexpr int DP = 8;     // padded input dimension held in registers
+
+template <int KIND>
+__global__ __launch_bounds__(256, 2) void post_partials_kernel(
+    const double* __restrict__ Xq, int nrows, const double* __restrict__ Xt, int n,
+    const double* __restrict__ U, int64_t ldu, const double* __restrict__ beta,
+    double outputscale, int nC, int nI, double* __restrict__ Spart, double* __restrict__ mpart) {
+  __shared__ __attribute__((aligned(16))) double Us[PK][PLD];
+  __shared__ __attribute__((aligned(16))) double Ks[PK][PLD];
+
+  // XCD-aware schedule: consecutive block ids are dealt round-robin over the
+  // 8 XCDs, so block b and b+8 share an L2.  XCD x takes the column tiles
+  // ci with (descending position) % 8 == x, heaviest (largest ci, longest
+  // triangular k-range) first, and sweeps all test-row tiles of a column tile
+  // back to back: the U panel of that column tile is read once into the XCD's
+  // L2 and reused by all of them.  Placement only affects speed.
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int slot = bid >> 3;
+  const int jj = slot / nI;
+  const int ii = slot - jj * nI;
+  const int pos = jj * 8 + xcd;
+  if (pos >= nC) return;
+  const int ci = nC - 1 - pos;
+  const int c0 = ci * PC;
+  const int i0 = ii * PI;
+  const int kend = min(n, c0 + PC);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+
+  // K*x tile role: this thread evaluates test row ti against 8 of the 16
+  // training points of each k-step (kh is wave-uniform -> scalar loads of Xt).
+  const int ti = tid & (PI - 1);
+  const int kh = __builtin_amdgcn_readfirstlane(tid >> 7);
+  const bool ivalid = (i0 + ti) < nrows;
+  double xi[DP];
+#pragma unroll
+  for (int t = 0; t < DP; ++t) xi[t] = ivalid ? Xq[(int64_t)(i0 + ti) * DP + t] : 0.0;
+
+  v4d acc[8][2];
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    acc[a][0] = v4d_zero();
+    acc[a][1] = v4d_zero();
+  }
+
+  double2 ru[4];
+  auto load_u = [&](int k0) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int e = tid + p * 256;
+      const int r = e >> 6;
+      const int cp = e & 63;
+      ru[p] = *reinterpret_cast<const double2*>(U + (int64_t)(k0 + r) * ldu + c0 + 2 * cp);
+    }
+  };
+
+  load_u(0);
+  for (int k0 = 0; k0 < kend; k0 += PK) {
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int e = tid + p * 256;
+      *reinterpret_cast<double2*>(&Us[e >> 6][2 * (e & 63)]) = ru[p];
+    }
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int r = kh * 8 + kk;
+      const int k = k0 + r;
+      double v = 0.0;
+      if (k < n) {
+        const double* xt = Xt + (int64_t)k * DP;
+        double d2 = 0.0;
+#pragma unroll
+        for (int t = 0; t < DP; ++t) {
+          const double df = xi[t] - xt[t];
+          d2 = fma(df, df, d2);
+        }
+        v = outputscale * kernel_from_d2<KIND>(d2);
+      }
+      Ks[r][ti] = ivalid ? v : 0.0;
+    }
+    __syncthreads();
+    if (k0 + PK < kend) load_u(k0 + PK);
+#pragma unroll
+    for (int ks = 0; ks < PK / 4; ++ks) {
+      const int kr = ks * 4 + (lane >> 4);
+      double a[8], b[2];
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) a[ct] = Us[kr][ct * 16 + (lane & 15)];
+#pragma unroll
+      for (int it = 0; it < 2; ++it) b[it] = Ks[kr][wave * 32 + it * 16 + (lane & 15)];
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+        for (int it = 0; it < 2; ++it) acc[ct][it] = mfma_f64(a[ct], b[it], acc[ct][it]);
+    }
+  }
+
+  // Epilogue: R R^T diagonal blocks and R beta for this workgroup's columns.
+  const int nrows16 = nI * (PI / 16);
+  const int nrows_pad = nI * PI;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    v4d P = v4d_zero();
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) P = mfma_f64(acc[ct][it][r], acc[ct][it][r], P);
+    const int row0 = i0 + wave * 32 + it * 16;
+    const int64_t tile = (int64_t)ci * nrows16 + row0 / 16;
+    double* sp = Spart + tile * 256;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sp[mfma_row(lane, r) * 16 + mfma_col(lane)] = P[r];
+
+    double m = 0.0;
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = c0 + ct * 16 + mfma_row(lane, r);
+        m = fma(acc[ct][it][r], (c < n) ? beta[c] : 0.0, m);
+      }
+    m += __shfl_xor(m, 16);
+    m += __shfl_xor(m, 32);
+    if (lane < 16) mpart[(int64_t)ci * nrows_pad + row0 + lane] = m;
+  }
+}
+
+// Scatter X (B x q x d) into the padded, lengthscale-scaled row layout
+// Xq[(b*Qp + a) * DP + t] = X[b][a][t] / ls[t]  (zeros elsewhere).
+__global__ void prepare_rows_kernel(const double* __restrict__ X, int B, int q, int d,
+                                    int Qp, const double* __restrict__ ls, int nrows_pad,
+                                    double* __restrict__ Xq) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)nrows_pad * DP) return;
+  const int64_t row = idx / DP;
+  const int t = (int)(idx % DP);
+  const int64_t b = row / Qp;
+  const int a = (int)(row % Qp);
+  double v = 0.0;
+  if (b < B && a < q && t < d) v = X[(b * q + a) * d + t] / ls[t];
+  Xq[idx] = v;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bo_post_geometry(int64_t B, int q, int64_t n, int* Qp, int* nrows_pad, int* nC) {
+  BO_CHECK_ARG(q >= 1 && q <= 16, "posterior kernels support 1 <= q <= 16 (got %d)", q);
+  int qp = 1;
+  while (qp < q) qp *= 2;
+  *Qp = qp;
+  *nrows_pad = (int)(ceil_div(B * qp, PI) * PI);
+  *nC = (int)ceil_div(n, PC);
+  return BO_OK;
+}
+
+int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthscale,
+                    double* Xq, void* stream) {
+  BO_CHECK_ARG(d <= DP, "fused posterior kernel supports d <= %d (got %d)", DP, d);
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, 1, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  const int64_t tot = (int64_t)nrows_pad * DP;
+  prepare_rows_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, as_stream(stream)>>>(
+      X, B, q, d, Qp, lengthscale, nrows_pad, Xq);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+int bo_post_partials(int kind, const double* Xq, int B, int q, const double* Xt_scaled,
+                     int64_t n, const double* U, int64_t ldu, const double* beta,
+                     double outputscale, double* Spart, double* mpart, void* stream) {
+  BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
+  BO_CHECK_ARG(ldu % 2 == 0 && ldu >= ceil_div(n, PC) * PC, "U leading dim %lld too small",
+               (long long)ldu);
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  const int nI = nrows_pad / PI;
+  const int nrows = B * Qp;
+  const int64_t blocks = 8 * ceil_div(nC, 8) * (int64_t)nI;
+  hipStream_t st = as_stream(stream);
+  if (kind == BO_RBF)
+    post_partials_kernel<BO_RBF><<<(unsigned)blocks, 256, 0, st>>>(
+        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart);
+  else
+    post_partials_kernel<BO_MATERN52><<<(unsigned)blocks, 256, 0, st>>>(
+        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,220 @@
+// Per-t-batch posterior finalisation + Monte-Carlo acquisition reduction.
+//
+// One workgroup per t-batch b (restart / raw sample):
+//   1. Sigma*_b = K**_b - sum_ct Spart[ct],  mu*_b = c + sum_ct mpart[ct]
+//      (the column-tile partials of post_partials_kernel, post.hip), then
+//      Standardize.untransform_posterior: mu' = ybar + s mu*, Sigma' = s^2 Sigma*
+//      (botorch/models/transforms/outcome.py:373-447).
+//   2. L_q = psd_safe_cholesky(Sigma') with the [G] jitter ladder applied per
+//      batch member: plain, then jitter0 * 10^i for i = 0..max_tries-1
+//      (linear_operator psd_safe_cholesky; botorch/__init__.py:47 sets 6 tries).
+//      A member that still fails reports info > 0; the host raises NotPSDError.
+//   3. f[s,a] = mu'_a + sum_{j<=a} L_q[a][j] Z[s][j]   (posteriors/gpytorch.py:85-126)
+//      and the acquisition reduction:
+//        qEI  : mean_s max_a relu(f - best_f)           (acquisition/monte_carlo.py:405-414)
+//        qNEI : mean_s max_a relu(f - best_f[s])        (:580-589, cached baseline best)
+//      q-max and the sample sum are wavefront shuffle reductions.
+#include "common.h"
+
+namespace {
+
+constexpr int QMAX = 16;
+constexpr int DP = 8;
+constexpr int THREADS = 256;
+
+enum QmcMode : int { QMC_POSTERIOR = 0, QMC_QEI = 1, QMC_QNEI = 2, QMC_CHOL = 3 };
+
+template <int KIND, int MODE>
+__global__ __launch_bounds__(THREADS) void qmc_kernel(
+    int q, int Qp, const double* __restrict__ Xq, const double* __restrict__ Spart,
+    const double* __restrict__ mpart, int nC, int nrows_pad, double outputscale,
+    double constant, double ymean, double ystd, const double* __restrict__ Z, int S,
+    double best_f, const double* __restrict__ best_f_s, int max_tries, double jitter0,
+    double* __restrict__ acq, double* __restrict__ mean_out, double* __restrict__ cov_out,
+    double* __restrict__ L_out, int* __restrict__ info_out, double* __restrict__ jitter_out) {
+  __shared__ double Sig[QMAX][QMAX + 1];
+  __shared__ double Lq[QMAX][QMAX + 1];
+  __shared__ double mu[QMAX];
+  __shared__ double red[THREADS / 64];
+  __shared__ int s_info;
+  __shared__ double s_jit;
+
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int row0 = b * Qp;               // first padded test row of this t-batch
+  const int tile = row0 >> 4;            // its 16-row MFMA tile
+  const int off = row0 & 15;             // offset inside the tile
+  const int nrows16 = nrows_pad >> 4;
+  const double s2 = ystd * ystd;
+
+  // 1. finalise the q x q covariance and the mean.
+  if (tid < q * q) {
+    const int a = tid / q, c = tid % q;
+    double acc = 0.0;
+    const double* sp = Spart + (int64_t)tile * 256 + (off + a) * 16 + (off + c);
+    for (int ct = 0; ct < nC; ++ct) acc += sp[(int64_t)ct * nrows16 * 256];
+    double kxx;
+    if (a == c) {
+      kxx = outputscale;
+    } else {
+      const double* xa = Xq + (int64_t)(row0 + a) * DP;
+      const double* xc = Xq + (int64_t)(row0 + c) * DP;
+      double d2 = 0.0;
+#pragma unroll
+      for (int t = 0; t < DP; ++t) {
+        const double df = xa[t] - xc[t];
+        d2 = fma(df, df, d2);
+      }
+      kxx = outputscale * kernel_from_d2<KIND>(d2);
+    }
+    const double v = s2 * (kxx - acc);
+    Sig[a][c] = v;
+    if (cov_out) cov_out[((int64_t)b * q + a) * q + c] = v;
+  }
+  if (tid < q) {
+    double m = 0.0;
+    const double* mp = mpart + row0 + tid;
+    for (int ct = 0; ct < nC; ++ct) m += mp[(int64_t)ct * nrows_pad];
+    const double v = ymean + ystd * (constant + m);
+    mu[tid] = v;
+    if (mean_out) mean_out[(int64_t)b * q + tid] = v;
+  }
+  __syncthreads();
+  if (MODE == QMC_POSTERIOR) return;
+
+  // 2. Cholesky with the jitter ladder (wave 0; lane a owns row a).
+  if (tid < 64) {
+    const int a = tid;
+    double jit = 0.0;
+    int info = 0;
+    for (int attempt = 0; attempt <= max_tries; ++attempt) {
+      if (attempt > 0) jit = jitter0 * pow(10.0, (double)(attempt - 1));
+      double r[QMAX];
+#pragma unroll
+      for (int j = 0; j < QMAX; ++j)
+        r[j] = (a < q && j < q && j <= a) ? Sig[a][j] + ((j == a) ? jit : 0.0) : 0.0;
+      info = 0;
+#pragma unroll
+      for (int j = 0; j < QMAX; ++j) {
+        if (j < q) {
+          const double ajj = __shfl(r[j], j);
+          if (!(ajj > 0.0) && info == 0) info = j + 1;
+          const double djj = sqrt(ajj);
+          double lij = (a == j) ? djj : r[j] / djj;
+          if (a < j) lij = 0.0;
+          r[j] = lij;
+#pragma unroll
+          for (int l = j + 1; l < QMAX; ++l) {
+            const double llj = __shfl(lij, l);
+            r[l] = fma(-lij, llj, r[l]);
+          }
+        }
+      }
+      if (info == 0) {
+        if (a < q)
+#pragma unroll
+          for (int j = 0; j < QMAX; ++j) Lq[a][j] = (j <= a && j < q) ? r[j] : 0.0;
+        break;
+      }
+    }
+    if (a == 0) {
+      s_info = info;
+      s_jit = jit;
+    }
+  }
+  __syncthreads();
+  const int info = s_info;
+  if (tid == 0) {
+    if (info_out) info_out[b] = info;
+    if (jitter_out) jitter_out[b] = s_jit;
+  }
+  if (L_out && tid < q * q) {
+    const int a = tid / q, c = tid % q;
+    L_out[((int64_t)b * q + a) * q + c] = info ? NAN : Lq[a][c];
+  }
+  if (MODE == QMC_CHOL) return;
+  if (info) {
+    if (tid == 0) acq[b] = NAN;
+    return;
+  }
+
+  // 3. samples and the reduction.
+  double sum = 0.0;
+  for (int s = tid; s < S; s += THREADS) {
+    const double* z = Z + (int64_t)s * q;
+    double zs[QMAX];
+#pragma unroll
+    for (int j = 0; j < QMAX; ++j) zs[j] = (j < q) ? z[j] : 0.0;
+    const double bf = (MODE == QMC_QNEI) ? best_f_s[s] : best_f;
+    double vmax = 0.0;
+#pragma unroll
+    for (int a = 0; a < QMAX; ++a) {
+      if (a < q) {
+        double f = mu[a];
+#pragma unroll
+        for (int j = 0; j <= a; ++j) f = fma(Lq[a][j], zs[j], f);
+        vmax = fmax(vmax, f - bf);
+      }
+    }
+    sum += vmax;
+  }
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  if ((tid & 63) == 0) red[tid >> 6] = sum;
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0.0;
+    for (int w = 0; w < THREADS / 64; ++w) t += red[w];
+    acq[b] = t / S;
+  }
+}
+
+template <int KIND>
+int launch_qmc(int mode, int B, int q, int Qp, const double* Xq, const double* Spart,
+               const double* mpart, int nC, int nrows_pad, double outputscale, double constant,
+               double ymean, double ystd, const double* Z, int S, double best_f,
+               const double* best_f_s, int max_tries, double jitter0, double* acq,
+               double* mean_out, double* cov_out, double* L_out, int* info_out,
+               double* jitter_out, hipStream_t st) {
+#define BO_QMC_ARGS                                                                          \
+  q, Qp, Xq, Spart, mpart, nC, nrows_pad, outputscale, constant, ymean, ystd, Z, S, best_f, \
+      best_f_s, max_tries, jitter0, acq, mean_out, cov_out, L_out, info_out, jitter_out
+  if (mode == QMC_POSTERIOR)
+    qmc_kernel<KIND, QMC_POSTERIOR><<<B, THREADS, 0, st>>>(BO_QMC_ARGS);
+  else if (mode == QMC_QEI)
+    qmc_kernel<KIND, QMC_QEI><<<B, THREADS, 0, st>>>(BO_QMC_ARGS);
+  else if (mode == QMC_QNEI)
+    qmc_kernel<KIND, QMC_QNEI><<<B, THREADS, 0, st>>>(BO_QMC_ARGS);
+  else
+    qmc_kernel<KIND, QMC_CHOL><<<B, THREADS, 0, st>>>(BO_QMC_ARGS);
+#undef BO_QMC_ARGS
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+}  // namespace
+
+extern "C" int bo_post_geometry(int64_t B, int q, int64_t n, int* Qp, int* nrows_pad, int* nC);
+
+extern "C" int bo_qmc_finalize(int kind, int mode, int B, int q, const double* Xq,
+                               const double* Spart, const double* mpart, int64_t n,
+                               double outputscale, double constant, double ymean, double ystd,
+                               const double* Z, int S, double best_f, const double* best_f_s,
+                               int max_tries, double jitter0, double* acq, double* mean_out,
+                               double* cov_out, double* L_out, int* info_out,
+                               double* jitter_out, void* stream) {
+  BO_CHECK_ARG(mode >= 0 && mode <= 3, "bo_qmc_finalize: bad mode %d", mode);
+  BO_CHECK_ARG(mode == QMC_POSTERIOR || mode == QMC_CHOL || (acq && Z && S > 0), "bo_qmc_finalize: missing MC args");
+  BO_CHECK_ARG(mode != QMC_QNEI || best_f_s, "bo_qmc_finalize: qNEI needs per-sample best_f");
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  if (B == 0) return BO_OK;
+  hipStream_t st = as_stream(stream);
+  if (kind == BO_RBF)
+    return launch_qmc<BO_RBF>(mode, B, q, Qp, Xq, Spart, mpart, nC, nrows_pad, outputscale,
+                              constant, ymean, ystd, Z, S, best_f, best_f_s, max_tries, jitter0,
+                              acq, mean_out, cov_out, L_out, info_out, jitter_out, st);
+  return launch_qmc<BO_MATERN52>(mode, B, q, Qp, Xq, Spart, mpart, nC, nrows_pad, outputscale,
+                                 constant, ymean, ystd, Z, S, best_f, best_f_s, max_tries,
+                                 jitter0, acq, mean_out, cov_out, L_out, info_out, jitter_out, st);
+}

@@ -1,0 +1,239 @@
+"""Tensor-level wrappers of the C ABI (device buffers in, device buffers out).
+
+Every function here enqueues HIP kernels from ``libbotorch_amd.so`` on the
+current torch stream of the tensors' device.  There is no CPU path: inputs
+must be fp64 tensors on a ROCm device, and a missing library raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+from torch.quasirandom import SobolEngine
+
+from . import _lib
+from ._lib import check, lib
+
+DP = 8  # padded input dimension of the fused posterior kernel
+CHOLESKY_MAX_TRIES = 6  # botorch/__init__.py:47
+CHOLESKY_JITTER_F64 = 1e-8  # [G] linear_operator.settings.cholesky_jitter (double)
+
+
+def _p(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(device: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _dev(*tensors: torch.Tensor) -> torch.device:
+    dev = tensors[0].device
+    for t in tensors:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError("botorch_amd kernels need ROCm device tensors (no CPU fallback)")
+        if t.dtype not in (torch.float64, torch.int64, torch.int32):
+            raise TypeError(f"expected fp64 tensors, got {t.dtype}")
+    return dev
+
+
+def gemm(A, B, transA=False, transB=False, alpha=1.0, beta=0.0, C=None, flags=0):
+    """C = alpha op(A) op(B) + beta C (2-D or batched 3-D row-major fp64)."""
+    dev = _dev(A, B)
+    batched = A.dim() == 3
+    A3 = A if batched else A.unsqueeze(0)
+    B3 = B if batched else B.unsqueeze(0)
+    A3, B3 = A3.contiguous(), B3.contiguous()
+    M = A3.shape[2] if transA else A3.shape[1]
+    K = A3.shape[1] if transA else A3.shape[2]
+    N = B3.shape[1] if transB else B3.shape[2]
+    batch = A3.shape[0]
+    if C is None:
+        C3 = torch.zeros(batch, M, N, dtype=torch.float64, device=dev)
+    else:
+        C3 = C if batched else C.unsqueeze(0)
+    check(lib().bo_gemm_f64(int(transA), int(transB), M, N, K, alpha, _p(A3), A3.shape[2],
+                            A3.stride(0), _p(B3), B3.shape[2], B3.stride(0), beta, _p(C3),
+                            C3.shape[2], C3.stride(0), batch, flags, _stream(dev)), "gemm")
+    return C3 if batched else C3.squeeze(0)
+
+
+def covar_matrix(X1, X2, lengthscale, kind=_lib.RBF, outputscale=1.0, diag_add=0.0):
+    dev = _dev(X1, X2, lengthscale)
+    n1, d = X1.shape
+    n2 = X2.shape[0]
+    K = torch.empty(n1, n2, dtype=torch.float64, device=dev)
+    check(lib().bo_covar_matrix(kind, _p(X1.contiguous()), n1, _p(X2.contiguous()), n2, d,
+                                _p(lengthscale.contiguous()), outputscale, diag_add, 0, _p(K),
+                                n2, n1, n2, _stream(dev)), "covar_matrix")
+    return K
+
+
+def padded_order(n: int) -> int:
+    return int(lib().bo_padded_order(n))
+
+
+def cholesky_inverse(A: torch.Tensor):
+    """Lower Cholesky factor and its inverse of an SPD matrix (np x np, np % 128 == 0
+    handled by padding with identity).  Returns (L, Linv, info)."""
+    dev = _dev(A)
+    n = A.shape[0]
+    np_ = padded_order(n)
+    W = torch.eye(np_, dtype=torch.float64, device=dev)
+    W[:n, :n] = torch.tril(A)
+    Linv = torch.empty_like(W)
+    work = torch.empty_like(W)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    check(lib().bo_cholesky_inverse(_p(W), _p(Linv), _p(work), np_, _p(info), _stream(dev)),
+          "cholesky_inverse")
+    return W[:n, :n], Linv[:n, :n], int(info.item())
+
+
+@dataclass
+class GPCache:
+    """Device-resident exact-GP prediction caches ([G] DefaultPredictionStrategy)."""
+    kind: int
+    n: int
+    d: int
+    np: int
+    Xt: torch.Tensor           # n x d raw training inputs
+    Xt_scaled: torch.Tensor    # n x 8, divided by the lengthscale (zero padded)
+    lengthscale: torch.Tensor  # d
+    outputscale: float
+    noise: float
+    constant: float
+    L: torch.Tensor            # np x np lower Cholesky factor of K + s2 I (+ jitter)
+    Linv: torch.Tensor         # np x np
+    U: torch.Tensor            # np x np = L^{-T}  (covar_cache)
+    beta: torch.Tensor         # n  = L^{-1} (y - c)
+    alpha: torch.Tensor        # n  = (K + s2 I)^{-1} (y - c)  (mean_cache)
+    jitter: float
+
+
+def build_gp_cache(Xt, y, lengthscale, noise, constant, kind=_lib.RBF, outputscale=1.0,
+                   max_tries=CHOLESKY_MAX_TRIES, jitter0=CHOLESKY_JITTER_F64) -> GPCache:
+    dev = _dev(Xt, y, lengthscale)
+    Xt = Xt.contiguous()
+    n, d = Xt.shape
+    if torch.isnan(Xt).any() or torch.isnan(y).any():
+        from .exceptions import NanError
+        raise NanError("training data contains NaN")
+    np_ = padded_order(n)
+    f64 = dict(dtype=torch.float64, device=dev)
+    L = torch.empty(np_, np_, **f64)
+    Linv = torch.empty(np_, np_, **f64)
+    U = torch.empty(np_, np_, **f64)
+    beta = torch.empty(n, **f64)
+    alpha = torch.empty(n, **f64)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    jit = ctypes.c_double(0.0)
+    ls = lengthscale.detach().reshape(-1).contiguous()
+    st = _stream(dev)
+    check(lib().bo_gp_cache_build(kind, _p(Xt), n, d, _p(ls), float(outputscale), float(noise),
+                                  float(constant), _p(y.contiguous()), _p(L), _p(Linv), _p(U),
+                                  _p(beta), _p(alpha), max_tries, jitter0, ctypes.byref(jit),
+                                  _p(info), st), "gp_cache_build")
+    if jit.value > 0:
+        import warnings
+        from .exceptions import NumericalWarning
+        warnings.warn(f"A not p.d., added jitter of {jit.value:.1e} to the diagonal",
+                      NumericalWarning)
+    Xs = torch.empty(n, DP, **f64)
+    if d <= DP:
+        check(lib().bo_scale_inputs(_p(Xt), n, d, _p(ls), ctypes.c_void_p(0), DP, _p(Xs), st),
+              "scale_inputs")
+    return GPCache(kind, n, d, np_, Xt, Xs, ls, float(outputscale), float(noise),
+                   float(constant), L, Linv, U, beta, alpha, jit.value)
+
+
+@dataclass
+class PostPartials:
+    B: int
+    q: int
+    Qp: int
+    nrows_pad: int
+    nC: int
+    Xq: torch.Tensor
+    Spart: torch.Tensor
+    mpart: torch.Tensor
+
+
+def geometry(B: int, q: int, n: int):
+    Qp, nrows, nC = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    check(lib().bo_post_geometry(B, q, n, ctypes.byref(Qp), ctypes.byref(nrows),
+                                 ctypes.byref(nC)), "post_geometry")
+    return Qp.value, nrows.value, nC.value
+
+
+def post_partials(cache: GPCache, X: torch.Tensor) -> PostPartials:
+    """Column-tile partials of R R^T and R beta for X (B x q x d)."""
+    dev = _dev(X)
+    B, q, d = X.shape
+    if d != cache.d:
+        raise ValueError(f"X has d={d}, model has d={cache.d}")
+    Qp, nrows_pad, nC = geometry(B, q, cache.n)
+    f64 = dict(dtype=torch.float64, device=dev)
+    Xq = torch.empty(nrows_pad, DP, **f64)
+    Spart = torch.empty(nC, nrows_pad // 16, 16, 16, **f64)
+    mpart = torch.empty(nC, nrows_pad, **f64)
+    st = _stream(dev)
+    check(lib().bo_prepare_rows(_p(X.contiguous()), B, q, d, _p(cache.lengthscale), _p(Xq), st),
+          "prepare_rows")
+    check(lib().bo_post_partials(cache.kind, _p(Xq), B, q, _p(cache.Xt_scaled), cache.n,
+                                 _p(cache.U), cache.np, _p(cache.beta), cache.outputscale,
+                                 _p(Spart), _p(mpart), st), "post_partials")
+    return PostPartials(B, q, Qp, nrows_pad, nC, Xq, Spart, mpart)
+
+
+def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd: float,
+                 Z: Optional[torch.Tensor] = None, best_f: float = 0.0,
+                 best_f_s: Optional[torch.Tensor] = None, want_mean=True, want_cov=True,
+                 want_L=False, max_tries=CHOLESKY_MAX_TRIES, jitter0=CHOLESKY_JITTER_F64):
+    dev = pp.Xq.device
+    B, q = pp.B, pp.q
+    f64 = dict(dtype=torch.float64, device=dev)
+    mean = torch.empty(B, q, **f64) if want_mean else None
+    cov = torch.empty(B, q, q, **f64) if want_cov else None
+    L = torch.empty(B, q, q, **f64) if want_L else None
+    need_mc = mode in (_lib.QMC_QEI, _lib.QMC_QNEI)
+    acq = torch.empty(B, **f64) if need_mc else None
+    info = torch.empty(B, dtype=torch.int32, device=dev) if mode != _lib.QMC_POSTERIOR else None
+    jit = torch.empty(B, **f64) if mode != _lib.QMC_POSTERIOR else None
+    S = Z.shape[0] if Z is not None else 0
+    if Z is not None:
+        Z = Z.reshape(S, q).contiguous()
+    check(lib().bo_qmc_finalize(cache.kind, mode, B, q, _p(pp.Xq), _p(pp.Spart), _p(pp.mpart),
+                                cache.n, cache.outputscale, cache.constant, float(ymean),
+                                float(ystd), _p(Z), S, float(best_f), _p(best_f_s), max_tries,
+                                jitter0, _p(acq), _p(mean), _p(cov), _p(L), _p(info), _p(jit),
+                                _stream(dev)), "qmc_finalize")
+    return dict(acq=acq, mean=mean, cov=cov, L=L, info=info, jitter=jit)
+
+
+def sobol_engine_state(dim: int, seed: int):
+    """Scrambled direction numbers + digital shift of torch's SobolEngine
+    (the engine the reference's NormalQMCEngine wraps, sampling/qmc.py:56)."""
+    eng = SobolEngine(dimension=dim, scramble=True, seed=seed)
+    return eng.sobolstate.clone(), eng.shift.clone()
+
+
+def sobol_normal(dim: int, n: int, seed: int, device, skip: int = 0) -> torch.Tensor:
+    """n x dim scrambled-Sobol N(0,1) samples generated on the device."""
+    state, shift = sobol_engine_state(dim, seed)
+    state = state.to(device)
+    shift = shift.to(device)
+    out = torch.empty(n, dim, dtype=torch.float64, device=device)
+    check(lib().bo_sobol_normal(_p(state), _p(shift), dim, n, skip, _p(out),
+                                _stream(torch.device(device))), "sobol_normal")
+    return out
+
+
+def probe_mfma_layout(device) -> torch.Tensor:
+    out = torch.empty(64, 8, dtype=torch.float64, device=device)
+    check(lib().bo_probe_mfma_f64_layout(_p(out), _stream(torch.device(device))), "probe")
+    return out

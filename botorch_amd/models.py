@@ -1,0 +1,327 @@
+"""Exact GP models with BoTorch's posterior API, backed by the gfx950 kernels.
+
+Mirrors botorch/models/gp_regression.py:68-254 (SingleTaskGP), the default
+modules of botorch/models/utils/gpytorch_modules.py:74-127, the Standardize
+outcome transform (botorch/models/transforms/outcome.py:217-447) and
+ModelListGP (botorch/models/model_list_gp_regression.py:24).  Hyperparameters
+are plain fp64 ``nn.Parameter``s holding the constrained values directly (the
+reference's constraints use ``transform=None``: raw value == value); their
+lower bounds are enforced by L-BFGS-B in ``fit.py`` exactly as
+botorch/optim/utils/model_utils.py:69-109 does.
+
+Eval-mode prediction caches (Cholesky factor, L^{-T}, alpha, beta) live on the
+device and are rebuilt when any hyperparameter or training tensor changes
+version, or on ``train()`` (mirrors [G] ExactGP dropping prediction_strategy).
+"""
+from __future__ import annotations
+
+import math
+import warnings
+from typing import List, Optional, Sequence, Union
+
+import torch
+from torch import nn
+
+from . import _lib
+from .exceptions import InputDataWarning, UnsupportedError
+
+MIN_INFERRED_NOISE_LEVEL = 1e-4  # gpytorch_modules.py:29
+LENGTHSCALE_LOWER = 2.5e-2       # gpytorch_modules.py:123
+SQRT2, SQRT3 = math.sqrt(2), math.sqrt(3)
+
+
+class LogNormalPrior:
+    """[G] LogNormalPrior(loc, scale) (torch LogNormal)."""
+
+    def __init__(self, loc: float, scale: float):
+        self.loc, self.scale = float(loc), float(scale)
+
+    @property
+    def mode(self) -> float:
+        return math.exp(self.loc - self.scale ** 2)
+
+    def log_prob(self, x: torch.Tensor) -> torch.Tensor:
+        lx = torch.log(x)
+        return (-((lx - self.loc) ** 2) / (2 * self.scale ** 2) - math.log(self.scale)
+                - 0.5 * math.log(2 * math.pi) - lx)
+
+
+class _Kernel(nn.Module):
+    kind = _lib.RBF
+
+    def __init__(self, ard_num_dims: int, lengthscale_prior: Optional[LogNormalPrior] = None,
+                 lengthscale_lower: float = LENGTHSCALE_LOWER, initial: Optional[float] = None):
+        super().__init__()
+        self.ard_num_dims = ard_num_dims
+        self.lengthscale_prior = lengthscale_prior
+        self.lengthscale_lower = lengthscale_lower
+        init = initial if initial is not None else (
+            lengthscale_prior.mode if lengthscale_prior is not None else 1.0)
+        self.raw_lengthscale = nn.Parameter(torch.full((1, ard_num_dims), init, dtype=torch.float64))
+
+    @property
+    def lengthscale(self) -> torch.Tensor:
+        return self.raw_lengthscale
+
+    @lengthscale.setter
+    def lengthscale(self, value):
+        with torch.no_grad():
+            self.raw_lengthscale.copy_(torch.as_tensor(value, dtype=torch.float64).expand_as(self.raw_lengthscale))
+
+    outputscale = 1.0
+
+
+class RBFKernel(_Kernel):
+    """exp(-||(x - x')/ell||^2 / 2)  ([G] RBFKernel)."""
+    kind = _lib.RBF
+
+
+class MaternKernel(_Kernel):
+    """Matern-5/2 ([G] MaternKernel(nu=2.5))."""
+    kind = _lib.MATERN52
+
+    def __init__(self, nu: float = 2.5, **kw):
+        if nu != 2.5:
+            raise UnsupportedError("only nu = 2.5 is on the accelerated path")
+        super().__init__(**kw)
+
+
+class ScaleKernel(nn.Module):
+    """outputscale * base_kernel ([G] ScaleKernel)."""
+
+    def __init__(self, base_kernel: _Kernel, outputscale: float = 1.0, outputscale_prior=None):
+        super().__init__()
+        self.base_kernel = base_kernel
+        self.outputscale_prior = outputscale_prior
+        self.raw_outputscale = nn.Parameter(torch.tensor(float(outputscale), dtype=torch.float64))
+
+    kind = property(lambda self: self.base_kernel.kind)
+    ard_num_dims = property(lambda self: self.base_kernel.ard_num_dims)
+
+    @property
+    def lengthscale(self):
+        return self.base_kernel.lengthscale
+
+    @property
+    def outputscale(self):
+        return self.raw_outputscale
+
+    @outputscale.setter
+    def outputscale(self, v):
+        with torch.no_grad():
+            self.raw_outputscale.fill_(float(v))
+
+
+class GaussianLikelihood(nn.Module):
+    """Homoskedastic Gaussian noise ([G] GaussianLikelihood) with BoTorch's
+    LogNormal(-4, 1) prior and noise >= 1e-4 (gpytorch_modules.py:74-97)."""
+
+    def __init__(self, noise_prior: Optional[LogNormalPrior] = None,
+                 noise_lower: float = MIN_INFERRED_NOISE_LEVEL, initial: Optional[float] = None):
+        super().__init__()
+        self.noise_prior = noise_prior
+        self.noise_lower = noise_lower
+        init = initial if initial is not None else (noise_prior.mode if noise_prior else 1e-4)
+        self.raw_noise = nn.Parameter(torch.tensor([init], dtype=torch.float64))
+
+    @property
+    def noise(self):
+        return self.raw_noise
+
+    @noise.setter
+    def noise(self, v):
+        with torch.no_grad():
+            self.raw_noise.copy_(torch.as_tensor(v, dtype=torch.float64).reshape(1))
+
+
+class ConstantMean(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.raw_constant = nn.Parameter(torch.tensor(0.0, dtype=torch.float64))
+
+    @property
+    def constant(self):
+        return self.raw_constant
+
+    @constant.setter
+    def constant(self, v):
+        with torch.no_grad():
+            self.raw_constant.fill_(float(v))
+
+
+def get_covar_module_with_dim_scaled_prior(ard_num_dims: int, use_rbf_kernel: bool = True):
+    """gpytorch_modules.py:100-127: LogNormal(sqrt2 + ln(d)/2, sqrt3) lengthscale
+    prior, initialised at its mode, lengthscale >= 0.025."""
+    prior = LogNormalPrior(SQRT2 + 0.5 * math.log(ard_num_dims), SQRT3)
+    cls = RBFKernel if use_rbf_kernel else MaternKernel
+    return cls(ard_num_dims=ard_num_dims, lengthscale_prior=prior)
+
+
+def get_gaussian_likelihood_with_lognormal_prior():
+    """gpytorch_modules.py:74-97."""
+    return GaussianLikelihood(noise_prior=LogNormalPrior(-4.0, 1.0))
+
+
+class Standardize(nn.Module):
+    """Outcome standardisation (botorch/models/transforms/outcome.py:217-447)."""
+
+    def __init__(self, m: int, min_stdv: float = 1e-8):
+        super().__init__()
+        self._m = m
+        self._min_stdv = min_stdv
+        self.register_buffer("means", torch.zeros(1, m, dtype=torch.float64))
+        self.register_buffer("stdvs", torch.ones(1, m, dtype=torch.float64))
+        self._is_trained = False
+
+    def forward(self, Y: torch.Tensor, Yvar: Optional[torch.Tensor] = None):
+        if self.training:
+            if Y.shape[-2] < 1:
+                raise ValueError("Can't standardize with no observations.")
+            if Y.shape[-2] == 1:
+                stdvs = torch.ones(1, Y.shape[-1], dtype=Y.dtype, device=Y.device)
+            else:
+                stdvs = Y.std(dim=-2, keepdim=True)
+            stdvs = stdvs.where(stdvs >= self._min_stdv, torch.full_like(stdvs, 1.0))
+            self.means = Y.mean(dim=-2, keepdim=True)
+            self.stdvs = stdvs
+            self._is_trained = True
+        Y_tf = (Y - self.means) / self.stdvs
+        Yvar_tf = Yvar / self.stdvs.pow(2) if Yvar is not None else None
+        return Y_tf, Yvar_tf
+
+    def untransform(self, Y, Yvar=None):
+        return self.means + self.stdvs * Y, (self.stdvs.pow(2) * Yvar if Yvar is not None else None)
+
+
+class Model(nn.Module):
+    """Abstract model with BoTorch's ``posterior`` contract (models/model.py:82-117)."""
+
+    _num_outputs = 1
+
+    @property
+    def num_outputs(self) -> int:
+        return self._num_outputs
+
+    def posterior(self, X, output_indices=None, observation_noise=False, posterior_transform=None):
+        raise NotImplementedError
+
+
+class SingleTaskGP(Model):
+    """Single-output exact GP (botorch/models/gp_regression.py:130-254).
+
+    Defaults: RBF-ARD kernel without outputscale, LogNormal priors,
+    ConstantMean, GaussianLikelihood, Standardize(m=1) outcome transform.
+    """
+
+    def __init__(self, train_X: torch.Tensor, train_Y: torch.Tensor,
+                 train_Yvar: Optional[torch.Tensor] = None, likelihood=None, covar_module=None,
+                 mean_module=None, outcome_transform="DEFAULT", input_transform=None):
+        super().__init__()
+        if train_Yvar is not None:
+            raise UnsupportedError("fixed-noise models are not on the accelerated path")
+        if input_transform is not None:
+            raise UnsupportedError("input transforms are not on the accelerated path")
+        if train_X.dim() != 2 or train_Y.dim() != 2 or train_Y.shape[-1] != 1:
+            raise UnsupportedError("SingleTaskGP here takes train_X n x d and train_Y n x 1")
+        train_X = train_X.to(torch.float64)
+        train_Y = train_Y.to(torch.float64)
+        if torch.isnan(train_X).any() or torch.isnan(train_Y).any():
+            from .exceptions import InputDataError
+            raise InputDataError("Input data contains NaN values.")
+        if outcome_transform == "DEFAULT":
+            outcome_transform = Standardize(m=1)
+        if outcome_transform is not None:
+            outcome_transform.train()
+            train_Y_tf, _ = outcome_transform(train_Y)
+            self.outcome_transform = outcome_transform
+        else:
+            train_Y_tf = train_Y
+        self._check_scaling(train_X, train_Y_tf)
+        self.train_inputs = (train_X,)
+        self.train_targets = train_Y_tf.squeeze(-1)
+        self._raw_train_Y = train_Y
+        d = train_X.shape[-1]
+        self.likelihood = likelihood if likelihood is not None else get_gaussian_likelihood_with_lognormal_prior()
+        self.mean_module = mean_module if mean_module is not None else ConstantMean()
+        self.covar_module = covar_module if covar_module is not None else get_covar_module_with_dim_scaled_prior(d)
+        self._cache = None
+        self._cache_key = None
+        self.to(train_X.device)
+
+    @staticmethod
+    def _check_scaling(X, Y):
+        """botorch/models/utils/assorted.py:219-261 (warnings only)."""
+        if X.numel() and (X.min() < -1e-8 or X.max() > 1 + 1e-8):
+            warnings.warn("Input data is not contained to the unit cube. Please consider "
+                          "min-max scaling the input data.", InputDataWarning)
+
+    # -- hyperparameter accessors ------------------------------------------------
+    @property
+    def kind(self) -> int:
+        return self.covar_module.kind
+
+    def hyper(self):
+        ls = self.covar_module.lengthscale.detach().reshape(-1)
+        os_ = float(self.covar_module.outputscale) if isinstance(self.covar_module, ScaleKernel) else 1.0
+        return ls, os_, float(self.likelihood.noise.detach()), float(self.mean_module.constant.detach())
+
+    def outcome_stats(self):
+        if hasattr(self, "outcome_transform"):
+            return float(self.outcome_transform.means.reshape(-1)[0]), float(self.outcome_transform.stdvs.reshape(-1)[0])
+        return 0.0, 1.0
+
+    def train(self, mode: bool = True):
+        if mode:
+            self._cache = None
+            self._cache_key = None
+        return super().train(mode)
+
+    def _key(self):
+        ps = [self.train_inputs[0], self.train_targets] + list(self.parameters())
+        return tuple((p.data_ptr(), p._version) for p in ps)
+
+    def prediction_cache(self):
+        """Device caches of [G] exact prediction; rebuilt on any change."""
+        from . import kernels
+        key = self._key()
+        if self._cache is None or self._cache_key != key:
+            ls, os_, noise, c = self.hyper()
+            self._cache = kernels.build_gp_cache(self.train_inputs[0], self.train_targets, ls,
+                                                 noise, c, kind=self.kind, outputscale=os_)
+            self._cache_key = key
+        return self._cache
+
+    def posterior(self, X: torch.Tensor, output_indices=None, observation_noise=False,
+                  posterior_transform=None):
+        """botorch/models/gpytorch.py:405-466."""
+        from .posteriors import GPyTorchPosterior
+        if output_indices not in (None, [0]):
+            raise UnsupportedError("single-output model")
+        self.eval()
+        post = GPyTorchPosterior.from_model(self, X, observation_noise=observation_noise)
+        if posterior_transform is not None:
+            return posterior_transform(post)
+        return post
+
+
+class ModelListGP(Model):
+    """Independent single-output GPs (botorch/models/model_list_gp_regression.py:24);
+    its posterior is block-diagonal across outputs (models/gpytorch.py:629-726)."""
+
+    def __init__(self, *models: SingleTaskGP):
+        super().__init__()
+        self.models = nn.ModuleList(models)
+        self._num_outputs = len(models)
+
+    def posterior(self, X, output_indices=None, observation_noise=False, posterior_transform=None):
+        from .posteriors import PosteriorList
+        idx = output_indices if output_indices is not None else range(len(self.models))
+        post = PosteriorList(*[self.models[i].posterior(X, observation_noise=observation_noise) for i in idx])
+        if posterior_transform is not None:
+            return posterior_transform(post)
+        return post
+
+    def train(self, mode: bool = True):
+        for m in self.models:
+            m.train(mode)
+        return super().train(mode)

@@ -1,0 +1,165 @@
+/*
+ * botorch_amd -- C ABI of the MI355X (gfx950) GP-posterior + MC-acquisition
+ * hot path.  Plain pointers and sizes only; every pointer argument named for
+ * a tensor is a DEVICE pointer (HBM) unless documented as host; every `stream`
+ * is a hipStream_t passed as void* (enqueue only -- the calls never
+ * synchronise, except bo_gp_cache_build, which reads the Cholesky status back
+ * once per jitter attempt, as the reference's psd_safe_cholesky does).
+ *
+ * All matrices are row-major fp64.  Return value: BO_OK (0) or a BO_ERR_*
+ * code; bo_last_error() describes the last failure of the calling thread.
+ *
+ * The reference (anand-12/botorch @ 2024-10-08) is pure Python over
+ * GPyTorch/linear_operator; it has no FFI.  Each entry point cites the
+ * reference interface whose computation it replaces; INTEGRATION.md shows the
+ * ctypes binding (botorch_amd/_lib.py) a maintainer adds on the reference side.
+ */
+#ifndef BOTORCH_AMD_H
+#define BOTORCH_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BO_ABI_VERSION 1
+
+/* status codes */
+#define BO_OK 0
+#define BO_ERR_ARG 1
+#define BO_ERR_HIP 2
+#define BO_ERR_NOT_PSD 3 /* maps to NotPSDError (botorch/exceptions/errors.py) */
+#define BO_ERR_NAN 4     /* maps to NanError */
+
+/* kernel families (botorch/models/utils/gpytorch_modules.py:100-127,
+ * botorch/models/fully_bayesian.py:81-92) */
+#define BO_KIND_RBF 0
+#define BO_KIND_MATERN52 1
+
+/* bo_gemm_f64 flags: structure of the operands (zero regions are skipped) */
+#define BO_GEMM_LOWER_C 1 /* write only C[m][n] with m >= n */
+#define BO_GEMM_A_LOWER 2 /* op(A)[m][k] == 0 for k > m */
+#define BO_GEMM_B_UPPER 4 /* op(B)[k][n] == 0 for k > n */
+#define BO_GEMM_A_UPPER 8 /* op(A)[m][k] == 0 for k < m */
+#define BO_GEMM_B_LOWER 16 /* op(B)[k][n] == 0 for k < n */
+
+/* qmc modes */
+#define BO_QMC_POSTERIOR 0
+#define BO_QMC_QEI 1
+#define BO_QMC_QNEI 2
+#define BO_QMC_CHOL 3 /* finalise + jittered q x q Cholesky only (no MC) */
+
+const char* bo_last_error(void);
+int bo_version(void);
+
+/* Hardware probe of the fp64 MFMA accumulator map; out: 64 x 8 doubles. */
+int bo_probe_mfma_f64_layout(double* out, void* stream);
+
+/* Batched C = alpha op(A) op(B) + beta C on the fp64 matrix cores (strides sA,
+ * sB, sC between batch members).  Building block of the Cholesky/inverse and
+ * of the qNEI cross-covariance; replaces the dense torch.matmul calls inside
+ * [G] linear_operator (e.g. MatmulLinearOperator under
+ * botorch/models/gpytorch.py:446). */
+int bo_gemm_f64(int transA, int transB, int M, int N, int K, double alpha, const double* A,
+                int64_t lda, int64_t sA, const double* B, int64_t ldb, int64_t sB,
+                double beta, double* C, int64_t ldc, int64_t sC, int batch, int flags,
+                void* stream);
+
+/* K[i][j] = outputscale * k(X1_i, X2_j) + diag_add * [i == j] over a rows x cols
+ * extent with an identity pad beyond (n1, n2); mode bit 1 zeroes the strict
+ * upper triangle.  X1: n1 x d, X2: n2 x d, lengthscale: d.
+ * Replaces [G] RBFKernel/MaternKernel(+ScaleKernel).forward
+ * (SingleTaskGP.forward, botorch/models/gp_regression.py:249-254). */
+int bo_covar_matrix(int kind, const double* X1, int64_t n1, const double* X2, int64_t n2,
+                    int d, const double* lengthscale, double outputscale, double diag_add,
+                    int mode, double* K, int64_t ldk, int64_t rows, int64_t cols, void* stream);
+
+/* Padded order np used by every n x n cache below (multiple of 128). */
+int64_t bo_padded_order(int64_t n);
+
+/* In-place blocked Cholesky of the lower-stored SPD matrix A (np x np, upper
+ * triangle zero) and its explicit inverse Linv (np x np).  work: np x np
+ * scratch.  *info (device int) = 0 or the 1-based order of the first failing
+ * leading minor (torch.linalg.cholesky_ex convention). */
+int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* info,
+                        void* stream);
+
+/* B = A^T for n x n matrices with leading dimension ld. */
+int bo_transpose(const double* A, double* B, int64_t n, int64_t ld, void* stream);
+
+/* y[i] = sum_k M[i][k] (x[k] - xshift), i, k < n. */
+int bo_gemv(const double* M, int64_t ld, int64_t n, const double* x, double xshift, double* y,
+            void* stream);
+
+/* Xs[i][t] = (X[i][t] - center[t]) / lengthscale[t] for t < d, 0 for d <= t < dp
+ * (center may be NULL). */
+int bo_scale_inputs(const double* X, int64_t n, int d, const double* lengthscale,
+                    const double* center, int dp, double* Xs, void* stream);
+
+/* Exact-GP training caches of an eval-mode SingleTaskGP ([G]
+ * DefaultPredictionStrategy.mean_cache / covar_cache, reached at
+ * botorch/models/gpytorch.py:446 under gpt_posterior_settings,
+ * botorch/models/utils/assorted.py:286-298):
+ *   L = psd_safe_cholesky(K + noise I)   (jitter ladder: 0, then jitter0*10^i,
+ *                                          i < max_tries; botorch/__init__.py:47)
+ *   Linv = L^{-1},  U = L^{-T} (covar_cache),
+ *   beta = L^{-1}(y - constant),  alpha = U beta (mean_cache).
+ * Xt: n x d, y: n (standardized targets).  L, Linv, U: np x np device buffers,
+ * beta, alpha: n.  jitter_used: HOST double (may be NULL).  info_dev: device int.
+ * Returns BO_ERR_NOT_PSD when the ladder is exhausted. */
+int bo_gp_cache_build(int kind, const double* Xt, int64_t n, int d, const double* lengthscale,
+                      double outputscale, double noise, double constant, const double* y,
+                      double* L, double* Linv, double* U, double* beta, double* alpha,
+                      int max_tries, double jitter0, double* jitter_used, int* info_dev,
+                      void* stream);
+
+/* Geometry of the fused posterior kernels for B t-batches of q points (1 <= q
+ * <= 16) over n training points: Qp = q rounded up to a power of two,
+ * nrows_pad = roundup(B*Qp, 128) test rows, nC = ceil(n/128) column tiles.
+ * Host pointers. */
+int bo_post_geometry(int64_t B, int q, int64_t n, int* Qp, int* nrows_pad, int* nC);
+
+/* Xq[(b*Qp + a)*8 + t] = X[b][a][t] / lengthscale[t] (X: B x q x d, d <= 8);
+ * Xq: nrows_pad x 8. */
+int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthscale,
+                    double* Xq, void* stream);
+
+/* Fused K*x build + R^T = U^T K*x^T GEMM + R R^T / R beta epilogue
+ * ([G] exact_predictive_mean / exact_predictive_covar under fast_pred_var,
+ * botorch/models/gpytorch.py:446).  Xt_scaled: n x 8 lengthscale-scaled
+ * training inputs; U: >= np x np with leading dim ldu; beta: n.
+ * Spart: nC x (nrows_pad/16) x 16 x 16,  mpart: nC x nrows_pad. */
+int bo_post_partials(int kind, const double* Xq, int B, int q, const double* Xt_scaled,
+                     int64_t n, const double* U, int64_t ldu, const double* beta,
+                     double outputscale, double* Spart, double* mpart, void* stream);
+
+/* Finalise the posterior of each t-batch and (mode != POSTERIOR) run the
+ * fused q x q psd_safe_cholesky + reparameterised sampling + MC reduction:
+ *   mean_out (B x q) = ymean + ystd (constant + R beta)
+ *   cov_out (B x q x q) = ystd^2 (K** - R R^T)       [Standardize.untransform_posterior,
+ *                                                     botorch/models/transforms/outcome.py:373-447]
+ *   L_out (B x q x q), info_out (B), jitter_out (B)  [posteriors/gpytorch.py:85-126]
+ *   acq (B): qEI  mean_s max_a relu(f - best_f)      [acquisition/monte_carlo.py:405-414]
+ *            qNEI mean_s max_a relu(f - best_f_s[s])  [acquisition/monte_carlo.py:580-589]
+ * Z: S x q base samples (SobolQMCNormalSampler, sampling/normal.py:178-209).
+ * Output pointers may be NULL when not needed (acq required for QEI/QNEI). */
+int bo_qmc_finalize(int kind, int mode, int B, int q, const double* Xq, const double* Spart,
+                    const double* mpart, int64_t n, double outputscale, double constant,
+                    double ymean, double ystd, const double* Z, int S, double best_f,
+                    const double* best_f_s, int max_tries, double jitter0, double* acq,
+                    double* mean_out, double* cov_out, double* L_out, int* info_out,
+                    double* jitter_out, void* stream);
+
+/* Scrambled Sobol N(0,1) samples, points skip..skip+n-1: out (n x dim).
+ * state: dim x 30 int64 scrambled direction numbers, shift: dim int64
+ * (torch.quasirandom.SobolEngine(dim, scramble=True, seed) state).
+ * Replaces draw_sobol_normal_samples (botorch/utils/sampling.py:108-137). */
+int bo_sobol_normal(const int64_t* state, const int64_t* shift, int dim, int64_t n,
+                    int64_t skip, double* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BOTORCH_AMD_H */

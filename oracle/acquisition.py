@@ -1,0 +1,140 @@
+"""CPU restatement of the MC (and analytic) acquisition functions on the path.
+
+TEST INFRASTRUCTURE ONLY (see ``oracle/__init__.py``).
+"""
+from __future__ import annotations
+
+import itertools
+import math
+
+import torch
+
+from .gp import ExactGPOracle, psd_safe_cholesky
+from .sampling import draw_sobol_normal_samples
+
+
+def mc_samples(mean, cov, Z):
+    """posteriors/gpytorch.py:85-126 -> [G] MultivariateNormal.rsample with base
+    samples: L = psd_safe_cholesky(Sigma'), f[s,b,i] = mu'[b,i] + sum_j L[b,i,j] Z[s,j]."""
+    L, _ = psd_safe_cholesky(cov)
+    return mean.unsqueeze(0) + torch.einsum("...ij,sj->s...i", L, Z)
+
+
+def qei_from_samples(samples, best_f):
+    """acquisition/monte_carlo.py:405-414 (_sample_forward) + q_reduction=amax,
+    sample_reduction=mean (:246-274)."""
+    return (samples - best_f).clamp_min(0).amax(dim=-1).mean(dim=0)
+
+
+def qei(model: ExactGPOracle, X, Z, best_f):
+    """qExpectedImprovement.forward (acquisition/monte_carlo.py:253-289, 405-414)."""
+    mean, cov = model.posterior(X)
+    return qei_from_samples(mc_samples(mean, cov, Z), best_f)
+
+
+def ei_analytic(model: ExactGPOracle, X, best_f, maximize=True):
+    """ExpectedImprovement.forward (acquisition/analytic.py:338-354, 84-108, 968-972)."""
+    mean, var = model.mean_var(X)
+    mean = mean.squeeze(-1)
+    sigma = var.squeeze(-1).clamp_min(1e-12).sqrt()
+    u = (mean - best_f) / sigma
+    if not maximize:
+        u = -u
+    return sigma * ei_helper(u)
+
+
+def ei_helper(u):
+    """phi(u) + u Phi(u) (analytic.py:968-972; utils/probability/utils.py:133-142)."""
+    phi = torch.exp(-0.5 * u * u) / math.sqrt(2 * math.pi)
+    Phi = 0.5 * torch.erfc(-u / math.sqrt(2))
+    return phi + u * Phi
+
+
+# -- qNEI with cached baseline root ----------------------------------------------
+def prune_inferior_points(model: ExactGPOracle, X, num_samples=2048, seed=0, max_frac=1.0):
+    """acquisition/utils.py:245-349 (unconstrained, identity objective; the
+    sampler seed is made explicit for determinism)."""
+    mean, cov = model.posterior(X)
+    Z = draw_sobol_normal_samples(X.shape[-2], num_samples, seed)
+    samples = mc_samples(mean, cov, Z)  # S x n
+    is_best = torch.argmax(samples, dim=-1)
+    idcs, counts = torch.unique(is_best, return_counts=True)
+    max_points = math.ceil(max_frac * X.size(-2))
+    if len(idcs) > max_points:
+        counts, order_idcs = torch.sort(counts, descending=True)
+        idcs = order_idcs[:max_points]  # reference quirk kept (utils.py:345-347)
+    return X[idcs]
+
+
+class QNEIOracle:
+    """qNoisyExpectedImprovement with cache_root=True (acquisition/monte_carlo.py:
+    441-625, cached_cholesky.py:94-186, utils/low_rank.py:85-173,
+    sampling/normal.py:68-131)."""
+
+    def __init__(self, model: ExactGPOracle, X_baseline, S: int, seed: int):
+        self.model = model
+        self.Xb = X_baseline
+        self.S = S
+        self.seed = seed
+        r = X_baseline.shape[-2]
+        mean_b, cov_b = model.posterior(X_baseline)
+        self.Zb = draw_sobol_normal_samples(r, S, seed)  # S x r
+        Lb, _ = psd_safe_cholesky(cov_b)
+        base_samples = mean_b.unsqueeze(0) + self.Zb @ Lb.mT  # S x r
+        self.best_f = base_samples.amax(dim=-1)  # S
+        self.L_rr = Lb  # root decomposition of the baseline covariance
+        self._zq = {}
+
+    def base_samples_q(self, q):
+        if q not in self._zq:
+            r = self.Xb.shape[-2]
+            full = draw_sobol_normal_samples(r + q, self.S, self.seed)
+            full[:, :r] = self.Zb
+            self._zq[q] = full
+        return self._zq[q]
+
+    def samples(self, X):
+        b, q, d = X.shape
+        r = self.Xb.shape[-2]
+        Xf = torch.cat([self.Xb.expand(b, r, d), X], dim=-2)
+        mean, cov = self.model.posterior(Xf)
+        bottom = cov[..., -q:, :]
+        bl, br = bottom[..., :r], bottom[..., r:]
+        bl_chol = torch.linalg.solve_triangular(self.L_rr, bl.mT, upper=False).mT
+        br_chol, _ = psd_safe_cholesky(br - bl_chol @ bl_chol.mT)
+        Lq = torch.cat([bl_chol, br_chol], dim=-1)  # b x q x (r+q)
+        Z = self.base_samples_q(q)  # S x (r+q)
+        return mean[..., -q:].unsqueeze(0) + torch.einsum("bij,sj->sbi", Lq, Z)
+
+    def __call__(self, X):
+        f = self.samples(X)
+        return (f - self.best_f.view(-1, 1, 1)).clamp_min(0).amax(dim=-1).mean(dim=0)
+
+
+# -- qEHVI -----------------------------------------------------------------------
+def qehvi_from_samples(obj, cell_lower, cell_upper):
+    """qExpectedHypervolumeImprovement._compute_qehvi (multi_objective/
+    monte_carlo.py:230-317): inclusion-exclusion over all nonempty q-subsets,
+    per hypercell; obj is S x b x q x m.  Returns b."""
+    S, b, q, m = obj.shape
+    total = torch.zeros(S, b, cell_lower.shape[0], dtype=obj.dtype)
+    for i in range(1, q + 1):
+        idx = torch.tensor(list(itertools.combinations(range(q), i)), dtype=torch.long)
+        sub = obj[:, :, idx.view(-1), :].view(S, b, idx.shape[0], i, m)
+        ov = sub.min(dim=-2).values  # S x b x C x m
+        ov = torch.minimum(ov.unsqueeze(-3), cell_upper.view(1, 1, -1, 1, m))
+        lengths = (ov - cell_lower.view(1, 1, -1, 1, m)).clamp_min(0.0)
+        areas = lengths.prod(dim=-1).sum(dim=-1)  # S x b x K
+        total += (-1) ** (i + 1) * areas
+    return total.sum(dim=-1).mean(dim=0)
+
+
+def qehvi(models, X, Z, cell_lower, cell_upper):
+    """ModelListGP posterior (independent outputs) + qEHVI.  Z is S x m x q
+    (see sampling.base_samples_multi_output)."""
+    samples = []
+    for t, mdl in enumerate(models):
+        mean, cov = mdl.posterior(X)
+        samples.append(mc_samples(mean, cov, Z[:, t, :]))
+    obj = torch.stack(samples, dim=-1)  # S x b x q x m
+    return qehvi_from_samples(obj, cell_lower, cell_upper)

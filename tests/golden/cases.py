@@ -1,0 +1,19 @@
+"""Fixture case lists shared by make_golden.py and the tests (pure data)."""
+
+# (d, n, seed) triples of the Sobol base samples the configs use:
+#   C2 q=8 S=256, C3 q=16 S=512, C4 q*m=24 S=128, C5 q=4 S=256, small cases.
+SOBOL_NORMAL_CASES = [
+    (1, 4, 0),
+    (3, 16, 1234),
+    (8, 256, 0),
+    (16, 512, 0),
+    (24, 128, 0),
+    (4, 256, 0),
+    (40, 64, 7),
+]
+
+SOBOL_BOX_CASES = [  # (n, q, d, seed)
+    (20, 1, 6, 0),
+    (64, 8, 6, 1),
+    (32, 16, 6, 1),
+]

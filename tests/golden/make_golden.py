@@ -1,0 +1,121 @@
+"""Generate the golden fixtures in ``tests/golden/`` from the reference BoTorch.
+
+Runs ONLY in the development container, where ``/root/reference`` exists.  It
+imports the gpytorch-free leaf modules of the reference (see ``_refload.py``)
+and records their outputs as data (inputs + expected outputs) in
+``golden.npz``.  The fixtures travel to the GPU box; the reference does not.
+
+Usage:  python tests/golden/make_golden.py
+
+Sources (reference file:line):
+  * draw_sobol_normal_samples  botorch/utils/sampling.py:108-137
+    (NormalQMCEngine.draw, botorch/sampling/qmc.py:60-98, inv_transform=True)
+  * draw_sobol_samples         botorch/utils/sampling.py:66-105
+  * Hartmann(dim=6)            botorch/test_functions/synthetic.py:359-455
+  * DTLZ2                      botorch/test_functions/multi_objective.py:420-450
+  * ndtr / phi                 botorch/utils/probability/utils.py:133-142
+  * NondominatedPartitioning / FastNondominatedPartitioning
+                               botorch/utils/multi_objective/box_decompositions/non_dominated.py
+  * is_non_dominated           botorch/utils/multi_objective/pareto.py:16-64
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import _refload  # noqa: E402
+
+from cases import SOBOL_BOX_CASES, SOBOL_NORMAL_CASES  # noqa: E402
+
+
+def main():
+    sampling = _refload.load("botorch.utils.sampling")
+    synth = _refload.load("botorch.test_functions.synthetic")
+    mo = _refload.load("botorch.test_functions.multi_objective")
+    prob = _refload.load("botorch.utils.probability.utils")
+    nd = _refload.load("botorch.utils.multi_objective.box_decompositions.non_dominated")
+    pareto = _refload.load("botorch.utils.multi_objective.pareto")
+
+    out = {}
+    for d, n, seed in SOBOL_NORMAL_CASES:
+        z = sampling.draw_sobol_normal_samples(d=d, n=n, dtype=torch.double, seed=seed)
+        out[f"sobol_normal_d{d}_n{n}_s{seed}"] = z.numpy()
+
+    bounds = torch.stack([torch.zeros(6, dtype=torch.double), torch.ones(6, dtype=torch.double)])
+    for n, q, d, seed in SOBOL_BOX_CASES:
+        b = torch.stack([torch.zeros(d, dtype=torch.double), torch.ones(d, dtype=torch.double)])
+        x = sampling.draw_sobol_samples(bounds=b, n=n, q=q, seed=seed)
+        out[f"sobol_box_n{n}_q{q}_d{d}_s{seed}"] = x.numpy()
+
+    # Hartmann6 (negate=True) on the C1/C2 training designs and a random set.
+    h6 = synth.Hartmann(dim=6, negate=True)
+    for key in ("sobol_box_n20_q1_d6_s0",):
+        X = torch.from_numpy(out[key]).squeeze(1)
+        out["hartmann6_X"] = X.numpy()
+        out["hartmann6_Y"] = h6(X).numpy()
+    g = torch.Generator().manual_seed(3)
+    Xr = torch.rand(257, 6, generator=g, dtype=torch.double)
+    out["hartmann6_rand_X"] = Xr.numpy()
+    out["hartmann6_rand_Y"] = h6(Xr).numpy()
+
+    # DTLZ2 (dim 6, 3 objectives, negate=True) on torch.rand(2048, 6) with seed 0.
+    dtlz = mo.DTLZ2(dim=6, num_objectives=3, negate=True)
+    g = torch.Generator().manual_seed(0)
+    Xd = torch.rand(2048, 6, generator=g, dtype=torch.double)
+    Yd = dtlz(Xd)
+    out["dtlz2_X"] = Xd.numpy()
+    out["dtlz2_Y"] = Yd.numpy()
+    ref = torch.full((3,), -1.1, dtype=torch.double)
+    part = nd.FastNondominatedPartitioning(ref_point=ref, Y=Yd)
+    cb = part.get_hypercell_bounds()
+    out["dtlz2_cells_lower"] = cb[0].numpy()
+    out["dtlz2_cells_upper"] = cb[1].numpy()
+    out["dtlz2_pareto_mask"] = pareto.is_non_dominated(Yd).numpy()
+    out["dtlz2_hv"] = np.array(part.compute_hypervolume().item())
+
+    # A small DTLZ2 subset (used by the fast CPU tests).
+    Ys = Yd[:64]
+    part_s = nd.FastNondominatedPartitioning(ref_point=ref, Y=Ys)
+    cbs = part_s.get_hypercell_bounds()
+    out["dtlz2_small_Y"] = Ys.numpy()
+    out["dtlz2_small_cells_lower"] = cbs[0].numpy()
+    out["dtlz2_small_cells_upper"] = cbs[1].numpy()
+    out["dtlz2_small_hv"] = np.array(part_s.compute_hypervolume().item())
+
+    # Box decompositions used by the reference's qEHVI known-answer tests
+    # (test/acquisition/multi_objective/test_monte_carlo.py:160-510).
+    ehvi_cases = {
+        "m2": ([[4.0, 5.0], [5.0, 5.0], [8.5, 3.5], [8.5, 3.0], [9.0, 1.0]], [0.0, 0.0]),
+        "m3a_refm1": ([[4.0, 2.0, 3.0], [3.0, 5.0, 1.0], [2.0, 4.0, 2.0], [1.0, 3.0, 4.0]], [-1.0] * 3),
+        "m3a_ref0": ([[4.0, 2.0, 3.0], [3.0, 5.0, 1.0], [2.0, 4.0, 2.0], [1.0, 3.0, 4.0]], [0.0] * 3),
+        "m3a_ref1": ([[4.0, 2.0, 3.0], [3.0, 5.0, 1.0], [2.0, 4.0, 2.0], [1.0, 3.0, 4.0]], [1.0] * 3),
+        "m3b_refm1": ([[4.0, 2.0, 3.0], [3.0, 5.0, 1.0], [2.0, 4.0, 2.0]], [-1.0] * 3),
+    }
+    for name, (pY, rp) in ehvi_cases.items():
+        pY = torch.tensor(pY, dtype=torch.double)
+        rp = torch.tensor(rp, dtype=torch.double)
+        for cls_name in ("NondominatedPartitioning", "FastNondominatedPartitioning"):
+            p = getattr(nd, cls_name)(ref_point=rp, Y=pY)
+            lo, hi = p.get_hypercell_bounds()
+            tag = "nd" if cls_name.startswith("Non") else "fnd"
+            out[f"ehvi_{name}_{tag}_lower"] = lo.numpy()
+            out[f"ehvi_{name}_{tag}_upper"] = hi.numpy()
+        out[f"ehvi_{name}_pareto_Y"] = pY.numpy()
+        out[f"ehvi_{name}_ref_point"] = rp.numpy()
+
+    # Normal CDF / PDF.
+    x = torch.linspace(-8, 8, 161, dtype=torch.double)
+    out["ndtr_x"] = x.numpy()
+    out["ndtr_y"] = prob.ndtr(x).numpy()
+    out["phi_y"] = prob.phi(x).numpy()
+
+    path = os.path.join(HERE, "golden.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path}: {len(out)} arrays, {os.path.getsize(path)} bytes")
+
+
+if __name__ == "__main__":
+    main()

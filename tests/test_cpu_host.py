@@ -1,0 +1,43 @@
+"""CPU-side checks: test functions vs. golden, the C ABI library loads and exports."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_hartmann_matches_reference(golden):
+    from botorch_amd.test_functions import Hartmann
+    h = Hartmann(negate=True)
+    for xk, yk in (("hartmann6_X", "hartmann6_Y"), ("hartmann6_rand_X", "hartmann6_rand_Y")):
+        y = h(torch.from_numpy(golden[xk])).numpy()
+        np.testing.assert_array_equal(y, golden[yk])
+
+
+def test_dtlz2_matches_reference(golden):
+    from botorch_amd.test_functions import DTLZ2
+    f = DTLZ2(dim=6, num_objectives=3, negate=True)
+    y = f(torch.from_numpy(golden["dtlz2_X"])).numpy()
+    np.testing.assert_array_equal(y, golden["dtlz2_Y"])
+
+
+def _header_symbols():
+    src = open(os.path.join(ROOT, "include", "botorch_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z0-9_]+\*?\s+\*?(bo_[a-z0-9_]+)\(", src, flags=re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from botorch_amd import _lib
+    syms = _header_symbols()
+    assert len(syms) >= 10
+    handle = ctypes.CDLL(_lib.LIB_PATH)
+    for s in syms:
+        assert hasattr(handle, s), s
+    assert set(syms) == set(_lib.exported_symbols()), set(syms) ^ set(_lib.exported_symbols())
+    lib = _lib.lib()
+    assert lib.bo_version() == 1
+    assert lib.bo_padded_order(4096) == 4096 and lib.bo_padded_order(20) == 128

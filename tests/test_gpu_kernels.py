@@ -1,0 +1,166 @@
+"""HIP kernels through the C ABI vs. the CPU oracle / torch fp64 references."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _hartmann_data(n, seed=0, d=6):
+    from botorch_amd.test_functions import Hartmann
+    from oracle.sampling import draw_sobol_samples
+    lo = torch.zeros(d, dtype=torch.float64)
+    X = draw_sobol_samples(lo, lo + 1, n, 1, seed).squeeze(1)
+    Y = Hartmann(dim=6, negate=True)(X[:, :6]).unsqueeze(-1)
+    return X, Y
+
+
+def test_mfma_f64_layout():
+    from botorch_amd import kernels
+    out = kernels.probe_mfma_layout(DEV).cpu()
+    np.testing.assert_array_equal(out[:, :4].numpy(), out[:, 4:].numpy())
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 64, 64), (130, 70, 33), (300, 257, 129), (1, 5, 3)])
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+def test_gemm_matches_torch(M, N, K, ta, tb):
+    from botorch_amd import kernels
+    g = torch.Generator().manual_seed(M * 7 + N)
+    A = torch.randn(K, M, generator=g, dtype=torch.float64) if ta else torch.randn(M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(N, K, generator=g, dtype=torch.float64) if tb else torch.randn(K, N, generator=g, dtype=torch.float64)
+    C0 = torch.randn(M, N, generator=g, dtype=torch.float64)
+    ref = 0.5 * ((A.T if ta else A) @ (B.T if tb else B)) - 2.0 * C0
+    out = kernels.gemm(A.to(DEV), B.to(DEV), ta, tb, alpha=0.5, beta=-2.0, C=C0.clone().to(DEV))
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-12, atol=1e-11)
+
+
+def test_gemm_batched_and_large():
+    from botorch_amd import kernels
+    g = torch.Generator().manual_seed(1)
+    A = torch.randn(3, 700, 300, generator=g, dtype=torch.float64)
+    B = torch.randn(3, 300, 650, generator=g, dtype=torch.float64)
+    out = kernels.gemm(A.to(DEV), B.to(DEV))
+    torch.testing.assert_close(out.cpu(), A @ B, rtol=1e-12, atol=1e-10)
+    A = torch.randn(2048, 512, generator=g, dtype=torch.float64)
+    B = torch.randn(512, 2048, generator=g, dtype=torch.float64)
+    out = kernels.gemm(A.to(DEV), B.to(DEV))
+    torch.testing.assert_close(out.cpu(), A @ B, rtol=1e-12, atol=1e-10)
+
+
+def test_gemm_triangular_flags():
+    from botorch_amd import kernels, _lib
+    g = torch.Generator().manual_seed(2)
+    n = 200
+    Lw = torch.tril(torch.randn(n, n, generator=g, dtype=torch.float64))
+    B = torch.randn(n, 90, generator=g, dtype=torch.float64)
+    out = kernels.gemm(Lw.to(DEV), B.to(DEV), flags=_lib.GEMM_A_LOWER)
+    torch.testing.assert_close(out.cpu(), Lw @ B, rtol=1e-12, atol=1e-11)
+    P = torch.randn(n, 40, generator=g, dtype=torch.float64)
+    C = torch.randn(n, n, generator=g, dtype=torch.float64)
+    out = kernels.gemm(P.to(DEV), P.to(DEV), False, True, alpha=-1.0, beta=1.0,
+                       C=C.clone().to(DEV), flags=_lib.GEMM_LOWER_C).cpu()
+    ref = C - P @ P.T
+    torch.testing.assert_close(torch.tril(out), torch.tril(ref), rtol=1e-12, atol=1e-11)
+    torch.testing.assert_close(torch.triu(out, 1), torch.triu(C, 1))
+
+
+@pytest.mark.parametrize("n", [20, 128, 333, 1024])
+def test_cholesky_inverse_matches_torch(n):
+    from botorch_amd import kernels
+    g = torch.Generator().manual_seed(n)
+    M = torch.randn(n, n, generator=g, dtype=torch.float64)
+    A = M @ M.T / n + torch.eye(n, dtype=torch.float64)
+    L, Linv, info = kernels.cholesky_inverse(A.to(DEV))
+    assert info == 0
+    Lr = torch.linalg.cholesky(A)
+    torch.testing.assert_close(L.cpu(), Lr, rtol=1e-10, atol=1e-12)
+    torch.testing.assert_close(Linv.cpu(), torch.linalg.inv(Lr), rtol=1e-9, atol=1e-11)
+
+
+def test_cholesky_reports_not_pd():
+    from botorch_amd import kernels
+    A = torch.eye(100, dtype=torch.float64)
+    A[57, 57] = -1.0
+    _, _, info = kernels.cholesky_inverse(A.to(DEV))
+    assert info == 58
+
+
+def _oracle_model(n, d=6, ls=None, noise=1e-3, const=0.1):
+    from oracle.gp import ExactGPOracle, GPHyper
+    X, Y = _hartmann_data(n, d=d)
+    h = GPHyper(ls if ls is not None else torch.full((d,), 0.35, dtype=torch.float64), noise, const)
+    return X, Y, ExactGPOracle(X, Y, h), h
+
+
+def _device_cache(X, Y, h, orc):
+    from botorch_amd import kernels
+    return kernels.build_gp_cache(X.to(DEV), orc.train_y.to(DEV), h.lengthscale.to(DEV),
+                                  h.noise, h.constant)
+
+
+@pytest.mark.parametrize("n", [37, 256, 1000])
+def test_gp_cache_matches_oracle(n):
+    X, Y, orc, h = _oracle_model(n)
+    c = _device_cache(X, Y, h, orc)
+    torch.testing.assert_close(c.U[:n, :n].cpu(), orc.LinvT, rtol=1e-8, atol=1e-9)
+    torch.testing.assert_close(c.alpha.cpu(), orc.alpha, rtol=1e-7, atol=1e-8)
+
+
+@pytest.mark.parametrize("n,B,q", [(37, 5, 3), (256, 33, 8), (300, 64, 16), (1000, 20, 1), (513, 9, 5)])
+def test_posterior_matches_oracle(n, B, q):
+    from botorch_amd import kernels, _lib
+    X, Y, orc, h = _oracle_model(n)
+    c = _device_cache(X, Y, h, orc)
+    g = torch.Generator().manual_seed(B)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64)
+    pp = kernels.post_partials(c, Xc.to(DEV))
+    out = kernels.qmc_finalize(c, pp, _lib.QMC_POSTERIOR, orc.ymean.item(), orc.ystd.item())
+    mean_r, cov_r = orc.posterior(Xc)
+    torch.testing.assert_close(out["mean"].cpu(), mean_r, rtol=1e-4, atol=1e-8)
+    var_r = cov_r.diagonal(dim1=-2, dim2=-1)
+    var = out["cov"].diagonal(dim1=-2, dim2=-1).cpu()
+    torch.testing.assert_close(var, var_r, rtol=1e-4, atol=1e-10)
+    torch.testing.assert_close(out["cov"].cpu(), cov_r, rtol=1e-4, atol=1e-9)
+
+
+@pytest.mark.parametrize("n,B,q,S", [(256, 16, 4, 128), (1024, 64, 8, 256)])
+def test_qei_matches_oracle(n, B, q, S):
+    from botorch_amd import kernels, _lib
+    from oracle.acquisition import qei
+    from oracle.sampling import draw_sobol_normal_samples
+    X, Y, orc, h = _oracle_model(n)
+    c = _device_cache(X, Y, h, orc)
+    g = torch.Generator().manual_seed(q)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64)
+    Z = draw_sobol_normal_samples(q, S, 0)
+    best_f = Y.max().item()
+    pp = kernels.post_partials(c, Xc.to(DEV))
+    out = kernels.qmc_finalize(c, pp, _lib.QMC_QEI, orc.ymean.item(), orc.ystd.item(),
+                               Z=Z.to(DEV), best_f=best_f, want_L=True)
+    ref = qei(orc, Xc, Z, best_f)
+    assert (out["info"].cpu() == 0).all()
+    torch.testing.assert_close(out["acq"].cpu(), ref, rtol=1e-2, atol=1e-6)
+    # much tighter in practice: the same fp64 algorithm
+    torch.testing.assert_close(out["acq"].cpu(), ref, rtol=1e-7, atol=1e-10)
+
+
+@pytest.mark.parametrize("d,n,seed", [(1, 4, 0), (3, 16, 1234), (8, 256, 0), (16, 512, 0), (40, 64, 7)])
+def test_sobol_normal_matches_golden(golden, d, n, seed):
+    from botorch_amd import kernels
+    z = kernels.sobol_normal(d, n, seed, DEV).cpu().numpy()
+    ref = golden[f"sobol_normal_d{d}_n{n}_s{seed}"]
+    np.testing.assert_allclose(z, ref, rtol=0, atol=1e-13)
+
+
+def test_not_psd_raises():
+    from botorch_amd import kernels
+    from botorch_amd.exceptions import NotPSDError
+    X = torch.rand(50, 6, dtype=torch.float64)
+    y = torch.randn(50, dtype=torch.float64)
+    with pytest.raises(NotPSDError):
+        kernels.build_gp_cache(X.to(DEV), y.to(DEV), torch.full((6,), 0.3, dtype=torch.float64, device=DEV),
+                               noise=-1.0, constant=0.0)

@@ -1,0 +1,28 @@
+#!/bin/bash
+# GPU-box driver: each GPU step under its own time limit; a crash, abort or
+# timeout ends the script (test failures, rc=1, do not).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: $name rc=$rc"; exit $rc; fi
+}
+for s in "$@"; do
+  case $s in
+    build) step build 600 make -j16 ;;
+    test) step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
+    testx) step pytest_gpu 1200 python -m pytest tests -m gpu -q -x -rf ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ;;
+    bench_short) step bench 600 python bench.py --steps 10 --warmup 2 ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    *) step custom 900 bash -c "$s" ;;
+  esac
+done
