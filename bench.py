@@ -54,10 +54,16 @@ def flops_post_partials(B, q, n, nrows_pad, nC):
 
 
 def cpu_cores():
+    """Host cores this process may use: the affinity mask, capped by
+    OMP_NUM_THREADS (the GPU box grants a 16-core share of a larger host)."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except Exception:
-        return os.cpu_count()
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        n = min(n, int(omp))
+    return n
 
 
 def cpu_model():
@@ -160,7 +166,7 @@ def main():
             ev[i][1].record(stream)
         out = kernels.qmc_finalize(cache, pp, _lib.QMC_QEI, ymean, ystd, Z=Z, best_f=best_f,
                                    want_mean=False, want_cov=False)
-        torch.max(out["acq"], dim=0, out=(best, torch.empty(1, dtype=torch.int64, device=dev).squeeze(0)))
+        torch.amax(out["acq"], dim=0, keepdim=True, out=best)
         if dist is not None:
             dist.all_reduce(best, op=dist.ReduceOp.MAX)
         return out, pp

@@ -36,7 +36,8 @@ template <int KIND>
 __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     const double* __restrict__ Xq, int nrows, const double* __restrict__ Xt, int n,
     const double* __restrict__ U, int64_t ldu, const double* __restrict__ beta,
-    double outputscale, int nC, int nI, double* __restrict__ Spart, double* __restrict__ mpart) {
+    double outputscale, int nC, int nI, double* __restrict__ Spart, double* __restrict__ mpart,
+    double* __restrict__ Rt) {
   __shared__ __attribute__((aligned(16))) double Us[PK][PLD];
   __shared__ __attribute__((aligned(16))) double Ks[PK][PLD];
 
@@ -134,6 +135,21 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   // Epilogue: R R^T diagonal blocks and R beta for this workgroup's columns.
   const int nrows16 = nI * (PI / 16);
   const int nrows_pad = nI * PI;
+  if (Rt != nullptr) {
+    // Gradient path: keep R^T (column c, test row i; ld = nrows_pad) for the
+    // backward's W = R L^{-1}... product.  Lanes 0-15 hold consecutive test rows,
+    // so each store instruction writes 128-B contiguous row segments.
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = c0 + ct * 16 + mfma_row(lane, r);
+          const int i = i0 + wave * 32 + it * 16 + mfma_col(lane);
+          Rt[(int64_t)c * nrows_pad + i] = acc[ct][it][r];
+        }
+  }
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     v4d P = v4d_zero();
@@ -206,7 +222,8 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
 
 int bo_post_partials(int kind, const double* Xq, int B, int q, const double* Xt_scaled,
                      int64_t n, const double* U, int64_t ldu, const double* beta,
-                     double outputscale, double* Spart, double* mpart, void* stream) {
+                     double outputscale, double* Spart, double* mpart, double* Rt,
+                     void* stream) {
   BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
   BO_CHECK_ARG(ldu % 2 == 0 && ldu >= ceil_div(n, PC) * PC, "U leading dim %lld too small",
                (long long)ldu);
@@ -219,10 +236,10 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, const double* Xt_
   hipStream_t st = as_stream(stream);
   if (kind == BO_RBF)
     post_partials_kernel<BO_RBF><<<(unsigned)blocks, 256, 0, st>>>(
-        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart);
+        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt);
   else
     post_partials_kernel<BO_MATERN52><<<(unsigned)blocks, 256, 0, st>>>(
-        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart);
+        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

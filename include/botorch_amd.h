@@ -129,10 +129,12 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
  * ([G] exact_predictive_mean / exact_predictive_covar under fast_pred_var,
  * botorch/models/gpytorch.py:446).  Xt_scaled: n x 8 lengthscale-scaled
  * training inputs; U: >= np x np with leading dim ldu; beta: n.
- * Spart: nC x (nrows_pad/16) x 16 x 16,  mpart: nC x nrows_pad. */
+ * Spart: nC x (nrows_pad/16) x 16 x 16,  mpart: nC x nrows_pad.
+ * Rt (nullable, gradient path): R^T, (nC*128) x nrows_pad. */
 int bo_post_partials(int kind, const double* Xq, int B, int q, const double* Xt_scaled,
                      int64_t n, const double* U, int64_t ldu, const double* beta,
-                     double outputscale, double* Spart, double* mpart, void* stream);
+                     double outputscale, double* Spart, double* mpart, double* Rt,
+                     void* stream);
 
 /* Finalise the posterior of each t-batch and (mode != POSTERIOR) run the
  * fused q x q psd_safe_cholesky + reparameterised sampling + MC reduction:
