@@ -46,7 +46,7 @@ def _dist_env():
     return ws, rank, local
 
 
-def flops_post_partials(B, q, n, nrows_pad, nC):
+def flops_post_partials(B, q, n):
     """Algorithmic flops of one post_partials launch:
     triangular R = K*x L^{-T}: (B q) n^2; R R^T diagonal blocks: 2 B q^2 n;
     R beta: 2 B q n; kernel rows: B q n (3 d + 3)."""
@@ -122,12 +122,57 @@ def cpu_baseline(Xtr, Ytr, Xc, best_f, budget_s=20.0):
     }
 
 
+def time_gp_fit(Xtr, Ytr, dev, cpu=True):
+    """GP-fit half of the metric: fit_gpytorch_mll (L-BFGS-B, exact MLL + gradient on
+    the device) from BoTorch's default initialisation, n=4096, d=6.  CPU side: one
+    closure (exact MLL + autograd gradient, torch fp64 restatement) on the host."""
+    from botorch_amd import fit as fitmod
+    from botorch_amd.models import SingleTaskGP
+    model = SingleTaskGP(Xtr.to(dev), Ytr.to(dev))
+    mll = fitmod.ExactMarginalLogLikelihood(model.likelihood, model)
+    calls = [0]
+    orig = fitmod.mll_value_and_grad
+
+    def counted(*a, **k):
+        calls[0] += 1
+        return orig(*a, **k)
+
+    fitmod.mll_value_and_grad = counted
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    fitmod.fit_gpytorch_mll(mll)
+    torch.cuda.synchronize(dev)
+    ms = 1e3 * (time.perf_counter() - t0)
+    fitmod.mll_value_and_grad = orig
+    out = {"ms": ms, "closures": calls[0], "ms_per_closure": ms / max(1, calls[0]),
+           "n": int(Xtr.shape[0]), "lengthscale": model.covar_module.lengthscale.detach().reshape(-1).tolist(),
+           "noise": float(model.likelihood.noise)}
+    if cpu:
+        from oracle.gp import neg_mll, standardize_fit
+        torch.set_num_threads(cpu_cores())
+        mu, sd = standardize_fit(Ytr)
+        y = ((Ytr - mu) / sd).squeeze(-1)
+        times = []
+        for _ in range(3):
+            ls = torch.full((D,), 0.5016, dtype=torch.float64, requires_grad=True)
+            nz = torch.tensor(6.7e-3, dtype=torch.float64, requires_grad=True)
+            c = torch.tensor(0.0, dtype=torch.float64, requires_grad=True)
+            t0 = time.perf_counter()
+            neg_mll(Xtr, y, ls, nz, c).backward()
+            times.append(time.perf_counter() - t0)
+        out["cpu_ms_per_closure"] = 1e3 * sorted(times)[1]
+        out["cpu_cores"] = torch.get_num_threads()
+        out["cpu_fit_ms_estimate"] = out["cpu_ms_per_closure"] * calls[0]
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fit", action="store_true", help="skip the GP-fit half of the metric")
     args = ap.parse_args()
 
     ws, rank, local = _dist_env()
@@ -138,8 +183,10 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    from botorch_amd import _lib, kernels
+    from botorch_amd import kernels
+    from botorch_amd.acquisition import qExpectedImprovement
     from botorch_amd.models import SingleTaskGP
+    from botorch_amd.sampling import SobolQMCNormalSampler
 
     Xtr, Ytr, Xc = build_problem(dev, RESTARTS, seed_offset=rank)
     best_f = Ytr.max().item()
@@ -148,38 +195,41 @@ def main():
     model.likelihood.noise = torch.tensor([NOISE], dtype=torch.float64)
     model.mean_module.constant = torch.tensor(CONSTANT, dtype=torch.float64)
     model.eval()
-    cache = model.prediction_cache()
-    ymean, ystd = model.outcome_stats()
-    Z = kernels.sobol_normal(Q, MC, 0, dev)
+    model.prediction_cache()  # the reference builds its caches on the first eval call
+    acqf = qExpectedImprovement(model, best_f, sampler=SobolQMCNormalSampler(torch.Size([MC]), seed=0))
     Xd = Xc.to(dev)
 
     stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    ev = {"post_partials_begin": [], "post_partials_end": []}
+
+    def hook(tag):
+        if timing[0]:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            ev[tag].append(e)
+
+    timing = [False]
+    kernels.TIMING_HOOK = hook
     best = torch.empty(1, dtype=torch.float64, device=dev)
 
     def step(i=None):
-        if i is not None:
-            ev[i][0].record(stream)
-        pp = kernels.post_partials(cache, Xd)
-        if i is not None:
-            ev[i][1].record(stream)
-        out = kernels.qmc_finalize(cache, pp, _lib.QMC_QEI, ymean, ystd, Z=Z, best_f=best_f,
-                                   want_mean=False, want_cov=False)
-        torch.amax(out["acq"], dim=0, keepdim=True, out=best)
+        with torch.no_grad():
+            acq = acqf(Xd)
+        torch.amax(acq, dim=0, keepdim=True, out=best)
         if dist is not None:
             dist.all_reduce(best, op=dist.ReduceOp.MAX)
-        return out, pp
+        return acq
 
     for _ in range(args.warmup):
-        out, pp = step()
+        step()
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    timing[0] = True
     t0 = time.perf_counter()
     for i in range(args.steps):
-        out, pp = step(i)
+        step(i)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -193,12 +243,16 @@ def main():
     evals_per_step = Q * RESTARTS * MC * ws
     value = evals_per_step * args.steps / elapsed
 
-    kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
+    timing[0] = False
+    kern_ms = sorted(a.elapsed_time(b) for a, b in zip(ev["post_partials_begin"], ev["post_partials_end"]))
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
-    fl = flops_post_partials(RESTARTS, Q, N_TRAIN, pp.nrows_pad, pp.nC)
+    fl = flops_post_partials(RESTARTS, Q, N_TRAIN)
     achieved = fl / (kern_avg_ms * 1e-3) / 1e12
     peak = 78.6  # MI355X dense FP64 matrix TFLOP/s (MI355X_MICROARCH.md / SURVEY.md 8(d))
 
+    gp_fit = None
+    if rank == 0 and not args.no_fit:
+        gp_fit = time_gp_fit(Xtr, Ytr, dev, cpu=(not args.no_cpu_baseline and ws == 1))
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and ws == 1:
@@ -225,6 +279,7 @@ def main():
                          "frac": achieved / peak, "traffic": None,
                          "kernel_ms": kern_avg_ms, "flops_per_launch": fl},
             "cpu_baseline": cpu,
+            "gp_fit": gp_fit,
         }
         if cpu:
             line["speedup_vs_cpu"] = value / cpu["value"]

@@ -26,6 +26,7 @@ _SIGNATURES = {
     "bo_last_error": (ctypes.c_char_p, []),
     "bo_version": (c_int, []),
     "bo_probe_mfma_f64_layout": (c_int, [_P, _P]),
+    "bo_probe_mfma_f64_rate": (c_int, [c_int, c_int, _P, _P]),
     "bo_gemm_f64": (c_int, [c_int, c_int, c_int, c_int, c_int, c_double, _P, c_int64, c_int64,
                             _P, c_int64, c_int64, c_double, _P, c_int64, c_int64, c_int, c_int,
                             _P]),
@@ -34,6 +35,11 @@ _SIGNATURES = {
     "bo_padded_order": (c_int64, [c_int64]),
     "bo_cholesky_inverse": (c_int, [_P, _P, _P, c_int64, _P, _P]),
     "bo_transpose": (c_int, [_P, _P, c_int64, c_int64, _P]),
+    "bo_cholesky_jitter": (c_int, [_P, c_int64, _P, _P, _P, c_int, c_double, POINTER(c_double),
+                                   _P, _P]),
+    "bo_chol_small": (c_int, [_P, c_int64, c_int, c_int, c_double, _P, _P, _P, _P]),
+    "bo_covar_blocks": (c_int, [c_int, _P, c_int64, c_int, c_int, _P, c_double, c_double, _P,
+                                _P]),
     "bo_gemv": (c_int, [_P, c_int64, c_int64, _P, c_double, _P, _P]),
     "bo_scale_inputs": (c_int, [_P, c_int64, c_int, _P, _P, c_int, _P, _P]),
     "bo_gp_cache_build": (c_int, [c_int, _P, c_int64, c_int, _P, c_double, c_double, c_double,
@@ -42,12 +48,18 @@ _SIGNATURES = {
     "bo_post_geometry": (c_int, [c_int64, c_int, c_int64, POINTER(c_int), POINTER(c_int),
                                  POINTER(c_int)]),
     "bo_prepare_rows": (c_int, [_P, c_int, c_int, c_int, _P, _P, _P]),
-    "bo_post_partials": (c_int, [c_int, _P, c_int, c_int, _P, c_int64, _P, c_int64, _P,
-                                 c_double, _P, _P, _P]),
+    "bo_post_partials": (c_int, [c_int, _P, c_int, c_int, c_int, _P, c_int64, _P, c_int64, _P,
+                                 c_double, _P, _P, _P, _P]),
     "bo_qmc_finalize": (c_int, [c_int, c_int, c_int, c_int, _P, _P, _P, c_int64, c_double,
                                 c_double, c_double, c_double, _P, c_int, c_double, _P, c_int,
                                 c_double, _P, _P, _P, _P, _P, _P, _P]),
     "bo_sobol_normal": (c_int, [_P, _P, c_int, c_int64, c_int64, _P, _P]),
+    "bo_mll_terms": (c_int, [c_int, _P, c_int64, c_int, _P, c_double, _P, _P, c_int64, _P, _P, _P,
+                             _P]),
+    "bo_qmc_backward": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, c_double, _P, _P, _P,
+                                _P, _P]),
+    "bo_post_backward": (c_int, [c_int, c_int, c_int, c_int, _P, _P, c_int64, _P, c_int64, _P,
+                                 _P, _P, _P, c_double, c_double, _P, _P]),
 }
 
 _lib = None

@@ -1,0 +1,238 @@
+"""Acquisition functions on the accelerated path (BoTorch-compatible API).
+
+MC family: acquisition/monte_carlo.py:60-645 (SampleReducingMCAcquisitionFunction,
+qExpectedImprovement, qNoisyExpectedImprovement); multi-objective qEHVI:
+acquisition/multi_objective/monte_carlo.py:146-322; analytic EI / PI / UCB:
+acquisition/analytic.py.
+
+For a SingleTaskGP with the identity objective and no constraints, ``forward``
+runs the fused gfx950 path -- post_partials (K*x + R = K*x L^{-T} + R R^T on
+the fp64 matrix cores) and qmc_finalize (q x q psd_safe_cholesky, Sobol
+reparameterisation, q-max / sample-mean reduction) -- as one autograd node whose
+backward is bo_qmc_backward + bo_post_backward.  Other objectives / models take
+the generic route (device posterior -> sampler -> torch reduction).
+"""
+from __future__ import annotations
+
+import math
+import warnings
+from typing import Callable, List, Optional, Union
+
+import torch
+from torch import nn
+
+from . import _lib, kernels
+from .exceptions import BotorchWarning, UnsupportedError
+from .posteriors import FUSED_QMAX
+from .sampling import MCSampler, SobolQMCNormalSampler, get_sampler
+
+
+# -- input handling (utils/transforms.py:146-336) -----------------------------
+def t_batch_mode(X: torch.Tensor, expected_q: Optional[int] = None) -> torch.Tensor:
+    if X.dim() == 2:
+        X = X.unsqueeze(0)
+    if expected_q is not None and X.shape[-2] != expected_q:
+        raise AssertionError(f"Expected X to be `batch_shape x q={expected_q} x d`, but got X with shape {tuple(X.shape)}.")
+    return X
+
+
+class AcquisitionFunction(nn.Module):
+    """acquisition/acquisition.py:33-74."""
+
+    def __init__(self, model):
+        super().__init__()
+        self.model = model
+        self.X_pending = None
+
+    def set_X_pending(self, X_pending: Optional[torch.Tensor] = None) -> None:
+        if X_pending is not None:
+            if X_pending.requires_grad:
+                warnings.warn("Pending points require a gradient but the acquisition function"
+                              " will not provide a gradient to these points.", BotorchWarning)
+            self.X_pending = X_pending.detach().clone()
+        else:
+            self.X_pending = X_pending
+
+    def _concat_pending(self, X: torch.Tensor) -> torch.Tensor:
+        """utils/transforms.py:312-336."""
+        if self.X_pending is not None:
+            Xp = self.X_pending.to(X).expand(*X.shape[:-2], *self.X_pending.shape[-2:])
+            X = torch.cat([X, Xp], dim=-2)
+        return X
+
+
+class MCObjective:
+    pass
+
+
+class IdentityMCObjective(MCObjective):
+    """acquisition/objective.py:288-298."""
+
+    def __call__(self, samples, X=None):
+        return samples.squeeze(-1)
+
+
+class MCAcquisitionFunction(AcquisitionFunction):
+    _default_sample_shape = torch.Size([512])
+
+    def __init__(self, model, sampler: Optional[MCSampler] = None, objective=None,
+                 posterior_transform=None, X_pending=None):
+        super().__init__(model)
+        if objective is None and model.num_outputs != 1 and posterior_transform is None:
+            raise UnsupportedError("Must specify an objective or a posterior transform when "
+                                   "using a multi-output model.")
+        self.sampler = sampler
+        self.objective = objective if objective is not None else IdentityMCObjective()
+        self.posterior_transform = posterior_transform
+        self.set_X_pending(X_pending)
+
+    @property
+    def sample_shape(self) -> torch.Size:
+        return self.sampler.sample_shape if self.sampler is not None else self._default_sample_shape
+
+    def _ensure_sampler(self, posterior=None):
+        if self.sampler is None:
+            self.sampler = get_sampler(posterior, sample_shape=self._default_sample_shape)
+        return self.sampler
+
+    def get_posterior_samples(self, posterior):
+        """acquisition/acquisition.py:109-146."""
+        return self._ensure_sampler(posterior)(posterior)
+
+    def _fused_eligible(self, X: torch.Tensor) -> bool:
+        m = self.model
+        return (hasattr(m, "prediction_cache") and isinstance(self.objective, IdentityMCObjective)
+                and self.posterior_transform is None and X.shape[-2] <= FUSED_QMAX
+                and X.shape[-1] <= kernels.DP and X.is_cuda
+                and len(self.sample_shape) == 1)
+
+
+class _FusedMC(torch.autograd.Function):
+    """qEI / qNEI value of B t-batches as one autograd node on the gfx950 path."""
+
+    @staticmethod
+    def forward(ctx, X3, acqf, mode, best_f, best_f_s, Z):
+        model = acqf.model
+        cache = model.prediction_cache()
+        ymean, ystd = model.outcome_stats()
+        need_grad = ctx.needs_input_grad[0]
+        if kernels.TIMING_HOOK is not None:
+            kernels.TIMING_HOOK("post_partials_begin")
+        pp = kernels.post_partials(cache, X3.detach(), store_R=need_grad)
+        if kernels.TIMING_HOOK is not None:
+            kernels.TIMING_HOOK("post_partials_end")
+        out = kernels.qmc_finalize(cache, pp, mode, ymean, ystd, Z=Z, best_f=best_f,
+                                   best_f_s=best_f_s, want_mean=need_grad, want_cov=False,
+                                   want_L=need_grad)
+        kernels._raise_not_psd(out["info"], out["jitter"], type(acqf).__name__)
+        if need_grad:
+            ctx.cache, ctx.pp, ctx.ystd, ctx.mode = cache, pp, ystd, mode
+            ctx.best_f, ctx.best_f_s, ctx.Z = best_f, best_f_s, Z
+            ctx.mean, ctx.L = out["mean"], out["L"]
+            ctx.W = kernels.w_matrix(cache, pp)
+        return out["acq"]
+
+    @staticmethod
+    def backward(ctx, dacq):
+        dmean, dcov = kernels.qmc_backward(ctx.mode, ctx.mean, ctx.L, ctx.Z, dacq.contiguous(),
+                                           ctx.best_f, ctx.best_f_s)
+        dX = kernels.post_backward(ctx.cache, ctx.pp, ctx.W, dmean, dcov, ctx.ystd)
+        return dX, None, None, None, None, None
+
+
+class qExpectedImprovement(MCAcquisitionFunction):
+    """MC batch EI (acquisition/monte_carlo.py:332-414):
+    qEI(X) = E[max_j max(Y_j - best_f, 0)]."""
+
+    def __init__(self, model, best_f: Union[float, torch.Tensor], sampler=None, objective=None,
+                 posterior_transform=None, X_pending=None, constraints=None, eta=1e-3):
+        super().__init__(model, sampler, objective, posterior_transform, X_pending)
+        if constraints is not None:
+            raise UnsupportedError("outcome constraints are not on the accelerated path")
+        self.register_buffer("best_f", torch.as_tensor(best_f, dtype=torch.float64))
+
+    def forward(self, X: torch.Tensor) -> torch.Tensor:
+        X = self._concat_pending(t_batch_mode(X))
+        batch = X.shape[:-2]
+        q, d = X.shape[-2], X.shape[-1]
+        X3 = X.reshape(-1, q, d)
+        if self._fused_eligible(X) and self.best_f.numel() == 1:
+            sampler = self._ensure_sampler()
+            Z = sampler.base_samples_2d(q, X.device)
+            acq = _FusedMC.apply(X3, self, _lib.QMC_QEI, float(self.best_f), None, Z)
+            return acq.reshape(batch)
+        posterior = self.model.posterior(X, posterior_transform=self.posterior_transform)
+        samples = self.get_posterior_samples(posterior)
+        obj = self.objective(samples, X=X)
+        bf = self.best_f.to(obj).unsqueeze(-1)
+        return (obj - bf).clamp_min(0).amax(dim=-1).mean(dim=0)
+
+
+# -- analytic ------------------------------------------------------------------------
+def _ndtr(x):
+    return 0.5 * torch.erfc(-x / math.sqrt(2))
+
+
+def _phi(x):
+    return torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+
+
+class AnalyticAcquisitionFunction(AcquisitionFunction):
+    def __init__(self, model, posterior_transform=None):
+        super().__init__(model)
+        self.posterior_transform = posterior_transform
+
+    def _mean_and_sigma(self, X, compute_sigma=True, min_var=1e-12):
+        """acquisition/analytic.py:84-108."""
+        posterior = self.model.posterior(X, posterior_transform=self.posterior_transform)
+        mean = posterior.mean.squeeze(-2).squeeze(-1)
+        if not compute_sigma:
+            return mean, None
+        sigma = posterior.variance.clamp_min(min_var).sqrt().view(mean.shape)
+        return mean, sigma
+
+
+class ExpectedImprovement(AnalyticAcquisitionFunction):
+    """acquisition/analytic.py:298-354: sigma (phi(u) + u Phi(u)), u = (mu - best_f)/sigma."""
+
+    def __init__(self, model, best_f, posterior_transform=None, maximize=True):
+        super().__init__(model, posterior_transform)
+        self.register_buffer("best_f", torch.as_tensor(best_f, dtype=torch.float64))
+        self.maximize = maximize
+
+    def forward(self, X):
+        X = t_batch_mode(X, expected_q=1)
+        mean, sigma = self._mean_and_sigma(X)
+        u = (mean - self.best_f.to(mean)) / sigma
+        if not self.maximize:
+            u = -u
+        return sigma * (_phi(u) + u * _ndtr(u))
+
+
+class ProbabilityOfImprovement(AnalyticAcquisitionFunction):
+    """acquisition/analytic.py (PI): Phi((mu - best_f)/sigma)."""
+
+    def __init__(self, model, best_f, posterior_transform=None, maximize=True):
+        super().__init__(model, posterior_transform)
+        self.register_buffer("best_f", torch.as_tensor(best_f, dtype=torch.float64))
+        self.maximize = maximize
+
+    def forward(self, X):
+        X = t_batch_mode(X, expected_q=1)
+        mean, sigma = self._mean_and_sigma(X)
+        u = (mean - self.best_f.to(mean)) / sigma
+        return _ndtr(u if self.maximize else -u)
+
+
+class UpperConfidenceBound(AnalyticAcquisitionFunction):
+    """acquisition/analytic.py (UCB): mu + sqrt(beta) sigma."""
+
+    def __init__(self, model, beta, posterior_transform=None, maximize=True):
+        super().__init__(model, posterior_transform)
+        self.register_buffer("beta", torch.as_tensor(beta, dtype=torch.float64))
+        self.maximize = maximize
+
+    def forward(self, X):
+        X = t_batch_mode(X, expected_q=1)
+        mean, sigma = self._mean_and_sigma(X)
+        return (mean if self.maximize else -mean) + self.beta.to(mean).sqrt() * sigma

@@ -328,3 +328,152 @@ int bo_gp_cache_build(int kind, const double* Xt, int64_t n, int d, const double
 }
 
 }  // extern "C"
+
+namespace {
+
+// K[b][a][c] = outputscale * k(X[b][a], X[b][c]) (+ diag_add on a == c),
+// X: B x q x d.  One thread per entry.
+template <int KIND>
+__global__ void covar_blocks_kernel(const double* __restrict__ X, int64_t B, int q, int d,
+                                    const double* __restrict__ ls, double outputscale,
+                                    double diag_add, double* __restrict__ K) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * q * q) return;
+  const int64_t b = idx / ((int64_t)q * q);
+  const int a = (int)((idx / q) % q), c = (int)(idx % q);
+  double v;
+  if (a == c) {
+    v = outputscale + diag_add;
+  } else {
+    const double* xa = X + (b * q + a) * d;
+    const double* xc = X + (b * q + c) * d;
+    double d2 = 0.0;
+    for (int t = 0; t < d; ++t) {
+      const double df = (xa[t] - xc[t]) / ls[t];
+      d2 = fma(df, df, d2);
+    }
+    v = outputscale * kernel_from_d2<KIND>(d2);
+  }
+  K[idx] = v;
+}
+
+// Batched small Cholesky (q <= 64) with the [G] jitter ladder per member:
+// one 64-thread workgroup per matrix, lane i owns row i in LDS.
+__global__ __launch_bounds__(64) void chol_small_kernel(const double* __restrict__ A, int q,
+                                                        int max_tries, double jitter0,
+                                                        double* __restrict__ L,
+                                                        int* __restrict__ info_out,
+                                                        double* __restrict__ jitter_out) {
+  __shared__ double M[64][65];
+  __shared__ int s_fail;
+  const int64_t b = blockIdx.x;
+  const int i = threadIdx.x;
+  const double* Ab = A + b * q * q;
+  double jit = 0.0;
+  int info = 0;
+  for (int attempt = 0; attempt <= max_tries; ++attempt) {
+    if (attempt > 0) jit = jitter0 * pow(10.0, (double)(attempt - 1));
+    if (i < q)
+      for (int c = 0; c < q; ++c) M[i][c] = (c <= i) ? Ab[i * q + c] + ((c == i) ? jit : 0.0) : 0.0;
+    if (i == 0) s_fail = 0;
+    __syncthreads();
+    for (int j = 0; j < q; ++j) {
+      const double ajj = M[j][j];
+      if (i == 0 && !(ajj > 0.0) && s_fail == 0) s_fail = j + 1;
+      const double djj = sqrt(ajj);
+      __syncthreads();
+      if (i == j) M[j][j] = djj;
+      if (i > j && i < q) M[i][j] = M[i][j] / djj;
+      __syncthreads();
+      if (i > j && i < q) {
+        const double lij = M[i][j];
+        for (int l = j + 1; l <= i; ++l) M[i][l] = fma(-lij, M[l][j], M[i][l]);
+      }
+      __syncthreads();
+    }
+    info = s_fail;
+    __syncthreads();
+    if (info == 0) break;
+  }
+  if (i < q)
+    for (int c = 0; c < q; ++c) L[(b * q + i) * q + c] = info ? NAN : ((c <= i) ? M[i][c] : 0.0);
+  if (i == 0) {
+    if (info_out) info_out[b] = info;
+    if (jitter_out) jitter_out[b] = jit;
+  }
+}
+
+// Keep the lower triangle of the n x n block, add jitter on its diagonal,
+// identity on the pad diagonal.
+__global__ void tril_jitter_kernel(double* __restrict__ L, int64_t n, int64_t np, double jitter) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= np * np) return;
+  const int64_t i = idx / np, j = idx % np;
+  if (i < n && j < n) {
+    if (j > i) L[idx] = 0.0;
+    else if (i == j) L[idx] += jitter;
+  } else if (i == j) {
+    L[idx] = 1.0;
+  }
+}
+
+}  // namespace
+
+extern "C" int bo_covar_blocks(int kind, const double* X, int64_t B, int q, int d,
+                               const double* lengthscale, double outputscale, double diag_add,
+                               double* K, void* stream) {
+  const int64_t tot = B * q * q;
+  if (tot == 0) return BO_OK;
+  hipStream_t st = as_stream(stream);
+  if (kind == BO_RBF)
+    covar_blocks_kernel<BO_RBF><<<(unsigned)ceil_div(tot, 256), 256, 0, st>>>(X, B, q, d, lengthscale, outputscale, diag_add, K);
+  else
+    covar_blocks_kernel<BO_MATERN52><<<(unsigned)ceil_div(tot, 256), 256, 0, st>>>(X, B, q, d, lengthscale, outputscale, diag_add, K);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+extern "C" int bo_chol_small(const double* A, int64_t B, int q, int max_tries, double jitter0,
+                             double* L, int* info, double* jitter, void* stream) {
+  BO_CHECK_ARG(q >= 1 && q <= 64, "bo_chol_small: q=%d (1..64)", q);
+  if (B == 0) return BO_OK;
+  chol_small_kernel<<<(unsigned)B, 64, 0, as_stream(stream)>>>(A, q, max_tries, jitter0, L, info,
+                                                              jitter);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+// Large single-matrix psd_safe_cholesky: factor (A + jitter I) for the ladder
+// 0, jitter0, 10 jitter0, ... (one host read of the status per attempt).
+// A: n x n (lower part read), L / Linv / work: np x np.
+extern "C" int bo_cholesky_jitter(const double* A, int64_t n, double* L, double* Linv,
+                                  double* work, int max_tries, double jitter0,
+                                  double* jitter_used, int* info_dev, void* stream) {
+  hipStream_t st = as_stream(stream);
+  const int64_t np = bo_padded_order(n);
+  double jitter = 0.0;
+  int info_h = 0;
+  for (int attempt = 0; attempt <= max_tries; ++attempt) {
+    if (attempt > 0) jitter = jitter0 * std::pow(10.0, (double)(attempt - 1));
+    // L <- tril(A) + jitter I, identity pad
+    BO_HIP(hipMemsetAsync(L, 0, sizeof(double) * np * np, st));
+    BO_HIP(hipMemcpy2DAsync(L, np * sizeof(double), A, n * sizeof(double), n * sizeof(double), n,
+                            hipMemcpyDeviceToDevice, st));
+    {
+      const int64_t tot = np * np;
+      tril_jitter_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, st>>>(L, n, np, jitter);
+      BO_LAUNCH_CHECK();
+    }
+    int s = bo_cholesky_inverse(L, Linv, work, np, info_dev, (void*)st);
+    if (s) return s;
+    BO_HIP(hipMemcpyAsync(&info_h, info_dev, sizeof(int), hipMemcpyDeviceToHost, st));
+    BO_HIP(hipStreamSynchronize(st));
+    if (info_h == 0) break;
+  }
+  if (jitter_used) *jitter_used = jitter;
+  if (info_h != 0) {
+    bo_set_error("Matrix not positive definite after repeatedly adding jitter up to %.1e", jitter);
+    return BO_ERR_NOT_PSD;
+  }
+  return BO_OK;
+}

@@ -1,0 +1,278 @@
+// Backward of the fused qEI/qNEI forward and of the batched exact posterior.
+//
+// gen_candidates_scipy differentiates -acqf(X).sum() w.r.t. X once per
+// L-BFGS-B iteration (botorch/generation/gen.py:194-222).  The chain is
+//   reduction (one-hot q-argmax of relu(f - best_f), 1/S)  ->  d mu', d L_q
+//   -> Cholesky backward (torch's linalg.cholesky backward, Murray 2016)  -> d Sigma'
+//   -> Standardize: d mu* = s d mu', d Sigma* = s^2 d Sigma'
+//   -> exact prediction: mu* = c + K*x alpha,  Sigma* = K** - K*x A^{-1} K*x^T
+//        d K*x = d mu* alpha^T - G W,   G = d Sigma* + d Sigma*^T,
+//        W = K*x A^{-1} = R L^{-1}  (computed on the gradient path of the forward)
+//        d K** = d Sigma*
+//   -> kernel derivative  dk/dx_i = -k (x_i - x_k)/ell^2 (RBF) and the
+//      Matern-5/2 form, reduced over the training points.
+// The model caches carry no gradient (detach_test_caches, botorch/models/
+// utils/assorted.py:286-298), so nothing flows to L^{-1} or alpha.
+#include "common.h"
+
+namespace {
+
+constexpr int QMAX = 16;
+constexpr int DP = 8;
+constexpr int THREADS = 256;
+constexpr int SMAX = 4096;  // samples staged in LDS per pass (winner masks)
+
+enum { MODE_QEI = 1, MODE_QNEI = 2 };
+
+// dk(x_i, x_k)/dx_i (scaled coordinates), as a factor g with dk = g * (x_i - x_k).
+template <int KIND>
+__device__ __forceinline__ double dkernel_factor(double d2, double outputscale) {
+  if (KIND == BO_RBF) {
+    return -outputscale * exp(-0.5 * d2);
+  } else {
+    const double r = sqrt(fmax(d2, 0.0));
+    const double s5r = 2.23606797749978969641 * r;
+    return -outputscale * (5.0 / 3.0) * (1.0 + s5r) * exp(-s5r);
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
+    int q, const double* __restrict__ mean, const double* __restrict__ Lq,
+    const double* __restrict__ Z, int S, double best_f, const double* __restrict__ best_f_s,
+    const double* __restrict__ dacq, double* __restrict__ dmean, double* __restrict__ dcov) {
+  __shared__ double L[QMAX][QMAX + 1];
+  __shared__ double Li[QMAX][QMAX + 1];   // L^{-1}
+  __shared__ double dL[QMAX][QMAX + 1];
+  __shared__ double Pm[QMAX][QMAX + 1];
+  __shared__ double Tm[QMAX][QMAX + 1];
+  __shared__ double mu[QMAX];
+  __shared__ unsigned short win[SMAX];
+  __shared__ double wgt[SMAX];
+
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (tid < q * q) {
+    const int a = tid / q, c = tid % q;
+    L[a][c] = Lq[((int64_t)b * q + a) * q + c];
+  }
+  if (tid < q) mu[tid] = mean[(int64_t)b * q + tid];
+  __syncthreads();
+  const double g = dacq[b] / (double)S;
+
+  double dmu_acc = 0.0, dl_acc = 0.0;
+  // thread (a, j), j <= a, accumulates dL[a][j]; threads 0..q-1 also dmu.
+  int ta = -1, tj = -1;
+  if (tid < q * q) {
+    ta = tid / q;
+    tj = tid % q;
+  }
+  for (int s0 = 0; s0 < S; s0 += SMAX) {
+    const int ns = min(SMAX, S - s0);
+    // Pass 1: the winning (maximal, non-clamped) q-index set per sample.
+    for (int s = tid; s < ns; s += THREADS) {
+      const double* z = Z + (int64_t)(s0 + s) * q;
+      const double bf = (MODE == MODE_QNEI) ? best_f_s[s0 + s] : best_f;
+      double v[QMAX];
+      double m = 0.0;
+#pragma unroll
+      for (int a = 0; a < QMAX; ++a) {
+        if (a < q) {
+          double f = mu[a];
+          for (int j = 0; j <= a; ++j) f = fma(L[a][j], z[j], f);
+          v[a] = f - bf;
+          m = fmax(m, fmax(v[a], 0.0));
+        }
+      }
+      // torch: amax splits the gradient evenly among all maximal entries;
+      // clamp_min(0) passes it where f - best_f >= 0.
+      unsigned mask = 0, cnt = 0;
+#pragma unroll
+      for (int a = 0; a < QMAX; ++a) {
+        if (a < q && fmax(v[a], 0.0) == m) {
+          ++cnt;
+          if (v[a] >= 0.0) mask |= 1u << a;
+        }
+      }
+      win[s] = (unsigned short)mask;
+      wgt[s] = cnt ? g / (double)cnt : 0.0;
+    }
+    __syncthreads();
+    // Pass 2: deterministic accumulation per (a, j).
+    if (ta >= 0 && tj <= ta) {
+      for (int s = 0; s < ns; ++s) {
+        if (win[s] & (1u << ta)) {
+          const double w = wgt[s];
+          dl_acc = fma(w, Z[(int64_t)(s0 + s) * q + tj], dl_acc);
+          if (tj == 0) dmu_acc += w;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (ta >= 0) {
+    dL[ta][tj] = (tj <= ta) ? dl_acc : 0.0;
+    if (tj == 0) dmean[(int64_t)b * q + ta] = dmu_acc;
+  }
+  // L^{-1} by forward substitution, one column per thread.
+  if (tid < q) {
+    const int c = tid;
+    for (int r = 0; r < q; ++r) {
+      double s = (r == c) ? 1.0 : 0.0;
+      for (int k = c; k < r; ++k) s = fma(-L[r][k], Li[k][c], s);
+      Li[r][c] = (r >= c) ? s / L[r][r] : 0.0;
+    }
+  }
+  __syncthreads();
+  // X = tril(L^T dL);  P = 0.5 (X + tril(X, -1)^T)   (torch cholesky_backward)
+  if (tid < q * q) {
+    const int i = tid / q, j = tid % q;
+    const int lo = i > j ? i : j;
+    double x = 0.0;
+    for (int k = lo; k < q; ++k) x = fma(L[k][i], dL[k][j], x);  // (L^T dL)[i][j]
+    // store X lower-only at [max][min]
+    if (i >= j) Tm[i][j] = x;
+  }
+  __syncthreads();
+  if (tid < q * q) {
+    const int i = tid / q, j = tid % q;
+    Pm[i][j] = 0.5 * ((i >= j) ? Tm[i][j] : Tm[j][i]);
+  }
+  __syncthreads();
+  // gA = L^{-T} P L^{-1}:  T = P L^{-1}, then gA = L^{-T} T
+  if (tid < q * q) {
+    const int i = tid / q, j = tid % q;
+    double x = 0.0;
+    for (int k = j; k < q; ++k) x = fma(Pm[i][k], Li[k][j], x);
+    Tm[i][j] = x;
+  }
+  __syncthreads();
+  if (tid < q * q) {
+    const int i = tid / q, j = tid % q;
+    double x = 0.0;
+    for (int k = i; k < q; ++k) x = fma(Li[k][i], Tm[k][j], x);
+    dcov[((int64_t)b * q + i) * q + j] = x;
+  }
+}
+
+// dX for one t-batch per workgroup.  TPA threads per test row a, striding k.
+template <int KIND, int ND>
+__global__ __launch_bounds__(THREADS) void post_backward_kernel(
+    int q, int Qp, const double* __restrict__ Xq, const double* __restrict__ Xt, int n,
+    const double* __restrict__ W, int64_t ldw, const double* __restrict__ alpha,
+    const double* __restrict__ dmean, const double* __restrict__ dcov,
+    const double* __restrict__ ls, double outputscale, double ystd, int d,
+    double* __restrict__ dX) {
+  __shared__ double G[QMAX][QMAX + 1];
+  __shared__ double dmu[QMAX];
+  __shared__ double xs[QMAX][DP];
+  __shared__ double red[THREADS][DP + 1];
+
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int row0 = b * Qp;
+  const double s2 = ystd * ystd;
+  if (tid < q * q) {
+    const int a = tid / q, c = tid % q;
+    const double* dc = dcov + (int64_t)b * q * q;
+    G[a][c] = s2 * (dc[a * q + c] + dc[c * q + a]);
+  }
+  if (tid < q) dmu[tid] = ystd * dmean[(int64_t)b * q + tid];
+  if (tid < q * DP) xs[tid / DP][tid % DP] = Xq[(int64_t)(row0 + tid / DP) * DP + tid % DP];
+  __syncthreads();
+
+  const int TPA = THREADS / Qp;
+  const int a = tid / TPA;
+  const int kk = tid % TPA;
+  double acc[ND];
+#pragma unroll
+  for (int t = 0; t < ND; ++t) acc[t] = 0.0;
+  if (a < q) {
+    double xa[ND];
+#pragma unroll
+    for (int t = 0; t < ND; ++t) xa[t] = xs[a][t];
+    const double dma = dmu[a];
+    for (int k = kk; k < n; k += TPA) {
+      double D = dma * alpha[k];
+      for (int j = 0; j < q; ++j) D = fma(-G[a][j], W[(int64_t)(row0 + j) * ldw + k], D);
+      const double* xt = Xt + (int64_t)k * DP;
+      double diff[ND];
+      double d2 = 0.0;
+#pragma unroll
+      for (int t = 0; t < ND; ++t) {
+        diff[t] = xa[t] - xt[t];
+        d2 = fma(diff[t], diff[t], d2);
+      }
+      const double f = D * dkernel_factor<KIND>(d2, outputscale);
+#pragma unroll
+      for (int t = 0; t < ND; ++t) acc[t] = fma(f, diff[t], acc[t]);
+    }
+    // K** terms: Sigma*[a][c] = K**(a, c) - ..., d K** = d Sigma* (c != a; the
+    // diagonal is the constant outputscale).
+    if (kk == 0) {
+      for (int c = 0; c < q; ++c) {
+        if (c == a) continue;
+        double diff[ND];
+        double d2 = 0.0;
+#pragma unroll
+        for (int t = 0; t < ND; ++t) {
+          diff[t] = xa[t] - xs[c][t];
+          d2 = fma(diff[t], diff[t], d2);
+        }
+        const double f = G[a][c] * dkernel_factor<KIND>(d2, outputscale);
+#pragma unroll
+        for (int t = 0; t < ND; ++t) acc[t] = fma(f, diff[t], acc[t]);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < ND; ++t) red[tid][t] = acc[t];
+  __syncthreads();
+  if (tid < q * d) {
+    const int ra = tid / d, t = tid % d;
+    double s = 0.0;
+    for (int u = 0; u < TPA; ++u) s += red[ra * TPA + u][t];
+    dX[((int64_t)b * q + ra) * d + t] = s / ls[t];
+  }
+}
+
+}  // namespace
+
+extern "C" int bo_qmc_backward(int mode, int B, int q, const double* mean, const double* Lq,
+                               const double* Z, int S, double best_f, const double* best_f_s,
+                               const double* dacq, double* dmean, double* dcov, void* stream) {
+  BO_CHECK_ARG(q >= 1 && q <= QMAX, "bo_qmc_backward: q=%d out of range", q);
+  BO_CHECK_ARG(mode == MODE_QEI || mode == MODE_QNEI, "bo_qmc_backward: bad mode %d", mode);
+  if (B == 0) return BO_OK;
+  hipStream_t st = as_stream(stream);
+  if (mode == MODE_QEI)
+    qmc_backward_kernel<MODE_QEI><<<B, THREADS, 0, st>>>(q, mean, Lq, Z, S, best_f, best_f_s, dacq, dmean, dcov);
+  else
+    qmc_backward_kernel<MODE_QNEI><<<B, THREADS, 0, st>>>(q, mean, Lq, Z, S, best_f, best_f_s, dacq, dmean, dcov);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+extern "C" int bo_post_backward(int kind, int B, int q, int d, const double* Xq,
+                                const double* Xt_scaled, int64_t n, const double* W, int64_t ldw,
+                                const double* alpha, const double* dmean, const double* dcov,
+                                const double* lengthscale, double outputscale, double ystd,
+                                double* dX, void* stream) {
+  BO_CHECK_ARG(q >= 1 && q <= QMAX && d >= 1 && d <= DP, "bo_post_backward: bad q/d");
+  if (B == 0) return BO_OK;
+  int Qp = 1;
+  while (Qp < q) Qp *= 2;
+  hipStream_t st = as_stream(stream);
+#define BO_PB(KIND, ND)                                                                      \
+  post_backward_kernel<KIND, ND><<<B, THREADS, 0, st>>>(q, Qp, Xq, Xt_scaled, (int)n, W, ldw, \
+                                                        alpha, dmean, dcov, lengthscale,      \
+                                                        outputscale, ystd, d, dX)
+  if (kind == BO_RBF) {
+    if (d == 6) BO_PB(BO_RBF, 6); else BO_PB(BO_RBF, 8);
+  } else {
+    if (d == 6) BO_PB(BO_MATERN52, 6); else BO_PB(BO_MATERN52, 8);
+  }
+#undef BO_PB
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}

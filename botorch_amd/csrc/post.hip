@@ -32,14 +32,33 @@ constexpr int PK = 16;    // k-step
 constexpr int PLD = 144;  // LDS row pitch (doubles): 2 x 144 dwords = 32 mod 64 banks
 constexpr int DP = 8;     // padded input dimension held in registers
 
-template <int KIND>
+// One kernel value k(x_i, x_k) from scaled coordinates (0 beyond n / invalid rows).
+template <int KIND, int ND>
+__device__ __forceinline__ double eval_kernel_row(const double (&xi)[ND], const double* __restrict__ Xt,
+                                                  int n, int k, double outputscale, bool ivalid) {
+  if (k >= n || !ivalid) return 0.0;
+  const double* xt = Xt + (int64_t)k * DP;
+  double d2 = 0.0;
+#pragma unroll
+  for (int t = 0; t < ND; ++t) {
+    const double df = xi[t] - xt[t];
+    d2 = fma(df, df, d2);
+  }
+  return outputscale * kernel_from_d2<KIND>(d2);
+}
+
+template <int KIND, int ND>
 __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     const double* __restrict__ Xq, int nrows, const double* __restrict__ Xt, int n,
     const double* __restrict__ U, int64_t ldu, const double* __restrict__ beta,
     double outputscale, int nC, int nI, double* __restrict__ Spart, double* __restrict__ mpart,
     double* __restrict__ Rt) {
-  __shared__ __attribute__((aligned(16))) double Us[PK][PLD];
-  __shared__ __attribute__((aligned(16))) double Ks[PK][PLD];
+  // Two LDS stages: while the MFMAs consume stage t, the U rows of step t+1
+  // are in flight to registers and this thread evaluates its 8 kernel values
+  // of step t+1 between the MFMAs (VALU work hidden under the matrix pipe);
+  // one barrier per k-step.
+  __shared__ __attribute__((aligned(16))) double Us[2][PK][PLD];
+  __shared__ __attribute__((aligned(16))) double Ks[2][PK][PLD];
 
   // XCD-aware schedule: consecutive block ids are dealt round-robin over the
   // 8 XCDs, so block b and b+8 share an L2.  XCD x takes the column tiles
@@ -58,6 +77,7 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   const int c0 = ci * PC;
   const int i0 = ii * PI;
   const int kend = min(n, c0 + PC);
+  const int nsteps = (kend + PK - 1) / PK;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -68,9 +88,9 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   const int ti = tid & (PI - 1);
   const int kh = __builtin_amdgcn_readfirstlane(tid >> 7);
   const bool ivalid = (i0 + ti) < nrows;
-  double xi[DP];
+  double xi[ND];
 #pragma unroll
-  for (int t = 0; t < DP; ++t) xi[t] = ivalid ? Xq[(int64_t)(i0 + ti) * DP + t] : 0.0;
+  for (int t = 0; t < ND; ++t) xi[t] = ivalid ? Xq[(int64_t)(i0 + ti) * DP + t] : 0.0;
 
   v4d acc[8][2];
 #pragma unroll
@@ -79,58 +99,61 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     acc[a][1] = v4d_zero();
   }
 
-  double2 ru[4];
-  auto load_u = [&](int k0) {
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int e = tid + p * 256;
-      const int r = e >> 6;
-      const int cp = e & 63;
-      ru[p] = *reinterpret_cast<const double2*>(U + (int64_t)(k0 + r) * ldu + c0 + 2 * cp);
-    }
-  };
+  // Per-thread staging registers: 4 x 16 B of U rows, 8 kernel values.
+  double u0x, u0y, u1x, u1y, u2x, u2y, u3x, u3y;
+  double kv[8];
+  const int urow = tid >> 6;          // + 4 p
+  const int ucol = c0 + 2 * (tid & 63);
+#define BO_LOAD_U(K0)                                                             \
+  {                                                                               \
+    const double* src = U + (int64_t)((K0) + urow) * ldu + ucol;                  \
+    const double2 v0 = *reinterpret_cast<const double2*>(src);                    \
+    const double2 v1 = *reinterpret_cast<const double2*>(src + 4 * ldu);          \
+    const double2 v2 = *reinterpret_cast<const double2*>(src + 8 * ldu);          \
+    const double2 v3 = *reinterpret_cast<const double2*>(src + 12 * ldu);         \
+    u0x = v0.x; u0y = v0.y; u1x = v1.x; u1y = v1.y;                               \
+    u2x = v2.x; u2y = v2.y; u3x = v3.x; u3y = v3.y;                               \
+  }
+#define BO_STORE(BUF)                                                             \
+  {                                                                               \
+    double* dst = &Us[BUF][urow][2 * (tid & 63)];                                 \
+    *reinterpret_cast<double2*>(dst) = make_double2(u0x, u0y);                    \
+    *reinterpret_cast<double2*>(dst + 4 * PLD) = make_double2(u1x, u1y);          \
+    *reinterpret_cast<double2*>(dst + 8 * PLD) = make_double2(u2x, u2y);          \
+    *reinterpret_cast<double2*>(dst + 12 * PLD) = make_double2(u3x, u3y);         \
+    _Pragma("unroll") for (int kk = 0; kk < 8; ++kk) Ks[BUF][kh * 8 + kk][ti] = kv[kk]; \
+  }
 
-  load_u(0);
-  for (int k0 = 0; k0 < kend; k0 += PK) {
-    __syncthreads();
+  BO_LOAD_U(0);
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int e = tid + p * 256;
-      *reinterpret_cast<double2*>(&Us[e >> 6][2 * (e & 63)]) = ru[p];
-    }
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int r = kh * 8 + kk;
-      const int k = k0 + r;
-      double v = 0.0;
-      if (k < n) {
-        const double* xt = Xt + (int64_t)k * DP;
-        double d2 = 0.0;
-#pragma unroll
-        for (int t = 0; t < DP; ++t) {
-          const double df = xi[t] - xt[t];
-          d2 = fma(df, df, d2);
-        }
-        v = outputscale * kernel_from_d2<KIND>(d2);
-      }
-      Ks[r][ti] = ivalid ? v : 0.0;
-    }
-    __syncthreads();
-    if (k0 + PK < kend) load_u(k0 + PK);
+  for (int kk = 0; kk < 8; ++kk) kv[kk] = eval_kernel_row<KIND, ND>(xi, Xt, n, kh * 8 + kk, outputscale, ivalid);
+  BO_STORE(0);
+  __syncthreads();
+  for (int t = 0; t < nsteps; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < nsteps;
+    const int knext = more ? (t + 1) * PK : t * PK;  // last step re-reads (unused)
+    BO_LOAD_U(knext);
 #pragma unroll
     for (int ks = 0; ks < PK / 4; ++ks) {
       const int kr = ks * 4 + (lane >> 4);
       double a[8], b[2];
 #pragma unroll
-      for (int ct = 0; ct < 8; ++ct) a[ct] = Us[kr][ct * 16 + (lane & 15)];
+      for (int ct = 0; ct < 8; ++ct) a[ct] = Us[cur][kr][ct * 16 + (lane & 15)];
 #pragma unroll
-      for (int it = 0; it < 2; ++it) b[it] = Ks[kr][wave * 32 + it * 16 + (lane & 15)];
+      for (int it = 0; it < 2; ++it) b[it] = Ks[cur][kr][wave * 32 + it * 16 + (lane & 15)];
 #pragma unroll
       for (int ct = 0; ct < 8; ++ct)
 #pragma unroll
         for (int it = 0; it < 2; ++it) acc[ct][it] = mfma_f64(a[ct], b[it], acc[ct][it]);
+      kv[2 * ks] = eval_kernel_row<KIND, ND>(xi, Xt, n, knext + kh * 8 + 2 * ks, outputscale, ivalid);
+      kv[2 * ks + 1] = eval_kernel_row<KIND, ND>(xi, Xt, n, knext + kh * 8 + 2 * ks + 1, outputscale, ivalid);
     }
+    if (more) BO_STORE(cur ^ 1);
+    __syncthreads();
   }
+#undef BO_LOAD_U
+#undef BO_STORE
 
   // Epilogue: R R^T diagonal blocks and R beta for this workgroup's columns.
   const int nrows16 = nI * (PI / 16);
@@ -220,8 +243,8 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
   return BO_OK;
 }
 
-int bo_post_partials(int kind, const double* Xq, int B, int q, const double* Xt_scaled,
-                     int64_t n, const double* U, int64_t ldu, const double* beta,
+int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
+                     const double* Xt_scaled, int64_t n, const double* U, int64_t ldu, const double* beta,
                      double outputscale, double* Spart, double* mpart, double* Rt,
                      void* stream) {
   BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
@@ -232,14 +255,31 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, const double* Xt_
   if (s) return s;
   const int nI = nrows_pad / PI;
   const int nrows = B * Qp;
+  BO_CHECK_ARG(d >= 1 && d <= DP, "fused posterior kernel supports 1 <= d <= %d", DP);
   const int64_t blocks = 8 * ceil_div(nC, 8) * (int64_t)nI;
   hipStream_t st = as_stream(stream);
-  if (kind == BO_RBF)
-    post_partials_kernel<BO_RBF><<<(unsigned)blocks, 256, 0, st>>>(
-        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt);
-  else
-    post_partials_kernel<BO_MATERN52><<<(unsigned)blocks, 256, 0, st>>>(
-        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt);
+  // One instantiation per active input dimension (the padded coordinates
+  // beyond d are zero, so fewer distance terms are exact, not approximate).
+#define BO_POST_LAUNCH(KIND, ND)                                                          \
+  post_partials_kernel<KIND, ND><<<(unsigned)blocks, 256, 0, st>>>(                       \
+      Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt)
+#define BO_POST_DISPATCH_D(KIND)                   \
+  switch (d) {                                     \
+    case 1: BO_POST_LAUNCH(KIND, 1); break;        \
+    case 2: BO_POST_LAUNCH(KIND, 2); break;        \
+    case 3: BO_POST_LAUNCH(KIND, 3); break;        \
+    case 4: BO_POST_LAUNCH(KIND, 4); break;        \
+    case 5: BO_POST_LAUNCH(KIND, 5); break;        \
+    case 6: BO_POST_LAUNCH(KIND, 6); break;        \
+    default: BO_POST_LAUNCH(KIND, 8); break;       \
+  }
+  if (kind == BO_RBF) {
+    BO_POST_DISPATCH_D(BO_RBF)
+  } else {
+    BO_POST_DISPATCH_D(BO_MATERN52)
+  }
+#undef BO_POST_DISPATCH_D
+#undef BO_POST_LAUNCH
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

@@ -17,7 +17,31 @@ __global__ void probe_kernel(double* out) {
     out[lane * 8 + 4 + r] = (double)(mfma_row(lane, r) * 16 + mfma_col(lane));
   }
 }
+// Peak-rate probe: every wave issues `iters` x 8 independent back-to-back
+// v_mfma_f64_16x16x4_f64 (operands in registers), 4 waves per CU-slot.
+__global__ __launch_bounds__(256) void rate_kernel(int iters, double* out) {
+  const int lane = threadIdx.x & 63;
+  double a = 1.0 + 1e-3 * lane, b = 1.0 - 1e-3 * lane;
+  v4d acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = v4d_zero();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = mfma_f64(a, b, acc[j]);
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+  if (s == 12345.678) out[0] = s;  // keep live
+}
 }  // namespace
+
+// flops = blocks * 4 waves * iters * 8 * 2048
+extern "C" int bo_probe_mfma_f64_rate(int blocks, int iters, double* out, void* stream) {
+  rate_kernel<<<blocks, 256, 0, as_stream(stream)>>>(iters, out);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
 
 extern "C" int bo_probe_mfma_f64_layout(double* out, void* stream) {
   probe_kernel<<<1, 64, 0, as_stream(stream)>>>(out);

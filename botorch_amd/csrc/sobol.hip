@@ -51,7 +51,10 @@ __device__ double erfinv_accurate(double y) {
   double x = p * y;
   const double k = 1.1283791670955126;  // 2 / sqrt(pi)
   for (int it = 0; it < 3; ++it) {
-    const double f = (ay < 0.5) ? erf(x) - y : -copysign(erfc(fabs(x)) - (1.0 - ay), y);
+    // erf(x) - y, written through erfc in the tails:  y > 0: (1 - y) - erfc(x),
+    // y < 0: erfc(|x|) - (1 - |y|).
+    const double f = (ay < 0.5) ? erf(x) - y
+                                : (erfc(fabs(x)) - (1.0 - ay)) * (y < 0.0 ? 1.0 : -1.0);
     const double fp = k * exp(-x * x);
     x = x - f / (fp + x * f);
   }

@@ -1,0 +1,193 @@
+"""GP hyperparameter fitting: fit_gpytorch_mll with an on-device exact MLL.
+
+Reference: botorch/fit.py:75-258 (fit_gpytorch_mll -> _fit_fallback: up to 5
+attempts, prior resampling between attempts, rollback, NotPSDError caught),
+optim/fit.py:47-110 (fit_gpytorch_mll_scipy: L-BFGS-B with bounds from the
+constraints, optim/utils/model_utils.py:69-109) and the closure
+optim/closures/model_closures.py:171-184 (-[G] ExactMarginalLogLikelihood).
+
+Each closure call: kernel matrix + blocked MFMA Cholesky with the jitter ladder
++ explicit inverse (bo_gp_cache_build), A^{-1} = U U^T (triangular MFMA GEMM),
+one pass of bo_mll_terms; the host reads back n x (d+5) row sums and forms
+the loss and its exact gradient (plus the LogNormal prior terms).
+"""
+from __future__ import annotations
+
+import math
+import time
+import warnings
+from typing import Optional
+
+import numpy as np
+import torch
+from scipy.optimize import minimize
+
+from . import _lib, kernels
+from ._lib import check, lib
+from .exceptions import NotPSDError, OptimizationWarning
+from .models import LogNormalPrior, ScaleKernel, SingleTaskGP
+
+
+class ExactMarginalLogLikelihood:
+    """[G] ExactMarginalLogLikelihood(likelihood, model)."""
+
+    def __init__(self, likelihood, model: SingleTaskGP):
+        self.likelihood = likelihood
+        self.model = model
+
+    def train(self):
+        self.model.train()
+        return self
+
+    def eval(self):
+        self.model.eval()
+        return self
+
+    @property
+    def training(self):
+        return self.model.training
+
+
+def _prior_terms(prior: Optional[LogNormalPrior], x: np.ndarray):
+    if prior is None:
+        return 0.0, np.zeros_like(x)
+    lx = np.log(x)
+    val = np.sum(-((lx - prior.loc) ** 2) / (2 * prior.scale ** 2) - math.log(prior.scale)
+                 - 0.5 * math.log(2 * math.pi) - lx)
+    grad = -(lx - prior.loc) / (prior.scale ** 2 * x) - 1.0 / x
+    return float(val), grad
+
+
+class _Layout:
+    """Flat parameter vector <-> model hyperparameters (order of
+    get_parameters_and_bounds: noise, constant, lengthscales[, outputscale])."""
+
+    def __init__(self, model: SingleTaskGP):
+        self.model = model
+        self.d = model.train_inputs[0].shape[-1]
+        self.has_os = isinstance(model.covar_module, ScaleKernel)
+        base = model.covar_module.base_kernel if self.has_os else model.covar_module
+        self.base = base
+        lo = [model.likelihood.noise_lower, -np.inf] + [base.lengthscale_lower] * self.d
+        if self.has_os:
+            lo.append(0.0)
+        self.bounds = [(None if not np.isfinite(l) else l, None) for l in lo]
+
+    def get(self) -> np.ndarray:
+        m = self.model
+        v = [float(m.likelihood.noise), float(m.mean_module.constant)]
+        v += self.base.lengthscale.detach().reshape(-1).cpu().tolist()
+        if self.has_os:
+            v.append(float(m.covar_module.outputscale))
+        return np.asarray(v, dtype=np.float64)
+
+    def set(self, x: np.ndarray) -> None:
+        m = self.model
+        m.likelihood.noise = torch.tensor([x[0]])
+        m.mean_module.constant = float(x[1])
+        self.base.lengthscale = torch.as_tensor(x[2:2 + self.d]).reshape(1, -1)
+        if self.has_os:
+            m.covar_module.outputscale = float(x[2 + self.d])
+
+
+def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout):
+    """Loss = -(log N(y | c, K + s2 I) + log priors) / n and its gradient."""
+    layout.set(x)
+    Xt = model.train_inputs[0]
+    y = model.train_targets
+    n, d = Xt.shape
+    noise, const = x[0], x[1]
+    ls = x[2:2 + d]
+    os_ = x[2 + d] if layout.has_os else 1.0
+    dev = Xt.device
+    ls_t = torch.as_tensor(ls, dtype=torch.float64, device=dev)
+    cache = kernels.build_gp_cache(Xt, y, ls_t, noise, const, kind=model.kind, outputscale=os_)
+    # A^{-1} = U U^T: lower triangle only, triangular operands (n^3/3 flops).
+    Ainv = torch.empty(cache.np, cache.np, dtype=torch.float64, device=dev)
+    st = kernels._stream(dev)
+    check(lib().bo_gemm_f64(0, 1, cache.np, cache.np, cache.np, 1.0, kernels._p(cache.U), cache.np,
+                            0, kernels._p(cache.U), cache.np, 0, 0.0, kernels._p(Ainv), cache.np, 0,
+                            1, _lib.GEMM_LOWER_C | _lib.GEMM_A_UPPER | _lib.GEMM_B_LOWER, st), "Ainv")
+    part = torch.empty(n, d + 5, dtype=torch.float64, device=dev)
+    check(lib().bo_mll_terms(model.kind, kernels._p(Xt.contiguous()), n, d, kernels._p(ls_t), os_,
+                             kernels._p(cache.L), kernels._p(Ainv), cache.np,
+                             kernels._p(cache.alpha), kernels._p(cache.beta), kernels._p(part), st),
+          "mll_terms")
+    s = part.sum(dim=0).cpu().numpy()
+    quad, logdet_half, sum_alpha = s[d + 3], s[d + 2], s[d + 4]
+    ll = -0.5 * quad - logdet_half - 0.5 * n * math.log(2 * math.pi)
+    g = np.zeros_like(x)
+    g[0] = 0.5 * s[d]                       # d ll / d noise
+    g[1] = sum_alpha                        # d ll / d constant
+    g[2:2 + d] = 0.5 * s[:d] / ls ** 3      # d ll / d lengthscale
+    if layout.has_os:
+        g[2 + d] = 0.5 * s[d + 1]
+    pv, pg = _prior_terms(model.likelihood.noise_prior, np.array([noise]))
+    ll += pv
+    g[0] += pg[0]
+    pv, pg = _prior_terms(layout.base.lengthscale_prior, ls)
+    ll += pv
+    g[2:2 + d] += pg
+    return -ll / n, -g / n
+
+
+def fit_gpytorch_mll_scipy(mll: ExactMarginalLogLikelihood, method="L-BFGS-B", options=None,
+                           callback=None, timeout_sec=None):
+    model = mll.model
+    layout = _Layout(model)
+    x0 = layout.get()
+
+    def f(x):
+        return mll_value_and_grad(model, x, layout)
+
+    res = minimize(f, x0, jac=True, method=method, bounds=layout.bounds, options=options or {},
+                   callback=callback)
+    layout.set(res.x)
+    if not res.success:
+        warnings.warn(f"`scipy_minimize` terminated with status {res.status}, displaying original "
+                      f"message from `scipy.optimize.minimize`: {res.message}", OptimizationWarning)
+    return res
+
+
+def _sample_all_priors(model: SingleTaskGP, layout: _Layout, gen: torch.Generator):
+    """sample_all_priors: draw free hyperparameters from their priors."""
+    x = layout.get()
+    base = layout.base
+    if model.likelihood.noise_prior is not None:
+        p = model.likelihood.noise_prior
+        x[0] = max(math.exp(p.loc + p.scale * torch.randn(1, generator=gen).item()),
+                   model.likelihood.noise_lower)
+    if base.lengthscale_prior is not None:
+        p = base.lengthscale_prior
+        z = torch.randn(layout.d, generator=gen, dtype=torch.float64).numpy()
+        x[2:2 + layout.d] = np.maximum(np.exp(p.loc + p.scale * z), base.lengthscale_lower)
+    layout.set(x)
+
+
+def fit_gpytorch_mll(mll: ExactMarginalLogLikelihood, optimizer_kwargs=None, max_attempts=5,
+                     **kwargs) -> ExactMarginalLogLikelihood:
+    """botorch/fit.py:75-258 (_fit_fallback)."""
+    optimizer_kwargs = optimizer_kwargs or {}
+    model = mll.model
+    mll.train()
+    layout = _Layout(model)
+    gen = torch.Generator().manual_seed(0)
+    ckpt = layout.get()
+    for attempt in range(1, max_attempts + 1):
+        if attempt > 1:
+            layout.set(ckpt)
+            _sample_all_priors(model, layout, gen)
+        try:
+            with warnings.catch_warnings(record=True) as ws:
+                warnings.simplefilter("always", category=OptimizationWarning)
+                fit_gpytorch_mll_scipy(mll, **optimizer_kwargs)
+            bad = [w for w in ws if issubclass(w.category, OptimizationWarning)
+                   and "ITERATIONS REACHED LIMIT" not in str(w.message).upper()
+                   and "timed out" not in str(w.message)]
+            if not bad:
+                return mll.eval()
+        except NotPSDError:
+            pass
+    layout.set(ckpt)
+    warnings.warn("All attempts to fit the model have failed.", OptimizationWarning)
+    return mll

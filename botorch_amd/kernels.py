@@ -21,6 +21,10 @@ DP = 8  # padded input dimension of the fused posterior kernel
 CHOLESKY_MAX_TRIES = 6  # botorch/__init__.py:47
 CHOLESKY_JITTER_F64 = 1e-8  # [G] linear_operator.settings.cholesky_jitter (double)
 
+# Optional callable(tag) invoked around the dominant kernel (bench.py records
+# HIP events on the current stream through it).
+TIMING_HOOK = None
+
 
 def _p(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
@@ -161,6 +165,7 @@ class PostPartials:
     Xq: torch.Tensor
     Spart: torch.Tensor
     mpart: torch.Tensor
+    Rt: Optional[torch.Tensor] = None  # R^T (nC*128 x nrows_pad) on the gradient path
 
 
 def geometry(B: int, q: int, n: int):
@@ -170,7 +175,7 @@ def geometry(B: int, q: int, n: int):
     return Qp.value, nrows.value, nC.value
 
 
-def post_partials(cache: GPCache, X: torch.Tensor) -> PostPartials:
+def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False) -> PostPartials:
     """Column-tile partials of R R^T and R beta for X (B x q x d)."""
     dev = _dev(X)
     B, q, d = X.shape
@@ -184,10 +189,11 @@ def post_partials(cache: GPCache, X: torch.Tensor) -> PostPartials:
     st = _stream(dev)
     check(lib().bo_prepare_rows(_p(X.contiguous()), B, q, d, _p(cache.lengthscale), _p(Xq), st),
           "prepare_rows")
-    check(lib().bo_post_partials(cache.kind, _p(Xq), B, q, _p(cache.Xt_scaled), cache.n,
+    Rt = torch.empty(nC * 128, nrows_pad, **f64) if store_R else None
+    check(lib().bo_post_partials(cache.kind, _p(Xq), B, q, d, _p(cache.Xt_scaled), cache.n,
                                  _p(cache.U), cache.np, _p(cache.beta), cache.outputscale,
-                                 _p(Spart), _p(mpart), st), "post_partials")
-    return PostPartials(B, q, Qp, nrows_pad, nC, Xq, Spart, mpart)
+                                 _p(Spart), _p(mpart), _p(Rt), st), "post_partials")
+    return PostPartials(B, q, Qp, nrows_pad, nC, Xq, Spart, mpart, Rt)
 
 
 def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd: float,
@@ -237,3 +243,123 @@ def probe_mfma_layout(device) -> torch.Tensor:
     out = torch.empty(64, 8, dtype=torch.float64, device=device)
     check(lib().bo_probe_mfma_f64_layout(_p(out), _stream(torch.device(device))), "probe")
     return out
+
+
+def w_matrix(cache: GPCache, pp: PostPartials) -> torch.Tensor:
+    """W = R L^{-1} = K*x (K + s2 I)^{-1}  (nrows_pad x np), from the stored R^T:
+    W[i][k] = sum_c R[i][c] U[k][c]  (U = L^{-T} upper -> op(B) zero below c < k)."""
+    if pp.Rt is None:
+        raise RuntimeError("post_partials(store_R=True) is required for gradients")
+    dev = pp.Rt.device
+    W = torch.empty(pp.nrows_pad, cache.np, dtype=torch.float64, device=dev)
+    K = pp.nC * 128
+    check(lib().bo_gemm_f64(1, 1, pp.nrows_pad, cache.np, K, 1.0, _p(pp.Rt), pp.nrows_pad, 0,
+                            _p(cache.U), cache.np, 0, 0.0, _p(W), cache.np, 0, 1,
+                            _lib.GEMM_B_LOWER, _stream(dev)), "w_matrix")
+    return W
+
+
+def qmc_backward(mode: int, mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor,
+                 dacq: torch.Tensor, best_f: float = 0.0,
+                 best_f_s: Optional[torch.Tensor] = None):
+    dev = mean.device
+    B, q = mean.shape
+    S = Z.shape[0]
+    dmean = torch.empty(B, q, dtype=torch.float64, device=dev)
+    dcov = torch.empty(B, q, q, dtype=torch.float64, device=dev)
+    check(lib().bo_qmc_backward(mode, B, q, _p(mean), _p(L), _p(Z.reshape(S, q).contiguous()), S,
+                                float(best_f), _p(best_f_s), _p(dacq.contiguous()), _p(dmean),
+                                _p(dcov), _stream(dev)), "qmc_backward")
+    return dmean, dcov
+
+
+def post_backward(cache: GPCache, pp: PostPartials, W: torch.Tensor, dmean: torch.Tensor,
+                  dcov: torch.Tensor, ystd: float) -> torch.Tensor:
+    dev = W.device
+    dX = torch.empty(pp.B, pp.q, cache.d, dtype=torch.float64, device=dev)
+    check(lib().bo_post_backward(cache.kind, pp.B, pp.q, cache.d, _p(pp.Xq), _p(cache.Xt_scaled),
+                                 cache.n, _p(W), W.shape[1], _p(cache.alpha),
+                                 _p(dmean.contiguous()), _p(dcov.contiguous()),
+                                 _p(cache.lengthscale), cache.outputscale, float(ystd), _p(dX),
+                                 _stream(dev)), "post_backward")
+    return dX
+
+
+def _raise_not_psd(info: torch.Tensor, jitter: torch.Tensor, what: str):
+    """Host check of a batched ladder (one D2H read, as [G] psd_safe_cholesky's
+    torch.any(info)); warns like [G] when jitter was added."""
+    packed = torch.stack([info.to(torch.float64).max(), jitter.max()]).cpu()
+    if packed[0] > 0:
+        from .exceptions import NotPSDError
+        raise NotPSDError(f"{what}: matrix not positive definite after repeatedly adding "
+                          f"jitter up to {CHOLESKY_JITTER_F64 * 10 ** (CHOLESKY_MAX_TRIES - 1):.1e}")
+    if packed[1] > 0:
+        import warnings
+        from .exceptions import NumericalWarning
+        warnings.warn(f"A not p.d., added jitter of {float(packed[1]):.1e} to the diagonal",
+                      NumericalWarning)
+
+
+def chol_jitter(A: torch.Tensor, max_tries=CHOLESKY_MAX_TRIES,
+                jitter0=CHOLESKY_JITTER_F64) -> torch.Tensor:
+    """psd_safe_cholesky of (..., q, q) on the device (batched kernel for q <= 64,
+    blocked MFMA Cholesky per matrix beyond)."""
+    dev = _dev(A)
+    q = A.shape[-1]
+    batch = A.shape[:-2]
+    A3 = A.reshape(-1, q, q).contiguous()
+    B = A3.shape[0]
+    if q <= 64:
+        L = torch.empty_like(A3)
+        info = torch.empty(B, dtype=torch.int32, device=dev)
+        jit = torch.empty(B, dtype=torch.float64, device=dev)
+        check(lib().bo_chol_small(_p(A3), B, q, max_tries, jitter0, _p(L), _p(info), _p(jit),
+                                  _stream(dev)), "chol_small")
+        _raise_not_psd(info, jit, "psd_safe_cholesky")
+        return L.reshape(*batch, q, q)
+    out = []
+    np_ = padded_order(q)
+    for b in range(B):
+        L = torch.empty(np_, np_, dtype=torch.float64, device=dev)
+        Linv = torch.empty_like(L)
+        work = torch.empty_like(L)
+        info = torch.zeros(1, dtype=torch.int32, device=dev)
+        jit = ctypes.c_double(0.0)
+        check(lib().bo_cholesky_jitter(_p(A3[b]), q, _p(L), _p(Linv), _p(work), max_tries, jitter0,
+                                       ctypes.byref(jit), _p(info), _stream(dev)), "cholesky_jitter")
+        if jit.value > 0:
+            import warnings
+            from .exceptions import NumericalWarning
+            warnings.warn(f"A not p.d., added jitter of {jit.value:.1e} to the diagonal",
+                          NumericalWarning)
+        out.append(L[:q, :q])
+    return torch.stack(out).reshape(*batch, q, q)
+
+
+def covar_blocks(X3: torch.Tensor, lengthscale, kind=_lib.RBF, outputscale=1.0, diag_add=0.0):
+    dev = _dev(X3)
+    B, q, d = X3.shape
+    K = torch.empty(B, q, q, dtype=torch.float64, device=dev)
+    check(lib().bo_covar_blocks(kind, _p(X3.contiguous()), B, q, d,
+                                _p(lengthscale.reshape(-1).contiguous()), outputscale, diag_add,
+                                _p(K), _stream(dev)), "covar_blocks")
+    return K
+
+
+def posterior_general(model, X3: torch.Tensor):
+    """Exact posterior of B t-batches of any q / d through the generic kernels:
+    K*x (covar_matrix), R = K*x L^{-T} (triangular MFMA GEMM), R R^T blocks
+    (batched GEMM), mean = c + K*x alpha.  Outcome space."""
+    cache = model.prediction_cache()
+    ymean, ystd = model.outcome_stats()
+    B, q, d = X3.shape
+    n = cache.n
+    X2 = X3.reshape(B * q, d).contiguous()
+    Kx = covar_matrix(X2, cache.Xt, cache.lengthscale, cache.kind, cache.outputscale)
+    R = gemm(Kx, cache.U[:n, :n], flags=_lib.GEMM_B_UPPER)
+    mean = gemm(Kx, cache.alpha.reshape(n, 1)).reshape(B, q)
+    RR = gemm(R.reshape(B, q, n), R.reshape(B, q, n), transB=True)
+    Kxx = covar_blocks(X3, cache.lengthscale, cache.kind, cache.outputscale)
+    cov = (Kxx - RR) * (ystd * ystd)
+    mean = ymean + ystd * (mean + cache.constant)
+    return mean, cov

@@ -1,0 +1,224 @@
+"""Multi-start acquisition optimisation: the callers of the hot path.
+
+Restates the call protocol of optimize_acqf (botorch/optim/optimize.py:246-543),
+gen_batch_initial_conditions (optim/initializers.py:243-438),
+initialize_q_batch[_nonneg] (:968-1037) and gen_candidates_scipy
+(generation/gen.py:46-298): scipy L-BFGS-B on the host over the flattened
+b x q x d restarts, one forward + autograd.grad of -acqf(X).sum() per function
+evaluation (the only host<->device boundary of the loop).
+
+Multi-GPU (``botorch_amd.distributed``): restarts are sharded over ranks and
+the final argmax/gather is one all-reduce.
+"""
+from __future__ import annotations
+
+import time
+import warnings
+from typing import Any, Callable, Dict, Optional, Tuple
+
+import numpy as np
+import torch
+from scipy.optimize import minimize
+
+from .exceptions import OptimizationWarning
+from .utils_sampling import draw_sobol_samples, manual_seed
+
+INIT_OPTION_KEYS = {"alpha", "batch_limit", "eta", "init_batch_limit", "nonnegative", "n_burnin",
+                    "sample_around_best", "sample_around_best_sigma",
+                    "sample_around_best_prob_perturb", "seed", "thinning"}
+
+
+class BadInitialCandidatesWarning(RuntimeWarning):
+    pass
+
+
+def columnwise_clamp(X, lower=None, upper=None, raise_on_violation=False):
+    """utils/transforms (optim/utils): clamp each column to [lower, upper]."""
+    Xout = X
+    if lower is not None:
+        Xout = torch.maximum(Xout, torch.as_tensor(lower).to(X))
+    if upper is not None:
+        Xout = torch.minimum(Xout, torch.as_tensor(upper).to(X))
+    if raise_on_violation and not torch.allclose(Xout, X):
+        raise RuntimeError("Original value(s) are out of bounds.")
+    return Xout
+
+
+def initialize_q_batch_nonneg(X, Y, n, eta=1.0, alpha=1e-4):
+    """optim/initializers.py:968-1037."""
+    n_samples = X.shape[0]
+    if n > n_samples:
+        raise RuntimeError("n cannot be larger than the number of provided samples")
+    elif n == n_samples:
+        return X
+    max_val, max_idx = torch.max(Y, dim=0)
+    if torch.any(max_val <= 0):
+        warnings.warn("All acquisition values for raw sampled points are nonpositive, so "
+                      "initial conditions are being selected randomly.", BadInitialCandidatesWarning)
+        return X[torch.randperm(n=n_samples, device=X.device)][:n]
+    pos = Y > 0
+    num_pos = pos.sum().item()
+    if num_pos < n:
+        remaining = (~pos).nonzero(as_tuple=False).view(-1)
+        rand = torch.randperm(remaining.shape[0], device=Y.device)
+        pos[remaining[rand[: n - num_pos]]] = 1
+        return X[pos]
+    alpha_pos = Y >= alpha * max_val
+    while alpha_pos.sum() < n:
+        alpha = 0.1 * alpha
+        alpha_pos = Y >= alpha * max_val
+    idx_pos = torch.arange(len(Y), device=Y.device)[alpha_pos]
+    weights = torch.exp(eta * (Y[alpha_pos] / max_val - 1))
+    idcs = idx_pos[torch.multinomial(weights, n)]
+    if max_idx not in idcs:
+        idcs[-1] = max_idx
+    return X[idcs]
+
+
+def initialize_q_batch(X, Y, n, eta=1.0):
+    """optim/initializers.py (Boltzmann sampling on standardized values)."""
+    n_samples = X.shape[0]
+    if n > n_samples:
+        raise RuntimeError("n cannot be larger than the number of provided samples")
+    elif n == n_samples:
+        return X
+    Ystd = Y.std()
+    if Ystd == 0:
+        warnings.warn("All acquisition values for raw samples points are the same for "
+                      "at least one batch. Choosing initial conditions at random.",
+                      BadInitialCandidatesWarning)
+        return X[torch.randperm(n=n_samples, device=X.device)][:n]
+    max_val, max_idx = torch.max(Y, dim=0)
+    Z = (Y - Y.mean()) / Ystd
+    weights = torch.exp(eta * Z)
+    while torch.isinf(weights).any():
+        weights = torch.exp(Z * eta)
+        eta *= 0.5
+    idcs = torch.multinomial(weights, n)
+    if max_idx not in idcs:
+        idcs[-1] = max_idx
+    return X[idcs]
+
+
+def _is_nonnegative(acqf) -> bool:
+    from .acquisition import (ExpectedImprovement, ProbabilityOfImprovement,
+                              qExpectedImprovement)
+    names = ("qExpectedImprovement", "qNoisyExpectedImprovement", "ExpectedImprovement",
+             "ProbabilityOfImprovement", "qExpectedHypervolumeImprovement")
+    return type(acqf).__name__ in names
+
+
+def gen_batch_initial_conditions(acq_function, bounds, q, num_restarts, raw_samples,
+                                 fixed_features=None, options=None, **kwargs):
+    """optim/initializers.py:243-438: Sobol raw samples on the host, forward-only
+    evaluation in chunks of init_batch_limit on the device, Boltzmann selection."""
+    options = options or {}
+    seed = options.get("seed")
+    batch_limit = options.get("init_batch_limit", options.get("batch_limit"))
+    device = bounds.device
+    bounds_cpu = bounds.cpu()
+    X_rnd = draw_sobol_samples(bounds=bounds_cpu, n=raw_samples, q=q, seed=seed)
+    with torch.no_grad():
+        if batch_limit is None:
+            batch_limit = X_rnd.shape[0]
+        ys = []
+        for start in range(0, X_rnd.shape[0], batch_limit):
+            ys.append(acq_function(X_rnd[start:start + batch_limit].to(device)).cpu())
+        Y_rnd = torch.cat(ys)
+    init = initialize_q_batch_nonneg if (options.get("nonnegative") or _is_nonnegative(acq_function)) \
+        else initialize_q_batch
+    kw = {"eta": options.get("eta", 1.0)}
+    if init is initialize_q_batch_nonneg and "alpha" in options:
+        kw["alpha"] = options["alpha"]
+    with manual_seed(seed):
+        ics = init(X_rnd, Y_rnd, num_restarts, **kw)
+    return ics.to(device)
+
+
+def gen_candidates_scipy(initial_conditions, acquisition_function, lower_bounds=None,
+                         upper_bounds=None, options=None, fixed_features=None,
+                         timeout_sec=None, **kwargs):
+    """generation/gen.py:46-298 (box constraints, L-BFGS-B, with_grad)."""
+    options = dict(options or {})
+    options = {**options, "maxiter": options.get("maxiter", 2000)}
+    clamped = columnwise_clamp(initial_conditions, lower_bounds, upper_bounds)
+    shapeX = clamped.shape
+    x0 = clamped.detach().reshape(-1).cpu().numpy()
+    d = shapeX[-1]
+    lb = (torch.as_tensor(lower_bounds).expand(shapeX).reshape(-1).cpu().numpy()
+          if lower_bounds is not None else np.full(x0.shape, -np.inf))
+    ub = (torch.as_tensor(upper_bounds).expand(shapeX).reshape(-1).cpu().numpy()
+          if upper_bounds is not None else np.full(x0.shape, np.inf))
+    scipy_bounds = list(zip(lb, ub))
+    with_grad = options.pop("with_grad", True)
+    method = options.pop("method", "L-BFGS-B")
+    callback = options.pop("callback", None)
+
+    def f_np_wrapper(x: np.ndarray):
+        if np.isnan(x).any():
+            raise RuntimeError(f"{np.isnan(x).sum()} elements of the {x.size} element array `x` are NaN.")
+        X = torch.from_numpy(x).to(initial_conditions).view(shapeX).contiguous().requires_grad_(True)
+        loss = -acquisition_function(X).sum()
+        grad = torch.autograd.grad(loss, X)[0].contiguous().view(-1).cpu().numpy()
+        if np.isnan(grad).any():
+            raise RuntimeError(f"{np.isnan(grad).sum()} elements of the {x.size} element gradient "
+                               "array `gradf` are NaN. This often indicates numerical issues.")
+        return loss.item(), grad
+
+    def f_only(x):
+        X = torch.from_numpy(x).to(initial_conditions).view(shapeX).contiguous()
+        with torch.no_grad():
+            return -acquisition_function(X).sum().item()
+
+    t0 = time.monotonic()
+    res = minimize(f_np_wrapper if with_grad else f_only, x0, method=method, jac=with_grad,
+                   bounds=scipy_bounds, callback=callback, options=options)
+    if not res.success and "ITERATIONS REACHED LIMIT" not in str(res.message):
+        warnings.warn(f"Optimization failed within `scipy.optimize.minimize` with status "
+                      f"{res.status} and message {res.message}.", OptimizationWarning)
+    candidates = torch.from_numpy(res.x).to(initial_conditions).reshape(shapeX)
+    clamped = columnwise_clamp(candidates, lower_bounds, upper_bounds, raise_on_violation=True)
+    with torch.no_grad():
+        acq = acquisition_function(clamped)
+    return clamped, acq
+
+
+def optimize_acqf(acq_function, bounds, q, num_restarts, raw_samples=None, options=None,
+                  batch_initial_conditions=None, return_best_only=True, gen_candidates=None,
+                  sequential=False, retry_on_optimization_warning=True, **kwargs):
+    """optim/optimize.py:397-543 -> _optimize_acqf_batch (:246-394): raw-sample
+    initialisation, batch_limit chunks through gen_candidates_scipy, one retry
+    on OptimizationWarning, argmax over restarts."""
+    if sequential:
+        raise NotImplementedError("sequential greedy optimisation is out of scope")
+    options = options or {}
+    gen_candidates = gen_candidates or gen_candidates_scipy
+    if batch_initial_conditions is None:
+        if raw_samples is None:
+            raise ValueError("Must specify `raw_samples` when `batch_initial_conditions` is None`.")
+        batch_initial_conditions = gen_batch_initial_conditions(
+            acq_function, bounds, q, num_restarts, raw_samples, options=options)
+    batch_limit = options.get("batch_limit", num_restarts)
+    gen_options = {k: v for k, v in options.items() if k not in INIT_OPTION_KEYS}
+
+    def _run(ics):
+        cands, vals, ws = [], [], []
+        for chunk in ics.split(batch_limit):
+            with warnings.catch_warnings(record=True) as w:
+                warnings.simplefilter("always", category=OptimizationWarning)
+                c, v = gen_candidates(chunk, acq_function, lower_bounds=bounds[0],
+                                      upper_bounds=bounds[1], options=gen_options)
+            ws += w
+            cands.append(c)
+            vals.append(v)
+        return torch.cat(cands), torch.cat([v.reshape(-1) for v in vals]), ws
+
+    cands, vals, ws = _run(batch_initial_conditions)
+    if retry_on_optimization_warning and any(issubclass(w.category, OptimizationWarning) for w in ws):
+        new_ics = gen_batch_initial_conditions(acq_function, bounds, q, num_restarts,
+                                               raw_samples or num_restarts, options=options)
+        cands, vals, ws = _run(new_ics)
+    if return_best_only:
+        best = torch.argmax(vals.view(-1), dim=0)
+        return cands[best], vals[best]
+    return cands, vals

@@ -56,6 +56,10 @@ int bo_version(void);
 /* Hardware probe of the fp64 MFMA accumulator map; out: 64 x 8 doubles. */
 int bo_probe_mfma_f64_layout(double* out, void* stream);
 
+/* Peak-rate probe: `blocks` x 256 threads, each wave issuing iters x 8
+ * independent fp64 MFMAs (2048 flop each).  out: 1 double (kept live). */
+int bo_probe_mfma_f64_rate(int blocks, int iters, double* out, void* stream);
+
 /* Batched C = alpha op(A) op(B) + beta C on the fp64 matrix cores (strides sA,
  * sB, sC between batch members).  Building block of the Cholesky/inverse and
  * of the qNEI cross-covariance; replaces the dense torch.matmul calls inside
@@ -84,6 +88,26 @@ int64_t bo_padded_order(int64_t n);
  * leading minor (torch.linalg.cholesky_ex convention). */
 int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* info,
                         void* stream);
+
+/* psd_safe_cholesky of one n x n matrix ([G] linear_operator, the ladder of
+ * botorch/__init__.py:47): factor A + jitter I for jitter = 0, jitter0,
+ * 10 jitter0, ... (max_tries increments).  L, Linv, work: np x np (identity
+ * pad); jitter_used: HOST double.  Used for the joint posterior over the qNEI
+ * baseline (acquisition/cached_cholesky.py:94-120, acquisition/utils.py:245-349). */
+int bo_cholesky_jitter(const double* A, int64_t n, double* L, double* Linv, double* work,
+                       int max_tries, double jitter0, double* jitter_used, int* info_dev,
+                       void* stream);
+
+/* Batched small psd_safe_cholesky (q <= 64), ladder applied per member
+ * ([G] MultivariateNormal root_decomposition, posteriors/gpytorch.py:121-123).
+ * A, L: B x q x q; info (B, nullable), jitter (B, nullable). */
+int bo_chol_small(const double* A, int64_t B, int q, int max_tries, double jitter0, double* L,
+                  int* info, double* jitter, void* stream);
+
+/* K[b] = outputscale * k(X[b], X[b]) (+ diag_add I), X: B x q x d, K: B x q x q. */
+int bo_covar_blocks(int kind, const double* X, int64_t B, int q, int d,
+                    const double* lengthscale, double outputscale, double diag_add, double* K,
+                    void* stream);
 
 /* B = A^T for n x n matrices with leading dimension ld. */
 int bo_transpose(const double* A, double* B, int64_t n, int64_t ld, void* stream);
@@ -131,8 +155,8 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
  * training inputs; U: >= np x np with leading dim ldu; beta: n.
  * Spart: nC x (nrows_pad/16) x 16 x 16,  mpart: nC x nrows_pad.
  * Rt (nullable, gradient path): R^T, (nC*128) x nrows_pad. */
-int bo_post_partials(int kind, const double* Xq, int B, int q, const double* Xt_scaled,
-                     int64_t n, const double* U, int64_t ldu, const double* beta,
+int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
+                     const double* Xt_scaled, int64_t n, const double* U, int64_t ldu, const double* beta,
                      double outputscale, double* Spart, double* mpart, double* Rt,
                      void* stream);
 
@@ -152,6 +176,39 @@ int bo_qmc_finalize(int kind, int mode, int B, int q, const double* Xq, const do
                     const double* best_f_s, int max_tries, double jitter0, double* acq,
                     double* mean_out, double* cov_out, double* L_out, int* info_out,
                     double* jitter_out, void* stream);
+
+/* Backward of the MC reduction + q x q Cholesky (gen_candidates_scipy's
+ * autograd.grad, botorch/generation/gen.py:194-222):
+ * dacq (B) -> dmean (B x q), dcov (B x q x q, symmetric) w.r.t. the outcome-
+ * space posterior (mean', Sigma'), given mean' and L_q from bo_qmc_finalize.
+ * mode: BO_QMC_QEI or BO_QMC_QNEI (best_f_s per sample).  torch semantics:
+ * amax splits ties evenly, clamp_min(0) passes the gradient at >= 0. */
+int bo_qmc_backward(int mode, int B, int q, const double* mean, const double* Lq,
+                    const double* Z, int S, double best_f, const double* best_f_s,
+                    const double* dacq, double* dmean, double* dcov, void* stream);
+
+/* Backward of the batched exact posterior w.r.t. the candidates X (B x q x d):
+ *   dK*x = ystd dmean alpha^T - G W,  G = ystd^2 (dcov + dcov^T),
+ *   W = R L^{-1} (nrows_pad x ldw, rows b*Qp + a), dK** = ystd^2 dcov,
+ * reduced through dk/dx.  Xq / Xt_scaled as for bo_post_partials.  Caches carry
+ * no gradient ([G] detach_test_caches, botorch/models/utils/assorted.py:286-298). */
+int bo_post_backward(int kind, int B, int q, int d, const double* Xq, const double* Xt_scaled,
+                     int64_t n, const double* W, int64_t ldw, const double* alpha,
+                     const double* dmean, const double* dcov, const double* lengthscale,
+                     double outputscale, double ystd, double* dX, void* stream);
+
+/* Exact-MLL terms for fit_gpytorch_mll (botorch/fit.py:75-258 ->
+ * optim/closures/model_closures.py:171-184, [G] ExactMarginalLogLikelihood),
+ * given bo_gp_cache_build's L, alpha, beta and Ainv = U U^T (lower triangle
+ * read; ld = np).  partial: n x (d+5) per-row sums
+ *   [0..d-1] sum_k w_ik W_ik outputscale g_ik (x_ij - x_kj)^2,   W = alpha alpha^T - Ainv
+ *   [d]      W_ii        [d+1] sum_k w_ik W_ik kbar_ik   [d+2] log L_ii
+ *   [d+3]    beta_i^2    [d+4] alpha_i          (w_ik = 2 for k < i, 1 for k = i)
+ * from which the host forms the loss and its gradient in (ell, noise, constant,
+ * outputscale) exactly. */
+int bo_mll_terms(int kind, const double* X, int64_t n, int d, const double* lengthscale,
+                 double outputscale, const double* L, const double* Ainv, int64_t ld,
+                 const double* alpha, const double* beta, double* partial, void* stream);
 
 /* Scrambled Sobol N(0,1) samples, points skip..skip+n-1: out (n x dim).
  * state: dim x 30 int64 scrambled direction numbers, shift: dim int64

@@ -1,0 +1,156 @@
+"""Public API (models / posteriors / samplers / acquisition) on the GPU vs. the oracle,
+values and gradients."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _setup(n=256, d=6, seed=0, ls=0.35, noise=1e-3, const=0.1):
+    from botorch_amd.models import SingleTaskGP
+    from botorch_amd.test_functions import Hartmann
+    from oracle.gp import ExactGPOracle, GPHyper
+    from oracle.sampling import draw_sobol_samples
+    lo = torch.zeros(d, dtype=torch.float64)
+    X = draw_sobol_samples(lo, lo + 1, n, 1, seed).squeeze(1)
+    Y = Hartmann(negate=True)(X[:, :6]).unsqueeze(-1)
+    m = SingleTaskGP(X.to(DEV), Y.to(DEV))
+    m.covar_module.lengthscale = torch.full((1, d), ls, dtype=torch.float64)
+    m.likelihood.noise = torch.tensor([noise])
+    m.mean_module.constant = const
+    m.eval()
+    orc = ExactGPOracle(X, Y, GPHyper(torch.full((d,), ls, dtype=torch.float64), noise, const))
+    return X, Y, m, orc
+
+
+def test_posterior_api_matches_oracle():
+    X, Y, m, orc = _setup()
+    Xc = torch.rand(7, 5, 6, dtype=torch.float64)
+    post = m.posterior(Xc.to(DEV))
+    assert post.mean.shape == (7, 5, 1) and post.variance.shape == (7, 5, 1)
+    mr, cr = orc.posterior(Xc)
+    torch.testing.assert_close(post.mean.squeeze(-1).cpu(), mr, rtol=1e-4, atol=1e-9)
+    torch.testing.assert_close(post.variance.squeeze(-1).cpu(), cr.diagonal(dim1=-2, dim2=-1), rtol=1e-4, atol=1e-10)
+    # 2-d input (q x d) -> batch shape ()
+    p2 = m.posterior(Xc[0].to(DEV))
+    assert p2.mean.shape == (5, 1)
+    # observation noise adds s^2 sigma^2 (test/models/test_gp_regression.py:131-157)
+    pn = m.posterior(Xc.to(DEV), observation_noise=True)
+    diff = (pn.variance - post.variance).cpu()
+    torch.testing.assert_close(diff, torch.full_like(diff, 1e-3 * orc.ystd.item() ** 2), rtol=1e-9, atol=1e-12)
+
+
+def test_posterior_gradient_matches_oracle():
+    X, Y, m, orc = _setup()
+    g = torch.Generator().manual_seed(3)
+    Xc = torch.rand(6, 4, 6, generator=g, dtype=torch.float64)
+    Xd = Xc.to(DEV).requires_grad_(True)
+    post = m.posterior(Xd)
+    loss = (post.mean.sum() + 3.0 * post.variance.sum()
+            + 0.7 * post.covariance_matrix[..., 0, 1].sum())
+    (gd,) = torch.autograd.grad(loss, Xd)
+    Xo = Xc.clone().requires_grad_(True)
+    mr, cr = orc.posterior(Xo)
+    lo = mr.sum() + 3.0 * cr.diagonal(dim1=-2, dim2=-1).sum() + 0.7 * cr[..., 0, 1].sum()
+    (go,) = torch.autograd.grad(lo, Xo)
+    torch.testing.assert_close(gd.cpu(), go, rtol=1e-5, atol=1e-8)
+
+
+def test_posterior_general_path_q_gt_16():
+    X, Y, m, orc = _setup()
+    Xc = torch.rand(2, 20, 6, dtype=torch.float64)
+    post = m.posterior(Xc.to(DEV))
+    mr, cr = orc.posterior(Xc)
+    torch.testing.assert_close(post.mean.squeeze(-1).cpu(), mr, rtol=1e-4, atol=1e-9)
+    torch.testing.assert_close(post.covariance_matrix.cpu(), cr, rtol=1e-4, atol=1e-9)
+
+
+@pytest.mark.parametrize("B,q,S", [(16, 4, 128), (40, 8, 256), (9, 16, 64), (5, 1, 32), (3, 3, 16)])
+def test_qei_api_value(B, q, S):
+    from botorch_amd.acquisition import qExpectedImprovement
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import qei
+    from oracle.sampling import draw_sobol_normal_samples
+    X, Y, m, orc = _setup()
+    best_f = Y.max().item()
+    acqf = qExpectedImprovement(m, best_f, sampler=SobolQMCNormalSampler(torch.Size([S]), seed=5))
+    Xc = torch.rand(B, q, 6, dtype=torch.float64)
+    with torch.no_grad():
+        v = acqf(Xc.to(DEV)).cpu()
+    ref = qei(orc, Xc, draw_sobol_normal_samples(q, S, 5), best_f)
+    torch.testing.assert_close(v, ref, rtol=1e-6, atol=1e-10)
+
+
+@pytest.mark.parametrize("B,q", [(8, 4), (3, 16), (4, 1), (2, 5)])
+def test_qei_gradient_matches_oracle(B, q):
+    from botorch_amd.acquisition import qExpectedImprovement
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import qei
+    from oracle.sampling import draw_sobol_normal_samples
+    X, Y, m, orc = _setup()
+    best_f = Y.max().item() - 0.3  # plenty of positive improvement
+    S = 128
+    acqf = qExpectedImprovement(m, best_f, sampler=SobolQMCNormalSampler(torch.Size([S]), seed=2))
+    g = torch.Generator().manual_seed(B * 10 + q)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64)
+    Xd = Xc.to(DEV).requires_grad_(True)
+    val = acqf(Xd)
+    (gd,) = torch.autograd.grad(val.sum(), Xd)
+    Xo = Xc.clone().requires_grad_(True)
+    ref = qei(orc, Xo, draw_sobol_normal_samples(q, S, 2), best_f)
+    (go,) = torch.autograd.grad(ref.sum(), Xo)
+    torch.testing.assert_close(val.detach().cpu(), ref.detach(), rtol=1e-6, atol=1e-10)
+    torch.testing.assert_close(gd.cpu(), go, rtol=1e-5, atol=1e-8)
+
+
+def test_analytic_ei_value_and_grad():
+    from botorch_amd.acquisition import ExpectedImprovement
+    from oracle.acquisition import ei_analytic
+    X, Y, m, orc = _setup()
+    best_f = Y.max().item()
+    Xc = torch.rand(11, 1, 6, dtype=torch.float64)
+    Xd = Xc.to(DEV).requires_grad_(True)
+    v = ExpectedImprovement(m, best_f)(Xd)
+    (gd,) = torch.autograd.grad(v.sum(), Xd)
+    Xo = Xc.clone().requires_grad_(True)
+    r = ei_analytic(orc, Xo, best_f)
+    (go,) = torch.autograd.grad(r.sum(), Xo)
+    torch.testing.assert_close(v.detach().cpu(), r.detach(), rtol=1e-5, atol=1e-10)
+    torch.testing.assert_close(gd.cpu(), go, rtol=1e-4, atol=1e-8)
+
+
+def test_sampler_base_samples_match_reference(golden):
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    X, Y, m, orc = _setup()
+    s = SobolQMCNormalSampler(torch.Size([256]), seed=0)
+    post = m.posterior(torch.rand(4, 8, 6, dtype=torch.float64, device=DEV))
+    samples = s(post)
+    assert samples.shape == (256, 4, 8, 1)
+    assert s.base_samples.shape == (256, 1, 8)
+    np.testing.assert_allclose(s.base_samples.squeeze(1).cpu().numpy(),
+                               golden["sobol_normal_d8_n256_s0"], rtol=0, atol=1e-13)
+
+
+@pytest.mark.parametrize("q", [3, 16, 40, 150])
+def test_chol_jitter_batched(q):
+    from botorch_amd import kernels
+    g = torch.Generator().manual_seed(q)
+    M = torch.randn(5, q, q, generator=g, dtype=torch.float64)
+    A = M @ M.mT + 0.1 * torch.eye(q, dtype=torch.float64)
+    L = kernels.chol_jitter(A.to(DEV)).cpu()
+    torch.testing.assert_close(L, torch.linalg.cholesky(A), rtol=1e-9, atol=1e-11)
+
+
+def test_chol_jitter_ladder_matches_reference_semantics():
+    """A singular PSD member gets the smallest sufficient jitter; others none."""
+    from botorch_amd import kernels
+    from botorch_amd.exceptions import NumericalWarning
+    from oracle.gp import psd_safe_cholesky
+    v = torch.tensor([[1.0, 2.0, 3.0]], dtype=torch.float64)
+    A = torch.stack([v.T @ v, torch.eye(3, dtype=torch.float64)])
+    with pytest.warns(NumericalWarning):
+        L = kernels.chol_jitter(A.to(DEV)).cpu()
+    Lr, jit = psd_safe_cholesky(A)
+    torch.testing.assert_close(L, Lr, rtol=1e-7, atol=1e-9)
