@@ -236,3 +236,130 @@ class UpperConfidenceBound(AnalyticAcquisitionFunction):
         X = t_batch_mode(X, expected_q=1)
         mean, sigma = self._mean_and_sigma(X)
         return (mean if self.maximize else -mean) + self.beta.to(mean).sqrt() * sigma
+
+
+# -- qNEI -------------------------------------------------------------------------------
+def prune_inferior_points(model, X, objective=None, posterior_transform=None, constraints=None,
+                          num_samples: int = 2048, max_frac: float = 1.0, sampler=None,
+                          marginalize_dim=None):
+    """acquisition/utils.py:245-349 (unconstrained): keep the points with non-zero
+    empirical probability of being the best under `num_samples` joint posterior
+    samples.  The joint n x n posterior, its jittered Cholesky and the sample GEMM
+    run on the device."""
+    if X.ndim > 2:
+        raise UnsupportedError("Batched inputs `X` are currently unsupported by prune_inferior_points")
+    if X.size(-2) == 0:
+        raise ValueError("X must have at least one point.")
+    if max_frac <= 0 or max_frac > 1.0:
+        raise ValueError(f"max_frac must take values in (0, 1], is {max_frac}")
+    if constraints is not None:
+        raise UnsupportedError("constraints are not on the accelerated path")
+    max_points = math.ceil(max_frac * X.size(-2))
+    with torch.no_grad():
+        posterior = model.posterior(X=X, posterior_transform=posterior_transform)
+        if sampler is None:
+            sampler = get_sampler(posterior, sample_shape=torch.Size([num_samples]))
+        samples = sampler(posterior)
+        obj = (objective or IdentityMCObjective())(samples, X=X)
+    is_best = torch.argmax(obj, dim=-1)
+    idcs, counts = torch.unique(is_best, return_counts=True)
+    if len(idcs) > max_points:
+        counts, order_idcs = torch.sort(counts, descending=True)
+        idcs = order_idcs[:max_points]  # reference quirk kept (utils.py:345-347)
+    return X[idcs]
+
+
+class qNoisyExpectedImprovement(MCAcquisitionFunction):
+    """MC batch noisy EI with the cached baseline root (acquisition/monte_carlo.py:
+    417-645, cached_cholesky.py:63-186, utils/low_rank.py:85-173):
+    qNEI(X) = E[max(max_j Y_j - max_i Y_base_i, 0)].
+
+    Construction (once): optional pruning of X_baseline, the baseline posterior,
+    its jittered Cholesky L_rr (with inverse), the baseline samples and their
+    per-sample best, and the device precomputations of the fused forward:
+    P_b = L_rr^{-1} K(X_b, X_tr) L^{-T} (r x n) and the scaled baseline inputs.
+    Forward (fused): post_partials (+ R^T), T = L_rr^{-1} Sigma'(X_b, X) as two
+    MFMA GEMMs (T = s^2 (L_rr^{-1} K_bX - P_b R^T)), the baseline sample term
+    F = Z_b T (one GEMM), then qmc_finalize in qNEI mode.
+    """
+
+    def __init__(self, model, X_baseline, sampler=None, objective=None, posterior_transform=None,
+                 X_pending=None, prune_baseline=True, cache_root=True, constraints=None,
+                 eta=1e-3, marginalize_dim=None):
+        super().__init__(model, sampler, objective, posterior_transform, X_pending)
+        if constraints is not None:
+            raise UnsupportedError("outcome constraints are not on the accelerated path")
+        if prune_baseline:
+            X_baseline = prune_inferior_points(model, X_baseline, objective=objective,
+                                               posterior_transform=posterior_transform)
+        self.register_buffer("X_baseline", X_baseline)
+        self._cache_root = cache_root
+        sampler = self._ensure_sampler()
+        S = sampler.sample_shape.numel()
+        r = X_baseline.shape[-2]
+        with torch.no_grad():
+            post = model.posterior(X_baseline, posterior_transform=posterior_transform)
+            mean_b = post.distribution.mean.reshape(1, r)
+            cov_b = post.distribution.covariance_matrix.reshape(r, r)
+            L_rr, Linv_rr, _ = kernels.cholesky_with_inverse(cov_b)
+            self.Z_base = kernels.sobol_normal(r, S, sampler.seed, X_baseline.device)
+            base = kernels.sample_mvn(mean_b, L_rr.unsqueeze(0).contiguous(), self.Z_base)
+            self.baseline_samples = base.reshape(S, r)
+            self.register_buffer("_baseline_best_f", self.baseline_samples.amax(dim=-1).contiguous())
+            self._baseline_L = L_rr.contiguous()
+            self._Linv_rr = Linv_rr.contiguous()
+            self._fused_ready = False
+            if hasattr(model, "prediction_cache") and X_baseline.shape[-1] <= kernels.DP:
+                cache = model.prediction_cache()
+                Kb = kernels.covar_matrix(X_baseline.contiguous(), cache.Xt, cache.lengthscale,
+                                          cache.kind, cache.outputscale)
+                R_b = kernels.gemm(Kb, cache.U[: cache.n, : cache.n], flags=_lib.GEMM_B_UPPER)
+                P_b = torch.zeros(r, cache.np, dtype=torch.float64, device=Kb.device)
+                P_b[:, : cache.n] = kernels.gemm(self._Linv_rr, R_b, flags=_lib.GEMM_A_LOWER)
+                self._P_b = P_b
+                self._Xb_scaled = torch.zeros(r, kernels.DP, dtype=torch.float64, device=Kb.device)
+                self._Xb_scaled[:, : cache.d] = X_baseline / cache.lengthscale
+                self._fused_ready = True
+        self._zq = {}
+
+    def _base_samples_q(self, q: int, device) -> torch.Tensor:
+        """The q new columns of the (r+q)-dim Sobol draw (sampling/normal.py:68-131)."""
+        if q not in self._zq:
+            r = self.X_baseline.shape[-2]
+            S = self.sampler.sample_shape.numel()
+            full = kernels.sobol_normal(r + q, S, self.sampler.seed, device)
+            self._zq[q] = full[:, r:].contiguous()
+        return self._zq[q]
+
+    def forward(self, X: torch.Tensor) -> torch.Tensor:
+        X = self._concat_pending(t_batch_mode(X))
+        batch = X.shape[:-2]
+        q, d = X.shape[-2], X.shape[-1]
+        X3 = X.reshape(-1, q, d)
+        if not (self._fused_eligible(X) and self._fused_ready):
+            raise UnsupportedError(
+                f"qNEI here needs the fused path (q <= {FUSED_QMAX}, d <= {kernels.DP}, identity objective)")
+        if X3.requires_grad:
+            raise UnsupportedError("qNEI gradients are not implemented yet on the fused path")
+        acq = _qnei_forward(self, X3.detach())
+        return acq.reshape(batch)
+
+
+def _qnei_forward(acqf: "qNoisyExpectedImprovement", X3: torch.Tensor) -> torch.Tensor:
+    model = acqf.model
+    cache = model.prediction_cache()
+    ymean, ystd = model.outcome_stats()
+    q = X3.shape[-2]
+    s2 = ystd * ystd
+    pp = kernels.post_partials(cache, X3, store_R=True)
+    ones = torch.ones(kernels.DP, dtype=torch.float64, device=X3.device)
+    Kbx = kernels.covar_matrix(acqf._Xb_scaled, pp.Xq, ones, cache.kind, cache.outputscale)
+    T = kernels.gemm(acqf._Linv_rr, Kbx, alpha=s2, flags=_lib.GEMM_A_LOWER)
+    T = kernels.gemm(acqf._P_b, pp.Rt, alpha=-s2, beta=1.0, C=T)
+    F = kernels.gemm(acqf.Z_base, T)
+    Zq = acqf._base_samples_q(q, X3.device)
+    out = kernels.qmc_finalize(cache, pp, _lib.QMC_QNEI, ymean, ystd, Z=Zq,
+                               best_f_s=acqf._baseline_best_f, want_mean=False, want_cov=False,
+                               T=T, F=F)
+    kernels._raise_not_psd(out["info"], out["jitter"], "qNoisyExpectedImprovement")
+    return out["acq"]

@@ -31,7 +31,13 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     double constant, double ymean, double ystd, const double* __restrict__ Z, int S,
     double best_f, const double* __restrict__ best_f_s, int max_tries, double jitter0,
     double* __restrict__ acq, double* __restrict__ mean_out, double* __restrict__ cov_out,
-    double* __restrict__ L_out, int* __restrict__ info_out, double* __restrict__ jitter_out) {
+    double* __restrict__ L_out, int* __restrict__ info_out, double* __restrict__ jitter_out,
+    const double* __restrict__ Tm, int r, int64_t ldT, const double* __restrict__ F,
+    int64_t ldF) {
+  // qNEI with the cached baseline root (utils/low_rank.py:85-173): Tm (r x ldT)
+  // holds bl_chol^T = L_rr^{-1} Sigma'(X_base, X) per padded test row and F
+  // (S x ldF) the samples' baseline term Z_base T; then
+  //   br = Sigma'_qq - T^T T,  f = mu' + F + chol(br) Z_q.
   __shared__ double Sig[QMAX][QMAX + 1];
   __shared__ double Lq[QMAX][QMAX + 1];
   __shared__ double mu[QMAX];
@@ -67,7 +73,12 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
       }
       kxx = outputscale * kernel_from_d2<KIND>(d2);
     }
-    const double v = s2 * (kxx - acc);
+    double v = s2 * (kxx - acc);
+    if (Tm != nullptr) {
+      double tt = 0.0;
+      for (int j = 0; j < r; ++j) tt = fma(Tm[j * ldT + row0 + a], Tm[j * ldT + row0 + c], tt);
+      v -= tt;
+    }
     Sig[a][c] = v;
     if (cov_out) cov_out[((int64_t)b * q + a) * q + c] = v;
   }
@@ -150,7 +161,7 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
 #pragma unroll
     for (int a = 0; a < QMAX; ++a) {
       if (a < q) {
-        double f = mu[a];
+        double f = mu[a] + ((F != nullptr) ? F[(int64_t)s * ldF + row0 + a] : 0.0);
 #pragma unroll
         for (int j = 0; j <= a; ++j) f = fma(Lq[a][j], zs[j], f);
         vmax = fmax(vmax, f - bf);
@@ -168,27 +179,41 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   }
 }
 
+struct QmcArgs {
+  int q, Qp;
+  const double *Xq, *Spart, *mpart;
+  int nC, nrows_pad;
+  double outputscale, constant, ymean, ystd;
+  const double* Z;
+  int S;
+  double best_f;
+  const double* best_f_s;
+  int max_tries;
+  double jitter0;
+  double *acq, *mean_out, *cov_out, *L_out;
+  int* info_out;
+  double* jitter_out;
+  const double* Tm;
+  int r;
+  int64_t ldT;
+  const double* F;
+  int64_t ldF;
+};
+
+template <int KIND, int MODE>
+void launch_mode(int B, const QmcArgs& a, hipStream_t st) {
+  qmc_kernel<KIND, MODE><<<B, THREADS, 0, st>>>(
+      a.q, a.Qp, a.Xq, a.Spart, a.mpart, a.nC, a.nrows_pad, a.outputscale, a.constant, a.ymean,
+      a.ystd, a.Z, a.S, a.best_f, a.best_f_s, a.max_tries, a.jitter0, a.acq, a.mean_out,
+      a.cov_out, a.L_out, a.info_out, a.jitter_out, a.Tm, a.r, a.ldT, a.F, a.ldF);
+}
+
 template <int KIND>
-int launch_qmc(int mode, int B, int q, int Qp, const double* Xq, const double* Spart,
-               const double* mpart, int nC, int nrows_pad, double outputscale, double constant,
-               double ymean, double ystd, const double* Z, int S, double best_f,
-               const double* best_f_s, int max_tries, double jitter0, double* acq,
-               double* mean_out, double* cov_out, double* L_out, int* info_out,
-               double* jitter_out, hipStream_t st) {
-#define BO_QMC_ARGS                                                                          \
-  q, Qp, Xq, Spart, mpart, nC, nrows_pad, outputscale, constant, ymean, ystd, Z, S, best_f, \
-      best_f_s, max_tries, jitter0, acq, mean_out, cov_out, L_out, info_out, jitter_out
-  if (mode == QMC_POSTERIOR)
-    qmc_kernel<KIND, QMC_POSTERIOR><<<B, THREADS, 0, st>>>(BO_QMC_ARGS);
-  else if (mode == QMC_QEI)
-    qmc_kernel<KIND, QMC_QEI><<<B, THREADS, 0, st>>>(BO_QMC_ARGS);
-  else if (mode == QMC_QNEI)
-    qmc_kernel<KIND, QMC_QNEI><<<B, THREADS, 0, st>>>(BO_QMC_ARGS);
-  else
-    qmc_kernel<KIND, QMC_CHOL><<<B, THREADS, 0, st>>>(BO_QMC_ARGS);
-#undef BO_QMC_ARGS
-  BO_LAUNCH_CHECK();
-  return BO_OK;
+void launch_qmc(int mode, int B, const QmcArgs& a, hipStream_t st) {
+  if (mode == QMC_POSTERIOR) launch_mode<KIND, QMC_POSTERIOR>(B, a, st);
+  else if (mode == QMC_QEI) launch_mode<KIND, QMC_QEI>(B, a, st);
+  else if (mode == QMC_QNEI) launch_mode<KIND, QMC_QNEI>(B, a, st);
+  else launch_mode<KIND, QMC_CHOL>(B, a, st);
 }
 
 }  // namespace
@@ -201,20 +226,25 @@ extern "C" int bo_qmc_finalize(int kind, int mode, int B, int q, const double* X
                                const double* Z, int S, double best_f, const double* best_f_s,
                                int max_tries, double jitter0, double* acq, double* mean_out,
                                double* cov_out, double* L_out, int* info_out,
-                               double* jitter_out, void* stream) {
+                               double* jitter_out, const double* Tm, int r, int64_t ldT,
+                               const double* F, int64_t ldF, void* stream) {
   BO_CHECK_ARG(mode >= 0 && mode <= 3, "bo_qmc_finalize: bad mode %d", mode);
-  BO_CHECK_ARG(mode == QMC_POSTERIOR || mode == QMC_CHOL || (acq && Z && S > 0), "bo_qmc_finalize: missing MC args");
+  BO_CHECK_ARG(mode == QMC_POSTERIOR || mode == QMC_CHOL || (acq && Z && S > 0),
+               "bo_qmc_finalize: missing MC args");
   BO_CHECK_ARG(mode != QMC_QNEI || best_f_s, "bo_qmc_finalize: qNEI needs per-sample best_f");
+  BO_CHECK_ARG((Tm == nullptr) == (F == nullptr) && (Tm == nullptr || r > 0),
+               "bo_qmc_finalize: cached-root qNEI needs both T and F");
   int Qp, nrows_pad, nC;
   int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
   if (s) return s;
   if (B == 0) return BO_OK;
+  QmcArgs a{q,      Qp,     Xq,       Spart,     mpart,     nC,      nrows_pad, outputscale,
+            constant, ymean, ystd,   Z,        S,         best_f,  best_f_s,  max_tries,
+            jitter0, acq,    mean_out, cov_out,  L_out,     info_out, jitter_out, Tm,
+            r,       ldT,    F,        ldF};
   hipStream_t st = as_stream(stream);
-  if (kind == BO_RBF)
-    return launch_qmc<BO_RBF>(mode, B, q, Qp, Xq, Spart, mpart, nC, nrows_pad, outputscale,
-                              constant, ymean, ystd, Z, S, best_f, best_f_s, max_tries, jitter0,
-                              acq, mean_out, cov_out, L_out, info_out, jitter_out, st);
-  return launch_qmc<BO_MATERN52>(mode, B, q, Qp, Xq, Spart, mpart, nC, nrows_pad, outputscale,
-                                 constant, ymean, ystd, Z, S, best_f, best_f_s, max_tries,
-                                 jitter0, acq, mean_out, cov_out, L_out, info_out, jitter_out, st);
+  if (kind == BO_RBF) launch_qmc<BO_RBF>(mode, B, a, st);
+  else launch_qmc<BO_MATERN52>(mode, B, a, st);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
 }

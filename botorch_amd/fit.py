@@ -75,15 +75,15 @@ class _Layout:
 
     def get(self) -> np.ndarray:
         m = self.model
-        v = [float(m.likelihood.noise), float(m.mean_module.constant)]
+        v = [float(m.likelihood.noise.detach()), float(m.mean_module.constant.detach())]
         v += self.base.lengthscale.detach().reshape(-1).cpu().tolist()
         if self.has_os:
-            v.append(float(m.covar_module.outputscale))
+            v.append(float(m.covar_module.outputscale.detach()))
         return np.asarray(v, dtype=np.float64)
 
     def set(self, x: np.ndarray) -> None:
         m = self.model
-        m.likelihood.noise = torch.tensor([x[0]])
+        m.likelihood.noise = torch.tensor([float(x[0])], dtype=torch.float64)
         m.mean_module.constant = float(x[1])
         self.base.lengthscale = torch.as_tensor(x[2:2 + self.d]).reshape(1, -1)
         if self.has_os:

@@ -199,7 +199,8 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False) -> Pos
 def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd: float,
                  Z: Optional[torch.Tensor] = None, best_f: float = 0.0,
                  best_f_s: Optional[torch.Tensor] = None, want_mean=True, want_cov=True,
-                 want_L=False, max_tries=CHOLESKY_MAX_TRIES, jitter0=CHOLESKY_JITTER_F64):
+                 want_L=False, max_tries=CHOLESKY_MAX_TRIES, jitter0=CHOLESKY_JITTER_F64,
+                 T: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None):
     dev = pp.Xq.device
     B, q = pp.B, pp.q
     f64 = dict(dtype=torch.float64, device=dev)
@@ -217,7 +218,9 @@ def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd
                                 cache.n, cache.outputscale, cache.constant, float(ymean),
                                 float(ystd), _p(Z), S, float(best_f), _p(best_f_s), max_tries,
                                 jitter0, _p(acq), _p(mean), _p(cov), _p(L), _p(info), _p(jit),
-                                _stream(dev)), "qmc_finalize")
+                                _p(T), T.shape[0] if T is not None else 0,
+                                T.shape[1] if T is not None else 0, _p(F),
+                                F.shape[1] if F is not None else 0, _stream(dev)), "qmc_finalize")
     return dict(acq=acq, mean=mean, cov=cov, L=L, info=info, jitter=jit)
 
 
@@ -363,3 +366,40 @@ def posterior_general(model, X3: torch.Tensor):
     cov = (Kxx - RR) * (ystd * ystd)
     mean = ymean + ystd * (mean + cache.constant)
     return mean, cov
+
+
+def cholesky_with_inverse(A: torch.Tensor, max_tries=CHOLESKY_MAX_TRIES,
+                          jitter0=CHOLESKY_JITTER_F64):
+    """psd_safe_cholesky of one n x n matrix on the device, with L^{-1}:
+    returns (L, Linv, jitter) as n x n views of np x np buffers."""
+    dev = _dev(A)
+    n = A.shape[-1]
+    np_ = padded_order(n)
+    L = torch.empty(np_, np_, dtype=torch.float64, device=dev)
+    Linv = torch.empty_like(L)
+    work = torch.empty_like(L)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    jit = ctypes.c_double(0.0)
+    check(lib().bo_cholesky_jitter(_p(A.contiguous()), n, _p(L), _p(Linv), _p(work), max_tries,
+                                   jitter0, ctypes.byref(jit), _p(info), _stream(dev)),
+          "cholesky_jitter")
+    if jit.value > 0:
+        import warnings
+        from .exceptions import NumericalWarning
+        warnings.warn(f"A not p.d., added jitter of {jit.value:.1e} to the diagonal",
+                      NumericalWarning)
+    return L[:n, :n], Linv[:n, :n], jit.value
+
+
+def sample_mvn(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor) -> torch.Tensor:
+    """f[s, b, i] = mean[b, i] + sum_j L[b, i, j] Z[s, j]  (S x B x q), as one
+    batched MFMA GEMM with the shared base samples broadcast (stride 0)."""
+    dev = _dev(mean, L, Z)
+    B, q = mean.shape
+    S = Z.shape[0]
+    Z = Z.reshape(S, q).contiguous()
+    L = L.contiguous()
+    out = torch.empty(B, S, q, dtype=torch.float64, device=dev)
+    check(lib().bo_gemm_f64(0, 1, S, q, q, 1.0, _p(Z), q, 0, _p(L), q, q * q, 0.0, _p(out), q,
+                            S * q, B, 0, _stream(dev)), "sample_mvn")
+    return out.permute(1, 0, 2) + mean.unsqueeze(0)

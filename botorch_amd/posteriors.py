@@ -143,8 +143,19 @@ class GPyTorchPosterior:
         if base_samples.shape[: len(sample_shape)] != sample_shape:
             raise RuntimeError("`sample_shape` disagrees with shape of `base_samples`.")
         L = self.distribution.scale_tril
+        mean = self.distribution.mean
+        batch, q = mean.shape[:-1], mean.shape[-1]
         Z = base_samples.to(L)
-        samples = self.distribution.mean + (L @ Z.unsqueeze(-1)).squeeze(-1)
+        nb = len(batch)
+        bstrides = Z.stride()[len(sample_shape): len(sample_shape) + nb]
+        if not torch.is_grad_enabled() or not (mean.requires_grad or L.requires_grad):
+            if all(s == 0 for s in bstrides) or all(b == 1 for b in Z.shape[len(sample_shape):-1]):
+                # base samples shared across t-batches (the collapsed sampler layout):
+                # one batched MFMA GEMM with the samples broadcast.
+                Z2 = Z.reshape(-1, *Z.shape[len(sample_shape):])[(slice(None),) + (0,) * nb]
+                f = kernels.sample_mvn(mean.reshape(-1, q), L.reshape(-1, q, q), Z2)
+                return f.reshape(*sample_shape, *batch, q, 1)
+        samples = mean + (L @ Z.unsqueeze(-1)).squeeze(-1)
         return samples.unsqueeze(-1)
 
     def rsample(self, sample_shape: Optional[torch.Size] = None):

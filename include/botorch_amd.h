@@ -169,13 +169,18 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
  *   acq (B): qEI  mean_s max_a relu(f - best_f)      [acquisition/monte_carlo.py:405-414]
  *            qNEI mean_s max_a relu(f - best_f_s[s])  [acquisition/monte_carlo.py:580-589]
  * Z: S x q base samples (SobolQMCNormalSampler, sampling/normal.py:178-209).
- * Output pointers may be NULL when not needed (acq required for QEI/QNEI). */
+ * Output pointers may be NULL when not needed (acq required for QEI/QNEI).
+ * Cached-root qNEI (utils/low_rank.py:85-173, acquisition/cached_cholesky.py):
+ * Tm (r x ldT) = L_rr^{-1} Sigma'(X_baseline, X) columns per padded test row,
+ * F (S x ldF) = Z_baseline Tm; then Sigma'_qq <- Sigma'_qq - Tm^T Tm and
+ * f = mean' + F + chol(.) Z (Z: the q new Sobol columns).  NULL otherwise. */
 int bo_qmc_finalize(int kind, int mode, int B, int q, const double* Xq, const double* Spart,
                     const double* mpart, int64_t n, double outputscale, double constant,
                     double ymean, double ystd, const double* Z, int S, double best_f,
                     const double* best_f_s, int max_tries, double jitter0, double* acq,
                     double* mean_out, double* cov_out, double* L_out, int* info_out,
-                    double* jitter_out, void* stream);
+                    double* jitter_out, const double* Tm, int r, int64_t ldT, const double* F,
+                    int64_t ldF, void* stream);
 
 /* Backward of the MC reduction + q x q Cholesky (gen_candidates_scipy's
  * autograd.grad, botorch/generation/gen.py:194-222):

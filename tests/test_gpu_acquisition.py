@@ -18,7 +18,7 @@ def _setup(n=256, d=6, seed=0, ls=0.35, noise=1e-3, const=0.1):
     Y = Hartmann(negate=True)(X[:, :6]).unsqueeze(-1)
     m = SingleTaskGP(X.to(DEV), Y.to(DEV))
     m.covar_module.lengthscale = torch.full((1, d), ls, dtype=torch.float64)
-    m.likelihood.noise = torch.tensor([noise])
+    m.likelihood.noise = torch.tensor([noise], dtype=torch.float64)
     m.mean_module.constant = const
     m.eval()
     orc = ExactGPOracle(X, Y, GPHyper(torch.full((d,), ls, dtype=torch.float64), noise, const))
@@ -154,3 +154,36 @@ def test_chol_jitter_ladder_matches_reference_semantics():
         L = kernels.chol_jitter(A.to(DEV)).cpu()
     Lr, jit = psd_safe_cholesky(A)
     torch.testing.assert_close(L, Lr, rtol=1e-7, atol=1e-9)
+
+
+@pytest.mark.parametrize("r,B,q,S", [(40, 16, 4, 128), (90, 12, 16, 256), (20, 5, 1, 64)])
+def test_qnei_cached_root_matches_oracle(r, B, q, S):
+    """qNEI (prune_baseline=False, cache_root=True) vs. the oracle's restatement of
+    sample_cached_cholesky; tolerance of north_star: 1e-2 on MC values."""
+    from botorch_amd.acquisition import qNoisyExpectedImprovement
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import QNEIOracle
+    X, Y, m, orc = _setup(n=200, noise=1e-2)
+    Xb = X[:r]
+    acqf = qNoisyExpectedImprovement(m, Xb.to(DEV), sampler=SobolQMCNormalSampler(torch.Size([S]), seed=11),
+                                     prune_baseline=False)
+    ref = QNEIOracle(orc, Xb, S, seed=11)
+    torch.testing.assert_close(acqf._baseline_best_f.cpu(), ref.best_f, rtol=1e-6, atol=1e-8)
+    g = torch.Generator().manual_seed(r)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64)
+    with torch.no_grad():
+        v = acqf(Xc.to(DEV)).cpu()
+    rv = ref(Xc)
+    torch.testing.assert_close(v, rv, rtol=1e-2, atol=1e-6)
+    torch.testing.assert_close(v, rv, rtol=1e-5, atol=1e-8)
+
+
+def test_prune_inferior_points_matches_oracle():
+    from botorch_amd.acquisition import prune_inferior_points
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import prune_inferior_points as prune_ref
+    X, Y, m, orc = _setup(n=300, noise=1e-2)
+    kept = prune_inferior_points(m, X.to(DEV), sampler=SobolQMCNormalSampler(torch.Size([512]), seed=3))
+    ref = prune_ref(orc, X, num_samples=512, seed=3)
+    assert kept.shape == ref.shape
+    torch.testing.assert_close(kept.cpu(), ref)

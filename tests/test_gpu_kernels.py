@@ -164,3 +164,27 @@ def test_not_psd_raises():
     with pytest.raises(NotPSDError):
         kernels.build_gp_cache(X.to(DEV), y.to(DEV), torch.full((6,), 0.3, dtype=torch.float64, device=DEV),
                                noise=-1.0, constant=0.0)
+
+
+def test_sobol_transform_accuracy_dense_grid():
+    """z(u) for every 30-bit u on a dense grid (state = 0, shift = u * 2^30)
+    against torch's CPU erfinv path (the reference's NormalQMCEngine)."""
+    from botorch_amd import kernels, _lib
+    import ctypes
+    g = torch.Generator().manual_seed(0)
+    ints = torch.cat([torch.randint(0, 2 ** 30, (20000,), generator=g),
+                      torch.arange(0, 64), 2 ** 30 - 1 - torch.arange(0, 64),
+                      2 ** 29 + torch.arange(-64, 64)]).to(torch.int64)
+    dim = ints.numel()
+    state = torch.zeros(dim, 30, dtype=torch.int64, device=DEV)
+    shift = ints.to(DEV)
+    out = torch.empty(1, dim, dtype=torch.float64, device=DEV)
+    _lib.check(_lib.lib().bo_sobol_normal(ctypes.c_void_p(state.data_ptr()), ctypes.c_void_p(shift.data_ptr()),
+                                          dim, 1, 0, ctypes.c_void_p(out.data_ptr()),
+                                          ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    u = ints.to(torch.float64) / 2 ** 30
+    v = 0.5 + (1 - torch.finfo(torch.float64).eps) * (u - 0.5)
+    ref = torch.erfinv(2 * v - 1) * math.sqrt(2)
+    err = (out.cpu().squeeze(0) - ref).abs()
+    i = int(err.argmax())
+    assert err.max() < 1e-13, f"max err {err.max():.3e} at u={u[i].item()!r} z={ref[i].item()!r} got {out.cpu()[0, i].item()!r}"
