@@ -16,49 +16,73 @@ namespace {
 
 constexpr int MAXBIT = 30;
 
+// Maclaurin series of erf for |x| <= 0.5 (terms fall by >= 4x: converged to
+// the last bit in < 25 terms).
+__device__ double erf_series(double x) {
+  const double x2 = x * x;
+  double term = x, sum = x;
+  for (int n = 1; n < 40; ++n) {
+    term *= -x2 / n;
+    const double c = term / (2 * n + 1);
+    sum += c;
+    if (fabs(c) <= 1e-18 * fabs(sum)) break;
+  }
+  return 1.1283791670955126 * sum;
+}
+
 // erfinv to ~1 ulp (torch's CPU erfinv is that accurate; the device library's
-// double erfinv is not -- measured 3.7e-7 relative near 0 on gfx950): Giles'
-// single-precision rational start, then three Halley steps on erf (erfc in
-// the tails, where 1 - |y| is exact and erf would cancel).
+// double erfinv is not -- measured 3.7e-7 relative near 0 on gfx950).  Start:
+// Giles' single-precision rational form, or for 1 - |y| < 1e-6 the asymptotic
+// erfc(x) ~ exp(-x^2) / (x sqrt(pi)); then Halley steps to convergence on
+// erf(x) - y through the series for |y| < 1/2, and on erfc(|x|) - (1 - |y|)
+// in the tails (1 - |y| is exact there, erf would cancel).
 __device__ double erfinv_accurate(double y) {
   const double ay = fabs(y);
   if (ay >= 1.0) return ay == 1.0 ? copysign(INFINITY, y) : NAN;
-  double w = -log((1.0 - y) * (1.0 + y));
-  double p;
-  if (w < 5.0) {
-    w -= 2.5;
-    p = 2.81022636e-08;
-    p = 3.43273939e-07 + p * w;
-    p = -3.5233877e-06 + p * w;
-    p = -4.39150654e-06 + p * w;
-    p = 0.00021858087 + p * w;
-    p = -0.00125372503 + p * w;
-    p = -0.00417768164 + p * w;
-    p = 0.246640727 + p * w;
-    p = 1.50140941 + p * w;
+  if (ay == 0.0) return y;
+  const double t = 1.0 - ay;  // exact for ay >= 1/2
+  double x;                   // |erfinv(y)|
+  if (t < 1e-6) {
+    x = sqrt(-log(t));
+    for (int i = 0; i < 4; ++i) x = sqrt(-log(t * x * 1.7724538509055160273));
   } else {
-    w = sqrt(w) - 3.0;
-    p = -0.000200214257;
-    p = 0.000100950558 + p * w;
-    p = 0.00134934322 + p * w;
-    p = -0.00367342844 + p * w;
-    p = 0.00573950773 + p * w;
-    p = -0.0076224613 + p * w;
-    p = 0.00943887047 + p * w;
-    p = 1.00167406 + p * w;
-    p = 2.83297682 + p * w;
+    double w = -log((1.0 - ay) * (1.0 + ay));
+    double p;
+    if (w < 5.0) {
+      w -= 2.5;
+      p = 2.81022636e-08;
+      p = 3.43273939e-07 + p * w;
+      p = -3.5233877e-06 + p * w;
+      p = -4.39150654e-06 + p * w;
+      p = 0.00021858087 + p * w;
+      p = -0.00125372503 + p * w;
+      p = -0.00417768164 + p * w;
+      p = 0.246640727 + p * w;
+      p = 1.50140941 + p * w;
+    } else {
+      w = sqrt(w) - 3.0;
+      p = -0.000200214257;
+      p = 0.000100950558 + p * w;
+      p = 0.00134934322 + p * w;
+      p = -0.00367342844 + p * w;
+      p = 0.00573950773 + p * w;
+      p = -0.0076224613 + p * w;
+      p = 0.00943887047 + p * w;
+      p = 1.00167406 + p * w;
+      p = 2.83297682 + p * w;
+    }
+    x = p * ay;
   }
-  double x = p * y;
   const double k = 1.1283791670955126;  // 2 / sqrt(pi)
-  for (int it = 0; it < 3; ++it) {
-    // erf(x) - y, written through erfc in the tails:  y > 0: (1 - y) - erfc(x),
-    // y < 0: erfc(|x|) - (1 - |y|).
-    const double f = (ay < 0.5) ? erf(x) - y
-                                : (erfc(fabs(x)) - (1.0 - ay)) * (y < 0.0 ? 1.0 : -1.0);
-    const double fp = k * exp(-x * x);
-    x = x - f / (fp + x * f);
+  for (int it = 0; it < 60; ++it) {
+    // g(x) = erf(x) - |y|  (= t - erfc(x) in the tails), g' = k exp(-x^2), g'' = -2 x g'
+    const double g = (ay < 0.5) ? erf_series(x) - ay : t - erfc(x);
+    const double gp = k * exp(-x * x);
+    const double dx = g / (gp + x * g);
+    x -= dx;
+    if (fabs(dx) <= 2e-16 * fabs(x)) break;
   }
-  return x;
+  return copysign(x, y);
 }
 
 __global__ void sobol_normal_kernel(const int64_t* __restrict__ state,

@@ -153,7 +153,7 @@ def test_sobol_normal_matches_golden(golden, d, n, seed):
     from botorch_amd import kernels
     z = kernels.sobol_normal(d, n, seed, DEV).cpu().numpy()
     ref = golden[f"sobol_normal_d{d}_n{n}_s{seed}"]
-    np.testing.assert_allclose(z, ref, rtol=0, atol=1e-13)
+    np.testing.assert_allclose(z, ref, rtol=4e-15, atol=4e-15)
 
 
 def test_not_psd_raises():
@@ -185,6 +185,6 @@ def test_sobol_transform_accuracy_dense_grid():
     u = ints.to(torch.float64) / 2 ** 30
     v = 0.5 + (1 - torch.finfo(torch.float64).eps) * (u - 0.5)
     ref = torch.erfinv(2 * v - 1) * math.sqrt(2)
-    err = (out.cpu().squeeze(0) - ref).abs()
+    err = (out.cpu().squeeze(0) - ref).abs() / ref.abs().clamp_min(1.0)
     i = int(err.argmax())
-    assert err.max() < 1e-13, f"max err {err.max():.3e} at u={u[i].item()!r} z={ref[i].item()!r} got {out.cpu()[0, i].item()!r}"
+    assert err.max() < 4e-15, f"max err {err.max():.3e} at u={u[i].item()!r} z={ref[i].item()!r} got {out.cpu()[0, i].item()!r}"
