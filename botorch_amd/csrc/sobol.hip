@@ -87,7 +87,7 @@ __device__ double erfinv_accurate(double y) {
 
 __global__ void sobol_normal_kernel(const int64_t* __restrict__ state,
                                     const int64_t* __restrict__ shift, int dim, int64_t n,
-                                    int64_t skip, double* __restrict__ out) {
+                                    int64_t skip, int first_f32, double* __restrict__ out) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= n * dim) return;
   const int64_t i = idx / dim + skip;
@@ -98,7 +98,11 @@ __global__ void sobol_normal_kernel(const int64_t* __restrict__ state,
 #pragma unroll
   for (int b = 0; b < MAXBIT; ++b)
     if ((g >> b) & 1ull) v ^= sj[b];
-  const double u = (double)v * (1.0 / 1073741824.0);
+  // torch's SobolEngine returns its first point as _first_point = quasi / 2**30
+  // computed at construction in the default dtype (float32 unless changed),
+  // so point 0 carries float32 rounding; every later point is exact.
+  const double u = (i == 0 && first_f32) ? (double)((float)v) * (1.0 / 1073741824.0)
+                                         : (double)v * (1.0 / 1073741824.0);
   const double eps = 2.220446049250313e-16;
   // Same op order as the reference (no fma contraction): v = 1/2 + (1-eps)(u-1/2).
   const double t = __dmul_rn(1.0 - eps, u - 0.5);
@@ -109,12 +113,12 @@ __global__ void sobol_normal_kernel(const int64_t* __restrict__ state,
 }  // namespace
 
 extern "C" int bo_sobol_normal(const int64_t* state, const int64_t* shift, int dim, int64_t n,
-                               int64_t skip, double* out, void* stream) {
+                               int64_t skip, int first_f32, double* out, void* stream) {
   BO_CHECK_ARG(dim > 0 && n >= 0 && skip >= 0, "bo_sobol_normal: bad shape");
   const int64_t tot = n * dim;
   if (tot == 0) return BO_OK;
   sobol_normal_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, as_stream(stream)>>>(
-      state, shift, dim, n, skip, out);
+      state, shift, dim, n, skip, first_f32, out);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

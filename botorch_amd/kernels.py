@@ -237,7 +237,8 @@ def sobol_normal(dim: int, n: int, seed: int, device, skip: int = 0) -> torch.Te
     state = state.to(device)
     shift = shift.to(device)
     out = torch.empty(n, dim, dtype=torch.float64, device=device)
-    check(lib().bo_sobol_normal(_p(state), _p(shift), dim, n, skip, _p(out),
+    first_f32 = int(torch.get_default_dtype() == torch.float32)
+    check(lib().bo_sobol_normal(_p(state), _p(shift), dim, n, skip, first_f32, _p(out),
                                 _stream(torch.device(device))), "sobol_normal")
     return out
 

@@ -218,9 +218,11 @@ int bo_mll_terms(int kind, const double* X, int64_t n, int d, const double* leng
 /* Scrambled Sobol N(0,1) samples, points skip..skip+n-1: out (n x dim).
  * state: dim x 30 int64 scrambled direction numbers, shift: dim int64
  * (torch.quasirandom.SobolEngine(dim, scramble=True, seed) state).
+ * first_f32: the engine's first point was formed in float32 (torch's default
+ * dtype at construction), so point 0 is rounded through float32 like it.
  * Replaces draw_sobol_normal_samples (botorch/utils/sampling.py:108-137). */
 int bo_sobol_normal(const int64_t* state, const int64_t* shift, int dim, int64_t n,
-                    int64_t skip, double* out, void* stream);
+                    int64_t skip, int first_f32, double* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -180,7 +180,7 @@ def test_sobol_transform_accuracy_dense_grid():
     shift = ints.to(DEV)
     out = torch.empty(1, dim, dtype=torch.float64, device=DEV)
     _lib.check(_lib.lib().bo_sobol_normal(ctypes.c_void_p(state.data_ptr()), ctypes.c_void_p(shift.data_ptr()),
-                                          dim, 1, 0, ctypes.c_void_p(out.data_ptr()),
+                                          dim, 1, 0, 0, ctypes.c_void_p(out.data_ptr()),
                                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     u = ints.to(torch.float64) / 2 ** 30
     v = 0.5 + (1 - torch.finfo(torch.float64).eps) * (u - 0.5)
