@@ -169,18 +169,28 @@ class qExpectedImprovement(MCAcquisitionFunction):
 
 
 # -- analytic ------------------------------------------------------------------------
+_INV_SQRT_2PI = 1 / math.sqrt(2 * math.pi)  # utils/probability/utils.py:27-29
+_NEG_INV_SQRT_2 = -(1 / math.sqrt(2))
+
+
 def _ndtr(x):
-    return 0.5 * torch.erfc(-x / math.sqrt(2))
+    """Standard normal CDF (utils/probability/utils.py:133-136)."""
+    return 0.5 * torch.erfc(_NEG_INV_SQRT_2 * x)
 
 
 def _phi(x):
-    return torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+    """Standard normal PDF (utils/probability/utils.py:139-142)."""
+    return _INV_SQRT_2PI * (-0.5 * x.square()).exp()
 
 
 class AnalyticAcquisitionFunction(AcquisitionFunction):
     def __init__(self, model, posterior_transform=None):
         super().__init__(model)
         self.posterior_transform = posterior_transform
+
+    def set_X_pending(self, X_pending=None) -> None:
+        """acquisition/analytic.py:78-82."""
+        raise UnsupportedError("Analytic acquisition functions do not account for X_pending yet.")
 
     def _mean_and_sigma(self, X, compute_sigma=True, min_var=1e-12):
         """acquisition/analytic.py:84-108."""
@@ -363,3 +373,83 @@ def _qnei_forward(acqf: "qNoisyExpectedImprovement", X3: torch.Tensor) -> torch.
                                T=T, F=F)
     kernels._raise_not_psd(out["info"], out["jitter"], "qNoisyExpectedImprovement")
     return out["acq"]
+
+
+# -- qEHVI ---------------------------------------------------------------------------
+class IdentityMCMultiOutputObjective(MCObjective):
+    """acquisition/multi_objective/objective.py (identity over outputs)."""
+
+    def __call__(self, samples, X=None):
+        return samples
+
+
+class qExpectedHypervolumeImprovement(MCAcquisitionFunction):
+    """MC qEHVI (acquisition/multi_objective/monte_carlo.py:146-322) over the
+    hypercells of a non-dominated partitioning.
+
+    Fused path (ModelListGP of SingleTaskGPs, identity objective): per output,
+    the exact posterior of the B t-batches (post_partials + the per-t-batch
+    jittered Cholesky, qmc_finalize in CHOL mode), then one bo_qehvi launch that
+    draws the non-interleaved Sobol samples and evaluates the inclusion-exclusion
+    hypervolume improvement over (sample, hypercell) pairs."""
+
+    _default_sample_shape = torch.Size([128])
+
+    def __init__(self, model, ref_point, partitioning, sampler=None, objective=None,
+                 constraints=None, X_pending=None, eta=1e-3, fat=False):
+        if len(ref_point) != partitioning.num_outcomes:
+            raise ValueError(
+                "The length of the reference point must match the number of outcomes. "
+                f"Got ref_point with {len(ref_point)} elements, but expected "
+                f"{partitioning.num_outcomes}.")
+        if constraints is not None:
+            raise UnsupportedError("outcome constraints are not on the accelerated path")
+        AcquisitionFunction.__init__(self, model)
+        self.sampler = sampler
+        self.objective = objective if objective is not None else IdentityMCMultiOutputObjective()
+        self.posterior_transform = None
+        self.set_X_pending(X_pending)
+        self.ref_point = torch.as_tensor(ref_point, dtype=torch.float64)
+        lo, hi = partitioning.get_hypercell_bounds()
+        self.cell_lower_bounds = lo.to(torch.float64)
+        self.cell_upper_bounds = hi.to(torch.float64)
+        self._dev_cells = {}
+
+    def _cells(self, device):
+        key = str(device)
+        if key not in self._dev_cells:
+            self._dev_cells[key] = (self.cell_lower_bounds.to(device).contiguous(),
+                                    self.cell_upper_bounds.to(device).contiguous())
+        return self._dev_cells[key]
+
+    def forward(self, X: torch.Tensor) -> torch.Tensor:
+        X = self._concat_pending(t_batch_mode(X))
+        batch = X.shape[:-2]
+        q, d = X.shape[-2], X.shape[-1]
+        X3 = X.reshape(-1, q, d)
+        models = getattr(self.model, "models", None)
+        if models is None or not all(hasattr(mm, "prediction_cache") for mm in models):
+            raise UnsupportedError("qEHVI here runs on a ModelListGP of SingleTaskGPs")
+        if not isinstance(self.objective, IdentityMCMultiOutputObjective):
+            raise UnsupportedError("only the identity multi-output objective is accelerated")
+        if X3.requires_grad:
+            raise UnsupportedError("qEHVI gradients are not implemented yet on the fused path")
+        if q > 12 or d > kernels.DP:
+            raise UnsupportedError("fused qEHVI supports q <= 12 and d <= 8")
+        m = len(models)
+        means, Ls = [], []
+        with torch.no_grad():
+            for mm in models:
+                cache = mm.prediction_cache()
+                ymean, ystd = mm.outcome_stats()
+                pp = kernels.post_partials(cache, X3)
+                out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
+                                           want_cov=False, want_L=True)
+                kernels._raise_not_psd(out["info"], out["jitter"], "qEHVI posterior root")
+                means.append(out["mean"])
+                Ls.append(out["L"])
+            sampler = self._ensure_sampler()
+            Z = sampler.base_samples_2d(q * m, X.device)
+            lo, hi = self._cells(X.device)
+            acq = kernels.qehvi(torch.stack(means), torch.stack(Ls), Z, lo, hi)
+        return acq.reshape(batch)

@@ -404,3 +404,28 @@ def sample_mvn(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor) -> torch.Te
     check(lib().bo_gemm_f64(0, 1, S, q, q, 1.0, _p(Z), q, 0, _p(L), q, q * q, 0.0, _p(out), q,
                             S * q, B, 0, _stream(dev)), "sample_mvn")
     return out.permute(1, 0, 2) + mean.unsqueeze(0)
+
+
+def qehvi(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor, cell_lo: torch.Tensor,
+          cell_hi: torch.Tensor) -> torch.Tensor:
+    """mean: m x B x q, L: m x B x q x q, Z: S x (q m) -> acq (B)."""
+    dev = _dev(mean, L, Z, cell_lo, cell_hi)
+    m, B, q = mean.shape
+    S = Z.shape[0]
+    acq = torch.empty(B, dtype=torch.float64, device=dev)
+    check(lib().bo_qehvi(B, q, m, _p(mean.contiguous()), _p(L.contiguous()),
+                         _p(Z.reshape(S, q * m).contiguous()), S, _p(cell_lo.contiguous()),
+                         _p(cell_hi.contiguous()), cell_lo.shape[0], _p(acq), _stream(dev)),
+          "qehvi")
+    return acq
+
+
+def mc_reduce(samples: torch.Tensor, best_f: float = 0.0,
+              best_f_s: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """samples: S x B x q -> qEI/qNEI value per t-batch."""
+    dev = _dev(samples)
+    S, B, q = samples.shape
+    acq = torch.empty(B, dtype=torch.float64, device=dev)
+    check(lib().bo_mc_reduce(S, B, q, _p(samples.contiguous()), float(best_f), _p(best_f_s),
+                             _p(acq), _stream(dev)), "mc_reduce")
+    return acq

@@ -215,6 +215,20 @@ int bo_mll_terms(int kind, const double* X, int64_t n, int d, const double* leng
                  double outputscale, const double* L, const double* Ainv, int64_t ld,
                  const double* alpha, const double* beta, double* partial, void* stream);
 
+/* qEHVI over hypercells ([lo, hi] K x m from the non-dominated partitioning,
+ * botorch/acquisition/multi_objective/monte_carlo.py:230-317) for B t-batches of
+ * q points of an m-output independent model (ModelListGP):
+ *   f[s][p][t] = mean[t][b][p] + sum_j L[t][b][p][j] Z[s][j m + t]
+ *   acq[b] = mean_s sum_k inclusion-exclusion volume.
+ * mean: m x B x q, L: m x B x q x q, Z: S x (q m).  2 <= m <= 4, q <= 12. */
+int bo_qehvi(int B, int q, int m, const double* mean, const double* L, const double* Z, int S,
+             const double* cell_lo, const double* cell_hi, int K, double* acq, void* stream);
+
+/* MC qEI / qNEI reduction of given samples (S x B x q):
+ * acq[b] = mean_s max(max_a samples[s][b][a] - bf_s, 0), bf_s = best_f_s[s] or best_f. */
+int bo_mc_reduce(int S, int B, int q, const double* samples, double best_f,
+                 const double* best_f_s, double* acq, void* stream);
+
 /* Scrambled Sobol N(0,1) samples, points skip..skip+n-1: out (n x dim).
  * state: dim x 30 int64 scrambled direction numbers, shift: dim int64
  * (torch.quasirandom.SobolEngine(dim, scramble=True, seed) state).

@@ -187,3 +187,35 @@ def test_prune_inferior_points_matches_oracle():
     ref = prune_ref(orc, X, num_samples=512, seed=3)
     assert kept.shape == ref.shape
     torch.testing.assert_close(kept.cpu(), ref)
+
+
+@pytest.mark.parametrize("B,q,S", [(6, 2, 64), (4, 4, 128)])
+def test_qehvi_api_matches_oracle(golden, B, q, S):
+    from botorch_amd.acquisition import qExpectedHypervolumeImprovement
+    from botorch_amd.models import ModelListGP, SingleTaskGP
+    from botorch_amd.multi_objective import FastNondominatedPartitioning
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import qehvi
+    from oracle.gp import ExactGPOracle, GPHyper
+    from oracle.sampling import base_samples_multi_output
+    X = torch.from_numpy(golden["dtlz2_X"][:96])
+    Y = torch.from_numpy(golden["dtlz2_Y"][:96])
+    models, oracles = [], []
+    for t in range(3):
+        mdl = SingleTaskGP(X.to(DEV), Y[:, t:t + 1].to(DEV))
+        mdl.covar_module.lengthscale = torch.full((1, 6), 0.6, dtype=torch.float64)
+        mdl.likelihood.noise = torch.tensor([1e-3], dtype=torch.float64)
+        models.append(mdl.eval())
+        oracles.append(ExactGPOracle(X, Y[:, t:t + 1], GPHyper(torch.full((6,), 0.6, dtype=torch.float64), 1e-3, 0.0)))
+    ref_point = torch.full((3,), -1.1, dtype=torch.float64)
+    part = FastNondominatedPartitioning(ref_point, Y)
+    acqf = qExpectedHypervolumeImprovement(ModelListGP(*models), ref_point.tolist(), part,
+                                           sampler=SobolQMCNormalSampler(torch.Size([S]), seed=4))
+    g = torch.Generator().manual_seed(q)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64)
+    with torch.no_grad():
+        v = acqf(Xc.to(DEV)).cpu()
+    lo, hi = part.get_hypercell_bounds()
+    ref = qehvi(oracles, Xc, base_samples_multi_output(S, q, 3, 4), lo, hi)
+    torch.testing.assert_close(v, ref, rtol=1e-2, atol=1e-8)
+    torch.testing.assert_close(v, ref, rtol=1e-7, atol=1e-10)
