@@ -140,6 +140,11 @@ class _FusedMC(torch.autograd.Function):
         return dX, None, None, None, None, None
 
 
+def _ensemble_mean(model, acq: torch.Tensor) -> torch.Tensor:
+    """Average over the MCMC batch of ensemble models (utils/transforms.py:289-293)."""
+    return acq.mean(dim=-1) if getattr(model, "_is_ensemble", False) else acq
+
+
 class qExpectedImprovement(MCAcquisitionFunction):
     """MC batch EI (acquisition/monte_carlo.py:332-414):
     qEI(X) = E[max_j max(Y_j - best_f, 0)]."""
@@ -165,7 +170,8 @@ class qExpectedImprovement(MCAcquisitionFunction):
         samples = self.get_posterior_samples(posterior)
         obj = self.objective(samples, X=X)
         bf = self.best_f.to(obj).unsqueeze(-1)
-        return (obj - bf).clamp_min(0).amax(dim=-1).mean(dim=0)
+        acq = (obj - bf).clamp_min(0).amax(dim=-1).mean(dim=0)
+        return _ensemble_mean(self.model, acq)
 
 
 # -- analytic ------------------------------------------------------------------------

@@ -262,7 +262,7 @@ class SingleTaskGP(Model):
 
     def hyper(self):
         ls = self.covar_module.lengthscale.detach().reshape(-1)
-        os_ = float(self.covar_module.outputscale) if isinstance(self.covar_module, ScaleKernel) else 1.0
+        os_ = float(self.covar_module.outputscale.detach()) if isinstance(self.covar_module, ScaleKernel) else 1.0
         return ls, os_, float(self.likelihood.noise.detach()), float(self.mean_module.constant.detach())
 
     def outcome_stats(self):
@@ -325,3 +325,133 @@ class ModelListGP(Model):
         for m in self.models:
             m.train(mode)
         return super().train(mode)
+
+
+MCMC_DIM = -3  # models/fully_bayesian.py: posterior batch dim of the MCMC samples
+
+
+def sample_saas_prior(d: int, num_samples: int, seed: int = 0, dtype=torch.float64):
+    """Hyperparameter sets from the SAAS prior (models/fully_bayesian.py:168-247):
+    outputscale ~ Gamma(2, 0.15), mean ~ N(0, 1), noise = 1e-4 + Gamma(0.9, 10),
+    tau^2 ~ HalfCauchy(0.1), inv_len^2 ~ HalfCauchy(1)^d, lengthscale =
+    (tau^2 inv_len^2)^{-1/2}.  (NUTS itself is out of scope: pyro is absent.)"""
+    g = torch.Generator().manual_seed(seed)
+    M = num_samples
+
+    def gamma(conc, rate, shape):
+        # Marsaglia-Tsang through torch's generator-aware _standard_gamma
+        return torch._standard_gamma(torch.full(shape, conc, dtype=dtype), generator=g) / rate
+
+    def half_cauchy(scale, shape):
+        u = torch.rand(shape, generator=g, dtype=dtype)
+        return scale * torch.tan(0.5 * math.pi * u)
+
+    tausq = half_cauchy(0.1, (M, 1))
+    inv_len_sq = half_cauchy(1.0, (M, d))
+    return {
+        "outputscale": gamma(2.0, 0.15, (M,)),
+        "mean": torch.randn(M, generator=g, dtype=dtype),
+        "noise": MIN_INFERRED_NOISE_LEVEL + gamma(0.9, 10.0, (M,)),
+        "lengthscale": (tausq * inv_len_sq).rsqrt(),
+    }
+
+
+class SaasFullyBayesianSingleTaskGP(Model):
+    """Fully Bayesian SAAS GP (models/fully_bayesian.py:315-546): M hyperparameter
+    sets (MCMC samples) of a ScaleKernel(Matern-5/2) GP with constant mean and
+    Gaussian noise, evaluated as an ensemble.  The posterior at X (b x q x d) has
+    batch shape b x M (X is broadcast over MCMC_DIM = -3); acquisition values are
+    averaged over M (utils/transforms.py:289-293).
+
+    Each member is an exact GP with its own device caches (Matern-5/2 kernel
+    matrix, blocked MFMA Cholesky, L^{-T}); the q-batch posterior runs through
+    the generic kernels (d = 50 exceeds the fused kernel's register-resident
+    inputs)."""
+
+    _is_fully_bayesian = True
+    _is_ensemble = True
+
+    def __init__(self, train_X, train_Y, train_Yvar=None, outcome_transform=None,
+                 input_transform=None, pyro_model=None):
+        super().__init__()
+        if not (train_X.ndim == train_Y.ndim == 2 and len(train_X) == len(train_Y)
+                and train_Y.shape[-1] == 1):
+            raise ValueError("Expected train_X to have shape n x d and train_Y to have shape n x 1")
+        if train_Yvar is not None or input_transform is not None:
+            raise UnsupportedError("fixed noise / input transforms are not on the accelerated path")
+        train_X = train_X.to(torch.float64)
+        train_Y = train_Y.to(torch.float64)
+        if outcome_transform is not None:
+            outcome_transform.train()
+            train_Y, _ = outcome_transform(train_Y)
+            self.outcome_transform = outcome_transform
+        self.train_inputs = (train_X,)
+        self.train_targets = train_Y.squeeze(-1)
+        self._members = None
+
+    def load_mcmc_samples(self, mcmc_samples) -> None:
+        """models/fully_bayesian.py:249-312 (batched modules from the samples)."""
+        X = self.train_inputs[0]
+        d = X.shape[-1]
+        M = len(mcmc_samples["mean"])
+        members = []
+        for i in range(M):
+            base = MaternKernel(ard_num_dims=d, lengthscale_lower=0.0, initial=1.0)
+            base.lengthscale = mcmc_samples["lengthscale"][i].reshape(1, d)
+            k = ScaleKernel(base, outputscale=float(mcmc_samples["outputscale"][i]))
+            lik = GaussianLikelihood(noise_lower=MIN_INFERRED_NOISE_LEVEL, initial=max(
+                float(mcmc_samples["noise"][i]), MIN_INFERRED_NOISE_LEVEL))
+            mean = ConstantMean()
+            mean.constant = float(mcmc_samples["mean"][i])
+            mdl = SingleTaskGP(X, self.train_targets.unsqueeze(-1), likelihood=lik, covar_module=k,
+                               mean_module=mean, outcome_transform=None)
+            members.append(mdl.eval())
+        self._members = nn.ModuleList(members)
+
+    @property
+    def num_mcmc_samples(self) -> int:
+        if self._members is None:
+            raise RuntimeError("Model has not been fitted. You need to call "
+                               "`fit_fully_bayesian_model_nuts` to fit the model.")
+        return len(self._members)
+
+    @property
+    def batch_shape(self) -> torch.Size:
+        return torch.Size([self.num_mcmc_samples])
+
+    def train(self, mode: bool = True):
+        super().train(mode)
+        if mode:
+            self._members = None
+        return self
+
+    def posterior(self, X, output_indices=None, observation_noise=False, posterior_transform=None):
+        """models/fully_bayesian.py:509-546 -> GaussianMixturePosterior (batch b x M)."""
+        from . import kernels
+        from .posteriors import GPyTorchPosterior, MultivariateNormal
+        M = self.num_mcmc_samples
+        batch, q, d = X.shape[:-2], X.shape[-2], X.shape[-1]
+        X3 = X.reshape(-1, q, d)
+        means, covs = [], []
+        for mdl in self._members:
+            mu, cov = kernels.posterior_general(mdl, X3)
+            if hasattr(self, "outcome_transform"):
+                tf = self.outcome_transform
+                s = float(tf.stdvs.reshape(-1)[0])
+                mu = float(tf.means.reshape(-1)[0]) + s * mu
+                cov = cov * (s * s)
+            if observation_noise is True:
+                cov = cov + mdl.likelihood.noise.reshape(()) * torch.eye(q, dtype=cov.dtype, device=cov.device)
+            means.append(mu)
+            covs.append(cov)
+        mean = torch.stack(means, dim=1).reshape(*batch, M, q)
+        cov = torch.stack(covs, dim=1).reshape(*batch, M, q, q)
+        post = GPyTorchPosterior(MultivariateNormal(mean, cov), model=self, X=X)
+        post._is_ensemble = True
+        return post if posterior_transform is None else posterior_transform(post)
+
+
+def fit_fully_bayesian_model_nuts(model, **kwargs):
+    """botorch/fit.py:335-391 -- NUTS over the SAAS prior needs pyro, which is not
+    available (out of scope); load hyperparameters with ``load_mcmc_samples``."""
+    raise UnsupportedError("NUTS fitting (pyro) is out of scope; use load_mcmc_samples")

@@ -138,3 +138,23 @@ def qehvi(models, X, Z, cell_lower, cell_upper):
         samples.append(mc_samples(mean, cov, Z[:, t, :]))
     obj = torch.stack(samples, dim=-1)  # S x b x q x m
     return qehvi_from_samples(obj, cell_lower, cell_upper)
+
+
+def saas_members(train_X, train_Y, mcmc_samples, standardize=False):
+    """SaasFullyBayesianSingleTaskGP.load_mcmc_samples (models/fully_bayesian.py:
+    267-312): one Matern-5/2 x outputscale exact GP per MCMC sample, noise
+    clamped at 1e-4."""
+    from .gp import MATERN52, GPHyper
+    out = []
+    for i in range(len(mcmc_samples["mean"])):
+        h = GPHyper(mcmc_samples["lengthscale"][i].double().reshape(-1),
+                    max(float(mcmc_samples["noise"][i]), 1e-4), float(mcmc_samples["mean"][i]),
+                    float(mcmc_samples["outputscale"][i]), MATERN52)
+        out.append(ExactGPOracle(train_X, train_Y, h, standardize=standardize))
+    return out
+
+
+def saas_qei(members, X, Z, best_f):
+    """qEI on the b x M mixture posterior (fully_bayesian.py:509-546), averaged
+    over MCMC_DIM by t_batch_mode_transform (utils/transforms.py:289-293)."""
+    return torch.stack([qei(m, X, Z, best_f) for m in members], dim=-1).mean(dim=-1)

@@ -219,3 +219,36 @@ def test_qehvi_api_matches_oracle(golden, B, q, S):
     ref = qehvi(oracles, Xc, base_samples_multi_output(S, q, 3, 4), lo, hi)
     torch.testing.assert_close(v, ref, rtol=1e-2, atol=1e-8)
     torch.testing.assert_close(v, ref, rtol=1e-7, atol=1e-10)
+
+
+@pytest.mark.parametrize("d,M,q", [(50, 16, 4), (10, 3, 2)])
+def test_saas_qei_matches_oracle(d, M, q):
+    """C5 shape: SAAS ensemble of M Matern-5/2 GPs, d=50, qEI averaged over MCMC_DIM."""
+    from botorch_amd.acquisition import qExpectedImprovement
+    from botorch_amd.models import SaasFullyBayesianSingleTaskGP, sample_saas_prior
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from botorch_amd.test_functions import Hartmann
+    from oracle.acquisition import saas_members, saas_qei
+    from oracle.sampling import base_samples_single_output, draw_sobol_samples
+    n, S, B = 256, 256, 12
+    lo = torch.zeros(d, dtype=torch.float64)
+    X = draw_sobol_samples(lo, lo + 1, n, 1, 0).squeeze(1)
+    Y = Hartmann(negate=True)(X[:, :6]).unsqueeze(-1)
+    Y = (Y - Y.mean()) / Y.std()
+    smp = sample_saas_prior(d, M, seed=0)
+    m = SaasFullyBayesianSingleTaskGP(X.to(DEV), Y.to(DEV))
+    m.load_mcmc_samples({k: v.to(DEV) for k, v in smp.items()})
+    m.eval()
+    Xc = draw_sobol_samples(lo, lo + 1, B, q, 1)
+    post = m.posterior(Xc.to(DEV))
+    assert post.mean.shape == (B, M, q, 1)
+    members = saas_members(X, Y, smp)
+    mr = torch.stack([mm.posterior(Xc)[0] for mm in members], dim=1)
+    torch.testing.assert_close(post.mean.squeeze(-1).cpu(), mr, rtol=1e-4, atol=1e-8)
+    best_f = float(Y.max())
+    acqf = qExpectedImprovement(m, best_f, sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
+    with torch.no_grad():
+        val = acqf(Xc.to(DEV)).cpu()
+    assert val.shape == (B,)
+    ref = saas_qei(members, Xc, base_samples_single_output(S, q, 0), best_f)
+    torch.testing.assert_close(val, ref, rtol=1e-2, atol=1e-6)
