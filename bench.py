@@ -53,6 +53,19 @@ def flops_post_partials(B, q, n):
     return B * q * n * n + 2 * B * q * q * n + 2 * B * q * n + B * q * n * (3 * D + 3)
 
 
+def pmc_traffic(kernel="post_partials_kernel<0, 6>"):
+    """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 PMC
+    summary (profiles/rNN/pmc_summary.json, written by tools/pmc_summary.py from
+    separate --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command,
+    FETCH_SIZE doubled per the gfx950 correction).  None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")))
+    if not files:
+        return None, None
+    e = json.load(open(files[-1])).get(kernel, {})
+    return e.get("hbm_bytes"), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_cores():
     """Host cores this process may use: the affinity mask, capped by
     OMP_NUM_THREADS (the GPU box grants a 16-core share of a larger host)."""
@@ -146,7 +159,7 @@ def time_gp_fit(Xtr, Ytr, dev, cpu=True):
     fitmod.mll_value_and_grad = orig
     out = {"ms": ms, "closures": calls[0], "ms_per_closure": ms / max(1, calls[0]),
            "n": int(Xtr.shape[0]), "lengthscale": model.covar_module.lengthscale.detach().reshape(-1).tolist(),
-           "noise": float(model.likelihood.noise)}
+           "noise": float(model.likelihood.noise.detach())}
     if cpu:
         from oracle.gp import neg_mll, standardize_fit
         torch.set_num_threads(cpu_cores())
@@ -249,6 +262,7 @@ def main():
     fl = flops_post_partials(RESTARTS, Q, N_TRAIN)
     achieved = fl / (kern_avg_ms * 1e-3) / 1e12
     peak = 78.6  # MI355X dense FP64 matrix TFLOP/s (MI355X_MICROARCH.md / SURVEY.md 8(d))
+    traffic, traffic_src = pmc_traffic()
 
     gp_fit = None
     if rank == 0 and not args.no_fit:
@@ -276,7 +290,8 @@ def main():
                        "parallelism": f"restart-sharded x{ws}"},
             "roofline": {"bound": "mfma", "kernel": "post_partials_kernel",
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": None,
+                         "frac": achieved / peak, "traffic": traffic,
+                         "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "kernel_ms": kern_avg_ms, "flops_per_launch": fl},
             "cpu_baseline": cpu,
             "gp_fit": gp_fit,
