@@ -55,14 +55,20 @@ _SIGNATURES = {
                                 c_double, _P, _P, _P, _P, _P, _P, _P, c_int, c_int64, _P,
                                 c_int64, _P]),
     "bo_qehvi": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, _P, _P, c_int, _P, _P]),
+    "bo_qehvi_backward": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, _P, _P, c_int, _P, _P, _P,
+                                  _P]),
+    "bo_chol_backward": (c_int, [c_int, c_int, _P, _P, _P, _P]),
+    "bo_probe_potrf_phases": (c_int, [_P, c_int64, _P, _P, _P, _P]),
+    "bo_kernel_grad": (c_int, [c_int, _P, c_int64, _P, c_int64, c_int, _P, c_double, _P, c_int64,
+                               c_int, c_int, _P, _P]),
     "bo_mc_reduce": (c_int, [c_int, c_int, c_int, _P, c_double, _P, _P, _P]),
     "bo_sobol_normal": (c_int, [_P, _P, c_int, c_int64, c_int64, c_int, _P, _P]),
     "bo_mll_terms": (c_int, [c_int, _P, c_int64, c_int, _P, c_double, _P, _P, c_int64, _P, _P, _P,
                              _P]),
-    "bo_qmc_backward": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, c_double, _P, _P, _P,
-                                _P, _P]),
+    "bo_qmc_backward": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, c_double, _P, _P,
+                                c_int64, _P, _P, _P, _P, _P]),
     "bo_post_backward": (c_int, [c_int, c_int, c_int, c_int, _P, _P, c_int64, _P, c_int64, _P,
-                                 _P, _P, _P, c_double, c_double, _P, _P]),
+                                 _P, _P, _P, c_int64, _P, c_double, c_double, c_int, _P, _P]),
 }
 
 _lib = None

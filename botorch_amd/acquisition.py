@@ -166,12 +166,85 @@ class qExpectedImprovement(MCAcquisitionFunction):
             Z = sampler.base_samples_2d(q, X.device)
             acq = _FusedMC.apply(X3, self, _lib.QMC_QEI, float(self.best_f), None, Z)
             return acq.reshape(batch)
+        if (getattr(self.model, "_is_fully_bayesian", False) and X.is_cuda
+                and isinstance(self.objective, IdentityMCObjective) and self.posterior_transform is None
+                and len(self.sample_shape) == 1 and self.best_f.numel() == 1 and q <= FUSED_QMAX):
+            sampler = self._ensure_sampler()
+            Z = sampler.base_samples_2d(q, X.device)
+            return _SaasQEI.apply(X3, self, float(self.best_f), Z).reshape(batch)
         posterior = self.model.posterior(X, posterior_transform=self.posterior_transform)
         samples = self.get_posterior_samples(posterior)
         obj = self.objective(samples, X=X)
         bf = self.best_f.to(obj).unsqueeze(-1)
         acq = (obj - bf).clamp_min(0).amax(dim=-1).mean(dim=0)
         return _ensemble_mean(self.model, acq)
+
+
+class _SaasQEI(torch.autograd.Function):
+    """qEI over the MCMC ensemble of a SAAS model (models/fully_bayesian.py:509-546,
+    averaged over MCMC_DIM as utils/transforms.py:289-293), any d <= 128.
+
+    Per member m (exact GP, Matern-5/2 x outputscale): K*x (bo_covar_matrix),
+    R = K*x L^{-T} and the R R^T blocks (MFMA GEMMs), jittered q x q root
+    (bo_cholesky ladder), reparameterised samples (batched GEMM) and the qEI
+    reduction (bo_mc_reduce).  Backward: bo_qmc_backward -> d mu, d Sigma;
+    d K*x = d mu alpha^T - G W (W = R L^{-1}); bo_kernel_grad for K*x and K**."""
+
+    @staticmethod
+    def forward(ctx, X3, acqf, best_f, Z):
+        model = acqf.model
+        B, q, d = X3.shape
+        X2 = X3.detach().reshape(B * q, d).contiguous()
+        need_grad = ctx.needs_input_grad[0]
+        ym, ys = 0.0, 1.0
+        if hasattr(model, "outcome_transform"):
+            ym = float(model.outcome_transform.means.reshape(-1)[0])
+            ys = float(model.outcome_transform.stdvs.reshape(-1)[0])
+        acq = None
+        saved = []
+        M = model.num_mcmc_samples
+        for mdl in model._members:
+            cache = mdl.prediction_cache()
+            n = cache.n
+            Kx = kernels.covar_matrix(X2, cache.Xt, cache.lengthscale, cache.kind, cache.outputscale)
+            R = kernels.gemm(Kx, cache.U[:n, :n], flags=_lib.GEMM_B_UPPER)
+            mean = kernels.gemm(Kx, cache.alpha.reshape(n, 1)).reshape(B, q)
+            RR = kernels.gemm(R.reshape(B, q, n), R.reshape(B, q, n), transB=True)
+            Kxx = kernels.covar_blocks(X3.detach(), cache.lengthscale, cache.kind, cache.outputscale)
+            cov = (Kxx - RR) * (ys * ys)
+            mean = ym + ys * (mean + cache.constant)
+            L = kernels.chol_jitter(cov)
+            f = kernels.sample_mvn(mean, L, Z)
+            a_m = kernels.mc_reduce(f, best_f)
+            acq = a_m if acq is None else acq + a_m
+            if need_grad:
+                saved.append((cache, Kx, R, mean, L))
+        acq = acq / M
+        if need_grad:
+            ctx.saved, ctx.X2, ctx.Z, ctx.best_f, ctx.shape, ctx.ys, ctx.M = (
+                saved, X2, Z, best_f, (B, q, d), ys, M)
+        return acq
+
+    @staticmethod
+    def backward(ctx, dacq):
+        B, q, d = ctx.shape
+        ys = ctx.ys
+        dX = None
+        da = (dacq / ctx.M).contiguous()
+        for cache, Kx, R, mean, L in ctx.saved:
+            n = cache.n
+            dmean, dcov = kernels.qmc_backward(_lib.QMC_QEI, mean, L, ctx.Z, da, ctx.best_f)
+            dmu = ys * dmean                                   # standardized space
+            G = (ys * ys) * (dcov + dcov.mT)
+            W = kernels.gemm(R, cache.U[:n, :n], transB=True, flags=_lib.GEMM_B_LOWER)
+            dK = dmu.reshape(B * q, 1) * cache.alpha.reshape(1, n)
+            kernels.gemm(G.contiguous(), W.reshape(B, q, n), alpha=-1.0, beta=1.0,
+                         C=dK.reshape(B, q, n))
+            dX = kernels.kernel_grad(ctx.X2, cache.Xt, dK, cache.lengthscale, cache.kind,
+                                     cache.outputscale, dX=dX)
+            dX = kernels.kernel_grad(ctx.X2, ctx.X2, G.reshape(B * q, q), cache.lengthscale,
+                                     cache.kind, cache.outputscale, group=q, dX=dX)
+        return dX.reshape(B, q, d), None, None, None
 
 
 # -- analytic ------------------------------------------------------------------------
@@ -333,6 +406,9 @@ class qNoisyExpectedImprovement(MCAcquisitionFunction):
                 P_b = torch.zeros(r, cache.np, dtype=torch.float64, device=Kb.device)
                 P_b[:, : cache.n] = kernels.gemm(self._Linv_rr, R_b, flags=_lib.GEMM_A_LOWER)
                 self._P_b = P_b
+                # Q_b = P_b U^T = L_rr^{-1} K(X_b, X_tr) A^{-1}  (gradient of the
+                # cross-covariance through R = K*x L^{-T})
+                self._Q_b = kernels.gemm(P_b, cache.U, transB=True, flags=_lib.GEMM_B_LOWER)
                 self._Xb_scaled = torch.zeros(r, kernels.DP, dtype=torch.float64, device=Kb.device)
                 self._Xb_scaled[:, : cache.d] = X_baseline / cache.lengthscale
                 self._fused_ready = True
@@ -355,33 +431,115 @@ class qNoisyExpectedImprovement(MCAcquisitionFunction):
         if not (self._fused_eligible(X) and self._fused_ready):
             raise UnsupportedError(
                 f"qNEI here needs the fused path (q <= {FUSED_QMAX}, d <= {kernels.DP}, identity objective)")
-        if X3.requires_grad:
-            raise UnsupportedError("qNEI gradients are not implemented yet on the fused path")
-        acq = _qnei_forward(self, X3.detach())
+        acq = _FusedQNEI.apply(X3, self)
         return acq.reshape(batch)
 
 
-def _qnei_forward(acqf: "qNoisyExpectedImprovement", X3: torch.Tensor) -> torch.Tensor:
-    model = acqf.model
-    cache = model.prediction_cache()
-    ymean, ystd = model.outcome_stats()
-    q = X3.shape[-2]
-    s2 = ystd * ystd
-    pp = kernels.post_partials(cache, X3, store_R=True)
-    ones = torch.ones(kernels.DP, dtype=torch.float64, device=X3.device)
-    Kbx = kernels.covar_matrix(acqf._Xb_scaled, pp.Xq, ones, cache.kind, cache.outputscale)
-    T = kernels.gemm(acqf._Linv_rr, Kbx, alpha=s2, flags=_lib.GEMM_A_LOWER)
-    T = kernels.gemm(acqf._P_b, pp.Rt, alpha=-s2, beta=1.0, C=T)
-    F = kernels.gemm(acqf.Z_base, T)
-    Zq = acqf._base_samples_q(q, X3.device)
-    out = kernels.qmc_finalize(cache, pp, _lib.QMC_QNEI, ymean, ystd, Z=Zq,
-                               best_f_s=acqf._baseline_best_f, want_mean=False, want_cov=False,
-                               T=T, F=F)
-    kernels._raise_not_psd(out["info"], out["jitter"], "qNoisyExpectedImprovement")
-    return out["acq"]
+class _FusedQNEI(torch.autograd.Function):
+    """qNEI value of B t-batches on the cached-root fused path, with its gradient.
+
+    Forward: post_partials (+ R^T), T = L_rr^{-1} Sigma'(X_b, X) =
+    s^2 (L_rr^{-1} K_bX - P_b R^T), F = Z_b T, qmc_finalize(QNEI) on
+    Sigma_cond = Sigma' - T^T T.
+    Backward (utils/low_rank.py:85-173 differentiated):
+      qmc_backward -> d mu', d Sigma_cond, dF;   dT = Z_b^T dF - T (G_b), G_b = dS + dS^T
+      d K*x += -s^2 dT^T Q_b   (Q_b = P_b U^T, through R = K*x L^{-T})
+      d K_bX = s^2 L_rr^{-T} dT (through K(X_b, X))
+    and post_backward reduces both through dk/dx."""
+
+    @staticmethod
+    def forward(ctx, X3, acqf):
+        model = acqf.model
+        cache = model.prediction_cache()
+        ymean, ystd = model.outcome_stats()
+        q = X3.shape[-2]
+        s2 = ystd * ystd
+        need_grad = ctx.needs_input_grad[0]
+        pp = kernels.post_partials(cache, X3.detach(), store_R=True)
+        ones = torch.ones(kernels.DP, dtype=torch.float64, device=X3.device)
+        Kbx = kernels.covar_matrix(acqf._Xb_scaled, pp.Xq, ones, cache.kind, cache.outputscale)
+        T = kernels.gemm(acqf._Linv_rr, Kbx, alpha=s2, flags=_lib.GEMM_A_LOWER)
+        T = kernels.gemm(acqf._P_b, pp.Rt, alpha=-s2, beta=1.0, C=T)
+        F = kernels.gemm(acqf.Z_base, T)
+        Zq = acqf._base_samples_q(q, X3.device)
+        out = kernels.qmc_finalize(cache, pp, _lib.QMC_QNEI, ymean, ystd, Z=Zq,
+                                   best_f_s=acqf._baseline_best_f, want_mean=need_grad,
+                                   want_cov=False, want_L=need_grad, T=T, F=F)
+        kernels._raise_not_psd(out["info"], out["jitter"], "qNoisyExpectedImprovement")
+        if need_grad:
+            ctx.acqf, ctx.cache, ctx.pp, ctx.ystd = acqf, cache, pp, ystd
+            ctx.T, ctx.F, ctx.Zq = T, F, Zq
+            ctx.mean, ctx.L = out["mean"], out["L"]
+            ctx.W = kernels.w_matrix(cache, pp)
+        return out["acq"]
+
+    @staticmethod
+    def backward(ctx, dacq):
+        acqf, cache, pp, ystd = ctx.acqf, ctx.cache, ctx.pp, ctx.ystd
+        s2 = ystd * ystd
+        B, q, Qp, nrows = pp.B, pp.q, pp.Qp, pp.nrows_pad
+        r = acqf._Linv_rr.shape[0]
+        dmean, dcov, dF = kernels.qmc_backward(_lib.QMC_QNEI, ctx.mean, ctx.L, ctx.Zq,
+                                               dacq.contiguous(), best_f_s=acqf._baseline_best_f,
+                                               F=ctx.F)
+        dT = kernels.gemm(acqf.Z_base, dF, transA=True)           # r x nrows_pad
+        G = (dcov + dcov.mT).contiguous()                         # B x q x q
+        kernels.gemm_strided(r, q, q, ctx.T, nrows, Qp, G, q, q * q, dT, nrows, Qp, B,
+                             alpha=-1.0, beta=1.0)                 # dT_b -= T_b G_b
+        E = kernels.gemm(dT, acqf._Q_b, transA=True, alpha=-s2)   # nrows_pad x np
+        dKbx = kernels.gemm(acqf._Linv_rr, dT, transA=True, alpha=s2, flags=_lib.GEMM_A_UPPER)
+        dX = kernels.post_backward(cache, pp, ctx.W, dmean, dcov, ystd, E=E)
+        dX = kernels.post_backward(cache, pp, None, None, None, ystd, E=dKbx.mT.contiguous(),
+                                   Xt_scaled=acqf._Xb_scaled, n=r, dX=dX)
+        return dX, None
 
 
 # -- qEHVI ---------------------------------------------------------------------------
+class _FusedQEHVI(torch.autograd.Function):
+    """qEHVI of B t-batches over a ModelListGP, with its gradient.
+
+    Forward: per output, post_partials + qmc_finalize(CHOL) (posterior mean and
+    jittered q x q root), then bo_qehvi over (sample, cell) pairs.
+    Backward: bo_qehvi_backward (inclusion-exclusion derivative) -> d mu_t, d L_t;
+    bo_chol_backward -> d Sigma_t; bo_post_backward per output model."""
+
+    @staticmethod
+    def forward(ctx, X3, acqf):
+        models = acqf.model.models
+        need_grad = ctx.needs_input_grad[0]
+        q = X3.shape[-2]
+        means, Ls, saved = [], [], []
+        for mm in models:
+            cache = mm.prediction_cache()
+            ymean, ystd = mm.outcome_stats()
+            pp = kernels.post_partials(cache, X3.detach(), store_R=need_grad)
+            out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
+                                       want_cov=False, want_L=True)
+            kernels._raise_not_psd(out["info"], out["jitter"], "qEHVI posterior root")
+            means.append(out["mean"])
+            Ls.append(out["L"])
+            if need_grad:
+                saved.append((cache, pp, ystd, kernels.w_matrix(cache, pp)))
+        sampler = acqf._ensure_sampler()
+        Z = sampler.base_samples_2d(q * len(models), X3.device)
+        lo, hi = acqf._cells(X3.device)
+        mean, L = torch.stack(means), torch.stack(Ls)
+        acq = kernels.qehvi(mean, L, Z, lo, hi)
+        if need_grad:
+            ctx.saved, ctx.mean, ctx.L, ctx.Z, ctx.cells = saved, mean, L, Z, (lo, hi)
+        return acq
+
+    @staticmethod
+    def backward(ctx, dacq):
+        lo, hi = ctx.cells
+        dmean, dL = kernels.qehvi_backward(ctx.mean, ctx.L, ctx.Z, lo, hi, dacq)
+        dX = None
+        for t, (cache, pp, ystd, W) in enumerate(ctx.saved):
+            dcov = kernels.chol_backward(ctx.L[t], dL[t])
+            dX = kernels.post_backward(cache, pp, W, dmean[t], dcov, ystd, dX=dX)
+        return dX, None
+
+
 class IdentityMCMultiOutputObjective(MCObjective):
     """acquisition/multi_objective/objective.py (identity over outputs)."""
 
@@ -438,24 +596,7 @@ class qExpectedHypervolumeImprovement(MCAcquisitionFunction):
             raise UnsupportedError("qEHVI here runs on a ModelListGP of SingleTaskGPs")
         if not isinstance(self.objective, IdentityMCMultiOutputObjective):
             raise UnsupportedError("only the identity multi-output objective is accelerated")
-        if X3.requires_grad:
-            raise UnsupportedError("qEHVI gradients are not implemented yet on the fused path")
         if q > 12 or d > kernels.DP:
             raise UnsupportedError("fused qEHVI supports q <= 12 and d <= 8")
-        m = len(models)
-        means, Ls = [], []
-        with torch.no_grad():
-            for mm in models:
-                cache = mm.prediction_cache()
-                ymean, ystd = mm.outcome_stats()
-                pp = kernels.post_partials(cache, X3)
-                out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
-                                           want_cov=False, want_L=True)
-                kernels._raise_not_psd(out["info"], out["jitter"], "qEHVI posterior root")
-                means.append(out["mean"])
-                Ls.append(out["L"])
-            sampler = self._ensure_sampler()
-            Z = sampler.base_samples_2d(q * m, X.device)
-            lo, hi = self._cells(X.device)
-            acq = kernels.qehvi(torch.stack(means), torch.stack(Ls), Z, lo, hi)
+        acq = _FusedQEHVI.apply(X3, self)
         return acq.reshape(batch)

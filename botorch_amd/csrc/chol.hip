@@ -13,7 +13,7 @@
 // K*x L^{-T} L^{-1} (y - c) = R beta), so beta is cached beside alpha.
 //
 // Layout in HBM: every n x n cache is stored row-major at the padded order
-// np = roundup(n, 128) with an identity pad, so the 64-wide diagonal blocks of
+// np = roundup(n, 128) with an identity pad, so the 128-wide diagonal blocks of
 // the right-looking factorisation never straddle the edge.
 #include <cstdarg>
 #include <cstring>
@@ -22,10 +22,12 @@
 #include "common.h"
 #include "gemm.h"
 
+int bo_potrf_block128(double* A, int64_t lda, int64_t k0, double* Linv, int64_t ldi, int* info,
+                      hipStream_t st);
+
 namespace {
 
-constexpr int NB = 32;   // diagonal block (one wave factors it, fully unrolled)
-constexpr int NBO = 128; // outer panel: the trailing SYRK runs once per 128 columns
+constexpr int NBO = 128; // panel width = diagonal block of potrf.hip
 
 // K[i][j] = outputscale * k(x_i, x_j) (+ diag_add on i == j), row-major with
 // leading dimension ldk, over a `rows x cols` padded extent (identity pad).
@@ -53,63 +55,6 @@ __global__ __launch_bounds__(256) void covar_matrix_kernel(
     if (i == j) v += diag_add;
   }
   K[i * ldk + j] = v;
-}
-
-// Factor the NB x NB diagonal block at (k0, k0) of the lower-stored matrix A
-// in place (one wave, one row per lane, column j broadcast through LDS) and
-// write its inverse into the same block of Linv.  A non-positive or NaN pivot
-// records info = k0 + j + 1 (1-based order of the failing leading minor, as
-// torch.linalg.cholesky_ex) for the first failing panel.
-// Launched with NB threads (half a wave; the upper lanes stay masked off).
-__global__ __launch_bounds__(NB) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
-                                                         int64_t k0, double* __restrict__ Linv,
-                                                         int64_t ldi, int* __restrict__ info) {
-  __shared__ double col[NB];
-  __shared__ double Ls[NB][NB + 1];
-  const int i = threadIdx.x;
-  double a[NB];
-  const double* row = A + (k0 + i) * lda + k0;
-#pragma unroll
-  for (int l = 0; l < NB; ++l) a[l] = (l <= i) ? row[l] : 0.0;
-
-  int fail = 0;
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const double ajj = __shfl(a[j], j);
-    if (!(ajj > 0.0) && fail == 0) fail = j + 1;
-    const double djj = sqrt(ajj);
-    double lij = a[j] / djj;
-    if (i == j) lij = djj;
-    if (i < j) lij = 0.0;
-    a[j] = lij;
-    col[i] = lij;
-    __syncthreads();
-#pragma unroll
-    for (int l = j + 1; l < NB; ++l) a[l] = fma(-lij, col[l], a[l]);
-    __syncthreads();
-  }
-  if (fail && i == 0) atomicCAS(info, 0, (int)(k0 + fail));
-
-  double* out = A + (k0 + i) * lda + k0;
-#pragma unroll
-  for (int l = 0; l < NB; ++l) {
-    const double v = (l <= i) ? a[l] : 0.0;
-    out[l] = v;
-    Ls[i][l] = v;
-  }
-  __syncthreads();
-  // Column c = lane of X = L^{-1}: forward substitution, L rows broadcast from LDS.
-  const int c = i;
-  double x[NB];
-#pragma unroll
-  for (int r = 0; r < NB; ++r) {
-    double s = (r == c) ? 1.0 : 0.0;
-#pragma unroll
-    for (int k = 0; k < r; ++k) s = fma(-Ls[r][k], x[k], s);
-    x[r] = s / Ls[r][r];
-  }
-#pragma unroll
-  for (int r = 0; r < NB; ++r) Linv[(k0 + r) * ldi + k0 + c] = (r >= c) ? x[r] : 0.0;
 }
 
 __global__ void transpose_kernel(const double* __restrict__ A, double* __restrict__ B,
@@ -168,7 +113,7 @@ const char* bo_last_error(void) { return g_err; }
 
 int bo_version(void) { return BO_ABI_VERSION; }
 
-// 128 = the fused posterior kernel's column tile (post.hip), a multiple of NB.
+// 128 = the fused posterior kernel's column tile (post.hip) = the Cholesky panel.
 int64_t bo_padded_order(int64_t n) { return ceil_div(n, 128) * 128; }
 
 int bo_covar_matrix(int kind, const double* X1, int64_t n1, const double* X2, int64_t n2,
@@ -196,49 +141,37 @@ int bo_gemm_f64(int ta, int tb, int M, int N, int K, double alpha, const double*
 
 int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* info,
                         void* stream) {
-  BO_CHECK_ARG(np > 0 && np % NB == 0, "bo_cholesky_inverse: order %lld not a multiple of %d",
-               (long long)np, NB);
+  BO_CHECK_ARG(np > 0 && np % NBO == 0, "bo_cholesky_inverse: order %lld not a multiple of %d",
+               (long long)np, NBO);
+  BO_CHECK_ARG(((uintptr_t)A & 15) == 0 && ((uintptr_t)Linv & 15) == 0,
+               "bo_cholesky_inverse: buffers must be 16-B aligned");
   hipStream_t st = as_stream(stream);
   BO_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
   BO_HIP(hipMemsetAsync(Linv, 0, sizeof(double) * np * np, st));
-  // Two-level right-looking factorisation.  Inside each 128-column outer
-  // panel: factor a 32 x 32 diagonal block (one wave), solve the rows below
-  // it as a GEMM against the block's inverse, and update only the rest of
-  // the outer panel; then one lower-triangle SYRK (K = 128) updates the
-  // trailing matrix, so the trailing matrix streams through HBM np/128
-  // times instead of np/32.
+  // Right-looking factorisation over 128-column panels: the diagonal block is
+  // factored AND inverted by one workgroup in LDS (potrf.hip); the panel below
+  // is solved as one MFMA GEMM against that inverse (into `work`, then copied
+  // back), and the trailing lower triangle takes one rank-128 SYRK.
   for (int64_t K0 = 0; K0 < np; K0 += NBO) {
-    const int64_t Kend = K0 + NBO < np ? K0 + NBO : np;
-    for (int64_t k0 = K0; k0 < Kend; k0 += NB) {
-      potrf_diag_kernel<<<1, NB, 0, st>>>(A, np, k0, Linv, np, info);
-      BO_LAUNCH_CHECK();
-      const int64_t rem = np - k0 - NB;
-      if (rem <= 0) break;
-      double* P = A + (k0 + NB) * np + k0;       // rem x NB panel
-      const double* Dinv = Linv + k0 * np + k0;  // NB x NB lower
-      // P <- P * Dinv^T  (in place: each workgroup reads its rows fully first)
-      int s = bo_gemm_f64_impl(0, 1, (int)rem, NB, NB, 1.0, P, np, 0, Dinv, np, 0, 0.0, P, np,
-                               0, 1, BO_GEMM_B_UPPER, st);
-      if (s) return s;
-      const int64_t inner = Kend - (k0 + NB);  // columns left in this outer panel
-      if (inner > 0) {
-        double* Ain = A + (k0 + NB) * np + (k0 + NB);
-        s = bo_gemm_f64_impl(0, 1, (int)rem, (int)inner, NB, -1.0, P, np, 0, P, np, 0, 1.0, Ain,
-                             np, 0, 1, BO_GEMM_LOWER_C, st);
-        if (s) return s;
-      }
-    }
-    const int64_t rem = np - Kend;
+    int s = bo_potrf_block128(A, np, K0, Linv, np, info, st);
+    if (s) return s;
+    const int64_t rem = np - K0 - NBO;
     if (rem <= 0) break;
-    double* Pb = A + Kend * np + K0;  // rem x 128
-    double* A22 = A + Kend * np + Kend;
-    int s = bo_gemm_f64_impl(0, 1, (int)rem, (int)rem, (int)(Kend - K0), -1.0, Pb, np, 0, Pb, np,
-                             0, 1.0, A22, np, 0, 1, BO_GEMM_LOWER_C, st);
+    double* P = A + (K0 + NBO) * np + K0;       // rem x 128 panel
+    const double* Dinv = Linv + K0 * np + K0;  // 128 x 128 lower
+    s = bo_gemm_f64_impl(0, 1, (int)rem, NBO, NBO, 1.0, P, np, 0, Dinv, np, 0, 0.0, work, NBO, 0,
+                         1, BO_GEMM_B_UPPER, st);
+    if (s) return s;
+    BO_HIP(hipMemcpy2DAsync(P, sizeof(double) * np, work, sizeof(double) * NBO,
+                            sizeof(double) * NBO, rem, hipMemcpyDeviceToDevice, st));
+    double* A22 = A + (K0 + NBO) * np + (K0 + NBO);
+    s = bo_gemm_f64_impl(0, 1, (int)rem, (int)rem, NBO, -1.0, work, NBO, 0, work, NBO, 0, 1.0, A22,
+                         np, 0, 1, BO_GEMM_LOWER_C, st);
     if (s) return s;
   }
   // Triangular inverse by recursive doubling over the inverted diagonal
   // blocks:  [L11 0; L21 L22]^{-1} = [X11 0; -X22 L21 X11  X22].
-  for (int64_t sz = NB; sz < np; sz *= 2) {
+  for (int64_t sz = NBO; sz < np; sz *= 2) {
     const int64_t stride = 2 * sz;
     const int64_t full = np / stride;          // pairs with a full-size second block
     const int64_t tail_r2 = full * stride + sz;  // second block start of a ragged pair

@@ -4,16 +4,24 @@
 //
 // Used by the blocked Cholesky (TRSM-as-GEMM against the inverted diagonal
 // block, SYRK trailing update restricted to the lower triangle), the
-// recursive-doubling triangular inverse, the MLL gradient's K^{-1} = U U^T
-// and the qNEI cross-covariance.  Triangular operands skip the all-zero
-// k-range of each tile (flags below), which halves the flops of L^{-1}-type
-// products exactly like the reference's dense GEMM would not.
+// recursive-doubling triangular inverse, the MLL gradient's K^{-1} = U U^T,
+// the qNEI cross-covariance and the generic posterior.  Triangular operands
+// skip the all-zero k-range of each tile (flags), which halves the flops of
+// L^{-1}-type products that a dense GEMM would spend on zeros.
 //
-// Tile: BM x BN per 256-thread workgroup (4 waves in a 2 x 2 grid), BK = 16.
-// LDS holds op(A) as As[k][m] and op(B) as Bs[k][n] (rows padded by 16
-// doubles so the two 16-lane halves of each ds_read_b64 lane group fall on
-// opposite bank halves); the next k-tile is prefetched into registers while
-// the current one feeds the MFMAs.
+// Workgroup: 256 threads = 4 waves in a 2 x 2 grid; tile BM x BN, k-step 16.
+// LDS holds op(A) as As[k][m] and op(B) as Bs[k][n] in two stages; each k-step
+// issues the next stage's global loads (16-B vector loads along the
+// contiguous dimension of the operand) before the MFMAs of the current stage
+// and writes them to the other stage after, so there is ONE barrier per
+// k-step and the HBM/L2 latency hides under 64 (128-tile) or 16 (64-tile)
+// MFMAs per wave.  Row pitch BM + 16 doubles puts the four 16-lane groups of
+// an operand read on alternating bank halves.
+//
+// Grid: a 1-D tile list (lower-triangle tiles only under BO_GEMM_LOWER_C),
+// dealt XCD-major: hardware hands consecutive block ids round-robin to the 8
+// XCDs, so block b runs on XCD b % 8; tile t = (b % 8) * per_xcd + b / 8 gives
+// each XCD a contiguous run of tiles that share A row panels in its own L2.
 #include "common.h"
 #include "gemm.h"
 
@@ -22,31 +30,115 @@ namespace {
 constexpr int BK = 16;
 constexpr int PAD = 16;
 
-template <int BM, int BN, bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm_f64_kernel(
+struct TileMap {
+  int tilesN;      // tiles along n
+  int ntiles;      // tiles per batch member
+  int per_xcd;     // ceil(ntiles / 8)
+  int lower;       // enumerate lower-triangle tiles only (BM == BN)
+};
+
+__device__ __forceinline__ void tile_coords(const TileMap& tm, int t, int& ti, int& tj) {
+  if (tm.lower) {
+    // t -> (ti, tj), tj <= ti, row-major over the lower triangle
+    int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((r + 1) * (r + 2) / 2 <= t) ++r;
+    while (r * (r + 1) / 2 > t) --r;
+    ti = r;
+    tj = t - r * (r + 1) / 2;
+  } else {
+    ti = t / tm.tilesN;
+    tj = t - ti * tm.tilesN;
+  }
+}
+
+// Stage loader for one operand.  KCONTIG: element (r, k) at P[r * ld + k]
+// (k contiguous), else at P[k * ld + r] (r contiguous).  R = tile extent along
+// the non-k dimension.  Each thread moves NV pairs of doubles per k-step.
+template <int R, bool KCONTIG>
+struct Stage {
+  static constexpr int NV = R * BK / 512;  // double2 per thread
+  double2 v[NV];
+
+  __device__ __forceinline__ void load(const double* __restrict__ P, int64_t ld, int r0, int k0,
+                                       int Rlim, int Klim, bool vec_ok, int tid) {
+#pragma unroll
+    for (int p = 0; p < NV; ++p) {
+      const int e = tid + p * 256;
+      int r, k;
+      if (KCONTIG) { k = 2 * (e % (BK / 2)); r = e / (BK / 2); }
+      else         { r = 2 * (e % (R / 2));  k = e / (R / 2); }
+      const int gr = r0 + r, gk = k0 + k;
+      double x = 0.0, y = 0.0;
+      if (KCONTIG) {
+        const double* src = P + (int64_t)gr * ld + gk;
+        if (gr < Rlim) {
+          if (vec_ok && gk + 1 < Klim) {
+            const double2 t = *reinterpret_cast<const double2*>(src);
+            x = t.x; y = t.y;
+          } else {
+            if (gk < Klim) x = src[0];
+            if (gk + 1 < Klim) y = src[1];
+          }
+        }
+      } else {
+        const double* src = P + (int64_t)gk * ld + gr;
+        if (gk < Klim) {
+          if (vec_ok && gr + 1 < Rlim) {
+            const double2 t = *reinterpret_cast<const double2*>(src);
+            x = t.x; y = t.y;
+          } else {
+            if (gr < Rlim) x = src[0];
+            if (gr + 1 < Rlim) y = src[1];
+          }
+        }
+      }
+      v[p] = make_double2(x, y);
+    }
+  }
+
+  __device__ __forceinline__ void store(double (*S)[R + PAD], int tid) const {
+#pragma unroll
+    for (int p = 0; p < NV; ++p) {
+      const int e = tid + p * 256;
+      if (KCONTIG) {
+        const int k = 2 * (e % (BK / 2)), r = e / (BK / 2);
+        S[k][r] = v[p].x;
+        S[k + 1][r] = v[p].y;
+      } else {
+        const int r = 2 * (e % (R / 2)), k = e / (R / 2);
+        *reinterpret_cast<double2*>(&S[k][r]) = v[p];
+      }
+    }
+  }
+};
+
+template <int BM, int BN, bool TA, bool TB, int MINB>
+__global__ __launch_bounds__(256, MINB) void gemm_f64_kernel(
     int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
     int64_t sA, const double* __restrict__ B, int64_t ldb, int64_t sB, double beta,
-    double* __restrict__ C, int64_t ldc, int64_t sC, int flags) {
-  constexpr int TM = BM / 32;  // MFMA tiles per wave along m (2x2 waves)
+    double* __restrict__ C, int64_t ldc, int64_t sC, int flags, TileMap tm, int vecA,
+    int vecB) {
+  constexpr int TM = BM / 32;  // MFMA tiles per wave along m (2 x 2 waves)
   constexpr int TN = BN / 32;
-  constexpr int LA = BM * BK / 256;  // A elements staged per thread
-  constexpr int LB = BN * BK / 256;
-  __shared__ double As[BK][BM + PAD];
-  __shared__ double Bs[BK][BN + PAD];
+  __shared__ __attribute__((aligned(16))) double As[2][BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) double Bs[2][BK][BN + PAD];
+
+  const int b = blockIdx.x;
+  const int t = (b & 7) * tm.per_xcd + (b >> 3);
+  if (t >= tm.ntiles) return;
+  int ti, tj;
+  tile_coords(tm, t, ti, tj);
+  const int m0 = ti * BM, n0 = tj * BN;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = (wave >> 1) * (BM / 2);
   const int wn = (wave & 1) * (BN / 2);
-  const int m0 = blockIdx.y * BM;
-  const int n0 = blockIdx.x * BN;
-  const int64_t bz = blockIdx.z;
+  const int64_t bz = blockIdx.y;
   A += bz * sA;
   B += bz * sB;
   C += bz * sC;
-
-  if ((flags & BO_GEMM_LOWER_C) && n0 > m0 + BM - 1) return;  // tile strictly above diagonal
 
   // k-range restricted by triangular operands (zero regions are skipped).
   int kbeg = 0, kend = K;
@@ -55,6 +147,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(
   if (flags & BO_GEMM_A_UPPER) kbeg = max(kbeg, m0);       // op(A)[m][k] = 0 for k < m
   if (flags & BO_GEMM_B_LOWER) kbeg = max(kbeg, n0);       // op(B)[k][n] = 0 for k < n
   kbeg = (kbeg / BK) * BK;
+  const int nsteps = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
   v4d acc[TM][TN];
 #pragma unroll
@@ -62,105 +155,114 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = v4d_zero();
 
-  double ra[LA], rb[LB];
+  // op(A) = A (row m, col k) stored [M][K] -> k contiguous unless TA.
+  Stage<BM, !TA> sa;
+  // op(B)[k][n]: stored [K][N] (n contiguous) unless TB ([N][K], k contiguous).
+  Stage<BN, TB> sb;
 
-  auto load_tiles = [&](int k0) {
-#pragma unroll
-    for (int p = 0; p < LA; ++p) {
-      int e = tid + p * 256;
-      int m, k;
-      if (TA) { m = e % BM; k = e / BM; }  // A stored [K][M]: m contiguous
-      else    { k = e % BK; m = e / BK; }  // A stored [M][K]: k contiguous
-      int gm = m0 + m, gk = k0 + k;
-      double v = 0.0;
-      if (gm < M && gk < K) v = TA ? A[(int64_t)gk * lda + gm] : A[(int64_t)gm * lda + gk];
-      ra[p] = v;
+  if (nsteps > 0) {
+    sa.load(A, lda, m0, kbeg, M, K, vecA, tid);
+    sb.load(B, ldb, n0, kbeg, N, K, vecB, tid);
+    sa.store(As[0], tid);
+    sb.store(Bs[0], tid);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const bool more = s + 1 < nsteps;
+    if (more) {
+      const int kn = kbeg + (s + 1) * BK;
+      sa.load(A, lda, m0, kn, M, K, vecA, tid);
+      sb.load(B, ldb, n0, kn, N, K, vecB, tid);
     }
-#pragma unroll
-    for (int p = 0; p < LB; ++p) {
-      int e = tid + p * 256;
-      int n, k;
-      if (TB) { k = e % BK; n = e / BK; }  // B stored [N][K]: k contiguous
-      else    { n = e % BN; k = e / BN; }  // B stored [K][N]: n contiguous
-      int gn = n0 + n, gk = k0 + k;
-      double v = 0.0;
-      if (gn < N && gk < K) v = TB ? B[(int64_t)gn * ldb + gk] : B[(int64_t)gk * ldb + gn];
-      rb[p] = v;
-    }
-  };
-  auto store_tiles = [&]() {
-#pragma unroll
-    for (int p = 0; p < LA; ++p) {
-      int e = tid + p * 256;
-      int m, k;
-      if (TA) { m = e % BM; k = e / BM; }
-      else    { k = e % BK; m = e / BK; }
-      As[k][m] = ra[p];
-    }
-#pragma unroll
-    for (int p = 0; p < LB; ++p) {
-      int e = tid + p * 256;
-      int n, k;
-      if (TB) { k = e % BK; n = e / BK; }
-      else    { n = e % BN; k = e / BN; }
-      Bs[k][n] = rb[p];
-    }
-  };
-
-  if (kbeg < kend) load_tiles(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();
-    store_tiles();
-    __syncthreads();
-    if (k0 + BK < kend) load_tiles(k0 + BK);
 #pragma unroll
     for (int ks = 0; ks < BK / 4; ++ks) {
       const int kr = ks * 4 + (lane >> 4);
-      double a[TM], b[TN];
+      double a[TM], bb[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[kr][wm + i * 16 + (lane & 15)];
+      for (int i = 0; i < TM; ++i) a[i] = As[cur][kr][wm + i * 16 + (lane & 15)];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = Bs[kr][wn + j * 16 + (lane & 15)];
+      for (int j = 0; j < TN; ++j) bb[j] = Bs[cur][kr][wn + j * 16 + (lane & 15)];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f64(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f64(a[i], bb[j], acc[i][j]);
     }
+    if (more) {
+      sa.store(As[cur ^ 1], tid);
+      sb.store(Bs[cur ^ 1], tid);
+    }
+    __syncthreads();
   }
 
-  // Epilogue.
+  // Epilogue.  The beta * C reads of one 16-row strip are all issued before
+  // any of its stores (a load after a store to the same array cannot be
+  // hoisted by the compiler, which would otherwise serialise one HBM round
+  // trip per element).
   const bool lower = flags & BO_GEMM_LOWER_C;
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < TM; ++i) {
+    double cv[TN][4];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int gm = m0 + wm + i * 16 + mfma_row(lane, r);
-        int gn = n0 + wn + j * 16 + mfma_col(lane);
-        if (gm < M && gn < N && (!lower || gm >= gn)) {
-          double* c = C + (int64_t)gm * ldc + gn;
-          double v = alpha * acc[i][j][r];
-          if (beta != 0.0) v += beta * (*c);
-          *c = v;
-        }
+        const int gm = m0 + wm + i * 16 + mfma_row(lane, r);
+        const int gn = n0 + wn + j * 16 + mfma_col(lane);
+        const bool ok = gm < M && gn < N && (!lower || gm >= gn);
+        cv[j][r] = (ok && beta != 0.0) ? C[(int64_t)gm * ldc + gn] : 0.0;
       }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gm = m0 + wm + i * 16 + mfma_row(lane, r);
+        const int gn = n0 + wn + j * 16 + mfma_col(lane);
+        if (gm < M && gn < N && (!lower || gm >= gn))
+          C[(int64_t)gm * ldc + gn] = fma(beta, cv[j][r], alpha * acc[i][j][r]);
+      }
+  }
 }
 
-template <int BM, int BN>
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+template <int BM, int BN, int MINB>
 int launch_gemm(bool ta, bool tb, int M, int N, int K, double alpha, const double* A,
                 int64_t lda, int64_t sA, const double* B, int64_t ldb, int64_t sB,
                 double beta, double* C, int64_t ldc, int64_t sC, int batch, int flags,
                 hipStream_t st) {
-  dim3 grid((unsigned)ceil_div(N, BN), (unsigned)ceil_div(M, BM), (unsigned)batch);
-  if (ta && tb)
-    gemm_f64_kernel<BM, BN, true, true><<<grid, 256, 0, st>>>(M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, flags);
-  else if (ta)
-    gemm_f64_kernel<BM, BN, true, false><<<grid, 256, 0, st>>>(M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, flags);
-  else if (tb)
-    gemm_f64_kernel<BM, BN, false, true><<<grid, 256, 0, st>>>(M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, flags);
-  else
-    gemm_f64_kernel<BM, BN, false, false><<<grid, 256, 0, st>>>(M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, flags);
+  TileMap tm;
+  const int tilesM = (int)ceil_div(M, BM);
+  tm.tilesN = (int)ceil_div(N, BN);
+  tm.lower = (BM == BN) && (flags & BO_GEMM_LOWER_C) ? 1 : 0;
+  if (tm.lower) {
+    // tiles with ti >= tj cover the lower triangle (N beyond M never needed)
+    const int tn = tm.tilesN < tilesM ? tm.tilesN : tilesM;
+    // rows ti < tilesM, cols tj <= min(ti, tn - 1): count = full triangle of tn
+    // rows plus (tilesM - tn) full rows of tn tiles.
+    if (tn == tilesM) {
+      tm.ntiles = tilesM * (tilesM + 1) / 2;
+    } else {
+      tm.lower = 0;  // ragged (N < M) lower request: plain grid, masked epilogue
+      tm.ntiles = tilesM * tm.tilesN;
+    }
+  } else {
+    tm.ntiles = tilesM * tm.tilesN;
+  }
+  tm.per_xcd = (int)ceil_div(tm.ntiles, 8);
+  // vector loads need 16-B aligned rows: base aligned, even leading dim and
+  // even batch stride
+  const int vecA = aligned16(A) && lda % 2 == 0 && (batch == 1 || sA % 2 == 0);
+  const int vecB = aligned16(B) && ldb % 2 == 0 && (batch == 1 || sB % 2 == 0);
+  dim3 grid((unsigned)(8 * tm.per_xcd), (unsigned)batch);
+#define BO_GEMM_GO(TA_, TB_)                                                                 \
+  gemm_f64_kernel<BM, BN, TA_, TB_, MINB><<<grid, 256, 0, st>>>(                            \
+      M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, flags, tm, vecA, vecB)
+  if (ta && tb) BO_GEMM_GO(true, true);
+  else if (ta) BO_GEMM_GO(true, false);
+  else if (tb) BO_GEMM_GO(false, true);
+  else BO_GEMM_GO(false, false);
+#undef BO_GEMM_GO
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
@@ -172,14 +274,16 @@ int bo_gemm_f64_impl(int ta, int tb, int M, int N, int K, double alpha, const do
                      double beta, double* C, int64_t ldc, int64_t sC, int batch, int flags,
                      hipStream_t st) {
   if (M <= 0 || N <= 0 || batch <= 0) return BO_OK;
-  if (K <= 0) {
-    // C = beta * C (alpha term is empty).
-    return launch_gemm<64, 64>(ta, tb, M, N, 0, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, flags, st);
-  }
-  // Large problems: 128 x 128 tiles (16 MFMA accumulators per wave); small
-  // ones keep 64 x 64 so the grid still covers the 256 CUs.
-  int64_t tiles128 = ceil_div(M, 128) * ceil_div(N, 128) * (int64_t)batch;
-  if (tiles128 >= 256)
-    return launch_gemm<128, 128>(ta, tb, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, flags, st);
-  return launch_gemm<64, 64>(ta, tb, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, flags, st);
+  if (K < 0) K = 0;  // C = beta * C (the alpha term is empty)
+  // Large problems: 128 x 128 tiles (16 MFMA accumulators per wave); smaller
+  // ones keep 64 x 64 so the grid still covers the 256 CUs.  Triangular
+  // operands (long, unbalanced k-ranges) also use 64 x 64 so the heaviest tile
+  // does not set the duration.
+  const int64_t tiles128 = ceil_div(M, 128) * ceil_div(N, 128) * (int64_t)batch;
+  const bool tri = flags & (BO_GEMM_A_UPPER | BO_GEMM_B_LOWER | BO_GEMM_A_LOWER | BO_GEMM_B_UPPER);
+  if (tiles128 >= 512 && !(tri && K > 1024))
+    return launch_gemm<128, 128, 1>(ta, tb, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc,
+                                    sC, batch, flags, st);
+  return launch_gemm<64, 64, 2>(ta, tb, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
+                                batch, flags, st);
 }

@@ -36,11 +36,82 @@ __device__ __forceinline__ double dkernel_factor(double d2, double outputscale) 
   }
 }
 
+// qNEI (cached root): the samples carry the baseline term F[s][row] =
+// (Z_base T)[s][row] (row = b * Qp + a); its cotangent dF (same layout) is the
+// winner weight, from which the host forms dT = Z_base^T dF.
+// torch's linalg.cholesky backward (Murray 2016) for one q x q factor held in
+// LDS: gA = L^{-T} Phi(L^T dL) L^{-1}, Phi = lower half with the diagonal
+// halved, symmetrised.  Writes the q x q result to out (row-major).
+__device__ __forceinline__ void chol_backward_lds(int q, double (*L)[QMAX + 1],
+                                                  double (*dL)[QMAX + 1], double (*Li)[QMAX + 1],
+                                                  double (*Pm)[QMAX + 1], double (*Tm)[QMAX + 1],
+                                                  double* __restrict__ out, int tid) {
+  // L^{-1} by forward substitution, one column per thread.
+  if (tid < q) {
+    const int c = tid;
+    for (int r = 0; r < q; ++r) {
+      double s = (r == c) ? 1.0 : 0.0;
+      for (int k = c; k < r; ++k) s = fma(-L[r][k], Li[k][c], s);
+      Li[r][c] = (r >= c) ? s / L[r][r] : 0.0;
+    }
+  }
+  __syncthreads();
+  // X = tril(L^T dL);  P = 0.5 (X + tril(X, -1)^T)   (torch cholesky_backward)
+  if (tid < q * q) {
+    const int i = tid / q, j = tid % q;
+    const int lo = i > j ? i : j;
+    double x = 0.0;
+    for (int k = lo; k < q; ++k) x = fma(L[k][i], dL[k][j], x);  // (L^T dL)[i][j]
+    if (i >= j) Tm[i][j] = x;
+  }
+  __syncthreads();
+  if (tid < q * q) {
+    const int i = tid / q, j = tid % q;
+    Pm[i][j] = 0.5 * ((i >= j) ? Tm[i][j] : Tm[j][i]);
+  }
+  __syncthreads();
+  // gA = L^{-T} P L^{-1}:  T = P L^{-1}, then gA = L^{-T} T
+  if (tid < q * q) {
+    const int i = tid / q, j = tid % q;
+    double x = 0.0;
+    for (int k = j; k < q; ++k) x = fma(Pm[i][k], Li[k][j], x);
+    Tm[i][j] = x;
+  }
+  __syncthreads();
+  if (tid < q * q) {
+    const int i = tid / q, j = tid % q;
+    double x = 0.0;
+    for (int k = i; k < q; ++k) x = fma(Li[k][i], Tm[k][j], x);
+    out[i * q + j] = x;
+  }
+}
+
+// Standalone batched Cholesky backward: dL (B x q x q, lower) -> dA.
+__global__ __launch_bounds__(THREADS) void chol_backward_kernel(int q, const double* __restrict__ Lg,
+                                                                const double* __restrict__ dLg,
+                                                                double* __restrict__ dA) {
+  __shared__ double L[QMAX][QMAX + 1];
+  __shared__ double dL[QMAX][QMAX + 1];
+  __shared__ double Li[QMAX][QMAX + 1];
+  __shared__ double Pm[QMAX][QMAX + 1];
+  __shared__ double Tm[QMAX][QMAX + 1];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (tid < q * q) {
+    const int a = tid / q, c = tid % q;
+    L[a][c] = Lg[((int64_t)b * q + a) * q + c];
+    dL[a][c] = (c <= a) ? dLg[((int64_t)b * q + a) * q + c] : 0.0;
+  }
+  __syncthreads();
+  chol_backward_lds(q, L, dL, Li, Pm, Tm, dA + (int64_t)b * q * q, tid);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
     int q, const double* __restrict__ mean, const double* __restrict__ Lq,
     const double* __restrict__ Z, int S, double best_f, const double* __restrict__ best_f_s,
-    const double* __restrict__ dacq, double* __restrict__ dmean, double* __restrict__ dcov) {
+    const double* __restrict__ dacq, double* __restrict__ dmean, double* __restrict__ dcov,
+    const double* __restrict__ F, int64_t ldF, int Qp, double* __restrict__ dF) {
   __shared__ double L[QMAX][QMAX + 1];
   __shared__ double Li[QMAX][QMAX + 1];   // L^{-1}
   __shared__ double dL[QMAX][QMAX + 1];
@@ -75,10 +146,12 @@ __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
       const double bf = (MODE == MODE_QNEI) ? best_f_s[s0 + s] : best_f;
       double v[QMAX];
       double m = 0.0;
+      const double* Fs = (MODE == MODE_QNEI) ? F + (int64_t)(s0 + s) * ldF + (int64_t)b * Qp : nullptr;
 #pragma unroll
       for (int a = 0; a < QMAX; ++a) {
         if (a < q) {
           double f = mu[a];
+          if (MODE == MODE_QNEI) f += Fs[a];
           for (int j = 0; j <= a; ++j) f = fma(L[a][j], z[j], f);
           v[a] = f - bf;
           m = fmax(m, fmax(v[a], 0.0));
@@ -96,6 +169,11 @@ __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
       }
       win[s] = (unsigned short)mask;
       wgt[s] = cnt ? g / (double)cnt : 0.0;
+      if (MODE == MODE_QNEI) {
+        double* dFs = dF + (int64_t)(s0 + s) * ldF + (int64_t)b * Qp;
+        const double w = wgt[s];
+        for (int a = 0; a < q; ++a) dFs[a] = (mask >> a & 1u) ? w : 0.0;
+      }
     }
     __syncthreads();
     // Pass 2: deterministic accumulation per (a, j).
@@ -114,45 +192,7 @@ __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
     dL[ta][tj] = (tj <= ta) ? dl_acc : 0.0;
     if (tj == 0) dmean[(int64_t)b * q + ta] = dmu_acc;
   }
-  // L^{-1} by forward substitution, one column per thread.
-  if (tid < q) {
-    const int c = tid;
-    for (int r = 0; r < q; ++r) {
-      double s = (r == c) ? 1.0 : 0.0;
-      for (int k = c; k < r; ++k) s = fma(-L[r][k], Li[k][c], s);
-      Li[r][c] = (r >= c) ? s / L[r][r] : 0.0;
-    }
-  }
-  __syncthreads();
-  // X = tril(L^T dL);  P = 0.5 (X + tril(X, -1)^T)   (torch cholesky_backward)
-  if (tid < q * q) {
-    const int i = tid / q, j = tid % q;
-    const int lo = i > j ? i : j;
-    double x = 0.0;
-    for (int k = lo; k < q; ++k) x = fma(L[k][i], dL[k][j], x);  // (L^T dL)[i][j]
-    // store X lower-only at [max][min]
-    if (i >= j) Tm[i][j] = x;
-  }
-  __syncthreads();
-  if (tid < q * q) {
-    const int i = tid / q, j = tid % q;
-    Pm[i][j] = 0.5 * ((i >= j) ? Tm[i][j] : Tm[j][i]);
-  }
-  __syncthreads();
-  // gA = L^{-T} P L^{-1}:  T = P L^{-1}, then gA = L^{-T} T
-  if (tid < q * q) {
-    const int i = tid / q, j = tid % q;
-    double x = 0.0;
-    for (int k = j; k < q; ++k) x = fma(Pm[i][k], Li[k][j], x);
-    Tm[i][j] = x;
-  }
-  __syncthreads();
-  if (tid < q * q) {
-    const int i = tid / q, j = tid % q;
-    double x = 0.0;
-    for (int k = i; k < q; ++k) x = fma(Li[k][i], Tm[k][j], x);
-    dcov[((int64_t)b * q + i) * q + j] = x;
-  }
+  chol_backward_lds(q, L, dL, Li, Pm, Tm, dcov + (int64_t)b * q * q, tid);
 }
 
 // dX for one t-batch per workgroup.  TPA threads per test row a, striding k.
@@ -161,7 +201,8 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
     int q, int Qp, const double* __restrict__ Xq, const double* __restrict__ Xt, int n,
     const double* __restrict__ W, int64_t ldw, const double* __restrict__ alpha,
     const double* __restrict__ dmean, const double* __restrict__ dcov,
-    const double* __restrict__ ls, double outputscale, double ystd, int d,
+    const double* __restrict__ E, int64_t lde,
+    const double* __restrict__ ls, double outputscale, double ystd, int d, int accumulate,
     double* __restrict__ dX) {
   __shared__ double G[QMAX][QMAX + 1];
   __shared__ double dmu[QMAX];
@@ -175,9 +216,9 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
   if (tid < q * q) {
     const int a = tid / q, c = tid % q;
     const double* dc = dcov + (int64_t)b * q * q;
-    G[a][c] = s2 * (dc[a * q + c] + dc[c * q + a]);
+    G[a][c] = dcov ? s2 * (dc[a * q + c] + dc[c * q + a]) : 0.0;
   }
-  if (tid < q) dmu[tid] = ystd * dmean[(int64_t)b * q + tid];
+  if (tid < q) dmu[tid] = dmean ? ystd * dmean[(int64_t)b * q + tid] : 0.0;
   if (tid < q * DP) xs[tid / DP][tid % DP] = Xq[(int64_t)(row0 + tid / DP) * DP + tid % DP];
   __syncthreads();
 
@@ -192,9 +233,12 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
 #pragma unroll
     for (int t = 0; t < ND; ++t) xa[t] = xs[a][t];
     const double dma = dmu[a];
+    const double* Ea = E ? E + (int64_t)(row0 + a) * lde : nullptr;
     for (int k = kk; k < n; k += TPA) {
-      double D = dma * alpha[k];
-      for (int j = 0; j < q; ++j) D = fma(-G[a][j], W[(int64_t)(row0 + j) * ldw + k], D);
+      double D = alpha ? dma * alpha[k] : 0.0;
+      if (W)
+        for (int j = 0; j < q; ++j) D = fma(-G[a][j], W[(int64_t)(row0 + j) * ldw + k], D);
+      if (Ea) D += Ea[k];
       const double* xt = Xt + (int64_t)k * DP;
       double diff[ND];
       double d2 = 0.0;
@@ -209,7 +253,7 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
     }
     // K** terms: Sigma*[a][c] = K**(a, c) - ..., d K** = d Sigma* (c != a; the
     // diagonal is the constant outputscale).
-    if (kk == 0) {
+    if (kk == 0 && dcov) {
       for (int c = 0; c < q; ++c) {
         if (c == a) continue;
         double diff[ND];
@@ -232,23 +276,112 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
     const int ra = tid / d, t = tid % d;
     double s = 0.0;
     for (int u = 0; u < TPA; ++u) s += red[ra * TPA + u][t];
-    dX[((int64_t)b * q + ra) * d + t] = s / ls[t];
+    double* o = dX + ((int64_t)b * q + ra) * d + t;
+    *o = accumulate ? *o + s / ls[t] : s / ls[t];
+  }
+}
+
+// Generic-d kernel-matrix gradient: dX[i][t] (+)= sum_k dK[i][k] d k(x_i, y_k) / d x_it
+// for inputs in the ORIGINAL scale (lengthscale ls per dim).  group > 0: row i
+// only sees the points of its own group (rows i / group * group ..; dK row
+// holds `group` entries) -- the K** term of a q-batch.  One workgroup per row.
+template <int KIND>
+__global__ __launch_bounds__(THREADS) void kernel_grad_kernel(
+    const double* __restrict__ X, const double* __restrict__ Y, int n, int d,
+    const double* __restrict__ ls, double outputscale, const double* __restrict__ dK,
+    int64_t ldk, int group, int accumulate, double* __restrict__ dX) {
+  constexpr int CH = 1024;
+  __shared__ double xi[128];
+  __shared__ double il2[128];
+  __shared__ double fk[CH];
+  __shared__ double part[THREADS];
+  const int64_t i = blockIdx.x;
+  const int tid = threadIdx.x;
+  const double* Yb = group > 0 ? Y + (i / group) * group * (int64_t)d : Y;
+  const int npts = group > 0 ? group : n;
+  for (int t = tid; t < d; t += THREADS) {
+    xi[t] = X[i * d + t];
+    il2[t] = 1.0 / (ls[t] * ls[t]);
+  }
+  __syncthreads();
+  // thread layout for the second phase: TT threads per dimension slice
+  double acc_t = 0.0;
+  const int t_own = tid % 128;  // dimension handled (d <= 128)
+  const int kslice = tid / 128;  // 2 slices of points
+  for (int k0 = 0; k0 < npts; k0 += CH) {
+    const int nk = min(CH, npts - k0);
+    for (int kk = tid; kk < nk; kk += THREADS) {
+      const double* y = Yb + (int64_t)(k0 + kk) * d;
+      double d2 = 0.0;
+      for (int t = 0; t < d; ++t) {
+        const double df = xi[t] - y[t];
+        d2 = fma(df * df, il2[t], d2);
+      }
+      const double D = dK[i * ldk + k0 + kk];
+      fk[kk] = (group > 0 && (k0 + kk) == (int)(i % group)) ? 0.0
+                                                            : D * dkernel_factor<KIND>(d2, outputscale);
+    }
+    __syncthreads();
+    if (t_own < d) {
+      for (int kk = kslice; kk < nk; kk += THREADS / 128) {
+        const double* y = Yb + (int64_t)(k0 + kk) * d;
+        acc_t = fma(fk[kk], xi[t_own] - y[t_own], acc_t);
+      }
+    }
+    __syncthreads();
+  }
+  part[tid] = acc_t;
+  __syncthreads();
+  if (tid < d) {
+    const double v = (part[tid] + part[tid + 128]) * il2[tid];
+    dX[i * d + tid] = accumulate ? dX[i * d + tid] + v : v;
   }
 }
 
 }  // namespace
 
+extern "C" int bo_kernel_grad(int kind, const double* X, int64_t rows, const double* Y, int64_t n,
+                              int d, const double* lengthscale, double outputscale,
+                              const double* dK, int64_t ldk, int group, int accumulate,
+                              double* dX, void* stream) {
+  BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bo_kernel_grad: bad kind %d", kind);
+  BO_CHECK_ARG(d >= 1 && d <= 128, "bo_kernel_grad: 1 <= d <= 128 (got %d)", d);
+  BO_CHECK_ARG(group == 0 || rows % group == 0, "bo_kernel_grad: rows not a multiple of group");
+  if (rows == 0) return BO_OK;
+  hipStream_t st = as_stream(stream);
+  if (kind == BO_RBF)
+    kernel_grad_kernel<BO_RBF><<<(unsigned)rows, THREADS, 0, st>>>(X, Y, (int)n, d, lengthscale, outputscale, dK, ldk, group, accumulate, dX);
+  else
+    kernel_grad_kernel<BO_MATERN52><<<(unsigned)rows, THREADS, 0, st>>>(X, Y, (int)n, d, lengthscale, outputscale, dK, ldk, group, accumulate, dX);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
 extern "C" int bo_qmc_backward(int mode, int B, int q, const double* mean, const double* Lq,
                                const double* Z, int S, double best_f, const double* best_f_s,
-                               const double* dacq, double* dmean, double* dcov, void* stream) {
+                               const double* F, int64_t ldF, const double* dacq, double* dmean,
+                               double* dcov, double* dF, void* stream) {
   BO_CHECK_ARG(q >= 1 && q <= QMAX, "bo_qmc_backward: q=%d out of range", q);
   BO_CHECK_ARG(mode == MODE_QEI || mode == MODE_QNEI, "bo_qmc_backward: bad mode %d", mode);
+  BO_CHECK_ARG(mode == MODE_QEI || (best_f_s && F && dF), "bo_qmc_backward: qNEI needs best_f_s, F, dF");
   if (B == 0) return BO_OK;
+  int Qp = 1;
+  while (Qp < q) Qp *= 2;
+  BO_CHECK_ARG(mode == MODE_QEI || ldF >= (int64_t)B * Qp, "bo_qmc_backward: ldF too small");
   hipStream_t st = as_stream(stream);
   if (mode == MODE_QEI)
-    qmc_backward_kernel<MODE_QEI><<<B, THREADS, 0, st>>>(q, mean, Lq, Z, S, best_f, best_f_s, dacq, dmean, dcov);
+    qmc_backward_kernel<MODE_QEI><<<B, THREADS, 0, st>>>(q, mean, Lq, Z, S, best_f, best_f_s, dacq, dmean, dcov, nullptr, 0, Qp, nullptr);
   else
-    qmc_backward_kernel<MODE_QNEI><<<B, THREADS, 0, st>>>(q, mean, Lq, Z, S, best_f, best_f_s, dacq, dmean, dcov);
+    qmc_backward_kernel<MODE_QNEI><<<B, THREADS, 0, st>>>(q, mean, Lq, Z, S, best_f, best_f_s, dacq, dmean, dcov, F, ldF, Qp, dF);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+extern "C" int bo_chol_backward(int B, int q, const double* L, const double* dL, double* dA,
+                                void* stream) {
+  BO_CHECK_ARG(q >= 1 && q <= QMAX, "bo_chol_backward: q=%d out of range", q);
+  if (B == 0) return BO_OK;
+  chol_backward_kernel<<<B, THREADS, 0, as_stream(stream)>>>(q, L, dL, dA);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
@@ -256,8 +389,9 @@ extern "C" int bo_qmc_backward(int mode, int B, int q, const double* mean, const
 extern "C" int bo_post_backward(int kind, int B, int q, int d, const double* Xq,
                                 const double* Xt_scaled, int64_t n, const double* W, int64_t ldw,
                                 const double* alpha, const double* dmean, const double* dcov,
-                                const double* lengthscale, double outputscale, double ystd,
-                                double* dX, void* stream) {
+                                const double* E, int64_t lde, const double* lengthscale,
+                                double outputscale, double ystd, int accumulate, double* dX,
+                                void* stream) {
   BO_CHECK_ARG(q >= 1 && q <= QMAX && d >= 1 && d <= DP, "bo_post_backward: bad q/d");
   if (B == 0) return BO_OK;
   int Qp = 1;
@@ -265,8 +399,9 @@ extern "C" int bo_post_backward(int kind, int B, int q, int d, const double* Xq,
   hipStream_t st = as_stream(stream);
 #define BO_PB(KIND, ND)                                                                      \
   post_backward_kernel<KIND, ND><<<B, THREADS, 0, st>>>(q, Qp, Xq, Xt_scaled, (int)n, W, ldw, \
-                                                        alpha, dmean, dcov, lengthscale,      \
-                                                        outputscale, ystd, d, dX)
+                                                        alpha, dmean, dcov, E, lde,           \
+                                                        lengthscale, outputscale, ystd, d,    \
+                                                        accumulate, dX)
   if (kind == BO_RBF) {
     if (d == 6) BO_PB(BO_RBF, 6); else BO_PB(BO_RBF, 8);
   } else {

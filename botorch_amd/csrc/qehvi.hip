@@ -102,6 +102,160 @@ __global__ __launch_bounds__(THREADS) void qehvi_kernel(
   }
 }
 
+// Backward of qehvi_kernel (gen_candidates_scipy's autograd.grad through
+// _compute_qehvi, monte_carlo.py:230-317): for every (sample, cell, subset T)
+// term sign * prod_t mn_t, the derivative w.r.t. f[s][p*][t] is
+// sign * prod_{t' != t} mn_t' where p* = argmin_{p in T} f_pt and the min is
+// not the cell's upper bound (min(u, .) passes no gradient to f there; a
+// clamped-at-lower term is zero with zero gradient).  df accumulates in LDS
+// (ds_add_f64), then dmean_t[p] = sum_s df[s][p][t] and
+// dL_t[p][j] = sum_s df[s][p][t] Z[s][j m + t] (j <= p), scaled by dacq / S.
+template <int M>
+__global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
+    int B, int q, const double* __restrict__ mean, const double* __restrict__ L,
+    const double* __restrict__ Z, int S, const double* __restrict__ lo,
+    const double* __restrict__ hi, int K, const double* __restrict__ dacq,
+    double* __restrict__ dmean, double* __restrict__ dL) {
+  constexpr int CH = LDS_SAMPLES_DOUBLES / 2;
+  __shared__ double f[CH];
+  __shared__ double df[CH];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int per_sample = q * M;
+  const int chunk = CH / per_sample;
+  const double g = dacq[b] / (double)S;
+  // entries owned by this thread: (t, p, j) with j <= p (j == p + 1 -> dmean)
+  const int nent = M * q * (q + 3) / 2;
+  double accv[2] = {0.0, 0.0};
+  for (int s0 = 0; s0 < S; s0 += chunk) {
+    const int ns = min(chunk, S - s0);
+    __syncthreads();
+    for (int e = tid; e < ns * per_sample; e += THREADS) {
+      const int s = e / per_sample;
+      const int p = (e / M) % q;
+      const int t = e % M;
+      const double* Lt = L + (((int64_t)t * B + b) * q + p) * q;
+      const double* zs = Z + (int64_t)(s0 + s) * q * M;
+      double v = mean[((int64_t)t * B + b) * q + p];
+      for (int j = 0; j <= p; ++j) v = fma(Lt[j], zs[j * M + t], v);
+      f[e] = v;
+      df[e] = 0.0;
+    }
+    __syncthreads();
+    for (int e = tid; e < ns * K; e += THREADS) {
+      const int s = e / K;
+      const int k = e % K;
+      double l[M], u[M];
+#pragma unroll
+      for (int t = 0; t < M; ++t) {
+        l[t] = lo[k * M + t];
+        u[t] = hi[k * M + t];
+      }
+      const double* fs = f + s * per_sample;
+      double a[QMAX][M];
+      unsigned act = 0;
+#pragma unroll
+      for (int p = 0; p < QMAX; ++p) {
+        bool ok = p < q;
+#pragma unroll
+        for (int t = 0; t < M; ++t) {
+          const double v = p < q ? fmin(u[t], fs[p * M + t]) - l[t] : 0.0;
+          a[p][t] = v;
+          ok = ok && (v > 0.0);
+        }
+        if (ok) act |= 1u << p;
+      }
+      double gacc[QMAX][M];
+#pragma unroll
+      for (int p = 0; p < QMAX; ++p)
+#pragma unroll
+        for (int t = 0; t < M; ++t) gacc[p][t] = 0.0;
+      for (unsigned sub = act; sub; sub = (sub - 1) & act) {
+        double mn[M];
+        int am[M];
+#pragma unroll
+        for (int t = 0; t < M; ++t) {
+          mn[t] = INFINITY;
+          am[t] = 0;
+        }
+#pragma unroll
+        for (int p = 0; p < QMAX; ++p)
+          if (sub & (1u << p))
+#pragma unroll
+            for (int t = 0; t < M; ++t)
+              if (a[p][t] < mn[t]) {
+                mn[t] = a[p][t];
+                am[t] = p;
+              }
+        const double sg = (__popc(sub) & 1) ? 1.0 : -1.0;
+#pragma unroll
+        for (int t = 0; t < M; ++t) {
+          double o = sg;
+#pragma unroll
+          for (int t2 = 0; t2 < M; ++t2)
+            if (t2 != t) o *= mn[t2];
+          // the min reaches f only where f < u (else the upper bound is active)
+#pragma unroll
+          for (int p = 0; p < QMAX; ++p)
+            if (p == am[t] && fs[p * M + t] < u[t]) gacc[p][t] += o;
+        }
+      }
+      if (act) {
+#pragma unroll
+        for (int p = 0; p < QMAX; ++p)
+#pragma unroll
+          for (int t = 0; t < M; ++t)
+            if (p < q && gacc[p][t] != 0.0) atomicAdd(&df[s * per_sample + p * M + t], gacc[p][t]);
+      }
+    }
+    __syncthreads();
+    for (int w = 0; w < 2; ++w) {
+      const int ent = tid + w * THREADS;
+      if (ent >= nent) continue;
+      const int per_t = q * (q + 3) / 2;
+      const int t = ent / per_t;
+      int r = ent % per_t;
+      int p = 0;
+      while (r >= p + 2) {
+        r -= p + 2;
+        ++p;
+      }
+      const int j = r;  // 0..p -> dL[p][j]; p + 1 -> dmean[p]
+      double acc = 0.0;
+      for (int s = 0; s < ns; ++s) {
+        const double d = df[s * per_sample + p * M + t];
+        acc = fma(d, (j <= p) ? Z[(int64_t)(s0 + s) * q * M + j * M + t] : 1.0, acc);
+      }
+      accv[w] += acc;
+    }
+  }
+  for (int w = 0; w < 2; ++w) {
+    const int ent = tid + w * THREADS;
+    if (ent >= nent) continue;
+    const int per_t = q * (q + 3) / 2;
+    const int t = ent / per_t;
+    int r = ent % per_t;
+    int p = 0;
+    while (r >= p + 2) {
+      r -= p + 2;
+      ++p;
+    }
+    const int j = r;
+    const double v = g * accv[w];
+    if (j <= p) {
+      double* dLt = dL + (((int64_t)t * B + b) * q + p) * q;
+      dLt[j] = v;
+    } else {
+      dmean[((int64_t)t * B + b) * q + p] = v;
+    }
+  }
+  // strict upper triangle of dL
+  for (int e = tid; e < M * q * q; e += THREADS) {
+    const int t = e / (q * q), p = (e / q) % q, j = e % q;
+    if (j > p) dL[(((int64_t)t * B + b) * q + p) * q + j] = 0.0;
+  }
+}
+
 // Generic MC qEI / qNEI reduction of given samples (S x B x q): the reduction
 // kernel of the non-fused path (custom posteriors), same semantics as the
 // fused one (acquisition/monte_carlo.py:405-414, 580-589).
@@ -145,6 +299,24 @@ extern "C" int bo_qehvi(int B, int q, int m, const double* mean, const double* L
     qehvi_kernel<3><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, acq);
   else
     qehvi_kernel<4><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, acq);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+extern "C" int bo_qehvi_backward(int B, int q, int m, const double* mean, const double* L,
+                                 const double* Z, int S, const double* cell_lo,
+                                 const double* cell_hi, int K, const double* dacq, double* dmean,
+                                 double* dL, void* stream) {
+  BO_CHECK_ARG(q >= 1 && q <= QMAX, "bo_qehvi_backward: 1 <= q <= %d (got %d)", QMAX, q);
+  BO_CHECK_ARG(m >= 2 && m <= MMAX, "bo_qehvi_backward: 2 <= m <= %d (got %d)", MMAX, m);
+  BO_CHECK_ARG(S > 0 && K >= 0, "bo_qehvi_backward: bad S/K");
+  if (B == 0) return BO_OK;
+  hipStream_t st = as_stream(stream);
+#define BO_QB(MM) qehvi_backward_kernel<MM><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, dacq, dmean, dL)
+  if (m == 2) BO_QB(2);
+  else if (m == 3) BO_QB(3);
+  else BO_QB(4);
+#undef BO_QB
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

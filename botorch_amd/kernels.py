@@ -67,6 +67,16 @@ def gemm(A, B, transA=False, transB=False, alpha=1.0, beta=0.0, C=None, flags=0)
     return C3 if batched else C3.squeeze(0)
 
 
+def gemm_strided(M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, alpha=1.0, beta=0.0,
+                 transA=False, transB=False, flags=0):
+    """Raw strided batched GEMM on tensors' storage (views with custom strides,
+    e.g. per-t-batch column blocks of a padded matrix)."""
+    dev = _dev(A, B, C)
+    check(lib().bo_gemm_f64(int(transA), int(transB), M, N, K, alpha, _p(A), lda, sA, _p(B), ldb,
+                            sB, beta, _p(C), ldc, sC, batch, flags, _stream(dev)), "gemm_strided")
+    return C
+
+
 def covar_matrix(X1, X2, lengthscale, kind=_lib.RBF, outputscale=1.0, diag_add=0.0):
     dev = _dev(X1, X2, lengthscale)
     n1, d = X1.shape
@@ -265,26 +275,45 @@ def w_matrix(cache: GPCache, pp: PostPartials) -> torch.Tensor:
 
 def qmc_backward(mode: int, mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor,
                  dacq: torch.Tensor, best_f: float = 0.0,
-                 best_f_s: Optional[torch.Tensor] = None):
+                 best_f_s: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None):
+    """dacq -> (dmean, dcov[, dF]).  qNEI passes F = Z_base T (S x nrows_pad) and
+    gets its cotangent dF back as a third output."""
     dev = mean.device
     B, q = mean.shape
     S = Z.shape[0]
     dmean = torch.empty(B, q, dtype=torch.float64, device=dev)
     dcov = torch.empty(B, q, q, dtype=torch.float64, device=dev)
+    dF = torch.zeros_like(F) if F is not None else None
     check(lib().bo_qmc_backward(mode, B, q, _p(mean), _p(L), _p(Z.reshape(S, q).contiguous()), S,
-                                float(best_f), _p(best_f_s), _p(dacq.contiguous()), _p(dmean),
-                                _p(dcov), _stream(dev)), "qmc_backward")
+                                float(best_f), _p(best_f_s), _p(F),
+                                F.shape[1] if F is not None else 0, _p(dacq.contiguous()),
+                                _p(dmean), _p(dcov), _p(dF), _stream(dev)), "qmc_backward")
+    if F is not None:
+        return dmean, dcov, dF
     return dmean, dcov
 
 
-def post_backward(cache: GPCache, pp: PostPartials, W: torch.Tensor, dmean: torch.Tensor,
-                  dcov: torch.Tensor, ystd: float) -> torch.Tensor:
-    dev = W.device
-    dX = torch.empty(pp.B, pp.q, cache.d, dtype=torch.float64, device=dev)
-    check(lib().bo_post_backward(cache.kind, pp.B, pp.q, cache.d, _p(pp.Xq), _p(cache.Xt_scaled),
-                                 cache.n, _p(W), W.shape[1], _p(cache.alpha),
-                                 _p(dmean.contiguous()), _p(dcov.contiguous()),
-                                 _p(cache.lengthscale), cache.outputscale, float(ystd), _p(dX),
+def post_backward(cache: GPCache, pp: PostPartials, W: Optional[torch.Tensor],
+                  dmean: Optional[torch.Tensor], dcov: Optional[torch.Tensor], ystd: float,
+                  E: Optional[torch.Tensor] = None, Xt_scaled: Optional[torch.Tensor] = None,
+                  n: Optional[int] = None, dX: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dX of the batched posterior: dK*x = ystd dmean alpha^T - G W (+ E), through
+    dk/dx over the training points.  With ``Xt_scaled``/``n`` (other points, e.g.
+    the qNEI baseline) and only ``E``, the gradient through K(points, X); ``dX``
+    given -> accumulated into it."""
+    dev = pp.Xq.device
+    acc = dX is not None
+    if dX is None:
+        dX = torch.empty(pp.B, pp.q, cache.d, dtype=torch.float64, device=dev)
+    other = Xt_scaled is not None
+    cont = lambda t: t.contiguous() if t is not None else None  # noqa: E731
+    W, E, dmean, dcov = cont(W), cont(E), cont(dmean), cont(dcov)
+    check(lib().bo_post_backward(cache.kind, pp.B, pp.q, cache.d, _p(pp.Xq),
+                                 _p(Xt_scaled if other else cache.Xt_scaled),
+                                 n if other else cache.n, _p(W), W.shape[1] if W is not None else 0,
+                                 None if other else _p(cache.alpha), _p(dmean), _p(dcov), _p(E),
+                                 E.shape[1] if E is not None else 0, _p(cache.lengthscale),
+                                 cache.outputscale, float(ystd), int(acc), _p(dX),
                                  _stream(dev)), "post_backward")
     return dX
 
@@ -418,6 +447,49 @@ def qehvi(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor, cell_lo: torch.T
                          _p(cell_hi.contiguous()), cell_lo.shape[0], _p(acq), _stream(dev)),
           "qehvi")
     return acq
+
+
+def qehvi_backward(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor, cell_lo: torch.Tensor,
+                   cell_hi: torch.Tensor, dacq: torch.Tensor):
+    """Backward of :func:`qehvi`: -> dmean (m x B x q), dL (m x B x q x q)."""
+    dev = _dev(mean, L, Z, cell_lo, cell_hi)
+    m, B, q = mean.shape
+    S = Z.shape[0]
+    dmean = torch.empty(m, B, q, dtype=torch.float64, device=dev)
+    dL = torch.empty(m, B, q, q, dtype=torch.float64, device=dev)
+    check(lib().bo_qehvi_backward(B, q, m, _p(mean.contiguous()), _p(L.contiguous()),
+                                  _p(Z.reshape(S, q * m).contiguous()), S,
+                                  _p(cell_lo.contiguous()), _p(cell_hi.contiguous()),
+                                  cell_lo.shape[0], _p(dacq.contiguous()), _p(dmean), _p(dL),
+                                  _stream(dev)), "qehvi_backward")
+    return dmean, dL
+
+
+def kernel_grad(X: torch.Tensor, Y: torch.Tensor, dK: torch.Tensor, lengthscale: torch.Tensor,
+                kind: int, outputscale: float = 1.0, group: int = 0,
+                dX: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dX (+)= sum_k dK[i, k] d k(X_i, Y_k)/dX_i for any d <= 128 (original scale)."""
+    dev = _dev(X, Y, dK)
+    rows, d = X.shape
+    acc = dX is not None
+    if dX is None:
+        dX = torch.empty(rows, d, dtype=torch.float64, device=dev)
+    dK = dK.contiguous()
+    check(lib().bo_kernel_grad(kind, _p(X.contiguous()), rows, _p(Y.contiguous()), Y.shape[0], d,
+                               _p(lengthscale.reshape(-1).contiguous()), float(outputscale),
+                               _p(dK), dK.shape[-1], group, int(acc), _p(dX), _stream(dev)),
+          "kernel_grad")
+    return dX
+
+
+def chol_backward(L: torch.Tensor, dL: torch.Tensor) -> torch.Tensor:
+    """Batched Cholesky backward (B x q x q) -> dA (torch linalg.cholesky semantics)."""
+    dev = _dev(L, dL)
+    B, q, _ = L.shape
+    dA = torch.empty(B, q, q, dtype=torch.float64, device=dev)
+    check(lib().bo_chol_backward(B, q, _p(L.contiguous()), _p(dL.contiguous()), _p(dA),
+                                 _stream(dev)), "chol_backward")
+    return dA
 
 
 def mc_reduce(samples: torch.Tensor, best_f: float = 0.0,

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 1
+#define BO_ABI_VERSION 2
 
 /* status codes */
 #define BO_OK 0
@@ -59,6 +59,11 @@ int bo_probe_mfma_f64_layout(double* out, void* stream);
 /* Peak-rate probe: `blocks` x 256 threads, each wave issuing iters x 8
  * independent fp64 MFMAs (2048 flop each).  out: 1 double (kept live). */
 int bo_probe_mfma_f64_rate(int blocks, int iters, double* out, void* stream);
+
+/* Phase-timing probe of the 128-block Cholesky kernel (potrf.hip) on the
+ * leading block of A (lda even, >= 128): 16 s_memtime stamps into tsc. */
+int bo_probe_potrf_phases(double* A, int64_t lda, double* Linv, int* info, long long* tsc,
+                          void* stream);
 
 /* Batched C = alpha op(A) op(B) + beta C on the fp64 matrix cores (strides sA,
  * sB, sC between batch members).  Building block of the Cholesky/inverse and
@@ -187,20 +192,40 @@ int bo_qmc_finalize(int kind, int mode, int B, int q, const double* Xq, const do
  * dacq (B) -> dmean (B x q), dcov (B x q x q, symmetric) w.r.t. the outcome-
  * space posterior (mean', Sigma'), given mean' and L_q from bo_qmc_finalize.
  * mode: BO_QMC_QEI or BO_QMC_QNEI (best_f_s per sample).  torch semantics:
- * amax splits ties evenly, clamp_min(0) passes the gradient at >= 0. */
+ * amax splits ties evenly, clamp_min(0) passes the gradient at >= 0.
+ * qNEI (cached root, utils/low_rank.py:85-173): the forward samples include
+ * F = Z_base T (S x ldF, rows b*Qp + a, as passed to bo_qmc_finalize); dF (same
+ * layout) receives its cotangent, from which dT = Z_base^T dF.  F/dF may be
+ * NULL for qEI. */
 int bo_qmc_backward(int mode, int B, int q, const double* mean, const double* Lq,
                     const double* Z, int S, double best_f, const double* best_f_s,
-                    const double* dacq, double* dmean, double* dcov, void* stream);
+                    const double* F, int64_t ldF, const double* dacq, double* dmean,
+                    double* dcov, double* dF, void* stream);
 
 /* Backward of the batched exact posterior w.r.t. the candidates X (B x q x d):
  *   dK*x = ystd dmean alpha^T - G W,  G = ystd^2 (dcov + dcov^T),
  *   W = R L^{-1} (nrows_pad x ldw, rows b*Qp + a), dK** = ystd^2 dcov,
- * reduced through dk/dx.  Xq / Xt_scaled as for bo_post_partials.  Caches carry
- * no gradient ([G] detach_test_caches, botorch/models/utils/assorted.py:286-298). */
+ *   + E (optional extra dK*x, nrows_pad x lde, same rows: the qNEI cross-
+ *     covariance terms),
+ * reduced through dk/dx.  Xq / Xt_scaled as for bo_post_partials.  W, alpha,
+ * dmean, dcov and E may each be NULL (term absent); accumulate != 0 adds into
+ * dX.  With Xt_scaled = the qNEI baseline points and only E, this is the
+ * gradient through K(X_baseline, X).  Caches carry no gradient ([G]
+ * detach_test_caches, botorch/models/utils/assorted.py:286-298). */
 int bo_post_backward(int kind, int B, int q, int d, const double* Xq, const double* Xt_scaled,
                      int64_t n, const double* W, int64_t ldw, const double* alpha,
-                     const double* dmean, const double* dcov, const double* lengthscale,
-                     double outputscale, double ystd, double* dX, void* stream);
+                     const double* dmean, const double* dcov, const double* E, int64_t lde,
+                     const double* lengthscale, double outputscale, double ystd, int accumulate,
+                     double* dX, void* stream);
+
+/* Kernel-matrix gradient for any d <= 128 (inputs in the original scale):
+ *   dX[i][t] (+)= sum_k dK[i][k] d k(X_i, Y_k) / d X_it,
+ * group > 0: row i pairs only with the `group` rows of its own block of Y
+ * (dK row = group entries) -- the K** term of q-batches.  Generic-d path of
+ * the posterior backward (SAAS, d = 50: models/fully_bayesian.py:509-546). */
+int bo_kernel_grad(int kind, const double* X, int64_t rows, const double* Y, int64_t n, int d,
+                   const double* lengthscale, double outputscale, const double* dK, int64_t ldk,
+                   int group, int accumulate, double* dX, void* stream);
 
 /* Exact-MLL terms for fit_gpytorch_mll (botorch/fit.py:75-258 ->
  * optim/closures/model_closures.py:171-184, [G] ExactMarginalLogLikelihood),
@@ -223,6 +248,17 @@ int bo_mll_terms(int kind, const double* X, int64_t n, int d, const double* leng
  * mean: m x B x q, L: m x B x q x q, Z: S x (q m).  2 <= m <= 4, q <= 12. */
 int bo_qehvi(int B, int q, int m, const double* mean, const double* L, const double* Z, int S,
              const double* cell_lo, const double* cell_hi, int K, double* acq, void* stream);
+
+/* Backward of bo_qehvi (autograd through _compute_qehvi,
+ * multi_objective/monte_carlo.py:230-317): dacq (B) -> dmean (m x B x q) and
+ * dL (m x B x q x q, lower) of the per-output posterior roots. */
+int bo_qehvi_backward(int B, int q, int m, const double* mean, const double* L, const double* Z,
+                      int S, const double* cell_lo, const double* cell_hi, int K,
+                      const double* dacq, double* dmean, double* dL, void* stream);
+
+/* Batched Cholesky backward (torch linalg.cholesky backward): L, dL (B x q x q,
+ * lower) -> dA (B x q x q, symmetric), q <= 16. */
+int bo_chol_backward(int B, int q, const double* L, const double* dL, double* dA, void* stream);
 
 /* MC qEI / qNEI reduction of given samples (S x B x q):
  * acq[b] = mean_s max(max_a samples[s][b][a] - bf_s, 0), bf_s = best_f_s[s] or best_f. */

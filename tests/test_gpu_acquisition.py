@@ -178,6 +178,31 @@ def test_qnei_cached_root_matches_oracle(r, B, q, S):
     torch.testing.assert_close(v, rv, rtol=1e-5, atol=1e-8)
 
 
+@pytest.mark.parametrize("r,B,q,S", [(40, 8, 4, 128), (25, 6, 16, 64), (12, 16, 2, 128)])
+def test_qnei_gradient_matches_oracle(r, B, q, S):
+    """d qNEI / dX through the cached-root path (utils/low_rank.py:85-173
+    differentiated) vs. torch autograd through the oracle restatement."""
+    from botorch_amd.acquisition import qNoisyExpectedImprovement
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import QNEIOracle
+    X, Y, m, orc = _setup(n=200, noise=1e-2)
+    Xb = X[:r]
+    acqf = qNoisyExpectedImprovement(m, Xb.to(DEV), sampler=SobolQMCNormalSampler(torch.Size([S]), seed=5),
+                                     prune_baseline=False)
+    ref = QNEIOracle(orc, Xb, S, seed=5)
+    g = torch.Generator().manual_seed(100 + r)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64)
+    Xd = Xc.to(DEV).requires_grad_(True)
+    v = acqf(Xd)
+    (gd,) = torch.autograd.grad(v.sum(), Xd)
+    Xo = Xc.clone().requires_grad_(True)
+    rv = ref(Xo)
+    (go,) = torch.autograd.grad(rv.sum(), Xo)
+    torch.testing.assert_close(v.detach().cpu(), rv.detach(), rtol=1e-5, atol=1e-8)
+    assert go.abs().max() > 0
+    torch.testing.assert_close(gd.cpu(), go, rtol=1e-5, atol=1e-8)
+
+
 def test_prune_inferior_points_matches_oracle():
     from botorch_amd.acquisition import prune_inferior_points
     from botorch_amd.sampling import SobolQMCNormalSampler
@@ -221,6 +246,44 @@ def test_qehvi_api_matches_oracle(golden, B, q, S):
     torch.testing.assert_close(v, ref, rtol=1e-7, atol=1e-10)
 
 
+@pytest.mark.parametrize("B,q,S", [(5, 2, 64), (3, 4, 128), (2, 8, 32)])
+def test_qehvi_gradient_matches_oracle(golden, B, q, S):
+    """d qEHVI / dX (bo_qehvi_backward + bo_chol_backward + bo_post_backward per
+    output) vs. torch autograd through the oracle's _compute_qehvi restatement."""
+    from botorch_amd.acquisition import qExpectedHypervolumeImprovement
+    from botorch_amd.models import ModelListGP, SingleTaskGP
+    from botorch_amd.multi_objective import FastNondominatedPartitioning
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import qehvi
+    from oracle.gp import ExactGPOracle, GPHyper
+    from oracle.sampling import base_samples_multi_output
+    X = torch.from_numpy(golden["dtlz2_X"][:96])
+    Y = torch.from_numpy(golden["dtlz2_Y"][:96])
+    models, oracles = [], []
+    for t in range(3):
+        mdl = SingleTaskGP(X.to(DEV), Y[:, t:t + 1].to(DEV))
+        mdl.covar_module.lengthscale = torch.full((1, 6), 0.6, dtype=torch.float64)
+        mdl.likelihood.noise = torch.tensor([1e-3], dtype=torch.float64)
+        models.append(mdl.eval())
+        oracles.append(ExactGPOracle(X, Y[:, t:t + 1], GPHyper(torch.full((6,), 0.6, dtype=torch.float64), 1e-3, 0.0)))
+    ref_point = torch.full((3,), -1.1, dtype=torch.float64)
+    part = FastNondominatedPartitioning(ref_point, Y)
+    acqf = qExpectedHypervolumeImprovement(ModelListGP(*models), ref_point.tolist(), part,
+                                           sampler=SobolQMCNormalSampler(torch.Size([S]), seed=9))
+    g = torch.Generator().manual_seed(50 + q)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64)
+    Xd = Xc.to(DEV).requires_grad_(True)
+    v = acqf(Xd)
+    (gd,) = torch.autograd.grad(v.sum(), Xd)
+    lo, hi = part.get_hypercell_bounds()
+    Xo = Xc.clone().requires_grad_(True)
+    ref = qehvi(oracles, Xo, base_samples_multi_output(S, q, 3, 9), lo, hi)
+    (go,) = torch.autograd.grad(ref.sum(), Xo)
+    torch.testing.assert_close(v.detach().cpu(), ref.detach(), rtol=1e-7, atol=1e-10)
+    assert go.abs().max() > 0
+    torch.testing.assert_close(gd.cpu(), go, rtol=1e-5, atol=1e-8)
+
+
 @pytest.mark.parametrize("d,M,q", [(50, 16, 4), (10, 3, 2)])
 def test_saas_qei_matches_oracle(d, M, q):
     """C5 shape: SAAS ensemble of M Matern-5/2 GPs, d=50, qEI averaged over MCMC_DIM."""
@@ -252,3 +315,37 @@ def test_saas_qei_matches_oracle(d, M, q):
     assert val.shape == (B,)
     ref = saas_qei(members, Xc, base_samples_single_output(S, q, 0), best_f)
     torch.testing.assert_close(val, ref, rtol=1e-2, atol=1e-6)
+
+
+@pytest.mark.parametrize("d,M,q", [(50, 4, 3), (10, 3, 2)])
+def test_saas_qei_gradient_matches_oracle(d, M, q):
+    """d qEI / dX over the SAAS ensemble (generic-d path: bo_kernel_grad) vs. torch
+    autograd through the oracle members."""
+    from botorch_amd.acquisition import qExpectedImprovement
+    from botorch_amd.models import SaasFullyBayesianSingleTaskGP, sample_saas_prior
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from botorch_amd.test_functions import Hartmann
+    from oracle.acquisition import saas_members, saas_qei
+    from oracle.sampling import base_samples_single_output, draw_sobol_samples
+    n, S, B = 64, 128, 6
+    lo = torch.zeros(d, dtype=torch.float64)
+    X = draw_sobol_samples(lo, lo + 1, n, 1, 0).squeeze(1)
+    Y = Hartmann(negate=True)(X[:, :6]).unsqueeze(-1)
+    Y = (Y - Y.mean()) / Y.std()
+    smp = sample_saas_prior(d, M, seed=1)
+    m = SaasFullyBayesianSingleTaskGP(X.to(DEV), Y.to(DEV))
+    m.load_mcmc_samples({k: v.to(DEV) for k, v in smp.items()})
+    m.eval()
+    best_f = float(Y.median())
+    acqf = qExpectedImprovement(m, best_f, sampler=SobolQMCNormalSampler(torch.Size([S]), seed=2))
+    Xc = draw_sobol_samples(lo, lo + 1, B, q, 3)
+    Xd = Xc.to(DEV).requires_grad_(True)
+    v = acqf(Xd)
+    (gd,) = torch.autograd.grad(v.sum(), Xd)
+    members = saas_members(X, Y, smp)
+    Xo = Xc.clone().requires_grad_(True)
+    ref = saas_qei(members, Xo, base_samples_single_output(S, q, 2), best_f)
+    (go,) = torch.autograd.grad(ref.sum(), Xo)
+    torch.testing.assert_close(v.detach().cpu(), ref.detach(), rtol=1e-6, atol=1e-9)
+    assert go.abs().max() > 0
+    torch.testing.assert_close(gd.cpu(), go, rtol=1e-5, atol=1e-8)
