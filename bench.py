@@ -135,6 +135,162 @@ def cpu_baseline(Xtr, Ytr, Xc, best_f, budget_s=20.0):
     }
 
 
+def _gpu_time(fn, steps=5, warmup=1):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def _cpu_time(fn, budget_s=4.0, max_runs=5):
+    fn()
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < max_runs and (len(times) < 2 or time.perf_counter() - t_start < budget_s):
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    return times[len(times) // 2], len(times)
+
+
+def other_configs(dev, cpu=True):
+    """The other SURVEY.md section 8 configurations, forward-only acq-evals/s on
+    this GPU beside the torch-fp64 CPU restatement (oracle/) on a bounded sample
+    of the same workload (C2 qEI, C3 qNEI with pruned baseline, C4 qEHVI over a
+    ModelListGP on DTLZ2, C5 SAAS qEI at d = 50)."""
+    from botorch_amd.acquisition import (qExpectedHypervolumeImprovement, qExpectedImprovement,
+                                         qNoisyExpectedImprovement)
+    from botorch_amd.models import (ModelListGP, SaasFullyBayesianSingleTaskGP, SingleTaskGP,
+                                    sample_saas_prior)
+    from botorch_amd.multi_objective import FastNondominatedPartitioning
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from botorch_amd.test_functions import DTLZ2, Hartmann
+    from botorch_amd.utils_sampling import draw_sobol_samples
+    from oracle import acquisition as oacq
+    from oracle.gp import MATERN52, ExactGPOracle, GPHyper
+    from oracle.sampling import base_samples_multi_output, base_samples_single_output
+    torch.set_num_threads(cpu_cores())
+    out = {}
+    f64 = torch.float64
+
+    def unit(d):
+        return torch.stack([torch.zeros(d, dtype=f64), torch.ones(d, dtype=f64)])
+
+    def stgp(X, Y, ls, noise, kind_matern=False):
+        m = SingleTaskGP(X.to(dev), Y.to(dev))
+        m.covar_module.lengthscale = torch.full((1, X.shape[-1]), ls, dtype=f64)
+        m.likelihood.noise = torch.tensor([noise], dtype=f64)
+        return m.eval()
+
+    # C2: qEI n=1024 d=6 q=8 S=256 b=64
+    n, q, S, b = 1024, 8, 256, 64
+    X = draw_sobol_samples(unit(6), n, 1, seed=0).squeeze(1)
+    Y = Hartmann(negate=True)(X).unsqueeze(-1)
+    Xc = draw_sobol_samples(unit(6), b, q, seed=1)
+    m = stgp(X, Y, LENGTHSCALE, NOISE)
+    acqf = qExpectedImprovement(m, float(Y.max()), sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
+    Xd = Xc.to(dev)
+    with torch.no_grad():
+        t = _gpu_time(lambda: acqf(Xd), steps=20, warmup=3)
+    e = {"config": "C2 qEI n=1024 d=6 q=8 S=256 b=64", "gpu_evals_per_s": q * S * b / t,
+         "gpu_ms": 1e3 * t}
+    if cpu:
+        orc = ExactGPOracle(X, Y, GPHyper(torch.full((6,), LENGTHSCALE, dtype=f64), NOISE, 0.0))
+        Z = base_samples_single_output(S, q, 0)
+        tc, runs = _cpu_time(lambda: oacq.qei(orc, Xc, Z, float(Y.max())))
+        e.update(cpu_evals_per_s=q * S * b / tc, cpu_sample=f"all {b} restarts, median of {runs}")
+    out["C2"] = e
+
+    # C3 qNEI: n=4096 d=6 q=16 S=512 b=512, X_baseline = X_tr pruned (2048 samples)
+    n, q, S, b = N_TRAIN, Q, MC, RESTARTS
+    X = draw_sobol_samples(unit(6), n, 1, seed=0).squeeze(1)
+    Y = Hartmann(negate=True)(X).unsqueeze(-1)
+    Xc = draw_sobol_samples(unit(6), b, q, seed=1)
+    m = stgp(X, Y, LENGTHSCALE, NOISE)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    acqf = qNoisyExpectedImprovement(m, X.to(dev), sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0),
+                                     prune_baseline=True)
+    torch.cuda.synchronize()
+    init_ms = 1e3 * (time.perf_counter() - t0)
+    r = int(acqf.X_baseline.shape[0])
+    Xd = Xc.to(dev)
+    with torch.no_grad():
+        t = _gpu_time(lambda: acqf(Xd), steps=10, warmup=2)
+    e = {"config": "C3 qNEI n=4096 d=6 q=16 S=512 b=512, pruned baseline (cache_root)",
+         "r": r, "init_ms": init_ms, "gpu_evals_per_s": q * S * b / t, "gpu_ms": 1e3 * t}
+    if cpu:
+        orc = ExactGPOracle(X, Y, GPHyper(torch.full((6,), LENGTHSCALE, dtype=f64), NOISE, 0.0))
+        Xb = acqf.X_baseline.cpu()
+        ref = oacq.QNEIOracle(orc, Xb, S, seed=0)
+        bs = 8
+        tc, runs = _cpu_time(lambda: ref(Xc[:bs]))
+        e.update(cpu_evals_per_s=q * S * bs / tc,
+                 cpu_sample=f"{bs} of {b} restarts (full (r+q) posterior as the reference), median of {runs}")
+    out["C3_qNEI"] = e
+
+    # C4: qEHVI, ModelListGP of 3 on DTLZ2 (n=2048, d=6), q=8, S=128, b=128
+    n, q, S, b, mo = 2048, 8, 128, 128, 3
+    g = torch.Generator().manual_seed(0)
+    X = torch.rand(n, 6, generator=g, dtype=f64)
+    Y = DTLZ2(dim=6, num_objectives=mo, negate=True).evaluate_true(X)
+    Y = -Y
+    models = [stgp(X, Y[:, t:t + 1], 0.6, 1e-3) for t in range(mo)]
+    ref_point = torch.full((mo,), -1.1, dtype=f64)
+    part = FastNondominatedPartitioning(ref_point, Y)
+    acqf = qExpectedHypervolumeImprovement(ModelListGP(*models), ref_point.tolist(), part,
+                                           sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
+    Xc = draw_sobol_samples(unit(6), b, q, seed=1)
+    Xd = Xc.to(dev)
+    with torch.no_grad():
+        t = _gpu_time(lambda: acqf(Xd), steps=5, warmup=1)
+    lo, hi = part.get_hypercell_bounds()
+    e = {"config": "C4 qEHVI ModelListGP(3) DTLZ2 n=2048 d=6 q=8 S=128 b=128",
+         "cells": int(lo.shape[0]), "gpu_evals_per_s": q * S * b / t, "gpu_ms": 1e3 * t}
+    if cpu:
+        orcs = [ExactGPOracle(X, Y[:, t:t + 1], GPHyper(torch.full((6,), 0.6, dtype=f64), 1e-3, 0.0))
+                for t in range(mo)]
+        Zm = base_samples_multi_output(S, q, mo, 0)
+        bs = 2
+        tc, runs = _cpu_time(lambda: oacq.qehvi(orcs, Xc[:bs], Zm, lo, hi), budget_s=6.0, max_runs=3)
+        e.update(cpu_evals_per_s=q * S * bs / tc, cpu_sample=f"{bs} of {b} restarts, median of {runs}")
+    out["C4_qEHVI"] = e
+
+    # C5: SAAS (M=16 prior draws), d=50, n=256, qEI q=4, S=256, b=64
+    d, n, M, q, S, b = 50, 256, 16, 4, 256, 64
+    X = draw_sobol_samples(unit(d), n, 1, seed=0).squeeze(1)
+    Y = Hartmann(negate=True)(X[:, :6]).unsqueeze(-1)
+    Y = (Y - Y.mean()) / Y.std()
+    smp = sample_saas_prior(d, M, seed=0)
+    m = SaasFullyBayesianSingleTaskGP(X.to(dev), Y.to(dev))
+    m.load_mcmc_samples({k: v.to(dev) for k, v in smp.items()})
+    m.eval()
+    acqf = qExpectedImprovement(m, float(Y.max()), sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
+    Xc = draw_sobol_samples(unit(d), b, q, seed=1)
+    Xd = Xc.to(dev)
+    with torch.no_grad():
+        t = _gpu_time(lambda: acqf(Xd), steps=10, warmup=2)
+    e = {"config": "C5 SAAS (16 prior draws) d=50 n=256 qEI q=4 S=256 b=64",
+         "gpu_evals_per_s": q * S * b * M / t, "gpu_ms": 1e3 * t,
+         "note": "evals counted per MCMC member (q x b x S x M)"}
+    if cpu:
+        members = oacq.saas_members(X, Y, smp)
+        Z = base_samples_single_output(S, q, 0)
+        bs = 16
+        tc, runs = _cpu_time(lambda: oacq.saas_qei(members, Xc[:bs], Z, float(Y.max())))
+        e.update(cpu_evals_per_s=q * S * bs * M / tc, cpu_sample=f"{bs} of {b} restarts, median of {runs}")
+    out["C5_SAAS"] = e
+    for v in out.values():
+        if "cpu_evals_per_s" in v:
+            v["speedup"] = v["gpu_evals_per_s"] / v["cpu_evals_per_s"]
+    return out
+
+
 def time_gp_fit(Xtr, Ytr, dev, cpu=True):
     """GP-fit half of the metric: fit_gpytorch_mll (L-BFGS-B, exact MLL + gradient on
     the device) from BoTorch's default initialisation, n=4096, d=6.  CPU side: one
@@ -186,6 +342,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fit", action="store_true", help="skip the GP-fit half of the metric")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the other section-8 configurations (C2, C3 qNEI, C4, C5)")
     args = ap.parse_args()
 
     ws, rank, local = _dist_env()
@@ -264,7 +422,20 @@ def main():
     peak = 78.6  # MI355X dense FP64 matrix TFLOP/s (MI355X_MICROARCH.md / SURVEY.md 8(d))
     traffic, traffic_src = pmc_traffic()
 
+    # forward + backward (the optimize_acqf call pattern, gen.py:194-222)
+    Xg = Xd.clone().requires_grad_(True)
+
+    def fwd_bwd():
+        v = acqf(Xg)
+        torch.autograd.grad(v.sum(), Xg)
+
+    fb_s = _gpu_time(fwd_bwd, steps=5, warmup=2)
+    fwd_bwd = {"evals_per_s": Q * RESTARTS * MC / fb_s, "ms": 1e3 * fb_s}
+
     gp_fit = None
+    extra = None
+    if rank == 0 and ws == 1 and not args.no_extra:
+        extra = other_configs(dev, cpu=not args.no_cpu_baseline)
     if rank == 0 and not args.no_fit:
         gp_fit = time_gp_fit(Xtr, Ytr, dev, cpu=(not args.no_cpu_baseline and ws == 1))
     if rank == 0:
@@ -294,7 +465,9 @@ def main():
                          "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "kernel_ms": kern_avg_ms, "flops_per_launch": fl},
             "cpu_baseline": cpu,
+            "fwd_bwd": fwd_bwd,
             "gp_fit": gp_fit,
+            "other_configs": extra,
         }
         if cpu:
             line["speedup_vs_cpu"] = value / cpu["value"]

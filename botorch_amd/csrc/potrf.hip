@@ -93,17 +93,21 @@ __device__ __forceinline__ int factor32(double* Sd, double* Dd, double* colbuf, 
       x[u][v] = (l == i) ? 1.0 : 0.0;
     }
   int fail = 0;
+  // 1/sqrt by v_rsq_f64 + two Newton steps (full fp64 accuracy): off the sqrt +
+  // divide macro sequences, and computed one step AHEAD (right after the next
+  // pivot's own update) so its latency hides under the step's other FMAs.
+  auto rsq_nr = [](double v) {
+    double r = __builtin_amdgcn_rsq(v);
+    r = r * fma(-0.5 * v * r, r, 1.5);
+    r = r * fma(-0.5 * v * r, r, 1.5);
+    return r;
+  };
+  double ajj = readlane_d(a[0][0], 0);
+  double inv = rsq_nr(ajj);
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
     const int jt = j >> 2, ju = j & 3;
-    // pivot from the owner lane (jt, jt)
-    const double ajj = readlane_d(a[ju][ju], jt * 9);
     if (!(ajj > 0.0) && fail == 0) fail = j + 1;
-    // 1/sqrt by v_rsq_f64 + two Newton steps (full fp64 accuracy), off the
-    // sqrt + divide macro sequences that would sit on the 32-step chain
-    double inv = __builtin_amdgcn_rsq(ajj);
-    inv = inv * fma(-0.5 * ajj * inv, inv, 1.5);
-    inv = inv * fma(-0.5 * ajj * inv, inv, 1.5);
     const double d = ajj * inv;
     // column j of L (owners: tj == jt) -> colbuf
     if (tj == jt) {
@@ -145,11 +149,19 @@ __device__ __forceinline__ int factor32(double* Sd, double* Dd, double* colbuf, 
     const double Lrm[4] = {(4 * ti + 0 > j) ? -r01.x : 0.0, (4 * ti + 1 > j) ? -r01.y : 0.0,
                            (4 * ti + 2 > j) ? -r23.x : 0.0, (4 * ti + 3 > j) ? -r23.y : 0.0};
     const double Xr[4] = {x01.x, x01.y, x23.x, x23.y};
+    // next pivot first: its element (u1, u1) of the owner lane (jt1, jt1)
+    const int j1 = j + 1;
+    const int u1 = j1 & 3;
+    if (j1 < 32) {
+      a[u1][u1] = fma(Lr[u1], Lcm[u1], a[u1][u1]);
+      ajj = readlane_d(a[u1][u1], (j1 >> 2) * 9);
+      inv = rsq_nr(ajj);
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        a[u][v] = fma(Lr[u], Lcm[v], a[u][v]);
+        if (!(j1 < 32 && u == u1 && v == u1)) a[u][v] = fma(Lr[u], Lcm[v], a[u][v]);
         x[u][v] = fma(Lrm[u], Xr[v], x[u][v]);
       }
   }
