@@ -234,6 +234,43 @@ def other_configs(dev, cpu=True):
                  cpu_sample=f"{bs} of {b} restarts (full (r+q) posterior as the reference), median of {runs}")
     out["C3_qNEI"] = e
 
+    # C3 with the section 8(f) rank-1 reductions: qLogEI (best_f = max Y) and
+    # qLogNEI on the same pruned baseline, fat=True / default temperatures.
+    from botorch_amd.acquisition import qLogExpectedImprovement, qLogNoisyExpectedImprovement
+    best = float(Y.max())
+    acqf = qLogExpectedImprovement(m, best, sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
+    with torch.no_grad():
+        t = _gpu_time(lambda: acqf(Xd), steps=10, warmup=2)
+    Xg = Xd.clone().requires_grad_(True)
+
+    def fb():
+        (gx,) = torch.autograd.grad(acqf(Xg).sum(), Xg)
+        return gx
+
+    tfb = _gpu_time(fb, steps=5, warmup=1)
+    e = {"config": "C3 qLogEI n=4096 d=6 q=16 S=512 b=512 (fat, tau_relu=1e-6, tau_max=1e-2)",
+         "gpu_evals_per_s": q * S * b / t, "gpu_ms": 1e3 * t,
+         "fwd_bwd_evals_per_s": q * S * b / tfb, "fwd_bwd_ms": 1e3 * tfb}
+    if cpu:
+        orc = ExactGPOracle(X, Y, GPHyper(torch.full((6,), LENGTHSCALE, dtype=f64), NOISE, 0.0))
+        Z = base_samples_single_output(S, q, 0)
+        bs = 64
+        tc, runs = _cpu_time(lambda: oacq.qlogei(orc, Xc[:bs], Z, best))
+        e.update(cpu_evals_per_s=q * S * bs / tc, cpu_sample=f"{bs} of {b} restarts, median of {runs}")
+    out["C3_qLogEI"] = e
+    acqf = qLogNoisyExpectedImprovement(m, X.to(dev), sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0),
+                                        prune_baseline=True)
+    with torch.no_grad():
+        t = _gpu_time(lambda: acqf(Xd), steps=10, warmup=2)
+    e = {"config": "C3 qLogNEI n=4096 d=6 q=16 S=512 b=512, pruned baseline (cache_root)",
+         "r": int(acqf.X_baseline.shape[0]), "gpu_evals_per_s": q * S * b / t, "gpu_ms": 1e3 * t}
+    if cpu:
+        ref = oacq.QNEIOracle(orc, acqf.X_baseline.cpu(), S, seed=0)
+        bs = 8
+        tc, runs = _cpu_time(lambda: oacq.qlognei(ref, Xc[:bs]))
+        e.update(cpu_evals_per_s=q * S * bs / tc, cpu_sample=f"{bs} of {b} restarts, median of {runs}")
+    out["C3_qLogNEI"] = e
+
     # C4: qEHVI, ModelListGP of 3 on DTLZ2 (n=2048, d=6), q=8, S=128, b=128
     n, q, S, b, mo = 2048, 8, 128, 128, 3
     g = torch.Generator().manual_seed(0)

@@ -17,7 +17,9 @@ LIB_PATH = os.path.join(_HERE, "libbotorch_amd.so")
 BO_OK, BO_ERR_ARG, BO_ERR_HIP, BO_ERR_NOT_PSD, BO_ERR_NAN = 0, 1, 2, 3, 4
 RBF, MATERN52 = 0, 1
 GEMM_LOWER_C, GEMM_A_LOWER, GEMM_B_UPPER, GEMM_A_UPPER, GEMM_B_LOWER = 1, 2, 4, 8, 16
-QMC_POSTERIOR, QMC_QEI, QMC_QNEI, QMC_CHOL = 0, 1, 2, 3
+QMC_POSTERIOR, QMC_QEI, QMC_QNEI, QMC_CHOL, QMC_QLOGEI, QMC_QLOGNEI = 0, 1, 2, 3, 4, 5
+LOG_MODES = (QMC_QLOGEI, QMC_QLOGNEI)
+ABI_VERSION = 3
 
 _P = c_void_p  # device pointers travel as void*
 
@@ -53,7 +55,7 @@ _SIGNATURES = {
     "bo_qmc_finalize": (c_int, [c_int, c_int, c_int, c_int, _P, _P, _P, c_int64, c_double,
                                 c_double, c_double, c_double, _P, c_int, c_double, _P, c_int,
                                 c_double, _P, _P, _P, _P, _P, _P, _P, c_int, c_int64, _P,
-                                c_int64, _P]),
+                                c_int64, c_int, c_double, c_double, _P]),
     "bo_qehvi": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, _P, _P, c_int, _P, _P]),
     "bo_qehvi_backward": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, _P, _P, c_int, _P, _P, _P,
                                   _P]),
@@ -66,7 +68,7 @@ _SIGNATURES = {
     "bo_mll_terms": (c_int, [c_int, _P, c_int64, c_int, _P, c_double, _P, _P, c_int64, _P, _P, _P,
                              _P]),
     "bo_qmc_backward": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, c_double, _P, _P,
-                                c_int64, _P, _P, _P, _P, _P]),
+                                c_int64, _P, _P, _P, _P, _P, c_int, c_double, c_double, _P]),
     "bo_post_backward": (c_int, [c_int, c_int, c_int, c_int, _P, _P, c_int64, _P, c_int64, _P,
                                  _P, _P, _P, c_int64, _P, c_double, c_double, c_int, _P, _P]),
 }
@@ -91,6 +93,9 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        if handle.bo_version() != ABI_VERSION:
+            raise NativeLibraryMissing(
+                f"{LIB_PATH} has ABI {handle.bo_version()}, expected {ABI_VERSION}: rebuild with `make`")
         _lib = handle
     return _lib
 

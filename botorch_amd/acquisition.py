@@ -22,7 +22,8 @@ import torch
 from torch import nn
 
 from . import _lib, kernels
-from .exceptions import BotorchWarning, UnsupportedError
+from .exceptions import BotorchError, BotorchWarning, UnsupportedError
+from .safe_math import TAU_MAX, TAU_RELU, fatmax, log_improvement, logmeanexp, smooth_amax
 from .posteriors import FUSED_QMAX
 from .sampling import MCSampler, SobolQMCNormalSampler, get_sampler
 
@@ -121,13 +122,15 @@ class _FusedMC(torch.autograd.Function):
         pp = kernels.post_partials(cache, X3.detach(), store_R=need_grad)
         if kernels.TIMING_HOOK is not None:
             kernels.TIMING_HOOK("post_partials_end")
+        lp = getattr(acqf, "_log_params", None)
         out = kernels.qmc_finalize(cache, pp, mode, ymean, ystd, Z=Z, best_f=best_f,
                                    best_f_s=best_f_s, want_mean=need_grad, want_cov=False,
-                                   want_L=need_grad)
+                                   want_L=need_grad, log_params=lp)
         kernels._raise_not_psd(out["info"], out["jitter"], type(acqf).__name__)
         if need_grad:
             ctx.cache, ctx.pp, ctx.ystd, ctx.mode = cache, pp, ystd, mode
             ctx.best_f, ctx.best_f_s, ctx.Z = best_f, best_f_s, Z
+            ctx.lp, ctx.acq = lp, out["acq"].detach().clone()
             ctx.mean, ctx.L = out["mean"], out["L"]
             ctx.W = kernels.w_matrix(cache, pp)
         return out["acq"]
@@ -135,7 +138,8 @@ class _FusedMC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dacq):
         dmean, dcov = kernels.qmc_backward(ctx.mode, ctx.mean, ctx.L, ctx.Z, dacq.contiguous(),
-                                           ctx.best_f, ctx.best_f_s)
+                                           ctx.best_f, ctx.best_f_s, acq_fwd=ctx.acq,
+                                           log_params=ctx.lp)
         dX = kernels.post_backward(ctx.cache, ctx.pp, ctx.W, dmean, dcov, ctx.ystd)
         return dX, None, None, None, None, None
 
@@ -414,6 +418,8 @@ class qNoisyExpectedImprovement(MCAcquisitionFunction):
                 self._fused_ready = True
         self._zq = {}
 
+    _fused_mode = _lib.QMC_QNEI
+
     def _base_samples_q(self, q: int, device) -> torch.Tensor:
         """The q new columns of the (r+q)-dim Sobol draw (sampling/normal.py:68-131)."""
         if q not in self._zq:
@@ -462,12 +468,14 @@ class _FusedQNEI(torch.autograd.Function):
         T = kernels.gemm(acqf._P_b, pp.Rt, alpha=-s2, beta=1.0, C=T)
         F = kernels.gemm(acqf.Z_base, T)
         Zq = acqf._base_samples_q(q, X3.device)
-        out = kernels.qmc_finalize(cache, pp, _lib.QMC_QNEI, ymean, ystd, Z=Zq,
+        lp = getattr(acqf, "_log_params", None)
+        out = kernels.qmc_finalize(cache, pp, acqf._fused_mode, ymean, ystd, Z=Zq,
                                    best_f_s=acqf._baseline_best_f, want_mean=need_grad,
-                                   want_cov=False, want_L=need_grad, T=T, F=F)
-        kernels._raise_not_psd(out["info"], out["jitter"], "qNoisyExpectedImprovement")
+                                   want_cov=False, want_L=need_grad, T=T, F=F, log_params=lp)
+        kernels._raise_not_psd(out["info"], out["jitter"], type(acqf).__name__)
         if need_grad:
             ctx.acqf, ctx.cache, ctx.pp, ctx.ystd = acqf, cache, pp, ystd
+            ctx.lp, ctx.acq = lp, out["acq"].detach().clone()
             ctx.T, ctx.F, ctx.Zq = T, F, Zq
             ctx.mean, ctx.L = out["mean"], out["L"]
             ctx.W = kernels.w_matrix(cache, pp)
@@ -479,9 +487,9 @@ class _FusedQNEI(torch.autograd.Function):
         s2 = ystd * ystd
         B, q, Qp, nrows = pp.B, pp.q, pp.Qp, pp.nrows_pad
         r = acqf._Linv_rr.shape[0]
-        dmean, dcov, dF = kernels.qmc_backward(_lib.QMC_QNEI, ctx.mean, ctx.L, ctx.Zq,
+        dmean, dcov, dF = kernels.qmc_backward(acqf._fused_mode, ctx.mean, ctx.L, ctx.Zq,
                                                dacq.contiguous(), best_f_s=acqf._baseline_best_f,
-                                               F=ctx.F)
+                                               F=ctx.F, acq_fwd=ctx.acq, log_params=ctx.lp)
         dT = kernels.gemm(acqf.Z_base, dF, transA=True)           # r x nrows_pad
         G = (dcov + dcov.mT).contiguous()                         # B x q x q
         kernels.gemm_strided(r, q, q, ctx.T, nrows, Qp, G, q, q * q, dT, nrows, Qp, B,
@@ -492,6 +500,94 @@ class _FusedQNEI(torch.autograd.Function):
         dX = kernels.post_backward(cache, pp, None, None, None, ystd, E=dKbx.mT.contiguous(),
                                    Xt_scaled=acqf._Xb_scaled, n=r, dX=dX)
         return dX, None
+
+
+# -- LogEI family ---------------------------------------------------------------------
+def _check_tau(tau, name: str):
+    """acquisition/logei.py:537-544."""
+    if isinstance(tau, torch.Tensor) and tau.numel() != 1:
+        raise ValueError(name + f" is not a scalar: {tau.numel() = }.")
+    if not (tau > 0):
+        raise ValueError(name + f" is non-positive: {tau = }.")
+    return tau
+
+
+class qLogExpectedImprovement(qExpectedImprovement):
+    """MC batch log expected improvement (acquisition/logei.py:137-234):
+    qLogEI(X) = logmeanexp_s q_reduce_j log_soft_clamp(Y_sj - best_f), with
+    q_reduce = fatmax(tau_max) and log_soft_clamp = log_fatplus(tau_relu) when
+    fat (default), else smooth_amax / log_softplus.
+
+    Fused path: bo_qmc_finalize in BO_QMC_QLOGEI mode (the same post_partials
+    posterior and q x q root as qEI; only the per-sample reduction differs),
+    backward through bo_qmc_backward's dense log-mode weights."""
+
+    _log = True
+
+    def __init__(self, model, best_f, sampler=None, objective=None, posterior_transform=None,
+                 X_pending=None, constraints=None, eta=1e-3, fat: bool = True,
+                 tau_max: float = TAU_MAX, tau_relu: float = TAU_RELU):
+        super().__init__(model, best_f, sampler, objective, posterior_transform, X_pending,
+                         constraints=constraints, eta=eta)
+        self.tau_max = _check_tau(tau_max, "tau_max")
+        self.tau_relu = _check_tau(tau_relu, "tau_relu")
+        self._fat = fat
+        self._log_params = (int(bool(fat)), float(tau_relu), float(tau_max))
+
+    def _reduce(self, obj: torch.Tensor, best_f: torch.Tensor) -> torch.Tensor:
+        """sample x batch x q objective -> batch (SampleReducingMCAcquisitionFunction.
+        forward, monte_carlo.py:253-289, with the LogEI reductions)."""
+        li = log_improvement(obj, best_f, tau=self.tau_relu, fat=self._fat)
+        q_red = fatmax if self._fat else smooth_amax
+        return logmeanexp(q_red(li, dim=-1, tau=self.tau_max), dim=0)
+
+    def forward(self, X: torch.Tensor) -> torch.Tensor:
+        X = self._concat_pending(t_batch_mode(X))
+        batch = X.shape[:-2]
+        q, d = X.shape[-2], X.shape[-1]
+        X3 = X.reshape(-1, q, d)
+        if self._fused_eligible(X) and self.best_f.numel() == 1:
+            sampler = self._ensure_sampler()
+            Z = sampler.base_samples_2d(q, X.device)
+            acq = _FusedMC.apply(X3, self, _lib.QMC_QLOGEI, float(self.best_f), None, Z)
+            return acq.reshape(batch)
+        posterior = self.model.posterior(X, posterior_transform=self.posterior_transform)
+        samples = self.get_posterior_samples(posterior)
+        obj = self.objective(samples, X=X)
+        bf = self.best_f.to(obj).expand(obj.shape[:-1]) if self.best_f.numel() == 1 else self.best_f.to(obj)
+        acq = self._reduce(obj, bf)
+        return _ensemble_mean(self.model, acq)
+
+
+class qLogNoisyExpectedImprovement(qNoisyExpectedImprovement):
+    """MC batch log noisy expected improvement with the cached baseline root
+    (acquisition/logei.py:236-507): the qNEI samples (cached_cholesky.py,
+    utils/low_rank.py:85-173) under the LogEI reductions against the per-sample
+    baseline best.  Unlike qNEI, ``prune_baseline`` defaults to False
+    (logei.py:270).  Fused path: bo_qmc_finalize / bo_qmc_backward in
+    BO_QMC_QLOGNEI mode."""
+
+    _log = True
+    _fused_mode = _lib.QMC_QLOGNEI
+
+    def __init__(self, model, X_baseline, sampler=None, objective=None, posterior_transform=None,
+                 X_pending=None, constraints=None, eta=1e-3, fat: bool = True,
+                 prune_baseline: bool = False, cache_root: bool = True,
+                 tau_max: float = TAU_MAX, tau_relu: float = TAU_RELU, marginalize_dim=None):
+        if not cache_root:
+            raise UnsupportedError("qLogNEI here runs with the cached baseline root (cache_root=True)")
+        super().__init__(model, X_baseline, sampler=sampler, objective=objective,
+                         posterior_transform=posterior_transform, X_pending=X_pending,
+                         prune_baseline=prune_baseline, cache_root=cache_root,
+                         constraints=constraints, eta=eta, marginalize_dim=marginalize_dim)
+        self.tau_max = _check_tau(tau_max, "tau_max")
+        self.tau_relu = _check_tau(tau_relu, "tau_relu")
+        self._fat = fat
+        self._log_params = (int(bool(fat)), float(tau_relu), float(tau_max))
+
+    def compute_best_f(self, obj: torch.Tensor) -> torch.Tensor:
+        """logei.py:422-446: the cached per-sample baseline best."""
+        return self._baseline_best_f.view(-1, *([1] * (obj.ndim - 2))).to(obj)
 
 
 # -- qEHVI ---------------------------------------------------------------------------

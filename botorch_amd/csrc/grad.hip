@@ -14,6 +14,7 @@
 // The model caches carry no gradient (detach_test_caches, botorch/models/
 // utils/assorted.py:286-298), so nothing flows to L^{-1} or alpha.
 #include "common.h"
+#include "logred.h"
 
 namespace {
 
@@ -22,7 +23,7 @@ constexpr int DP = 8;
 constexpr int THREADS = 256;
 constexpr int SMAX = 4096;  // samples staged in LDS per pass (winner masks)
 
-enum { MODE_QEI = 1, MODE_QNEI = 2 };
+enum { MODE_QEI = 1, MODE_QNEI = 2, MODE_QLOGEI = 4, MODE_QLOGNEI = 5 };
 
 // dk(x_i, x_k)/dx_i (scaled coordinates), as a factor g with dk = g * (x_i - x_k).
 template <int KIND>
@@ -184,6 +185,92 @@ __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
           dl_acc = fma(w, Z[(int64_t)(s0 + s) * q + tj], dl_acc);
           if (tj == 0) dmu_acc += w;
         }
+      }
+    }
+    __syncthreads();
+  }
+  if (ta >= 0) {
+    dL[ta][tj] = (tj <= ta) ? dl_acc : 0.0;
+    if (tj == 0) dmean[(int64_t)b * q + ta] = dmu_acc;
+  }
+  chol_backward_lds(q, L, dL, Li, Pm, Tm, dcov + (int64_t)b * q * q, tid);
+}
+
+// Backward of the qLogEI / qLogNEI reduction (logred.h):  with u_s the q-reduced
+// smoothed log improvement of sample s and acq = logmeanexp_s u_s,
+//   d acq / d u_s = exp(u_s - acq) / S,
+//   w[s][a] = dacq * exp(u_s - acq) / S * du_s/dli_a * dli_a/dz_a   (z = f - best_f),
+// then d mu'_a = sum_s w[s][a],  dL[a][j] = sum_s w[s][a] Z[s][j]  (dense weights,
+// staged per sample chunk in LDS), and the q x q Cholesky backward as for qEI.
+// LOGNEI also returns dF[s][b*Qp + a] = w[s][a] (the cached-root baseline term).
+template <bool PERSAMPLE>
+__global__ __launch_bounds__(THREADS) void qmc_log_backward_kernel(
+    int q, const double* __restrict__ mean, const double* __restrict__ Lq,
+    const double* __restrict__ Z, int S, double best_f, const double* __restrict__ best_f_s,
+    const double* __restrict__ acq_fwd, LogRedParams lp, const double* __restrict__ dacq,
+    double* __restrict__ dmean, double* __restrict__ dcov, const double* __restrict__ F,
+    int64_t ldF, int Qp, double* __restrict__ dF) {
+  constexpr int SL = 512;  // samples per LDS chunk
+  __shared__ double L[QMAX][QMAX + 1];
+  __shared__ double Li[QMAX][QMAX + 1];
+  __shared__ double dL[QMAX][QMAX + 1];
+  __shared__ double Pm[QMAX][QMAX + 1];
+  __shared__ double Tm[QMAX][QMAX + 1];
+  __shared__ double mu[QMAX];
+  __shared__ double w[SL][QMAX + 1];
+
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (tid < q * q) {
+    const int a = tid / q, c = tid % q;
+    L[a][c] = Lq[((int64_t)b * q + a) * q + c];
+  }
+  if (tid < q) mu[tid] = mean[(int64_t)b * q + tid];
+  __syncthreads();
+  const double g = dacq[b] / (double)S;
+  const double a_fwd = acq_fwd[b];
+
+  double dmu_acc = 0.0, dl_acc = 0.0;
+  int ta = -1, tj = -1;
+  if (tid < q * q) {
+    ta = tid / q;
+    tj = tid % q;
+  }
+  for (int s0 = 0; s0 < S; s0 += SL) {
+    const int ns = min(SL, S - s0);
+    for (int s = tid; s < ns; s += THREADS) {
+      const double* z = Z + (int64_t)(s0 + s) * q;
+      const double bf = PERSAMPLE ? best_f_s[s0 + s] : best_f;
+      const double* Fs = PERSAMPLE ? F + (int64_t)(s0 + s) * ldF + (int64_t)b * Qp : nullptr;
+      double li[QMAX], dli[QMAX], gq[QMAX];
+#pragma unroll
+      for (int a = 0; a < QMAX; ++a) {
+        li[a] = 0.0;
+        dli[a] = 0.0;
+        if (a < q) {
+          double f = mu[a];
+          if (PERSAMPLE) f += Fs[a];
+          for (int j = 0; j <= a; ++j) f = fma(L[a][j], z[j], f);
+          li[a] = log_soft_relu(f - bf, lp, &dli[a]);
+        }
+      }
+      const double u = log_q_reduce<QMAX>(li, q, lp, &gq);
+      const double ws = g * exp(u - a_fwd);
+#pragma unroll
+      for (int a = 0; a < QMAX; ++a) {
+        if (a < q) {
+          const double v = ws * gq[a] * dli[a];
+          w[s][a] = v;
+          if (PERSAMPLE) dF[(int64_t)(s0 + s) * ldF + (int64_t)b * Qp + a] = v;
+        }
+      }
+    }
+    __syncthreads();
+    if (ta >= 0 && tj <= ta) {
+      for (int s = 0; s < ns; ++s) {
+        const double v = w[s][ta];
+        dl_acc = fma(v, Z[(int64_t)(s0 + s) * q + tj], dl_acc);
+        if (tj == 0) dmu_acc += v;
       }
     }
     __syncthreads();
@@ -360,19 +447,31 @@ extern "C" int bo_kernel_grad(int kind, const double* X, int64_t rows, const dou
 extern "C" int bo_qmc_backward(int mode, int B, int q, const double* mean, const double* Lq,
                                const double* Z, int S, double best_f, const double* best_f_s,
                                const double* F, int64_t ldF, const double* dacq, double* dmean,
-                               double* dcov, double* dF, void* stream) {
+                               double* dcov, double* dF, const double* acq_fwd, int fat,
+                               double tau_relu, double tau_max, void* stream) {
   BO_CHECK_ARG(q >= 1 && q <= QMAX, "bo_qmc_backward: q=%d out of range", q);
-  BO_CHECK_ARG(mode == MODE_QEI || mode == MODE_QNEI, "bo_qmc_backward: bad mode %d", mode);
-  BO_CHECK_ARG(mode == MODE_QEI || (best_f_s && F && dF), "bo_qmc_backward: qNEI needs best_f_s, F, dF");
+  BO_CHECK_ARG(mode == MODE_QEI || mode == MODE_QNEI || mode == MODE_QLOGEI || mode == MODE_QLOGNEI,
+               "bo_qmc_backward: bad mode %d", mode);
+  const bool per_sample = mode == MODE_QNEI || mode == MODE_QLOGNEI;
+  const bool logm = mode == MODE_QLOGEI || mode == MODE_QLOGNEI;
+  BO_CHECK_ARG(!per_sample || (best_f_s && F && dF),
+               "bo_qmc_backward: qNEI / qLogNEI need best_f_s, F, dF");
+  BO_CHECK_ARG(!logm || (acq_fwd && tau_relu > 0.0 && tau_max > 0.0),
+               "bo_qmc_backward: log modes need the forward values and positive temperatures");
   if (B == 0) return BO_OK;
   int Qp = 1;
   while (Qp < q) Qp *= 2;
-  BO_CHECK_ARG(mode == MODE_QEI || ldF >= (int64_t)B * Qp, "bo_qmc_backward: ldF too small");
+  BO_CHECK_ARG(!per_sample || ldF >= (int64_t)B * Qp, "bo_qmc_backward: ldF too small");
   hipStream_t st = as_stream(stream);
+  const LogRedParams lp{tau_relu, tau_max, fat};
   if (mode == MODE_QEI)
     qmc_backward_kernel<MODE_QEI><<<B, THREADS, 0, st>>>(q, mean, Lq, Z, S, best_f, best_f_s, dacq, dmean, dcov, nullptr, 0, Qp, nullptr);
-  else
+  else if (mode == MODE_QNEI)
     qmc_backward_kernel<MODE_QNEI><<<B, THREADS, 0, st>>>(q, mean, Lq, Z, S, best_f, best_f_s, dacq, dmean, dcov, F, ldF, Qp, dF);
+  else if (mode == MODE_QLOGEI)
+    qmc_log_backward_kernel<false><<<B, THREADS, 0, st>>>(q, mean, Lq, Z, S, best_f, best_f_s, acq_fwd, lp, dacq, dmean, dcov, nullptr, 0, Qp, nullptr);
+  else
+    qmc_log_backward_kernel<true><<<B, THREADS, 0, st>>>(q, mean, Lq, Z, S, best_f, best_f_s, acq_fwd, lp, dacq, dmean, dcov, F, ldF, Qp, dF);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

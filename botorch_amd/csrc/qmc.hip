@@ -13,8 +13,12 @@
 //      and the acquisition reduction:
 //        qEI  : mean_s max_a relu(f - best_f)           (acquisition/monte_carlo.py:405-414)
 //        qNEI : mean_s max_a relu(f - best_f[s])        (:580-589, cached baseline best)
-//      q-max and the sample sum are wavefront shuffle reductions.
+//        qLogEI / qLogNEI : logmeanexp_s fatmax_a log_fatplus(f - best_f(s))
+//                           (acquisition/logei.py:122, 219-234, 347-362; logred.h)
+//      q-max and the sample sum are wavefront shuffle reductions (an online
+//      (max, sum-exp) pair for logmeanexp).
 #include "common.h"
+#include "logred.h"
 
 namespace {
 
@@ -22,7 +26,21 @@ constexpr int QMAX = 16;
 constexpr int DP = 8;
 constexpr int THREADS = 256;
 
-enum QmcMode : int { QMC_POSTERIOR = 0, QMC_QEI = 1, QMC_QNEI = 2, QMC_CHOL = 3 };
+enum QmcMode : int {
+  QMC_POSTERIOR = 0,
+  QMC_QEI = 1,
+  QMC_QNEI = 2,
+  QMC_CHOL = 3,
+  QMC_QLOGEI = 4,
+  QMC_QLOGNEI = 5
+};
+
+__host__ __device__ constexpr bool per_sample_best(int mode) {
+  return mode == QMC_QNEI || mode == QMC_QLOGNEI;
+}
+__host__ __device__ constexpr bool log_mode(int mode) {
+  return mode == QMC_QLOGEI || mode == QMC_QLOGNEI;
+}
 
 template <int KIND, int MODE>
 __global__ __launch_bounds__(THREADS) void qmc_kernel(
@@ -33,7 +51,7 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     double* __restrict__ acq, double* __restrict__ mean_out, double* __restrict__ cov_out,
     double* __restrict__ L_out, int* __restrict__ info_out, double* __restrict__ jitter_out,
     const double* __restrict__ Tm, int r, int64_t ldT, const double* __restrict__ F,
-    int64_t ldF) {
+    int64_t ldF, LogRedParams lp) {
   // qNEI with the cached baseline root (utils/low_rank.py:85-173): Tm (r x ldT)
   // holds bl_chol^T = L_rr^{-1} Sigma'(X_base, X) per padded test row and F
   // (S x ldF) the samples' baseline term Z_base T; then
@@ -42,6 +60,7 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   __shared__ double Lq[QMAX][QMAX + 1];
   __shared__ double mu[QMAX];
   __shared__ double red[THREADS / 64];
+  __shared__ double red2[THREADS / 64];
   __shared__ int s_info;
   __shared__ double s_jit;
 
@@ -151,23 +170,45 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
 
   // 3. samples and the reduction.
   double sum = 0.0;
+  LseAcc lse{-INFINITY, 0.0};
   for (int s = tid; s < S; s += THREADS) {
     const double* z = Z + (int64_t)s * q;
     double zs[QMAX];
 #pragma unroll
     for (int j = 0; j < QMAX; ++j) zs[j] = (j < q) ? z[j] : 0.0;
-    const double bf = (MODE == QMC_QNEI) ? best_f_s[s] : best_f;
+    const double bf = per_sample_best(MODE) ? best_f_s[s] : best_f;
     double vmax = 0.0;
+    double li[QMAX];
 #pragma unroll
     for (int a = 0; a < QMAX; ++a) {
+      li[a] = 0.0;
       if (a < q) {
         double f = mu[a] + ((F != nullptr) ? F[(int64_t)s * ldF + row0 + a] : 0.0);
 #pragma unroll
         for (int j = 0; j <= a; ++j) f = fma(Lq[a][j], zs[j], f);
-        vmax = fmax(vmax, f - bf);
+        if (log_mode(MODE)) li[a] = log_soft_relu(f - bf, lp, nullptr);
+        else vmax = fmax(vmax, f - bf);
       }
     }
-    sum += vmax;
+    if (log_mode(MODE)) lse = lse_push(lse, log_q_reduce<QMAX>(li, q, lp, nullptr));
+    else sum += vmax;
+  }
+  if (log_mode(MODE)) {
+    for (int o = 32; o > 0; o >>= 1) {
+      LseAcc other{__shfl_xor(lse.m, o), __shfl_xor(lse.s, o)};
+      lse = lse_merge(lse, other);
+    }
+    if ((tid & 63) == 0) {
+      red[tid >> 6] = lse.m;
+      red2[tid >> 6] = lse.s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      LseAcc t{-INFINITY, 0.0};
+      for (int w = 0; w < THREADS / 64; ++w) t = lse_merge(t, LseAcc{red[w], red2[w]});
+      acq[b] = t.m + log(t.s) - log((double)S);
+    }
+    return;
   }
   for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
   if ((tid & 63) == 0) red[tid >> 6] = sum;
@@ -198,6 +239,7 @@ struct QmcArgs {
   int64_t ldT;
   const double* F;
   int64_t ldF;
+  LogRedParams lp;
 };
 
 template <int KIND, int MODE>
@@ -205,7 +247,7 @@ void launch_mode(int B, const QmcArgs& a, hipStream_t st) {
   qmc_kernel<KIND, MODE><<<B, THREADS, 0, st>>>(
       a.q, a.Qp, a.Xq, a.Spart, a.mpart, a.nC, a.nrows_pad, a.outputscale, a.constant, a.ymean,
       a.ystd, a.Z, a.S, a.best_f, a.best_f_s, a.max_tries, a.jitter0, a.acq, a.mean_out,
-      a.cov_out, a.L_out, a.info_out, a.jitter_out, a.Tm, a.r, a.ldT, a.F, a.ldF);
+      a.cov_out, a.L_out, a.info_out, a.jitter_out, a.Tm, a.r, a.ldT, a.F, a.ldF, a.lp);
 }
 
 template <int KIND>
@@ -213,6 +255,8 @@ void launch_qmc(int mode, int B, const QmcArgs& a, hipStream_t st) {
   if (mode == QMC_POSTERIOR) launch_mode<KIND, QMC_POSTERIOR>(B, a, st);
   else if (mode == QMC_QEI) launch_mode<KIND, QMC_QEI>(B, a, st);
   else if (mode == QMC_QNEI) launch_mode<KIND, QMC_QNEI>(B, a, st);
+  else if (mode == QMC_QLOGEI) launch_mode<KIND, QMC_QLOGEI>(B, a, st);
+  else if (mode == QMC_QLOGNEI) launch_mode<KIND, QMC_QLOGNEI>(B, a, st);
   else launch_mode<KIND, QMC_CHOL>(B, a, st);
 }
 
@@ -227,11 +271,15 @@ extern "C" int bo_qmc_finalize(int kind, int mode, int B, int q, const double* X
                                int max_tries, double jitter0, double* acq, double* mean_out,
                                double* cov_out, double* L_out, int* info_out,
                                double* jitter_out, const double* Tm, int r, int64_t ldT,
-                               const double* F, int64_t ldF, void* stream) {
-  BO_CHECK_ARG(mode >= 0 && mode <= 3, "bo_qmc_finalize: bad mode %d", mode);
+                               const double* F, int64_t ldF, int fat, double tau_relu,
+                               double tau_max, void* stream) {
+  BO_CHECK_ARG(mode >= 0 && mode <= 5, "bo_qmc_finalize: bad mode %d", mode);
+  BO_CHECK_ARG(!log_mode(mode) || (tau_relu > 0.0 && tau_max > 0.0),
+               "bo_qmc_finalize: tau_relu and tau_max must be positive");
   BO_CHECK_ARG(mode == QMC_POSTERIOR || mode == QMC_CHOL || (acq && Z && S > 0),
                "bo_qmc_finalize: missing MC args");
-  BO_CHECK_ARG(mode != QMC_QNEI || best_f_s, "bo_qmc_finalize: qNEI needs per-sample best_f");
+  BO_CHECK_ARG(!per_sample_best(mode) || best_f_s,
+               "bo_qmc_finalize: qNEI / qLogNEI need per-sample best_f");
   BO_CHECK_ARG((Tm == nullptr) == (F == nullptr) && (Tm == nullptr || r > 0),
                "bo_qmc_finalize: cached-root qNEI needs both T and F");
   int Qp, nrows_pad, nC;
@@ -241,7 +289,7 @@ extern "C" int bo_qmc_finalize(int kind, int mode, int B, int q, const double* X
   QmcArgs a{q,      Qp,     Xq,       Spart,     mpart,     nC,      nrows_pad, outputscale,
             constant, ymean, ystd,   Z,        S,         best_f,  best_f_s,  max_tries,
             jitter0, acq,    mean_out, cov_out,  L_out,     info_out, jitter_out, Tm,
-            r,       ldT,    F,        ldF};
+            r,       ldT,    F,        ldF,      LogRedParams{tau_relu, tau_max, fat}};
   hipStream_t st = as_stream(stream);
   if (kind == BO_RBF) launch_qmc<BO_RBF>(mode, B, a, st);
   else launch_qmc<BO_MATERN52>(mode, B, a, st);

@@ -210,14 +210,17 @@ def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd
                  Z: Optional[torch.Tensor] = None, best_f: float = 0.0,
                  best_f_s: Optional[torch.Tensor] = None, want_mean=True, want_cov=True,
                  want_L=False, max_tries=CHOLESKY_MAX_TRIES, jitter0=CHOLESKY_JITTER_F64,
-                 T: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None):
+                 T: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,
+                 log_params: Optional[tuple] = None):
+    """log_params = (fat, tau_relu, tau_max) for the qLogEI / qLogNEI modes."""
     dev = pp.Xq.device
     B, q = pp.B, pp.q
     f64 = dict(dtype=torch.float64, device=dev)
     mean = torch.empty(B, q, **f64) if want_mean else None
     cov = torch.empty(B, q, q, **f64) if want_cov else None
     L = torch.empty(B, q, q, **f64) if want_L else None
-    need_mc = mode in (_lib.QMC_QEI, _lib.QMC_QNEI)
+    need_mc = mode in (_lib.QMC_QEI, _lib.QMC_QNEI) + _lib.LOG_MODES
+    fat, tau_relu, tau_max = log_params if log_params is not None else (1, 1.0, 1.0)
     acq = torch.empty(B, **f64) if need_mc else None
     info = torch.empty(B, dtype=torch.int32, device=dev) if mode != _lib.QMC_POSTERIOR else None
     jit = torch.empty(B, **f64) if mode != _lib.QMC_POSTERIOR else None
@@ -230,7 +233,8 @@ def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd
                                 jitter0, _p(acq), _p(mean), _p(cov), _p(L), _p(info), _p(jit),
                                 _p(T), T.shape[0] if T is not None else 0,
                                 T.shape[1] if T is not None else 0, _p(F),
-                                F.shape[1] if F is not None else 0, _stream(dev)), "qmc_finalize")
+                                F.shape[1] if F is not None else 0, int(bool(fat)),
+                                float(tau_relu), float(tau_max), _stream(dev)), "qmc_finalize")
     return dict(acq=acq, mean=mean, cov=cov, L=L, info=info, jitter=jit)
 
 
@@ -275,19 +279,25 @@ def w_matrix(cache: GPCache, pp: PostPartials) -> torch.Tensor:
 
 def qmc_backward(mode: int, mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor,
                  dacq: torch.Tensor, best_f: float = 0.0,
-                 best_f_s: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None):
+                 best_f_s: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,
+                 acq_fwd: Optional[torch.Tensor] = None, log_params: Optional[tuple] = None):
     """dacq -> (dmean, dcov[, dF]).  qNEI passes F = Z_base T (S x nrows_pad) and
-    gets its cotangent dF back as a third output."""
+    gets its cotangent dF back as a third output.  The log modes also take the
+    forward values acq_fwd and log_params = (fat, tau_relu, tau_max)."""
     dev = mean.device
     B, q = mean.shape
     S = Z.shape[0]
     dmean = torch.empty(B, q, dtype=torch.float64, device=dev)
     dcov = torch.empty(B, q, q, dtype=torch.float64, device=dev)
     dF = torch.zeros_like(F) if F is not None else None
+    fat, tau_relu, tau_max = log_params if log_params is not None else (1, 1.0, 1.0)
+    if acq_fwd is not None:
+        acq_fwd = acq_fwd.contiguous()
     check(lib().bo_qmc_backward(mode, B, q, _p(mean), _p(L), _p(Z.reshape(S, q).contiguous()), S,
                                 float(best_f), _p(best_f_s), _p(F),
                                 F.shape[1] if F is not None else 0, _p(dacq.contiguous()),
-                                _p(dmean), _p(dcov), _p(dF), _stream(dev)), "qmc_backward")
+                                _p(dmean), _p(dcov), _p(dF), _p(acq_fwd), int(bool(fat)),
+                                float(tau_relu), float(tau_max), _stream(dev)), "qmc_backward")
     if F is not None:
         return dmean, dcov, dF
     return dmean, dcov

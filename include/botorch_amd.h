@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 2
+#define BO_ABI_VERSION 3
 
 /* status codes */
 #define BO_OK 0
@@ -49,6 +49,8 @@ extern "C" {
 #define BO_QMC_QEI 1
 #define BO_QMC_QNEI 2
 #define BO_QMC_CHOL 3 /* finalise + jittered q x q Cholesky only (no MC) */
+#define BO_QMC_QLOGEI 4  /* qLogExpectedImprovement (acquisition/logei.py:137-234) */
+#define BO_QMC_QLOGNEI 5 /* qLogNoisyExpectedImprovement, cached root (logei.py:236-507) */
 
 const char* bo_last_error(void);
 int bo_version(void);
@@ -173,6 +175,12 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
  *   L_out (B x q x q), info_out (B), jitter_out (B)  [posteriors/gpytorch.py:85-126]
  *   acq (B): qEI  mean_s max_a relu(f - best_f)      [acquisition/monte_carlo.py:405-414]
  *            qNEI mean_s max_a relu(f - best_f_s[s])  [acquisition/monte_carlo.py:580-589]
+ *            qLogEI / qLogNEI (best_f / best_f_s[s]):
+ *              logmeanexp_s fatmax_a log_fatplus(f - best_f, tau_relu)   (fat != 0)
+ *              logmeanexp_s smooth_amax_a log_softplus(f - best_f, tau_relu) (fat == 0)
+ *              with the q-reduction at temperature tau_max
+ *              [acquisition/logei.py:122, 219-234, 347-362, 509-534;
+ *               utils/safe_math.py:209-352]; fat/tau_* are ignored by other modes
  * Z: S x q base samples (SobolQMCNormalSampler, sampling/normal.py:178-209).
  * Output pointers may be NULL when not needed (acq required for QEI/QNEI).
  * Cached-root qNEI (utils/low_rank.py:85-173, acquisition/cached_cholesky.py):
@@ -185,7 +193,7 @@ int bo_qmc_finalize(int kind, int mode, int B, int q, const double* Xq, const do
                     const double* best_f_s, int max_tries, double jitter0, double* acq,
                     double* mean_out, double* cov_out, double* L_out, int* info_out,
                     double* jitter_out, const double* Tm, int r, int64_t ldT, const double* F,
-                    int64_t ldF, void* stream);
+                    int64_t ldF, int fat, double tau_relu, double tau_max, void* stream);
 
 /* Backward of the MC reduction + q x q Cholesky (gen_candidates_scipy's
  * autograd.grad, botorch/generation/gen.py:194-222):
@@ -196,11 +204,14 @@ int bo_qmc_finalize(int kind, int mode, int B, int q, const double* Xq, const do
  * qNEI (cached root, utils/low_rank.py:85-173): the forward samples include
  * F = Z_base T (S x ldF, rows b*Qp + a, as passed to bo_qmc_finalize); dF (same
  * layout) receives its cotangent, from which dT = Z_base^T dF.  F/dF may be
- * NULL for qEI. */
+ * NULL for qEI.  Log modes (BO_QMC_QLOGEI / BO_QMC_QLOGNEI) also take the
+ * forward values acq_fwd (B) and the forward's fat / tau_relu / tau_max; their
+ * weights are dense over (sample, q) rather than one-hot. */
 int bo_qmc_backward(int mode, int B, int q, const double* mean, const double* Lq,
                     const double* Z, int S, double best_f, const double* best_f_s,
                     const double* F, int64_t ldF, const double* dacq, double* dmean,
-                    double* dcov, double* dF, void* stream);
+                    double* dcov, double* dF, const double* acq_fwd, int fat, double tau_relu,
+                    double tau_max, void* stream);
 
 /* Backward of the batched exact posterior w.r.t. the candidates X (B x q x d):
  *   dK*x = ystd dmean alpha^T - G W,  G = ystd^2 (dcov + dcov^T),

@@ -111,6 +111,74 @@ class QNEIOracle:
         return (f - self.best_f.view(-1, 1, 1)).clamp_min(0).amax(dim=-1).mean(dim=0)
 
 
+# -- LogEI family (acquisition/logei.py; utils/safe_math.py) -------------------------
+TAU_RELU = 1e-6  # logei.py:66
+TAU_MAX = 1e-2   # logei.py:67
+
+
+def _softplus(x):
+    """torch.nn.functional.softplus(x), beta = 1, threshold = 20."""
+    return torch.where(x > 20, x, torch.log1p(torch.exp(x.clamp_max(20))))
+
+
+def log_fatplus(z, tau):
+    """safe_math.py:293-320: log(tau (softplus(z/tau) + 0.1 / (1 + (z/tau)^2)))."""
+    x = z / tau
+    return torch.log(tau * (_softplus(x) + 0.1 / (1 + x * x)))
+
+
+def log_softplus(z, tau):
+    """safe_math.py:226-247 (fp64: below z/tau = -35 the asymptote z/tau + log tau;
+    above z/tau = 32 softplus is the identity)."""
+    x = z / tau
+    lo = x <= -35
+    hi = x > 32
+    mid = torch.log(tau * torch.log1p(torch.exp(x.clamp(-35, 32))))
+    return torch.where(lo, x + math.log(tau), torch.where(hi, torch.log(z.abs().clamp_min(1e-300)), mid))
+
+
+def fatmax(x, tau, dim=-1):
+    """safe_math.py:323-352 with alpha = 2 (_pareto at :454-478 reduces to
+    2 / (2 + 2y + y^2)), anchored at the maximum as _inf_max_helper (:149-187)."""
+    M = x.amax(dim=dim, keepdim=True)
+    y = (M - x) / tau
+    return (M + tau * torch.log((2.0 / (2.0 + 2.0 * y + y * y)).sum(dim=dim, keepdim=True))).squeeze(dim)
+
+
+def smooth_amax(x, tau, dim=-1):
+    """safe_math.py:250-273: tau logsumexp(x / tau)."""
+    return tau * torch.logsumexp(x / tau, dim=dim)
+
+
+def logmeanexp(x, dim=0):
+    """safe_math.py:209-223."""
+    return torch.logsumexp(x, dim=dim) - math.log(x.shape[dim])
+
+
+def qlogei_from_samples(samples, best_f, fat=True, tau_relu=TAU_RELU, tau_max=TAU_MAX):
+    """qLogExpectedImprovement / qLogNEI reduction of S x b x q samples;
+    best_f is a scalar or per-sample (S) tensor (logei.py:122, 219-234, 509-534)."""
+    bf = torch.as_tensor(best_f, dtype=samples.dtype)
+    if bf.ndim == 1:
+        bf = bf.view(-1, *([1] * (samples.ndim - 1)))
+    z = samples - bf
+    li = log_fatplus(z, tau_relu) if fat else log_softplus(z, tau_relu)
+    u = fatmax(li, tau_max) if fat else smooth_amax(li, tau_max)
+    return logmeanexp(u, dim=0)
+
+
+def qlogei(model: ExactGPOracle, X, Z, best_f, **kw):
+    """qLogExpectedImprovement.forward on an exact GP."""
+    mean, cov = model.posterior(X)
+    return qlogei_from_samples(mc_samples(mean, cov, Z), best_f, **kw)
+
+
+def qlognei(oracle: "QNEIOracle", X, **kw):
+    """qLogNoisyExpectedImprovement (cache_root=True, logei.py:236-507): the
+    cached-root qNEI samples against the per-sample baseline best."""
+    return qlogei_from_samples(oracle.samples(X), oracle.best_f, **kw)
+
+
 # -- qEHVI -----------------------------------------------------------------------
 def qehvi_from_samples(obj, cell_lower, cell_upper):
     """qExpectedHypervolumeImprovement._compute_qehvi (multi_objective/

@@ -17,3 +17,12 @@ SOBOL_BOX_CASES = [  # (n, q, d, seed)
     (64, 8, 6, 1),
     (32, 16, 6, 1),
 ]
+
+# LogEI reduction cases: tag -> (fat, tau_relu, tau_max); the first is the
+# reference default (acquisition/logei.py:66-67, fat=True).
+LOGEI_CASES = {
+    "default": (True, 1e-6, 1e-2),
+    "nofat": (False, 1e-6, 1e-2),
+    "fat_wide": (True, 0.1, 0.5),
+    "nofat_wide": (False, 0.1, 0.5),
+}

@@ -17,6 +17,9 @@ Sources (reference file:line):
   * NondominatedPartitioning / FastNondominatedPartitioning
                                botorch/utils/multi_objective/box_decompositions/non_dominated.py
   * is_non_dominated           botorch/utils/multi_objective/pareto.py:16-64
+  * log_fatplus / log_softplus / fatmax / smooth_amax / logmeanexp
+                               botorch/utils/safe_math.py:209-352, composed as
+                               acquisition/logei.py:122, 219-234, 509-534
 """
 import os
 import sys
@@ -28,7 +31,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import _refload  # noqa: E402
 
-from cases import SOBOL_BOX_CASES, SOBOL_NORMAL_CASES  # noqa: E402
+from cases import LOGEI_CASES, SOBOL_BOX_CASES, SOBOL_NORMAL_CASES  # noqa: E402
 
 
 def main():
@@ -111,6 +114,24 @@ def main():
     out["ndtr_x"] = x.numpy()
     out["ndtr_y"] = prob.ndtr(x).numpy()
     out["phi_y"] = prob.phi(x).numpy()
+
+    # LogEI reductions (values and gradients w.r.t. the samples).
+    sm = _refload.load("botorch.utils.safe_math")
+    g = torch.Generator().manual_seed(11)
+    obj = 0.3 * torch.randn(64, 5, 4, generator=g, dtype=torch.double)
+    bf_s = 0.2 + 0.1 * torch.randn(64, generator=g, dtype=torch.double)
+    out["logei_obj"] = obj.numpy()
+    out["logei_best_f_s"] = bf_s.numpy()
+    for tag, (fat, tau_relu, tau_max) in LOGEI_CASES.items():
+        for bname, bf in (("scalar", torch.full((64,), 0.2, dtype=torch.double)), ("persample", bf_s)):
+            x = obj.clone().requires_grad_(True)
+            z = x - bf.view(-1, 1, 1)
+            li = (sm.log_fatplus if fat else sm.log_softplus)(z, tau=tau_relu)
+            u = (sm.fatmax if fat else sm.smooth_amax)(li, dim=-1, tau=tau_max)
+            acq = sm.logmeanexp(u, dim=0)
+            (gx,) = torch.autograd.grad(acq.sum(), x)
+            out[f"logei_{tag}_{bname}_acq"] = acq.detach().numpy()
+            out[f"logei_{tag}_{bname}_grad"] = gx.numpy()
 
     path = os.path.join(HERE, "golden.npz")
     np.savez_compressed(path, **out)

@@ -17,8 +17,9 @@ step() {  # name timeout cmd...
 for s in "$@"; do
   case $s in
     build) step build 600 make -j16 ;;
-    test) step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
-    testx) step pytest_gpu 1200 python -m pytest tests -m gpu -q -x -rf ;;
+    test) step pytest_gpu 1200 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
+    testx) step pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x -rf --timeout 120 --timeout-method thread ;;
+    testlog) step pytest_logei 600 python -u -m pytest tests/test_gpu_logei.py -q -rf --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     bench_short) step bench 600 python bench.py --steps 10 --warmup 2 ;;
