@@ -258,6 +258,31 @@ def other_configs(dev, cpu=True):
         tc, runs = _cpu_time(lambda: oacq.qlogei(orc, Xc[:bs], Z, best))
         e.update(cpu_evals_per_s=q * S * bs / tc, cpu_sample=f"{bs} of {b} restarts, median of {runs}")
     out["C3_qLogEI"] = e
+
+    # Section 8(f) rank 2: raw-sample initialisation of optimize_acqf at C3 scale
+    # (2048 raw q=16 designs, 512 restarts, init_batch_limit 512): on-device
+    # Sobol designs + chunked forward + Boltzmann selection, against the
+    # reference's protocol (host Sobol draw, per-chunk .cpu(), host selection).
+    from botorch_amd.optim import (gen_batch_initial_conditions, initialize_q_batch_nonneg)
+    from botorch_amd.utils_sampling import draw_sobol_samples as host_sobol
+    acq_ei = qExpectedImprovement(m, best - 0.3, sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
+    bounds_d = unit(6).to(dev)
+    raw = 2048
+    opts = {"seed": 0, "init_batch_limit": 512}
+    t_dev = _gpu_time(lambda: gen_batch_initial_conditions(acq_ei, bounds_d, q, b, raw, options=opts),
+                      steps=5, warmup=1)
+
+    def host_protocol():
+        Xr = host_sobol(unit(6), raw, q, seed=0)
+        with torch.no_grad():
+            Yr = torch.cat([acq_ei(Xr[i:i + 512].to(dev)).cpu() for i in range(0, raw, 512)])
+        return initialize_q_batch_nonneg(Xr, Yr, b).to(dev)
+
+    t_host = _gpu_time(host_protocol, steps=5, warmup=1)
+    out["C3_init"] = {"config": "C3 gen_batch_initial_conditions: qEI, 2048 raw x q=16, 512 restarts, "
+                                "S=512, init_batch_limit=512",
+                      "device_ms": 1e3 * t_dev, "host_roundtrip_ms": 1e3 * t_host,
+                      "raw_evals_per_s": raw * q * S / t_dev}
     acqf = qLogNoisyExpectedImprovement(m, X.to(dev), sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0),
                                         prune_baseline=True)
     with torch.no_grad():

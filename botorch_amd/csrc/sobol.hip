@@ -110,7 +110,45 @@ __global__ void sobol_normal_kernel(const int64_t* __restrict__ state,
   out[idx] = erfinv_accurate(__dsub_rn(__dmul_rn(2.0, vv), 1.0)) * 1.4142135623730951;
 }
 
+// Box-scaled raw designs: out[i][j] = lower[j % d] + range[j % d] * u_i[j]
+// (draw_sobol_samples, botorch/utils/sampling.py:66-105: engine over q*d
+// dimensions, draw(n, dtype=double), then lower + rng * raw -- product and sum
+// rounded separately, as torch evaluates them).
+__global__ void sobol_box_kernel(const int64_t* __restrict__ state,
+                                 const int64_t* __restrict__ shift, int dim, int64_t n,
+                                 int64_t skip, int first_f32, const double* __restrict__ lower,
+                                 const double* __restrict__ range, int d,
+                                 double* __restrict__ out) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * dim) return;
+  const int64_t i = idx / dim + skip;
+  const int j = (int)(idx % dim);
+  const uint64_t g = (uint64_t)i ^ ((uint64_t)i >> 1);
+  int64_t v = shift[j];
+  const int64_t* sj = state + (int64_t)j * MAXBIT;
+#pragma unroll
+  for (int b = 0; b < MAXBIT; ++b)
+    if ((g >> b) & 1ull) v ^= sj[b];
+  const double u = (i == 0 && first_f32) ? (double)((float)v) * (1.0 / 1073741824.0)
+                                         : (double)v * (1.0 / 1073741824.0);
+  const int t = j % d;
+  out[idx] = __dadd_rn(lower[t], __dmul_rn(range[t], u));
+}
+
 }  // namespace
+
+extern "C" int bo_sobol_box(const int64_t* state, const int64_t* shift, int dim, int64_t n,
+                            int64_t skip, int first_f32, const double* lower, const double* range,
+                            int d, double* out, void* stream) {
+  BO_CHECK_ARG(dim > 0 && n >= 0 && skip >= 0 && d > 0 && dim % d == 0,
+               "bo_sobol_box: bad shape (dim %d, d %d)", dim, d);
+  const int64_t tot = n * dim;
+  if (tot == 0) return BO_OK;
+  sobol_box_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, as_stream(stream)>>>(
+      state, shift, dim, n, skip, first_f32, lower, range, d, out);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
 
 extern "C" int bo_sobol_normal(const int64_t* state, const int64_t* shift, int dim, int64_t n,
                                int64_t skip, int first_f32, double* out, void* stream) {

@@ -6,6 +6,7 @@ must be fp64 tensors on a ROCm device, and a missing library raises.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import math
 from dataclasses import dataclass
@@ -26,8 +27,19 @@ CHOLESKY_JITTER_F64 = 1e-8  # [G] linear_operator.settings.cholesky_jitter (doub
 TIMING_HOOK = None
 
 
+# Tensors whose pointers were handed to the C ABI most recently.  A call such as
+# lib().bo_x(_p(a.contiguous()), _p(b.to(dev))) would otherwise drop each
+# temporary as soon as _p returns -- before the launch is enqueued -- and the
+# caching allocator could hand the same block to the next temporary of the same
+# argument list.  Holding the last few references spans any one call.
+_KEEPALIVE = collections.deque(maxlen=64)
+
+
 def _p(t: Optional[torch.Tensor]):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+    if t is None:
+        return ctypes.c_void_p(0)
+    _KEEPALIVE.append(t)
+    return ctypes.c_void_p(t.data_ptr())
 
 
 def _stream(device: torch.device):
@@ -254,6 +266,22 @@ def sobol_normal(dim: int, n: int, seed: int, device, skip: int = 0) -> torch.Te
     first_f32 = int(torch.get_default_dtype() == torch.float32)
     check(lib().bo_sobol_normal(_p(state), _p(shift), dim, n, skip, first_f32, _p(out),
                                 _stream(torch.device(device))), "sobol_normal")
+    return out
+
+
+def sobol_box(bounds: torch.Tensor, n: int, q: int, seed: Optional[int]) -> torch.Tensor:
+    """n x q x d scrambled-Sobol raw designs in the box ``bounds`` (2 x d, on the
+    device), bit-identical to draw_sobol_samples (botorch/utils/sampling.py:66-105)."""
+    dev = bounds.device
+    d = bounds.shape[-1]
+    state, shift = sobol_engine_state(q * d, seed)
+    state, shift = state.to(dev), shift.to(dev)  # keep alive across the launch
+    lower = bounds[0].to(torch.float64).contiguous()
+    rng = (bounds[1] - bounds[0]).to(torch.float64).contiguous()
+    out = torch.empty(n, q, d, dtype=torch.float64, device=dev)
+    first_f32 = int(torch.get_default_dtype() == torch.float32)
+    check(lib().bo_sobol_box(_p(state), _p(shift), q * d, n, 0, first_f32,
+                             _p(lower), _p(rng), d, _p(out), _stream(dev)), "sobol_box")
     return out
 
 

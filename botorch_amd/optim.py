@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import time
 import warnings
+from contextlib import contextmanager
 from typing import Any, Callable, Dict, Optional, Tuple
 
 import numpy as np
@@ -45,7 +46,7 @@ def columnwise_clamp(X, lower=None, upper=None, raise_on_violation=False):
 
 
 def initialize_q_batch_nonneg(X, Y, n, eta=1.0, alpha=1e-4):
-    """optim/initializers.py:968-1037."""
+    """optim/initializers.py:1041-1112 (device-agnostic: runs where X and Y live)."""
     n_samples = X.shape[0]
     if n > n_samples:
         raise RuntimeError("n cannot be larger than the number of provided samples")
@@ -75,64 +76,154 @@ def initialize_q_batch_nonneg(X, Y, n, eta=1.0, alpha=1e-4):
     return X[idcs]
 
 
+def _batched_multinomial(weights, num_samples):
+    """utils/sampling.py batched_multinomial: one multinomial per leading row."""
+    flat = weights.reshape(-1, weights.shape[-1])
+    out = torch.multinomial(flat, num_samples)
+    return out.view(*weights.shape[:-1], num_samples)
+
+
 def initialize_q_batch(X, Y, n, eta=1.0):
-    """optim/initializers.py (Boltzmann sampling on standardized values)."""
+    """optim/initializers.py:968-1038: Boltzmann sampling on the standardized
+    values, per batch_shape entry (X: b x batch_shape x q x d, Y: b x batch_shape)."""
     n_samples = X.shape[0]
+    batch_shape = X.shape[1:-2] or torch.Size()
     if n > n_samples:
-        raise RuntimeError("n cannot be larger than the number of provided samples")
+        raise RuntimeError(f"n ({n}) cannot be larger than the number of provided samples ({n_samples})")
     elif n == n_samples:
         return X
-    Ystd = Y.std()
-    if Ystd == 0:
+    Ystd = Y.std(dim=0)
+    if torch.any(Ystd == 0):
         warnings.warn("All acquisition values for raw samples points are the same for "
                       "at least one batch. Choosing initial conditions at random.",
                       BadInitialCandidatesWarning)
         return X[torch.randperm(n=n_samples, device=X.device)][:n]
     max_val, max_idx = torch.max(Y, dim=0)
-    Z = (Y - Y.mean()) / Ystd
-    weights = torch.exp(eta * Z)
+    Z = (Y - Y.mean(dim=0)) / Ystd
+    etaZ = eta * Z
+    weights = torch.exp(etaZ)
     while torch.isinf(weights).any():
-        weights = torch.exp(Z * eta)
-        eta *= 0.5
-    idcs = torch.multinomial(weights, n)
+        etaZ *= 0.5
+        weights = torch.exp(etaZ)
+    if batch_shape == torch.Size():
+        idcs = torch.multinomial(weights, n)
+    else:
+        idcs = _batched_multinomial(weights.permute(*range(1, len(batch_shape) + 1), 0),
+                                    n).permute(-1, *range(len(batch_shape)))
     if max_idx not in idcs:
         idcs[-1] = max_idx
-    return X[idcs]
+    if batch_shape == torch.Size():
+        return X[idcs]
+    return X.gather(dim=0, index=idcs.view(*idcs.shape, 1, 1).expand(n, *X.shape[1:]))
 
 
-def _is_nonnegative(acqf) -> bool:
-    from .acquisition import (ExpectedImprovement, ProbabilityOfImprovement,
-                              qExpectedImprovement)
-    names = ("qExpectedImprovement", "qNoisyExpectedImprovement", "ExpectedImprovement",
-             "ProbabilityOfImprovement", "qExpectedHypervolumeImprovement")
-    return type(acqf).__name__ in names
+_NONNEGATIVE = ("ExpectedImprovement", "ConstrainedExpectedImprovement", "ProbabilityOfImprovement",
+                "NoisyExpectedImprovement", "qExpectedImprovement", "qNoisyExpectedImprovement",
+                "qProbabilityOfImprovement", "ExpectedHypervolumeImprovement",
+                "qExpectedHypervolumeImprovement", "qNoisyExpectedHypervolumeImprovement")
+
+
+def is_nonnegative(acq_function) -> bool:
+    """optim/initializers.py:1272-1300 (by class: the LogEI family is not
+    non-negative even where it derives from the qEI classes here)."""
+    return type(acq_function).__name__ in _NONNEGATIVE
+
+
+_is_nonnegative = is_nonnegative
+
+
+@contextmanager
+def _seeded(seed, device):
+    """manual_seed(seed) for the CPU and, when used, the current GPU generator,
+    restoring both afterwards (utils/sampling.py:40-63 extended to the device)."""
+    if seed is None:
+        yield
+        return
+    devices = [device.index if device.index is not None else torch.cuda.current_device()] \
+        if device.type == "cuda" else []
+    with torch.random.fork_rng(devices=devices):
+        torch.manual_seed(seed)
+        yield
+
+
+def draw_raw_samples(bounds, n, q, seed=None):
+    """Raw q-batch designs for the initialiser: on the device (bo_sobol_box,
+    bit-identical to draw_sobol_samples) when ``bounds`` lives there, on the
+    host (the reference's own path) otherwise."""
+    if bounds.is_cuda:
+        from . import kernels
+        return kernels.sobol_box(bounds.to(torch.float64), n, q, seed).to(bounds.dtype)
+    return draw_sobol_samples(bounds=bounds.cpu(), n=n, q=q, seed=seed)
+
+
+def evaluate_raw_samples(acq_function, X_rnd, batch_limit=None):
+    """Forward-only acquisition values of the raw designs in chunks of
+    ``batch_limit`` (initializers.py:411-423), kept where they are computed: on
+    the GPU path the values never leave the device (no per-chunk ``.cpu()``)."""
+    if batch_limit is None:
+        batch_limit = X_rnd.shape[0]
+    with torch.no_grad():
+        ys = [acq_function(X_rnd[s:s + batch_limit]) for s in range(0, X_rnd.shape[0], batch_limit)]
+    return torch.cat([y.reshape(-1) for y in ys])
 
 
 def gen_batch_initial_conditions(acq_function, bounds, q, num_restarts, raw_samples,
-                                 fixed_features=None, options=None, **kwargs):
-    """optim/initializers.py:243-438: Sobol raw samples on the host, forward-only
-    evaluation in chunks of init_batch_limit on the device, Boltzmann selection."""
+                                 fixed_features=None, options=None, inequality_constraints=None,
+                                 equality_constraints=None, generator=None, fixed_X_fantasies=None,
+                                 **kwargs):
+    """optim/initializers.py:243-438: Sobol raw samples, forward-only evaluation
+    in chunks of init_batch_limit, Boltzmann selection; retried with up to 5x
+    the raw samples (seed + 1 each time) while the selection warns.
+
+    MI355X path (bounds on the GPU): the raw designs are generated on the
+    device (bo_sobol_box), evaluated there chunk by chunk, and the selection
+    runs on the device tensors -- the reference's per-chunk host round trip
+    (initializers.py:416-420) is gone."""
+    if bounds.isinf().any():
+        raise NotImplementedError("Currently only finite values in `bounds` are supported for "
+                                  "generating initial conditions for optimization.")
+    if inequality_constraints or equality_constraints or generator is not None \
+            or fixed_X_fantasies is not None:
+        raise NotImplementedError("constrained / custom-generator initialisation is out of scope")
     options = options or {}
+    if options.get("sample_around_best", False):
+        raise NotImplementedError("sample_around_best is out of scope")
     seed = options.get("seed")
     batch_limit = options.get("init_batch_limit", options.get("batch_limit"))
-    device = bounds.device
-    bounds_cpu = bounds.cpu()
-    X_rnd = draw_sobol_samples(bounds=bounds_cpu, n=raw_samples, q=q, seed=seed)
-    with torch.no_grad():
-        if batch_limit is None:
-            batch_limit = X_rnd.shape[0]
-        ys = []
-        for start in range(0, X_rnd.shape[0], batch_limit):
-            ys.append(acq_function(X_rnd[start:start + batch_limit].to(device)).cpu())
-        Y_rnd = torch.cat(ys)
-    init = initialize_q_batch_nonneg if (options.get("nonnegative") or _is_nonnegative(acq_function)) \
-        else initialize_q_batch
-    kw = {"eta": options.get("eta", 1.0)}
-    if init is initialize_q_batch_nonneg and "alpha" in options:
-        kw["alpha"] = options["alpha"]
-    with manual_seed(seed):
-        ics = init(X_rnd, Y_rnd, num_restarts, **kw)
-    return ics.to(device)
+    init_kwargs = {}
+    if "eta" in options:
+        init_kwargs["eta"] = options.get("eta")
+    if options.get("nonnegative") or is_nonnegative(acq_function):
+        init_func = initialize_q_batch_nonneg
+        if "alpha" in options:
+            init_kwargs["alpha"] = options.get("alpha")
+    else:
+        init_func = initialize_q_batch
+    q = 1 if q is None else q
+    factor, max_factor = 1, 5
+    while factor < max_factor:
+        with warnings.catch_warnings(record=True) as ws:
+            warnings.simplefilter("always", category=BadInitialCandidatesWarning)
+            n = raw_samples * factor
+            X_rnd = draw_raw_samples(bounds, n, q, seed)
+            if fixed_features:
+                for k, v in fixed_features.items():
+                    X_rnd[..., k] = v
+            Y_rnd = evaluate_raw_samples(acq_function, X_rnd.to(bounds.device), batch_limit)
+            # Seeded selection (the reference draws it from the global RNG): every
+            # rank of optimize_acqf_sharded / every rerun picks reproducibly.
+            with _seeded(seed, Y_rnd.device):
+                ics = init_func(X=X_rnd.to(Y_rnd.device), Y=Y_rnd, n=num_restarts, **init_kwargs)
+            ics = ics.to(device=bounds.device)
+            if not any(issubclass(w.category, BadInitialCandidatesWarning) for w in ws):
+                return ics
+            if factor < max_factor:
+                factor += 1
+                if seed is not None:
+                    seed += 1
+    warnings.warn("Unable to find non-zero acquisition function values - initial conditions "
+                  "are being selected randomly.", BadInitialCandidatesWarning)
+    return ics
 
 
 def gen_candidates_scipy(initial_conditions, acquisition_function, lower_bounds=None,

@@ -285,6 +285,15 @@ int bo_mc_reduce(int S, int B, int q, const double* samples, double best_f,
 int bo_sobol_normal(const int64_t* state, const int64_t* shift, int dim, int64_t n,
                     int64_t skip, int first_f32, double* out, void* stream);
 
+/* Scrambled Sobol raw designs in a box, points skip..skip+n-1: out (n x dim),
+ * dim = q * d, out[i][j] = lower[j % d] + range[j % d] * u_i[j] (device
+ * lower/range of length d).  Same engine state as bo_sobol_normal.
+ * Replaces draw_sobol_samples (botorch/utils/sampling.py:66-105) in
+ * gen_batch_initial_conditions (botorch/optim/initializers.py:350-362). */
+int bo_sobol_box(const int64_t* state, const int64_t* shift, int dim, int64_t n, int64_t skip,
+                 int first_f32, const double* lower, const double* range, int d, double* out,
+                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

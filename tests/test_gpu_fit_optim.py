@@ -82,3 +82,45 @@ def test_optimize_acqf_qei_end_to_end():
     assert val.item() >= 0.9 * base
     with torch.no_grad():
         torch.testing.assert_close(acqf(cand.unsqueeze(0)).reshape(()), val.reshape(()))
+
+
+@pytest.mark.parametrize("n,q,d,seed", [(20, 1, 6, 0), (64, 8, 6, 1), (32, 16, 6, 1)])
+def test_device_sobol_box_matches_reference(golden, n, q, d, seed):
+    """bo_sobol_box is bit-identical to the reference's draw_sobol_samples."""
+    from botorch_amd import kernels
+    bounds = torch.stack([torch.zeros(d), torch.ones(d)]).to(torch.float64).to(DEV)
+    x = kernels.sobol_box(bounds, n, q, seed).cpu().numpy()
+    np.testing.assert_array_equal(x, golden[f"sobol_box_n{n}_q{q}_d{d}_s{seed}"])
+    # a non-unit box matches the host restatement bit for bit
+    from botorch_amd.utils_sampling import draw_sobol_samples
+    b2 = torch.tensor([[-2.0] * d, [3.5] * d], dtype=torch.float64)
+    torch.testing.assert_close(kernels.sobol_box(b2.to(DEV), n, q, seed).cpu(),
+                               draw_sobol_samples(b2, n, q, seed=seed), rtol=0, atol=0)
+
+
+def test_gen_batch_initial_conditions_on_device():
+    """Raw designs, their forward-only values and the Boltzmann selection stay
+    on the device; the picks are raw designs and include the best one."""
+    from botorch_amd.acquisition import qExpectedImprovement, qLogExpectedImprovement
+    from botorch_amd.models import SingleTaskGP
+    from botorch_amd.optim import evaluate_raw_samples, gen_batch_initial_conditions
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from botorch_amd.utils_sampling import draw_sobol_samples
+    X, Y = _data(128)
+    m = SingleTaskGP(X.to(DEV), Y.to(DEV)).eval()
+    bounds = torch.stack([torch.zeros(6), torch.ones(6)]).to(torch.float64).to(DEV)
+    for cls, bf in ((qExpectedImprovement, Y.max().item() - 0.5), (qLogExpectedImprovement, Y.max().item())):
+        acqf = cls(m, bf, sampler=SobolQMCNormalSampler(torch.Size([64]), seed=0))
+        ics = gen_batch_initial_conditions(acqf, bounds, q=4, num_restarts=6, raw_samples=96,
+                                           options={"seed": 3, "init_batch_limit": 40})
+        assert ics.is_cuda and ics.shape == (6, 4, 6)
+        raw = draw_sobol_samples(bounds.cpu(), 96, 4, seed=3)
+        yr = evaluate_raw_samples(acqf, raw.to(DEV), 40).cpu()
+        with torch.no_grad():
+            torch.testing.assert_close(yr, acqf(raw.to(DEV)).cpu(), rtol=1e-12, atol=0)
+        hits = [(raw == ic).all(-1).all(-1).nonzero().flatten().tolist() for ic in ics.cpu()]
+        assert all(len(h) == 1 for h in hits)
+        assert int(yr.argmax()) in [h[0] for h in hits]
+        again = gen_batch_initial_conditions(acqf, bounds, q=4, num_restarts=6, raw_samples=96,
+                                             options={"seed": 3, "init_batch_limit": 40})
+        assert torch.equal(ics, again)

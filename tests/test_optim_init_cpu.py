@@ -1,0 +1,102 @@
+"""Raw-sample initialisation semantics (optim/initializers.py), mirroring the
+reference's test/optim/test_initializers.py:89-180 on CPU tensors."""
+import warnings
+
+import pytest
+import torch
+
+from botorch_amd.optim import (BadInitialCandidatesWarning, gen_batch_initial_conditions,
+                               initialize_q_batch, initialize_q_batch_nonneg, is_nonnegative)
+
+
+@pytest.mark.parametrize("dtype", [torch.float, torch.double])
+def test_initialize_q_batch_nonneg(dtype):
+    X = torch.rand(5, 3, 4, dtype=dtype)
+    Y = torch.rand(5, dtype=dtype)
+    ics = initialize_q_batch_nonneg(X=X, Y=Y, n=2)
+    assert ics.shape == (2, 3, 4) and ics.dtype == dtype
+    assert torch.equal(initialize_q_batch_nonneg(X=X, Y=Y, n=5), X)
+    ics = initialize_q_batch_nonneg(X=X, Y=torch.ones(5, dtype=dtype), n=2)
+    assert ics.shape == (2, 3, 4)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        ics = initialize_q_batch_nonneg(X=X, Y=torch.zeros(5, dtype=dtype), n=2)
+    assert len(w) == 1 and issubclass(w[-1].category, BadInitialCandidatesWarning)
+    assert ics.shape == (2, 3, 4)
+    with pytest.raises(RuntimeError):
+        initialize_q_batch_nonneg(X=X, Y=Y, n=10)
+    Y = torch.arange(5, dtype=dtype) - 3  # one positive value
+    ics = initialize_q_batch_nonneg(X=X, Y=Y, n=2)
+    assert torch.equal(ics[0], X[-1]) or torch.equal(ics[1], X[-1])
+    ics = initialize_q_batch_nonneg(X=X, Y=torch.arange(5, dtype=dtype), n=2, alpha=1.0)
+    assert ics.shape == (2, 3, 4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float, torch.double])
+@pytest.mark.parametrize("batch_shape", [torch.Size(), [3, 2], (2,)])
+def test_initialize_q_batch(dtype, batch_shape):
+    X = torch.rand(5, *batch_shape, 3, 4, dtype=dtype)
+    Y = torch.rand(5, *batch_shape, dtype=dtype)
+    ics = initialize_q_batch(X=X, Y=Y, n=2)
+    assert ics.shape == torch.Size([2, *batch_shape, 3, 4])
+    assert torch.equal(initialize_q_batch(X=X, Y=Y, n=5), X)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        ics = initialize_q_batch(X=X, Y=torch.zeros(5, dtype=dtype), n=2)
+    assert len(w) == 1 and issubclass(w[-1].category, BadInitialCandidatesWarning)
+    with pytest.raises(RuntimeError):
+        initialize_q_batch(X=X, Y=Y, n=10)
+    # the best raw sample is always kept
+    Y = torch.rand(5, *batch_shape, dtype=dtype)
+    ics = initialize_q_batch(X=X, Y=Y, n=2, eta=0.01)
+    if batch_shape == torch.Size():
+        assert any(torch.equal(ics[k], X[int(Y.argmax())]) for k in range(2))
+
+
+def test_initialize_q_batch_large_eta_z():
+    X = torch.rand(5, 3, 4, dtype=torch.double)
+    Y = torch.tensor([-1e12, 0, 0, 0, 1e12], dtype=torch.double)
+    assert initialize_q_batch(X=X, Y=Y, n=2, eta=100).shape[0] == 2
+
+
+def test_gen_batch_initial_conditions_rejects_inf_bounds():
+    bounds = torch.rand(2, 2)
+    bounds[0, 1] = float("inf")
+    with pytest.raises(NotImplementedError, match="only finite values"):
+        gen_batch_initial_conditions(lambda X: X.sum((-1, -2)), bounds, q=1, num_restarts=2,
+                                     raw_samples=2)
+
+
+def test_gen_batch_initial_conditions_host_path():
+    from botorch_amd.utils_sampling import draw_sobol_samples
+    bounds = torch.tensor([[0.0, -1.0], [1.0, 2.0]], dtype=torch.double)
+
+    def acqf(X):
+        return -((X - 0.3) ** 2).sum((-1, -2))
+
+    ics = gen_batch_initial_conditions(acqf, bounds, q=3, num_restarts=4, raw_samples=16,
+                                       options={"seed": 7})
+    raw = draw_sobol_samples(bounds, 16, 3, seed=7)
+    assert ics.shape == (4, 3, 2)
+    # every initial condition is one of the raw designs, the best among them
+    hits = [(raw == ic).all(-1).all(-1).nonzero().flatten().tolist() for ic in ics]
+    assert all(len(h) == 1 for h in hits)
+    assert int(acqf(raw).argmax()) in [h[0] for h in hits]
+    # reproducible under the seed
+    again = gen_batch_initial_conditions(acqf, bounds, q=3, num_restarts=4, raw_samples=16,
+                                         options={"seed": 7})
+    assert torch.equal(ics, again)
+
+
+def test_is_nonnegative_follows_reference_list():
+    from botorch_amd import acquisition as A
+
+    class Dummy:
+        pass
+
+    assert not is_nonnegative(Dummy())
+    for cls in (A.qExpectedImprovement, A.qNoisyExpectedImprovement, A.ExpectedImprovement,
+                A.qExpectedHypervolumeImprovement):
+        assert is_nonnegative(object.__new__(cls))
+    for cls in (A.qLogExpectedImprovement, A.qLogNoisyExpectedImprovement, A.UpperConfidenceBound):
+        assert not is_nonnegative(object.__new__(cls))
