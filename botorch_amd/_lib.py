@@ -29,6 +29,7 @@ _SIGNATURES = {
     "bo_version": (c_int, []),
     "bo_probe_mfma_f64_layout": (c_int, [_P, _P]),
     "bo_probe_mfma_f64_rate": (c_int, [c_int, c_int, _P, _P]),
+    "bo_probe_valu_f64": (c_int, [c_int, _P, _P]),
     "bo_gemm_f64": (c_int, [c_int, c_int, c_int, c_int, c_int, c_double, _P, c_int64, c_int64,
                             _P, c_int64, c_int64, c_double, _P, c_int64, c_int64, c_int, c_int,
                             _P]),

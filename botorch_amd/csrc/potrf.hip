@@ -349,7 +349,6 @@ __global__ __launch_bounds__(256) void potrf_block_kernel(double* __restrict__ A
   }
   BO_TSC(15);
 }
-#undef BO_TSC
 
 }  // namespace
 

@@ -34,7 +34,63 @@ __global__ __launch_bounds__(256) void rate_kernel(int iters, double* out) {
   for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
   if (s == 12345.678) out[0] = s;  // keep live
 }
+// fp64 VALU latency / issue probe (one workgroup of `waves` waves; wave 0
+// lane 0 records s_memtime ticks): out[0] = ticks for 256 dependent v_fma_f64,
+// out[1] = ticks for 256 x 8 independent v_fma_f64 (8 chains), out[2] =
+// ticks for 64 v_rsq_f64 + 2 Newton steps chained, out[3] = ticks for 256
+// dependent ds_read_b64 -> v_add round trips (LDS latency).
+__global__ void valu_probe_kernel(double seed, long long* out) {
+  __shared__ double buf[256];
+  const int tid = threadIdx.x;
+  buf[tid & 255] = seed + tid;
+  __syncthreads();
+  double a = seed + tid, b = 1.0 + 1e-9 * tid;
+  long long t0 = clock64();
+#pragma unroll 16
+  for (int i = 0; i < 256; ++i) a = fma(a, b, 1e-7);
+  long long t1 = clock64();
+  double c[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c[j] = a + j;
+  long long t2 = clock64();
+#pragma unroll 4
+  for (int i = 0; i < 256; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = fma(c[j], b, 1e-7);
+  long long t3 = clock64();
+  double r = c[0] + c[7] + 2.0;
+#pragma unroll 4
+  for (int i = 0; i < 64; ++i) {
+    double q = __builtin_amdgcn_rsq(r);
+    const double h = -0.5 * r;
+    q = q * fma(h * q, q, 1.5);
+    q = q * fma(h * q, q, 1.5);
+    r = 2.0 + q;
+  }
+  long long t4 = clock64();
+  int idx = tid & 255;
+  double acc = 0.0;
+  for (int i = 0; i < 256; ++i) {
+    const double v = buf[idx];
+    acc += v;
+    idx = ((int)v + i) & 255;
+  }
+  long long t5 = clock64();
+  if (tid == 0) {
+    out[0] = t1 - t0;
+    out[1] = t3 - t2;
+    out[2] = t4 - t3;
+    out[3] = t5 - t4;
+  }
+  if (a + r + acc == 1234.5) out[4] = 1;
+}
 }  // namespace
+
+extern "C" int bo_probe_valu_f64(int waves, long long* out, void* stream) {
+  valu_probe_kernel<<<1, 64 * waves, 0, as_stream(stream)>>>(1.5, out);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
 
 // flops = blocks * 4 waves * iters * 8 * 2048
 extern "C" int bo_probe_mfma_f64_rate(int blocks, int iters, double* out, void* stream) {

@@ -61,6 +61,10 @@ int bo_probe_mfma_f64_layout(double* out, void* stream);
 /* Peak-rate probe: `blocks` x 256 threads, each wave issuing iters x 8
  * independent fp64 MFMAs (2048 flop each).  out: 1 double (kept live). */
 int bo_probe_mfma_f64_rate(int blocks, int iters, double* out, void* stream);
+/* fp64 VALU / LDS latency probe (tools/probe_rate.py): out[0..3] = s_memtime
+ * ticks of 256 dependent FMAs, 256 x 8 independent FMAs, 64 rsq+2NR chains,
+ * 256 dependent LDS reads, with `waves` waves in the workgroup. */
+int bo_probe_valu_f64(int waves, long long* out, void* stream);
 
 /* Phase-timing probe of the 128-block Cholesky kernel (potrf.hip) on the
  * leading block of A (lda even, >= 128): 16 s_memtime stamps into tsc. */

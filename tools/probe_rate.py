@@ -25,4 +25,13 @@ for blocks in (256, 512, 1024, 2048):
     ms = e0.elapsed_time(e1)
     fl = blocks * 4 * iters * 8 * 2048
     res[blocks] = fl / (ms * 1e-3) / 1e12
-print(json.dumps({"fp64_mfma_tflops": res}))
+valu = {}
+for waves in (1, 4, 8):
+    o = torch.zeros(8, dtype=torch.int64, device=dev)
+    for _ in range(2):
+        _lib.check(_lib.lib().bo_probe_valu_f64(waves, ctypes.c_void_p(o.data_ptr()), st))
+    torch.cuda.synchronize()
+    t = o.cpu().tolist()
+    valu[waves] = {"dep_fma_cyc": t[0] / 256, "indep_fma_cyc": t[1] / 2048,
+                   "rsq2nr_chain_cyc": t[2] / 64, "lds_dep_read_cyc": t[3] / 256}
+print(json.dumps({"fp64_mfma_tflops": res, "valu_f64": valu}))
