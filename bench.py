@@ -193,6 +193,7 @@ def other_configs(dev, cpu=True):
     Y = Hartmann(negate=True)(X).unsqueeze(-1)
     Xc = draw_sobol_samples(unit(6), b, q, seed=1)
     m = stgp(X, Y, LENGTHSCALE, NOISE)
+    m_c2, bf_c2 = m, float(Y.max()) - 0.3
     acqf = qExpectedImprovement(m, float(Y.max()), sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
     Xd = Xc.to(dev)
     with torch.no_grad():
@@ -295,6 +296,29 @@ def other_configs(dev, cpu=True):
         tc, runs = _cpu_time(lambda: oacq.qlognei(ref, Xc[:bs]))
         e.update(cpu_evals_per_s=q * S * bs / tc, cpu_sample=f"{bs} of {b} restarts, median of {runs}")
     out["C3_qLogNEI"] = e
+
+    # Section 8(f) rank 3: optimize_acqf end to end (raw-sample init + candidate
+    # generation) with the reference's host scipy L-BFGS-B loop vs the
+    # device-resident multi-start L-BFGS (gen_candidates_device), C2 and C3 models.
+    from botorch_amd.optim import gen_candidates_device, gen_candidates_scipy, optimize_acqf
+    for tag, (mm, bfv, qq, SS, bb, raw_n) in {
+            "C2": (m_c2, bf_c2, 8, 256, 64, 512),
+            "C3": (m, best - 0.3, Q, MC, 128, 1024)}.items():
+        acq_o = qExpectedImprovement(mm, bfv, sampler=SobolQMCNormalSampler(torch.Size([SS]), seed=0))
+        bnd = unit(6).to(dev)
+        res = {}
+        for gname, gen in (("scipy", gen_candidates_scipy), ("device", gen_candidates_device)):
+            opts = {"seed": 0, "maxiter": 100}
+            optimize_acqf(acq_o, bnd, qq, bb, raw_n, options=opts, gen_candidates=gen)  # warm-up
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            cand, val = optimize_acqf(acq_o, bnd, qq, bb, raw_n, options=opts, gen_candidates=gen)
+            torch.cuda.synchronize()
+            res[gname] = {"ms": 1e3 * (time.perf_counter() - t0), "best_acq": float(val)}
+        res["device_evals"] = int(gen_candidates_device.last_evals)
+        out[f"{tag}_optimize_acqf"] = {
+            "config": f"{tag} optimize_acqf qEI q={qq} S={SS} restarts={bb} raw={raw_n} maxiter=100",
+            **res, "speedup": res["scipy"]["ms"] / res["device"]["ms"]}
 
     # C4: qEHVI, ModelListGP of 3 on DTLZ2 (n=2048, d=6), q=8, S=128, b=128
     n, q, S, b, mo = 2048, 8, 128, 128, 3

@@ -12,6 +12,7 @@ the final argmax/gather is one all-reduce.
 """
 from __future__ import annotations
 
+import math
 import time
 import warnings
 from contextlib import contextmanager
@@ -272,6 +273,91 @@ def gen_candidates_scipy(initial_conditions, acquisition_function, lower_bounds=
     with torch.no_grad():
         acq = acquisition_function(clamped)
     return clamped, acq
+
+
+class _LBFGSState:
+    """Device buffers of the multi-start projected L-BFGS (bo_lbfgs_step)."""
+
+    def __init__(self, X0: torch.Tensor, m: int):
+        B, n = X0.shape[0], X0[0].numel()
+        f64 = dict(dtype=torch.float64, device=X0.device)
+        i32 = dict(dtype=torch.int32, device=X0.device)
+        self.B, self.n, self.m = B, n, m
+        self.x = torch.empty(B, n, **f64)
+        self.g = torch.empty(B, n, **f64)
+        self.xt = X0.reshape(B, n).to(torch.float64).clone()
+        self.d = torch.zeros(B, n, **f64)
+        self.f = torch.empty(B, **f64)
+        self.alpha = torch.ones(B, **f64)
+        self.S = torch.empty(B, m, n, **f64)
+        self.Y = torch.empty(B, m, n, **f64)
+        self.rho = torch.zeros(B, m, **f64)
+        self.hcount = torch.zeros(B, **i32)
+        self.hhead = torch.zeros(B, **i32)
+        self.status = torch.full((B,), -1, **i32)
+        self.nacc = torch.zeros(B, **i32)
+
+
+def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds=None,
+                          upper_bounds=None, options=None, fixed_features=None, timeout_sec=None,
+                          **kwargs):
+    """Device-resident replacement of gen_candidates_scipy (generation/gen.py:
+    46-298): every restart runs its own projected
+    L-BFGS (history ``maxcor``, Armijo backtracking, scipy's default
+    ``ftol`` / ``gtol``) on the GPU.  One evaluation = one batched forward +
+    backward of the acquisition at all trial points + one bo_lbfgs_step launch;
+    the iterate, gradient and history never leave HBM, and the host reads the
+    (B,) status vector only every ``check_every`` evaluations.
+
+    ``maxiter`` bounds the function evaluations per restart (scipy's own
+    ``maxfun`` analogue); returns (candidates b x q x d, acq values b)."""
+    from . import kernels
+    from ._lib import check, lib
+    if fixed_features:
+        raise NotImplementedError("fixed_features is not supported by the device optimiser")
+    options = dict(options or {})
+    maxiter = int(options.get("maxiter", 200))
+    m = int(options.get("maxcor", 10))
+    ftol = float(options.get("ftol", 1e7 * np.finfo(float).eps))  # scipy factr 1e7
+    pgtol = float(options.get("gtol", 1e-5))
+    check_every = int(options.get("check_every", 8))
+    X0 = columnwise_clamp(initial_conditions, lower_bounds, upper_bounds).detach()
+    if not X0.is_cuda:
+        raise RuntimeError("gen_candidates_device runs on ROCm device tensors")
+    shapeX = X0.shape
+    st = _LBFGSState(X0, m)
+    d = shapeX[-1]
+    lo = (torch.as_tensor(lower_bounds, dtype=torch.float64, device=X0.device).expand(shapeX[-2:])
+          .reshape(-1).contiguous() if lower_bounds is not None
+          else torch.full((st.n,), -math.inf, dtype=torch.float64, device=X0.device))
+    hi = (torch.as_tensor(upper_bounds, dtype=torch.float64, device=X0.device).expand(shapeX[-2:])
+          .reshape(-1).contiguous() if upper_bounds is not None
+          else torch.full((st.n,), math.inf, dtype=torch.float64, device=X0.device))
+    stream = kernels._stream(X0.device)
+    P = kernels._p
+    t0 = time.monotonic()
+    for it in range(maxiter + 1):
+        Xt = st.xt.view(shapeX).detach().requires_grad_(True)
+        ft = -acquisition_function(Xt)
+        (gt,) = torch.autograd.grad(ft.sum(), Xt)
+        ft = ft.detach().reshape(-1).to(torch.float64).contiguous()
+        gt = gt.reshape(st.B, st.n).to(torch.float64).contiguous()
+        check(lib().bo_lbfgs_step(st.B, st.n, m, P(st.x), P(st.f), P(st.g), P(st.xt), P(ft), P(gt),
+                                  P(st.d), P(st.alpha), P(st.S), P(st.Y), P(st.rho), P(st.hcount),
+                                  P(st.hhead), P(st.status), P(st.nacc), P(lo), P(hi), 1e-4, ftol,
+                                  pgtol, 1e-12, stream), "lbfgs_step")
+        if (it + 1) % check_every == 0 or it == maxiter:
+            if bool((st.status > 0).all()):
+                break
+            if timeout_sec is not None and time.monotonic() - t0 > timeout_sec:
+                break
+    cands = st.x.view(shapeX).to(initial_conditions.dtype)
+    cands = columnwise_clamp(cands, lower_bounds, upper_bounds)
+    with torch.no_grad():
+        acq = acquisition_function(cands)
+    gen_candidates_device.last_state = st
+    gen_candidates_device.last_evals = it + 1
+    return cands, acq
 
 
 def optimize_acqf(acq_function, bounds, q, num_restarts, raw_samples=None, options=None,

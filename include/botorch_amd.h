@@ -289,6 +289,22 @@ int bo_mc_reduce(int S, int B, int q, const double* samples, double best_f,
 int bo_sobol_normal(const int64_t* state, const int64_t* shift, int dim, int64_t n,
                     int64_t skip, int first_f32, double* out, void* stream);
 
+/* One function evaluation of the device-resident multi-start projected L-BFGS
+ * (replaces scipy L-BFGS-B in gen_candidates_scipy, botorch/generation/gen.py:
+ * 194-267).  B restarts of dimension n, history m (<= 32).  The caller fills
+ * ft (B) / gt (B x n) with the objective (-acq) and its gradient at the trial
+ * points xt; the step accepts (Armijo, c1) or backtracks, updates x / f / g
+ * and the (S, Y, rho) ring, tests convergence (status: 1 projected gradient
+ * <= pgtol, 2 relative decrease <= ftol, 3 step below min_alpha; -1 on the first
+ * call = take xt as the start), and writes the next trial points to xt.
+ * x, g, xt, gt, d: B x n; S, Y: B x m x n; f, alpha: B; rho: B x m;
+ * hcount, hhead, status, nacc (accepted steps): B int32; lower, upper: n. */
+int bo_lbfgs_step(int B, int n, int m, double* x, double* f, double* g, double* xt,
+                  const double* ft, const double* gt, double* d, double* alpha, double* S,
+                  double* Y, double* rho, int* hcount, int* hhead, int* status, int* nacc,
+                  const double* lower, const double* upper, double c1, double ftol,
+                  double pgtol, double min_alpha, void* stream);
+
 /* Scrambled Sobol raw designs in a box, points skip..skip+n-1: out (n x dim),
  * dim = q * d, out[i][j] = lower[j % d] + range[j % d] * u_i[j] (device
  * lower/range of length d).  Same engine state as bo_sobol_normal.
