@@ -347,6 +347,32 @@ def other_configs(dev, cpu=True):
         e.update(cpu_evals_per_s=q * S * bs / tc, cpu_sample=f"{bs} of {b} restarts, median of {runs}")
     out["C4_qEHVI"] = e
 
+    # Section 8(f) rank 4: qNEHVI on the C4 models, X_baseline = the 2048
+    # training inputs pruned (prune_baseline=True), S=128 per-sample box
+    # decompositions (host, as the reference for m > 2), cached baseline roots.
+    from botorch_amd.acquisition import qNoisyExpectedHypervolumeImprovement
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    acqf = qNoisyExpectedHypervolumeImprovement(ModelListGP(*models), ref_point.tolist(), X.to(dev),
+                                                sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0),
+                                                prune_baseline=True)
+    torch.cuda.synchronize()
+    init_ms = 1e3 * (time.perf_counter() - t0)
+    with torch.no_grad():
+        t = _gpu_time(lambda: acqf(Xd), steps=5, warmup=1)
+    Xg = Xd.clone().requires_grad_(True)
+
+    def fb_nehvi():
+        (gx,) = torch.autograd.grad(acqf(Xg).sum(), Xg)
+        return gx
+
+    tfb = _gpu_time(fb_nehvi, steps=3, warmup=1)
+    out["C4_qNEHVI"] = {"config": "C4 qNEHVI ModelListGP(3) DTLZ2 n=2048 d=6 q=8 S=128 b=128, pruned baseline",
+                        "r": int(acqf.X_baseline.shape[0]),
+                        "cells_per_sample_max": int(acqf.cell_lower_bounds.shape[1]),
+                        "init_ms": init_ms, "gpu_evals_per_s": q * S * b / t, "gpu_ms": 1e3 * t,
+                        "fwd_bwd_ms": 1e3 * tfb}
+
     # C5: SAAS (M=16 prior draws), d=50, n=256, qEI q=4, S=256, b=64
     d, n, M, q, S, b = 50, 256, 16, 4, 256, 64
     X = draw_sobol_samples(unit(d), n, 1, seed=0).squeeze(1)

@@ -362,6 +362,71 @@ def prune_inferior_points(model, X, objective=None, posterior_transform=None, co
     return X[idcs]
 
 
+class _CachedBaselineRoot:
+    """Cached-root state of one exact-GP output over X_baseline
+    (acquisition/cached_cholesky.py:94-120, utils/low_rank.py:85-173) and the
+    fused-path pieces built on it.
+
+    Construction: the baseline posterior (outcome space), its jittered
+    Cholesky L_rr with inverse, the baseline samples mean_b + Z_base L_rr^T, and
+    P_b = L_rr^{-1} K(X_b, X_tr) L^{-T} (r x np), Q_b = P_b U^T, the scaled
+    baseline inputs.  forward(): T = L_rr^{-1} Sigma'(X_b, X) = s^2 (L_rr^{-1}
+    K_bX - P_b R^T) (two MFMA GEMMs) and the sample term F = Z_base T.
+    backward(): dT = Z_base^T dF - T G (G = dSigma + dSigma^T) pushed through
+    both GEMMs to dK*x (E = -s^2 dT^T Q_b) and d K_bX (s^2 L_rr^{-T} dT)."""
+
+    def __init__(self, model, X_baseline, Z_base, posterior_transform=None):
+        r = X_baseline.shape[-2]
+        self.Z_base = Z_base
+        with torch.no_grad():
+            post = model.posterior(X_baseline, posterior_transform=posterior_transform)
+            mean_b = post.distribution.mean.reshape(1, r)
+            cov_b = post.distribution.covariance_matrix.reshape(r, r)
+            L_rr, Linv_rr, _ = kernels.cholesky_with_inverse(cov_b)
+            base = kernels.sample_mvn(mean_b, L_rr.unsqueeze(0).contiguous(), Z_base)
+            self.samples = base.reshape(Z_base.shape[0], r)
+            self.L = L_rr.contiguous()
+            self.Linv = Linv_rr.contiguous()
+            self.fused_ready = False
+            if hasattr(model, "prediction_cache") and X_baseline.shape[-1] <= kernels.DP:
+                cache = model.prediction_cache()
+                Kb = kernels.covar_matrix(X_baseline.contiguous(), cache.Xt, cache.lengthscale,
+                                          cache.kind, cache.outputscale)
+                R_b = kernels.gemm(Kb, cache.U[: cache.n, : cache.n], flags=_lib.GEMM_B_UPPER)
+                P_b = torch.zeros(r, cache.np, dtype=torch.float64, device=Kb.device)
+                P_b[:, : cache.n] = kernels.gemm(self.Linv, R_b, flags=_lib.GEMM_A_LOWER)
+                self.P_b = P_b
+                # Q_b = P_b U^T = L_rr^{-1} K(X_b, X_tr) A^{-1}  (gradient of the
+                # cross-covariance through R = K*x L^{-T})
+                self.Q_b = kernels.gemm(P_b, cache.U, transB=True, flags=_lib.GEMM_B_LOWER)
+                self.Xb_scaled = torch.zeros(r, kernels.DP, dtype=torch.float64, device=Kb.device)
+                self.Xb_scaled[:, : cache.d] = X_baseline / cache.lengthscale
+                self.fused_ready = True
+
+    def forward(self, cache, pp, ystd):
+        s2 = ystd * ystd
+        ones = torch.ones(kernels.DP, dtype=torch.float64, device=pp.Xq.device)
+        Kbx = kernels.covar_matrix(self.Xb_scaled, pp.Xq, ones, cache.kind, cache.outputscale)
+        T = kernels.gemm(self.Linv, Kbx, alpha=s2, flags=_lib.GEMM_A_LOWER)
+        T = kernels.gemm(self.P_b, pp.Rt, alpha=-s2, beta=1.0, C=T)
+        F = kernels.gemm(self.Z_base, T)
+        return T, F
+
+    def backward(self, cache, pp, W, dmean, dcov, dF, T, ystd, dX=None):
+        s2 = ystd * ystd
+        B, q, Qp, nrows = pp.B, pp.q, pp.Qp, pp.nrows_pad
+        r = self.Linv.shape[0]
+        dT = kernels.gemm(self.Z_base, dF, transA=True)            # r x nrows_pad
+        G = (dcov + dcov.mT).contiguous()                          # B x q x q
+        kernels.gemm_strided(r, q, q, T, nrows, Qp, G, q, q * q, dT, nrows, Qp, B,
+                             alpha=-1.0, beta=1.0)                  # dT_b -= T_b G_b
+        E = kernels.gemm(dT, self.Q_b, transA=True, alpha=-s2)     # nrows_pad x np
+        dKbx = kernels.gemm(self.Linv, dT, transA=True, alpha=s2, flags=_lib.GEMM_A_UPPER)
+        dX = kernels.post_backward(cache, pp, W, dmean, dcov, ystd, E=E, dX=dX)
+        return kernels.post_backward(cache, pp, None, None, None, ystd, E=dKbx.mT.contiguous(),
+                                     Xt_scaled=self.Xb_scaled, n=r, dX=dX)
+
+
 class qNoisyExpectedImprovement(MCAcquisitionFunction):
     """MC batch noisy EI with the cached baseline root (acquisition/monte_carlo.py:
     417-645, cached_cholesky.py:63-186, utils/low_rank.py:85-173):
@@ -390,32 +455,14 @@ class qNoisyExpectedImprovement(MCAcquisitionFunction):
         sampler = self._ensure_sampler()
         S = sampler.sample_shape.numel()
         r = X_baseline.shape[-2]
-        with torch.no_grad():
-            post = model.posterior(X_baseline, posterior_transform=posterior_transform)
-            mean_b = post.distribution.mean.reshape(1, r)
-            cov_b = post.distribution.covariance_matrix.reshape(r, r)
-            L_rr, Linv_rr, _ = kernels.cholesky_with_inverse(cov_b)
-            self.Z_base = kernels.sobol_normal(r, S, sampler.seed, X_baseline.device)
-            base = kernels.sample_mvn(mean_b, L_rr.unsqueeze(0).contiguous(), self.Z_base)
-            self.baseline_samples = base.reshape(S, r)
-            self.register_buffer("_baseline_best_f", self.baseline_samples.amax(dim=-1).contiguous())
-            self._baseline_L = L_rr.contiguous()
-            self._Linv_rr = Linv_rr.contiguous()
-            self._fused_ready = False
-            if hasattr(model, "prediction_cache") and X_baseline.shape[-1] <= kernels.DP:
-                cache = model.prediction_cache()
-                Kb = kernels.covar_matrix(X_baseline.contiguous(), cache.Xt, cache.lengthscale,
-                                          cache.kind, cache.outputscale)
-                R_b = kernels.gemm(Kb, cache.U[: cache.n, : cache.n], flags=_lib.GEMM_B_UPPER)
-                P_b = torch.zeros(r, cache.np, dtype=torch.float64, device=Kb.device)
-                P_b[:, : cache.n] = kernels.gemm(self._Linv_rr, R_b, flags=_lib.GEMM_A_LOWER)
-                self._P_b = P_b
-                # Q_b = P_b U^T = L_rr^{-1} K(X_b, X_tr) A^{-1}  (gradient of the
-                # cross-covariance through R = K*x L^{-T})
-                self._Q_b = kernels.gemm(P_b, cache.U, transB=True, flags=_lib.GEMM_B_LOWER)
-                self._Xb_scaled = torch.zeros(r, kernels.DP, dtype=torch.float64, device=Kb.device)
-                self._Xb_scaled[:, : cache.d] = X_baseline / cache.lengthscale
-                self._fused_ready = True
+        Z_base = kernels.sobol_normal(r, S, sampler.seed, X_baseline.device)
+        self._root = _CachedBaselineRoot(model, X_baseline, Z_base, posterior_transform)
+        self.Z_base = Z_base
+        self.baseline_samples = self._root.samples
+        self.register_buffer("_baseline_best_f", self.baseline_samples.amax(dim=-1).contiguous())
+        self._baseline_L = self._root.L
+        self._Linv_rr = self._root.Linv
+        self._fused_ready = self._root.fused_ready
         self._zq = {}
 
     _fused_mode = _lib.QMC_QNEI
@@ -459,14 +506,9 @@ class _FusedQNEI(torch.autograd.Function):
         cache = model.prediction_cache()
         ymean, ystd = model.outcome_stats()
         q = X3.shape[-2]
-        s2 = ystd * ystd
         need_grad = ctx.needs_input_grad[0]
         pp = kernels.post_partials(cache, X3.detach(), store_R=True)
-        ones = torch.ones(kernels.DP, dtype=torch.float64, device=X3.device)
-        Kbx = kernels.covar_matrix(acqf._Xb_scaled, pp.Xq, ones, cache.kind, cache.outputscale)
-        T = kernels.gemm(acqf._Linv_rr, Kbx, alpha=s2, flags=_lib.GEMM_A_LOWER)
-        T = kernels.gemm(acqf._P_b, pp.Rt, alpha=-s2, beta=1.0, C=T)
-        F = kernels.gemm(acqf.Z_base, T)
+        T, F = acqf._root.forward(cache, pp, ystd)
         Zq = acqf._base_samples_q(q, X3.device)
         lp = getattr(acqf, "_log_params", None)
         out = kernels.qmc_finalize(cache, pp, acqf._fused_mode, ymean, ystd, Z=Zq,
@@ -484,21 +526,10 @@ class _FusedQNEI(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dacq):
         acqf, cache, pp, ystd = ctx.acqf, ctx.cache, ctx.pp, ctx.ystd
-        s2 = ystd * ystd
-        B, q, Qp, nrows = pp.B, pp.q, pp.Qp, pp.nrows_pad
-        r = acqf._Linv_rr.shape[0]
         dmean, dcov, dF = kernels.qmc_backward(acqf._fused_mode, ctx.mean, ctx.L, ctx.Zq,
                                                dacq.contiguous(), best_f_s=acqf._baseline_best_f,
                                                F=ctx.F, acq_fwd=ctx.acq, log_params=ctx.lp)
-        dT = kernels.gemm(acqf.Z_base, dF, transA=True)           # r x nrows_pad
-        G = (dcov + dcov.mT).contiguous()                         # B x q x q
-        kernels.gemm_strided(r, q, q, ctx.T, nrows, Qp, G, q, q * q, dT, nrows, Qp, B,
-                             alpha=-1.0, beta=1.0)                 # dT_b -= T_b G_b
-        E = kernels.gemm(dT, acqf._Q_b, transA=True, alpha=-s2)   # nrows_pad x np
-        dKbx = kernels.gemm(acqf._Linv_rr, dT, transA=True, alpha=s2, flags=_lib.GEMM_A_UPPER)
-        dX = kernels.post_backward(cache, pp, ctx.W, dmean, dcov, ystd, E=E)
-        dX = kernels.post_backward(cache, pp, None, None, None, ystd, E=dKbx.mT.contiguous(),
-                                   Xt_scaled=acqf._Xb_scaled, n=r, dX=dX)
+        dX = acqf._root.backward(cache, pp, ctx.W, dmean, dcov, dF, ctx.T, ystd)
         return dX, None
 
 
@@ -696,3 +727,235 @@ class qExpectedHypervolumeImprovement(MCAcquisitionFunction):
             raise UnsupportedError("fused qEHVI supports q <= 12 and d <= 8")
         acq = _FusedQEHVI.apply(X3, self)
         return acq.reshape(batch)
+
+
+# -- qNEHVI ------------------------------------------------------------------------------
+def prune_inferior_points_multi_objective(model, X, ref_point, objective=None, constraints=None,
+                                          num_samples: int = 2048, max_frac: float = 1.0,
+                                          marginalize_dim=None, chunk: int = 64):
+    """acquisition/multi_objective/utils.py:77-161 (unconstrained, identity
+    objective): keep the points with a positive probability of being
+    Pareto-optimal and better than ref_point under ``num_samples`` joint
+    posterior samples (drawn on the device; Pareto masks in sample chunks)."""
+    from .multi_objective import is_non_dominated
+    if X.ndim > 2:
+        raise UnsupportedError("Batched inputs `X` are currently unsupported by "
+                               "prune_inferior_points_multi_objective")
+    if max_frac <= 0 or max_frac > 1.0:
+        raise ValueError(f"max_frac must take values in (0, 1], is {max_frac}")
+    if constraints is not None:
+        raise UnsupportedError("constraints are not on the accelerated path")
+    max_points = math.ceil(max_frac * X.size(-2))
+    ref = torch.as_tensor(ref_point, dtype=torch.float64, device=X.device)
+    models = getattr(model, "models", [model])
+    n, m = X.shape[-2], len(models)
+    with torch.no_grad():
+        # joint samples of the independent outputs: Sobol dimension n m,
+        # point-major / output-minor base samples (get_sampler on the MTMVN)
+        if n * m <= 21201:
+            Z = kernels.sobol_normal(n * m, num_samples, None, X.device).view(num_samples, n, m)
+        else:
+            Z = torch.randn(num_samples, n, m, dtype=torch.float64, device=X.device)
+        cols = []
+        for t, mm in enumerate(models):
+            post = mm.posterior(X)
+            mean = post.distribution.mean.reshape(1, n)
+            L, _, _ = kernels.cholesky_with_inverse(post.distribution.covariance_matrix.reshape(n, n))
+            cols.append(kernels.sample_mvn(mean, L.unsqueeze(0).contiguous(),
+                                           Z[:, :, t].contiguous()).reshape(num_samples, n))
+        obj = torch.stack(cols, dim=-1)  # S x n x m
+        if objective is not None:
+            obj = objective(obj, X=X)
+        hits = torch.zeros(n, dtype=torch.float64, device=X.device)
+        for s0 in range(0, obj.shape[0], chunk):
+            o = obj[s0:s0 + chunk]
+            mask = is_non_dominated(o, deduplicate=False) & (o > ref).all(dim=-1)
+            hits += mask.to(torch.float64).sum(dim=0)
+    probs = hits / obj.shape[0]
+    idcs = probs.nonzero().view(-1)
+    if idcs.shape[0] > max_points:
+        counts, order_idcs = torch.sort(probs, descending=True)
+        idcs = order_idcs[:max_points]
+    return X[idcs]
+
+
+class _FusedQNEHVI(torch.autograd.Function):
+    """qNEHVI of B t-batches over a ModelListGP with cached baseline roots,
+    with its gradient.
+
+    Forward, per output t: post_partials (+ R^T), the cached-root terms
+    T_t = L_rr,t^{-1} Sigma'_t(X_b, X) and F_t = Z_b,t T_t (two MFMA GEMMs + one),
+    qmc_finalize(CHOL) on Sigma'_t - T_t^T T_t -> mean_t, L_t; then one bo_qehvi
+    launch over (sample, per-sample hypercell) pairs with f = mean + F + L Z_q.
+    Backward: bo_qehvi_backward (d mean, d L, d F) -> bo_chol_backward ->
+    the cached-root backward of each output (dT = Z_b^T dF - T G)."""
+
+    @staticmethod
+    def forward(ctx, X3, acqf):
+        models = acqf.model.models
+        need_grad = ctx.needs_input_grad[0]
+        q = X3.shape[-2]
+        means, Ls, Fs, saved = [], [], [], []
+        pp = None
+        for t, mm in enumerate(models):
+            cache = mm.prediction_cache()
+            ymean, ystd = mm.outcome_stats()
+            pp = kernels.post_partials(cache, X3.detach(), store_R=True)
+            T, F = acqf._roots[t].forward(cache, pp, ystd)
+            out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
+                                       want_cov=False, want_L=True, T=T, F=F)
+            kernels._raise_not_psd(out["info"], out["jitter"], "qNEHVI posterior root")
+            means.append(out["mean"])
+            Ls.append(out["L"])
+            Fs.append(F)
+            if need_grad:
+                saved.append((cache, pp, ystd, T, kernels.w_matrix(cache, pp)))
+        Zq = acqf._base_samples_q(q, X3.device)
+        lo, hi = acqf._cells
+        mean, L, F = torch.stack(means), torch.stack(Ls), torch.stack(Fs)
+        acq = kernels.qehvi(mean, L, Zq, lo, hi, F=F, Qp=pp.Qp)
+        if need_grad:
+            ctx.acqf, ctx.saved, ctx.mean, ctx.L, ctx.F, ctx.Zq, ctx.Qp = (
+                acqf, saved, mean, L, F, Zq, pp.Qp)
+        return acq
+
+    @staticmethod
+    def backward(ctx, dacq):
+        lo, hi = ctx.acqf._cells
+        dmean, dL, dF = kernels.qehvi_backward(ctx.mean, ctx.L, ctx.Zq, lo, hi, dacq, F=ctx.F,
+                                               Qp=ctx.Qp)
+        dX = None
+        for t, (cache, pp, ystd, T, W) in enumerate(ctx.saved):
+            dcov = kernels.chol_backward(ctx.L[t], dL[t])
+            dX = ctx.acqf._roots[t].backward(cache, pp, W, dmean[t], dcov, dF[t].contiguous(), T,
+                                             ystd, dX=dX)
+        return dX, None
+
+
+class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
+    """MC q-noisy expected hypervolume improvement (acquisition/multi_objective/
+    monte_carlo.py:325-468; NoisyExpectedHypervolumeMixin,
+    utils/multi_objective/hypervolume.py:507-835) for a ModelListGP of
+    SingleTaskGPs with the cached baseline root (cache_root=True) and the
+    incremental formulation (incremental_nehvi=True):
+
+      qNEHVI(X) = mean_s HVI(f_s(X) | Pareto front of f_s(X_baseline)).
+
+    Construction: the joint baseline samples (Sobol dimension r m), one exact
+    box decomposition of the non-dominated region per sample
+    (FastNondominatedPartitioning on the host, as the reference does for m > 2),
+    padded with empty cells to a common count (BoxDecompositionList), resident on
+    the device as S x K x m.  Forward / backward: _FusedQNEHVI.  Pending points
+    join the baseline (cache_pending=True, max_iep=0) and the decompositions are
+    rebuilt."""
+
+    _default_sample_shape = torch.Size([128])
+
+    def __init__(self, model, ref_point, X_baseline, sampler=None, objective=None,
+                 constraints=None, X_pending=None, eta=1e-3, fat=False, prune_baseline=False,
+                 alpha=0.0, cache_pending=True, max_iep=0, incremental_nehvi=True,
+                 cache_root=True, marginalize_dim=None):
+        if len(ref_point) < 2:
+            raise ValueError("NoisyExpectedHypervolumeMixin supports m>=2 outcomes "
+                             f"but ref_point has length {len(ref_point)}, which is smaller than 2.")
+        if X_baseline.ndim > 2:
+            raise UnsupportedError("NoisyExpectedHypervolumeMixin does not support batched "
+                                   f"X_baseline. Expected 2 dims, got {X_baseline.ndim}.")
+        if constraints is not None:
+            raise UnsupportedError("outcome constraints are not on the accelerated path")
+        if not (cache_root and incremental_nehvi and cache_pending and max_iep == 0):
+            raise UnsupportedError("qNEHVI here runs with cache_root, incremental_nehvi, "
+                                   "cache_pending and max_iep=0 (the reference defaults)")
+        if alpha > 0:
+            raise UnsupportedError("approximate partitioning (alpha > 0) is out of scope")
+        models = getattr(model, "models", None)
+        if models is None or not all(hasattr(mm, "prediction_cache") for mm in models):
+            raise UnsupportedError("qNEHVI here runs on a ModelListGP of SingleTaskGPs")
+        if len(models) != len(ref_point):
+            raise ValueError("The length of the reference point must match the number of outcomes.")
+        AcquisitionFunction.__init__(self, model)
+        self.sampler = sampler
+        self.objective = objective if objective is not None else IdentityMCMultiOutputObjective()
+        if not isinstance(self.objective, IdentityMCMultiOutputObjective):
+            raise UnsupportedError("only the identity multi-output objective is accelerated")
+        self.posterior_transform = None
+        self.ref_point = torch.as_tensor(ref_point, dtype=torch.float64, device=X_baseline.device)
+        self.fat = fat
+        self.alpha = alpha
+        self.X_pending = None
+        if prune_baseline:
+            X_baseline = prune_inferior_points_multi_objective(model, X_baseline, self.ref_point)
+        self._X_baseline = X_baseline
+        self._X_baseline_and_pending = X_baseline
+        self.register_buffer("_prev_nehvi", torch.tensor(0.0, dtype=torch.float64))
+        self._set_cell_bounds()
+        if X_pending is not None:
+            self.set_X_pending(X_pending)
+
+    @property
+    def X_baseline(self) -> torch.Tensor:
+        return self._X_baseline_and_pending
+
+    def set_X_pending(self, X_pending=None) -> None:
+        """hypervolume.py:766-800 with cache_pending=True, max_iep=0 and the
+        incremental formulation: pending points join the baseline."""
+        if X_pending is None:
+            self.X_pending = None
+            return
+        if X_pending.requires_grad:
+            warnings.warn("Pending points require a gradient but the acquisition function"
+                          " will not provide a gradient to these points.", BotorchWarning)
+        X_pending = X_pending.detach().clone()
+        self._X_baseline_and_pending = torch.cat([self._X_baseline, X_pending], dim=-2)
+        self._set_cell_bounds()
+        self.X_pending = None
+
+    def _set_cell_bounds(self) -> None:
+        """hypervolume.py:627-700: baseline samples and one box decomposition per
+        MC sample (host), padded to a common cell count (box_decomposition_list.py:
+        62-94), then resident on the device."""
+        from .multi_objective import FastNondominatedPartitioning
+        Xb = self.X_baseline
+        models = self.model.models
+        r, m = Xb.shape[-2], len(models)
+        if r == 0:
+            raise UnsupportedError("qNEHVI here needs at least one baseline point")
+        sampler = self._ensure_sampler()
+        S = sampler.sample_shape.numel()
+        Zb = kernels.sobol_normal(r * m, S, sampler.seed, Xb.device).view(S, r, m)
+        self._roots = [_CachedBaselineRoot(mm, Xb, Zb[:, :, t].contiguous())
+                       for t, mm in enumerate(models)]
+        if not all(rt.fused_ready for rt in self._roots):
+            raise UnsupportedError(f"qNEHVI here needs d <= {kernels.DP}")
+        Y = torch.stack([rt.samples for rt in self._roots], dim=-1).cpu()  # S x r x m
+        ref = self.ref_point.cpu()
+        bounds = [FastNondominatedPartitioning(ref, Y[s]).get_hypercell_bounds() for s in range(S)]
+        K = max(b.shape[-2] for b in bounds)
+        pad = [torch.cat([b, torch.zeros(2, K - b.shape[-2], m, dtype=b.dtype)], dim=-2)
+               if b.shape[-2] < K else b for b in bounds]
+        cells = torch.stack(pad, dim=1).to(Xb.device)  # 2 x S x K x m
+        self.cell_lower_bounds = cells[0].contiguous()
+        self.cell_upper_bounds = cells[1].contiguous()
+        self._cells = (self.cell_lower_bounds, self.cell_upper_bounds)
+        self.baseline_samples = Y
+        self._zq = {}
+
+    def _base_samples_q(self, q: int, device) -> torch.Tensor:
+        """The q m new columns of the (r+q) m-dim Sobol draw (sampling/normal.py:
+        68-131): point-major, output-minor, i.e. column p m + t for new point p."""
+        if q not in self._zq:
+            r, m = self.X_baseline.shape[-2], len(self.model.models)
+            S = self.sampler.sample_shape.numel()
+            full = kernels.sobol_normal((r + q) * m, S, self.sampler.seed, device)
+            self._zq[q] = full[:, r * m:].contiguous()
+        return self._zq[q]
+
+    def forward(self, X: torch.Tensor) -> torch.Tensor:
+        X = t_batch_mode(X)
+        batch = X.shape[:-2]
+        q, d = X.shape[-2], X.shape[-1]
+        if q > 12 or d > kernels.DP or not X.is_cuda:
+            raise UnsupportedError(f"fused qNEHVI supports q <= 12 and d <= {kernels.DP} on the device")
+        X3 = X.reshape(-1, q, d)
+        acq = _FusedQNEHVI.apply(X3, self)
+        return acq.reshape(batch) + self._prev_nehvi.to(acq)

@@ -25,11 +25,35 @@ constexpr int QMAX = 12;
 constexpr int MMAX = 4;
 constexpr int LDS_SAMPLES_DOUBLES = 6144;  // 48 KiB of samples per pass
 
+// Optional extensions used by qNEHVI (cached baseline root, per-sample box
+// decompositions): cstride > 0 gives every sample its own K cells
+// (lo/hi + s * cstride); F (m x S x ldF, output stride sF) adds the baseline
+// term Z_base T of the cached-root samples at row b * Qp + p.
+struct QehviExt {
+  int64_t cstride;
+  const double* F;
+  int64_t ldF, sF;
+  int Qp;
+};
+
+template <int M>
+__device__ __forceinline__ double sample_value(int B, int b, int q, int p, int t, int s,
+                                               const double* __restrict__ mean,
+                                               const double* __restrict__ L,
+                                               const double* __restrict__ Z, const QehviExt& ex) {
+  const double* Lt = L + (((int64_t)t * B + b) * q + p) * q;
+  const double* zs = Z + (int64_t)s * q * M;
+  double v = mean[((int64_t)t * B + b) * q + p];
+  if (ex.F) v += ex.F[t * ex.sF + (int64_t)s * ex.ldF + (int64_t)b * ex.Qp + p];
+  for (int j = 0; j <= p; ++j) v = fma(Lt[j], zs[j * M + t], v);
+  return v;
+}
+
 template <int M>
 __global__ __launch_bounds__(THREADS) void qehvi_kernel(
     int B, int q, const double* __restrict__ mean, const double* __restrict__ L,
     const double* __restrict__ Z, int S, const double* __restrict__ lo,
-    const double* __restrict__ hi, int K, double* __restrict__ acq) {
+    const double* __restrict__ hi, int K, QehviExt ex, double* __restrict__ acq) {
   __shared__ double f[LDS_SAMPLES_DOUBLES];
   __shared__ double red[THREADS / 64];
   const int b = blockIdx.x;
@@ -42,23 +66,18 @@ __global__ __launch_bounds__(THREADS) void qehvi_kernel(
     __syncthreads();
     for (int e = tid; e < ns * per_sample; e += THREADS) {
       const int s = e / per_sample;
-      const int p = (e / M) % q;
-      const int t = e % M;
-      const double* Lt = L + (((int64_t)t * B + b) * q + p) * q;
-      const double* zs = Z + (int64_t)(s0 + s) * q * M;
-      double v = mean[((int64_t)t * B + b) * q + p];
-      for (int j = 0; j <= p; ++j) v = fma(Lt[j], zs[j * M + t], v);
-      f[e] = v;
+      f[e] = sample_value<M>(B, b, q, (e / M) % q, e % M, s0 + s, mean, L, Z, ex);
     }
     __syncthreads();
     for (int e = tid; e < ns * K; e += THREADS) {
       const int s = e / K;
       const int k = e % K;
       double l[M], u[M];
+      const int64_t co = (int64_t)(s0 + s) * ex.cstride + (int64_t)k * M;
 #pragma unroll
       for (int t = 0; t < M; ++t) {
-        l[t] = lo[k * M + t];
-        u[t] = hi[k * M + t];
+        l[t] = lo[co + t];
+        u[t] = hi[co + t];
       }
       const double* fs = f + s * per_sample;
       double a[QMAX][M];
@@ -114,8 +133,8 @@ template <int M>
 __global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
     int B, int q, const double* __restrict__ mean, const double* __restrict__ L,
     const double* __restrict__ Z, int S, const double* __restrict__ lo,
-    const double* __restrict__ hi, int K, const double* __restrict__ dacq,
-    double* __restrict__ dmean, double* __restrict__ dL) {
+    const double* __restrict__ hi, int K, QehviExt ex, const double* __restrict__ dacq,
+    double* __restrict__ dmean, double* __restrict__ dL, double* __restrict__ dF) {
   constexpr int CH = LDS_SAMPLES_DOUBLES / 2;
   __shared__ double f[CH];
   __shared__ double df[CH];
@@ -132,13 +151,7 @@ __global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
     __syncthreads();
     for (int e = tid; e < ns * per_sample; e += THREADS) {
       const int s = e / per_sample;
-      const int p = (e / M) % q;
-      const int t = e % M;
-      const double* Lt = L + (((int64_t)t * B + b) * q + p) * q;
-      const double* zs = Z + (int64_t)(s0 + s) * q * M;
-      double v = mean[((int64_t)t * B + b) * q + p];
-      for (int j = 0; j <= p; ++j) v = fma(Lt[j], zs[j * M + t], v);
-      f[e] = v;
+      f[e] = sample_value<M>(B, b, q, (e / M) % q, e % M, s0 + s, mean, L, Z, ex);
       df[e] = 0.0;
     }
     __syncthreads();
@@ -146,10 +159,11 @@ __global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
       const int s = e / K;
       const int k = e % K;
       double l[M], u[M];
+      const int64_t co = (int64_t)(s0 + s) * ex.cstride + (int64_t)k * M;
 #pragma unroll
       for (int t = 0; t < M; ++t) {
-        l[t] = lo[k * M + t];
-        u[t] = hi[k * M + t];
+        l[t] = lo[co + t];
+        u[t] = hi[co + t];
       }
       const double* fs = f + s * per_sample;
       double a[QMAX][M];
@@ -209,6 +223,12 @@ __global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
       }
     }
     __syncthreads();
+    if (dF) {  // cotangent of the cached-root baseline term (rows b * Qp + p)
+      for (int e = tid; e < ns * per_sample; e += THREADS) {
+        const int s = e / per_sample, p = (e / M) % q, t = e % M;
+        dF[t * ex.sF + (int64_t)(s0 + s) * ex.ldF + (int64_t)b * ex.Qp + p] = g * df[e];
+      }
+    }
     for (int w = 0; w < 2; ++w) {
       const int ent = tid + w * THREADS;
       if (ent >= nent) continue;
@@ -286,33 +306,41 @@ __global__ __launch_bounds__(THREADS) void mc_reduce_kernel(
 }  // namespace
 
 extern "C" int bo_qehvi(int B, int q, int m, const double* mean, const double* L, const double* Z,
-                        int S, const double* cell_lo, const double* cell_hi, int K, double* acq,
-                        void* stream) {
+                        int S, const double* cell_lo, const double* cell_hi, int K,
+                        int64_t cell_stride, const double* F, int64_t ldF, int64_t sF, int Qp,
+                        double* acq, void* stream) {
   BO_CHECK_ARG(q >= 1 && q <= QMAX, "bo_qehvi: 1 <= q <= %d (got %d)", QMAX, q);
   BO_CHECK_ARG(m >= 2 && m <= MMAX, "bo_qehvi: 2 <= m <= %d (got %d)", MMAX, m);
-  BO_CHECK_ARG(S > 0 && K >= 0, "bo_qehvi: bad S/K");
+  BO_CHECK_ARG(S > 0 && K >= 0 && cell_stride >= 0, "bo_qehvi: bad S/K/cell_stride");
+  BO_CHECK_ARG(F == nullptr || (Qp >= q && ldF >= (int64_t)B * Qp), "bo_qehvi: bad F layout");
   if (B == 0) return BO_OK;
   hipStream_t st = as_stream(stream);
+  const QehviExt ex{cell_stride, F, ldF, sF, Qp};
   if (m == 2)
-    qehvi_kernel<2><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, acq);
+    qehvi_kernel<2><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, acq);
   else if (m == 3)
-    qehvi_kernel<3><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, acq);
+    qehvi_kernel<3><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, acq);
   else
-    qehvi_kernel<4><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, acq);
+    qehvi_kernel<4><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, acq);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
 
 extern "C" int bo_qehvi_backward(int B, int q, int m, const double* mean, const double* L,
                                  const double* Z, int S, const double* cell_lo,
-                                 const double* cell_hi, int K, const double* dacq, double* dmean,
-                                 double* dL, void* stream) {
+                                 const double* cell_hi, int K, int64_t cell_stride,
+                                 const double* F, int64_t ldF, int64_t sF, int Qp,
+                                 const double* dacq, double* dmean, double* dL, double* dF,
+                                 void* stream) {
   BO_CHECK_ARG(q >= 1 && q <= QMAX, "bo_qehvi_backward: 1 <= q <= %d (got %d)", QMAX, q);
   BO_CHECK_ARG(m >= 2 && m <= MMAX, "bo_qehvi_backward: 2 <= m <= %d (got %d)", MMAX, m);
-  BO_CHECK_ARG(S > 0 && K >= 0, "bo_qehvi_backward: bad S/K");
+  BO_CHECK_ARG(S > 0 && K >= 0 && cell_stride >= 0, "bo_qehvi_backward: bad S/K/cell_stride");
+  BO_CHECK_ARG((F == nullptr) == (dF == nullptr), "bo_qehvi_backward: F and dF go together");
+  BO_CHECK_ARG(F == nullptr || (Qp >= q && ldF >= (int64_t)B * Qp), "bo_qehvi_backward: bad F layout");
   if (B == 0) return BO_OK;
   hipStream_t st = as_stream(stream);
-#define BO_QB(MM) qehvi_backward_kernel<MM><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, dacq, dmean, dL)
+  const QehviExt ex{cell_stride, F, ldF, sF, Qp};
+#define BO_QB(MM) qehvi_backward_kernel<MM><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, dacq, dmean, dL, dF)
   if (m == 2) BO_QB(2);
   else if (m == 3) BO_QB(3);
   else BO_QB(4);

@@ -473,33 +473,56 @@ def sample_mvn(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor) -> torch.Te
     return out.permute(1, 0, 2) + mean.unsqueeze(0)
 
 
+def _cells_layout(cell_lo: torch.Tensor, S: int):
+    """(K, cell_stride): shared K x m cells, or per-sample S x K x m cells."""
+    if cell_lo.dim() == 3:
+        if cell_lo.shape[0] != S:
+            raise ValueError(f"per-sample cells for {cell_lo.shape[0]} samples, expected {S}")
+        return cell_lo.shape[1], cell_lo.shape[1] * cell_lo.shape[2]
+    return cell_lo.shape[0], 0
+
+
 def qehvi(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor, cell_lo: torch.Tensor,
-          cell_hi: torch.Tensor) -> torch.Tensor:
-    """mean: m x B x q, L: m x B x q x q, Z: S x (q m) -> acq (B)."""
+          cell_hi: torch.Tensor, F: Optional[torch.Tensor] = None, Qp: int = 0) -> torch.Tensor:
+    """mean: m x B x q, L: m x B x q x q, Z: S x (q m) -> acq (B).  Cells K x m
+    (shared) or S x K x m (per sample, qNEHVI); F: m x S x ldF cached-root
+    baseline term (rows b * Qp + p)."""
     dev = _dev(mean, L, Z, cell_lo, cell_hi)
     m, B, q = mean.shape
     S = Z.shape[0]
+    K, cstride = _cells_layout(cell_lo, S)
     acq = torch.empty(B, dtype=torch.float64, device=dev)
+    Fc = F.contiguous() if F is not None else None
     check(lib().bo_qehvi(B, q, m, _p(mean.contiguous()), _p(L.contiguous()),
                          _p(Z.reshape(S, q * m).contiguous()), S, _p(cell_lo.contiguous()),
-                         _p(cell_hi.contiguous()), cell_lo.shape[0], _p(acq), _stream(dev)),
+                         _p(cell_hi.contiguous()), K, cstride, _p(Fc),
+                         Fc.shape[-1] if Fc is not None else 0,
+                         Fc.shape[-1] * S if Fc is not None else 0, Qp, _p(acq), _stream(dev)),
           "qehvi")
     return acq
 
 
 def qehvi_backward(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor, cell_lo: torch.Tensor,
-                   cell_hi: torch.Tensor, dacq: torch.Tensor):
-    """Backward of :func:`qehvi`: -> dmean (m x B x q), dL (m x B x q x q)."""
+                   cell_hi: torch.Tensor, dacq: torch.Tensor, F: Optional[torch.Tensor] = None,
+                   Qp: int = 0):
+    """Backward of :func:`qehvi`: -> dmean (m x B x q), dL (m x B x q x q)[, dF]."""
     dev = _dev(mean, L, Z, cell_lo, cell_hi)
     m, B, q = mean.shape
     S = Z.shape[0]
+    K, cstride = _cells_layout(cell_lo, S)
     dmean = torch.empty(m, B, q, dtype=torch.float64, device=dev)
     dL = torch.empty(m, B, q, q, dtype=torch.float64, device=dev)
+    Fc = F.contiguous() if F is not None else None
+    dF = torch.zeros_like(Fc) if Fc is not None else None
     check(lib().bo_qehvi_backward(B, q, m, _p(mean.contiguous()), _p(L.contiguous()),
                                   _p(Z.reshape(S, q * m).contiguous()), S,
-                                  _p(cell_lo.contiguous()), _p(cell_hi.contiguous()),
-                                  cell_lo.shape[0], _p(dacq.contiguous()), _p(dmean), _p(dL),
+                                  _p(cell_lo.contiguous()), _p(cell_hi.contiguous()), K, cstride,
+                                  _p(Fc), Fc.shape[-1] if Fc is not None else 0,
+                                  Fc.shape[-1] * S if Fc is not None else 0, Qp,
+                                  _p(dacq.contiguous()), _p(dmean), _p(dL), _p(dF),
                                   _stream(dev)), "qehvi_backward")
+    if F is not None:
+        return dmean, dL, dF
     return dmean, dL
 
 

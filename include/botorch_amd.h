@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 3
+#define BO_ABI_VERSION 4
 
 /* status codes */
 #define BO_OK 0
@@ -260,16 +260,24 @@ int bo_mll_terms(int kind, const double* X, int64_t n, int d, const double* leng
  * q points of an m-output independent model (ModelListGP):
  *   f[s][p][t] = mean[t][b][p] + sum_j L[t][b][p][j] Z[s][j m + t]
  *   acq[b] = mean_s sum_k inclusion-exclusion volume.
- * mean: m x B x q, L: m x B x q x q, Z: S x (q m).  2 <= m <= 4, q <= 12. */
+ * mean: m x B x q, L: m x B x q x q, Z: S x (q m).  2 <= m <= 4, q <= 12.
+ * cell_stride 0: one set of K cells for every sample; > 0 (qNEHVI,
+ * NoisyExpectedHypervolumeMixin, botorch/utils/multi_objective/hypervolume.py:
+ * 507-835): sample s reads its own cells at cell_lo/hi + s * cell_stride (padded
+ * with empty cells as BoxDecompositionList does).  F (nullable): the cached-root
+ * baseline term added to f (m x S x ldF, output stride sF, row b * Qp + p). */
 int bo_qehvi(int B, int q, int m, const double* mean, const double* L, const double* Z, int S,
-             const double* cell_lo, const double* cell_hi, int K, double* acq, void* stream);
+             const double* cell_lo, const double* cell_hi, int K, int64_t cell_stride,
+             const double* F, int64_t ldF, int64_t sF, int Qp, double* acq, void* stream);
 
 /* Backward of bo_qehvi (autograd through _compute_qehvi,
  * multi_objective/monte_carlo.py:230-317): dacq (B) -> dmean (m x B x q) and
- * dL (m x B x q x q, lower) of the per-output posterior roots. */
+ * dL (m x B x q x q, lower) of the per-output posterior roots, and (with F)
+ * dF (the cotangent of F, same layout) from which dT = Z_base^T dF. */
 int bo_qehvi_backward(int B, int q, int m, const double* mean, const double* L, const double* Z,
                       int S, const double* cell_lo, const double* cell_hi, int K,
-                      const double* dacq, double* dmean, double* dL, void* stream);
+                      int64_t cell_stride, const double* F, int64_t ldF, int64_t sF, int Qp,
+                      const double* dacq, double* dmean, double* dL, double* dF, void* stream);
 
 /* Batched Cholesky backward (torch linalg.cholesky backward): L, dL (B x q x q,
  * lower) -> dA (B x q x q, symmetric), q <= 16. */

@@ -208,6 +208,98 @@ def qehvi(models, X, Z, cell_lower, cell_upper):
     return qehvi_from_samples(obj, cell_lower, cell_upper)
 
 
+# -- qNEHVI (multi_objective/monte_carlo.py:325-468; utils/multi_objective/
+#    hypervolume.py:507-835) ---------------------------------------------------------
+def hypervolume(Y, ref):
+    """Exact dominated hypervolume of the points Y (n x m, maximisation) above
+    ref, m in {2, 3}, by slicing (an independent restatement of what
+    DominatedPartitioning.compute_hypervolume returns, box_decompositions/
+    dominated.py; pinned by tests/golden hv_* fixtures)."""
+    Y = Y[(Y > ref).all(dim=-1)]
+    if Y.shape[0] == 0:
+        return Y.new_zeros(())
+    m = Y.shape[-1]
+    if m == 2:
+        order = torch.argsort(Y[:, 0], descending=True)
+        P = Y[order]
+        best2 = torch.cummax(P[:, 1], dim=0).values
+        x_next = torch.cat([P[1:, 0], ref[:1]])
+        return ((P[:, 0] - x_next) * (best2 - ref[1])).sum()
+    if m == 3:
+        order = torch.argsort(Y[:, 2], descending=True)
+        P = Y[order]
+        z_next = torch.cat([P[1:, 2], ref[2:3]])
+        total = Y.new_zeros(())
+        for i in range(P.shape[0]):
+            total = total + hypervolume(P[: i + 1, :2], ref[:2]) * (P[i, 2] - z_next[i])
+        return total
+    raise NotImplementedError("hypervolume oracle covers m = 2, 3")
+
+
+class QNEHVIOracle:
+    """qNoisyExpectedHypervolumeImprovement on a list of independent exact GPs
+    with the cached baseline root (cache_root=True, incremental, no pending
+    points): per MC sample s, the improvement of the new q points over the
+    hypervolume dominated by f_s(X_baseline), averaged over samples.
+
+    Base samples: the baseline draw has Sobol dimension r m (point-major,
+    output-minor: z[s, i m + t]); the forward draw has dimension (r + q) m with
+    its first r m columns replaced by the baseline draw
+    (sampling/normal.py:68-131), so the new points use columns r m + p m + t."""
+
+    def __init__(self, models, X_baseline, ref_point, S: int, seed: int):
+        self.models = models
+        self.Xb = X_baseline
+        self.ref = torch.as_tensor(ref_point, dtype=torch.float64)
+        self.S, self.seed = S, seed
+        r, m = X_baseline.shape[0], len(models)
+        self.Zb = draw_sobol_normal_samples(r * m, S, seed).view(S, r, m)
+        self.L_rr, base = [], []
+        for t, mdl in enumerate(models):
+            mean_b, cov_b = mdl.posterior(X_baseline)
+            Lb, _ = psd_safe_cholesky(cov_b)
+            self.L_rr.append(Lb)
+            base.append(mean_b.unsqueeze(0) + self.Zb[:, :, t] @ Lb.mT)
+        self.Y_base = torch.stack(base, dim=-1)  # S x r x m
+        self.initial_hv = torch.stack([hypervolume(self.Y_base[s], self.ref) for s in range(S)])
+
+    def samples(self, X):
+        """S x b x q x m joint samples at the new points."""
+        b, q, d = X.shape
+        r, m = self.Xb.shape[0], len(self.models)
+        Zq = draw_sobol_normal_samples((r + q) * m, self.S, self.seed).view(self.S, r + q, m)[:, r:, :]
+        out = []
+        Xf = torch.cat([self.Xb.expand(b, r, d), X], dim=-2)
+        for t, mdl in enumerate(self.models):
+            mean, cov = mdl.posterior(Xf)
+            bottom = cov[..., -q:, :]
+            bl = torch.linalg.solve_triangular(self.L_rr[t], bottom[..., :r].mT, upper=False).mT
+            br_chol, _ = psd_safe_cholesky(bottom[..., r:] - bl @ bl.mT)
+            f = (mean[..., -q:].unsqueeze(0) + torch.einsum("bir,sr->sbi", bl, self.Zb[:, :, t])
+                 + torch.einsum("bij,sj->sbi", br_chol, Zq[:, :, t]))
+            out.append(f)
+        return torch.stack(out, dim=-1)
+
+    def value_exact(self, X):
+        """mean_s [HV(front_s + new points) - HV(front_s)] by exact hypervolumes."""
+        f = self.samples(X).detach()
+        S, b = f.shape[0], f.shape[1]
+        res = torch.zeros(b, dtype=torch.float64)
+        for j in range(b):
+            acc = 0.0
+            for s in range(S):
+                acc += (hypervolume(torch.cat([self.Y_base[s], f[s, j]]), self.ref) - self.initial_hv[s]).item()
+            res[j] = acc / S
+        return res
+
+    def value_cells(self, X, cell_lo, cell_hi):
+        """The same quantity through per-sample hypercells (S x K x m; the
+        inclusion-exclusion of qehvi_from_samples per sample), differentiable."""
+        f = self.samples(X)  # S x b x q x m
+        vals = [qehvi_from_samples(f[s:s + 1], cell_lo[s], cell_hi[s]) for s in range(f.shape[0])]
+        return torch.stack(vals, dim=0).mean(dim=0)
+
+
 def saas_members(train_X, train_Y, mcmc_samples, standardize=False):
     """SaasFullyBayesianSingleTaskGP.load_mcmc_samples (models/fully_bayesian.py:
     267-312): one Matern-5/2 x outputscale exact GP per MCMC sample, noise

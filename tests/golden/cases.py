@@ -26,3 +26,6 @@ LOGEI_CASES = {
     "fat_wide": (True, 0.1, 0.5),
     "nofat_wide": (False, 0.1, 0.5),
 }
+
+# Dominated-hypervolume fixtures: (m objectives, n points).
+HV_CASES = [(2, 30), (3, 25), (3, 8)]

@@ -17,6 +17,8 @@ Sources (reference file:line):
   * NondominatedPartitioning / FastNondominatedPartitioning
                                botorch/utils/multi_objective/box_decompositions/non_dominated.py
   * is_non_dominated           botorch/utils/multi_objective/pareto.py:16-64
+  * DominatedPartitioning.compute_hypervolume
+                               botorch/utils/multi_objective/box_decompositions/dominated.py
   * log_fatplus / log_softplus / fatmax / smooth_amax / logmeanexp
                                botorch/utils/safe_math.py:209-352, composed as
                                acquisition/logei.py:122, 219-234, 509-534
@@ -31,7 +33,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import _refload  # noqa: E402
 
-from cases import LOGEI_CASES, SOBOL_BOX_CASES, SOBOL_NORMAL_CASES  # noqa: E402
+from cases import HV_CASES, LOGEI_CASES, SOBOL_BOX_CASES, SOBOL_NORMAL_CASES  # noqa: E402
 
 
 def main():
@@ -132,6 +134,24 @@ def main():
             (gx,) = torch.autograd.grad(acq.sum(), x)
             out[f"logei_{tag}_{bname}_acq"] = acq.detach().numpy()
             out[f"logei_{tag}_{bname}_grad"] = gx.numpy()
+
+    # Exact dominated hypervolumes (DominatedPartitioning.compute_hypervolume,
+    # box_decompositions/dominated.py) of random point sets, with and without
+    # one extra point: HV differences are the qNEHVI per-sample improvements.
+    dom = _refload.load("botorch.utils.multi_objective.box_decompositions.dominated")
+    g = torch.Generator().manual_seed(21)
+    for m_, n_ in HV_CASES:
+        Y = torch.rand(n_, m_, generator=g, dtype=torch.double)
+        ref = torch.full((m_,), 0.1, dtype=torch.double)
+        extra = torch.rand(4, m_, generator=g, dtype=torch.double) * 1.2
+        hv = dom.DominatedPartitioning(ref_point=ref, Y=Y).compute_hypervolume()
+        hv_plus = [dom.DominatedPartitioning(ref_point=ref, Y=torch.cat([Y, e.view(1, -1)]))
+                   .compute_hypervolume().item() for e in extra]
+        out[f"hv_m{m_}_n{n_}_Y"] = Y.numpy()
+        out[f"hv_m{m_}_n{n_}_ref"] = ref.numpy()
+        out[f"hv_m{m_}_n{n_}_hv"] = np.array(hv.item())
+        out[f"hv_m{m_}_n{n_}_extra"] = extra.numpy()
+        out[f"hv_m{m_}_n{n_}_hv_plus"] = np.array(hv_plus)
 
     path = os.path.join(HERE, "golden.npz")
     np.savez_compressed(path, **out)
