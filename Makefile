@@ -6,7 +6,10 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function \
             -Wno-unused-variable -munsafe-fp-atomics
 SRC := $(wildcard botorch_amd/csrc/*.hip)
-OBJ := $(patsubst botorch_amd/csrc/%.hip,build/%.o,$(SRC))
+CPPSRC := $(wildcard botorch_amd/csrc/*.cpp)
+OBJ := $(patsubst botorch_amd/csrc/%.hip,build/%.o,$(SRC)) $(patsubst botorch_amd/csrc/%.cpp,build/%.o,$(CPPSRC))
+CXX ?= g++
+CXXFLAGS ?= -O3 -std=c++17 -fPIC -pthread -Wall
 HDR := $(wildcard botorch_amd/csrc/*.h) include/botorch_amd.h
 LIB := botorch_amd/libbotorch_amd.so
 
@@ -16,8 +19,13 @@ build/%.o: botorch_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# host-only native code (no device code): plain g++
+build/%.o: botorch_amd/csrc/%.cpp $(HDR)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
 $(LIB): $(OBJ)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(OBJ) -o $@
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(OBJ) -pthread -o $@
 
 clean:
 	rm -rf build $(LIB)

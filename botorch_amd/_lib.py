@@ -69,6 +69,8 @@ _SIGNATURES = {
     "bo_sobol_normal": (c_int, [_P, _P, c_int, c_int64, c_int64, c_int, _P, _P]),
     "bo_lbfgs_step": (c_int, [c_int, c_int, c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P, _P, c_double, c_double, c_double, c_double, _P]),
+    "bo_nd_partition_host": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, POINTER(c_int64), _P,
+                                     _P, c_int]),
     "bo_sobol_box": (c_int, [_P, _P, c_int, c_int64, c_int64, c_int, _P, _P, c_int, _P, _P]),
     "bo_mll_terms": (c_int, [c_int, _P, c_int64, c_int, _P, c_double, _P, _P, c_int64, _P, _P, _P,
                              _P]),

@@ -912,9 +912,8 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
 
     def _set_cell_bounds(self) -> None:
         """hypervolume.py:627-700: baseline samples and one box decomposition per
-        MC sample (host), padded to a common cell count (box_decomposition_list.py:
-        62-94), then resident on the device."""
-        from .multi_objective import FastNondominatedPartitioning
+        MC sample (native host threads), padded to a common cell count
+        (box_decomposition_list.py:62-94), then resident on the device."""
         Xb = self.X_baseline
         models = self.model.models
         r, m = Xb.shape[-2], len(models)
@@ -928,14 +927,9 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
         if not all(rt.fused_ready for rt in self._roots):
             raise UnsupportedError(f"qNEHVI here needs d <= {kernels.DP}")
         Y = torch.stack([rt.samples for rt in self._roots], dim=-1).cpu()  # S x r x m
-        ref = self.ref_point.cpu()
-        bounds = [FastNondominatedPartitioning(ref, Y[s]).get_hypercell_bounds() for s in range(S)]
-        K = max(b.shape[-2] for b in bounds)
-        pad = [torch.cat([b, torch.zeros(2, K - b.shape[-2], m, dtype=b.dtype)], dim=-2)
-               if b.shape[-2] < K else b for b in bounds]
-        cells = torch.stack(pad, dim=1).to(Xb.device)  # 2 x S x K x m
-        self.cell_lower_bounds = cells[0].contiguous()
-        self.cell_upper_bounds = cells[1].contiguous()
+        lo, hi = kernels.nd_partition_host(Y, self.ref_point.cpu())  # native, threaded
+        self.cell_lower_bounds = lo.to(Xb.device)
+        self.cell_upper_bounds = hi.to(Xb.device)
         self._cells = (self.cell_lower_bounds, self.cell_upper_bounds)
         self.baseline_samples = Y
         self._zq = {}

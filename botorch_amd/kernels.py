@@ -9,6 +9,7 @@ from __future__ import annotations
 import collections
 import ctypes
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -471,6 +472,34 @@ def sample_mvn(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor) -> torch.Te
     check(lib().bo_gemm_f64(0, 1, S, q, q, 1.0, _p(Z), q, 0, _p(L), q, q * q, 0.0, _p(out), q,
                             S * q, B, 0, _stream(dev)), "sample_mvn")
     return out.permute(1, 0, 2) + mean.unsqueeze(0)
+
+
+def nd_partition_host(Y: torch.Tensor, ref_point: torch.Tensor, nthreads: int = 0):
+    """Exact non-dominated box decompositions of S point sets (host, native
+    threads): Y (S x n x m, or n x m) -> (lo, hi) each S x K x m (K x m for a
+    single set), padded with empty cells as BoxDecompositionList does."""
+    single = Y.dim() == 2
+    Yc = Y.detach().to("cpu", torch.float64).contiguous()
+    if single:
+        Yc = Yc.unsqueeze(0)
+    S, n, m = Yc.shape
+    ref = ref_point.detach().to("cpu", torch.float64).contiguous()
+    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    K = ctypes.c_int64(0)
+    cap = max(64, 8 * n)
+    while True:
+        lo = torch.empty(S, cap, m, dtype=torch.float64)
+        hi = torch.empty(S, cap, m, dtype=torch.float64)
+        st = lib().bo_nd_partition_host(_p(Yc), S, n, m, _p(ref), cap, ctypes.byref(K), _p(lo),
+                                        _p(hi), nthreads)
+        if st == _lib.BO_ERR_ARG and K.value > cap:
+            cap = int(K.value)  # one retry with the exact size
+            continue
+        check(st, "nd_partition_host")
+        break
+    Kc = max(int(K.value), 1)
+    lo, hi = lo[:, :Kc].contiguous(), hi[:, :Kc].contiguous()
+    return (lo[0], hi[0]) if single else (lo, hi)
 
 
 def _cells_layout(cell_lo: torch.Tensor, S: int):

@@ -313,6 +313,19 @@ int bo_lbfgs_step(int B, int n, int m, double* x, double* f, double* g, double* 
                   const double* lower, const double* upper, double c1, double ftol,
                   double pgtol, double min_alpha, void* stream);
 
+/* HOST function (plain host pointers; no GPU involved): exact non-dominated
+ * box decompositions of S point sets Y (S x n x m, maximisation) w.r.t. ref (m),
+ * FastNondominatedPartitioning per set (botorch/utils/multi_objective/
+ * box_decompositions/non_dominated.py:353-457, utils.py:103-288), padded with
+ * empty all-zero cells to the common maximum K (box_decomposition_list.py:
+ * 62-94).  *K_out receives K; with cell_lo / cell_hi NULL the call only sizes,
+ * else they receive S x K_cap x m (BO_ERR_ARG if K > K_cap).  The per-sample
+ * decompositions of qNEHVI (utils/multi_objective/hypervolume.py:680-700) run
+ * on `nthreads` host threads. */
+int bo_nd_partition_host(const double* Y, int64_t S, int64_t n, int m, const double* ref,
+                         int64_t K_cap, int64_t* K_out, double* cell_lo, double* cell_hi,
+                         int nthreads);
+
 /* Scrambled Sobol raw designs in a box, points skip..skip+n-1: out (n x dim),
  * dim = q * d, out[i][j] = lower[j % d] + range[j % d] * u_i[j] (device
  * lower/range of length d).  Same engine state as bo_sobol_normal.
