@@ -36,6 +36,9 @@ _SIGNATURES = {
     "bo_covar_matrix": (c_int, [c_int, _P, c_int64, _P, c_int64, c_int, _P, c_double, c_double,
                                 c_int, _P, c_int64, c_int64, c_int64, _P]),
     "bo_padded_order": (c_int64, [c_int64]),
+    "bo_covar_batched": (c_int, [c_int, _P, c_int64, c_int64, c_int, _P, c_int64, c_int64, c_int,
+                                 c_int, _P, c_int64, c_int64, _P, c_int64, c_int64, _P, c_int64,
+                                 c_int64, c_int64, c_int, c_int, _P]),
     "bo_cholesky_inverse": (c_int, [_P, _P, _P, c_int64, _P, _P]),
     "bo_transpose": (c_int, [_P, _P, c_int64, c_int64, _P]),
     "bo_cholesky_jitter": (c_int, [_P, c_int64, _P, _P, _P, c_int, c_double, POINTER(c_double),

@@ -186,68 +186,71 @@ class qExpectedImprovement(MCAcquisitionFunction):
 
 class _SaasQEI(torch.autograd.Function):
     """qEI over the MCMC ensemble of a SAAS model (models/fully_bayesian.py:509-546,
-    averaged over MCMC_DIM as utils/transforms.py:289-293), any d <= 128.
+    averaged over MCMC_DIM as utils/transforms.py:289-293), any d <= 128, with
+    all M members batched into each launch.
 
-    Per member m (exact GP, Matern-5/2 x outputscale): K*x (bo_covar_matrix),
-    R = K*x L^{-T} and the R R^T blocks (MFMA GEMMs), jittered q x q root
-    (bo_cholesky ladder), reparameterised samples (batched GEMM) and the qEI
-    reduction (bo_mc_reduce).  Backward: bo_qmc_backward -> d mu, d Sigma;
-    d K*x = d mu alpha^T - G W (W = R L^{-1}); bo_kernel_grad for K*x and K**."""
+    Forward: K*x of every member (one bo_covar_batched, Matern-5/2 x outputscale),
+    R = K*x L_m^{-T} and the means (batched MFMA GEMMs over M), the R R^T blocks
+    (batched over M x B), K** (one bo_covar_batched over M x B), the jittered
+    q x q roots (bo_chol_small over M x B), reparameterised samples (one batched
+    GEMM) and the qEI reduction (bo_mc_reduce over M x B), averaged over M.
+    Backward: bo_qmc_backward over M x B -> d mu, d Sigma; d K*x = d mu alpha^T
+    - G W (W = R L^{-1}, batched GEMMs); bo_kernel_grad per member for K*x and K**."""
 
     @staticmethod
     def forward(ctx, X3, acqf, best_f, Z):
         model = acqf.model
         B, q, d = X3.shape
+        dev = X3.device
         X2 = X3.detach().reshape(B * q, d).contiguous()
         need_grad = ctx.needs_input_grad[0]
         ym, ys = 0.0, 1.0
         if hasattr(model, "outcome_transform"):
             ym = float(model.outcome_transform.means.reshape(-1)[0])
             ys = float(model.outcome_transform.stdvs.reshape(-1)[0])
-        acq = None
-        saved = []
-        M = model.num_mcmc_samples
-        for mdl in model._members:
-            cache = mdl.prediction_cache()
-            n = cache.n
-            Kx = kernels.covar_matrix(X2, cache.Xt, cache.lengthscale, cache.kind, cache.outputscale)
-            R = kernels.gemm(Kx, cache.U[:n, :n], flags=_lib.GEMM_B_UPPER)
-            mean = kernels.gemm(Kx, cache.alpha.reshape(n, 1)).reshape(B, q)
-            RR = kernels.gemm(R.reshape(B, q, n), R.reshape(B, q, n), transB=True)
-            Kxx = kernels.covar_blocks(X3.detach(), cache.lengthscale, cache.kind, cache.outputscale)
-            cov = (Kxx - RR) * (ys * ys)
-            mean = ym + ys * (mean + cache.constant)
-            L = kernels.chol_jitter(cov)
-            f = kernels.sample_mvn(mean, L, Z)
-            a_m = kernels.mc_reduce(f, best_f)
-            acq = a_m if acq is None else acq + a_m
-            if need_grad:
-                saved.append((cache, Kx, R, mean, L))
-        acq = acq / M
+        ens = model.ensemble_cache()
+        M, n = ens["U"].shape[0], ens["n"]
+        f64 = dict(dtype=torch.float64, device=dev)
+        Bq = B * q
+        Kx = torch.empty(M, Bq, n, **f64)
+        kernels.covar_batched(ens["kind"], X2, (0, 0), Bq, ens["Xt"], (0, 0), n, d, ens["ls"],
+                              (d, 0), ens["os"], (1, 0), Kx, (Bq * n, 0), n, M, 1)
+        R = kernels.gemm(Kx, ens["U"], flags=_lib.GEMM_B_UPPER)              # M x Bq x n
+        mean = kernels.gemm(Kx, ens["alpha"].unsqueeze(-1)).reshape(M, B, q)
+        RR = kernels.gemm(R.view(M * B, q, n), R.view(M * B, q, n), transB=True)  # MB x q x q
+        Kxx = torch.empty(M * B, q, q, **f64)
+        kernels.covar_batched(ens["kind"], X2, (0, q * d), q, X2, (0, q * d), q, d, ens["ls"],
+                              (d, 0), ens["os"], (1, 0), Kxx, (B * q * q, q * q), q, M, B)
+        cov = (Kxx - RR) * (ys * ys)
+        mean = ym + ys * (mean + ens["const"].view(M, 1, 1))
+        L = kernels.chol_jitter(cov)                                          # MB x q x q
+        f = kernels.sample_mvn(mean.reshape(M * B, q), L, Z)                  # S x MB x q
+        acq = kernels.mc_reduce(f, best_f).view(M, B).mean(dim=0)
         if need_grad:
-            ctx.saved, ctx.X2, ctx.Z, ctx.best_f, ctx.shape, ctx.ys, ctx.M = (
-                saved, X2, Z, best_f, (B, q, d), ys, M)
+            ctx.ens, ctx.X2, ctx.Z, ctx.best_f, ctx.shape, ctx.ys = ens, X2, Z, best_f, (B, q, d), ys
+            ctx.R, ctx.mean, ctx.L = R, mean.reshape(M * B, q), L
         return acq
 
     @staticmethod
     def backward(ctx, dacq):
         B, q, d = ctx.shape
-        ys = ctx.ys
+        ens, ys = ctx.ens, ctx.ys
+        M, n = ens["U"].shape[0], ens["n"]
+        da = (dacq / M).repeat(M).contiguous()                                # MB
+        dmean, dcov = kernels.qmc_backward(_lib.QMC_QEI, ctx.mean, ctx.L, ctx.Z, da, ctx.best_f)
+        dmu = (ys * dmean).reshape(M, B * q)                                  # standardized
+        G = ((ys * ys) * (dcov + dcov.mT)).contiguous()                       # MB x q x q
+        W = kernels.gemm(ctx.R, ens["U"], transB=True, flags=_lib.GEMM_B_LOWER)  # M x Bq x n
+        dK = (dmu.unsqueeze(-1) * ens["alpha"].unsqueeze(1)).contiguous()    # M x Bq x n
+        kernels.gemm(G, W.view(M * B, q, n), alpha=-1.0, beta=1.0, C=dK.view(M * B, q, n))
+        Gm = G.view(M, B * q, q)
         dX = None
-        da = (dacq / ctx.M).contiguous()
-        for cache, Kx, R, mean, L in ctx.saved:
-            n = cache.n
-            dmean, dcov = kernels.qmc_backward(_lib.QMC_QEI, mean, L, ctx.Z, da, ctx.best_f)
-            dmu = ys * dmean                                   # standardized space
-            G = (ys * ys) * (dcov + dcov.mT)
-            W = kernels.gemm(R, cache.U[:n, :n], transB=True, flags=_lib.GEMM_B_LOWER)
-            dK = dmu.reshape(B * q, 1) * cache.alpha.reshape(1, n)
-            kernels.gemm(G.contiguous(), W.reshape(B, q, n), alpha=-1.0, beta=1.0,
-                         C=dK.reshape(B, q, n))
-            dX = kernels.kernel_grad(ctx.X2, cache.Xt, dK, cache.lengthscale, cache.kind,
-                                     cache.outputscale, dX=dX)
-            dX = kernels.kernel_grad(ctx.X2, ctx.X2, G.reshape(B * q, q), cache.lengthscale,
-                                     cache.kind, cache.outputscale, group=q, dX=dX)
+        for mi in range(M):
+            ls = ens["ls"][mi]
+            os_ = ens["os_host"][mi]
+            dX = kernels.kernel_grad(ctx.X2, ens["Xt"], dK[mi], ls, ens["kind"], os_, dX=dX)
+            dX = kernels.kernel_grad(ctx.X2, ctx.X2, Gm[mi].contiguous(), ls, ens["kind"], os_,
+                                     group=q, dX=dX)
         return dX.reshape(B, q, d), None, None, None
 
 

@@ -57,6 +57,36 @@ __global__ __launch_bounds__(256) void covar_matrix_kernel(
   K[i * ldk + j] = v;
 }
 
+// Two-level batched covariance: batch z = o * inner + i reads its inputs at
+// X1 + o s1o + i s1i (n1 x d), X2 + o s2o + i s2i (n2 x d), its lengthscales at
+// ls + o slo + i sli (d) and outputscale os[o soo + i soi], and writes
+// K + o sKo + i sKi (n1 x n2, leading dimension ldk).  The SAAS ensemble
+// (models/fully_bayesian.py:276-281) evaluates all M members' K*x (outer = M,
+// shared test rows) and all M x B q x q blocks K** (outer = M, inner = B) in
+// one launch each.
+template <int KIND>
+__global__ __launch_bounds__(256) void covar_batched_kernel(
+    const double* __restrict__ X1, int64_t s1o, int64_t s1i, int n1,
+    const double* __restrict__ X2, int64_t s2o, int64_t s2i, int n2, int d,
+    const double* __restrict__ ls, int64_t slo, int64_t sli, const double* __restrict__ os,
+    int64_t soo, int64_t soi, double* __restrict__ K, int64_t sKo, int64_t sKi, int64_t ldk,
+    int inner) {
+  const int z = blockIdx.z;
+  const int o = z / inner, i = z % inner;
+  const int row = blockIdx.y;
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= n1 || col >= n2) return;
+  const double* x1 = X1 + o * s1o + i * s1i + (int64_t)row * d;
+  const double* x2 = X2 + o * s2o + i * s2i + (int64_t)col * d;
+  const double* l = ls + o * slo + i * sli;
+  double d2 = 0.0;
+  for (int t = 0; t < d; ++t) {
+    const double diff = (x1[t] - x2[t]) / l[t];
+    d2 = fma(diff, diff, d2);
+  }
+  K[o * sKo + i * sKi + (int64_t)row * ldk + col] = os[o * soo + i * soi] * kernel_from_d2<KIND>(d2);
+}
+
 __global__ void transpose_kernel(const double* __restrict__ A, double* __restrict__ B,
                                  int64_t n, int64_t ld) {
   __shared__ double tile[32][33];
@@ -154,6 +184,30 @@ int bo_covar_matrix(int kind, const double* X1, int64_t n1, const double* X2, in
     covar_matrix_kernel<BO_RBF><<<grid, 256, 0, st>>>(X1, n1, X2, n2, d, lengthscale, outputscale, diag_add, mode, K, ldk, rows, cols);
   else
     covar_matrix_kernel<BO_MATERN52><<<grid, 256, 0, st>>>(X1, n1, X2, n2, d, lengthscale, outputscale, diag_add, mode, K, ldk, rows, cols);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+int bo_covar_batched(int kind, const double* X1, int64_t s1o, int64_t s1i, int n1,
+                     const double* X2, int64_t s2o, int64_t s2i, int n2, int d, const double* ls,
+                     int64_t slo, int64_t sli, const double* os, int64_t soo, int64_t soi,
+                     double* K, int64_t sKo, int64_t sKi, int64_t ldk, int outer, int inner,
+                     void* stream) {
+  BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bo_covar_batched: bad kind %d", kind);
+  BO_CHECK_ARG(d > 0 && n1 >= 0 && n2 >= 0 && ldk >= n2 && outer >= 1 && inner >= 1,
+               "bo_covar_batched: bad shape");
+  BO_CHECK_ARG(n1 <= 65535 && (int64_t)outer * inner <= 65535, "bo_covar_batched: grid too large");
+  if (n1 == 0 || n2 == 0) return BO_OK;
+  dim3 grid((unsigned)ceil_div(n2, 256), (unsigned)n1, (unsigned)(outer * inner));
+  hipStream_t st = as_stream(stream);
+  if (kind == BO_RBF)
+    covar_batched_kernel<BO_RBF><<<grid, 256, 0, st>>>(X1, s1o, s1i, n1, X2, s2o, s2i, n2, d, ls,
+                                                         slo, sli, os, soo, soi, K, sKo, sKi, ldk,
+                                                         inner);
+  else
+    covar_batched_kernel<BO_MATERN52><<<grid, 256, 0, st>>>(X1, s1o, s1i, n1, X2, s2o, s2i, n2, d,
+                                                              ls, slo, sli, os, soo, soi, K, sKo,
+                                                              sKi, ldk, inner);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

@@ -101,6 +101,16 @@ def covar_matrix(X1, X2, lengthscale, kind=_lib.RBF, outputscale=1.0, diag_add=0
     return K
 
 
+def covar_batched(kind, X1, s1, n1, X2, s2, n2, d, ls, sl, os_, so, K, sK, ldk, outer, inner):
+    """bo_covar_batched on raw storage: every stride argument is an (outer, inner)
+    pair of element strides."""
+    dev = _dev(X1, X2, ls, os_, K)
+    check(lib().bo_covar_batched(kind, _p(X1), s1[0], s1[1], n1, _p(X2), s2[0], s2[1], n2, d,
+                                 _p(ls), sl[0], sl[1], _p(os_), so[0], so[1], _p(K), sK[0], sK[1],
+                                 ldk, outer, inner, _stream(dev)), "covar_batched")
+    return K
+
+
 def padded_order(n: int) -> int:
     return int(lib().bo_padded_order(n))
 

@@ -388,6 +388,29 @@ class SaasFullyBayesianSingleTaskGP(Model):
         self.train_inputs = (train_X,)
         self.train_targets = train_Y.squeeze(-1)
         self._members = None
+        self._ens = None
+        self._ens_key = None
+
+    def ensemble_cache(self):
+        """The members' prediction caches stacked for the batched ensemble path:
+        U (M x n x n, each L_m^{-T}), alpha (M x n), lengthscale (M x d),
+        outputscale (M), constant (M); rebuilt whenever a member's cache is."""
+        caches = [m.prediction_cache() for m in self._members]
+        key = tuple(id(c) for c in caches)
+        if self._ens is None or self._ens_key != key:
+            n = caches[0].n
+            dev = caches[0].U.device
+            f64 = dict(dtype=torch.float64, device=dev)
+            self._ens = dict(
+                n=n, kind=caches[0].kind, Xt=caches[0].Xt.contiguous(),
+                U=torch.stack([c.U[:n, :n] for c in caches]).contiguous(),
+                alpha=torch.stack([c.alpha.reshape(-1)[:n] for c in caches]).contiguous(),
+                ls=torch.stack([c.lengthscale.reshape(-1) for c in caches]).contiguous(),
+                os=torch.tensor([c.outputscale for c in caches], **f64),
+                os_host=[float(c.outputscale) for c in caches],
+                const=torch.tensor([c.constant for c in caches], **f64))
+            self._ens_key = key
+        return self._ens
 
     def load_mcmc_samples(self, mcmc_samples) -> None:
         """models/fully_bayesian.py:249-312 (batched modules from the samples)."""
@@ -407,6 +430,7 @@ class SaasFullyBayesianSingleTaskGP(Model):
                                mean_module=mean, outcome_transform=None)
             members.append(mdl.eval())
         self._members = nn.ModuleList(members)
+        self._ens = None
 
     @property
     def num_mcmc_samples(self) -> int:

@@ -93,6 +93,19 @@ int bo_covar_matrix(int kind, const double* X1, int64_t n1, const double* X2, in
 /* Padded order np used by every n x n cache below (multiple of 128). */
 int64_t bo_padded_order(int64_t n);
 
+/* Two-level batched covariance (batch z = o * inner + i, o < outer, i < inner):
+ * K[o][i] (n1 x n2, leading dim ldk, at K + o sKo + i sKi) =
+ *   os[o soo + i soi] * k((X1[o][i] - X2[o][i]) / ls[o][i]),
+ * X1 at X1 + o s1o + i s1i (n1 x d), X2 likewise, ls at ls + o slo + i sli (d).
+ * Strides are in elements (0 = shared).  The SAAS ensemble's K*x of all M
+ * members and K** of all M x B t-batches (models/fully_bayesian.py:276-281),
+ * one launch each. */
+int bo_covar_batched(int kind, const double* X1, int64_t s1o, int64_t s1i, int n1,
+                     const double* X2, int64_t s2o, int64_t s2i, int n2, int d, const double* ls,
+                     int64_t slo, int64_t sli, const double* os, int64_t soo, int64_t soi,
+                     double* K, int64_t sKo, int64_t sKi, int64_t ldk, int outer, int inner,
+                     void* stream);
+
 /* In-place blocked Cholesky of the lower-stored SPD matrix A (np x np, upper
  * triangle zero) and its explicit inverse Linv (np x np).  work: np x np
  * scratch.  *info (device int) = 0 or the 1-based order of the first failing
