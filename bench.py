@@ -585,6 +585,7 @@ def main():
             line["speedup_vs_cpu"] = value / cpu["value"]
         print(json.dumps(line), flush=True)
     if dist is not None:
+        dist.barrier()  # rank 0's CPU baseline / report must finish before teardown
         dist.destroy_process_group()
 
 

@@ -20,6 +20,12 @@
 // R beta; post_finalize sums them over the column tiles.  R itself is never
 // materialised (C3: 268 MB saved per forward).
 //
+// Small problems (C2: 8 column tiles x 4 row tiles = 32 workgroups for 256
+// CUs) run split-k: each column tile's triangular k-range is cut into chunks,
+// every (chunk, column tile, row tile) is a workgroup that writes its partial
+// R^T accumulators to a workspace, and post_splitk_reduce_kernel sums the
+// chunks in chunk order (deterministic) and runs the same epilogue.
+//
 // Test rows are laid out per t-batch: row b*Qp + a, a < q, Qp = q rounded up
 // to a power of two <= 16, so every t-batch sits inside one 16-row MFMA tile.
 #include "common.h"
@@ -31,6 +37,8 @@ constexpr int PI = 128;   // test rows i per workgroup
 constexpr int PK = 16;    // k-step
 constexpr int PLD = 144;  // LDS row pitch (doubles): 2 x 144 dwords = 32 mod 64 banks
 constexpr int DP = 8;     // padded input dimension held in registers
+constexpr int kSplitMinWgs = 256;      // split-k below this many (column, row) tiles
+constexpr int kTileDoubles = 32 * 64;  // one 16-row x 128-column R^T tile
 
 // One kernel value k(x_i, x_k) from scaled coordinates (0 beyond n / invalid rows).
 template <int KIND, int ND>
@@ -47,12 +55,74 @@ __device__ __forceinline__ double eval_kernel_row(const double (&xi)[ND], const 
   return outputscale * kernel_from_d2<KIND>(d2);
 }
 
-template <int KIND, int ND>
+// Number of k-chunks of column tile ci, and the chunks of all tiles before it
+// (the split-k workspace stores only non-empty chunks).
+__host__ __device__ __forceinline__ int splitk_chunks(int ci, int n, int kc_len) {
+  const int e = ci * PC + PC;
+  const int kfull = n < e ? n : e;
+  return (kfull + kc_len - 1) / kc_len;
+}
+__host__ __device__ __forceinline__ int64_t splitk_base(int ci, int n, int kc_len) {
+  int64_t s = 0;
+  for (int c = 0; c < ci; ++c) s += splitk_chunks(c, n, kc_len);
+  return s;
+}
+
+// Epilogue of one 16-row tile (rows row0..row0+15) of column tile ci, given
+// its R^T accumulators acc[ct] (columns ci*128 + 16 ct + mfma_row, rows row0 +
+// mfma_col).  post_store_rt: the R^T store of the gradient path (lanes 0-15
+// hold consecutive test rows, so each store writes 128-B row segments).
+// post_epilogue: the 16 x 16 block of R R^T over the tile's 128 columns (the
+// accumulator register is a valid A and B operand at once: 4 MFMAs per
+// accumulator, no data movement) and the partial R beta.
+__device__ __forceinline__ void post_store_rt(const v4d (&acc)[8], int ci, int row0, int lane,
+                                              int nI, double* __restrict__ Rt) {
+  const int c0 = ci * PC;
+  const int nrows_pad = nI * PI;
+#pragma unroll
+  for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = c0 + ct * 16 + mfma_row(lane, r);
+      Rt[(int64_t)c * nrows_pad + row0 + mfma_col(lane)] = acc[ct][r];
+    }
+}
+
+__device__ __forceinline__ void post_epilogue(const v4d (&acc)[8], int ci, int row0, int lane,
+                                              int n, const double* __restrict__ beta, int nI,
+                                              double* __restrict__ Spart,
+                                              double* __restrict__ mpart) {
+  const int c0 = ci * PC;
+  const int nrows16 = nI * (PI / 16);
+  const int nrows_pad = nI * PI;
+  v4d P = v4d_zero();
+#pragma unroll
+  for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) P = mfma_f64(acc[ct][r], acc[ct][r], P);
+  double* sp = Spart + ((int64_t)ci * nrows16 + row0 / 16) * 256;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) sp[mfma_row(lane, r) * 16 + mfma_col(lane)] = P[r];
+
+  double m = 0.0;
+#pragma unroll
+  for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = c0 + ct * 16 + mfma_row(lane, r);
+      m = fma(acc[ct][r], (c < n) ? beta[c] : 0.0, m);
+    }
+  m += __shfl_xor(m, 16);
+  m += __shfl_xor(m, 32);
+  if (lane < 16) mpart[(int64_t)ci * nrows_pad + row0 + lane] = m;
+}
+
+template <int KIND, int ND, bool SPLIT>
 __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     const double* __restrict__ Xq, int nrows, const double* __restrict__ Xt, int n,
     const double* __restrict__ U, int64_t ldu, const double* __restrict__ beta,
     double outputscale, int nC, int nI, double* __restrict__ Spart, double* __restrict__ mpart,
-    double* __restrict__ Rt) {
+    double* __restrict__ Rt, int kc_len, double* __restrict__ work) {
   // Two LDS stages: while the MFMAs consume stage t, the U rows of step t+1
   // are in flight to registers and this thread evaluates its 8 kernel values
   // of step t+1 between the MFMAs (VALU work hidden under the matrix pipe);
@@ -60,24 +130,38 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   __shared__ __attribute__((aligned(16))) double Us[2][PK][PLD];
   __shared__ __attribute__((aligned(16))) double Ks[2][PK][PLD];
 
-  // XCD-aware schedule: consecutive block ids are dealt round-robin over the
-  // 8 XCDs, so block b and b+8 share an L2.  XCD x takes the column tiles
-  // ci with (descending position) % 8 == x, heaviest (largest ci, longest
-  // triangular k-range) first, and sweeps all test-row tiles of a column tile
-  // back to back: the U panel of that column tile is read once into the XCD's
-  // L2 and reused by all of them.  Placement only affects speed.
   const int bid = blockIdx.x;
-  const int xcd = bid & 7;
-  const int slot = bid >> 3;
-  const int jj = slot / nI;
-  const int ii = slot - jj * nI;
-  const int pos = jj * 8 + xcd;
-  if (pos >= nC) return;
-  const int ci = nC - 1 - pos;
+  int ci, ii, kc = 0, kbeg = 0, kend;
+  if constexpr (SPLIT) {
+    // Split-k: block -> (column tile, chunk, row tile), row tiles fastest so
+    // neighbouring blocks read the same U chunk.
+    const int nk = (n + kc_len - 1) / kc_len;
+    ii = bid % nI;
+    const int rest = bid / nI;
+    kc = rest % nk;
+    ci = rest / nk;
+    if (ci >= nC || kc >= splitk_chunks(ci, n, kc_len)) return;
+    kbeg = kc * kc_len;
+    kend = min(min(n, ci * PC + PC), kbeg + kc_len);
+  } else {
+    // XCD-aware schedule: consecutive block ids are dealt round-robin over the
+    // 8 XCDs, so block b and b+8 share an L2.  XCD x takes the column tiles
+    // ci with (descending position) % 8 == x, heaviest (largest ci, longest
+    // triangular k-range) first, and sweeps all test-row tiles of a column
+    // tile back to back: the U panel of that column tile is read once into the
+    // XCD's L2 and reused by all of them.  Placement only affects speed.
+    const int xcd = bid & 7;
+    const int slot = bid >> 3;
+    const int jj = slot / nI;
+    ii = slot - jj * nI;
+    const int pos = jj * 8 + xcd;
+    if (pos >= nC) return;
+    ci = nC - 1 - pos;
+    kend = min(n, ci * PC + PC);
+  }
   const int c0 = ci * PC;
   const int i0 = ii * PI;
-  const int kend = min(n, c0 + PC);
-  const int nsteps = (kend + PK - 1) / PK;
+  const int nsteps = (kend - kbeg + PK - 1) / PK;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -92,7 +176,7 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
 #pragma unroll
   for (int t = 0; t < ND; ++t) xi[t] = ivalid ? Xq[(int64_t)(i0 + ti) * DP + t] : 0.0;
 
-  v4d acc[8][2];
+  v4d acc[8][2];  // [16-column sub-tile ct][16-row sub-tile it]
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
     acc[a][0] = v4d_zero();
@@ -124,15 +208,16 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     _Pragma("unroll") for (int kk = 0; kk < 8; ++kk) Ks[BUF][kh * 8 + kk][ti] = kv[kk]; \
   }
 
-  BO_LOAD_U(0);
+  BO_LOAD_U(kbeg);
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) kv[kk] = eval_kernel_row<KIND, ND>(xi, Xt, n, kh * 8 + kk, outputscale, ivalid);
+  for (int kk = 0; kk < 8; ++kk)
+    kv[kk] = eval_kernel_row<KIND, ND>(xi, Xt, n, kbeg + kh * 8 + kk, outputscale, ivalid);
   BO_STORE(0);
   __syncthreads();
   for (int t = 0; t < nsteps; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < nsteps;
-    const int knext = more ? (t + 1) * PK : t * PK;  // last step re-reads (unused)
+    const int knext = kbeg + (more ? (t + 1) * PK : t * PK);  // last step re-reads (unused)
     BO_LOAD_U(knext);
 #pragma unroll
     for (int ks = 0; ks < PK / 4; ++ks) {
@@ -155,49 +240,87 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
 #undef BO_LOAD_U
 #undef BO_STORE
 
-  // Epilogue: R R^T diagonal blocks and R beta for this workgroup's columns.
-  const int nrows16 = nI * (PI / 16);
-  const int nrows_pad = nI * PI;
-  if (Rt != nullptr) {
-    // Gradient path: keep R^T (column c, test row i; ld = nrows_pad) for the
-    // backward's W = R L^{-1}... product.  Lanes 0-15 hold consecutive test rows,
-    // so each store instruction writes 128-B contiguous row segments.
+  if constexpr (SPLIT) {
+    // Partial R^T of this chunk: register-major, lane-minor per 16-row tile,
+    // so every store instruction writes 512 contiguous bytes.
+    const int64_t chunk = splitk_base(ci, n, kc_len) + kc;
 #pragma unroll
-    for (int ct = 0; ct < 8; ++ct)
+    for (int it = 0; it < 2; ++it) {
+      const int rt = ii * (PI / 16) + wave * 2 + it;
+      double* w = work + (chunk * (nI * (PI / 16)) + rt) * kTileDoubles + lane;
 #pragma unroll
-      for (int it = 0; it < 2; ++it)
+      for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[(ct * 4 + r) * 64] = acc[ct][it][r];
+    }
+  } else {
+    // Same epilogue as post_store_rt + post_epilogue, written out over the
+    // [ct][it] accumulators (passing sub-arrays costs this kernel spills).
+    const int nrows16 = nI * (PI / 16);
+    const int nrows_pad = nI * PI;
+    if (Rt != nullptr) {
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = c0 + ct * 16 + mfma_row(lane, r);
+            const int i = i0 + wave * 32 + it * 16 + mfma_col(lane);
+            Rt[(int64_t)c * nrows_pad + i] = acc[ct][it][r];
+          }
+    }
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      v4d P = v4d_zero();
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) P = mfma_f64(acc[ct][it][r], acc[ct][it][r], P);
+      const int row0 = i0 + wave * 32 + it * 16;
+      double* sp = Spart + ((int64_t)ci * nrows16 + row0 / 16) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sp[mfma_row(lane, r) * 16 + mfma_col(lane)] = P[r];
+      double m = 0.0;
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = c0 + ct * 16 + mfma_row(lane, r);
-          const int i = i0 + wave * 32 + it * 16 + mfma_col(lane);
-          Rt[(int64_t)c * nrows_pad + i] = acc[ct][it][r];
+          m = fma(acc[ct][it][r], (c < n) ? beta[c] : 0.0, m);
         }
+      m += __shfl_xor(m, 16);
+      m += __shfl_xor(m, 32);
+      if (lane < 16) mpart[(int64_t)ci * nrows_pad + row0 + lane] = m;
+    }
   }
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    v4d P = v4d_zero();
-#pragma unroll
-    for (int ct = 0; ct < 8; ++ct)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) P = mfma_f64(acc[ct][it][r], acc[ct][it][r], P);
-    const int row0 = i0 + wave * 32 + it * 16;
-    const int64_t tile = (int64_t)ci * nrows16 + row0 / 16;
-    double* sp = Spart + tile * 256;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sp[mfma_row(lane, r) * 16 + mfma_col(lane)] = P[r];
+}
 
-    double m = 0.0;
+// Split-k reduction: one wave per (column tile, 16-row tile) sums the chunk
+// partials in chunk order and runs the epilogue.
+__global__ __launch_bounds__(64) void post_splitk_reduce_kernel(
+    const double* __restrict__ work, int n, int nC, int nI, int kc_len,
+    const double* __restrict__ beta, double* __restrict__ Spart, double* __restrict__ mpart,
+    double* __restrict__ Rt) {
+  const int nrows16 = nI * (PI / 16);
+  const int rt = blockIdx.x % nrows16;
+  const int ci = blockIdx.x / nrows16;
+  if (ci >= nC) return;
+  const int lane = threadIdx.x;
+  const int nk = splitk_chunks(ci, n, kc_len);
+  const int64_t base = splitk_base(ci, n, kc_len);
+  v4d acc[8];
+#pragma unroll
+  for (int ct = 0; ct < 8; ++ct) acc[ct] = v4d_zero();
+  for (int kc = 0; kc < nk; ++kc) {
+    const double* w = work + ((base + kc) * nrows16 + rt) * kTileDoubles + lane;
 #pragma unroll
     for (int ct = 0; ct < 8; ++ct)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = c0 + ct * 16 + mfma_row(lane, r);
-        m = fma(acc[ct][it][r], (c < n) ? beta[c] : 0.0, m);
-      }
-    m += __shfl_xor(m, 16);
-    m += __shfl_xor(m, 32);
-    if (lane < 16) mpart[(int64_t)ci * nrows_pad + row0 + lane] = m;
+      for (int r = 0; r < 4; ++r) acc[ct][r] += w[(ct * 4 + r) * 64];
   }
+  if (Rt != nullptr) post_store_rt(acc, ci, rt * 16, lane, nI, Rt);
+  post_epilogue(acc, ci, rt * 16, lane, n, beta, nI, Spart, mpart);
 }
 
 // Scatter X (B x q x d) into the padded, lengthscale-scaled row layout
@@ -230,6 +353,30 @@ int bo_post_geometry(int64_t B, int q, int64_t n, int* Qp, int* nrows_pad, int* 
   return BO_OK;
 }
 
+int bo_post_split_plan(int64_t B, int q, int64_t n, int min_wgs, int* kc_len,
+                       int64_t* work_elems) {
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  const int64_t nI = nrows_pad / PI;
+  if (min_wgs <= 0) min_wgs = kSplitMinWgs;
+  *kc_len = 0;
+  *work_elems = 0;
+  if ((int64_t)nC * nI >= min_wgs) return BO_OK;
+  // Largest power-of-two chunk (64..1024 rows) that yields min_wgs workgroups:
+  // fewer chunks mean less workspace traffic and a shorter reduction.
+  int best = 0;
+  for (int kc = 1024; kc >= 64; kc /= 2) {
+    if (kc >= n) continue;
+    best = kc;
+    if (splitk_base(nC, (int)n, kc) * nI >= min_wgs) break;
+  }
+  if (best == 0) return BO_OK;
+  *kc_len = best;
+  *work_elems = splitk_base(nC, (int)n, best) * nrows_pad * PC;
+  return BO_OK;
+}
+
 int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthscale,
                     double* Xq, void* stream) {
   BO_CHECK_ARG(d <= DP, "fused posterior kernel supports d <= %d (got %d)", DP, d);
@@ -246,23 +393,32 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
 int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
                      const double* Xt_scaled, int64_t n, const double* U, int64_t ldu, const double* beta,
                      double outputscale, double* Spart, double* mpart, double* Rt,
-                     void* stream) {
+                     int kc_len, double* work, void* stream) {
   BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
   BO_CHECK_ARG(ldu % 2 == 0 && ldu >= ceil_div(n, PC) * PC, "U leading dim %lld too small",
                (long long)ldu);
+  BO_CHECK_ARG(kc_len == 0 || (kc_len > 0 && kc_len % PK == 0 && work != nullptr),
+               "split-k chunk %d must be a positive multiple of %d with a workspace", kc_len, PK);
   int Qp, nrows_pad, nC;
   int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
   if (s) return s;
   const int nI = nrows_pad / PI;
   const int nrows = B * Qp;
   BO_CHECK_ARG(d >= 1 && d <= DP, "fused posterior kernel supports 1 <= d <= %d", DP);
-  const int64_t blocks = 8 * ceil_div(nC, 8) * (int64_t)nI;
+  const int64_t blocks = kc_len > 0 ? (int64_t)nC * ceil_div(n, kc_len) * nI
+                                    : 8 * ceil_div(nC, 8) * (int64_t)nI;
   hipStream_t st = as_stream(stream);
   // One instantiation per active input dimension (the padded coordinates
   // beyond d are zero, so fewer distance terms are exact, not approximate).
-#define BO_POST_LAUNCH(KIND, ND)                                                          \
-  post_partials_kernel<KIND, ND><<<(unsigned)blocks, 256, 0, st>>>(                       \
-      Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt)
+#define BO_POST_LAUNCH(KIND, ND)                                                            \
+  if (kc_len > 0)                                                                           \
+    post_partials_kernel<KIND, ND, true><<<(unsigned)blocks, 256, 0, st>>>(                 \
+        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,  \
+        kc_len, work);                                                                      \
+  else                                                                                      \
+    post_partials_kernel<KIND, ND, false><<<(unsigned)blocks, 256, 0, st>>>(                \
+        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,  \
+        0, nullptr)
 #define BO_POST_DISPATCH_D(KIND)                   \
   switch (d) {                                     \
     case 1: BO_POST_LAUNCH(KIND, 1); break;        \
@@ -281,6 +437,11 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
 #undef BO_POST_DISPATCH_D
 #undef BO_POST_LAUNCH
   BO_LAUNCH_CHECK();
+  if (kc_len > 0) {
+    post_splitk_reduce_kernel<<<(unsigned)(nC * (nrows_pad / 16)), 64, 0, st>>>(
+        work, (int)n, nC, nI, kc_len, beta, Spart, mpart, Rt);
+    BO_LAUNCH_CHECK();
+  }
   return BO_OK;
 }
 

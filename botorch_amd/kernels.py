@@ -208,8 +208,18 @@ def geometry(B: int, q: int, n: int):
     return Qp.value, nrows.value, nC.value
 
 
-def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False) -> PostPartials:
-    """Column-tile partials of R R^T and R beta for X (B x q x d)."""
+def split_plan(B: int, q: int, n: int, min_wgs: int = 0):
+    """(kc_len, workspace doubles) of the split-k posterior; kc_len = 0: no split."""
+    kc, we = ctypes.c_int(), ctypes.c_int64()
+    check(lib().bo_post_split_plan(B, q, n, min_wgs, ctypes.byref(kc), ctypes.byref(we)),
+          "post_split_plan")
+    return kc.value, we.value
+
+
+def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
+                  split: Optional[int] = None) -> PostPartials:
+    """Column-tile partials of R R^T and R beta for X (B x q x d).  ``split``:
+    None = the library's plan, 0 = never split-k, k > 0 = chunks of k rows."""
     dev = _dev(X)
     B, q, d = X.shape
     if d != cache.d:
@@ -223,9 +233,19 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False) -> Pos
     check(lib().bo_prepare_rows(_p(X.contiguous()), B, q, d, _p(cache.lengthscale), _p(Xq), st),
           "prepare_rows")
     Rt = torch.empty(nC * 128, nrows_pad, **f64) if store_R else None
+    if split is None:
+        kc_len, work_elems = split_plan(B, q, cache.n)
+    elif split > 0:
+        kc_len = int(split)
+        nk = [-(-min(cache.n, (c + 1) * 128) // kc_len) for c in range(nC)]
+        work_elems = sum(nk) * nrows_pad * 128
+    else:
+        kc_len, work_elems = 0, 0
+    work = torch.empty(work_elems, **f64) if kc_len else None
     check(lib().bo_post_partials(cache.kind, _p(Xq), B, q, d, _p(cache.Xt_scaled), cache.n,
                                  _p(cache.U), cache.np, _p(cache.beta), cache.outputscale,
-                                 _p(Spart), _p(mpart), _p(Rt), st), "post_partials")
+                                 _p(Spart), _p(mpart), _p(Rt), kc_len, _p(work), st),
+          "post_partials")
     return PostPartials(B, q, Qp, nrows_pad, nC, Xq, Spart, mpart, Rt)
 
 

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 4
+#define BO_ABI_VERSION 5
 
 /* status codes */
 #define BO_OK 0
@@ -178,11 +178,21 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
  * botorch/models/gpytorch.py:446).  Xt_scaled: n x 8 lengthscale-scaled
  * training inputs; U: >= np x np with leading dim ldu; beta: n.
  * Spart: nC x (nrows_pad/16) x 16 x 16,  mpart: nC x nrows_pad.
- * Rt (nullable, gradient path): R^T, (nC*128) x nrows_pad. */
+ * Rt (nullable, gradient path): R^T, (nC*128) x nrows_pad.
+ * kc_len > 0 runs split-k (chunks of kc_len training rows, then a reduction
+ * in chunk order) with `work` >= work_elems doubles from bo_post_split_plan;
+ * kc_len = 0: one workgroup per (column tile, row tile), work unused. */
 int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
                      const double* Xt_scaled, int64_t n, const double* U, int64_t ldu, const double* beta,
                      double outputscale, double* Spart, double* mpart, double* Rt,
-                     void* stream);
+                     int kc_len, double* work, void* stream);
+
+/* Split-k plan of bo_post_partials (host pointers): kc_len = 0 when the
+ * column-tile x row-tile grid already has >= min_wgs workgroups (min_wgs <= 0:
+ * the built-in 256), else the largest power-of-two chunk in 64..1024 that
+ * reaches min_wgs, and the workspace size in doubles. */
+int bo_post_split_plan(int64_t B, int q, int64_t n, int min_wgs, int* kc_len,
+                       int64_t* work_elems);
 
 /* Finalise the posterior of each t-batch and (mode != POSTERIOR) run the
  * fused q x q psd_safe_cholesky + reparameterised sampling + MC reduction:

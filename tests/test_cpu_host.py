@@ -39,5 +39,17 @@ def test_library_exports_every_header_symbol():
         assert hasattr(handle, s), s
     assert set(syms) == set(_lib.exported_symbols()), set(syms) ^ set(_lib.exported_symbols())
     lib = _lib.lib()
-    assert lib.bo_version() == _lib.ABI_VERSION == 4
+    assert lib.bo_version() == _lib.ABI_VERSION == 5
     assert lib.bo_padded_order(4096) == 4096 and lib.bo_padded_order(20) == 128
+
+
+def test_split_plan_geometry():
+    """Host-side split-k plan of bo_post_partials (no GPU call)."""
+    from botorch_amd import kernels
+    assert kernels.split_plan(512, 16, 4096)[0] == 0      # C3: 32 x 64 tiles, no split
+    kc, work = kernels.split_plan(64, 8, 1024)            # C2: 8 x 4 tiles
+    assert kc in (64, 128, 256, 512) and work > 0
+    # workspace = non-empty chunks x padded rows x 128 columns
+    nk = sum(-(-min(1024, (c + 1) * 128) // kc) for c in range(8))
+    assert work == nk * 512 * 128
+    assert kernels.split_plan(64, 8, 1024, min_wgs=16)[0] == 0

@@ -127,6 +127,29 @@ def test_posterior_matches_oracle(n, B, q):
     torch.testing.assert_close(out["cov"].cpu(), cov_r, rtol=1e-4, atol=1e-9)
 
 
+@pytest.mark.parametrize("n,B,q,split", [(1024, 64, 8, None), (1024, 64, 8, 64), (1000, 20, 3, 128),
+                                         (513, 9, 5, 256), (300, 33, 16, 64)])
+def test_post_partials_split_k(n, B, q, split):
+    """Split-k (chunked k-range + ordered reduction) against the one-pass kernel
+    and the oracle: same Spart / mpart / R^T up to fp64 summation order."""
+    from botorch_amd import kernels, _lib
+    X, Y, orc, h = _oracle_model(n)
+    c = _device_cache(X, Y, h, orc)
+    g = torch.Generator().manual_seed(n + B)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64).to(DEV)
+    kc, _ = kernels.split_plan(B, q, n)
+    if split is None:
+        assert kc > 0  # C2 geometry (32 tiles) is planned as split-k
+    one = kernels.post_partials(c, Xc, store_R=True, split=0)
+    spl = kernels.post_partials(c, Xc, store_R=True, split=split)
+    for a, b in ((one.Spart, spl.Spart), (one.mpart, spl.mpart), (one.Rt, spl.Rt)):
+        torch.testing.assert_close(b, a, rtol=1e-11, atol=1e-13)
+    out = kernels.qmc_finalize(c, spl, _lib.QMC_POSTERIOR, orc.ymean.item(), orc.ystd.item())
+    mean_r, cov_r = orc.posterior(Xc.cpu())
+    torch.testing.assert_close(out["mean"].cpu(), mean_r, rtol=1e-4, atol=1e-8)
+    torch.testing.assert_close(out["cov"].cpu(), cov_r, rtol=1e-4, atol=1e-9)
+
+
 @pytest.mark.parametrize("n,B,q,S", [(256, 16, 4, 128), (1024, 64, 8, 256)])
 def test_qei_matches_oracle(n, B, q, S):
     from botorch_amd import kernels, _lib

@@ -2,6 +2,8 @@
 restatement and the product's generic-route torch module against the
 reference's own outputs (tests/golden, made by make_golden.py from the
 reference safe_math), values and gradients w.r.t. the samples."""
+import math
+
 import pytest
 import torch
 
@@ -51,8 +53,66 @@ def test_generic_route_logei_matches_reference(golden, tag, bname):
 
 def test_check_tau_rejects_bad_temperatures():
     from botorch_amd.acquisition import _check_tau
+    with pytest.raises(ValueError, match="tau_max is not a scalar:"):
+        _check_tau(torch.tensor([1, 2]), "tau_max")
+    with pytest.raises(ValueError, match="tau_relu is non-positive:"):
+        _check_tau(-2, "tau_relu")
     with pytest.raises(ValueError):
         _check_tau(0.0, "tau_max")
-    with pytest.raises(ValueError):
-        _check_tau(torch.tensor([1.0, 2.0]), "tau_relu")
     assert _check_tau(1e-2, "tau_max") == 1e-2
+
+
+# Known answers of the reference's own tests (test/acquisition/test_logei.py):
+# a mocked posterior returns the same samples for every MC draw, so qEI is
+# known exactly and exp(qLogEI) must sit within the smoothing temperatures
+# above it.  Checked on the oracle restatement and on the product's generic
+# torch route (both run on the CPU).
+def _logei_routes():
+    from oracle.acquisition import qlogei_from_samples
+    from botorch_amd.safe_math import (TAU_MAX, TAU_RELU, fatmax, log_improvement,
+                                       logmeanexp)
+
+    def product(samples, best_f):
+        bf = torch.as_tensor(best_f, dtype=samples.dtype)
+        if bf.dim():  # per-sample best_f (S,) against S x b x q samples
+            bf = bf.view(-1, *([1] * (samples.dim() - 2)))
+        li = log_improvement(samples, bf, tau=TAU_RELU, fat=True)
+        return logmeanexp(fatmax(li, dim=-1, tau=TAU_MAX), dim=0)
+
+    return {"oracle": lambda s, bf: qlogei_from_samples(s, bf), "product": product}
+
+
+@pytest.mark.parametrize("route", ["oracle", "product"])
+def test_logei_known_answers_single_point(route):
+    """test_logei.py:116-172: q = 1, samples identically 0."""
+    from botorch_amd.safe_math import TAU_RELU
+    f = _logei_routes()[route]
+    samples = torch.zeros(2, 1, 1, dtype=torch.float64)  # S x b x q
+    v = f(samples, 0.0).exp().item()
+    assert 0 < v <= TAU_RELU
+    v = f(samples, -1.0).exp().item()
+    assert 1.0 <= v <= 1.0 + TAU_RELU
+    lv = f(samples, 1.0).item()
+    assert 0.0 <= math.exp(lv) <= TAU_RELU
+    assert -100 < lv < -1  # large negative log value with non-vanishing gradient
+    x = samples.clone().requires_grad_(True)
+    (g,) = torch.autograd.grad(f(x, 1.0).sum(), x)
+    assert torch.isfinite(g).all() and g.abs().sum() > 0
+
+
+@pytest.mark.parametrize("route", ["oracle", "product"])
+def test_logei_known_answers_batch(route):
+    """test_logei.py:222-273: b = 2, q = 2, samples[0, 0] = 1, else 0."""
+    from botorch_amd.safe_math import TAU_MAX, TAU_RELU
+    f = _logei_routes()[route]
+    samples = torch.zeros(3, 2, 2, dtype=torch.float64)
+    samples[:, 0, 0] = 1.0
+    v = f(samples, 0.0).exp()
+    assert 1.0 <= v[0].item() <= 1.0 + TAU_RELU
+    assert 0 < v[1].item() <= TAU_RELU
+    v = f(samples, torch.zeros(3, dtype=torch.float64)).exp()  # per-sample best_f
+    assert 1.0 <= v[0].item() <= 1.0 + TAU_RELU
+    assert 0 < v[1].item() <= TAU_RELU
+    v = f(samples, -1.0).exp()
+    assert 1.999 <= v[0].item() <= 2.0 + TAU_RELU + TAU_MAX
+    assert 1.0 <= v[1].item() <= 1.0 + TAU_RELU + TAU_MAX
