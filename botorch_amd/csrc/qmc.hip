@@ -296,3 +296,44 @@ extern "C" int bo_qmc_finalize(int kind, int mode, int B, int q, const double* X
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
+
+namespace {
+
+// out[0] = max_b info[b] (as double), out[1] = max_b jitter[b]: the two facts
+// the host needs after a batched jitter ladder (fail -> NotPSDError, jitter
+// added -> NumericalWarning), in one launch and one 16-byte read-back.
+__global__ __launch_bounds__(256) void ladder_status_kernel(const int* __restrict__ info,
+                                                            const double* __restrict__ jitter,
+                                                            int64_t B, double* __restrict__ out) {
+  __shared__ double red[2][4];
+  double mi = 0.0, mj = 0.0;
+  for (int64_t b = threadIdx.x; b < B; b += 256) {
+    mi = fmax(mi, (double)info[b]);
+    mj = fmax(mj, jitter[b]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mi = fmax(mi, __shfl_xor(mi, o));
+    mj = fmax(mj, __shfl_xor(mj, o));
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][wave] = mi;
+    red[1][wave] = mj;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[0] = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
+    out[1] = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+  }
+}
+
+}  // namespace
+
+extern "C" int bo_ladder_status(const int* info, const double* jitter, int64_t B, double* out,
+                                void* stream) {
+  BO_CHECK_ARG(B >= 0 && info && jitter && out, "bo_ladder_status: bad arguments");
+  ladder_status_kernel<<<1, 256, 0, as_stream(stream)>>>(info, jitter, B, out);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}

@@ -390,7 +390,10 @@ def post_backward(cache: GPCache, pp: PostPartials, W: Optional[torch.Tensor],
 def _raise_not_psd(info: torch.Tensor, jitter: torch.Tensor, what: str):
     """Host check of a batched ladder (one D2H read, as [G] psd_safe_cholesky's
     torch.any(info)); warns like [G] when jitter was added."""
-    packed = torch.stack([info.to(torch.float64).max(), jitter.max()]).cpu()
+    packed = torch.empty(2, dtype=torch.float64, device=info.device)
+    check(lib().bo_ladder_status(_p(info.contiguous()), _p(jitter.contiguous()), info.numel(),
+                                 _p(packed), _stream(info.device)), "ladder_status")
+    packed = packed.cpu()
     if packed[0] > 0:
         from .exceptions import NotPSDError
         raise NotPSDError(f"{what}: matrix not positive definite after repeatedly adding "

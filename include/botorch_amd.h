@@ -122,6 +122,12 @@ int bo_cholesky_jitter(const double* A, int64_t n, double* L, double* Linv, doub
                        int max_tries, double jitter0, double* jitter_used, int* info_dev,
                        void* stream);
 
+/* Outcome of a batched jitter ladder (info, jitter: B entries from
+ * bo_qmc_finalize / bo_chol_small): out[0] = max info (0: all factored),
+ * out[1] = max jitter added.  One launch; the caller reads 16 bytes back, as
+ * [G] psd_safe_cholesky's torch.any(info) check does. */
+int bo_ladder_status(const int* info, const double* jitter, int64_t B, double* out, void* stream);
+
 /* Batched small psd_safe_cholesky (q <= 64), ladder applied per member
  * ([G] MultivariateNormal root_decomposition, posteriors/gpytorch.py:121-123).
  * A, L: B x q x q; info (B, nullable), jitter (B, nullable). */
