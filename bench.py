@@ -454,6 +454,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fit", action="store_true", help="skip the GP-fit half of the metric")
+    ap.add_argument("--no-bwd", action="store_true", help="skip the forward+backward timing")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the other section-8 configurations (C2, C3 qNEI, C4, C5)")
     args = ap.parse_args()
@@ -541,8 +542,11 @@ def main():
         v = acqf(Xg)
         torch.autograd.grad(v.sum(), Xg)
 
-    fb_s = _gpu_time(fwd_bwd, steps=5, warmup=2)
-    fwd_bwd = {"evals_per_s": Q * RESTARTS * MC / fb_s, "ms": 1e3 * fb_s}
+    if args.no_bwd:  # PMC passes: forward launches only (the gradient path also writes R^T)
+        fwd_bwd = None
+    else:
+        fb_s = _gpu_time(fwd_bwd, steps=5, warmup=2)
+        fwd_bwd = {"evals_per_s": Q * RESTARTS * MC / fb_s, "ms": 1e3 * fb_s}
 
     gp_fit = None
     extra = None

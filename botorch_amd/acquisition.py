@@ -204,10 +204,7 @@ class _SaasQEI(torch.autograd.Function):
         dev = X3.device
         X2 = X3.detach().reshape(B * q, d).contiguous()
         need_grad = ctx.needs_input_grad[0]
-        ym, ys = 0.0, 1.0
-        if hasattr(model, "outcome_transform"):
-            ym = float(model.outcome_transform.means.reshape(-1)[0])
-            ys = float(model.outcome_transform.stdvs.reshape(-1)[0])
+        ym, ys = model.outcome_stats()
         ens = model.ensemble_cache()
         M, n = ens["U"].shape[0], ens["n"]
         f64 = dict(dtype=torch.float64, device=dev)

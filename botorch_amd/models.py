@@ -185,6 +185,7 @@ class Standardize(nn.Module):
             self.means = Y.mean(dim=-2, keepdim=True)
             self.stdvs = stdvs
             self._is_trained = True
+            self._generation = getattr(self, "_generation", 0) + 1
         Y_tf = (Y - self.means) / self.stdvs
         Yvar_tf = Yvar / self.stdvs.pow(2) if Yvar is not None else None
         return Y_tf, Yvar_tf
@@ -204,6 +205,20 @@ class Model(nn.Module):
 
     def posterior(self, X, output_indices=None, observation_noise=False, posterior_transform=None):
         raise NotImplementedError
+
+    def outcome_stats(self):
+        """(mean, std) of the Standardize transform as host floats, read back once
+        per change of the buffers (not per acquisition call: each read is a
+        device-to-host sync)."""
+        if not hasattr(self, "outcome_transform"):
+            return 0.0, 1.0
+        ot = self.outcome_transform
+        m, s = ot.means, ot.stdvs
+        key = (getattr(ot, "_generation", 0), m.data_ptr(), m._version, s.data_ptr(), s._version)
+        if getattr(self, "_ostats_key", None) != key:
+            self._ostats = (float(m.reshape(-1)[0]), float(s.reshape(-1)[0]))
+            self._ostats_key = key
+        return self._ostats
 
 
 class SingleTaskGP(Model):
@@ -264,11 +279,6 @@ class SingleTaskGP(Model):
         ls = self.covar_module.lengthscale.detach().reshape(-1)
         os_ = float(self.covar_module.outputscale.detach()) if isinstance(self.covar_module, ScaleKernel) else 1.0
         return ls, os_, float(self.likelihood.noise.detach()), float(self.mean_module.constant.detach())
-
-    def outcome_stats(self):
-        if hasattr(self, "outcome_transform"):
-            return float(self.outcome_transform.means.reshape(-1)[0]), float(self.outcome_transform.stdvs.reshape(-1)[0])
-        return 0.0, 1.0
 
     def train(self, mode: bool = True):
         if mode:

@@ -23,16 +23,22 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     bench_short) step bench 600 python bench.py --steps 10 --warmup 2 ;;
-    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fit ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fit --no-extra ;;
     prof_fit) step prof_fit 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fit -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
-    pmc_fetch) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fit ;;
-    pmc_write) step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fit ;;
-    pmc_mfma) step pmc_mfma 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_mfma -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fit ;;
+    pmc_fetch) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fit --no-extra --no-bwd ;;
+    pmc_write) step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fit --no-extra --no-bwd ;;
+    pmc_mfma) step pmc_mfma 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_mfma -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fit --no-extra --no-bwd ;;
     prof_small) step prof_small 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_small -o run --output-format csv -- python tools/prof_small.py c2 ;;
     prof_chol) export BO_ONLY=chol; step prof_chol 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_chol -o run --output-format csv -- python tools/bench_linalg.py ;;
     potrf) step potrf 120 python tools/probe_potrf.py ;;
     linalg) step linalg 300 python tools/bench_linalg.py ;;
     probe) step probe 120 python tools/probe_rate.py ;;
+    # summarise PMC passes on the box and drop the bulky per-dispatch traces
+    # (gpurun copies gpurun_out/ back only below 64 MiB)
+    finish) python tools/pmc_summary.py gpurun_out/pmc_summary.json gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_mfma || true
+            find gpurun_out -name '*_trace.csv' -size +2M -delete
+            find gpurun_out -name 'run_counter_collection.csv' -delete
+            du -sh gpurun_out ;;
     *) step custom 900 bash -c "$s" ;;
   esac
 done
