@@ -30,6 +30,8 @@
 // to a power of two <= 16, so every t-batch sits inside one 16-row MFMA tile.
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int PC = 128;   // training columns c per workgroup
@@ -37,7 +39,9 @@ constexpr int PI = 128;   // test rows i per workgroup
 constexpr int PK = 16;    // k-step
 constexpr int PLD = 144;  // LDS row pitch (doubles): 2 x 144 dwords = 32 mod 64 banks
 constexpr int DP = 8;     // padded input dimension held in registers
-constexpr int kSplitMinWgs = 256;      // split-k below this many (column, row) tiles
+constexpr int kSlots = 512;            // resident workgroups: 256 CUs x 2 (launch bounds)
+constexpr int kWgOverheadSteps = 4;    // prologue + epilogue of a workgroup, in k-steps
+constexpr int kReduceSteps = 3;        // the split-k reduction launch, in k-steps
 constexpr int kTileDoubles = 32 * 64;  // one 16-row x 128-column R^T tile
 
 // One kernel value k(x_i, x_k) from scaled coordinates (0 beyond n / invalid rows).
@@ -353,27 +357,36 @@ int bo_post_geometry(int64_t B, int q, int64_t n, int* Qp, int* nrows_pad, int* 
   return BO_OK;
 }
 
-int bo_post_split_plan(int64_t B, int q, int64_t n, int min_wgs, int* kc_len,
+int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len,
                        int64_t* work_elems) {
   int Qp, nrows_pad, nC;
   int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
   if (s) return s;
   const int64_t nI = nrows_pad / PI;
-  if (min_wgs <= 0) min_wgs = kSplitMinWgs;
+  if (slots <= 0) slots = kSlots;
   *kc_len = 0;
   *work_elems = 0;
-  if ((int64_t)nC * nI >= min_wgs) return BO_OK;
-  // Largest power-of-two chunk (64..1024 rows) that yields min_wgs workgroups:
-  // fewer chunks mean less workspace traffic and a shorter reduction.
-  int best = 0;
-  for (int kc = 1024; kc >= 64; kc /= 2) {
-    if (kc >= n) continue;
-    best = kc;
-    if (splitk_base(nC, (int)n, kc) * nI >= min_wgs) break;
+  // Cost model in k-step units (measured on MI355X, tools/tune_split.py):
+  //  one pass: the heaviest-first schedule ends at max(total steps / slots,
+  //            longest column tile) plus a per-workgroup overhead per round;
+  //  split-k:  every round of workgroups lasts one chunk (kc / 16 steps) plus
+  //            the overhead, plus the reduction launch.  Ties go to the
+  //            shorter chunk.
+  const int64_t steps = nI * splitk_base(nC, (int)n, PK);
+  const int64_t longest = splitk_chunks(nC - 1, (int)n, PK);
+  const int64_t one_pass = std::max(ceil_div(steps, slots), longest) +
+                           kWgOverheadSteps * ceil_div((int64_t)nC * nI, slots);
+  int64_t best_cost = one_pass;
+  for (int kc = 64; kc <= 1024; kc *= 2) {
+    if (kc >= n) break;
+    const int64_t wgs = nI * splitk_base(nC, (int)n, kc);
+    const int64_t cost = ceil_div(wgs, slots) * (kc / PK + kWgOverheadSteps) + kReduceSteps;
+    if (cost < best_cost) {
+      best_cost = cost;
+      *kc_len = kc;
+    }
   }
-  if (best == 0) return BO_OK;
-  *kc_len = best;
-  *work_elems = splitk_base(nC, (int)n, best) * nrows_pad * PC;
+  if (*kc_len) *work_elems = splitk_base(nC, (int)n, *kc_len) * nrows_pad * PC;
   return BO_OK;
 }
 

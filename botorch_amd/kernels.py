@@ -208,10 +208,10 @@ def geometry(B: int, q: int, n: int):
     return Qp.value, nrows.value, nC.value
 
 
-def split_plan(B: int, q: int, n: int, min_wgs: int = 0):
-    """(kc_len, workspace doubles) of the split-k posterior; kc_len = 0: no split."""
+def split_plan(B: int, q: int, n: int, slots: int = 0):
+    """(kc_len, workspace doubles) of the split-k posterior; kc_len = 0: one pass."""
     kc, we = ctypes.c_int(), ctypes.c_int64()
-    check(lib().bo_post_split_plan(B, q, n, min_wgs, ctypes.byref(kc), ctypes.byref(we)),
+    check(lib().bo_post_split_plan(B, q, n, slots, ctypes.byref(kc), ctypes.byref(we)),
           "post_split_plan")
     return kc.value, we.value
 

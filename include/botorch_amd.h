@@ -193,11 +193,11 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
                      double outputscale, double* Spart, double* mpart, double* Rt,
                      int kc_len, double* work, void* stream);
 
-/* Split-k plan of bo_post_partials (host pointers): kc_len = 0 when the
- * column-tile x row-tile grid already has >= min_wgs workgroups (min_wgs <= 0:
- * the built-in 256), else the largest power-of-two chunk in 64..1024 that
- * reaches min_wgs, and the workspace size in doubles. */
-int bo_post_split_plan(int64_t B, int q, int64_t n, int min_wgs, int* kc_len,
+/* Split-k plan of bo_post_partials (host pointers): the chunk length in
+ * {64, ..., 1024} (or 0 = one pass) that minimises a k-step cost model of the
+ * triangular grid over `slots` resident workgroups (slots <= 0: 512 = 256 CUs
+ * x 2), and the workspace size in doubles. */
+int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len,
                        int64_t* work_elems);
 
 /* Finalise the posterior of each t-batch and (mode != POSTERIOR) run the
