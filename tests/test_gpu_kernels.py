@@ -38,6 +38,39 @@ def test_gemm_matches_torch(M, N, K, ta, tb):
     torch.testing.assert_close(out.cpu(), ref, rtol=1e-12, atol=1e-11)
 
 
+@pytest.mark.parametrize("M,N,K,batch", [(4, 4, 256, 1024), (16, 16, 3, 7), (1, 16, 33, 5), (9, 2, 100, 3)])
+@pytest.mark.parametrize("ta,tb", [(False, True), (True, False), (True, True)])
+def test_gemm_small_batched(M, N, K, batch, ta, tb):
+    """M, N <= 16 take the one-wave-per-member kernel."""
+    from botorch_amd import kernels
+    g = torch.Generator().manual_seed(M + 3 * N + K)
+    A = torch.randn(batch, *((K, M) if ta else (M, K)), generator=g, dtype=torch.float64)
+    B = torch.randn(batch, *((N, K) if tb else (K, N)), generator=g, dtype=torch.float64)
+    C0 = torch.randn(batch, M, N, generator=g, dtype=torch.float64)
+    ref = 2.0 * ((A.mT if ta else A) @ (B.mT if tb else B)) + 0.5 * C0
+    out = kernels.gemm(A.to(DEV), B.to(DEV), ta, tb, alpha=2.0, beta=0.5, C=C0.clone().to(DEV))
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-12, atol=1e-11)
+
+
+def test_gemm_small_flags():
+    from botorch_amd import kernels, _lib
+    g = torch.Generator().manual_seed(5)
+    L = torch.randn(12, 12, generator=g, dtype=torch.float64)  # lower part used
+    B = torch.randn(12, 7, generator=g, dtype=torch.float64)
+    out = kernels.gemm(L.to(DEV), B.to(DEV), flags=_lib.GEMM_A_LOWER).cpu()
+    torch.testing.assert_close(out, torch.tril(L) @ B, rtol=1e-12, atol=1e-12)
+    P = torch.randn(10, 30, generator=g, dtype=torch.float64)
+    C = torch.randn(10, 10, generator=g, dtype=torch.float64)
+    out = kernels.gemm(P.to(DEV), P.to(DEV), False, True, alpha=-1.0, beta=1.0,
+                       C=C.clone().to(DEV), flags=_lib.GEMM_LOWER_C).cpu()
+    torch.testing.assert_close(torch.tril(out), torch.tril(C - P @ P.T), rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(torch.triu(out, 1), torch.triu(C, 1))
+    U = torch.randn(9, 9, generator=g, dtype=torch.float64)
+    X = torch.randn(5, 9, generator=g, dtype=torch.float64)
+    out = kernels.gemm(X.to(DEV), U.to(DEV), flags=_lib.GEMM_B_UPPER).cpu()
+    torch.testing.assert_close(out, X @ torch.triu(U), rtol=1e-12, atol=1e-12)
+
+
 def test_gemm_batched_and_large():
     from botorch_amd import kernels
     g = torch.Generator().manual_seed(1)
