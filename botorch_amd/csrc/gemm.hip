@@ -271,29 +271,35 @@ int launch_gemm(bool ta, bool tb, int M, int N, int K, double alpha, const doubl
 
 namespace {
 
-// Tiny products (M, N <= 16, e.g. the q x q blocks R_b R_b^T of the SAAS
-// ensemble: 1024 members of 4 x 256 x 4): one wave per batch member, one
-// 16 x 16 MFMA accumulator, k in steps of 4 (a 128 x 128 tile would spend
-// three orders of magnitude more flops on padding).  Structure flags mask the
-// operands exactly as the tiled kernel's k-range skipping does.
+// Narrow products (N <= 16 with M <= 16 or a short k-range, e.g. the q x q
+// blocks R_b R_b^T of the SAAS ensemble -- 1024 members of 4 x 256 x 4 -- or
+// the reparameterised samples Z L_b^T, 256 x 4 x 4 per member): one wave per
+// (batch member, 16-row block), one 16 x 16 MFMA accumulator, k in steps of 4
+// (a 128 x 128 tile would spend orders of magnitude more flops on padding).
+// Structure flags mask the operands exactly as the tiled kernel's k-range
+// skipping does.
 __global__ __launch_bounds__(256) void gemm_small_kernel(
     int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda, int64_t sA,
     int ta, const double* __restrict__ B, int64_t ldb, int64_t sB, int tb, double beta,
     double* __restrict__ C, int64_t ldc, int64_t sC, int batch, int flags) {
   const int lane = threadIdx.x & 63;
-  const int64_t z = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (z >= batch) return;
+  const int mblocks = (M + 15) >> 4;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= (int64_t)batch * mblocks) return;
+  const int64_t z = w / mblocks;
+  const int m0 = (int)(w - z * mblocks) * 16;
   const double* Az = A + z * sA;
   const double* Bz = B + z * sB;
-  const int r16 = lane & 15;  // A fragment row i / B fragment column j
+  const int r16 = lane & 15;  // A fragment row m0 + r16 / B fragment column j
   const int kq = lane >> 4;
+  const int ia = m0 + r16;
   v4d acc = v4d_zero();
   for (int k0 = 0; k0 < K; k0 += 4) {
     const int k = k0 + kq;
     double a = 0.0, b = 0.0;
-    if (r16 < M && k < K) {
-      a = ta ? Az[(int64_t)k * lda + r16] : Az[(int64_t)r16 * lda + k];
-      if (((flags & BO_GEMM_A_LOWER) && k > r16) || ((flags & BO_GEMM_A_UPPER) && k < r16)) a = 0.0;
+    if (ia < M && k < K) {
+      a = ta ? Az[(int64_t)k * lda + ia] : Az[(int64_t)ia * lda + k];
+      if (((flags & BO_GEMM_A_LOWER) && k > ia) || ((flags & BO_GEMM_A_UPPER) && k < ia)) a = 0.0;
     }
     if (r16 < N && k < K) {
       b = tb ? Bz[(int64_t)r16 * ldb + k] : Bz[(int64_t)k * ldb + r16];
@@ -304,7 +310,7 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(
   double* Cz = C + z * sC;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int i = mfma_row(lane, r), j = mfma_col(lane);
+    const int i = m0 + mfma_row(lane, r), j = mfma_col(lane);
     if (i < M && j < N && (!(flags & BO_GEMM_LOWER_C) || i >= j)) {
       double c = alpha * acc[r];
       if (beta != 0.0) c = fma(beta, Cz[(int64_t)i * ldc + j], c);
@@ -321,8 +327,9 @@ int bo_gemm_f64_impl(int ta, int tb, int M, int N, int K, double alpha, const do
                      hipStream_t st) {
   if (M <= 0 || N <= 0 || batch <= 0) return BO_OK;
   if (K < 0) K = 0;  // C = beta * C (the alpha term is empty)
-  if (M <= 16 && N <= 16) {
-    gemm_small_kernel<<<(unsigned)ceil_div(batch, 4), 256, 0, st>>>(
+  if (N <= 16 && (M <= 16 || K <= 256)) {
+    const int64_t waves = (int64_t)batch * ceil_div(M, 16);
+    gemm_small_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, st>>>(
         M, N, K, alpha, A, lda, sA, ta, B, ldb, sB, tb, beta, C, ldc, sC, batch, flags);
     BO_LAUNCH_CHECK();
     return BO_OK;

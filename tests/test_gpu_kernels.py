@@ -38,10 +38,11 @@ def test_gemm_matches_torch(M, N, K, ta, tb):
     torch.testing.assert_close(out.cpu(), ref, rtol=1e-12, atol=1e-11)
 
 
-@pytest.mark.parametrize("M,N,K,batch", [(4, 4, 256, 1024), (16, 16, 3, 7), (1, 16, 33, 5), (9, 2, 100, 3)])
+@pytest.mark.parametrize("M,N,K,batch", [(4, 4, 256, 1024), (16, 16, 3, 7), (1, 16, 33, 5), (9, 2, 100, 3),
+                                         (256, 4, 4, 64), (77, 1, 256, 3), (300, 16, 17, 2)])
 @pytest.mark.parametrize("ta,tb", [(False, True), (True, False), (True, True)])
 def test_gemm_small_batched(M, N, K, batch, ta, tb):
-    """M, N <= 16 take the one-wave-per-member kernel."""
+    """N <= 16 with M <= 16 or K <= 256 take the one-wave-per-16-rows kernel."""
     from botorch_amd import kernels
     g = torch.Generator().manual_seed(M + 3 * N + K)
     A = torch.randn(batch, *((K, M) if ta else (M, K)), generator=g, dtype=torch.float64)
