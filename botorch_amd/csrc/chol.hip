@@ -64,6 +64,9 @@ __global__ __launch_bounds__(256) void covar_matrix_kernel(
 // (models/fully_bayesian.py:276-281) evaluates all M members' K*x (outer = M,
 // shared test rows) and all M x B q x q blocks K** (outer = M, inner = B) in
 // one launch each.
+constexpr int CB_ROWS = 8;     // X1 rows per workgroup (x2 loads reused across them)
+constexpr int CB_DMAX = 512;   // inputs staged in LDS
+
 template <int KIND>
 __global__ __launch_bounds__(256) void covar_batched_kernel(
     const double* __restrict__ X1, int64_t s1o, int64_t s1i, int n1,
@@ -71,20 +74,43 @@ __global__ __launch_bounds__(256) void covar_batched_kernel(
     const double* __restrict__ ls, int64_t slo, int64_t sli, const double* __restrict__ os,
     int64_t soo, int64_t soi, double* __restrict__ K, int64_t sKo, int64_t sKi, int64_t ldk,
     int inner) {
+  // The member's inverse lengthscales and its CB_ROWS scaled X1 rows live in
+  // LDS (one reciprocal per dimension per workgroup, not one divide per
+  // element); each thread owns one X2 column and reuses every x2 load for all
+  // CB_ROWS rows.
+  __shared__ double invl[CB_DMAX];
+  __shared__ double x1s[CB_ROWS][CB_DMAX];
   const int z = blockIdx.z;
   const int o = z / inner, i = z % inner;
-  const int row = blockIdx.y;
+  const int row0 = blockIdx.y * CB_ROWS;
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= n1 || col >= n2) return;
-  const double* x1 = X1 + o * s1o + i * s1i + (int64_t)row * d;
-  const double* x2 = X2 + o * s2o + i * s2i + (int64_t)col * d;
   const double* l = ls + o * slo + i * sli;
-  double d2 = 0.0;
-  for (int t = 0; t < d; ++t) {
-    const double diff = (x1[t] - x2[t]) / l[t];
-    d2 = fma(diff, diff, d2);
+  for (int t = threadIdx.x; t < d; t += blockDim.x) invl[t] = 1.0 / l[t];
+  __syncthreads();
+  const double* x1 = X1 + o * s1o + i * s1i;
+  for (int e = threadIdx.x; e < CB_ROWS * d; e += blockDim.x) {
+    const int r = e / d, t = e - r * d;
+    x1s[r][t] = (row0 + r < n1) ? x1[(int64_t)(row0 + r) * d + t] * invl[t] : 0.0;
   }
-  K[o * sKo + i * sKi + (int64_t)row * ldk + col] = os[o * soo + i * soi] * kernel_from_d2<KIND>(d2);
+  __syncthreads();
+  if (col >= n2) return;
+  const double* x2 = X2 + o * s2o + i * s2i + (int64_t)col * d;
+  double d2[CB_ROWS];
+#pragma unroll
+  for (int r = 0; r < CB_ROWS; ++r) d2[r] = 0.0;
+  for (int t = 0; t < d; ++t) {
+    const double v = x2[t] * invl[t];
+#pragma unroll
+    for (int r = 0; r < CB_ROWS; ++r) {
+      const double diff = x1s[r][t] - v;
+      d2[r] = fma(diff, diff, d2[r]);
+    }
+  }
+  const double scale = os[o * soo + i * soi];
+  double* Kz = K + o * sKo + i * sKi;
+#pragma unroll
+  for (int r = 0; r < CB_ROWS; ++r)
+    if (row0 + r < n1) Kz[(int64_t)(row0 + r) * ldk + col] = scale * kernel_from_d2<KIND>(d2[r]);
 }
 
 __global__ void transpose_kernel(const double* __restrict__ A, double* __restrict__ B,
@@ -196,16 +222,20 @@ int bo_covar_batched(int kind, const double* X1, int64_t s1o, int64_t s1i, int n
   BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bo_covar_batched: bad kind %d", kind);
   BO_CHECK_ARG(d > 0 && n1 >= 0 && n2 >= 0 && ldk >= n2 && outer >= 1 && inner >= 1,
                "bo_covar_batched: bad shape");
-  BO_CHECK_ARG(n1 <= 65535 && (int64_t)outer * inner <= 65535, "bo_covar_batched: grid too large");
+  BO_CHECK_ARG(d <= CB_DMAX, "bo_covar_batched: d = %d > %d", d, CB_DMAX);
+  BO_CHECK_ARG(ceil_div(n1, CB_ROWS) <= 65535 && (int64_t)outer * inner <= 65535,
+               "bo_covar_batched: grid too large");
   if (n1 == 0 || n2 == 0) return BO_OK;
-  dim3 grid((unsigned)ceil_div(n2, 256), (unsigned)n1, (unsigned)(outer * inner));
+  const int threads = n2 >= 256 ? 256 : (int)(ceil_div(n2, 64) * 64);
+  dim3 grid((unsigned)ceil_div(n2, threads), (unsigned)ceil_div(n1, CB_ROWS),
+            (unsigned)(outer * inner));
   hipStream_t st = as_stream(stream);
   if (kind == BO_RBF)
-    covar_batched_kernel<BO_RBF><<<grid, 256, 0, st>>>(X1, s1o, s1i, n1, X2, s2o, s2i, n2, d, ls,
+    covar_batched_kernel<BO_RBF><<<grid, threads, 0, st>>>(X1, s1o, s1i, n1, X2, s2o, s2i, n2, d, ls,
                                                          slo, sli, os, soo, soi, K, sKo, sKi, ldk,
                                                          inner);
   else
-    covar_batched_kernel<BO_MATERN52><<<grid, 256, 0, st>>>(X1, s1o, s1i, n1, X2, s2o, s2i, n2, d,
+    covar_batched_kernel<BO_MATERN52><<<grid, threads, 0, st>>>(X1, s1o, s1i, n1, X2, s2o, s2i, n2, d,
                                                               ls, slo, sli, os, soo, soi, K, sKo,
                                                               sKi, ldk, inner);
   BO_LAUNCH_CHECK();

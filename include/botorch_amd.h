@@ -97,7 +97,7 @@ int64_t bo_padded_order(int64_t n);
  * K[o][i] (n1 x n2, leading dim ldk, at K + o sKo + i sKi) =
  *   os[o soo + i soi] * k((X1[o][i] - X2[o][i]) / ls[o][i]),
  * X1 at X1 + o s1o + i s1i (n1 x d), X2 likewise, ls at ls + o slo + i sli (d).
- * Strides are in elements (0 = shared).  The SAAS ensemble's K*x of all M
+ * Strides are in elements (0 = shared); d <= 512.  The SAAS ensemble's K*x of all M
  * members and K** of all M x B t-batches (models/fully_bayesian.py:276-281),
  * one launch each. */
 int bo_covar_batched(int kind, const double* X1, int64_t s1o, int64_t s1i, int n1,

@@ -245,3 +245,27 @@ def test_sobol_transform_accuracy_dense_grid():
     err = (out.cpu().squeeze(0) - ref).abs() / ref.abs().clamp_min(1.0)
     i = int(err.argmax())
     assert err.max() < 4e-15, f"max err {err.max():.3e} at u={u[i].item()!r} z={ref[i].item()!r} got {out.cpu()[0, i].item()!r}"
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("n1,n2,d,outer,inner", [(13, 300, 50, 3, 2), (4, 4, 6, 16, 64), (256, 256, 50, 2, 1)])
+def test_covar_batched_matches_torch(kind, n1, n2, d, outer, inner):
+    """bo_covar_batched: per-(outer, inner) lengthscales / outputscales, X1 per
+    inner member, X2 shared (the SAAS K*x and K** launches)."""
+    from botorch_amd import kernels
+    g = torch.Generator().manual_seed(n1 + n2 + d)
+    X1 = torch.rand(inner, n1, d, generator=g, dtype=torch.float64)
+    X2 = torch.rand(n2, d, generator=g, dtype=torch.float64)
+    ls = 0.2 + torch.rand(outer, d, generator=g, dtype=torch.float64)
+    os_ = 0.5 + torch.rand(outer, generator=g, dtype=torch.float64)
+    K = torch.empty(outer, inner, n1, n2, dtype=torch.float64, device=DEV)
+    kernels.covar_batched(kind, X1.to(DEV), (0, n1 * d), n1, X2.to(DEV), (0, 0), n2, d, ls.to(DEV),
+                          (d, 0), os_.to(DEV), (1, 0), K, (inner * n1 * n2, n1 * n2), n2, outer, inner)
+    r = torch.cdist(X1.unsqueeze(0) / ls.view(outer, 1, 1, d), (X2 / ls.view(outer, 1, d)).unsqueeze(1))
+    if kind == 0:
+        ref = torch.exp(-0.5 * r * r)
+    else:
+        s5 = math.sqrt(5.0) * r
+        ref = (1 + s5 + s5 * s5 / 3) * torch.exp(-s5)
+    ref = os_.view(outer, 1, 1, 1) * ref
+    torch.testing.assert_close(K.cpu(), ref, rtol=1e-10, atol=1e-12)
