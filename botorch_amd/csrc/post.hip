@@ -57,7 +57,7 @@ __device__ __forceinline__ double eval_kernel_row(const double (&xi)[ND], const 
     d2 = fma(df, df, d2);
   }
 #ifdef BO_PROBE_CHEAP_KERNEL  // timing probe only (tools): no exp, wrong values
-  return outputscale * d2;
+  return outputscale * d2 * 0.0;  // keeps the distance FMAs, drops the exp
 #else
   return outputscale * kernel_from_d2<KIND>(d2);
 #endif
