@@ -31,7 +31,6 @@
 #include "common.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace {
 
@@ -305,157 +304,6 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   }
 }
 
-// Wide variant: 256 training columns x 64 test rows per workgroup (two
-// 128-column tiles of the Spart/mpart/Rt layout; wave w owns rows 16 w..16 w+15
-// across all 256 columns), and every lane evaluates the K*x values it feeds to
-// the matrix cores itself -- lane l owns row 16 w + (l & 15) at k = 4 ks +
-// (l >> 4), exactly its B-operand fragment -- so K*x never touches LDS and
-// each kernel value (one exp) serves 256 columns instead of 128.  LDS holds
-// only the U stage (2 x 16 x 272 doubles = 70 KB, two workgroups per CU).
-// Column tile 2 ciw needs k < c0 + 128 only (U is upper triangular), so the
-// k-steps past it issue the right half's MFMAs alone.
-constexpr int PCW = 256;
-constexpr int PIW = 64;
-constexpr int PLDW = 272;  // 544 dwords = 32 mod 64 banks, as PLD
-
-template <int KIND, int ND>
-__global__ __launch_bounds__(256, 2) void post_partials_wide_kernel(
-    const double* __restrict__ Xq, int nrows, const double* __restrict__ Xt, int n,
-    const double* __restrict__ U, int64_t ldu, const double* __restrict__ beta,
-    double outputscale, int nC, int nCW, int nIW, int nI, double* __restrict__ Spart,
-    double* __restrict__ mpart, double* __restrict__ Rt) {
-  __shared__ __attribute__((aligned(16))) double Us[2][PK][PLDW];
-
-  // XCD-aware, heaviest-first placement as in post_partials_kernel.
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7;
-  const int slot = bid >> 3;
-  const int jj = slot / nIW;
-  const int ii = slot - jj * nIW;
-  const int pos = jj * 8 + xcd;
-  if (pos >= nCW) return;
-  const int ciw = nCW - 1 - pos;
-  const int c0 = ciw * PCW;
-  const int kend = min(n, c0 + PCW);
-  const int khalf = min(n, c0 + PC);            // left half: k < khalf only
-  const bool has_right = 2 * ciw + 1 < nC;      // right half inside U
-  const int nsteps = (kend + PK - 1) / PK;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int l15 = lane & 15;
-  const int kq = lane >> 4;
-  const int row0 = ii * PIW + wave * 16;        // this wave's 16-row tile
-  const int row = row0 + l15;                   // this lane's B-operand row
-  const bool iv = row < nrows;
-  double xi[ND];
-#pragma unroll
-  for (int t = 0; t < ND; ++t) xi[t] = iv ? Xq[(int64_t)row * DP + t] : 0.0;
-
-  v4d acc[16];
-#pragma unroll
-  for (int a = 0; a < 16; ++a) acc[a] = v4d_zero();
-
-  // U stage: thread moves rows urow + 2 p (p < 8) of one column pair.
-  const int urow = tid >> 7;
-  const int ucl = 2 * (tid & 127);
-  const bool uload = ucl < PC || has_right;
-  double2 ust[8];
-#define BO_LOAD_UW(K0)                                                               \
-  {                                                                                  \
-    const double* src = U + (int64_t)((K0) + urow) * ldu + c0 + ucl;                 \
-    _Pragma("unroll") for (int p = 0; p < 8; ++p)                                    \
-      ust[p] = uload ? *reinterpret_cast<const double2*>(src + 2 * p * ldu)          \
-                     : make_double2(0.0, 0.0);                                       \
-  }
-#define BO_STORE_UW(BUF)                                                             \
-  {                                                                                  \
-    _Pragma("unroll") for (int p = 0; p < 8; ++p)                                    \
-      *reinterpret_cast<double2*>(&Us[BUF][urow + 2 * p][ucl]) = ust[p];             \
-  }
-#define BO_EVAL_K(K0, DST)                                                           \
-  {                                                                                  \
-    _Pragma("unroll") for (int ks = 0; ks < 4; ++ks) {                              \
-      const int k = (K0) + 4 * ks + kq;                                              \
-      double d2 = 0.0;                                                               \
-      _Pragma("unroll") for (int t = 0; t < ND; ++t) {                              \
-        const double df = xi[t] - (k < n ? Xt[(int64_t)k * DP + t] : 0.0);           \
-        d2 = fma(df, df, d2);                                                        \
-      }                                                                              \
-      DST[ks] = (k < n && iv) ? outputscale * kernel_from_d2<KIND>(d2) : 0.0;        \
-    }                                                                                \
-  }
-
-  double kv[4];
-  BO_LOAD_UW(0);
-  BO_EVAL_K(0, kv);
-  BO_STORE_UW(0);
-  __syncthreads();
-  // k-steps before khalf feed both 128-column halves, the rest only the right.
-#define BO_STEP(CT0)                                                                 \
-  {                                                                                  \
-    const int cur = t & 1;                                                           \
-    const bool more = t + 1 < nsteps;                                                \
-    const int knext = more ? (t + 1) * PK : t * PK;                                  \
-    BO_LOAD_UW(knext);                                                               \
-    _Pragma("unroll") for (int ks = 0; ks < 4; ++ks) {                              \
-      const int kr = ks * 4 + kq;                                                    \
-      _Pragma("unroll") for (int ct = CT0; ct < 16; ++ct)                           \
-        acc[ct] = mfma_f64(Us[cur][kr][ct * 16 + l15], kv[ks], acc[ct]);            \
-    }                                                                                \
-    BO_EVAL_K(knext, kv);                                                            \
-    if (more) BO_STORE_UW(cur ^ 1);                                                  \
-    __syncthreads();                                                                 \
-  }
-  const int tsplit = min(nsteps, (khalf + PK - 1) / PK);
-  int t = 0;
-  for (; t < tsplit; ++t) BO_STEP(0)
-  for (; t < nsteps; ++t) BO_STEP(8)
-#undef BO_STEP
-#undef BO_LOAD_UW
-#undef BO_STORE_UW
-#undef BO_EVAL_K
-
-  // Epilogue per 128-column half h (Spart / mpart / Rt tile 2 ciw + h).
-  const int nrows16 = nI * (PI / 16);
-  const int nrows_pad = nI * PI;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int cit = 2 * ciw + h;
-    if (cit >= nC) break;
-    const int cb = cit * PC;
-    if (Rt != nullptr) {
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = cb + ct * 16 + mfma_row(lane, r);
-          Rt[(int64_t)c * nrows_pad + row0 + mfma_col(lane)] = acc[h * 8 + ct][r];
-        }
-    }
-    v4d P = v4d_zero();
-#pragma unroll
-    for (int ct = 0; ct < 8; ++ct)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) P = mfma_f64(acc[h * 8 + ct][r], acc[h * 8 + ct][r], P);
-    double* sp = Spart + ((int64_t)cit * nrows16 + row0 / 16) * 256;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sp[mfma_row(lane, r) * 16 + mfma_col(lane)] = P[r];
-    double m = 0.0;
-#pragma unroll
-    for (int ct = 0; ct < 8; ++ct)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = cb + ct * 16 + mfma_row(lane, r);
-        m = fma(acc[h * 8 + ct][r], (c < n) ? beta[c] : 0.0, m);
-      }
-    m += __shfl_xor(m, 16);
-    m += __shfl_xor(m, 32);
-    if (lane < 16) mpart[(int64_t)cit * nrows_pad + row0 + lane] = m;
-  }
-}
-
 // Split-k reduction: one wave per (column tile, 16-row tile) sums the chunk
 // partials in chunk order and runs the epilogue.
 __global__ __launch_bounds__(64) void post_splitk_reduce_kernel(
@@ -577,37 +425,6 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
   const int64_t blocks = kc_len > 0 ? (int64_t)nC * ceil_div(n, kc_len) * nI
                                     : 8 * ceil_div(nC, 8) * (int64_t)nI;
   hipStream_t st = as_stream(stream);
-  static const int wide = [] {
-    const char* e = getenv("BO_POST_WIDE");
-    return e != nullptr && e[0] == '1';
-  }();
-  if (wide && kc_len == 0) {
-    const int nCW = (int)ceil_div(n, PCW);
-    const int nIW = nrows_pad / PIW;
-    const int64_t wblocks = 8 * ceil_div(nCW, 8) * (int64_t)nIW;
-#define BO_WIDE_LAUNCH(KIND, ND)                                                             \
-  post_partials_wide_kernel<KIND, ND><<<(unsigned)wblocks, 256, 0, st>>>(                    \
-      Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nCW, nIW, nI, Spart, mpart, Rt)
-#define BO_WIDE_DISPATCH_D(KIND)                  \
-  switch (d) {                                    \
-    case 1: BO_WIDE_LAUNCH(KIND, 1); break;       \
-    case 2: BO_WIDE_LAUNCH(KIND, 2); break;       \
-    case 3: BO_WIDE_LAUNCH(KIND, 3); break;       \
-    case 4: BO_WIDE_LAUNCH(KIND, 4); break;       \
-    case 5: BO_WIDE_LAUNCH(KIND, 5); break;       \
-    case 6: BO_WIDE_LAUNCH(KIND, 6); break;       \
-    default: BO_WIDE_LAUNCH(KIND, 8); break;      \
-  }
-    if (kind == BO_RBF) {
-      BO_WIDE_DISPATCH_D(BO_RBF)
-    } else {
-      BO_WIDE_DISPATCH_D(BO_MATERN52)
-    }
-#undef BO_WIDE_DISPATCH_D
-#undef BO_WIDE_LAUNCH
-    BO_LAUNCH_CHECK();
-    return BO_OK;
-  }
   // One instantiation per active input dimension (the padded coordinates
   // beyond d are zero, so fewer distance terms are exact, not approximate).
 #define BO_POST_LAUNCH(KIND, ND)                                                            \
