@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""C2 qEI and C5 SAAS qEI forward loops (for rocprofv3 --kernel-trace): where
-does the time of the small configurations go?"""
+"""C2 qEI, C5 SAAS qEI and C3 qNEI forward loops (for rocprofv3
+--kernel-trace): where does the time of the non-headline configurations go?"""
 import os
 import sys
 import time
@@ -63,3 +63,23 @@ if which in ("c5", "both"):
             acqf(Xd)
         torch.cuda.synchronize()
     print("C5 ms", 1e3 * (time.perf_counter() - t0) / 20)
+if which in ("c3nei",):
+    from botorch_amd.acquisition import qNoisyExpectedImprovement
+    X = draw_sobol_samples(unit(6), 4096, 1, seed=0).squeeze(1)
+    Y = Hartmann(negate=True)(X).unsqueeze(-1)
+    m = SingleTaskGP(X.to(dev), Y.to(dev))
+    m.covar_module.lengthscale = torch.full((1, 6), bench.LENGTHSCALE, dtype=f64)
+    m.likelihood.noise = torch.tensor([bench.NOISE], dtype=f64)
+    m.eval()
+    acqf = qNoisyExpectedImprovement(m, X.to(dev), sampler=SobolQMCNormalSampler(torch.Size([512]), seed=0),
+                                     prune_baseline=True)
+    Xd = draw_sobol_samples(unit(6), 512, 16, seed=1).to(dev)
+    with torch.no_grad():
+        for _ in range(2):
+            acqf(Xd)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(10):
+            acqf(Xd)
+        torch.cuda.synchronize()
+    print("C3 qNEI ms", 1e3 * (time.perf_counter() - t0) / 10, "r", acqf.X_baseline.shape[0])
