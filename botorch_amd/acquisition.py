@@ -408,7 +408,10 @@ class _CachedBaselineRoot:
         ones = torch.ones(kernels.DP, dtype=torch.float64, device=pp.Xq.device)
         Kbx = kernels.covar_matrix(self.Xb_scaled, pp.Xq, ones, cache.kind, cache.outputscale)
         T = kernels.gemm(self.Linv, Kbx, alpha=s2, flags=_lib.GEMM_A_LOWER)
-        T = kernels.gemm(self.P_b, pp.Rt, alpha=-s2, beta=1.0, C=T)
+        if pp.Cx is not None:   # P_b R^T = Q_b K*x^T, fused into the posterior pass
+            T.add_(pp.Cx, alpha=-s2)
+        else:
+            T = kernels.gemm(self.P_b, pp.Rt, alpha=-s2, beta=1.0, C=T)
         F = kernels.gemm(self.Z_base, T)
         return T, F
 
@@ -507,7 +510,7 @@ class _FusedQNEI(torch.autograd.Function):
         ymean, ystd = model.outcome_stats()
         q = X3.shape[-2]
         need_grad = ctx.needs_input_grad[0]
-        pp = kernels.post_partials(cache, X3.detach(), store_R=True)
+        pp = kernels.post_partials(cache, X3.detach(), store_R=need_grad, cross=acqf._root.Q_b)
         T, F = acqf._root.forward(cache, pp, ystd)
         Zq = acqf._base_samples_q(q, X3.device)
         lp = getattr(acqf, "_log_params", None)
@@ -800,7 +803,8 @@ class _FusedQNEHVI(torch.autograd.Function):
         for t, mm in enumerate(models):
             cache = mm.prediction_cache()
             ymean, ystd = mm.outcome_stats()
-            pp = kernels.post_partials(cache, X3.detach(), store_R=True)
+            pp = kernels.post_partials(cache, X3.detach(), store_R=need_grad,
+                                       cross=acqf._roots[t].Q_b)
             T, F = acqf._roots[t].forward(cache, pp, ystd)
             out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
                                        want_cov=False, want_L=True, T=T, F=F)

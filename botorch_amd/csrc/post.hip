@@ -125,12 +125,13 @@ __device__ __forceinline__ void post_epilogue(const v4d (&acc)[8], int ci, int r
   if (lane < 16) mpart[(int64_t)ci * nrows_pad + row0 + lane] = m;
 }
 
-template <int KIND, int ND, bool SPLIT>
+template <int KIND, int ND, bool SPLIT, bool CROSS>
 __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     const double* __restrict__ Xq, int nrows, const double* __restrict__ Xt, int n,
     const double* __restrict__ U, int64_t ldu, const double* __restrict__ beta,
     double outputscale, int nC, int nI, double* __restrict__ Spart, double* __restrict__ mpart,
-    double* __restrict__ Rt, int kc_len, double* __restrict__ work) {
+    double* __restrict__ Rt, int kc_len, double* __restrict__ work,
+    const double* __restrict__ Qc, int rq, int64_t ldq, double* __restrict__ Cx) {
   // Two LDS stages: while the MFMAs consume stage t, the U rows of step t+1
   // are in flight to registers and this thread evaluates its 8 kernel values
   // of step t+1 between the MFMAs (VALU work hidden under the matrix pipe);
@@ -190,6 +191,21 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     acc[a][0] = v4d_zero();
     acc[a][1] = v4d_zero();
   }
+  // Cross term (CROSS): the last column tile's workgroups stream every k of
+  // K*x through LDS, so they also accumulate Cx = Qc K*x^T for rq <= 16 extra
+  // rows of Qc (2 MFMAs per 16 of the tile's own): the qNEI cross-covariance
+  // P_b R^T = Q_b K*x^T without materialising R.
+  const bool cross = CROSS && ci == nC - 1;
+  v4d accx[2] = {v4d_zero(), v4d_zero()};
+  double qa[4] = {0.0, 0.0, 0.0, 0.0};
+  const bool qrow = CROSS && (lane & 15) < rq;
+#define BO_LOAD_Q(K0)                                                              \
+  if (cross) {                                                                     \
+    _Pragma("unroll") for (int ks = 0; ks < 4; ++ks) {                            \
+      const int kk = (K0) + ks * 4 + (lane >> 4);                                  \
+      qa[ks] = (qrow && kk < n) ? Qc[(int64_t)(lane & 15) * ldq + kk] : 0.0;       \
+    }                                                                              \
+  }
 
   // Per-thread staging registers: 4 x 16 B of U rows, 8 kernel values.
   double u0x, u0y, u1x, u1y, u2x, u2y, u3x, u3y;
@@ -226,6 +242,7 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     const int cur = t & 1;
     const bool more = t + 1 < nsteps;
     const int knext = kbeg + (more ? (t + 1) * PK : t * PK);  // last step re-reads (unused)
+    BO_LOAD_Q(kbeg + t * PK);
     BO_LOAD_U(knext);
 #pragma unroll
     for (int ks = 0; ks < PK / 4; ++ks) {
@@ -239,6 +256,10 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
       for (int ct = 0; ct < 8; ++ct)
 #pragma unroll
         for (int it = 0; it < 2; ++it) acc[ct][it] = mfma_f64(a[ct], b[it], acc[ct][it]);
+      if (cross) {
+        accx[0] = mfma_f64(qa[ks], b[0], accx[0]);
+        accx[1] = mfma_f64(qa[ks], b[1], accx[1]);
+      }
       kv[2 * ks] = eval_kernel_row<KIND, ND>(xi, Xt, n, knext + kh * 8 + 2 * ks, outputscale, ivalid);
       kv[2 * ks + 1] = eval_kernel_row<KIND, ND>(xi, Xt, n, knext + kh * 8 + 2 * ks + 1, outputscale, ivalid);
     }
@@ -247,6 +268,17 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   }
 #undef BO_LOAD_U
 #undef BO_STORE
+#undef BO_LOAD_Q
+  if (cross) {
+    const int nrows_pad = nI * PI;
+#pragma unroll
+    for (int it = 0; it < 2; ++it)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = mfma_row(lane, r);
+        if (j < rq) Cx[(int64_t)j * nrows_pad + i0 + wave * 32 + it * 16 + mfma_col(lane)] = accx[it][r];
+      }
+  }
 
   if constexpr (SPLIT) {
     // Partial R^T of this chunk: register-major, lane-minor per 16-row tile,
@@ -410,7 +442,10 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
 int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
                      const double* Xt_scaled, int64_t n, const double* U, int64_t ldu, const double* beta,
                      double outputscale, double* Spart, double* mpart, double* Rt,
-                     int kc_len, double* work, void* stream) {
+                     int kc_len, double* work, const double* Qc, int rq, int64_t ldq, double* Cx,
+                     void* stream) {
+  BO_CHECK_ARG(Qc == nullptr || (kc_len == 0 && rq >= 1 && rq <= 16 && ldq >= n && Cx != nullptr),
+               "cross term: one-pass only, 1 <= rq <= 16 rows (got %d), ldq >= n, Cx given", rq);
   BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
   BO_CHECK_ARG(ldu % 2 == 0 && ldu >= ceil_div(n, PC) * PC, "U leading dim %lld too small",
                (long long)ldu);
@@ -429,13 +464,17 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
   // beyond d are zero, so fewer distance terms are exact, not approximate).
 #define BO_POST_LAUNCH(KIND, ND)                                                            \
   if (kc_len > 0)                                                                           \
-    post_partials_kernel<KIND, ND, true><<<(unsigned)blocks, 256, 0, st>>>(                 \
+    post_partials_kernel<KIND, ND, true, false><<<(unsigned)blocks, 256, 0, st>>>(          \
         Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,  \
-        kc_len, work);                                                                      \
+        kc_len, work, nullptr, 0, 0, nullptr);                                              \
+  else if (Qc != nullptr)                                                                   \
+    post_partials_kernel<KIND, ND, false, true><<<(unsigned)blocks, 256, 0, st>>>(          \
+        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,  \
+        0, nullptr, Qc, rq, ldq, Cx);                                                       \
   else                                                                                      \
-    post_partials_kernel<KIND, ND, false><<<(unsigned)blocks, 256, 0, st>>>(                \
+    post_partials_kernel<KIND, ND, false, false><<<(unsigned)blocks, 256, 0, st>>>(         \
         Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,  \
-        0, nullptr)
+        0, nullptr, nullptr, 0, 0, nullptr)
 #define BO_POST_DISPATCH_D(KIND)                   \
   switch (d) {                                     \
     case 1: BO_POST_LAUNCH(KIND, 1); break;        \

@@ -199,6 +199,7 @@ class PostPartials:
     Spart: torch.Tensor
     mpart: torch.Tensor
     Rt: Optional[torch.Tensor] = None  # R^T (nC*128 x nrows_pad) on the gradient path
+    Cx: Optional[torch.Tensor] = None  # cross K*x^T (rq x nrows_pad), fused cross term
 
 
 def geometry(B: int, q: int, n: int):
@@ -217,9 +218,12 @@ def split_plan(B: int, q: int, n: int, slots: int = 0):
 
 
 def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
-                  split: Optional[int] = None) -> PostPartials:
+                  split: Optional[int] = None, cross: Optional[torch.Tensor] = None) -> PostPartials:
     """Column-tile partials of R R^T and R beta for X (B x q x d).  ``split``:
-    None = the library's plan, 0 = never split-k, k > 0 = chunks of k rows."""
+    None = the library's plan, 0 = never split-k, k > 0 = chunks of k rows.
+    ``cross`` (rq <= 16 rows x >= n): also return pp.Cx = cross K*x^T
+    (rq x nrows_pad) from the same pass -- on one-pass plans only; under a
+    split-k plan pp.Cx is None and R^T is stored instead."""
     dev = _dev(X)
     B, q, d = X.shape
     if d != cache.d:
@@ -242,11 +246,20 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
     else:
         kc_len, work_elems = 0, 0
     work = torch.empty(work_elems, **f64) if kc_len else None
+    Cx = None
+    if cross is not None and cross.shape[0] <= 16 and kc_len == 0:
+        cross = cross.contiguous()
+        Cx = torch.empty(cross.shape[0], nrows_pad, **f64)
+    elif cross is not None and Rt is None:
+        Rt = torch.empty(nC * 128, nrows_pad, **f64)  # the caller forms the cross term from R^T
     check(lib().bo_post_partials(cache.kind, _p(Xq), B, q, d, _p(cache.Xt_scaled), cache.n,
                                  _p(cache.U), cache.np, _p(cache.beta), cache.outputscale,
-                                 _p(Spart), _p(mpart), _p(Rt), kc_len, _p(work), st),
+                                 _p(Spart), _p(mpart), _p(Rt), kc_len, _p(work),
+                                 _p(cross if Cx is not None else None),
+                                 cross.shape[0] if Cx is not None else 0,
+                                 cross.shape[1] if Cx is not None else 0, _p(Cx), st),
           "post_partials")
-    return PostPartials(B, q, Qp, nrows_pad, nC, Xq, Spart, mpart, Rt)
+    return PostPartials(B, q, Qp, nrows_pad, nC, Xq, Spart, mpart, Rt, Cx)
 
 
 def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd: float,

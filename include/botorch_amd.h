@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 5
+#define BO_ABI_VERSION 6
 
 /* status codes */
 #define BO_OK 0
@@ -187,11 +187,16 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
  * Rt (nullable, gradient path): R^T, (nC*128) x nrows_pad.
  * kc_len > 0 runs split-k (chunks of kc_len training rows, then a reduction
  * in chunk order) with `work` >= work_elems doubles from bo_post_split_plan;
- * kc_len = 0: one workgroup per (column tile, row tile), work unused. */
+ * kc_len = 0: one workgroup per (column tile, row tile), work unused.
+ * Qc (nullable, one-pass only): rq <= 16 rows (leading dim ldq >= n) whose
+ * products with K*x are returned as Cx = Qc K*x^T (rq x nrows_pad) -- the
+ * qNEI cross-covariance P_b R^T = Q_b K*x^T, Q_b = P_b U^T
+ * (acquisition/cached_cholesky.py:94-120), without storing R. */
 int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
                      const double* Xt_scaled, int64_t n, const double* U, int64_t ldu, const double* beta,
                      double outputscale, double* Spart, double* mpart, double* Rt,
-                     int kc_len, double* work, void* stream);
+                     int kc_len, double* work, const double* Qc, int rq, int64_t ldq, double* Cx,
+                     void* stream);
 
 /* Split-k plan of bo_post_partials (host pointers): the chunk length in
  * {64, ..., 1024} (or 0 = one pass) that minimises a k-step cost model of the

@@ -269,3 +269,28 @@ def test_covar_batched_matches_torch(kind, n1, n2, d, outer, inner):
         ref = (1 + s5 + s5 * s5 / 3) * torch.exp(-s5)
     ref = os_.view(outer, 1, 1, 1) * ref
     torch.testing.assert_close(K.cpu(), ref, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("n,B,q,rq", [(4096, 512, 16, 1), (1000, 40, 4, 7), (300, 64, 16, 16)])
+def test_post_partials_cross_term(n, B, q, rq):
+    """Fused cross term Cx = Qc K*x^T (last column tile's workgroups) against
+    Qc U R^T from the stored R^T; Spart / mpart unchanged by it."""
+    from botorch_amd import kernels
+    X, Y, orc, h = _oracle_model(n)
+    c = _device_cache(X, Y, h, orc)
+    g = torch.Generator().manual_seed(n + rq)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64).to(DEV)
+    P = torch.zeros(rq, c.np, dtype=torch.float64)
+    P[:, :n] = torch.randn(rq, n, generator=g, dtype=torch.float64)
+    Qc = kernels.gemm(P.to(DEV), c.U, transB=True)            # rq x np = P U^T
+    kc, _ = kernels.split_plan(B, q, n)
+    ref = kernels.post_partials(c, Xc, store_R=True, split=0)
+    pp = kernels.post_partials(c, Xc, split=0, cross=Qc)
+    assert pp.Cx is not None and pp.Rt is None
+    want = P.to(DEV) @ ref.Rt[: c.np]                          # P R^T
+    torch.testing.assert_close(pp.Cx, want, rtol=1e-10, atol=1e-12)
+    torch.testing.assert_close(pp.Spart, ref.Spart, rtol=0, atol=0)
+    torch.testing.assert_close(pp.mpart, ref.mpart, rtol=0, atol=0)
+    if kc:  # split-k plans fall back to R^T for the caller's GEMM
+        sp = kernels.post_partials(c, Xc, cross=Qc)
+        assert sp.Cx is None and sp.Rt is not None
