@@ -238,34 +238,42 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     kv[kk] = eval_kernel_row<KIND, ND>(xi, Xt, n, kbeg + kh * 8 + kk, outputscale, ivalid);
   BO_STORE(0);
   __syncthreads();
-  for (int t = 0; t < nsteps; ++t) {
-    const int cur = t & 1;
-    const bool more = t + 1 < nsteps;
-    const int knext = kbeg + (more ? (t + 1) * PK : t * PK);  // last step re-reads (unused)
-    BO_LOAD_Q(kbeg + t * PK);
-    BO_LOAD_U(knext);
-#pragma unroll
-    for (int ks = 0; ks < PK / 4; ++ks) {
-      const int kr = ks * 4 + (lane >> 4);
-      double a[8], b[2];
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct) a[ct] = Us[cur][kr][ct * 16 + (lane & 15)];
-#pragma unroll
-      for (int it = 0; it < 2; ++it) b[it] = Ks[cur][kr][wave * 32 + it * 16 + (lane & 15)];
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct)
-#pragma unroll
-        for (int it = 0; it < 2; ++it) acc[ct][it] = mfma_f64(a[ct], b[it], acc[ct][it]);
-      if (cross) {
-        accx[0] = mfma_f64(qa[ks], b[0], accx[0]);
-        accx[1] = mfma_f64(qa[ks], b[1], accx[1]);
-      }
-      kv[2 * ks] = eval_kernel_row<KIND, ND>(xi, Xt, n, knext + kh * 8 + 2 * ks, outputscale, ivalid);
-      kv[2 * ks + 1] = eval_kernel_row<KIND, ND>(xi, Xt, n, knext + kh * 8 + 2 * ks + 1, outputscale, ivalid);
-    }
-    if (more) BO_STORE(cur ^ 1);
-    __syncthreads();
+  // One k-step; XMFMA = the cross-term MFMAs (cross workgroups only: a
+  // separate copy of the loop keeps the common loop free of branches, which
+  // would split its MFMA / kernel-evaluation interleaving).
+#define BO_KSTEP(XLOAD, XMFMA)                                                       \
+  {                                                                                  \
+    const int cur = t & 1;                                                           \
+    const bool more = t + 1 < nsteps;                                                \
+    const int knext = kbeg + (more ? (t + 1) * PK : t * PK);                         \
+    XLOAD                                                                            \
+    BO_LOAD_U(knext);                                                                \
+    _Pragma("unroll") for (int ks = 0; ks < PK / 4; ++ks) {                         \
+      const int kr = ks * 4 + (lane >> 4);                                           \
+      double a[8], b[2];                                                             \
+      _Pragma("unroll") for (int ct = 0; ct < 8; ++ct) a[ct] = Us[cur][kr][ct * 16 + (lane & 15)]; \
+      _Pragma("unroll") for (int it = 0; it < 2; ++it)                              \
+        b[it] = Ks[cur][kr][wave * 32 + it * 16 + (lane & 15)];                      \
+      _Pragma("unroll") for (int ct = 0; ct < 8; ++ct)                              \
+        _Pragma("unroll") for (int it = 0; it < 2; ++it)                            \
+          acc[ct][it] = mfma_f64(a[ct], b[it], acc[ct][it]);                         \
+      XMFMA                                                                          \
+      kv[2 * ks] = eval_kernel_row<KIND, ND>(xi, Xt, n, knext + kh * 8 + 2 * ks, outputscale, ivalid); \
+      kv[2 * ks + 1] =                                                               \
+          eval_kernel_row<KIND, ND>(xi, Xt, n, knext + kh * 8 + 2 * ks + 1, outputscale, ivalid); \
+    }                                                                                \
+    if (more) BO_STORE(cur ^ 1);                                                     \
+    __syncthreads();                                                                 \
   }
+  if (cross) {
+    for (int t = 0; t < nsteps; ++t)
+      BO_KSTEP(BO_LOAD_Q(kbeg + t * PK),
+               accx[0] = mfma_f64(qa[ks], b[0], accx[0]);
+               accx[1] = mfma_f64(qa[ks], b[1], accx[1]);)
+  } else {
+    for (int t = 0; t < nsteps; ++t) BO_KSTEP(, )
+  }
+#undef BO_KSTEP
 #undef BO_LOAD_U
 #undef BO_STORE
 #undef BO_LOAD_Q
