@@ -191,11 +191,13 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     acc[a][0] = v4d_zero();
     acc[a][1] = v4d_zero();
   }
-  // Cross term (CROSS): the last column tile's workgroups stream every k of
-  // K*x through LDS, so they also accumulate Cx = Qc K*x^T for rq <= 16 extra
-  // rows of Qc (2 MFMAs per 16 of the tile's own): the qNEI cross-covariance
-  // P_b R^T = Q_b K*x^T without materialising R.
-  const bool cross = CROSS && ci == nC - 1;
+  // Cross term (CROSS): while K*x streams through LDS, accumulate
+  // Cx = Qc K*x^T for rq <= 16 extra rows of Qc (2 MFMAs per 16 of the tile's
+  // own) -- the qNEI cross-covariance P_b R^T = Q_b K*x^T without
+  // materialising R.  Column tile ci takes the k-block [128 ci, 128 ci + 128),
+  // the last steps of its own range, and writes a partial Cx[ci]; spreading
+  // the extra MFMAs over all tiles keeps the longest tiles' length unchanged.
+  const bool cross = CROSS;
   v4d accx[2] = {v4d_zero(), v4d_zero()};
   double qa[4] = {0.0, 0.0, 0.0, 0.0};
   const bool qrow = CROSS && (lane & 15) < rq;
@@ -265,13 +267,16 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     if (more) BO_STORE(cur ^ 1);                                                     \
     __syncthreads();                                                                 \
   }
+  int t = 0;
   if (cross) {
-    for (int t = 0; t < nsteps; ++t)
+    const int tc = min(nsteps, c0 / PK);
+    for (; t < tc; ++t) BO_KSTEP(, )
+    for (; t < nsteps; ++t)
       BO_KSTEP(BO_LOAD_Q(kbeg + t * PK),
                accx[0] = mfma_f64(qa[ks], b[0], accx[0]);
                accx[1] = mfma_f64(qa[ks], b[1], accx[1]);)
   } else {
-    for (int t = 0; t < nsteps; ++t) BO_KSTEP(, )
+    for (; t < nsteps; ++t) BO_KSTEP(, )
   }
 #undef BO_KSTEP
 #undef BO_LOAD_U
@@ -284,7 +289,9 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = mfma_row(lane, r);
-        if (j < rq) Cx[(int64_t)j * nrows_pad + i0 + wave * 32 + it * 16 + mfma_col(lane)] = accx[it][r];
+        if (j < rq)
+          Cx[((int64_t)ci * rq + j) * nrows_pad + i0 + wave * 32 + it * 16 + mfma_col(lane)] =
+              accx[it][r];
       }
   }
 

@@ -249,7 +249,7 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
     Cx = None
     if cross is not None and cross.shape[0] <= 16 and kc_len == 0:
         cross = cross.contiguous()
-        Cx = torch.empty(cross.shape[0], nrows_pad, **f64)
+        Cx = torch.empty(nC, cross.shape[0], nrows_pad, **f64)  # column-tile partials
     elif cross is not None and Rt is None:
         Rt = torch.empty(nC * 128, nrows_pad, **f64)  # the caller forms the cross term from R^T
     check(lib().bo_post_partials(cache.kind, _p(Xq), B, q, d, _p(cache.Xt_scaled), cache.n,
@@ -259,7 +259,8 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
                                  cross.shape[0] if Cx is not None else 0,
                                  cross.shape[1] if Cx is not None else 0, _p(Cx), st),
           "post_partials")
-    return PostPartials(B, q, Qp, nrows_pad, nC, Xq, Spart, mpart, Rt, Cx)
+    return PostPartials(B, q, Qp, nrows_pad, nC, Xq, Spart, mpart, Rt,
+                        Cx.sum(dim=0) if Cx is not None else None)
 
 
 def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd: float,

@@ -189,7 +189,8 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
  * in chunk order) with `work` >= work_elems doubles from bo_post_split_plan;
  * kc_len = 0: one workgroup per (column tile, row tile), work unused.
  * Qc (nullable, one-pass only): rq <= 16 rows (leading dim ldq >= n) whose
- * products with K*x are returned as Cx = Qc K*x^T (rq x nrows_pad) -- the
+ * products with K*x are returned as nC column-tile partials
+ * Cx[ci] (nC x rq x nrows_pad; sum over ci = Qc K*x^T) -- the
  * qNEI cross-covariance P_b R^T = Q_b K*x^T, Q_b = P_b U^T
  * (acquisition/cached_cholesky.py:94-120), without storing R. */
 int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
