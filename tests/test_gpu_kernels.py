@@ -53,6 +53,27 @@ def test_gemm_small_batched(M, N, K, batch, ta, tb):
     torch.testing.assert_close(out.cpu(), ref, rtol=1e-12, atol=1e-11)
 
 
+@pytest.mark.parametrize("M,N,K,flags", [(3968, 128, 128, 4), (2432, 128, 128, 1), (200, 100, 37, 0),
+                                          (1000, 33, 256, 2)])
+def test_gemm_strip_panels(M, N, K, flags):
+    """N <= 128, short k, few tiles: the 16 x 128 strip kernel (Cholesky panels)."""
+    from botorch_amd import kernels
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    Bm = torch.randn(N, K, generator=g, dtype=torch.float64)
+    C0 = torch.randn(M, N, generator=g, dtype=torch.float64)
+    Aop = torch.tril(A) if flags & 2 else A
+    Bop = torch.triu(Bm.T) if flags & 4 else Bm.T          # op(B) = B^T (tb)
+    ref = -1.0 * (Aop @ Bop) + C0
+    out = kernels.gemm(A.to(DEV), Bm.to(DEV), False, True, alpha=-1.0, beta=1.0,
+                       C=C0.clone().to(DEV), flags=flags).cpu()
+    if flags & 1:
+        torch.testing.assert_close(torch.tril(out), torch.tril(ref), rtol=1e-12, atol=1e-11)
+        torch.testing.assert_close(torch.triu(out, 1), torch.triu(C0, 1))
+    else:
+        torch.testing.assert_close(out, ref, rtol=1e-12, atol=1e-11)
+
+
 def test_gemm_small_flags():
     from botorch_amd import kernels, _lib
     g = torch.Generator().manual_seed(5)
