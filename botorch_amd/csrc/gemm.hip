@@ -278,60 +278,45 @@ namespace {
 // (a 128 x 128 tile would spend orders of magnitude more flops on padding).
 // Structure flags mask the operands exactly as the tiled kernel's k-range
 // skipping does.
-template <int NT>
 __global__ __launch_bounds__(256) void gemm_small_kernel(
     int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda, int64_t sA,
     int ta, const double* __restrict__ B, int64_t ldb, int64_t sB, int tb, double beta,
     double* __restrict__ C, int64_t ldc, int64_t sC, int batch, int flags) {
-  // One wave per (batch member, 16-row block, group of 16 NT columns); NT
-  // accumulators share each A fragment.
   const int lane = threadIdx.x & 63;
   const int mblocks = (M + 15) >> 4;
-  const int ngroups = (N + 16 * NT - 1) / (16 * NT);
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (w >= (int64_t)batch * mblocks * ngroups) return;
-  const int64_t z = w / ((int64_t)mblocks * ngroups);
-  const int rest = (int)(w - z * mblocks * ngroups);
-  const int m0 = (rest / ngroups) * 16;
-  const int n0 = (rest % ngroups) * 16 * NT;
+  if (w >= (int64_t)batch * mblocks) return;
+  const int64_t z = w / mblocks;
+  const int m0 = (int)(w - z * mblocks) * 16;
   const double* Az = A + z * sA;
   const double* Bz = B + z * sB;
-  const int r16 = lane & 15;  // A fragment row m0 + r16 / B fragment column
+  const int r16 = lane & 15;  // A fragment row m0 + r16 / B fragment column j
   const int kq = lane >> 4;
   const int ia = m0 + r16;
-  v4d acc[NT];
-#pragma unroll
-  for (int c = 0; c < NT; ++c) acc[c] = v4d_zero();
+  v4d acc = v4d_zero();
   for (int k0 = 0; k0 < K; k0 += 4) {
     const int k = k0 + kq;
-    double a = 0.0;
+    double a = 0.0, b = 0.0;
     if (ia < M && k < K) {
       a = ta ? Az[(int64_t)k * lda + ia] : Az[(int64_t)ia * lda + k];
       if (((flags & BO_GEMM_A_LOWER) && k > ia) || ((flags & BO_GEMM_A_UPPER) && k < ia)) a = 0.0;
     }
-#pragma unroll
-    for (int c = 0; c < NT; ++c) {
-      const int jb = n0 + c * 16 + r16;
-      double b = 0.0;
-      if (jb < N && k < K) {
-        b = tb ? Bz[(int64_t)jb * ldb + k] : Bz[(int64_t)k * ldb + jb];
-        if (((flags & BO_GEMM_B_UPPER) && k > jb) || ((flags & BO_GEMM_B_LOWER) && k < jb)) b = 0.0;
-      }
-      acc[c] = mfma_f64(a, b, acc[c]);
+    if (r16 < N && k < K) {
+      b = tb ? Bz[(int64_t)r16 * ldb + k] : Bz[(int64_t)k * ldb + r16];
+      if (((flags & BO_GEMM_B_UPPER) && k > r16) || ((flags & BO_GEMM_B_LOWER) && k < r16)) b = 0.0;
     }
+    acc = mfma_f64(a, b, acc);
   }
   double* Cz = C + z * sC;
 #pragma unroll
-  for (int c = 0; c < NT; ++c)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = m0 + mfma_row(lane, r), j = n0 + c * 16 + mfma_col(lane);
-      if (i < M && j < N && (!(flags & BO_GEMM_LOWER_C) || i >= j)) {
-        double v = alpha * acc[c][r];
-        if (beta != 0.0) v = fma(beta, Cz[(int64_t)i * ldc + j], v);
-        Cz[(int64_t)i * ldc + j] = v;
-      }
+  for (int r = 0; r < 4; ++r) {
+    const int i = m0 + mfma_row(lane, r), j = mfma_col(lane);
+    if (i < M && j < N && (!(flags & BO_GEMM_LOWER_C) || i >= j)) {
+      double c = alpha * acc[r];
+      if (beta != 0.0) c = fma(beta, Cz[(int64_t)i * ldc + j], c);
+      Cz[(int64_t)i * ldc + j] = c;
     }
+  }
 }
 
 }  // namespace
@@ -344,19 +329,7 @@ int bo_gemm_f64_impl(int ta, int tb, int M, int N, int K, double alpha, const do
   if (K < 0) K = 0;  // C = beta * C (the alpha term is empty)
   if (N <= 16 && (M <= 16 || K <= 256)) {
     const int64_t waves = (int64_t)batch * ceil_div(M, 16);
-    gemm_small_kernel<1><<<(unsigned)ceil_div(waves, 4), 256, 0, st>>>(
-        M, N, K, alpha, A, lda, sA, ta, B, ldb, sB, tb, beta, C, ldc, sC, batch, flags);
-    BO_LAUNCH_CHECK();
-    return BO_OK;
-  }
-  // Panel products of the blocked Cholesky (rem x 128 x 128: the solve against
-  // the inverted diagonal block and the look-ahead update) and other short-k,
-  // narrow products whose 64 x 64 tile grid would leave most CUs idle while
-  // each tile walks its k-steps through LDS: one wave per 16 x 128 strip,
-  // operands straight from L1/L2.
-  if (N <= 128 && K <= 256 && ceil_div(M, 64) * ceil_div(N, 64) * (int64_t)batch < 512) {
-    const int64_t waves = (int64_t)batch * ceil_div(M, 16) * ceil_div(N, 128);
-    gemm_small_kernel<8><<<(unsigned)ceil_div(waves, 4), 256, 0, st>>>(
+    gemm_small_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, st>>>(
         M, N, K, alpha, A, lda, sA, ta, B, ldb, sB, tb, beta, C, ldc, sC, batch, flags);
     BO_LAUNCH_CHECK();
     return BO_OK;

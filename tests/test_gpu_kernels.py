@@ -56,7 +56,7 @@ def test_gemm_small_batched(M, N, K, batch, ta, tb):
 @pytest.mark.parametrize("M,N,K,flags", [(3968, 128, 128, 4), (2432, 128, 128, 1), (200, 100, 37, 0),
                                           (1000, 33, 256, 2)])
 def test_gemm_strip_panels(M, N, K, flags):
-    """N <= 128, short k, few tiles: the 16 x 128 strip kernel (Cholesky panels)."""
+    """The blocked Cholesky panel shapes (rem x 128 x 128, triangular / lower-C flags)."""
     from botorch_amd import kernels
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g, dtype=torch.float64)
