@@ -343,11 +343,13 @@ __global__ __launch_bounds__(256, 1) void gemm_shortk_kernel(
   if ((flags & BO_GEMM_LOWER_C) && n0 > m0 + SK_T - 1) return;  // tile above the diagonal
   const double* Az = A + z * sA;
   const double* Bz = B + z * sB;
-  const int KP = (K + 3) & ~3;  // k padded to the MFMA's 4
+  // The slabs are always SK_K deep (zero beyond K): compile-time index
+  // arithmetic (shifts and masks) instead of divisions by a runtime K.
+  constexpr int KP = SK_K;
   // Element e of a slab: the contiguous global dimension varies fastest.
   // op(A)[m][k]: ta -> A[k][m] (m contiguous), else A[m][k] (k contiguous).
   constexpr int BATCH = 16;
-  const int total = SK_T * KP;
+  constexpr int total = SK_T * KP;
   for (int e0 = 0; e0 < total; e0 += 256 * BATCH) {
     double va[BATCH], vb[BATCH];
 #pragma unroll
@@ -392,7 +394,8 @@ __global__ __launch_bounds__(256, 1) void gemm_shortk_kernel(
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
   v4d acc[2][2] = {{v4d_zero(), v4d_zero()}, {v4d_zero(), v4d_zero()}};
-  for (int k0 = 0; k0 < KP; k0 += 4) {
+  const int kmax = (K + 3) & ~3;
+  for (int k0 = 0; k0 < kmax; k0 += 4) {
     const int kr = k0 + (lane >> 4);
     double a[2], b[2];
 #pragma unroll
