@@ -319,114 +319,6 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(
   }
 }
 
-// Short-k tiles (K <= 128): the 64 x 64 output tile's whole op(A) (64 x K) and
-// op(B) (K x 64) slabs are loaded into LDS in one go -- every global load of
-// the tile in flight together -- and then consumed by the MFMAs.  The
-// pipelined tile kernel walks k in 16-wide stages and pays one L2/HBM round
-// trip per stage; for the blocked Cholesky's panel solves and look-ahead
-// updates (rem x 128 x 128, grids of a few dozen tiles) that round-trip chain
-// was the whole duration.  One workgroup per CU (147 KB of LDS).
-constexpr int SK_T = 64;        // tile
-constexpr int SK_K = 128;       // max k
-constexpr int SK_P = SK_T + 8;  // LDS pitch (doubles)
-
-__global__ __launch_bounds__(256, 1) void gemm_shortk_kernel(
-    int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda, int64_t sA,
-    int ta, const double* __restrict__ B, int64_t ldb, int64_t sB, int tb, double beta,
-    double* __restrict__ C, int64_t ldc, int64_t sC, int flags, int tilesN) {
-  __shared__ __attribute__((aligned(16))) double As[SK_K][SK_P];  // As[k][m] = op(A)[m0+m][k]
-  __shared__ __attribute__((aligned(16))) double Bs[SK_K][SK_P];  // Bs[k][n] = op(B)[k][n0+n]
-  const int tid = threadIdx.x;
-  const int64_t z = blockIdx.y;
-  const int ti = blockIdx.x / tilesN, tj = blockIdx.x - (blockIdx.x / tilesN) * tilesN;
-  const int m0 = ti * SK_T, n0 = tj * SK_T;
-  if ((flags & BO_GEMM_LOWER_C) && n0 > m0 + SK_T - 1) return;  // tile above the diagonal
-  const double* Az = A + z * sA;
-  const double* Bz = B + z * sB;
-  // The slabs are always SK_K deep (zero beyond K): compile-time index
-  // arithmetic (shifts and masks) instead of divisions by a runtime K.
-  constexpr int KP = SK_K;
-  // Element e of a slab: the contiguous global dimension varies fastest.
-  // op(A)[m][k]: ta -> A[k][m] (m contiguous), else A[m][k] (k contiguous).
-  constexpr int BATCH = 16;
-  constexpr int total = SK_T * KP;
-  for (int e0 = 0; e0 < total; e0 += 256 * BATCH) {
-    double va[BATCH], vb[BATCH];
-#pragma unroll
-    for (int u = 0; u < BATCH; ++u) {
-      const int e = e0 + u * 256 + tid;
-      va[u] = 0.0;
-      vb[u] = 0.0;
-      if (e < total) {
-        int m, k;
-        if (ta) { m = e % SK_T; k = e / SK_T; } else { k = e % KP; m = e / KP; }
-        const int gm = m0 + m;
-        if (gm < M && k < K) {
-          const double v = ta ? Az[(int64_t)k * lda + gm] : Az[(int64_t)gm * lda + k];
-          const bool zero = ((flags & BO_GEMM_A_LOWER) && k > gm) || ((flags & BO_GEMM_A_UPPER) && k < gm);
-          va[u] = zero ? 0.0 : v;
-        }
-        int n, kb;
-        if (tb) { kb = e % KP; n = e / KP; } else { n = e % SK_T; kb = e / SK_T; }
-        const int gn = n0 + n;
-        if (gn < N && kb < K) {
-          const double v = tb ? Bz[(int64_t)gn * ldb + kb] : Bz[(int64_t)kb * ldb + gn];
-          const bool zero = ((flags & BO_GEMM_B_UPPER) && kb > gn) || ((flags & BO_GEMM_B_LOWER) && kb < gn);
-          vb[u] = zero ? 0.0 : v;
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < BATCH; ++u) {
-      const int e = e0 + u * 256 + tid;
-      if (e < total) {
-        int m, k;
-        if (ta) { m = e % SK_T; k = e / SK_T; } else { k = e % KP; m = e / KP; }
-        As[k][m] = va[u];
-        int n, kb;
-        if (tb) { kb = e % KP; n = e / KP; } else { n = e % SK_T; kb = e / SK_T; }
-        Bs[kb][n] = vb[u];
-      }
-    }
-  }
-  __syncthreads();
-  // 4 waves in a 2 x 2 grid of 32 x 32 sub-tiles, 2 x 2 MFMA accumulators each.
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-  v4d acc[2][2] = {{v4d_zero(), v4d_zero()}, {v4d_zero(), v4d_zero()}};
-  const int kmax = (K + 3) & ~3;
-  for (int k0 = 0; k0 < kmax; k0 += 4) {
-    const int kr = k0 + (lane >> 4);
-    double a[2], b[2];
-#pragma unroll
-    for (int x = 0; x < 2; ++x) {
-      a[x] = As[kr][wm + x * 16 + (lane & 15)];
-      b[x] = Bs[kr][wn + x * 16 + (lane & 15)];
-    }
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int y = 0; y < 2; ++y) acc[x][y] = mfma_f64(a[x], b[y], acc[x][y]);
-  }
-  // D(row, col) = sum_k A(row, k) B(k, col) with row = mfma_row(lane, r) of the
-  // A fragment's m and col = mfma_col(lane) of the B fragment's n.
-  double* Cz = C + z * sC;
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = m0 + wm + x * 16 + mfma_row(lane, r);
-        const int j = n0 + wn + y * 16 + mfma_col(lane);
-        if (i < M && j < N && (!(flags & BO_GEMM_LOWER_C) || i >= j)) {
-          double v = alpha * acc[x][y][r];
-          if (beta != 0.0) v = fma(beta, Cz[(int64_t)i * ldc + j], v);
-          Cz[(int64_t)i * ldc + j] = v;
-        }
-      }
-}
-
 }  // namespace
 
 int bo_gemm_f64_impl(int ta, int tb, int M, int N, int K, double alpha, const double* A,
@@ -439,15 +331,6 @@ int bo_gemm_f64_impl(int ta, int tb, int M, int N, int K, double alpha, const do
     const int64_t waves = (int64_t)batch * ceil_div(M, 16);
     gemm_small_kernel<<<(unsigned)ceil_div(waves, 4), 256, 0, st>>>(
         M, N, K, alpha, A, lda, sA, ta, B, ldb, sB, tb, beta, C, ldc, sC, batch, flags);
-    BO_LAUNCH_CHECK();
-    return BO_OK;
-  }
-  const int64_t tiles64 = ceil_div(M, 64) * ceil_div(N, 64) * (int64_t)batch;
-  if (K <= SK_K && tiles64 < 512 && batch <= 65535) {
-    const int tilesN = (int)ceil_div(N, SK_T);
-    dim3 grid((unsigned)(ceil_div(M, SK_T) * tilesN), (unsigned)batch);
-    gemm_shortk_kernel<<<grid, 256, 0, st>>>(M, N, K, alpha, A, lda, sA, ta, B, ldb, sB, tb, beta,
-                                             C, ldc, sC, flags, tilesN);
     BO_LAUNCH_CHECK();
     return BO_OK;
   }
