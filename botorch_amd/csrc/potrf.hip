@@ -7,10 +7,11 @@
 // held in LDS (128 rows at pitch 130 doubles = 133 KB of the CU's 160 KB) and
 // factored as four 32-column sub-panels:
 //   F1  wave 0 factors the 32 x 32 diagonal sub-block AND builds its inverse in
-//       one sweep: each lane owns a 4 x 4 tile of L and of X = L^{-1}; step j
-//       broadcasts column j of L and row j of X through LDS and applies the
-//       rank-1 updates of both (right-looking Cholesky + right-looking
-//       forward substitution), so the sequential chain is 32 short steps;
+//       one sweep: each lane owns a 4 x 4 tile of L and of X = L^{-1}; a step
+//       factors a 2 x 2 pivot block, broadcasts columns j, j+1 of L and rows
+//       j, j+1 of X through LDS and applies the rank-2 updates of both
+//       (right-looking Cholesky + right-looking forward substitution), so the
+//       sequential chain is 16 short steps;
 //   F2  the sub-panel below is solved against that inverse on the fp64 MFMA
 //       (each wave owns whole 16-row strips and updates them in place);
 //   F3  the trailing lower triangle of the block takes the rank-32 update on the
@@ -79,7 +80,10 @@ __device__ __forceinline__ void tri_index(int t, int& tr, int& tc) {
 
 // Factor the 32 x 32 block at Sd (in place, lower; upper zeroed) and write its
 // inverse (lower, upper zeroed) at Dd.  One wave; lane = (ti, tj) owns rows
-// 4 ti.., cols 4 tj.. of both L and X.  Returns the 1-based failing pivot or 0.
+// 4 ti.., cols 4 tj.. of both L and X.  Two columns per step (a 2 x 2 pivot
+// block): the sequential chain -- pivot broadcast, 1/sqrt, column broadcast
+// through LDS -- runs 16 times instead of 32, each step applying a rank-2
+// update.  Returns the 1-based failing pivot or 0.
 __device__ __forceinline__ int factor32(double* Sd, double* Dd, double* colbuf, double* rowbuf,
                                         int lane) {
   const int ti = lane >> 3, tj = lane & 7;
@@ -93,76 +97,111 @@ __device__ __forceinline__ int factor32(double* Sd, double* Dd, double* colbuf, 
       x[u][v] = (l == i) ? 1.0 : 0.0;
     }
   int fail = 0;
-  // 1/sqrt by v_rsq_f64 + two Newton steps (full fp64 accuracy): off the sqrt +
-  // divide macro sequences, and computed one step AHEAD (right after the next
-  // pivot's own update) so its latency hides under the step's other FMAs.
+  // 1/sqrt by v_rsq_f64 + two Newton steps (full fp64 accuracy).
   auto rsq_nr = [](double v) {
     double r = __builtin_amdgcn_rsq(v);
     r = r * fma(-0.5 * v * r, r, 1.5);
     r = r * fma(-0.5 * v * r, r, 1.5);
     return r;
   };
-  double ajj = readlane_d(a[0][0], 0);
-  double inv = rsq_nr(ajj);
+  // Pivot block of step j (rows/cols j, j+1), from the owner lane (jt, jt):
+  //   L00 = sqrt(p00), L10 = p10 / L00, L11 = sqrt(p11 - L10^2).
+  double p00 = readlane_d(a[0][0], 0), p10 = readlane_d(a[1][0], 0),
+         p11 = readlane_d(a[1][1], 0);
+  double inv0 = rsq_nr(p00);
+  double L10 = p10 * inv0;
+  double s11 = fma(-L10, L10, p11);
+  double inv1 = rsq_nr(s11);
 #pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    const int jt = j >> 2, ju = j & 3;
-    if (!(ajj > 0.0) && fail == 0) fail = j + 1;
-    const double d = ajj * inv;
-    // column j of L (owners: tj == jt) -> colbuf
+  for (int j = 0; j < 32; j += 2) {
+    const int jt = j >> 2, ju = j & 3;  // ju in {0, 2}
+    if (fail == 0) {
+      if (!(p00 > 0.0)) fail = j + 1;
+      else if (!(s11 > 0.0)) fail = j + 2;
+    }
+    const double L00 = p00 * inv0, L11 = s11 * inv1;
+    // columns j, j+1 of L (owners: tj == jt) -> colbuf[0..31], colbuf[32..63]
     if (tj == jt) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int i = 4 * ti + u;
-        const double lij = (i > j) ? a[u][ju] * inv : ((i == j) ? d : 0.0);
-        a[u][ju] = lij;
-        colbuf[i] = lij;
+        const double c0 = (i > j) ? a[u][ju] * inv0 : ((i == j) ? L00 : 0.0);
+        const double c1 = (i > j + 1) ? fma(-c0, L10, a[u][ju + 1]) * inv1 : ((i == j + 1) ? L11 : 0.0);
+        a[u][ju] = c0;
+        a[u][ju + 1] = c1;
+        colbuf[i] = c0;
+        colbuf[32 + i] = c1;
       }
     }
-    // row j of X scaled by 1/L_jj (owners: ti == jt) -> rowbuf
+    // rows j, j+1 of X (owners: ti == jt): forward substitution by the pivot block
     if (ti == jt) {
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        x[ju][v] *= inv;
-        rowbuf[4 * tj + v] = x[ju][v];
+        const double xj = x[ju][v] * inv0;
+        const double xj1 = fma(-L10, xj, x[ju + 1][v]) * inv1;
+        x[ju][v] = xj;
+        x[ju + 1][v] = xj1;
+        rowbuf[4 * tj + v] = xj;
+        rowbuf[32 + 4 * tj + v] = xj1;
       }
     }
-    // One wave: its LDS operations execute in program order, so other lanes'
-    // stores above are visible to the loads below without a barrier.  The
-    // empty asm is a compiler-only fence: the loads are re-issued after the
-    // stores (other lanes' writes are invisible to the compiler's per-thread
-    // view) and may still be batched.
+    // One wave: its LDS operations execute in program order (see the
+    // compiler-only fences), so the other lanes' stores above are visible.
     asm volatile("" ::: "memory");
-    const double2 r01 = *reinterpret_cast<const double2*>(colbuf + 4 * ti);
-    const double2 r23 = *reinterpret_cast<const double2*>(colbuf + 4 * ti + 2);
-    const double2 c01 = *reinterpret_cast<const double2*>(colbuf + 4 * tj);
-    const double2 c23 = *reinterpret_cast<const double2*>(colbuf + 4 * tj + 2);
-    const double2 x01 = *reinterpret_cast<const double2*>(rowbuf + 4 * tj);
-    const double2 x23 = *reinterpret_cast<const double2*>(rowbuf + 4 * tj + 2);
+    double Lr0[4], Lr1[4], Lc0[4], Lc1[4], X0[4], X1[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const double2 r0 = *reinterpret_cast<const double2*>(colbuf + 4 * ti + 2 * h);
+      const double2 r1 = *reinterpret_cast<const double2*>(colbuf + 32 + 4 * ti + 2 * h);
+      const double2 q0 = *reinterpret_cast<const double2*>(colbuf + 4 * tj + 2 * h);
+      const double2 q1 = *reinterpret_cast<const double2*>(colbuf + 32 + 4 * tj + 2 * h);
+      const double2 y0 = *reinterpret_cast<const double2*>(rowbuf + 4 * tj + 2 * h);
+      const double2 y1 = *reinterpret_cast<const double2*>(rowbuf + 32 + 4 * tj + 2 * h);
+      Lr0[2 * h] = r0.x; Lr0[2 * h + 1] = r0.y;
+      Lr1[2 * h] = r1.x; Lr1[2 * h + 1] = r1.y;
+      Lc0[2 * h] = q0.x; Lc0[2 * h + 1] = q0.y;
+      Lc1[2 * h] = q1.x; Lc1[2 * h + 1] = q1.y;
+      X0[2 * h] = y0.x; X0[2 * h + 1] = y0.y;
+      X1[2 * h] = y1.x; X1[2 * h + 1] = y1.y;
+    }
     asm volatile("" ::: "memory");
-    // Masks folded into the broadcast operands (4 selects instead of 32):
-    // Cholesky update only for columns l > j (rows < j have L = 0 already),
-    // substitution only for rows i > j.
-    const double Lr[4] = {r01.x, r01.y, r23.x, r23.y};
-    const double Lcm[4] = {(4 * tj + 0 > j) ? -c01.x : 0.0, (4 * tj + 1 > j) ? -c01.y : 0.0,
-                           (4 * tj + 2 > j) ? -c23.x : 0.0, (4 * tj + 3 > j) ? -c23.y : 0.0};
-    const double Lrm[4] = {(4 * ti + 0 > j) ? -r01.x : 0.0, (4 * ti + 1 > j) ? -r01.y : 0.0,
-                           (4 * ti + 2 > j) ? -r23.x : 0.0, (4 * ti + 3 > j) ? -r23.y : 0.0};
-    const double Xr[4] = {x01.x, x01.y, x23.x, x23.y};
-    // next pivot first: its element (u1, u1) of the owner lane (jt1, jt1)
-    const int j1 = j + 1;
+    // Masks folded into the broadcast operands: the Cholesky update touches
+    // columns l > j+1 only, the substitution rows i > j+1 only.
+    double Lcm0[4], Lcm1[4], Lrm0[4], Lrm1[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const bool cl = 4 * tj + v > j + 1;
+      Lcm0[v] = cl ? -Lc0[v] : 0.0;
+      Lcm1[v] = cl ? -Lc1[v] : 0.0;
+      const bool rw = 4 * ti + v > j + 1;
+      Lrm0[v] = rw ? -Lr0[v] : 0.0;
+      Lrm1[v] = rw ? -Lr1[v] : 0.0;
+    }
+    // next pivot block first (its rsq chain then overlaps the bulk update)
+    const int j1 = j + 2;
     const int u1 = j1 & 3;
     if (j1 < 32) {
-      a[u1][u1] = fma(Lr[u1], Lcm[u1], a[u1][u1]);
-      ajj = readlane_d(a[u1][u1], (j1 >> 2) * 9);
-      inv = rsq_nr(ajj);
+      a[u1][u1] = fma(Lr1[u1], Lcm1[u1], fma(Lr0[u1], Lcm0[u1], a[u1][u1]));
+      a[u1 + 1][u1] = fma(Lr1[u1 + 1], Lcm1[u1], fma(Lr0[u1 + 1], Lcm0[u1], a[u1 + 1][u1]));
+      a[u1 + 1][u1 + 1] =
+          fma(Lr1[u1 + 1], Lcm1[u1 + 1], fma(Lr0[u1 + 1], Lcm0[u1 + 1], a[u1 + 1][u1 + 1]));
+      const int src = (j1 >> 2) * 9;
+      p00 = readlane_d(a[u1][u1], src);
+      p10 = readlane_d(a[u1 + 1][u1], src);
+      p11 = readlane_d(a[u1 + 1][u1 + 1], src);
+      inv0 = rsq_nr(p00);
+      L10 = p10 * inv0;
+      s11 = fma(-L10, L10, p11);
+      inv1 = rsq_nr(s11);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        if (!(j1 < 32 && u == u1 && v == u1)) a[u][v] = fma(Lr[u], Lcm[v], a[u][v]);
-        x[u][v] = fma(Lrm[u], Xr[v], x[u][v]);
+        const bool early = j1 < 32 && ((u == u1 && v == u1) || (u == u1 + 1 && v == u1) ||
+                                       (u == u1 + 1 && v == u1 + 1));
+        if (!early) a[u][v] = fma(Lr1[u], Lcm1[v], fma(Lr0[u], Lcm0[v], a[u][v]));
+        x[u][v] = fma(Lrm1[u], X1[v], fma(Lrm0[u], X0[v], x[u][v]));
       }
   }
   if (lane < 64) {
@@ -188,8 +227,8 @@ __global__ __launch_bounds__(256) void potrf_block_kernel(double* __restrict__ A
                                                           int64_t ldi, int* __restrict__ info,
                                                           long long* __restrict__ tsc) {
   __shared__ __attribute__((aligned(16))) double S[DB * SP];
-  __shared__ __attribute__((aligned(16))) double colbuf[32];
-  __shared__ __attribute__((aligned(16))) double rowbuf[32];
+  __shared__ __attribute__((aligned(16))) double colbuf[64];
+  __shared__ __attribute__((aligned(16))) double rowbuf[64];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
