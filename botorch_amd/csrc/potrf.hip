@@ -112,9 +112,15 @@ __device__ __forceinline__ int factor32(double* Sd, double* Dd, double* colbuf, 
   double L10 = p10 * inv0;
   double s11 = fma(-L10, L10, p11);
   double inv1 = rsq_nr(s11);
+  // Outer loop over 4-column lane blocks NOT unrolled: the straight-line
+  // 16-step body would be several thousand instructions that stream through
+  // the instruction cache every call; the inner pair of 2-column steps is
+  // unrolled so every register index (ju, u1) stays compile-time.
+#pragma unroll 1
+  for (int jt = 0; jt < 8; ++jt)
 #pragma unroll
-  for (int j = 0; j < 32; j += 2) {
-    const int jt = j >> 2, ju = j & 3;  // ju in {0, 2}
+  for (int ju = 0; ju < 4; ju += 2) {
+    const int j = 4 * jt + ju;
     if (fail == 0) {
       if (!(p00 > 0.0)) fail = j + 1;
       else if (!(s11 > 0.0)) fail = j + 2;
@@ -179,7 +185,7 @@ __device__ __forceinline__ int factor32(double* Sd, double* Dd, double* colbuf, 
     }
     // next pivot block first (its rsq chain then overlaps the bulk update)
     const int j1 = j + 2;
-    const int u1 = j1 & 3;
+    const int u1 = (ju + 2) & 3;
     if (j1 < 32) {
       a[u1][u1] = fma(Lr1[u1], Lcm1[u1], fma(Lr0[u1], Lcm0[u1], a[u1][u1]));
       a[u1 + 1][u1] = fma(Lr1[u1 + 1], Lcm1[u1], fma(Lr0[u1 + 1], Lcm0[u1], a[u1 + 1][u1]));
