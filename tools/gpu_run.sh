@@ -23,7 +23,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     bench_short) step bench 600 python bench.py --steps 10 --warmup 2 ;;
-    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fit --no-extra ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fit --no-extra --no-bwd ;;
     prof_fit) step prof_fit 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fit -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmc_fetch) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fit --no-extra --no-bwd ;;
     pmc_write) step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fit --no-extra --no-bwd ;;
