@@ -6,12 +6,12 @@
 // root_inv_decomposition's L^{-T}, botorch/__init__.py:44).  The block is
 // held in LDS (128 rows at pitch 130 doubles = 133 KB of the CU's 160 KB) and
 // factored as four 32-column sub-panels:
-//   F1  wave 0 factors the 32 x 32 diagonal sub-block AND builds its inverse in
-//       one sweep: each lane owns a 4 x 4 tile of L and of X = L^{-1}; a step
-//       factors a 2 x 2 pivot block, broadcasts columns j, j+1 of L and rows
-//       j, j+1 of X through LDS and applies the rank-2 updates of both
-//       (right-looking Cholesky + right-looking forward substitution), so the
-//       sequential chain is 16 short steps;
+//   F1  waves 0 and 1 factor the 32 x 32 diagonal sub-block AND build its
+//       inverse in one sweep: each lane owns a 4 x 4 tile, of L on wave 0 and
+//       of X = L^{-1} on wave 1; a step factors a 2 x 2 pivot block and applies
+//       rank-2 updates (right-looking Cholesky on wave 0, right-looking forward
+//       substitution on wave 1, one step behind, columns and pivots passed
+//       through LDS), 16 steps with one barrier each;
 //   F2  the sub-panel below is solved against that inverse on the fp64 MFMA
 //       (each wave owns whole 16-row strips and updates them in place);
 //   F3  the trailing lower triangle of the block takes the rank-32 update on the
@@ -79,22 +79,27 @@ __device__ __forceinline__ void tri_index(int t, int& tr, int& tc) {
 }
 
 // Factor the 32 x 32 block at Sd (in place, lower; upper zeroed) and write its
-// inverse (lower, upper zeroed) at Dd.  One wave; lane = (ti, tj) owns rows
-// 4 ti.., cols 4 tj.. of both L and X.  Two columns per step (a 2 x 2 pivot
-// block): the sequential chain -- pivot broadcast, 1/sqrt, column broadcast
-// through LDS -- runs 16 times instead of 32, each step applying a rank-2
-// update.  Returns the 1-based failing pivot or 0.
-__device__ __forceinline__ int factor32(double* Sd, double* Dd, double* colbuf, double* rowbuf,
-                                        int lane) {
+// inverse (lower, upper zeroed) at Dd.  Called by all four waves of the
+// workgroup; two of them work.  Lane = (ti, tj) owns rows 4 ti.., cols 4 tj..
+// of its wave's matrix: wave 0 holds L (right-looking Cholesky), wave 1 holds
+// X = L^{-1} (right-looking forward substitution).  A step factors a 2 x 2
+// pivot block and applies a rank-2 update, 16 steps in all.  Wave 0 publishes
+// the step's two L columns and pivot scalars in LDS (double-buffered by step
+// parity); wave 1 applies step s - 1 while wave 0 runs step s, one workgroup
+// barrier per step, so the two halves of the fp64 work (1024 FMAs per lane
+// each) overlap instead of queueing on one wave.  Returns (wave 0) the
+// 1-based failing pivot or 0.
+__device__ __forceinline__ int factor32(double* Sd, double* Dd, double* colbuf, double* pivbuf,
+                                        double* rowbuf, int lane, int wave) {
   const int ti = lane >> 3, tj = lane & 7;
-  double a[4][4], x[4][4];
+  const bool wL = wave == 0, wX = wave == 1;
+  double m[4][4];  // wave 0: a (-> L), wave 1: x (-> X)
 #pragma unroll
   for (int u = 0; u < 4; ++u)
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int i = 4 * ti + u, l = 4 * tj + v;
-      a[u][v] = (l <= i) ? Sd[i * SP + l] : 0.0;
-      x[u][v] = (l == i) ? 1.0 : 0.0;
+      m[u][v] = wL ? ((l <= i) ? Sd[i * SP + l] : 0.0) : ((l == i) ? 1.0 : 0.0);
     }
   int fail = 0;
   // 1/sqrt by v_rsq_f64 + two Newton steps (full fp64 accuracy).
@@ -104,122 +109,154 @@ __device__ __forceinline__ int factor32(double* Sd, double* Dd, double* colbuf, 
     r = r * fma(-0.5 * v * r, r, 1.5);
     return r;
   };
-  // Pivot block of step j (rows/cols j, j+1), from the owner lane (jt, jt):
-  //   L00 = sqrt(p00), L10 = p10 / L00, L11 = sqrt(p11 - L10^2).
-  double p00 = readlane_d(a[0][0], 0), p10 = readlane_d(a[1][0], 0),
-         p11 = readlane_d(a[1][1], 0);
-  double inv0 = rsq_nr(p00);
-  double L10 = p10 * inv0;
-  double s11 = fma(-L10, L10, p11);
-  double inv1 = rsq_nr(s11);
-  // Outer loop over 4-column lane blocks NOT unrolled: the straight-line
-  // 16-step body would be several thousand instructions that stream through
-  // the instruction cache every call; the inner pair of 2-column steps is
-  // unrolled so every register index (ju, u1) stays compile-time.
+  double p00 = 0.0, p10 = 0.0, p11 = 0.0, inv0 = 0.0, L10 = 0.0, s11 = 0.0, inv1 = 0.0;
+  if (wL) {
+    p00 = readlane_d(m[0][0], 0);
+    p10 = readlane_d(m[1][0], 0);
+    p11 = readlane_d(m[1][1], 0);
+    inv0 = rsq_nr(p00);
+    L10 = p10 * inv0;
+    s11 = fma(-L10, L10, p11);
+    inv1 = rsq_nr(s11);
+  }
+
+  // Wave 0, step j: columns j, j+1 -> colbuf[buf], pivot scalars -> pivbuf[buf],
+  // rank-2 Cholesky update (next pivot block first).
+#define BO_L_STEP(JU)                                                                     \
+  {                                                                                       \
+    const int ju = (JU);                                                                  \
+    const int j = 4 * jt + ju;                                                            \
+    const int buf = (j >> 1) & 1;                                                         \
+    double* cb = colbuf + buf * 64;                                                       \
+    if (fail == 0) {                                                                      \
+      if (!(p00 > 0.0)) fail = j + 1;                                                     \
+      else if (!(s11 > 0.0)) fail = j + 2;                                                \
+    }                                                                                     \
+    const double L00 = p00 * inv0, L11 = s11 * inv1;                                      \
+    if (tj == jt) {                                                                       \
+      _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                    \
+        const int i = 4 * ti + u;                                                         \
+        const double c0 = (i > j) ? m[u][ju] * inv0 : ((i == j) ? L00 : 0.0);            \
+        const double c1 =                                                                 \
+            (i > j + 1) ? fma(-c0, L10, m[u][ju + 1]) * inv1 : ((i == j + 1) ? L11 : 0.0); \
+        m[u][ju] = c0;                                                                    \
+        m[u][ju + 1] = c1;                                                                \
+        cb[i] = c0;                                                                       \
+        cb[32 + i] = c1;                                                                  \
+      }                                                                                   \
+    }                                                                                     \
+    if (lane == 0) {                                                                      \
+      pivbuf[buf * 4 + 0] = inv0;                                                         \
+      pivbuf[buf * 4 + 1] = L10;                                                          \
+      pivbuf[buf * 4 + 2] = inv1;                                                         \
+    }                                                                                     \
+    asm volatile("" ::: "memory");                                                        \
+    double Lr0[4], Lr1[4], Lcm0[4], Lcm1[4];                                              \
+    _Pragma("unroll") for (int h = 0; h < 2; ++h) {                                      \
+      const double2 r0 = *reinterpret_cast<const double2*>(cb + 4 * ti + 2 * h);          \
+      const double2 r1 = *reinterpret_cast<const double2*>(cb + 32 + 4 * ti + 2 * h);     \
+      const double2 q0 = *reinterpret_cast<const double2*>(cb + 4 * tj + 2 * h);          \
+      const double2 q1 = *reinterpret_cast<const double2*>(cb + 32 + 4 * tj + 2 * h);     \
+      Lr0[2 * h] = r0.x; Lr0[2 * h + 1] = r0.y;                                           \
+      Lr1[2 * h] = r1.x; Lr1[2 * h + 1] = r1.y;                                           \
+      Lcm0[2 * h] = q0.x; Lcm0[2 * h + 1] = q0.y;                                         \
+      Lcm1[2 * h] = q1.x; Lcm1[2 * h + 1] = q1.y;                                         \
+    }                                                                                     \
+    asm volatile("" ::: "memory");                                                        \
+    _Pragma("unroll") for (int v = 0; v < 4; ++v) {                                      \
+      const bool cl = 4 * tj + v > j + 1;                                                 \
+      Lcm0[v] = cl ? -Lcm0[v] : 0.0;                                                      \
+      Lcm1[v] = cl ? -Lcm1[v] : 0.0;                                                      \
+    }                                                                                     \
+    const int j1 = j + 2;                                                                 \
+    const int u1 = (ju + 2) & 3;                                                          \
+    if (j1 < 32) {                                                                        \
+      m[u1][u1] = fma(Lr1[u1], Lcm1[u1], fma(Lr0[u1], Lcm0[u1], m[u1][u1]));              \
+      m[u1 + 1][u1] = fma(Lr1[u1 + 1], Lcm1[u1], fma(Lr0[u1 + 1], Lcm0[u1], m[u1 + 1][u1])); \
+      m[u1 + 1][u1 + 1] =                                                                 \
+          fma(Lr1[u1 + 1], Lcm1[u1 + 1], fma(Lr0[u1 + 1], Lcm0[u1 + 1], m[u1 + 1][u1 + 1])); \
+      const int src = (j1 >> 2) * 9;                                                      \
+      p00 = readlane_d(m[u1][u1], src);                                                   \
+      p10 = readlane_d(m[u1 + 1][u1], src);                                               \
+      p11 = readlane_d(m[u1 + 1][u1 + 1], src);                                           \
+      inv0 = rsq_nr(p00);                                                                 \
+      L10 = p10 * inv0;                                                                   \
+      s11 = fma(-L10, L10, p11);                                                          \
+      inv1 = rsq_nr(s11);                                                                 \
+    }                                                                                     \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u)                                        \
+      _Pragma("unroll") for (int v = 0; v < 4; ++v) {                                    \
+        const bool early = j1 < 32 && ((u == u1 && v == u1) || (u == u1 + 1 && v == u1) || \
+                                       (u == u1 + 1 && v == u1 + 1));                     \
+        if (!early) m[u][v] = fma(Lr1[u], Lcm1[v], fma(Lr0[u], Lcm0[v], m[u][v]));        \
+      }                                                                                   \
+  }
+  // Wave 1, step j (published by wave 0 one barrier earlier): rows j, j+1 of X
+  // scaled by the pivot block, then the rank-2 substitution update.
+#define BO_X_STEP(JT, JU)                                                                 \
+  {                                                                                       \
+    const int jtx = (JT), ju = (JU);                                                      \
+    const int j = 4 * jtx + ju;                                                           \
+    const int buf = (j >> 1) & 1;                                                         \
+    const double* cb = colbuf + buf * 64;                                                 \
+    const double xi0 = pivbuf[buf * 4 + 0], xl10 = pivbuf[buf * 4 + 1],                   \
+                 xi1 = pivbuf[buf * 4 + 2];                                               \
+    if (ti == jtx) {                                                                      \
+      _Pragma("unroll") for (int v = 0; v < 4; ++v) {                                    \
+        const double xj = m[ju][v] * xi0;                                                 \
+        const double xj1 = fma(-xl10, xj, m[ju + 1][v]) * xi1;                            \
+        m[ju][v] = xj;                                                                    \
+        m[ju + 1][v] = xj1;                                                               \
+        rowbuf[4 * tj + v] = xj;                                                          \
+        rowbuf[32 + 4 * tj + v] = xj1;                                                    \
+      }                                                                                   \
+    }                                                                                     \
+    asm volatile("" ::: "memory");                                                        \
+    double Lrm0[4], Lrm1[4], X0[4], X1[4];                                                \
+    _Pragma("unroll") for (int h = 0; h < 2; ++h) {                                      \
+      const double2 r0 = *reinterpret_cast<const double2*>(cb + 4 * ti + 2 * h);          \
+      const double2 r1 = *reinterpret_cast<const double2*>(cb + 32 + 4 * ti + 2 * h);     \
+      const double2 y0 = *reinterpret_cast<const double2*>(rowbuf + 4 * tj + 2 * h);      \
+      const double2 y1 = *reinterpret_cast<const double2*>(rowbuf + 32 + 4 * tj + 2 * h); \
+      Lrm0[2 * h] = r0.x; Lrm0[2 * h + 1] = r0.y;                                         \
+      Lrm1[2 * h] = r1.x; Lrm1[2 * h + 1] = r1.y;                                         \
+      X0[2 * h] = y0.x; X0[2 * h + 1] = y0.y;                                             \
+      X1[2 * h] = y1.x; X1[2 * h + 1] = y1.y;                                             \
+    }                                                                                     \
+    asm volatile("" ::: "memory");                                                        \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                      \
+      const bool rw = 4 * ti + u > j + 1;                                                 \
+      Lrm0[u] = rw ? -Lrm0[u] : 0.0;                                                      \
+      Lrm1[u] = rw ? -Lrm1[u] : 0.0;                                                      \
+    }                                                                                     \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u)                                        \
+      _Pragma("unroll") for (int v = 0; v < 4; ++v)                                      \
+        m[u][v] = fma(Lrm1[u], X1[v], fma(Lrm0[u], X0[v], m[u][v]));                      \
+  }
+
+  // Iteration (jt, ju): wave 0 runs step 4 jt + ju, wave 1 the step before it.
+  // The outer loop is not unrolled (instruction-cache footprint); the inner
+  // pair is, so register indices stay compile-time.
 #pragma unroll 1
-  for (int jt = 0; jt < 8; ++jt)
+  for (int jt = 0; jt < 8; ++jt) {
+    if (wL) BO_L_STEP(0)
+    if (wX && jt > 0) BO_X_STEP(jt - 1, 2)
+    __syncthreads();
+    if (wL) BO_L_STEP(2)
+    if (wX) BO_X_STEP(jt, 0)
+    __syncthreads();
+  }
+  if (wX) BO_X_STEP(7, 2)
+#undef BO_L_STEP
+#undef BO_X_STEP
 #pragma unroll
-  for (int ju = 0; ju < 4; ju += 2) {
-    const int j = 4 * jt + ju;
-    if (fail == 0) {
-      if (!(p00 > 0.0)) fail = j + 1;
-      else if (!(s11 > 0.0)) fail = j + 2;
-    }
-    const double L00 = p00 * inv0, L11 = s11 * inv1;
-    // columns j, j+1 of L (owners: tj == jt) -> colbuf[0..31], colbuf[32..63]
-    if (tj == jt) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = 4 * ti + u;
-        const double c0 = (i > j) ? a[u][ju] * inv0 : ((i == j) ? L00 : 0.0);
-        const double c1 = (i > j + 1) ? fma(-c0, L10, a[u][ju + 1]) * inv1 : ((i == j + 1) ? L11 : 0.0);
-        a[u][ju] = c0;
-        a[u][ju + 1] = c1;
-        colbuf[i] = c0;
-        colbuf[32 + i] = c1;
-      }
-    }
-    // rows j, j+1 of X (owners: ti == jt): forward substitution by the pivot block
-    if (ti == jt) {
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const double xj = x[ju][v] * inv0;
-        const double xj1 = fma(-L10, xj, x[ju + 1][v]) * inv1;
-        x[ju][v] = xj;
-        x[ju + 1][v] = xj1;
-        rowbuf[4 * tj + v] = xj;
-        rowbuf[32 + 4 * tj + v] = xj1;
-      }
-    }
-    // One wave: its LDS operations execute in program order (see the
-    // compiler-only fences), so the other lanes' stores above are visible.
-    asm volatile("" ::: "memory");
-    double Lr0[4], Lr1[4], Lc0[4], Lc1[4], X0[4], X1[4];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const double2 r0 = *reinterpret_cast<const double2*>(colbuf + 4 * ti + 2 * h);
-      const double2 r1 = *reinterpret_cast<const double2*>(colbuf + 32 + 4 * ti + 2 * h);
-      const double2 q0 = *reinterpret_cast<const double2*>(colbuf + 4 * tj + 2 * h);
-      const double2 q1 = *reinterpret_cast<const double2*>(colbuf + 32 + 4 * tj + 2 * h);
-      const double2 y0 = *reinterpret_cast<const double2*>(rowbuf + 4 * tj + 2 * h);
-      const double2 y1 = *reinterpret_cast<const double2*>(rowbuf + 32 + 4 * tj + 2 * h);
-      Lr0[2 * h] = r0.x; Lr0[2 * h + 1] = r0.y;
-      Lr1[2 * h] = r1.x; Lr1[2 * h + 1] = r1.y;
-      Lc0[2 * h] = q0.x; Lc0[2 * h + 1] = q0.y;
-      Lc1[2 * h] = q1.x; Lc1[2 * h + 1] = q1.y;
-      X0[2 * h] = y0.x; X0[2 * h + 1] = y0.y;
-      X1[2 * h] = y1.x; X1[2 * h + 1] = y1.y;
-    }
-    asm volatile("" ::: "memory");
-    // Masks folded into the broadcast operands: the Cholesky update touches
-    // columns l > j+1 only, the substitution rows i > j+1 only.
-    double Lcm0[4], Lcm1[4], Lrm0[4], Lrm1[4];
+  for (int u = 0; u < 4; ++u)
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const bool cl = 4 * tj + v > j + 1;
-      Lcm0[v] = cl ? -Lc0[v] : 0.0;
-      Lcm1[v] = cl ? -Lc1[v] : 0.0;
-      const bool rw = 4 * ti + v > j + 1;
-      Lrm0[v] = rw ? -Lr0[v] : 0.0;
-      Lrm1[v] = rw ? -Lr1[v] : 0.0;
+      const int i = 4 * ti + u, l = 4 * tj + v;
+      if (wL) Sd[i * SP + l] = (l <= i) ? m[u][v] : 0.0;
+      if (wX) Dd[i * SP + l] = (l <= i) ? m[u][v] : 0.0;
     }
-    // next pivot block first (its rsq chain then overlaps the bulk update)
-    const int j1 = j + 2;
-    const int u1 = (ju + 2) & 3;
-    if (j1 < 32) {
-      a[u1][u1] = fma(Lr1[u1], Lcm1[u1], fma(Lr0[u1], Lcm0[u1], a[u1][u1]));
-      a[u1 + 1][u1] = fma(Lr1[u1 + 1], Lcm1[u1], fma(Lr0[u1 + 1], Lcm0[u1], a[u1 + 1][u1]));
-      a[u1 + 1][u1 + 1] =
-          fma(Lr1[u1 + 1], Lcm1[u1 + 1], fma(Lr0[u1 + 1], Lcm0[u1 + 1], a[u1 + 1][u1 + 1]));
-      const int src = (j1 >> 2) * 9;
-      p00 = readlane_d(a[u1][u1], src);
-      p10 = readlane_d(a[u1 + 1][u1], src);
-      p11 = readlane_d(a[u1 + 1][u1 + 1], src);
-      inv0 = rsq_nr(p00);
-      L10 = p10 * inv0;
-      s11 = fma(-L10, L10, p11);
-      inv1 = rsq_nr(s11);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const bool early = j1 < 32 && ((u == u1 && v == u1) || (u == u1 + 1 && v == u1) ||
-                                       (u == u1 + 1 && v == u1 + 1));
-        if (!early) a[u][v] = fma(Lr1[u], Lcm1[v], fma(Lr0[u], Lcm0[v], a[u][v]));
-        x[u][v] = fma(Lrm1[u], X1[v], fma(Lrm0[u], X0[v], x[u][v]));
-      }
-  }
-  if (lane < 64) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int i = 4 * ti + u, l = 4 * tj + v;
-        Sd[i * SP + l] = (l <= i) ? a[u][v] : 0.0;
-        Dd[i * SP + l] = (l <= i) ? x[u][v] : 0.0;
-      }
-  }
   return fail;
 }
 
@@ -233,7 +270,8 @@ __global__ __launch_bounds__(256) void potrf_block_kernel(double* __restrict__ A
                                                           int64_t ldi, int* __restrict__ info,
                                                           long long* __restrict__ tsc) {
   __shared__ __attribute__((aligned(16))) double S[DB * SP];
-  __shared__ __attribute__((aligned(16))) double colbuf[64];
+  __shared__ __attribute__((aligned(16))) double colbuf[2 * 64];
+  __shared__ __attribute__((aligned(16))) double pivbuf[8];
   __shared__ __attribute__((aligned(16))) double rowbuf[64];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -269,9 +307,9 @@ __global__ __launch_bounds__(256) void potrf_block_kernel(double* __restrict__ A
   for (int s = 0; s < 4; ++s) {
     const int c = 32 * s;
     // ---- F1: factor + invert the 32 x 32 diagonal sub-block (wave 0) ----
-    if (wave == 0) {
-      const int fail = factor32(S + c * SP + c, S + dinv_at(s), colbuf, rowbuf, lane);
-      if (fail && lane == 0) atomicCAS(info, 0, (int)(k0 + c + fail));
+    {
+      const int fail = factor32(S + c * SP + c, S + dinv_at(s), colbuf, pivbuf, rowbuf, lane, wave);
+      if (wave == 0 && fail && lane == 0) atomicCAS(info, 0, (int)(k0 + c + fail));
     }
     __syncthreads();
     BO_TSC(2 + 3 * s);
