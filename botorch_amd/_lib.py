@@ -45,6 +45,7 @@ _SIGNATURES = {
                                    _P, _P]),
     "bo_chol_small": (c_int, [_P, c_int64, c_int, c_int, c_double, _P, _P, _P, _P]),
     "bo_ladder_status": (c_int, [_P, _P, c_int64, _P, _P]),
+    "bo_pareto_mask": (c_int, [_P, c_int64, c_int, c_int, c_int, c_int, _P, _P]),
     "bo_covar_blocks": (c_int, [c_int, _P, c_int64, c_int, c_int, _P, c_double, c_double, _P,
                                 _P]),
     "bo_gemv": (c_int, [_P, c_int64, c_int64, _P, c_double, _P, _P]),

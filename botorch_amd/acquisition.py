@@ -770,8 +770,10 @@ def prune_inferior_points_multi_objective(model, X, ref_point, objective=None, c
         if objective is not None:
             obj = objective(obj, X=X)
         hits = torch.zeros(n, dtype=torch.float64, device=X.device)
-        for s0 in range(0, obj.shape[0], chunk):
-            o = obj[s0:s0 + chunk]
+        # one device launch for all samples (bo_pareto_mask); host tensors chunked
+        step = obj.shape[0] if obj.is_cuda else chunk
+        for s0 in range(0, obj.shape[0], step):
+            o = obj[s0:s0 + step]
             mask = is_non_dominated(o, deduplicate=False) & (o > ref).all(dim=-1)
             hits += mask.to(torch.float64).sum(dim=0)
     probs = hits / obj.shape[0]

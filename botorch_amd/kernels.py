@@ -638,3 +638,17 @@ def mc_reduce(samples: torch.Tensor, best_f: float = 0.0,
     check(lib().bo_mc_reduce(S, B, q, _p(samples.contiguous()), float(best_f), _p(best_f_s),
                              _p(acq), _stream(dev)), "mc_reduce")
     return acq
+
+
+def pareto_mask(Y: torch.Tensor, maximize: bool = True, deduplicate: bool = True) -> torch.Tensor:
+    """Non-dominated mask of (..., n, m) point sets on the device (bool, ... x n)."""
+    dev = _dev(Y)
+    n, m = Y.shape[-2], Y.shape[-1]
+    Y3 = Y.reshape(-1, n, m).contiguous()
+    S = Y3.shape[0]
+    out = torch.empty(S, n, dtype=torch.uint8, device=dev)
+    for s0 in range(0, S, 65535):
+        s1 = min(S, s0 + 65535)
+        check(lib().bo_pareto_mask(_p(Y3[s0:s1]), s1 - s0, n, m, int(maximize), int(deduplicate),
+                                   _p(out[s0:s1]), _stream(dev)), "pareto_mask")
+    return out.bool().reshape(Y.shape[:-1])

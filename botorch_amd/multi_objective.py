@@ -15,10 +15,15 @@ import torch
 
 
 def is_non_dominated(Y: torch.Tensor, maximize: bool = True, deduplicate: bool = True) -> torch.Tensor:
-    """pareto.py:16-64 (pairwise form; n x m, no batch)."""
+    """pareto.py:16-64: device fp64 inputs run bo_pareto_mask (any batch
+    shape, m <= 8, one launch); host inputs the pairwise torch form (the loop
+    form beyond n = 2000, as the reference)."""
     n = Y.shape[-2]
     if n == 0:
         return torch.zeros(Y.shape[:-1], dtype=torch.bool, device=Y.device)
+    if Y.is_cuda and Y.dtype == torch.float64 and Y.shape[-1] <= 8:
+        from . import kernels
+        return kernels.pareto_mask(Y, maximize, deduplicate)
     if n > 2000:
         return _is_non_dominated_loop(Y, maximize, deduplicate)
     Y1 = Y.unsqueeze(-3)

@@ -128,6 +128,14 @@ int bo_cholesky_jitter(const double* A, int64_t n, double* L, double* Linv, doub
  * [G] psd_safe_cholesky's torch.any(info) check does. */
 int bo_ladder_status(const int* info, const double* jitter, int64_t B, double* out, void* stream);
 
+/* Pareto masks of S point sets (Y: S x n x m, m <= 8; out: S x n bytes, 1 =
+ * non-dominated): no other point is >= in every objective and > in one
+ * (maximize; <= / < otherwise); dedup also drops later copies of equal points.
+ * botorch/utils/multi_objective/pareto.py:16-64 over the S joint samples of
+ * prune_inferior_points_multi_objective (acquisition/multi_objective/utils.py:77-161). */
+int bo_pareto_mask(const double* Y, int64_t S, int n, int m, int maximize, int dedup,
+                   unsigned char* out, void* stream);
+
 /* Batched small psd_safe_cholesky (q <= 64), ladder applied per member
  * ([G] MultivariateNormal root_decomposition, posteriors/gpytorch.py:121-123).
  * A, L: B x q x q; info (B, nullable), jitter (B, nullable). */
