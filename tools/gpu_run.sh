@@ -24,7 +24,7 @@ for s in "$@"; do
     bench) step bench 600 python bench.py ;;
     bench_short) step bench 600 python bench.py --steps 10 --warmup 2 ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fit --no-extra --no-bwd ;;
-    prof_fit) step prof_fit 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fit -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    prof_fit) step prof_fit 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fit -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extra --no-bwd ;;
     pmc_fetch) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fit --no-extra --no-bwd ;;
     pmc_write) step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fit --no-extra --no-bwd ;;
     pmc_mfma) step pmc_mfma 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_mfma -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fit --no-extra --no-bwd ;;
