@@ -160,10 +160,6 @@ struct SideStream {
   hipStream_t stream = nullptr;
   hipEvent_t solved = nullptr;     // panel solve of step k done (caller's stream)
   hipEvent_t bulk_done = nullptr;  // BULK_k done (side stream)
-  hipStream_t inv = nullptr;       // row blocks of L^{-1} (third stream)
-  hipEvent_t diag_done = nullptr;  // diagonal block k factored + inverted (caller's stream)
-  hipEvent_t copied = nullptr;     // panel k copied back into A (side stream)
-  hipEvent_t inv_done = nullptr;   // last row block of L^{-1} written (third stream)
 };
 
 static SideStream* side_stream() {
@@ -180,11 +176,6 @@ static SideStream* side_stream() {
       return nullptr;
     if (hipEventCreateWithFlags(&s.solved, hipEventDisableTiming) != hipSuccess) return nullptr;
     if (hipEventCreateWithFlags(&s.bulk_done, hipEventDisableTiming) != hipSuccess) return nullptr;
-    if (hipStreamCreateWithPriority(&s.inv, hipStreamNonBlocking, least) != hipSuccess)
-      return nullptr;
-    if (hipEventCreateWithFlags(&s.diag_done, hipEventDisableTiming) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&s.copied, hipEventDisableTiming) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&s.inv_done, hipEventDisableTiming) != hipSuccess) return nullptr;
   }
   return &s;
 }
@@ -284,32 +275,9 @@ int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* 
   // (BULK_k's input is only overwritten by the solve of step k+2, after LA_{k+1}).
   double* Wbuf[2] = {work, work + np * NBO};
   bool bulk_pending = false;
-  // Row blocks of L^{-1} ride along on a third low-priority stream, one step
-  // behind the diagonal factorisation:
-  //   X[k, 0:k] = -X_kk (L[k, 0:k] X[0:k, 0:k])
-  // needs row block k of L (final once panel k-1 is copied back into A) and
-  // X_kk (from the diagonal kernel of step k); the earlier rows of X are
-  // already written by this stream.  What is left after the last diagonal
-  // block is one row block, not a log2(np/128)-level recursive doubling.
-  // 128 x np scratch of the third stream: past both W halves, or (np = 256,
-  // one panel only) in the unused second half.
-  double* Tbuf = np >= 3 * NBO ? work + 2 * np * NBO : work + np * NBO;
   for (int64_t K0 = 0, k = 0; K0 < np; K0 += NBO, ++k) {
     int s = bo_potrf_block128(A, np, K0, Linv, np, info, st);
     if (s) return s;
-    if (K0 > 0) {
-      BO_HIP(hipEventRecord(side->diag_done, st));
-      BO_HIP(hipStreamWaitEvent(side->inv, side->diag_done, 0));
-      BO_HIP(hipStreamWaitEvent(side->inv, side->copied, 0));  // panel k-1 back in A
-      // T = L[k, 0:K0] X[0:K0, 0:K0]   (X lower)
-      s = bo_gemm_f64_impl(0, 0, NBO, (int)K0, (int)K0, 1.0, A + K0 * np, np, 0, Linv, np, 0, 0.0,
-                           Tbuf, np, 0, 1, BO_GEMM_B_LOWER, side->inv);
-      if (s) return s;
-      // X[k, 0:K0] = -X_kk T   (X_kk lower)
-      s = bo_gemm_f64_impl(0, 0, NBO, (int)K0, NBO, -1.0, Linv + K0 * np + K0, np, 0, Tbuf, np, 0,
-                           0.0, Linv + K0 * np, np, 0, 1, BO_GEMM_A_LOWER, side->inv);
-      if (s) return s;
-    }
     const int64_t rem = np - K0 - NBO;
     if (rem <= 0) break;
     double* W = Wbuf[k & 1];
@@ -326,7 +294,6 @@ int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* 
     // cols >= K0 + 256, lower triangle, from rows NBO.. of W.
     BO_HIP(hipMemcpy2DAsync(P, sizeof(double) * np, W, sizeof(double) * NBO,
                             sizeof(double) * NBO, rem, hipMemcpyDeviceToDevice, side->stream));
-    BO_HIP(hipEventRecord(side->copied, side->stream));
     if (rem > NBO) {
       s = bo_gemm_f64_impl(0, 1, (int)(rem - NBO), (int)(rem - NBO), NBO, -1.0, W + NBO * NBO,
                            NBO, 0, W + NBO * NBO, NBO, 0, 1.0, A22 + NBO * np + NBO, np, 0, 1,
@@ -342,9 +309,33 @@ int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* 
     bulk_pending = true;
   }
   if (bulk_pending) BO_HIP(hipStreamWaitEvent(st, side->bulk_done, 0));
-  if (np > NBO) {
-    BO_HIP(hipEventRecord(side->inv_done, side->inv));
-    BO_HIP(hipStreamWaitEvent(st, side->inv_done, 0));
+  // Triangular inverse by recursive doubling over the inverted diagonal
+  // blocks:  [L11 0; L21 L22]^{-1} = [X11 0; -X22 L21 X11  X22].
+  for (int64_t sz = NBO; sz < np; sz *= 2) {
+    const int64_t stride = 2 * sz;
+    const int64_t full = np / stride;          // pairs with a full-size second block
+    const int64_t tail_r2 = full * stride + sz;  // second block start of a ragged pair
+    for (int pass = 0; pass < 2; ++pass) {
+      int64_t npairs, r1, t;
+      if (pass == 0) { npairs = full; r1 = 0; t = sz; }
+      else {
+        if (tail_r2 >= np) break;
+        npairs = 1; r1 = full * stride; t = np - tail_r2;
+      }
+      if (npairs == 0) continue;
+      const int64_t r2 = r1 + sz;
+      const int64_t sBlk = stride * (np + 1);  // diagonal step between pairs
+      // T = L21 * X11     (t x sz)
+      int s = bo_gemm_f64_impl(0, 0, (int)t, (int)sz, (int)sz, 1.0, A + r2 * np + r1, np, sBlk,
+                               Linv + r1 * np + r1, np, sBlk, 0.0, work, sz, t * sz, (int)npairs,
+                               BO_GEMM_B_LOWER, st);
+      if (s) return s;
+      // X21 = -X22 * T     (t x sz)
+      s = bo_gemm_f64_impl(0, 0, (int)t, (int)sz, (int)t, -1.0, Linv + r2 * np + r2, np, sBlk,
+                           work, sz, t * sz, 0.0, Linv + r2 * np + r1, np, sBlk, (int)npairs,
+                           BO_GEMM_A_LOWER, st);
+      if (s) return s;
+    }
   }
   return BO_OK;
 }
