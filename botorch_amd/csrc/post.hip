@@ -448,6 +448,7 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
   int s = bo_post_geometry(B, q, 1, &Qp, &nrows_pad, &nC);
   if (s) return s;
   const int64_t tot = (int64_t)nrows_pad * DP;
+  if (tot == 0) return BO_OK;  // no t-batches
   prepare_rows_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, as_stream(stream)>>>(
       X, B, q, d, Qp, lengthscale, nrows_pad, Xq);
   BO_LAUNCH_CHECK();
@@ -471,6 +472,7 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
   if (s) return s;
   const int nI = nrows_pad / PI;
   const int nrows = B * Qp;
+  if (nI == 0) return BO_OK;  // no t-batches: nothing to launch
   BO_CHECK_ARG(d >= 1 && d <= DP, "fused posterior kernel supports 1 <= d <= %d", DP);
   const int64_t blocks = kc_len > 0 ? (int64_t)nC * ceil_div(n, kc_len) * nI
                                     : 8 * ceil_div(nC, 8) * (int64_t)nI;

@@ -349,3 +349,24 @@ def test_saas_qei_gradient_matches_oracle(d, M, q):
     torch.testing.assert_close(v.detach().cpu(), ref.detach(), rtol=1e-6, atol=1e-9)
     assert go.abs().max() > 0
     torch.testing.assert_close(gd.cpu(), go, rtol=1e-5, atol=1e-8)
+
+
+def test_qei_edge_shapes():
+    """Empty t-batch, extra batch dimensions, a ragged n (not a multiple of 128)."""
+    from botorch_amd.acquisition import qExpectedImprovement
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import qei
+    from oracle.sampling import draw_sobol_normal_samples
+    X, Y, m, orc = _setup(n=300)
+    best_f = Y.max().item()
+    acqf = qExpectedImprovement(m, best_f, sampler=SobolQMCNormalSampler(torch.Size([64]), seed=3))
+    with torch.no_grad():
+        v0 = acqf(torch.empty(0, 4, 6, dtype=torch.float64, device=DEV))
+        assert v0.shape == (0,)
+        Xc = torch.rand(2, 3, 4, 6, dtype=torch.float64)
+        v = acqf(Xc.to(DEV)).cpu()
+    assert v.shape == (2, 3)
+    ref = qei(orc, Xc.reshape(6, 4, 6), draw_sobol_normal_samples(4, 64, 3), best_f).reshape(2, 3)
+    torch.testing.assert_close(v, ref, rtol=1e-6, atol=1e-10)
+    post = m.posterior(torch.empty(0, 4, 6, dtype=torch.float64, device=DEV))
+    assert post.mean.shape == (0, 4, 1)
