@@ -417,6 +417,7 @@ int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len,
   if (slots <= 0) slots = kSlots;
   *kc_len = 0;
   *work_elems = 0;
+  if (nI == 0) return BO_OK;  // no t-batches
   // Cost model in k-step units (measured on MI355X, tools/tune_split.py):
   //  one pass: the heaviest-first schedule ends at max(total steps / slots,
   //            longest column tile) plus a per-workgroup overhead per round;
@@ -465,6 +466,7 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
   BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
   BO_CHECK_ARG(ldu % 2 == 0 && ldu >= ceil_div(n, PC) * PC, "U leading dim %lld too small",
                (long long)ldu);
+  if (B == 0) return BO_OK;  // no t-batches: nothing to launch
   BO_CHECK_ARG(kc_len == 0 || (kc_len > 0 && kc_len % PK == 0 && work != nullptr),
                "split-k chunk %d must be a positive multiple of %d with a workspace", kc_len, PK);
   int Qp, nrows_pad, nC;
