@@ -274,6 +274,7 @@ extern "C" int bo_qmc_finalize(int kind, int mode, int B, int q, const double* X
                                const double* F, int64_t ldF, int fat, double tau_relu,
                                double tau_max, void* stream) {
   BO_CHECK_ARG(mode >= 0 && mode <= 5, "bo_qmc_finalize: bad mode %d", mode);
+  if (B == 0) return BO_OK;  // no t-batches (empty outputs may carry null pointers)
   BO_CHECK_ARG(!log_mode(mode) || (tau_relu > 0.0 && tau_max > 0.0),
                "bo_qmc_finalize: tau_relu and tau_max must be positive");
   BO_CHECK_ARG(mode == QMC_POSTERIOR || mode == QMC_CHOL || (acq && Z && S > 0),

@@ -404,6 +404,8 @@ def post_backward(cache: GPCache, pp: PostPartials, W: Optional[torch.Tensor],
 def _raise_not_psd(info: torch.Tensor, jitter: torch.Tensor, what: str):
     """Host check of a batched ladder (one D2H read, as [G] psd_safe_cholesky's
     torch.any(info)); warns like [G] when jitter was added."""
+    if info.numel() == 0:
+        return
     packed = torch.empty(2, dtype=torch.float64, device=info.device)
     check(lib().bo_ladder_status(_p(info.contiguous()), _p(jitter.contiguous()), info.numel(),
                                  _p(packed), _stream(info.device)), "ladder_status")
