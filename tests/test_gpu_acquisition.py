@@ -370,3 +370,28 @@ def test_qei_edge_shapes():
     torch.testing.assert_close(v, ref, rtol=1e-6, atol=1e-10)
     post = m.posterior(torch.empty(0, 4, 6, dtype=torch.float64, device=DEV))
     assert post.mean.shape == (0, 4, 1)
+
+
+def test_empty_batches_all_acquisitions(golden):
+    """A zero-size t-batch returns an empty value for every fused acquisition."""
+    from botorch_amd.acquisition import (qExpectedHypervolumeImprovement, qLogExpectedImprovement,
+                                         qLogNoisyExpectedImprovement, qNoisyExpectedImprovement)
+    from botorch_amd.models import ModelListGP, SingleTaskGP
+    from botorch_amd.multi_objective import FastNondominatedPartitioning
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    X, Y, m, orc = _setup(n=200, noise=1e-2)
+    empty = torch.empty(0, 3, 6, dtype=torch.float64, device=DEV)
+    acqfs = [qLogExpectedImprovement(m, Y.max().item()),
+             qNoisyExpectedImprovement(m, X[:20].to(DEV), prune_baseline=False),
+             qLogNoisyExpectedImprovement(m, X[:20].to(DEV))]
+    Xm = torch.from_numpy(golden["dtlz2_X"][:64])
+    Ym = torch.from_numpy(golden["dtlz2_Y"][:64])
+    models = [SingleTaskGP(Xm.to(DEV), Ym[:, t:t + 1].to(DEV)).eval() for t in range(3)]
+    ref_point = torch.full((3,), -1.1, dtype=torch.float64)
+    acqfs.append(qExpectedHypervolumeImprovement(
+        ModelListGP(*models), ref_point.tolist(), FastNondominatedPartitioning(ref_point, Ym),
+        sampler=SobolQMCNormalSampler(torch.Size([32]), seed=0)))
+    with torch.no_grad():
+        for a in acqfs:
+            v = a(empty)
+            assert v.shape == (0,), type(a).__name__
