@@ -125,7 +125,7 @@ __device__ __forceinline__ void post_epilogue(const v4d (&acc)[8], int ci, int r
   if (lane < 16) mpart[(int64_t)ci * nrows_pad + row0 + lane] = m;
 }
 
-template <int KIND, int ND, bool SPLIT, bool CROSS>
+template <int KIND, int ND, bool SPLIT, bool CROSS, bool PRE = false>
 __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     const double* __restrict__ Xq, int nrows, const double* __restrict__ Xt, int n,
     const double* __restrict__ U, int64_t ldu, const double* __restrict__ beta,
@@ -234,10 +234,15 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     _Pragma("unroll") for (int kk = 0; kk < 8; ++kk) Ks[BUF][kh * 8 + kk][ti] = kv[kk]; \
   }
 
+  // K*x value (row ti, training point k): evaluated in registers, or (PRE,
+  // timing experiment) read from a precomputed K*x^T (np x nrows_pad).
+#define BO_KVAL(K)                                                                         \
+  (PRE ? work[(int64_t)(K) * (nI * PI) + i0 + ti]                                          \
+       : eval_kernel_row<KIND, ND>(xi, Xt, n, (K), outputscale, ivalid))
   BO_LOAD_U(kbeg);
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk)
-    kv[kk] = eval_kernel_row<KIND, ND>(xi, Xt, n, kbeg + kh * 8 + kk, outputscale, ivalid);
+    kv[kk] = BO_KVAL(kbeg + kh * 8 + kk);
   BO_STORE(0);
   __syncthreads();
   // One k-step; XMFMA = the cross-term MFMAs (cross workgroups only: a
@@ -260,9 +265,8 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
         _Pragma("unroll") for (int it = 0; it < 2; ++it)                            \
           acc[ct][it] = mfma_f64(a[ct], b[it], acc[ct][it]);                         \
       XMFMA                                                                          \
-      kv[2 * ks] = eval_kernel_row<KIND, ND>(xi, Xt, n, knext + kh * 8 + 2 * ks, outputscale, ivalid); \
-      kv[2 * ks + 1] =                                                               \
-          eval_kernel_row<KIND, ND>(xi, Xt, n, knext + kh * 8 + 2 * ks + 1, outputscale, ivalid); \
+      kv[2 * ks] = BO_KVAL(knext + kh * 8 + 2 * ks);                                \
+      kv[2 * ks + 1] = BO_KVAL(knext + kh * 8 + 2 * ks + 1);                        \
     }                                                                                \
     if (more) BO_STORE(cur ^ 1);                                                     \
     __syncthreads();                                                                 \
@@ -279,6 +283,7 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     for (; t < nsteps; ++t) BO_KSTEP(, )
   }
 #undef BO_KSTEP
+#undef BO_KVAL
 #undef BO_LOAD_U
 #undef BO_STORE
 #undef BO_LOAD_Q
@@ -348,6 +353,27 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
       m += __shfl_xor(m, 32);
       if (lane < 16) mpart[(int64_t)ci * nrows_pad + row0 + lane] = m;
     }
+  }
+}
+
+// K*x^T for the PRE timing experiment: Kt[k][i] = outputscale k(x_i, x_k),
+// zero for k >= n or invalid rows; np x nrows_pad.
+template <int KIND, int ND>
+__global__ __launch_bounds__(256) void kxt_build_kernel(const double* __restrict__ Xq, int nrows,
+                                                        const double* __restrict__ Xt, int n,
+                                                        int np, int nrows_pad, double outputscale,
+                                                        double* __restrict__ Kt) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int k0 = blockIdx.y * 16;
+  const bool iv = i < nrows;
+  double xi[ND];
+#pragma unroll
+  for (int t = 0; t < ND; ++t) xi[t] = iv ? Xq[(int64_t)i * DP + t] : 0.0;
+  if (i >= nrows_pad) return;
+#pragma unroll 4
+  for (int kk = 0; kk < 16; ++kk) {
+    const int k = k0 + kk;
+    if (k < np) Kt[(int64_t)k * nrows_pad + i] = eval_kernel_row<KIND, ND>(xi, Xt, n, k, outputscale, iv);
   }
 }
 
@@ -467,6 +493,9 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
   BO_CHECK_ARG(ldu % 2 == 0 && ldu >= ceil_div(n, PC) * PC, "U leading dim %lld too small",
                (long long)ldu);
   if (B == 0) return BO_OK;  // no t-batches: nothing to launch
+  const bool pre = kc_len < 0;  // timing experiment: precomputed K*x^T in `work`
+  if (pre) kc_len = 0;
+  BO_CHECK_ARG(!pre || work != nullptr, "precomputed K*x needs a workspace");
   BO_CHECK_ARG(kc_len == 0 || (kc_len > 0 && kc_len % PK == 0 && work != nullptr),
                "split-k chunk %d must be a positive multiple of %d with a workspace", kc_len, PK);
   int Qp, nrows_pad, nC;
@@ -482,7 +511,15 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
   // One instantiation per active input dimension (the padded coordinates
   // beyond d are zero, so fewer distance terms are exact, not approximate).
 #define BO_POST_LAUNCH(KIND, ND)                                                            \
-  if (kc_len > 0)                                                                           \
+  if (pre) {                                                                                \
+    const int np = (int)(ceil_div(n, PC) * PC);                                             \
+    kxt_build_kernel<KIND, ND><<<dim3((unsigned)(nrows_pad / 256 + (nrows_pad % 256 != 0)), \
+                                      (unsigned)(np / 16)), 256, 0, st>>>(                  \
+        Xq, nrows, Xt_scaled, (int)n, np, nrows_pad, outputscale, work);                    \
+    post_partials_kernel<KIND, ND, false, false, true><<<(unsigned)blocks, 256, 0, st>>>(   \
+        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,  \
+        0, work, nullptr, 0, 0, nullptr);                                                   \
+  } else if (kc_len > 0)                                                                    \
     post_partials_kernel<KIND, ND, true, false><<<(unsigned)blocks, 256, 0, st>>>(          \
         Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,  \
         kc_len, work, nullptr, 0, 0, nullptr);                                              \

@@ -245,6 +245,8 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
         work_elems = sum(nk) * nrows_pad * 128
     else:
         kc_len, work_elems = 0, 0
+    if kc_len == 0 and cross is None and os.environ.get("BO_POST_PRECOMP") == "1":
+        kc_len, work_elems = -1, cache.np * nrows_pad  # timing experiment: K*x^T precomputed
     work = torch.empty(work_elems, **f64) if kc_len else None
     Cx = None
     if cross is not None and cross.shape[0] <= 16 and kc_len == 0:
