@@ -49,8 +49,9 @@ def _dist_env():
 def flops_post_partials(B, q, n):
     """Algorithmic flops of one post_partials launch:
     triangular R = K*x L^{-T}: (B q) n^2; R R^T diagonal blocks: 2 B q^2 n;
-    R beta: 2 B q n; kernel rows: B q n (3 d + 3)."""
-    return B * q * n * n + 2 * B * q * q * n + 2 * B * q * n + B * q * n * (3 * D + 3)
+    R beta: 2 B q n.  The kernel rows K*x (B q n (3 d + 3) flops plus one exp
+    each) are built beforehand by bo_post_kxt and are not counted here."""
+    return B * q * n * n + 2 * B * q * q * n + 2 * B * q * n
 
 
 def pmc_traffic(kernel="post_partials_kernel<0, 6, false, false>"):

@@ -117,11 +117,7 @@ class _FusedMC(torch.autograd.Function):
         cache = model.prediction_cache()
         ymean, ystd = model.outcome_stats()
         need_grad = ctx.needs_input_grad[0]
-        if kernels.TIMING_HOOK is not None:
-            kernels.TIMING_HOOK("post_partials_begin")
         pp = kernels.post_partials(cache, X3.detach(), store_R=need_grad)
-        if kernels.TIMING_HOOK is not None:
-            kernels.TIMING_HOOK("post_partials_end")
         lp = getattr(acqf, "_log_params", None)
         out = kernels.qmc_finalize(cache, pp, mode, ymean, ystd, Z=Z, best_f=best_f,
                                    best_f_s=best_f_s, want_mean=need_grad, want_cov=False,

@@ -131,7 +131,8 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     const double* __restrict__ U, int64_t ldu, const double* __restrict__ beta,
     double outputscale, int nC, int nI, double* __restrict__ Spart, double* __restrict__ mpart,
     double* __restrict__ Rt, int kc_len, double* __restrict__ work,
-    const double* __restrict__ Qc, int rq, int64_t ldq, double* __restrict__ Cx) {
+    const double* __restrict__ Qc, int rq, int64_t ldq, double* __restrict__ Cx,
+    const double* __restrict__ Kt) {
   // Two LDS stages: while the MFMAs consume stage t, the U rows of step t+1
   // are in flight to registers and this thread evaluates its 8 kernel values
   // of step t+1 between the MFMAs (VALU work hidden under the matrix pipe);
@@ -234,10 +235,10 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     _Pragma("unroll") for (int kk = 0; kk < 8; ++kk) Ks[BUF][kh * 8 + kk][ti] = kv[kk]; \
   }
 
-  // K*x value (row ti, training point k): evaluated in registers, or (PRE,
-  // timing experiment) read from a precomputed K*x^T (np x nrows_pad).
+  // K*x value (row ti, training point k): read from the K*x^T that
+  // bo_post_kxt built (PRE), or evaluated in registers between the MFMAs.
 #define BO_KVAL(K)                                                                         \
-  (PRE ? work[(int64_t)(K) * (nI * PI) + i0 + ti]                                          \
+  (PRE ? Kt[(int64_t)(K) * (nI * PI) + i0 + ti]                                            \
        : eval_kernel_row<KIND, ND>(xi, Xt, n, (K), outputscale, ivalid))
   BO_LOAD_U(kbeg);
 #pragma unroll
@@ -356,8 +357,12 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   }
 }
 
-// K*x^T for the PRE timing experiment: Kt[k][i] = outputscale k(x_i, x_k),
-// zero for k >= n or invalid rows; np x nrows_pad.
+// K*x^T once per call: Kt[k][i] = outputscale k(x_i, x_k), zero for k >= n
+// or padding rows; np x nrows_pad.  The one-pass grid re-reads each K*x tile
+// from L2/HBM for every column tile whose k-range covers it (nC / 2 times on
+// average) instead of re-evaluating its exponentials each time: at C3 the
+// posterior kernel runs 3.0 ms from precomputed values against 3.7 ms with
+// the exponentials between its MFMAs, for 0.08 ms of build.
 template <int KIND, int ND>
 __global__ __launch_bounds__(256) void kxt_build_kernel(const double* __restrict__ Xq, int nrows,
                                                         const double* __restrict__ Xt, int n,
@@ -482,20 +487,54 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
   return BO_OK;
 }
 
+int bo_post_kxt(int kind, const double* Xq, int B, int q, int d, const double* Xt_scaled,
+                int64_t n, double outputscale, double* Kt, void* stream) {
+  BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
+  BO_CHECK_ARG(d >= 1 && d <= DP, "fused posterior kernel supports 1 <= d <= %d", DP);
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  if (nrows_pad == 0) return BO_OK;
+  const int np = nC * PC;
+  const int nrows = B * Qp;
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((unsigned)ceil_div(nrows_pad, 256), (unsigned)(np / 16));
+#define BO_KXT(KIND, ND)                                                                   \
+  kxt_build_kernel<KIND, ND><<<grid, 256, 0, st>>>(Xq, nrows, Xt_scaled, (int)n, np, nrows_pad, \
+                                                   outputscale, Kt)
+#define BO_KXT_D(KIND)                       \
+  switch (d) {                               \
+    case 1: BO_KXT(KIND, 1); break;          \
+    case 2: BO_KXT(KIND, 2); break;          \
+    case 3: BO_KXT(KIND, 3); break;          \
+    case 4: BO_KXT(KIND, 4); break;          \
+    case 5: BO_KXT(KIND, 5); break;          \
+    case 6: BO_KXT(KIND, 6); break;          \
+    default: BO_KXT(KIND, 8); break;         \
+  }
+  if (kind == BO_RBF) {
+    BO_KXT_D(BO_RBF)
+  } else {
+    BO_KXT_D(BO_MATERN52)
+  }
+#undef BO_KXT_D
+#undef BO_KXT
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
 int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
                      const double* Xt_scaled, int64_t n, const double* U, int64_t ldu, const double* beta,
                      double outputscale, double* Spart, double* mpart, double* Rt,
                      int kc_len, double* work, const double* Qc, int rq, int64_t ldq, double* Cx,
-                     void* stream) {
+                     const double* Kt, void* stream) {
   BO_CHECK_ARG(Qc == nullptr || (kc_len == 0 && rq >= 1 && rq <= 16 && ldq >= n && Cx != nullptr),
                "cross term: one-pass only, 1 <= rq <= 16 rows (got %d), ldq >= n, Cx given", rq);
   BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
   BO_CHECK_ARG(ldu % 2 == 0 && ldu >= ceil_div(n, PC) * PC, "U leading dim %lld too small",
                (long long)ldu);
   if (B == 0) return BO_OK;  // no t-batches: nothing to launch
-  const bool pre = kc_len < 0;  // timing experiment: precomputed K*x^T in `work`
-  if (pre) kc_len = 0;
-  BO_CHECK_ARG(!pre || work != nullptr, "precomputed K*x needs a workspace");
+  const bool pre = Kt != nullptr;
   BO_CHECK_ARG(kc_len == 0 || (kc_len > 0 && kc_len % PK == 0 && work != nullptr),
                "split-k chunk %d must be a positive multiple of %d with a workspace", kc_len, PK);
   int Qp, nrows_pad, nC;
@@ -510,27 +549,21 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
   hipStream_t st = as_stream(stream);
   // One instantiation per active input dimension (the padded coordinates
   // beyond d are zero, so fewer distance terms are exact, not approximate).
+#define BO_POST_GO(KIND, ND, SPL, CRS, PRE_)                                                \
+  post_partials_kernel<KIND, ND, SPL, CRS, PRE_><<<(unsigned)blocks, 256, 0, st>>>(          \
+      Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,    \
+      kc_len, work, Qc, rq, ldq, Cx, Kt)
 #define BO_POST_LAUNCH(KIND, ND)                                                            \
-  if (pre) {                                                                                \
-    const int np = (int)(ceil_div(n, PC) * PC);                                             \
-    kxt_build_kernel<KIND, ND><<<dim3((unsigned)(nrows_pad / 256 + (nrows_pad % 256 != 0)), \
-                                      (unsigned)(np / 16)), 256, 0, st>>>(                  \
-        Xq, nrows, Xt_scaled, (int)n, np, nrows_pad, outputscale, work);                    \
-    post_partials_kernel<KIND, ND, false, false, true><<<(unsigned)blocks, 256, 0, st>>>(   \
-        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,  \
-        0, work, nullptr, 0, 0, nullptr);                                                   \
-  } else if (kc_len > 0)                                                                    \
-    post_partials_kernel<KIND, ND, true, false><<<(unsigned)blocks, 256, 0, st>>>(          \
-        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,  \
-        kc_len, work, nullptr, 0, 0, nullptr);                                              \
-  else if (Qc != nullptr)                                                                   \
-    post_partials_kernel<KIND, ND, false, true><<<(unsigned)blocks, 256, 0, st>>>(          \
-        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,  \
-        0, nullptr, Qc, rq, ldq, Cx);                                                       \
-  else                                                                                      \
-    post_partials_kernel<KIND, ND, false, false><<<(unsigned)blocks, 256, 0, st>>>(         \
-        Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,  \
-        0, nullptr, nullptr, 0, 0, nullptr)
+  if (kc_len > 0) {                                                                         \
+    if (pre) BO_POST_GO(KIND, ND, true, false, true);                                       \
+    else BO_POST_GO(KIND, ND, true, false, false);                                          \
+  } else if (Qc != nullptr) {                                                               \
+    if (pre) BO_POST_GO(KIND, ND, false, true, true);                                       \
+    else BO_POST_GO(KIND, ND, false, true, false);                                          \
+  } else {                                                                                  \
+    if (pre) BO_POST_GO(KIND, ND, false, false, true);                                      \
+    else BO_POST_GO(KIND, ND, false, false, false);                                         \
+  }
 #define BO_POST_DISPATCH_D(KIND)                   \
   switch (d) {                                     \
     case 1: BO_POST_LAUNCH(KIND, 1); break;        \
@@ -548,6 +581,7 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
   }
 #undef BO_POST_DISPATCH_D
 #undef BO_POST_LAUNCH
+#undef BO_POST_GO
   BO_LAUNCH_CHECK();
   if (kc_len > 0) {
     post_splitk_reduce_kernel<<<(unsigned)(nC * (nrows_pad / 16)), 64, 0, st>>>(

@@ -20,11 +20,12 @@ from . import _lib
 from ._lib import check, lib
 
 DP = 8  # padded input dimension of the fused posterior kernel
+KXT_MAX_BYTES = 4 << 30  # largest K*x^T workspace built per posterior call
 CHOLESKY_MAX_TRIES = 6  # botorch/__init__.py:47
 CHOLESKY_JITTER_F64 = 1e-8  # [G] linear_operator.settings.cholesky_jitter (double)
 
-# Optional callable(tag) invoked around the dominant kernel (bench.py records
-# HIP events on the current stream through it).
+# Optional callable(tag) invoked around the bo_post_partials launch (bench.py
+# records HIP events on the current stream through it).
 TIMING_HOOK = None
 
 
@@ -218,12 +219,15 @@ def split_plan(B: int, q: int, n: int, slots: int = 0):
 
 
 def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
-                  split: Optional[int] = None, cross: Optional[torch.Tensor] = None) -> PostPartials:
+                  split: Optional[int] = None, cross: Optional[torch.Tensor] = None,
+                  kxt: Optional[bool] = None) -> PostPartials:
     """Column-tile partials of R R^T and R beta for X (B x q x d).  ``split``:
     None = the library's plan, 0 = never split-k, k > 0 = chunks of k rows.
     ``cross`` (rq <= 16 rows x >= n): also return pp.Cx = cross K*x^T
     (rq x nrows_pad) from the same pass -- on one-pass plans only; under a
-    split-k plan pp.Cx is None and R^T is stored instead."""
+    split-k plan pp.Cx is None and R^T is stored instead.  ``kxt``: build
+    K*x^T first and read it in the posterior kernel (None: when it fits
+    KXT_MAX_BYTES)."""
     dev = _dev(X)
     B, q, d = X.shape
     if d != cache.d:
@@ -245,22 +249,33 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
         work_elems = sum(nk) * nrows_pad * 128
     else:
         kc_len, work_elems = 0, 0
-    if kc_len == 0 and cross is None and os.environ.get("BO_POST_PRECOMP") == "1":
-        kc_len, work_elems = -1, cache.np * nrows_pad  # timing experiment: K*x^T precomputed
     work = torch.empty(work_elems, **f64) if kc_len else None
+    # K*x^T built once and read by every column tile (instead of re-evaluating
+    # the kernel there), within a memory cap
+    Kt = None
+    if kxt is None:
+        kxt = cache.np * nrows_pad * 8 <= KXT_MAX_BYTES
+    if kxt:
+        Kt = torch.empty(cache.np, nrows_pad, **f64)
+        check(lib().bo_post_kxt(cache.kind, _p(Xq), B, q, d, _p(cache.Xt_scaled), cache.n,
+                                cache.outputscale, _p(Kt), st), "post_kxt")
     Cx = None
     if cross is not None and cross.shape[0] <= 16 and kc_len == 0:
         cross = cross.contiguous()
         Cx = torch.empty(nC, cross.shape[0], nrows_pad, **f64)  # column-tile partials
     elif cross is not None and Rt is None:
         Rt = torch.empty(nC * 128, nrows_pad, **f64)  # the caller forms the cross term from R^T
+    if TIMING_HOOK is not None:
+        TIMING_HOOK("post_partials_begin")
     check(lib().bo_post_partials(cache.kind, _p(Xq), B, q, d, _p(cache.Xt_scaled), cache.n,
                                  _p(cache.U), cache.np, _p(cache.beta), cache.outputscale,
                                  _p(Spart), _p(mpart), _p(Rt), kc_len, _p(work),
                                  _p(cross if Cx is not None else None),
                                  cross.shape[0] if Cx is not None else 0,
-                                 cross.shape[1] if Cx is not None else 0, _p(Cx), st),
+                                 cross.shape[1] if Cx is not None else 0, _p(Cx), _p(Kt), st),
           "post_partials")
+    if TIMING_HOOK is not None:
+        TIMING_HOOK("post_partials_end")
     return PostPartials(B, q, Qp, nrows_pad, nC, Xq, Spart, mpart, Rt,
                         Cx.sum(dim=0) if Cx is not None else None)
 

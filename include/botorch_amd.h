@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 6
+#define BO_ABI_VERSION 7
 
 /* status codes */
 #define BO_OK 0
@@ -200,12 +200,20 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
  * products with K*x are returned as nC column-tile partials
  * Cx[ci] (nC x rq x nrows_pad; sum over ci = Qc K*x^T) -- the
  * qNEI cross-covariance P_b R^T = Q_b K*x^T, Q_b = P_b U^T
- * (acquisition/cached_cholesky.py:94-120), without storing R. */
+ * (acquisition/cached_cholesky.py:94-120), without storing R.
+ * Kt (nullable): K*x^T from bo_post_kxt (read instead of evaluated). */
 int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
                      const double* Xt_scaled, int64_t n, const double* U, int64_t ldu, const double* beta,
                      double outputscale, double* Spart, double* mpart, double* Rt,
                      int kc_len, double* work, const double* Qc, int rq, int64_t ldq, double* Cx,
-                     void* stream);
+                     const double* Kt, void* stream);
+
+/* K*x^T of the same call, np x nrows_pad (np = 128 nC): Kt[k][i] =
+ * outputscale k(x_i, x_k), zero for k >= n and padding rows.  Passed to
+ * bo_post_partials as Kt, the posterior kernel reads these values instead of
+ * evaluating each one again for every column tile that covers it. */
+int bo_post_kxt(int kind, const double* Xq, int B, int q, int d, const double* Xt_scaled,
+                int64_t n, double outputscale, double* Kt, void* stream);
 
 /* Split-k plan of bo_post_partials (host pointers): the chunk length in
  * {64, ..., 1024} (or 0 = one pass) that minimises a k-step cost model of the
