@@ -4,8 +4,8 @@
 Workload (BASELINE.json metric, SURVEY.md section 8 config C3 at N=1):
 SingleTaskGP on Hartmann6, n=4096, d=6, fp64, Standardize; qExpectedImprovement
 with q=16, 512 restarts (t-batches) per GPU, 512 Sobol-QMC samples.  A "step" is
-one acquisition forward over the whole batch: fused kernel-row build + R = K*x
-L^{-T} GEMM + R R^T epilogue (post_partials), then per-t-batch finalisation,
+one acquisition forward over the whole batch: the kernel rows K*x^T (bo_post_kxt),
+the R = K*x L^{-T} GEMM + R R^T epilogue (post_partials), then per-t-batch finalisation,
 jittered q x q Cholesky, reparameterised sampling and the MC reduction
 (qmc_finalize), then the cross-rank argmax (one all-reduce).  Model caches
 (Cholesky, L^{-T}) are built once before timing, as the reference builds them
@@ -54,7 +54,7 @@ def flops_post_partials(B, q, n):
     return B * q * n * n + 2 * B * q * q * n + 2 * B * q * n
 
 
-def pmc_traffic(kernel="post_partials_kernel<0, 6, false, false>"):
+def pmc_traffic(kernel="post_partials_kernel<0, 6, false, false, true>"):
     """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 PMC
     summary (profiles/rNN/pmc_summary.json, written by tools/pmc_summary.py from
     separate --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command,
