@@ -10,8 +10,9 @@
 //
 // post_partials_kernel computes R^T tile by tile as an MFMA GEMM
 //   R^T[c][i] = sum_k U[k][c] K*x[i][k],   U = L^{-T} (upper triangular)
-// with the K*x tile generated on the fly from the lengthscale-scaled inputs
-// (never written to HBM) and U streamed from HBM/L2.  Because the R^T tile's
+// with the K*x tile read from K*x^T (built once per call by kxt_build_kernel)
+// or, above the memory cap, generated on the fly from the lengthscale-scaled
+// inputs, and U streamed from HBM/L2.  Because the R^T tile's
 // MFMA accumulators have the test row on the lane and the training column on
 // (lane>>4, register), the same accumulator register is simultaneously a
 // valid A and B operand of a second MFMA, so  R_b R_b^T  over the tile's 128
