@@ -282,7 +282,16 @@ __global__ __launch_bounds__(THREADS) void qmc_log_backward_kernel(
   chol_backward_lds(q, L, dL, Li, Pm, Tm, dcov + (int64_t)b * q * q, tid);
 }
 
-// dX for one t-batch per workgroup.  TPA threads per test row a, striding k.
+static_assert(THREADS == QMAX * QMAX, "post_backward: one G entry per thread");
+
+// dX for one t-batch per workgroup.  The G W term is a (16 x 16) x (16 x 16k)
+// product per block of 16 training points, so each wave runs it on the matrix
+// cores: A = G[a][j] (fixed for the kernel, in registers), B = W[j][k] (the
+// t-batch's 16 W rows, 128-B row segments, each element read once), and the
+// accumulator leaves lane (jq, kc) with D for rows jq + 4r and training point
+// k0 + kc -- fixed rows per lane, so their coordinates stay in registers while
+// the lane evaluates dk/dx for its 4 (row, point) pairs.  The waves stride over
+// the 16-point blocks; per-row sums are combined by shuffles and LDS.
 template <int KIND, int ND>
 __global__ __launch_bounds__(THREADS) void post_backward_kernel(
     int q, int Qp, const double* __restrict__ Xq, const double* __restrict__ Xt, int n,
@@ -294,76 +303,106 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
   __shared__ double G[QMAX][QMAX + 1];
   __shared__ double dmu[QMAX];
   __shared__ double xs[QMAX][DP];
-  __shared__ double red[THREADS][DP + 1];
+  __shared__ double red[THREADS / 64][QMAX][DP + 1];
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int row0 = b * Qp;
   const double s2 = ystd * ystd;
-  if (tid < q * q) {
-    const int a = tid / q, c = tid % q;
-    const double* dc = dcov + (int64_t)b * q * q;
-    G[a][c] = dcov ? s2 * (dc[a * q + c] + dc[c * q + a]) : 0.0;
+  {  // THREADS == QMAX * QMAX: one entry of G per thread, zero outside q x q
+    const int a = tid / QMAX, c = tid % QMAX;
+    const double* dc = dcov ? dcov + (int64_t)b * q * q : nullptr;
+    G[a][c] = (dc && a < q && c < q) ? s2 * (dc[a * q + c] + dc[c * q + a]) : 0.0;
   }
-  if (tid < q) dmu[tid] = dmean ? ystd * dmean[(int64_t)b * q + tid] : 0.0;
-  if (tid < q * DP) xs[tid / DP][tid % DP] = Xq[(int64_t)(row0 + tid / DP) * DP + tid % DP];
+  if (tid < QMAX) dmu[tid] = (dmean && tid < q) ? ystd * dmean[(int64_t)b * q + tid] : 0.0;
+  if (tid < QMAX * DP) {
+    const int a = tid / DP, t = tid % DP;
+    xs[a][t] = a < q ? Xq[(int64_t)(row0 + a) * DP + t] : 0.0;
+  }
   __syncthreads();
 
-  const int TPA = THREADS / Qp;
-  const int a = tid / TPA;
-  const int kk = tid % TPA;
-  double acc[ND];
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int kc = lane & 15;   // training point within a 16-block (MFMA column)
+  const int jq = lane >> 4;   // MFMA inner index; output rows jq + 4 r
+  double ga[4], dm[4], xa[4][ND], acc[4][ND];
 #pragma unroll
-  for (int t = 0; t < ND; ++t) acc[t] = 0.0;
-  if (a < q) {
-    double xa[ND];
+  for (int s = 0; s < 4; ++s) ga[s] = G[kc][4 * s + jq];
 #pragma unroll
-    for (int t = 0; t < ND; ++t) xa[t] = xs[a][t];
-    const double dma = dmu[a];
-    const double* Ea = E ? E + (int64_t)(row0 + a) * lde : nullptr;
-    for (int k = kk; k < n; k += TPA) {
-      double D = alpha ? dma * alpha[k] : 0.0;
-      if (W)
-        for (int j = 0; j < q; ++j) D = fma(-G[a][j], W[(int64_t)(row0 + j) * ldw + k], D);
-      if (Ea) D += Ea[k];
-      const double* xt = Xt + (int64_t)k * DP;
+  for (int r = 0; r < 4; ++r) {
+    dm[r] = dmu[jq + 4 * r];
+#pragma unroll
+    for (int t = 0; t < ND; ++t) {
+      xa[r][t] = xs[jq + 4 * r][t];
+      acc[r][t] = 0.0;
+    }
+  }
+  for (int k0 = wave * 16; k0 < n; k0 += 16 * (THREADS / 64)) {  // wave-uniform trip count
+    const int k = k0 + kc;
+    const bool kv = k < n;
+    v4d c = v4d_zero();
+    if (W) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int j = 4 * s + jq;
+        const double wb = (j < q && kv) ? W[(int64_t)(row0 + j) * ldw + k] : 0.0;
+        c = mfma_f64(ga[s], wb, c);
+      }
+    }
+    const double al = (alpha && kv) ? alpha[k] : 0.0;
+    double xt[ND];
+#pragma unroll
+    for (int t = 0; t < ND; ++t) xt[t] = kv ? Xt[(int64_t)k * DP + t] : 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = jq + 4 * r;
+      double D = fma(dm[r], al, -c[r]);
+      if (E && a < q && kv) D += E[(int64_t)(row0 + a) * lde + k];
       double diff[ND];
       double d2 = 0.0;
 #pragma unroll
       for (int t = 0; t < ND; ++t) {
-        diff[t] = xa[t] - xt[t];
+        diff[t] = xa[r][t] - xt[t];
         d2 = fma(diff[t], diff[t], d2);
       }
       const double f = D * dkernel_factor<KIND>(d2, outputscale);
 #pragma unroll
-      for (int t = 0; t < ND; ++t) acc[t] = fma(f, diff[t], acc[t]);
-    }
-    // K** terms: Sigma*[a][c] = K**(a, c) - ..., d K** = d Sigma* (c != a; the
-    // diagonal is the constant outputscale).
-    if (kk == 0 && dcov) {
-      for (int c = 0; c < q; ++c) {
-        if (c == a) continue;
-        double diff[ND];
-        double d2 = 0.0;
-#pragma unroll
-        for (int t = 0; t < ND; ++t) {
-          diff[t] = xa[t] - xs[c][t];
-          d2 = fma(diff[t], diff[t], d2);
-        }
-        const double f = G[a][c] * dkernel_factor<KIND>(d2, outputscale);
-#pragma unroll
-        for (int t = 0; t < ND; ++t) acc[t] = fma(f, diff[t], acc[t]);
-      }
+      for (int t = 0; t < ND; ++t) acc[r][t] = fma(f, diff[t], acc[r][t]);
     }
   }
+  // sum over the 16 lanes of a row group (kc), then over the waves
 #pragma unroll
-  for (int t = 0; t < ND; ++t) red[tid][t] = acc[t];
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int t = 0; t < ND; ++t) {
+      double v = acc[r][t];
+      v += __shfl_xor(v, 1);
+      v += __shfl_xor(v, 2);
+      v += __shfl_xor(v, 4);
+      v += __shfl_xor(v, 8);
+      if (kc == 0) red[wave][jq + 4 * r][t] = v;
+    }
   __syncthreads();
   if (tid < q * d) {
-    const int ra = tid / d, t = tid % d;
+    const int a = tid / d, t = tid % d;
     double s = 0.0;
-    for (int u = 0; u < TPA; ++u) s += red[ra * TPA + u][t];
-    double* o = dX + ((int64_t)b * q + ra) * d + t;
+#pragma unroll
+    for (int w = 0; w < THREADS / 64; ++w) s += red[w][a][t];
+    // K** terms: Sigma*[a][c] = K**(a, c) - ..., d K** = d Sigma* (c != a; the
+    // diagonal is the constant outputscale).
+    if (dcov) {
+      for (int c = 0; c < q; ++c) {
+        if (c == a) continue;
+        double d2 = 0.0;
+#pragma unroll
+        for (int u = 0; u < ND; ++u) {
+          const double df = xs[a][u] - xs[c][u];
+          d2 = fma(df, df, d2);
+        }
+        s = fma(G[a][c] * dkernel_factor<KIND>(d2, outputscale), xs[a][t] - xs[c][t], s);
+      }
+    }
+    double* o = dX + ((int64_t)b * q + a) * d + t;
     *o = accumulate ? *o + s / ls[t] : s / ls[t];
   }
 }

@@ -30,6 +30,7 @@ for s in "$@"; do
     pmc_mfma) step pmc_mfma 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_mfma -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fit --no-extra --no-bwd ;;
     prof_small) step prof_small 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_small -o run --output-format csv -- python tools/prof_small.py c2 ;;
     prof_chol) export BO_ONLY=chol; step prof_chol 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_chol -o run --output-format csv -- python tools/bench_linalg.py ;;
+    prof_bwd) step prof_bwd 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bwd -o run --output-format csv -- python tools/prof_bwd.py ;;
     potrf) step potrf 120 python tools/probe_potrf.py ;;
     linalg) step linalg 300 python tools/bench_linalg.py ;;
     probe) step probe 120 python tools/probe_rate.py ;;
