@@ -19,7 +19,7 @@ RBF, MATERN52 = 0, 1
 GEMM_LOWER_C, GEMM_A_LOWER, GEMM_B_UPPER, GEMM_A_UPPER, GEMM_B_LOWER = 1, 2, 4, 8, 16
 QMC_POSTERIOR, QMC_QEI, QMC_QNEI, QMC_CHOL, QMC_QLOGEI, QMC_QLOGNEI = 0, 1, 2, 3, 4, 5
 LOG_MODES = (QMC_QLOGEI, QMC_QLOGNEI)
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _P = c_void_p  # device pointers travel as void*
 
@@ -60,6 +60,7 @@ _SIGNATURES = {
                                  c_double, _P, _P, _P, c_int, _P, _P, c_int, c_int64, _P, _P,
                                  _P]),
     "bo_post_kxt": (c_int, [c_int, _P, c_int, c_int, c_int, _P, c_int64, c_double, _P, _P]),
+    "bo_post_w": (c_int, [_P, c_int64, _P, c_int, c_int, c_int64, _P, _P]),
     "bo_post_split_plan": (c_int, [c_int64, c_int, c_int64, c_int, POINTER(c_int),
                                    POINTER(c_int64)]),
     "bo_qmc_finalize": (c_int, [c_int, c_int, c_int, c_int, _P, _P, _P, c_int64, c_double,
@@ -86,7 +87,8 @@ _SIGNATURES = {
     "bo_qmc_backward": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, c_double, _P, _P,
                                 c_int64, _P, _P, _P, _P, _P, c_int, c_double, c_double, _P]),
     "bo_post_backward": (c_int, [c_int, c_int, c_int, c_int, _P, _P, c_int64, _P, c_int64, _P,
-                                 _P, _P, _P, c_int64, _P, c_double, c_double, c_int, _P, _P]),
+                                 _P, _P, _P, c_int64, _P, c_double, c_double, c_int, _P, c_int,
+                                 _P]),
 }
 
 _lib = None

@@ -299,7 +299,7 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
     const double* __restrict__ dmean, const double* __restrict__ dcov,
     const double* __restrict__ E, int64_t lde,
     const double* __restrict__ ls, double outputscale, double ystd, int d, int accumulate,
-    double* __restrict__ dX) {
+    double* __restrict__ dX, int wkm) {
   __shared__ double G[QMAX][QMAX + 1];
   __shared__ double dmu[QMAX];
   __shared__ double xs[QMAX][DP];
@@ -337,7 +337,9 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
       acc[r][t] = 0.0;
     }
   }
-  for (int k0 = wave * 16; k0 < n; k0 += 16 * (THREADS / 64)) {  // wave-uniform trip count
+  // two 16-point blocks per iteration (independent MFMA / exp chains); the
+  // second one's points past n are masked like any ragged block
+  auto block = [&](int k0) {
     const int k = k0 + kc;
     const bool kv = k < n;
     v4d c = v4d_zero();
@@ -345,7 +347,8 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int j = 4 * s + jq;
-        const double wb = (j < q && kv) ? W[(int64_t)(row0 + j) * ldw + k] : 0.0;
+        const int64_t wi = wkm ? (int64_t)k * ldw + row0 + j : (int64_t)(row0 + j) * ldw + k;
+        const double wb = (j < q && kv) ? W[wi] : 0.0;
         c = mfma_f64(ga[s], wb, c);
       }
     }
@@ -369,6 +372,11 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
 #pragma unroll
       for (int t = 0; t < ND; ++t) acc[r][t] = fma(f, diff[t], acc[r][t]);
     }
+  };
+  constexpr int KSTRIDE = 16 * (THREADS / 64);
+  for (int k0 = wave * 16; k0 < n; k0 += 2 * KSTRIDE) {  // wave-uniform trip count
+    block(k0);
+    block(k0 + KSTRIDE);
   }
   // sum over the 16 lanes of a row group (kc), then over the waves
 #pragma unroll
@@ -529,7 +537,7 @@ extern "C" int bo_post_backward(int kind, int B, int q, int d, const double* Xq,
                                 const double* alpha, const double* dmean, const double* dcov,
                                 const double* E, int64_t lde, const double* lengthscale,
                                 double outputscale, double ystd, int accumulate, double* dX,
-                                void* stream) {
+                                int w_kmajor, void* stream) {
   BO_CHECK_ARG(q >= 1 && q <= QMAX && d >= 1 && d <= DP, "bo_post_backward: bad q/d");
   if (B == 0) return BO_OK;
   int Qp = 1;
@@ -539,7 +547,7 @@ extern "C" int bo_post_backward(int kind, int B, int q, int d, const double* Xq,
   post_backward_kernel<KIND, ND><<<B, THREADS, 0, st>>>(q, Qp, Xq, Xt_scaled, (int)n, W, ldw, \
                                                         alpha, dmean, dcov, E, lde,           \
                                                         lengthscale, outputscale, ystd, d,    \
-                                                        accumulate, dX)
+                                                        accumulate, dX, w_kmajor)
   if (kind == BO_RBF) {
     if (d == 6) BO_PB(BO_RBF, 6); else BO_PB(BO_RBF, 8);
   } else {

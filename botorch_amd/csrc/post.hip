@@ -126,7 +126,7 @@ __device__ __forceinline__ void post_epilogue(const v4d (&acc)[8], int ci, int r
   if (lane < 16) mpart[(int64_t)ci * nrows_pad + row0 + lane] = m;
 }
 
-template <int KIND, int ND, bool SPLIT, bool CROSS, bool PRE = false>
+template <int KIND, int ND, bool SPLIT, bool CROSS, bool PRE = false, bool LOWERK = false>
 __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     const double* __restrict__ Xq, int nrows, const double* __restrict__ Xt, int n,
     const double* __restrict__ U, int64_t ldu, const double* __restrict__ beta,
@@ -188,6 +188,13 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     if (pos >= nC) return;
     ci = nC - 1 - pos;
     kend = min(n, ci * PC + PC);
+  }
+  if constexpr (LOWERK) {
+    // W^T = L^{-T} R^T (bo_post_w): column tile ci reads k in [128 ci, n),
+    // so the heaviest tiles are the SMALLEST ci -- mirror the schedule's order.
+    ci = nC - 1 - ci;
+    kbeg = ci * PC;
+    kend = n;
   }
   const int c0 = ci * PC;
   const int i0 = ii * PI;
@@ -351,6 +358,7 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
             Rt[(int64_t)c * nrows_pad + i] = acc[ct][it][r];
           }
     }
+    if constexpr (LOWERK) return;  // W^T only
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       v4d P = v4d_zero();
@@ -612,6 +620,29 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
         work, (int)n, nC, nI, kc_len, beta, Spart, mpart, Rt);
     BO_LAUNCH_CHECK();
   }
+  return BO_OK;
+}
+
+int bo_post_w(const double* Linv, int64_t ldl, const double* Rt, int B, int q, int64_t n,
+              double* Wt, void* stream) {
+  BO_CHECK_ARG(ldl % 2 == 0 && ldl >= ceil_div(n, PC) * PC, "L^{-1} leading dim %lld too small",
+               (long long)ldl);
+  if (B == 0) return BO_OK;
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  const int nI = nrows_pad / PI;
+  if (nI == 0) return BO_OK;
+  if (nC % 8 != 0 || nI % 8 != 0) {
+    bo_set_error("bo_post_w: %d column x %d row tiles do not form 8 x 8 super-tiles", nC, nI);
+    return BO_ERR_ARG;
+  }
+  const int64_t blocks = 512 * (int64_t)ceil_div((nC / 8) * (nI / 8), 8);
+  post_partials_kernel<BO_RBF, 1, false, false, true, true><<<(unsigned)blocks, 256, 0,
+                                                                as_stream(stream)>>>(
+      Rt, 0, Rt, (int)n, Linv, ldl, nullptr, 0.0, nC, nI, nullptr, nullptr, Wt, 0,
+      nullptr, nullptr, 0, 0, nullptr, Rt, 1);
+  BO_LAUNCH_CHECK();
   return BO_OK;
 }
 

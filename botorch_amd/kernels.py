@@ -353,18 +353,33 @@ def probe_mfma_layout(device) -> torch.Tensor:
     return out
 
 
-def w_matrix(cache: GPCache, pp: PostPartials) -> torch.Tensor:
-    """W = R L^{-1} = K*x (K + s2 I)^{-1}  (nrows_pad x np), from the stored R^T:
-    W[i][k] = sum_c R[i][c] U[k][c]  (U = L^{-T} upper -> op(B) zero below c < k)."""
+@dataclass
+class WMat:
+    """W = R L^{-1} for post_backward: ``t`` is W (nrows_pad x np) or, with
+    ``kmajor``, W^T (np x nrows_pad) as bo_post_w writes it."""
+    t: torch.Tensor
+    kmajor: bool
+
+
+def w_matrix(cache: GPCache, pp: PostPartials) -> WMat:
+    """W = R L^{-1} = K*x (K + s2 I)^{-1}, from the stored R^T.  Grids of 8 x 8
+    super-tiles: W^T = L^{-T} R^T on the posterior kernel's MFMA tiles
+    (bo_post_w); otherwise the GEMM W[i][k] = sum_c R[i][c] U[k][c] (U = L^{-T}
+    upper -> op(B) zero below c < k)."""
     if pp.Rt is None:
         raise RuntimeError("post_partials(store_R=True) is required for gradients")
     dev = pp.Rt.device
+    if pp.nC % 8 == 0 and (pp.nrows_pad // 128) % 8 == 0:
+        Wt = torch.empty(cache.np, pp.nrows_pad, dtype=torch.float64, device=dev)
+        check(lib().bo_post_w(_p(cache.Linv), cache.np, _p(pp.Rt), pp.B, pp.q, cache.n, _p(Wt),
+                              _stream(dev)), "post_w")
+        return WMat(Wt, True)
     W = torch.empty(pp.nrows_pad, cache.np, dtype=torch.float64, device=dev)
     K = pp.nC * 128
     check(lib().bo_gemm_f64(1, 1, pp.nrows_pad, cache.np, K, 1.0, _p(pp.Rt), pp.nrows_pad, 0,
                             _p(cache.U), cache.np, 0, 0.0, _p(W), cache.np, 0, 1,
                             _lib.GEMM_B_LOWER, _stream(dev)), "w_matrix")
-    return W
+    return WMat(W, False)
 
 
 def qmc_backward(mode: int, mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor,
@@ -393,7 +408,7 @@ def qmc_backward(mode: int, mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor
     return dmean, dcov
 
 
-def post_backward(cache: GPCache, pp: PostPartials, W: Optional[torch.Tensor],
+def post_backward(cache: GPCache, pp: PostPartials, W: Optional[WMat],
                   dmean: Optional[torch.Tensor], dcov: Optional[torch.Tensor], ystd: float,
                   E: Optional[torch.Tensor] = None, Xt_scaled: Optional[torch.Tensor] = None,
                   n: Optional[int] = None, dX: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -407,14 +422,18 @@ def post_backward(cache: GPCache, pp: PostPartials, W: Optional[torch.Tensor],
         dX = torch.empty(pp.B, pp.q, cache.d, dtype=torch.float64, device=dev)
     other = Xt_scaled is not None
     cont = lambda t: t.contiguous() if t is not None else None  # noqa: E731
-    W, E, dmean, dcov = cont(W), cont(E), cont(dmean), cont(dcov)
+    if isinstance(W, torch.Tensor):
+        W = WMat(W, False)
+    kmajor = W is not None and W.kmajor
+    W = cont(W.t) if W is not None else None
+    E, dmean, dcov = cont(E), cont(dmean), cont(dcov)
     check(lib().bo_post_backward(cache.kind, pp.B, pp.q, cache.d, _p(pp.Xq),
                                  _p(Xt_scaled if other else cache.Xt_scaled),
                                  n if other else cache.n, _p(W), W.shape[1] if W is not None else 0,
                                  None if other else _p(cache.alpha), _p(dmean), _p(dcov), _p(E),
                                  E.shape[1] if E is not None else 0, _p(cache.lengthscale),
                                  cache.outputscale, float(ystd), int(acc), _p(dX),
-                                 _stream(dev)), "post_backward")
+                                 int(kmajor), _stream(dev)), "post_backward")
     return dX
 
 

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 7
+#define BO_ABI_VERSION 8
 
 /* status codes */
 #define BO_OK 0
@@ -215,6 +215,15 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
 int bo_post_kxt(int kind, const double* Xq, int B, int q, int d, const double* Xt_scaled,
                 int64_t n, double outputscale, double* Kt, void* stream);
 
+/* W^T = L^{-T} R^T = (K*x (K + s2 I)^{-1})^T for the posterior backward, np x
+ * nrows_pad, from bo_post_partials' stored R^T (np x nrows_pad) and L^{-1}
+ * (lower, ld ldl): the posterior kernel's MFMA tiles over the lower k-range
+ * k >= c of each column (the second forward-size contraction of the gradient,
+ * SURVEY.md 8(a) a14).  BO_ERR_ARG when the tile grid does not form 8 x 8
+ * super-tiles (the caller then uses bo_gemm_f64). */
+int bo_post_w(const double* Linv, int64_t ldl, const double* Rt, int B, int q, int64_t n,
+              double* Wt, void* stream);
+
 /* Split-k plan of bo_post_partials (host pointers): the chunk length in
  * {64, ..., 1024} (or 0 = one pass) that minimises a k-step cost model of the
  * triangular grid over `slots` resident workgroups (slots <= 0: 512 = 256 CUs
@@ -270,7 +279,8 @@ int bo_qmc_backward(int mode, int B, int q, const double* mean, const double* Lq
 
 /* Backward of the batched exact posterior w.r.t. the candidates X (B x q x d):
  *   dK*x = ystd dmean alpha^T - G W,  G = ystd^2 (dcov + dcov^T),
- *   W = R L^{-1} (nrows_pad x ldw, rows b*Qp + a), dK** = ystd^2 dcov,
+ *   W = R L^{-1} (nrows_pad x ldw, rows b*Qp + a; w_kmajor != 0: W^T as
+ *   bo_post_w writes it, np x ldw), dK** = ystd^2 dcov,
  *   + E (optional extra dK*x, nrows_pad x lde, same rows: the qNEI cross-
  *     covariance terms),
  * reduced through dk/dx.  Xq / Xt_scaled as for bo_post_partials.  W, alpha,
@@ -282,7 +292,7 @@ int bo_post_backward(int kind, int B, int q, int d, const double* Xq, const doub
                      int64_t n, const double* W, int64_t ldw, const double* alpha,
                      const double* dmean, const double* dcov, const double* E, int64_t lde,
                      const double* lengthscale, double outputscale, double ystd, int accumulate,
-                     double* dX, void* stream);
+                     double* dX, int w_kmajor, void* stream);
 
 /* Kernel-matrix gradient for any d <= 128 (inputs in the original scale):
  *   dX[i][t] (+)= sum_k dK[i][k] d k(X_i, Y_k) / d X_it,

@@ -395,3 +395,52 @@ def test_empty_batches_all_acquisitions(golden):
         for a in acqfs:
             v = a(empty)
             assert v.shape == (0,), type(a).__name__
+
+
+@pytest.mark.parametrize("B,q", [(64, 16), (128, 8)])
+def test_qei_gradient_post_w_path(B, q):
+    """Grids of 8 x 8 super-tiles (n = 1024, B * Qp = 1024) take W^T = L^{-T} R^T
+    from bo_post_w instead of the GEMM: W against the GEMM route, and the qEI
+    value and gradient against the oracle."""
+    from botorch_amd import _lib, kernels
+    from botorch_amd.acquisition import qExpectedImprovement
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import qei
+    from oracle.sampling import draw_sobol_normal_samples
+    X, Y, m, orc = _setup(n=1024)
+    g = torch.Generator().manual_seed(B + q)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64)
+    cache = m.prediction_cache()
+    pp = kernels.post_partials(cache, Xc.to(DEV), store_R=True)
+    assert pp.nC % 8 == 0 and (pp.nrows_pad // 128) % 8 == 0
+    W = kernels.w_matrix(cache, pp)
+    assert W.kmajor and W.t.shape == (cache.np, pp.nrows_pad)
+    Wg = kernels.gemm(pp.Rt, cache.U, transA=True, transB=True, flags=_lib.GEMM_B_LOWER)
+    torch.testing.assert_close(W.t.T.cpu(), Wg.cpu(), rtol=1e-10, atol=1e-11)
+
+    best_f = Y.max().item() - 0.3
+    S = 64
+    acqf = qExpectedImprovement(m, best_f, sampler=SobolQMCNormalSampler(torch.Size([S]), seed=3))
+    Xd = Xc.to(DEV).requires_grad_(True)
+    val = acqf(Xd)
+    (gd,) = torch.autograd.grad(val.sum(), Xd)
+    Xo = Xc.clone().requires_grad_(True)
+    ref = qei(orc, Xo, draw_sobol_normal_samples(q, S, 3), best_f)
+    (go,) = torch.autograd.grad(ref.sum(), Xo)
+    torch.testing.assert_close(val.detach().cpu(), ref.detach(), rtol=1e-6, atol=1e-10)
+    torch.testing.assert_close(gd.cpu(), go, rtol=1e-5, atol=1e-8)
+
+
+def test_post_w_full_size_matches_gemm():
+    """bo_post_w at the C3 training size (n = 4096, 32 column tiles, the
+    mirrored heaviest-first schedule) against the triangular GEMM route."""
+    from botorch_amd import _lib, kernels
+    X, Y, m, orc = _setup(n=4096)
+    g = torch.Generator().manual_seed(7)
+    Xc = torch.rand(64, 16, 6, generator=g, dtype=torch.float64)
+    cache = m.prediction_cache()
+    pp = kernels.post_partials(cache, Xc.to(DEV), store_R=True)
+    W = kernels.w_matrix(cache, pp)
+    assert W.kmajor
+    Wg = kernels.gemm(pp.Rt, cache.U, transA=True, transB=True, flags=_lib.GEMM_B_LOWER)
+    torch.testing.assert_close(W.t.T, Wg, rtol=1e-10, atol=1e-10)
