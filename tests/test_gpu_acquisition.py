@@ -399,9 +399,10 @@ def test_empty_batches_all_acquisitions(golden):
 
 @pytest.mark.parametrize("B,q", [(64, 16), (128, 8)])
 def test_qei_gradient_post_w_path(B, q):
-    """Grids of 8 x 8 super-tiles (n = 1024, B * Qp = 1024) take W^T = L^{-T} R^T
-    from bo_post_w instead of the GEMM: W against the GEMM route, and the qEI
-    value and gradient against the oracle."""
+    """Grids of 8 x 8 super-tiles (n = 1024, B * Qp = 1024) can take W^T =
+    L^{-T} R^T from bo_post_w instead of the GEMM: W (forced) against the GEMM
+    route, and the qEI value and gradient through the API (GEMM route at this
+    grid size) against the oracle."""
     from botorch_amd import _lib, kernels
     from botorch_amd.acquisition import qExpectedImprovement
     from botorch_amd.sampling import SobolQMCNormalSampler
@@ -413,10 +414,16 @@ def test_qei_gradient_post_w_path(B, q):
     cache = m.prediction_cache()
     pp = kernels.post_partials(cache, Xc.to(DEV), store_R=True)
     assert pp.nC % 8 == 0 and (pp.nrows_pad // 128) % 8 == 0
-    W = kernels.w_matrix(cache, pp)
+    W = kernels.w_matrix(cache, pp, post_w=True)
     assert W.kmajor and W.t.shape == (cache.np, pp.nrows_pad)
     Wg = kernels.gemm(pp.Rt, cache.U, transA=True, transB=True, flags=_lib.GEMM_B_LOWER)
     torch.testing.assert_close(W.t.T.cpu(), Wg.cpu(), rtol=1e-10, atol=1e-11)
+    # post_backward reading W^T k-major == reading W row-major
+    dmean = torch.randn(B, q, generator=g, dtype=torch.float64).to(DEV)
+    dcov = torch.randn(B, q, q, generator=g, dtype=torch.float64).to(DEV)
+    dx_k = kernels.post_backward(cache, pp, W, dmean, dcov, 0.7)
+    dx_r = kernels.post_backward(cache, pp, kernels.WMat(Wg, False), dmean, dcov, 0.7)
+    torch.testing.assert_close(dx_k, dx_r, rtol=1e-10, atol=1e-12)
 
     best_f = Y.max().item() - 0.3
     S = 64
@@ -440,7 +447,7 @@ def test_post_w_full_size_matches_gemm():
     Xc = torch.rand(64, 16, 6, generator=g, dtype=torch.float64)
     cache = m.prediction_cache()
     pp = kernels.post_partials(cache, Xc.to(DEV), store_R=True)
-    W = kernels.w_matrix(cache, pp)
+    W = kernels.w_matrix(cache, pp, post_w=True)
     assert W.kmajor
     Wg = kernels.gemm(pp.Rt, cache.U, transA=True, transB=True, flags=_lib.GEMM_B_LOWER)
     torch.testing.assert_close(W.t.T, Wg, rtol=1e-10, atol=1e-10)
