@@ -259,7 +259,9 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     *reinterpret_cast<double2*>(dst + 4 * PLD) = make_double2(u1x, u1y);          \
     *reinterpret_cast<double2*>(dst + 8 * PLD) = make_double2(u2x, u2y);          \
     *reinterpret_cast<double2*>(dst + 12 * PLD) = make_double2(u3x, u3y);         \
-    _Pragma("unroll") for (int kk = 0; kk < 8; ++kk) Ks[BUF][kh * 8 + kk][ti] = kv[kk]; \
+    if (!PRE) {                                                                   \
+      _Pragma("unroll") for (int kk = 0; kk < 8; ++kk) Ks[BUF][kh * 8 + kk][ti] = kv[kk]; \
+    }                                                                             \
   }
 
   // K*x value (row ti, training point k): read from the K*x^T that
@@ -267,10 +269,24 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
 #define BO_KVAL(K)                                                                         \
   (PRE ? Kt[(int64_t)(K) * (nI * PI) + i0 + ti]                                            \
        : eval_kernel_row<KIND, ND>(xi, Xt, n, (K), outputscale, ivalid))
+  // PRE: the MFMA B operands (K*x^T rows k, 16 consecutive test rows per
+  // 16 lanes = one 128-B segment) go from L2 straight into registers one
+  // k-step ahead (bn -> bc); only U is staged through LDS.
+  double bc[2][4], bn[2][4];
+  const double* ktw = PRE ? Kt + i0 + wave * 32 + (lane & 15) + (int64_t)(lane >> 4) * (nI * PI)
+                          : nullptr;
+#define BO_LOAD_B(K0, DST)                                                          \
+  _Pragma("unroll") for (int it = 0; it < 2; ++it)                                 \
+    _Pragma("unroll") for (int ks = 0; ks < 4; ++ks)                              \
+      DST[it][ks] = ktw[(int64_t)((K0) + 4 * ks) * (nI * PI) + it * 16];
   BO_LOAD_U(kbeg);
+  if (PRE) {
+    BO_LOAD_B(kbeg, bc);
+  } else {
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk)
-    kv[kk] = BO_KVAL(kbeg + kh * 8 + kk);
+    for (int kk = 0; kk < 8; ++kk)
+      kv[kk] = BO_KVAL(kbeg + kh * 8 + kk);
+  }
   BO_STORE(0);
   __syncthreads();
   // One k-step; XMFMA = the cross-term MFMAs (cross workgroups only: a
@@ -283,20 +299,27 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     const int knext = kbeg + (more ? (t + 1) * PK : t * PK);                         \
     XLOAD                                                                            \
     BO_LOAD_U(knext);                                                                \
+    if (PRE) { BO_LOAD_B(knext, bn); }                                               \
     _Pragma("unroll") for (int ks = 0; ks < PK / 4; ++ks) {                         \
       const int kr = ks * 4 + (lane >> 4);                                           \
       double a[8], b[2];                                                             \
       _Pragma("unroll") for (int ct = 0; ct < 8; ++ct) a[ct] = Us[cur][kr][ct * 16 + (lane & 15)]; \
       _Pragma("unroll") for (int it = 0; it < 2; ++it)                              \
-        b[it] = Ks[cur][kr][wave * 32 + it * 16 + (lane & 15)];                      \
+        b[it] = PRE ? bc[it][ks] : Ks[cur][kr][wave * 32 + it * 16 + (lane & 15)];   \
       _Pragma("unroll") for (int ct = 0; ct < 8; ++ct)                              \
         _Pragma("unroll") for (int it = 0; it < 2; ++it)                            \
           acc[ct][it] = mfma_f64(a[ct], b[it], acc[ct][it]);                         \
       XMFMA                                                                          \
-      kv[2 * ks] = BO_KVAL(knext + kh * 8 + 2 * ks);                                \
-      kv[2 * ks + 1] = BO_KVAL(knext + kh * 8 + 2 * ks + 1);                        \
+      if (!PRE) {                                                                    \
+        kv[2 * ks] = BO_KVAL(knext + kh * 8 + 2 * ks);                              \
+        kv[2 * ks + 1] = BO_KVAL(knext + kh * 8 + 2 * ks + 1);                      \
+      }                                                                              \
     }                                                                                \
     if (more) BO_STORE(cur ^ 1);                                                     \
+    if (PRE) {                                                                       \
+      _Pragma("unroll") for (int it = 0; it < 2; ++it)                              \
+        _Pragma("unroll") for (int ks = 0; ks < 4; ++ks) bc[it][ks] = bn[it][ks];   \
+    }                                                                                \
     __syncthreads();                                                                 \
   }
   int t = 0;
@@ -315,6 +338,7 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
 #undef BO_LOAD_U
 #undef BO_STORE
 #undef BO_LOAD_Q
+#undef BO_LOAD_B
   if (cross) {
     const int nrows_pad = nI * PI;
 #pragma unroll
