@@ -54,7 +54,7 @@ def flops_post_partials(B, q, n):
     return B * q * n * n + 2 * B * q * q * n + 2 * B * q * n
 
 
-def pmc_traffic(kernel="post_partials_kernel<0, 6, false, false, true>"):
+def pmc_traffic(kernel="post_partials_kernel<0, 6, false, false, true, false>"):
     """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 PMC
     summary (profiles/rNN/pmc_summary.json, written by tools/pmc_summary.py from
     separate --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command,
