@@ -125,7 +125,7 @@ def test_gemm_triangular_flags():
     torch.testing.assert_close(torch.triu(out, 1), torch.triu(C, 1))
 
 
-@pytest.mark.parametrize("n", [20, 128, 333, 1024])
+@pytest.mark.parametrize("n", [20, 128, 333, 1024, 2900])
 def test_cholesky_inverse_matches_torch(n):
     from botorch_amd import kernels
     g = torch.Generator().manual_seed(n)
