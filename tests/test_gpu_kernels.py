@@ -317,3 +317,27 @@ def test_post_partials_cross_term(n, B, q, rq):
     if kc:  # split-k plans fall back to R^T for the caller's GEMM
         sp = kernels.post_partials(c, Xc, cross=Qc)
         assert sp.Cx is None and sp.Rt is not None
+
+
+def test_posterior_full_c3_matches_oracle():
+    """The default C3 plan (n = 4096, 512 t-batches x q = 16: one pass, grouped
+    8 x 8 super-tile schedule, K*x^T B operands from L2) on all 512 t-batches,
+    checked against the oracle on t-batches from the first, middle and last
+    super-tiles, and against the path that evaluates K*x inside the kernel."""
+    from botorch_amd import _lib, kernels
+    X, Y, orc, h = _oracle_model(4096)
+    c = _device_cache(X, Y, h, orc)
+    g = torch.Generator().manual_seed(11)
+    Xc = torch.rand(512, 16, 6, generator=g, dtype=torch.float64)
+    kc, _ = kernels.split_plan(512, 16, 4096)
+    assert kc == 0
+    pp = kernels.post_partials(c, Xc.to(DEV))
+    out = kernels.qmc_finalize(c, pp, _lib.QMC_POSTERIOR, orc.ymean.item(), orc.ystd.item())
+    idx = torch.tensor([0, 1, 7, 8, 255, 256, 300, 504, 510, 511])
+    mr, cr = orc.posterior(Xc[idx])
+    torch.testing.assert_close(out["mean"].cpu()[idx], mr, rtol=1e-4, atol=1e-9)
+    torch.testing.assert_close(out["cov"].cpu()[idx], cr, rtol=1e-4, atol=1e-9)
+    pe = kernels.post_partials(c, Xc.to(DEV), kxt=False)
+    oe = kernels.qmc_finalize(c, pe, _lib.QMC_POSTERIOR, orc.ymean.item(), orc.ystd.item())
+    torch.testing.assert_close(out["mean"], oe["mean"], rtol=1e-11, atol=1e-12)
+    torch.testing.assert_close(out["cov"], oe["cov"], rtol=1e-9, atol=1e-12)
