@@ -101,7 +101,8 @@ def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout):
     os_ = x[2 + d] if layout.has_os else 1.0
     dev = Xt.device
     ls_t = torch.as_tensor(ls, dtype=torch.float64, device=dev)
-    cache = kernels.build_gp_cache(Xt, y, ls_t, noise, const, kind=model.kind, outputscale=os_)
+    cache = kernels.build_gp_cache(Xt, y, ls_t, noise, const, kind=model.kind, outputscale=os_,
+                                   check_nan=False)  # checked once in fit_gpytorch_mll_scipy
     # A^{-1} = U U^T: lower triangle only, triangular operands (n^3/3 flops).
     Ainv = torch.empty(cache.np, cache.np, dtype=torch.float64, device=dev)
     st = kernels._stream(dev)
@@ -136,6 +137,9 @@ def fit_gpytorch_mll_scipy(mll: ExactMarginalLogLikelihood, method="L-BFGS-B", o
     model = mll.model
     layout = _Layout(model)
     x0 = layout.get()
+    if torch.isnan(model.train_inputs[0]).any() or torch.isnan(model.train_targets).any():
+        from .exceptions import NanError
+        raise NanError("training data contains NaN")
 
     def f(x):
         return mll_value_and_grad(model, x, layout)

@@ -154,11 +154,15 @@ class GPCache:
 
 
 def build_gp_cache(Xt, y, lengthscale, noise, constant, kind=_lib.RBF, outputscale=1.0,
-                   max_tries=CHOLESKY_MAX_TRIES, jitter0=CHOLESKY_JITTER_F64) -> GPCache:
+                   max_tries=CHOLESKY_MAX_TRIES, jitter0=CHOLESKY_JITTER_F64,
+                   check_nan: bool = True) -> GPCache:
+    """``check_nan=False``: the caller has already checked Xt and y (the MLL
+    closure checks once per fit, not once per evaluation: each check is a
+    device-to-host sync)."""
     dev = _dev(Xt, y, lengthscale)
     Xt = Xt.contiguous()
     n, d = Xt.shape
-    if torch.isnan(Xt).any() or torch.isnan(y).any():
+    if check_nan and (torch.isnan(Xt).any() or torch.isnan(y).any()):
         from .exceptions import NanError
         raise NanError("training data contains NaN")
     np_ = padded_order(n)

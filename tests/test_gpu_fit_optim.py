@@ -200,3 +200,17 @@ def test_device_lbfgs_qei_reaches_scipy_values():
     assert (vd >= v0 - 1e-12).all()
     st = gen_candidates_device.last_state
     assert (st.nacc.cpu() > 0).any()
+
+
+def test_fit_rejects_nan_training_data():
+    """NaN inputs raise NanError once, before the first closure (the closure
+    itself skips the per-evaluation check)."""
+    from botorch_amd.exceptions import NanError
+    from botorch_amd.fit import ExactMarginalLogLikelihood, fit_gpytorch_mll_scipy
+    from botorch_amd.models import SingleTaskGP
+    X = torch.rand(40, 6, dtype=torch.float64)
+    Y = X.sum(dim=-1, keepdim=True)
+    m = SingleTaskGP(X.to(DEV), Y.to(DEV))
+    m.train_inputs[0][3, 2] = float("nan")
+    with pytest.raises(NanError):
+        fit_gpytorch_mll_scipy(ExactMarginalLogLikelihood(m.likelihood, m))
