@@ -14,6 +14,7 @@ the generic route (device posterior -> sampler -> torch reduction).
 """
 from __future__ import annotations
 
+import copy
 import math
 import warnings
 from typing import Callable, List, Optional, Union
@@ -22,10 +23,14 @@ import torch
 from torch import nn
 
 from . import _lib, kernels
-from .exceptions import BotorchError, BotorchWarning, UnsupportedError
+from .exceptions import BotorchError, BotorchWarning, NanError, NotPSDError, UnsupportedError
 from .safe_math import TAU_MAX, TAU_RELU, fatmax, log_improvement, logmeanexp, smooth_amax
+from .objective import (ConstrainedMCObjective, GenericMCObjective, IdentityMCObjective,
+                        MCAcquisitionObjective, MCObjective, compute_best_feasible_objective,
+                        compute_feasibility_indicator, compute_smoothed_feasibility_indicator,
+                        repeat_to_match_aug_dim)
 from .posteriors import FUSED_QMAX
-from .sampling import MCSampler, SobolQMCNormalSampler, get_sampler
+from .sampling import MCSampler, ShapeOnlyPosterior, SobolQMCNormalSampler, get_sampler
 
 
 # -- input handling (utils/transforms.py:146-336) -----------------------------
@@ -62,29 +67,34 @@ class AcquisitionFunction(nn.Module):
         return X
 
 
-class MCObjective:
-    pass
-
-
-class IdentityMCObjective(MCObjective):
-    """acquisition/objective.py:288-298."""
-
-    def __call__(self, samples, X=None):
-        return samples.squeeze(-1)
-
-
 class MCAcquisitionFunction(AcquisitionFunction):
+    """acquisition/acquisition.py:77-146 + SampleReducingMCAcquisitionFunction
+    (acquisition/monte_carlo.py:155-330): samples -> objective -> per-sample
+    utility -> constraint weighting -> q reduction -> sample reduction.
+
+    Subclasses run a fused gfx950 kernel chain when the configuration allows
+    (``_fused_eligible``) and otherwise this generic route, whose posterior,
+    root decomposition and base samples are still the device kernels."""
+
     _default_sample_shape = torch.Size([512])
+    _log = False
 
     def __init__(self, model, sampler: Optional[MCSampler] = None, objective=None,
-                 posterior_transform=None, X_pending=None):
+                 posterior_transform=None, X_pending=None, constraints=None, eta=1e-3,
+                 fat: bool = False):
         super().__init__(model)
+        if constraints is not None and isinstance(objective, ConstrainedMCObjective):
+            raise ValueError("ConstrainedMCObjective as well as constraints passed to constructor."
+                             "Choose one or the other, preferably the latter.")
         if objective is None and model.num_outputs != 1 and posterior_transform is None:
             raise UnsupportedError("Must specify an objective or a posterior transform when "
                                    "using a multi-output model.")
         self.sampler = sampler
         self.objective = objective if objective is not None else IdentityMCObjective()
         self.posterior_transform = posterior_transform
+        self._constraints = constraints
+        self._eta = eta
+        self._fat = fat
         self.set_X_pending(X_pending)
 
     @property
@@ -102,10 +112,44 @@ class MCAcquisitionFunction(AcquisitionFunction):
 
     def _fused_eligible(self, X: torch.Tensor) -> bool:
         m = self.model
-        return (hasattr(m, "prediction_cache") and isinstance(self.objective, IdentityMCObjective)
-                and self.posterior_transform is None and X.shape[-2] <= FUSED_QMAX
-                and X.shape[-1] <= kernels.DP and X.is_cuda
+        return (hasattr(m, "prediction_cache") and type(self.objective) is IdentityMCObjective
+                and self.posterior_transform is None and self._constraints is None
+                and X.shape[-2] <= FUSED_QMAX and X.shape[-1] <= kernels.DP and X.is_cuda
                 and len(self.sample_shape) == 1)
+
+    # -- generic route (monte_carlo.py:253-330) -----------------------------------------
+    def _sample_forward(self, obj: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def _q_reduction(self, acqval: torch.Tensor) -> torch.Tensor:
+        return acqval.amax(dim=-1)
+
+    def _sample_reduction(self, acqval: torch.Tensor) -> torch.Tensor:
+        return acqval.mean(dim=tuple(range(len(self.sample_shape))))
+
+    def _apply_constraints(self, acqval: torch.Tensor, samples: torch.Tensor) -> torch.Tensor:
+        """monte_carlo.py:305-330: weight (or, in log space, shift) the utility by
+        the smoothed feasibility indicator."""
+        if self._constraints is not None:
+            if not self._log and (acqval < 0).any():
+                raise ValueError("Constraint-weighting requires unconstrained "
+                                 "acquisition values to be non-negative.")
+            ind = compute_smoothed_feasibility_indicator(constraints=self._constraints,
+                                                         samples=samples, eta=self._eta,
+                                                         log=self._log, fat=self._fat)
+            acqval = acqval.add(ind) if self._log else acqval.mul(ind)
+        return acqval
+
+    def _get_samples_and_objectives(self, X: torch.Tensor):
+        posterior = self.model.posterior(X, posterior_transform=self.posterior_transform)
+        samples = self.get_posterior_samples(posterior)
+        return samples, self.objective(samples, X=X)
+
+    def _generic_forward(self, X: torch.Tensor) -> torch.Tensor:
+        samples, obj = self._get_samples_and_objectives(X)
+        samples = repeat_to_match_aug_dim(target_tensor=samples, reference_tensor=obj)
+        acqval = self._apply_constraints(self._sample_forward(obj), samples)
+        return _ensemble_mean(self.model, self._sample_reduction(self._q_reduction(acqval)))
 
 
 class _FusedMC(torch.autograd.Function):
@@ -147,14 +191,18 @@ def _ensemble_mean(model, acq: torch.Tensor) -> torch.Tensor:
 
 class qExpectedImprovement(MCAcquisitionFunction):
     """MC batch EI (acquisition/monte_carlo.py:332-414):
-    qEI(X) = E[max_j max(Y_j - best_f, 0)]."""
+    qEI(X) = E[max_j max(Y_j - best_f, 0)], optionally weighted by smoothed
+    outcome constraints (``constraints``, ``eta``)."""
 
     def __init__(self, model, best_f: Union[float, torch.Tensor], sampler=None, objective=None,
                  posterior_transform=None, X_pending=None, constraints=None, eta=1e-3):
-        super().__init__(model, sampler, objective, posterior_transform, X_pending)
-        if constraints is not None:
-            raise UnsupportedError("outcome constraints are not on the accelerated path")
+        super().__init__(model, sampler, objective, posterior_transform, X_pending,
+                         constraints=constraints, eta=eta)
         self.register_buffer("best_f", torch.as_tensor(best_f, dtype=torch.float64))
+
+    def _sample_forward(self, obj: torch.Tensor) -> torch.Tensor:
+        """monte_carlo.py:405-414."""
+        return (obj - self.best_f.unsqueeze(-1).to(obj)).clamp_min(0)
 
     def forward(self, X: torch.Tensor) -> torch.Tensor:
         X = self._concat_pending(t_batch_mode(X))
@@ -166,18 +214,14 @@ class qExpectedImprovement(MCAcquisitionFunction):
             Z = sampler.base_samples_2d(q, X.device)
             acq = _FusedMC.apply(X3, self, _lib.QMC_QEI, float(self.best_f), None, Z)
             return acq.reshape(batch)
-        if (getattr(self.model, "_is_fully_bayesian", False) and X.is_cuda
-                and isinstance(self.objective, IdentityMCObjective) and self.posterior_transform is None
-                and len(self.sample_shape) == 1 and self.best_f.numel() == 1 and q <= FUSED_QMAX):
+        if (getattr(self.model, "_is_fully_bayesian", False) and X.is_cuda and not self._log
+                and type(self.objective) is IdentityMCObjective and self.posterior_transform is None
+                and self._constraints is None and len(self.sample_shape) == 1
+                and self.best_f.numel() == 1 and q <= FUSED_QMAX):
             sampler = self._ensure_sampler()
             Z = sampler.base_samples_2d(q, X.device)
             return _SaasQEI.apply(X3, self, float(self.best_f), Z).reshape(batch)
-        posterior = self.model.posterior(X, posterior_transform=self.posterior_transform)
-        samples = self.get_posterior_samples(posterior)
-        obj = self.objective(samples, X=X)
-        bf = self.best_f.to(obj).unsqueeze(-1)
-        acq = (obj - bf).clamp_min(0).amax(dim=-1).mean(dim=0)
-        return _ensemble_mean(self.model, acq)
+        return self._generic_forward(X)
 
 
 class _SaasQEI(torch.autograd.Function):
@@ -331,31 +375,96 @@ class UpperConfidenceBound(AnalyticAcquisitionFunction):
 def prune_inferior_points(model, X, objective=None, posterior_transform=None, constraints=None,
                           num_samples: int = 2048, max_frac: float = 1.0, sampler=None,
                           marginalize_dim=None):
-    """acquisition/utils.py:245-349 (unconstrained): keep the points with non-zero
-    empirical probability of being the best under `num_samples` joint posterior
-    samples.  The joint n x n posterior, its jittered Cholesky and the sample GEMM
-    run on the device."""
+    """acquisition/utils.py:245-349: keep the points with non-zero empirical
+    probability of being the best (feasible) point under ``num_samples`` joint
+    posterior samples.  The joint n x n posterior, its jittered Cholesky and the
+    sample GEMM run on the device."""
+    if marginalize_dim is None and getattr(model, "_is_ensemble", False):
+        marginalize_dim = MCMC_DIM
     if X.ndim > 2:
         raise UnsupportedError("Batched inputs `X` are currently unsupported by prune_inferior_points")
     if X.size(-2) == 0:
         raise ValueError("X must have at least one point.")
     if max_frac <= 0 or max_frac > 1.0:
         raise ValueError(f"max_frac must take values in (0, 1], is {max_frac}")
-    if constraints is not None:
-        raise UnsupportedError("constraints are not on the accelerated path")
     max_points = math.ceil(max_frac * X.size(-2))
     with torch.no_grad():
         posterior = model.posterior(X=X, posterior_transform=posterior_transform)
         if sampler is None:
             sampler = get_sampler(posterior, sample_shape=torch.Size([num_samples]))
         samples = sampler(posterior)
-        obj = (objective or IdentityMCObjective())(samples, X=X)
-    is_best = torch.argmax(obj, dim=-1)
+        if objective is None:
+            objective = IdentityMCObjective()
+        obj_vals = objective(samples, X=X)
+    if obj_vals.ndim > 2:
+        if obj_vals.ndim == 3 and marginalize_dim is not None:
+            if marginalize_dim < 0:
+                marginalize_dim = 1 + (marginalize_dim % obj_vals.ndim)
+            obj_vals = obj_vals.mean(dim=marginalize_dim)
+        else:
+            raise UnsupportedError("Models with multiple batch dims are currently unsupported by"
+                                   " prune_inferior_points.")
+    infeas = ~compute_feasibility_indicator(constraints=constraints, samples=samples,
+                                            marginalize_dim=marginalize_dim)
+    if infeas.any():
+        obj_vals[infeas] = obj_vals.min() - 1
+    is_best = torch.argmax(obj_vals, dim=-1)
     idcs, counts = torch.unique(is_best, return_counts=True)
     if len(idcs) > max_points:
         counts, order_idcs = torch.sort(counts, descending=True)
         idcs = order_idcs[:max_points]  # reference quirk kept (utils.py:345-347)
     return X[idcs]
+
+
+MCMC_DIM = -3  # models/fully_bayesian.py
+
+
+def supports_cache_root(model, posterior_transform=None) -> bool:
+    """acquisition/cached_cholesky.py:34-51, for the models built here: exact
+    GPs (SingleTaskGP, the SAAS ensemble) with a linear (Standardize) outcome
+    transform.  A ModelListGP is cached here only under a scalarising posterior
+    transform (its joint root is then single-output); without one the full
+    joint samples are drawn instead."""
+    if hasattr(model, "models"):
+        return posterior_transform is not None and all(supports_cache_root(m) for m in model.models)
+    return hasattr(model, "prediction_cache") or getattr(model, "_is_fully_bayesian", False)
+
+
+def sample_cached_cholesky(posterior, baseline_L: torch.Tensor, q: int, base_samples: torch.Tensor,
+                           sample_shape: torch.Size, max_tries: int = 6) -> torch.Tensor:
+    """utils/low_rank.py:85-173 for a single-output joint posterior over
+    (X_baseline, X): the q new rows of the joint Cholesky from the cached
+    baseline root (bl = K_qb L_bb^{-T}, br = psd_safe_cholesky(K_qq - bl bl^T)),
+    then samples = mean_q + [bl, br] Z (Z the joint base samples).  Raises
+    NanError on non-finite samples."""
+    from .exceptions import NanError
+    from .posteriors import _CholJitter
+    mvn = posterior.distribution
+    cov = mvn.covariance_matrix
+    bottom = cov[..., -q:, :]
+    bl, br = bottom.split([bottom.shape[-1] - q, q], dim=-1)
+    bl_chol = torch.linalg.solve_triangular(baseline_L.to(bl), bl.transpose(-2, -1),
+                                            upper=False).transpose(-2, -1)
+    br_to_chol = br - bl_chol @ bl_chol.transpose(-2, -1)
+    if torch.is_grad_enabled() and br_to_chol.requires_grad:
+        br_chol = _CholJitter.apply(br_to_chol)
+    else:
+        br_chol = kernels.chol_jitter(br_to_chol, max_tries=max_tries)
+    new_Lq = torch.cat([bl_chol, br_chol], dim=-1)                     # batch x q x (r + q)
+    mean = mvn.mean[..., -q:]                                          # batch x q
+    n_tot = new_Lq.shape[-1]
+    Z = base_samples.reshape(*sample_shape, -1, n_tot)
+    if Z.shape[len(sample_shape)] != 1:
+        raise UnsupportedError("sample_cached_cholesky here takes base samples shared over t-batches")
+    Z = Z.reshape(-1, n_tot).to(new_Lq)                               # S' x (r + q)
+    f = torch.matmul(Z, new_Lq.reshape(-1, q, n_tot).mT)              # B' x S' x q
+    f = f.permute(1, 0, 2) + mean.reshape(1, -1, q)
+    res = f.reshape(*sample_shape, *mean.shape[:-1], q, 1)
+    bad_nan, bad_inf = bool(torch.isnan(res).any()), bool(torch.isinf(res).any())
+    if bad_nan or bad_inf:
+        what = " and ".join(w for w, b in (("nans", bad_nan), ("infs", bad_inf)) if b)
+        raise NanError(f"Samples contain {what}.")
+    return res
 
 
 class _CachedBaselineRoot:
@@ -427,64 +536,201 @@ class _CachedBaselineRoot:
 
 
 class qNoisyExpectedImprovement(MCAcquisitionFunction):
-    """MC batch noisy EI with the cached baseline root (acquisition/monte_carlo.py:
-    417-645, cached_cholesky.py:63-186, utils/low_rank.py:85-173):
+    """MC batch noisy EI (acquisition/monte_carlo.py:417-645, cached_cholesky.py:
+    63-186, utils/low_rank.py:85-173):
     qNEI(X) = E[max(max_j Y_j - max_i Y_base_i, 0)].
 
-    Construction (once): optional pruning of X_baseline, the baseline posterior,
-    its jittered Cholesky L_rr (with inverse), the baseline samples and their
-    per-sample best, and the device precomputations of the fused forward:
-    P_b = L_rr^{-1} K(X_b, X_tr) L^{-T} (r x n) and the scaled baseline inputs.
-    Forward (fused): post_partials (+ R^T), T = L_rr^{-1} Sigma'(X_b, X) as two
-    MFMA GEMMs (T = s^2 (L_rr^{-1} K_bX - P_b R^T)), the baseline sample term
-    F = Z_b T (one GEMM), then qmc_finalize in qNEI mode.
+    ``cache_root=True`` (default): the baseline posterior, its jittered root
+    L_rr and the baseline samples are computed once; ``base_sampler`` keeps the
+    baseline base samples and every forward reuses them as the leading columns
+    of the joint (r + q) draw (sampling/normal.py:68-131).  For a SingleTaskGP
+    with the identity objective, q <= 16 and d <= 8 the forward is the fused
+    chain (post_partials with the cross term, T = L_rr^{-1} Sigma'(X_b, X),
+    F = Z_b T, qmc_finalize(QNEI)); otherwise the joint posterior over
+    (X_baseline, X) goes through sample_cached_cholesky.  A NotPSD/NaN failure
+    of either falls back to standard joint sampling with a BotorchWarning
+    (cached_cholesky.py:141-165).  ``cache_root=False``: every forward samples
+    the joint (r + q) posterior and takes the baseline best from those samples.
     """
+
+    _fused_mode = _lib.QMC_QNEI
 
     def __init__(self, model, X_baseline, sampler=None, objective=None, posterior_transform=None,
                  X_pending=None, prune_baseline=True, cache_root=True, constraints=None,
                  eta=1e-3, marginalize_dim=None):
-        super().__init__(model, sampler, objective, posterior_transform, X_pending)
-        if constraints is not None:
-            raise UnsupportedError("outcome constraints are not on the accelerated path")
-        if prune_baseline:
-            X_baseline = prune_inferior_points(model, X_baseline, objective=objective,
-                                               posterior_transform=posterior_transform)
-        self.register_buffer("X_baseline", X_baseline)
-        self._cache_root = cache_root
-        sampler = self._ensure_sampler()
-        S = sampler.sample_shape.numel()
-        r = X_baseline.shape[-2]
-        Z_base = kernels.sobol_normal(r, S, sampler.seed, X_baseline.device)
-        self._root = _CachedBaselineRoot(model, X_baseline, Z_base, posterior_transform)
-        self.Z_base = Z_base
-        self.baseline_samples = self._root.samples
-        self.register_buffer("_baseline_best_f", self.baseline_samples.amax(dim=-1).contiguous())
-        self._baseline_L = self._root.L
-        self._Linv_rr = self._root.Linv
-        self._fused_ready = self._root.fused_ready
-        self._zq = {}
+        super().__init__(model, sampler, objective, posterior_transform, X_pending,
+                         constraints=constraints, eta=eta)
+        self._init_baseline(model, X_baseline, prune_baseline, cache_root, marginalize_dim)
 
-    _fused_mode = _lib.QMC_QNEI
+    def _init_baseline(self, model, X_baseline, prune_baseline, cache_root, marginalize_dim):
+        if cache_root and not supports_cache_root(model, self.posterior_transform):
+            warnings.warn("`cache_root` is only supported here for exact GPs (or a ModelListGP "
+                          f"under a scalarising posterior transform); got {type(model)}. "
+                          "Setting `cache_root = False`.", RuntimeWarning)
+            cache_root = False
+        self._cache_root = cache_root
+        if prune_baseline:
+            X_baseline = prune_inferior_points(model, X_baseline, objective=self.objective,
+                                               posterior_transform=self.posterior_transform,
+                                               constraints=self._constraints,
+                                               marginalize_dim=marginalize_dim)
+        self.register_buffer("X_baseline", X_baseline)
+        self.baseline_samples = None
+        self.baseline_obj = None
+        self.base_sampler = None
+        self._root = None
+        self._zq = None
+        if not self._cache_root:
+            return
+        self.q_in = -1
+        r = X_baseline.shape[-2]
+        fusable = (hasattr(model, "prediction_cache") and type(self.objective) is IdentityMCObjective
+                   and self.posterior_transform is None and self._constraints is None
+                   and X_baseline.ndim == 2 and X_baseline.shape[-1] <= kernels.DP
+                   and X_baseline.is_cuda and len(self.sample_shape) == 1)
+        with torch.no_grad():
+            if fusable:
+                # the sampler's own base samples over X_baseline (S x r), then the
+                # device root + fused precomputations on them
+                sampler = self._ensure_sampler()
+                sampler._construct_base_samples(ShapeOnlyPosterior(torch.Size(), r, X_baseline.device))
+                Z_base = sampler.base_samples.reshape(-1, r).contiguous()
+                self._root = _CachedBaselineRoot(model, X_baseline, Z_base)
+                baseline_samples = self._root.samples.reshape(*self.sample_shape, r, 1)
+                baseline_L = self._root.L
+            else:
+                posterior = self.model.posterior(X_baseline, posterior_transform=self.posterior_transform)
+                baseline_samples = self.get_posterior_samples(posterior)
+                baseline_L = posterior.distribution.scale_tril
+            baseline_obj = self.objective(baseline_samples, X=X_baseline)
+        self.base_sampler = copy.deepcopy(self.sampler)
+        self.baseline_samples = baseline_samples
+        self.baseline_obj = baseline_obj
+        self.register_buffer("_baseline_best_f", self._compute_best_feasible_objective(
+            samples=baseline_samples, obj=baseline_obj).contiguous())
+        self._baseline_L_t = baseline_L
+
+    @property
+    def _baseline_L(self) -> torch.Tensor:
+        return self._baseline_L_t
+
+    @_baseline_L.setter
+    def _baseline_L(self, L: torch.Tensor) -> None:
+        # a replaced root invalidates the fused precomputations built on the old one
+        self._baseline_L_t = L
+        self._root = None
+
+    @property
+    def _fused_ready(self) -> bool:
+        return self._root is not None and self._root.fused_ready
+
+    def _compute_best_feasible_objective(self, samples, obj):
+        """monte_carlo.py:628-645."""
+        return compute_best_feasible_objective(samples=samples, obj=obj,
+                                               constraints=self._constraints, model=self.model,
+                                               objective=self.objective,
+                                               posterior_transform=self.posterior_transform,
+                                               X_baseline=self.X_baseline)
+
+    def compute_best_f(self, obj: torch.Tensor) -> torch.Tensor:
+        """monte_carlo.py:540-563: the (cached or per-forward) best feasible
+        baseline objective, viewed against obj without its q dimension."""
+        if self._cache_root:
+            val = self._baseline_best_f
+        else:
+            val = self._compute_best_feasible_objective(samples=self.baseline_samples,
+                                                        obj=self.baseline_obj)
+        n_sample_dims = len(self.sample_shape)
+        view_shape = torch.Size([*val.shape[:n_sample_dims],
+                                 *(1,) * (obj.ndim - val.ndim - 1),
+                                 *val.shape[n_sample_dims:]])
+        return val.view(view_shape).to(obj)
+
+    def _sample_forward(self, obj: torch.Tensor) -> torch.Tensor:
+        """monte_carlo.py:565-575."""
+        return (obj - self.compute_best_f(obj).unsqueeze(-1)).clamp_min(0)
+
+    # -- joint base samples (cached_cholesky.py:167-186) ----------------------------------
+    def _set_sampler(self, q_in: int, posterior) -> None:
+        if self.q_in != q_in and self.base_sampler is not None:
+            self.sampler._update_base_samples(posterior=posterior, base_sampler=self.base_sampler)
+            self.q_in = q_in
+            self._zq = None
 
     def _base_samples_q(self, q: int, device) -> torch.Tensor:
-        """The q new columns of the (r+q)-dim Sobol draw (sampling/normal.py:68-131)."""
-        if q not in self._zq:
-            r = self.X_baseline.shape[-2]
-            S = self.sampler.sample_shape.numel()
-            full = kernels.sobol_normal(r + q, S, self.sampler.seed, device)
-            self._zq[q] = full[:, r:].contiguous()
-        return self._zq[q]
+        """The q new columns of the joint (r + q) base samples (S x q) for the
+        fused path; the leading r columns are the cached baseline ones."""
+        r = self.X_baseline.shape[-2]
+        S = self.sample_shape.numel()
+        bs = self.sampler.base_samples
+        if self.q_in != q or bs is None or bs.numel() != S * (r + q):
+            self.q_in = -1
+            self._set_sampler(q, ShapeOnlyPosterior(torch.Size([1]), r + q, device))
+            bs = self.sampler.base_samples
+        key = (q, bs.data_ptr(), bs._version)
+        if self._zq is None or self._zq[0] != key:
+            self._zq = (key, bs.reshape(S, r + q)[:, r:].contiguous())
+        return self._zq[1]
+
+    def _get_f_X_samples(self, posterior, q_in: int) -> torch.Tensor:
+        """cached_cholesky.py:122-165."""
+        if self._cache_root and self._baseline_L is not None:
+            try:
+                return sample_cached_cholesky(posterior=posterior, baseline_L=self._baseline_L,
+                                              q=q_in, base_samples=self.sampler.base_samples,
+                                              sample_shape=self.sampler.sample_shape)
+            except (NanError, NotPSDError):
+                warnings.warn("Low-rank cholesky updates failed due NaNs or due to an "
+                              "ill-conditioned covariance matrix. Falling back to standard "
+                              "sampling.", BotorchWarning)
+        samples = self.get_posterior_samples(posterior)
+        return samples[..., -q_in:, :]
+
+    def _joint_posterior(self, X: torch.Tensor):
+        Xb = self.X_baseline
+        X_full = torch.cat([Xb.expand(*X.shape[:-2], *Xb.shape[-2:]), X], dim=-2)
+        return X_full, self.model.posterior(X_full, posterior_transform=self.posterior_transform)
+
+    def _get_samples_and_objectives(self, X: torch.Tensor):
+        """monte_carlo.py:577-626."""
+        q = X.shape[-2]
+        X_full, posterior = self._joint_posterior(X)
+        if not self._cache_root:
+            samples_full = self.get_posterior_samples(posterior)
+            samples = samples_full[..., -q:, :]
+            obj_full = self.objective(samples_full, X=X_full)
+            self.baseline_obj, obj = obj_full[..., :-q], obj_full[..., -q:]
+            self.baseline_samples = samples_full[..., :-q, :]
+        else:
+            self._set_sampler(q_in=q, posterior=posterior)
+            samples = self._get_f_X_samples(posterior=posterior, q_in=q)
+            obj = self.objective(samples, X=X_full[..., -q:, :])
+        return samples, obj
+
+    def _fallback_forward(self, X: torch.Tensor) -> torch.Tensor:
+        """Standard joint sampling after a failed low-rank update of the fused path
+        (cached_cholesky.py:147-165): the cached baseline best is kept."""
+        q = X.shape[-2]
+        X_full, posterior = self._joint_posterior(X)
+        self._set_sampler(q_in=q, posterior=posterior)
+        samples = self.get_posterior_samples(posterior)[..., -q:, :]
+        obj = self.objective(samples, X=X)
+        acqval = self._apply_constraints(self._sample_forward(obj), samples)
+        return _ensemble_mean(self.model, self._sample_reduction(self._q_reduction(acqval)))
 
     def forward(self, X: torch.Tensor) -> torch.Tensor:
         X = self._concat_pending(t_batch_mode(X))
         batch = X.shape[:-2]
         q, d = X.shape[-2], X.shape[-1]
-        X3 = X.reshape(-1, q, d)
-        if not (self._fused_eligible(X) and self._fused_ready):
-            raise UnsupportedError(
-                f"qNEI here needs the fused path (q <= {FUSED_QMAX}, d <= {kernels.DP}, identity objective)")
-        acq = _FusedQNEI.apply(X3, self)
-        return acq.reshape(batch)
+        if self._fused_ready and self._fused_eligible(X):
+            try:
+                return _FusedQNEI.apply(X.reshape(-1, q, d), self).reshape(batch)
+            except (NotPSDError, NanError):
+                warnings.warn("Low-rank cholesky updates failed due NaNs or due to an "
+                              "ill-conditioned covariance matrix. Falling back to standard "
+                              "sampling.", BotorchWarning)
+                return self._fallback_forward(X)
+        return self._generic_forward(X)
 
 
 class _FusedQNEI(torch.autograd.Function):
@@ -543,10 +789,11 @@ def _check_tau(tau, name: str):
 
 
 class qLogExpectedImprovement(qExpectedImprovement):
-    """MC batch log expected improvement (acquisition/logei.py:137-234):
+    """MC batch log expected improvement (acquisition/logei.py:71-234):
     qLogEI(X) = logmeanexp_s q_reduce_j log_soft_clamp(Y_sj - best_f), with
     q_reduce = fatmax(tau_max) and log_soft_clamp = log_fatplus(tau_relu) when
-    fat (default), else smooth_amax / log_softplus.
+    fat (default), else smooth_amax / log_softplus; constraints add the
+    log-feasibility (fatmoid when fat).
 
     Fused path: bo_qmc_finalize in BO_QMC_QLOGEI mode (the same post_partials
     posterior and q x q root as qEI; only the per-sample reduction differs),
@@ -564,38 +811,35 @@ class qLogExpectedImprovement(qExpectedImprovement):
         self._fat = fat
         self._log_params = (int(bool(fat)), float(tau_relu), float(tau_max))
 
-    def _reduce(self, obj: torch.Tensor, best_f: torch.Tensor) -> torch.Tensor:
-        """sample x batch x q objective -> batch (SampleReducingMCAcquisitionFunction.
-        forward, monte_carlo.py:253-289, with the LogEI reductions)."""
-        li = log_improvement(obj, best_f, tau=self.tau_relu, fat=self._fat)
-        q_red = fatmax if self._fat else smooth_amax
-        return logmeanexp(q_red(li, dim=-1, tau=self.tau_max), dim=0)
+    def _sample_forward(self, obj: torch.Tensor) -> torch.Tensor:
+        """logei.py:219-234."""
+        return log_improvement(obj, self.best_f, tau=self.tau_relu, fat=self._fat)
+
+    def _q_reduction(self, acqval: torch.Tensor) -> torch.Tensor:
+        return (fatmax if self._fat else smooth_amax)(acqval, dim=-1, tau=self.tau_max)
+
+    def _sample_reduction(self, acqval: torch.Tensor) -> torch.Tensor:
+        return logmeanexp(acqval, dim=tuple(range(len(self.sample_shape))))
 
     def forward(self, X: torch.Tensor) -> torch.Tensor:
         X = self._concat_pending(t_batch_mode(X))
         batch = X.shape[:-2]
         q, d = X.shape[-2], X.shape[-1]
-        X3 = X.reshape(-1, q, d)
         if self._fused_eligible(X) and self.best_f.numel() == 1:
             sampler = self._ensure_sampler()
             Z = sampler.base_samples_2d(q, X.device)
-            acq = _FusedMC.apply(X3, self, _lib.QMC_QLOGEI, float(self.best_f), None, Z)
+            acq = _FusedMC.apply(X.reshape(-1, q, d), self, _lib.QMC_QLOGEI, float(self.best_f),
+                                 None, Z)
             return acq.reshape(batch)
-        posterior = self.model.posterior(X, posterior_transform=self.posterior_transform)
-        samples = self.get_posterior_samples(posterior)
-        obj = self.objective(samples, X=X)
-        bf = self.best_f.to(obj).expand(obj.shape[:-1]) if self.best_f.numel() == 1 else self.best_f.to(obj)
-        acq = self._reduce(obj, bf)
-        return _ensemble_mean(self.model, acq)
+        return self._generic_forward(X)
 
 
 class qLogNoisyExpectedImprovement(qNoisyExpectedImprovement):
-    """MC batch log noisy expected improvement with the cached baseline root
-    (acquisition/logei.py:236-507): the qNEI samples (cached_cholesky.py,
-    utils/low_rank.py:85-173) under the LogEI reductions against the per-sample
-    baseline best.  Unlike qNEI, ``prune_baseline`` defaults to False
-    (logei.py:270).  Fused path: bo_qmc_finalize / bo_qmc_backward in
-    BO_QMC_QLOGNEI mode."""
+    """MC batch log noisy expected improvement (acquisition/logei.py:236-507):
+    the qNEI samples (cached root or full joint, as qNoisyExpectedImprovement)
+    under the LogEI reductions against the per-sample baseline best.  Unlike
+    qNEI, ``prune_baseline`` defaults to False (logei.py:270).  Fused path:
+    bo_qmc_finalize / bo_qmc_backward in BO_QMC_QLOGNEI mode."""
 
     _log = True
     _fused_mode = _lib.QMC_QLOGNEI
@@ -604,20 +848,22 @@ class qLogNoisyExpectedImprovement(qNoisyExpectedImprovement):
                  X_pending=None, constraints=None, eta=1e-3, fat: bool = True,
                  prune_baseline: bool = False, cache_root: bool = True,
                  tau_max: float = TAU_MAX, tau_relu: float = TAU_RELU, marginalize_dim=None):
-        if not cache_root:
-            raise UnsupportedError("qLogNEI here runs with the cached baseline root (cache_root=True)")
-        super().__init__(model, X_baseline, sampler=sampler, objective=objective,
-                         posterior_transform=posterior_transform, X_pending=X_pending,
-                         prune_baseline=prune_baseline, cache_root=cache_root,
-                         constraints=constraints, eta=eta, marginalize_dim=marginalize_dim)
+        MCAcquisitionFunction.__init__(self, model, sampler, objective, posterior_transform,
+                                       X_pending, constraints=constraints, eta=eta, fat=fat)
         self.tau_max = _check_tau(tau_max, "tau_max")
         self.tau_relu = _check_tau(tau_relu, "tau_relu")
-        self._fat = fat
         self._log_params = (int(bool(fat)), float(tau_relu), float(tau_max))
+        self._init_baseline(model, X_baseline, prune_baseline, cache_root, marginalize_dim)
 
-    def compute_best_f(self, obj: torch.Tensor) -> torch.Tensor:
-        """logei.py:422-446: the cached per-sample baseline best."""
-        return self._baseline_best_f.view(-1, *([1] * (obj.ndim - 2))).to(obj)
+    def _sample_forward(self, obj: torch.Tensor) -> torch.Tensor:
+        """logei.py:347-362."""
+        return log_improvement(obj, self.compute_best_f(obj), tau=self.tau_relu, fat=self._fat)
+
+    def _q_reduction(self, acqval: torch.Tensor) -> torch.Tensor:
+        return (fatmax if self._fat else smooth_amax)(acqval, dim=-1, tau=self.tau_max)
+
+    def _sample_reduction(self, acqval: torch.Tensor) -> torch.Tensor:
+        return logmeanexp(acqval, dim=tuple(range(len(self.sample_shape))))
 
 
 # -- qEHVI ---------------------------------------------------------------------------
@@ -669,7 +915,7 @@ class _FusedQEHVI(torch.autograd.Function):
 class IdentityMCMultiOutputObjective(MCObjective):
     """acquisition/multi_objective/objective.py (identity over outputs)."""
 
-    def __call__(self, samples, X=None):
+    def forward(self, samples, X=None):
         return samples
 
 

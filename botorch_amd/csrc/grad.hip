@@ -107,6 +107,63 @@ __global__ __launch_bounds__(THREADS) void chol_backward_kernel(int q, const dou
   chol_backward_lds(q, L, dL, Li, Pm, Tm, dA + (int64_t)b * q * q, tid);
 }
 
+// Batched Cholesky backward for 16 < q <= 64 (the joint (r+q) roots of the
+// generic qNEI route and the q x q roots of large q-batches): the same algebra
+// as chol_backward_lds with element loops over q x q and four 64 x 65 LDS
+// planes (133 KB of gfx950's 160 KB); dL is read straight from global memory.
+constexpr int QBIG = 64;
+__global__ __launch_bounds__(THREADS) void chol_backward_big_kernel(
+    int q, const double* __restrict__ Lg, const double* __restrict__ dLg, double* __restrict__ dA) {
+  __shared__ double L[QBIG][QBIG + 1];
+  __shared__ double Li[QBIG][QBIG + 1];
+  __shared__ double Pm[QBIG][QBIG + 1];
+  __shared__ double Tm[QBIG][QBIG + 1];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int qq = q * q;
+  const double* Lb = Lg + (int64_t)b * qq;
+  const double* dLb = dLg + (int64_t)b * qq;
+  for (int e = tid; e < qq; e += THREADS) L[e / q][e % q] = Lb[e];
+  __syncthreads();
+  // L^{-1}: one column per thread (forward substitution)
+  for (int c = tid; c < q; c += THREADS) {
+    for (int r = 0; r < q; ++r) {
+      double s = (r == c) ? 1.0 : 0.0;
+      for (int k = c; k < r; ++k) s = fma(-L[r][k], Li[k][c], s);
+      Li[r][c] = (r >= c) ? s / L[r][r] : 0.0;
+    }
+  }
+  // X = tril(L^T tril(dL))
+  for (int e = tid; e < qq; e += THREADS) {
+    const int i = e / q, j = e % q;
+    if (i >= j) {
+      double x = 0.0;
+      for (int k = i; k < q; ++k) x = fma(L[k][i], dLb[k * q + j], x);
+      Tm[i][j] = x;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < qq; e += THREADS) {
+    const int i = e / q, j = e % q;
+    Pm[i][j] = 0.5 * ((i >= j) ? Tm[i][j] : Tm[j][i]);
+  }
+  __syncthreads();
+  for (int e = tid; e < qq; e += THREADS) {  // T = P L^{-1}
+    const int i = e / q, j = e % q;
+    double x = 0.0;
+    for (int k = j; k < q; ++k) x = fma(Pm[i][k], Li[k][j], x);
+    Tm[i][j] = x;
+  }
+  __syncthreads();
+  double* out = dA + (int64_t)b * qq;
+  for (int e = tid; e < qq; e += THREADS) {  // gA = L^{-T} T
+    const int i = e / q, j = e % q;
+    double x = 0.0;
+    for (int k = i; k < q; ++k) x = fma(Li[k][i], Tm[k][j], x);
+    out[e] = x;
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
     int q, const double* __restrict__ mean, const double* __restrict__ Lq,
@@ -525,9 +582,12 @@ extern "C" int bo_qmc_backward(int mode, int B, int q, const double* mean, const
 
 extern "C" int bo_chol_backward(int B, int q, const double* L, const double* dL, double* dA,
                                 void* stream) {
-  BO_CHECK_ARG(q >= 1 && q <= QMAX, "bo_chol_backward: q=%d out of range", q);
+  BO_CHECK_ARG(q >= 1 && q <= QBIG, "bo_chol_backward: q=%d out of range (1..64)", q);
   if (B == 0) return BO_OK;
-  chol_backward_kernel<<<B, THREADS, 0, as_stream(stream)>>>(q, L, dL, dA);
+  if (q <= QMAX)
+    chol_backward_kernel<<<B, THREADS, 0, as_stream(stream)>>>(q, L, dL, dA);
+  else
+    chol_backward_big_kernel<<<B, THREADS, 0, as_stream(stream)>>>(q, L, dL, dA);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

@@ -461,21 +461,22 @@ class SaasFullyBayesianSingleTaskGP(Model):
 
     def posterior(self, X, output_indices=None, observation_noise=False, posterior_transform=None):
         """models/fully_bayesian.py:509-546 -> GaussianMixturePosterior (batch b x M)."""
-        from . import kernels
-        from .posteriors import GPyTorchPosterior, MultivariateNormal
+        from .posteriors import GPyTorchPosterior, MultivariateNormal, posterior_moments
         M = self.num_mcmc_samples
         batch, q, d = X.shape[:-2], X.shape[-2], X.shape[-1]
         X3 = X.reshape(-1, q, d)
         means, covs = [], []
         for mdl in self._members:
-            mu, cov = kernels.posterior_general(mdl, X3)
+            mu, cov = posterior_moments(mdl, X3)  # differentiable (generic kernels at d > 8)
+            if observation_noise is True:
+                # noise joins in the model's (standardised) space, before the
+                # outcome untransform (models/gpytorch.py:446-466)
+                cov = cov + mdl.likelihood.noise.reshape(()) * torch.eye(q, dtype=cov.dtype, device=cov.device)
             if hasattr(self, "outcome_transform"):
                 tf = self.outcome_transform
                 s = float(tf.stdvs.reshape(-1)[0])
                 mu = float(tf.means.reshape(-1)[0]) + s * mu
                 cov = cov * (s * s)
-            if observation_noise is True:
-                cov = cov + mdl.likelihood.noise.reshape(()) * torch.eye(q, dtype=cov.dtype, device=cov.device)
             means.append(mu)
             covs.append(cov)
         mean = torch.stack(means, dim=1).reshape(*batch, M, q)

@@ -97,3 +97,35 @@ def log_improvement(Y: torch.Tensor, best_f: torch.Tensor, tau, fat: bool) -> to
     best_f broadcasts against Y without its q dimension."""
     log_soft_clamp = log_fatplus if fat else log_softplus
     return log_soft_clamp(Y - best_f.unsqueeze(-1).to(Y), tau=tau)
+
+
+def log1pexp(x: torch.Tensor) -> torch.Tensor:
+    """safe_math.py:84-94: log(1 + exp(x)), switching form above x = 18."""
+    mask = x <= 18
+    return torch.where(mask, x.masked_fill(~mask, 0).exp().log1p(),
+                       (lambda z: z + (-z).exp())(x.masked_fill(mask, 0)))
+
+
+def logexpit(X: torch.Tensor) -> torch.Tensor:
+    """safe_math.py:97-99: log of the logistic sigmoid."""
+    return -log1pexp(-X)
+
+
+_INV_SQRT_3 = math.sqrt(1 / 3)
+
+
+def cauchy(x: torch.Tensor) -> torch.Tensor:
+    """safe_math.py:449-451: un-normalised Cauchy density."""
+    return 1 / (1 + x.square())
+
+
+def fatmoid(X: torch.Tensor, tau=1.0) -> torch.Tensor:
+    """safe_math.py:429-446: fat-tailed smooth Heaviside (inflection at 1/sqrt 3)."""
+    X = X / tau
+    m = _INV_SQRT_3
+    return torch.where(X < 0, 2 / 3 * cauchy(X - m), 1 - 2 / 3 * cauchy(X + m))
+
+
+def log_fatmoid(X: torch.Tensor, tau=1.0) -> torch.Tensor:
+    """safe_math.py:422-426."""
+    return fatmoid(X, tau=tau).log()

@@ -341,7 +341,7 @@ int bo_qehvi_backward(int B, int q, int m, const double* mean, const double* L, 
                       const double* dacq, double* dmean, double* dL, double* dF, void* stream);
 
 /* Batched Cholesky backward (torch linalg.cholesky backward): L, dL (B x q x q,
- * lower) -> dA (B x q x q, symmetric), q <= 16. */
+ * lower) -> dA (B x q x q, symmetric), q <= 64. */
 int bo_chol_backward(int B, int q, const double* L, const double* dL, double* dA, void* stream);
 
 /* MC qEI / qNEI reduction of given samples (S x B x q):

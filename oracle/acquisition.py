@@ -111,6 +111,38 @@ class QNEIOracle:
         return (f - self.best_f.view(-1, 1, 1)).clamp_min(0).amax(dim=-1).mean(dim=0)
 
 
+def qnei_full_joint(model: ExactGPOracle, X_baseline, X, Z_joint, sample_slice=None):
+    """qNoisyExpectedImprovement with cache_root=False (acquisition/monte_carlo.py:
+    577-626, 540-575): samples of the joint posterior over (X_baseline, X) with
+    the joint base samples Z_joint (S x (r+q)); per-sample best over the
+    baseline columns, improvement of the last q columns."""
+    b, q, d = X.shape
+    r = X_baseline.shape[-2]
+    Xf = torch.cat([X_baseline.expand(b, r, d), X], dim=-2)
+    mean, cov = model.posterior(Xf)
+    f = mc_samples(mean, cov, Z_joint)                  # S x b x (r+q)
+    best = f[..., :r].amax(dim=-1)                      # S x b
+    return (f[..., r:] - best.unsqueeze(-1)).clamp_min(0).amax(dim=-1).mean(dim=0)
+
+
+def smoothed_feasibility(constraints, samples, eta):
+    """utils/objective.py:134-180 (log=False, fat=False): prod_i sigmoid(-c_i / eta)."""
+    ind = torch.ones_like(samples[..., 0])
+    for c in constraints:
+        ind = ind * torch.sigmoid(-c(samples) / eta)
+    return ind
+
+
+def qei_constrained(model: ExactGPOracle, X, Z, best_f, constraints, eta=1e-3):
+    """qExpectedImprovement with outcome constraints (monte_carlo.py:253-330):
+    relu(f - best_f) weighted per sample and point by the smoothed feasibility
+    of the samples, then max over q and mean over samples."""
+    mean, cov = model.posterior(X)
+    f = mc_samples(mean, cov, Z)                        # S x b x q
+    w = smoothed_feasibility(constraints, f.unsqueeze(-1), eta)
+    return ((f - best_f).clamp_min(0) * w).amax(dim=-1).mean(dim=0)
+
+
 # -- LogEI family (acquisition/logei.py; utils/safe_math.py) -------------------------
 TAU_RELU = 1e-6  # logei.py:66
 TAU_MAX = 1e-2   # logei.py:67

@@ -22,6 +22,8 @@ Sources (reference file:line):
   * log_fatplus / log_softplus / fatmax / smooth_amax / logmeanexp
                                botorch/utils/safe_math.py:209-352, composed as
                                acquisition/logei.py:122, 219-234, 509-534
+  * compute_feasibility_indicator / compute_smoothed_feasibility_indicator
+                               botorch/utils/objective.py:101-180
 """
 import os
 import sys
@@ -152,6 +154,23 @@ def main():
         out[f"hv_m{m_}_n{n_}_hv"] = np.array(hv.item())
         out[f"hv_m{m_}_n{n_}_extra"] = extra.numpy()
         out[f"hv_m{m_}_n{n_}_hv_plus"] = np.array(hv_plus)
+
+    # Outcome-constraint indicators (utils/objective.py:101-180) on fixed samples
+    # with two constraints, all (log, fat) variants, scalar and per-constraint eta.
+    objmod = _refload.load("botorch.utils.objective")
+    g = torch.Generator().manual_seed(31)
+    smp = torch.randn(16, 3, 4, 2, generator=g, dtype=torch.double)
+    out["feas_samples"] = smp.numpy()
+    cons = [lambda Z: Z[..., 0] - 0.2, lambda Z: 0.5 * Z[..., 1] + Z[..., 0] - 0.4]
+    out["feas_hard"] = objmod.compute_feasibility_indicator(cons, smp).numpy()
+    for log in (False, True):
+        for fat in (False, True):
+            for ename, eta in (("e1", 1e-1), ("e2", torch.tensor([0.05, 0.3], dtype=torch.double))):
+                x = smp.clone().requires_grad_(True)
+                ind = objmod.compute_smoothed_feasibility_indicator(cons, x, eta, log=log, fat=fat)
+                (gx,) = torch.autograd.grad(ind.sum(), x)
+                out[f"feas_l{int(log)}_f{int(fat)}_{ename}"] = ind.detach().numpy()
+                out[f"feas_l{int(log)}_f{int(fat)}_{ename}_grad"] = gx.numpy()
 
     path = os.path.join(HERE, "golden.npz")
     np.savez_compressed(path, **out)
