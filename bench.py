@@ -11,10 +11,17 @@ jittered q x q Cholesky, reparameterised sampling and the MC reduction
 (Cholesky, L^{-T}) are built once before timing, as the reference builds them
 on the first eval-mode call.
 
-Multi-GPU: one process per GPU (torchrun), each rank evaluates its own 512
-restarts (weak scaling, no data-path collective); the step ends with one
-all-reduce(MAX) of the best acquisition value (the argmax/gather of
-optimize_acqf, botorch/optim/optimize.py:384-387).
+Multi-GPU: one process per GPU (torchrun).  Default (weak scaling): each rank
+evaluates its own 512 restarts, no data-path collective, and the step ends
+with one all-reduce(MAX) of the best acquisition value (the argmax/gather of
+optimize_acqf, botorch/optim/optimize.py:384-387).  ``--strong``: the 512
+restarts of ONE global candidate draw are sharded over the ranks
+(distributed.shard_range, north_star's "512 restarts sharded over 8 GPUs"),
+and the step ends with the values gathered by one all-reduce of a zeroed
+512-entry buffer (distributed.allgather_rows) and the global argmax.  On one
+GPU the line also carries the projected strong-scaling curve: the same step at
+b = 512/W restarts for W = 2, 4, 8 (a projection from single-GPU timings,
+collectives excluded).
 
 Prints ONE JSON line (rank 0).
 """
@@ -456,6 +463,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fit", action="store_true", help="skip the GP-fit half of the metric")
     ap.add_argument("--no-bwd", action="store_true", help="skip the forward+backward timing")
+    ap.add_argument("--strong", action="store_true",
+                    help="shard the 512 restarts over the ranks (strong scaling)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the other section-8 configurations (C2, C3 qNEI, C4, C5)")
     args = ap.parse_args()
@@ -473,7 +482,14 @@ def main():
     from botorch_amd.models import SingleTaskGP
     from botorch_amd.sampling import SobolQMCNormalSampler
 
-    Xtr, Ytr, Xc = build_problem(dev, RESTARTS, seed_offset=rank)
+    from botorch_amd.distributed import allgather_rows, shard_range
+    r0, r1 = 0, RESTARTS
+    if args.strong:  # one global draw, each rank its contiguous slice
+        Xtr, Ytr, Xc = build_problem(dev, RESTARTS, seed_offset=0)
+        r0, r1 = shard_range(RESTARTS, ws, rank)
+        Xc = Xc[r0:r1]
+    else:
+        Xtr, Ytr, Xc = build_problem(dev, RESTARTS, seed_offset=rank)
     best_f = Ytr.max().item()
     model = SingleTaskGP(Xtr.to(dev), Ytr.to(dev))
     model.covar_module.lengthscale = torch.full((1, D), LENGTHSCALE, dtype=torch.float64)
@@ -500,6 +516,10 @@ def main():
     def step(i=None):
         with torch.no_grad():
             acq = acqf(Xd)
+        if args.strong:
+            allv = allgather_rows(acq, RESTARTS)   # every rank: all 512 values
+            torch.amax(allv, dim=0, keepdim=True, out=best)
+            return allv
         torch.amax(acq, dim=0, keepdim=True, out=best)
         if dist is not None:
             dist.all_reduce(best, op=dist.ReduceOp.MAX)
@@ -525,13 +545,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     ms_step = 1e3 * elapsed / args.steps
-    evals_per_step = Q * RESTARTS * MC * ws
+    evals_per_step = Q * RESTARTS * MC * (1 if args.strong else ws)
     value = evals_per_step * args.steps / elapsed
 
     timing[0] = False
     kern_ms = sorted(a.elapsed_time(b) for a, b in zip(ev["post_partials_begin"], ev["post_partials_end"]))
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
-    fl = flops_post_partials(RESTARTS, Q, N_TRAIN)
+    fl = flops_post_partials(r1 - r0, Q, N_TRAIN)
     achieved = fl / (kern_avg_ms * 1e-3) / 1e12
     peak = 78.6  # MI355X dense FP64 matrix TFLOP/s (MI355X_MICROARCH.md / SURVEY.md 8(d))
     traffic, traffic_src = pmc_traffic()
@@ -547,8 +567,19 @@ def main():
         fwd_bwd = None
     else:
         fb_s = _gpu_time(fwd_bwd, steps=5, warmup=2)
-        fwd_bwd = {"evals_per_s": Q * RESTARTS * MC / fb_s, "ms": 1e3 * fb_s}
+        fwd_bwd = {"evals_per_s": Q * (r1 - r0) * MC / fb_s, "ms": 1e3 * fb_s}
 
+    strong_proj = None
+    if ws == 1 and not args.no_extra:
+        # the per-rank shard of the strong split, timed on this GPU (projection)
+        strong_proj = {"note": "projection: the C3 qEI step at b = 512/W restarts on one GPU, "
+                               "collectives excluded; value = 512*q*S / step time"}
+        for W in (1, 2, 4, 8):
+            Xs = Xd[: RESTARTS // W]
+            with torch.no_grad():
+                tW = _gpu_time(lambda: acqf(Xs), steps=10, warmup=2)
+            strong_proj[f"W{W}"] = {"restarts_per_gpu": RESTARTS // W, "ms": 1e3 * tW,
+                                    "projected_value": Q * RESTARTS * MC / tW}
     gp_fit = None
     extra = None
     if rank == 0 and ws == 1 and not args.no_extra:
@@ -568,13 +599,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: Hartmann6 on Sobol(seed 0) training inputs, Sobol(seed 1+rank) candidates",
-            "config": {"workload": "C3 qEI forward: SingleTaskGP n=4096 d=6, q=16, "
-                                   "512 restarts/GPU, 512 Sobol MC samples",
-                       "n": N_TRAIN, "d": D, "q": Q, "restarts_per_gpu": RESTARTS, "mc": MC,
+            "data": "synthetic: Hartmann6 on Sobol(seed 0) training inputs, "
+                    + ("Sobol(seed 1) candidates, rank slice" if args.strong
+                       else "Sobol(seed 1+rank) candidates"),
+            "config": {"workload": ("C3 qEI forward: SingleTaskGP n=4096 d=6, q=16, "
+                                    + ("512 restarts sharded over the GPUs" if args.strong
+                                       else "512 restarts/GPU") + ", 512 Sobol MC samples"),
+                       "n": N_TRAIN, "d": D, "q": Q, "restarts_per_gpu": r1 - r0, "mc": MC,
                        "parallelism": f"restart-sharded x{ws}"},
             "roofline": {"bound": "mfma", "kernel": "post_partials_kernel",
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
@@ -583,6 +617,7 @@ def main():
                          "kernel_ms": kern_avg_ms, "flops_per_launch": fl},
             "cpu_baseline": cpu,
             "fwd_bwd": fwd_bwd,
+            "strong_scaling_projection": strong_proj,
             "gp_fit": gp_fit,
             "other_configs": extra,
         }

@@ -1,37 +1,49 @@
-"""Multi-GPU sharding of the candidate batch (one process per GPU).
+"""Multi-GPU sharding of optimize_acqf's candidate batch (one process per GPU).
 
-The reference optimises all ``num_restarts`` starting points of
-``optimize_acqf`` (optim/optimize.py:246-394) jointly on one device and then
-takes ``argmax`` over restarts.  Restarts are independent L-BFGS-B problems
-(gen_candidates_scipy sums their acquisition values, so their gradients never
-mix), so the batch partitions across ranks with no data-path exchange:
+The reference evaluates all ``raw_samples`` designs, picks ``num_restarts``
+starting points from the whole set (optim/initializers.py:411-426), optimises
+them in ``batch_limit`` chunks (optim/optimize.py:335-365) and takes one argmax
+over all restarts (:384-387).  The sharded version keeps every one of those
+decisions global, so W ranks return what one process returns:
 
-* rank r draws its own ``raw_samples / W`` Sobol raw points (seed + r),
-  picks ``num_restarts / W`` starting points from them with the same
-  Boltzmann rule as ``initialize_q_batch`` (optim/initializers.py:1116-1190),
-  and runs the local optimisation on its own GPU;
-* the only collective is ONE all-gather of a packed ``[value, candidate]``
-  row per rank at the end (the "argmax/gather" of the north star), after
-  which every rank holds the global best candidate.
+* every rank draws the same global raw designs (the seeded Sobol draw is
+  deterministic; an unseeded call takes rank 0's seed) and evaluates the
+  contiguous slice ``shard_range(raw, W, rank)`` of them;
+* one all-reduce(SUM) of a zeroed length-``raw`` buffer, each rank writing its
+  slice, gives every rank all raw values;
+* rank 0 runs the Boltzmann selection on the host values from its global CPU
+  generator -- the reference's own call -- and broadcasts the picked indices;
+* each rank optimises the contiguous restart slice ``shard_range(num_restarts,
+  W, rank)`` in ``batch_limit`` chunks;
+* one all-reduce(SUM) of a zeroed ``num_restarts x (1 + q d)`` buffer of
+  ``[value, candidate]`` rows gives every rank all restarts; the argmax over
+  them is the reference's (ties to the lowest restart index).
 
-With W = 1 this is exactly :func:`botorch_amd.optim.optimize_acqf`.
+W ranks reproduce one process bit for bit when the single process runs the
+same chunks: ``init_batch_limit = raw / W`` and ``batch_limit =
+num_restarts / W`` (each scipy L-BFGS-B run is over one chunk, so the chunk
+boundaries are part of the reference's semantics).
+
 Process groups come from ``torch.distributed`` (``nccl`` = RCCL over xGMI on
-the GPU node, ``gloo`` in the CPU tests).
+the GPU node, ``gloo`` in the CPU tests); buffers live on the acquisition's
+device, so RCCL moves device memory.
 """
 from __future__ import annotations
 
+import warnings
 from typing import Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
-from .optim import optimize_acqf
+from .optim import (BadInitialCandidatesWarning, draw_raw_samples, evaluate_raw_samples,
+                    gen_candidates_scipy, generate_in_chunks, init_options, select_initial_indices)
 
 
-def world() -> Tuple[int, int]:
-    """(world_size, rank) of the default group, (1, 0) when not initialised."""
+def world(group=None) -> Tuple[int, int]:
+    """(world_size, rank) of ``group``, (1, 0) when not initialised."""
     if dist.is_available() and dist.is_initialized():
-        return dist.get_world_size(), dist.get_rank()
+        return dist.get_world_size(group), dist.get_rank(group)
     return 1, 0
 
 
@@ -45,48 +57,125 @@ def shard_range(total: int, world_size: int, rank: int) -> Tuple[int, int]:
     return start, start + base + (1 if rank < extra else 0)
 
 
+def allgather_rows(local: torch.Tensor, total: int, group=None) -> torch.Tensor:
+    """Rows [start, stop) of a ``total``-row table from each rank -> the whole
+    table on every rank, with ONE all-reduce(SUM) of a zeroed buffer (adding
+    zeros is exact in fp64)."""
+    ws, rank = world(group)
+    s0, s1 = shard_range(total, ws, rank)
+    if local.shape[0] != s1 - s0:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} rows, owns {s1 - s0}")
+    if ws == 1:
+        return local
+    buf = local.new_zeros((total,) + tuple(local.shape[1:]))
+    buf[s0:s1] = local
+    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    return buf
+
+
+def _broadcast_from_rank0(t: torch.Tensor, group=None) -> torch.Tensor:
+    if world(group)[0] > 1:
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    return t
+
+
 def gather_argmax(value: torch.Tensor, candidate: torch.Tensor, group=None
                   ) -> Tuple[torch.Tensor, torch.Tensor, int]:
-    """Global argmax of per-rank (value, candidate) with ONE all-gather.
-
-    ``value`` is a scalar, ``candidate`` any shape (identical across ranks).
-    Returns (best_candidate, best_value, owner_rank) on every rank; ties go to
-    the lowest rank, as ``torch.argmax`` over the concatenated restarts would.
-    """
-    ws = dist.get_world_size(group) if dist.is_initialized() else 1
+    """Global argmax of one (value, candidate) per rank with one all-reduce;
+    ties go to the lowest rank, as ``torch.argmax`` over the concatenation."""
+    ws, rank = world(group)
     if ws == 1:
         return candidate, value.reshape(()), 0
-    packed = torch.cat([value.reshape(1).to(torch.float64),
-                        candidate.reshape(-1).to(torch.float64)])
-    rows = [torch.empty_like(packed) for _ in range(ws)]
-    dist.all_gather(rows, packed, group=group)
-    table = torch.stack(rows)
+    row = torch.cat([value.reshape(1).to(torch.float64), candidate.reshape(-1).to(torch.float64)])
+    table = torch.zeros(ws, row.numel(), dtype=torch.float64, device=row.device)
+    table[rank] = row
+    dist.all_reduce(table, op=dist.ReduceOp.SUM, group=group)
     owner = int(torch.argmax(table[:, 0]).item())
     best = table[owner]
-    return (best[1:].reshape(candidate.shape).to(candidate.dtype), best[0].to(value.dtype), owner)
+    return best[1:].reshape(candidate.shape).to(candidate.dtype), best[0].to(value.dtype), owner
+
+
+def gen_batch_initial_conditions_sharded(acq_function, bounds, q, num_restarts, raw_samples,
+                                         options=None, group=None):
+    """gen_batch_initial_conditions (initializers.py:243-438) with the raw-sample
+    evaluation sharded over the ranks; returns all ``num_restarts`` initial
+    conditions (identical on every rank)."""
+    ws, rank = world(group)
+    seed, batch_limit, init_func, init_kwargs = init_options(acq_function, bounds, options)
+    dev = bounds.device
+    if seed is None and ws > 1:   # one seed for the global draw: rank 0's
+        s = torch.randint(0, 2 ** 31 - 1, (1,), dtype=torch.int64).to(dev)
+        seed = int(_broadcast_from_rank0(s, group).item())
+    q = 1 if q is None else q
+    factor, max_factor = 1, 5
+    while factor < max_factor:
+        n = raw_samples * factor
+        X_rnd = draw_raw_samples(bounds, n, q, seed)
+        s0, s1 = shard_range(n, ws, rank)
+        y = evaluate_raw_samples(acq_function, X_rnd[s0:s1].to(dev), batch_limit)
+        Y_rnd = allgather_rows(y.to(torch.float64), n, group)
+        # [warned, picks...] from rank 0's selection
+        msg = torch.zeros(1 + num_restarts, dtype=torch.int64)
+        if rank == 0:
+            idx, warned = select_initial_indices(init_func, Y_rnd, num_restarts, init_kwargs)
+            msg[0] = int(warned)
+            msg[1:] = idx
+        msg = _broadcast_from_rank0(msg.to(Y_rnd.device), group).cpu()
+        ics = X_rnd[msg[1:].to(X_rnd.device)].to(dev)
+        if not bool(msg[0]):
+            return ics
+        if factor < max_factor:
+            factor += 1
+            if seed is not None:
+                seed += 1
+    warnings.warn("Unable to find non-zero acquisition function values - initial conditions "
+                  "are being selected randomly.", BadInitialCandidatesWarning)
+    return ics
 
 
 def optimize_acqf_sharded(acq_function, bounds, q: int, num_restarts: int,
                           raw_samples: Optional[int] = None, options=None, group=None,
+                          batch_initial_conditions=None, return_best_only: bool = True,
+                          gen_candidates=None, retry_on_optimization_warning: bool = True,
                           **kwargs):
-    """``optimize_acqf`` with restarts and raw samples partitioned over the
-    ranks of ``group``; returns the global (candidate q x d, value) on every rank.
-
-    Each rank must hold the same model / acquisition function (they are
-    replicated: the caches are O(n^2) and built once per rank)."""
-    ws = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
-    if num_restarts < ws:
-        raise ValueError(f"num_restarts={num_restarts} < world size {ws}")
+    """``optimize_acqf`` (optimize.py:397-543) with the raw samples and the
+    restarts partitioned over the ranks of ``group``; returns the global
+    (candidate q x d, value) -- or all restarts with ``return_best_only=False``
+    -- on every rank.  Each rank holds the same replicated model and
+    acquisition function (its caches are built locally)."""
+    ws, rank = world(group)
     options = dict(options or {})
-    r0, r1 = shard_range(num_restarts, ws, rank)
-    raw_local = None
-    if raw_samples is not None:
-        s0, s1 = shard_range(raw_samples, ws, rank)
-        raw_local = max(s1 - s0, r1 - r0)
-    if options.get("seed") is not None:
-        options["seed"] = int(options["seed"]) + rank
-    cand, val = optimize_acqf(acq_function, bounds, q, r1 - r0, raw_local, options=options,
-                              **kwargs)
-    best, best_val, _ = gather_argmax(val, cand, group)
-    return best, best_val
+    gen_candidates = gen_candidates or gen_candidates_scipy
+    if batch_initial_conditions is None:
+        if raw_samples is None:
+            raise ValueError("Must specify `raw_samples` when `batch_initial_conditions` is None`.")
+        batch_initial_conditions = gen_batch_initial_conditions_sharded(
+            acq_function, bounds, q, num_restarts, raw_samples, options=options, group=group)
+    b = batch_initial_conditions.shape[0]
+    batch_limit = options.get("batch_limit", b)
+    r0, r1 = shard_range(b, ws, rank)
+
+    def _run(ics):
+        c, v, warned = generate_in_chunks(acq_function, ics[r0:r1], bounds, batch_limit, options,
+                                          gen_candidates)
+        flag = torch.tensor([float(warned)], dtype=torch.float64, device=ics.device)
+        if ws > 1:
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        return c, v, bool(flag.item())
+
+    cands, vals, warned = _run(batch_initial_conditions)
+    if retry_on_optimization_warning and warned:
+        new_ics = gen_batch_initial_conditions_sharded(acq_function, bounds, q, num_restarts,
+                                                       raw_samples or num_restarts, options=options,
+                                                       group=group)
+        cands, vals, warned = _run(new_ics)
+    shape = batch_initial_conditions.shape[1:]
+    rows = torch.cat([vals.reshape(-1, 1).to(torch.float64),
+                      cands.reshape(vals.numel(), -1).to(torch.float64)], dim=1)
+    table = allgather_rows(rows.to(batch_initial_conditions.device), b, group)
+    all_vals = table[:, 0].to(vals.dtype)
+    all_cands = table[:, 1:].reshape(b, *shape).to(batch_initial_conditions.dtype)
+    if return_best_only:
+        best = torch.argmax(all_vals, dim=0)
+        return all_cands[best], all_vals[best]
+    return all_cands, all_vals

@@ -160,32 +160,22 @@ def draw_raw_samples(bounds, n, q, seed=None):
 def evaluate_raw_samples(acq_function, X_rnd, batch_limit=None):
     """Forward-only acquisition values of the raw designs in chunks of
     ``batch_limit`` (initializers.py:411-423), kept where they are computed: on
-    the GPU path the values never leave the device (no per-chunk ``.cpu()``)."""
+    the GPU path the values stay on the device (no per-chunk ``.cpu()``)."""
     if batch_limit is None:
         batch_limit = X_rnd.shape[0]
+    if X_rnd.shape[0] == 0:
+        return X_rnd.new_empty(0)
     with torch.no_grad():
         ys = [acq_function(X_rnd[s:s + batch_limit]) for s in range(0, X_rnd.shape[0], batch_limit)]
     return torch.cat([y.reshape(-1) for y in ys])
 
 
-def gen_batch_initial_conditions(acq_function, bounds, q, num_restarts, raw_samples,
-                                 fixed_features=None, options=None, inequality_constraints=None,
-                                 equality_constraints=None, generator=None, fixed_X_fantasies=None,
-                                 **kwargs):
-    """optim/initializers.py:243-438: Sobol raw samples, forward-only evaluation
-    in chunks of init_batch_limit, Boltzmann selection; retried with up to 5x
-    the raw samples (seed + 1 each time) while the selection warns.
-
-    MI355X path (bounds on the GPU): the raw designs are generated on the
-    device (bo_sobol_box), evaluated there chunk by chunk, and the selection
-    runs on the device tensors -- the reference's per-chunk host round trip
-    (initializers.py:416-420) is gone."""
+def init_options(acq_function, bounds, options):
+    """The option handling of gen_batch_initial_conditions (initializers.py:
+    305-345): (seed, init_batch_limit, init_func, init_kwargs)."""
     if bounds.isinf().any():
         raise NotImplementedError("Currently only finite values in `bounds` are supported for "
                                   "generating initial conditions for optimization.")
-    if inequality_constraints or equality_constraints or generator is not None \
-            or fixed_X_fantasies is not None:
-        raise NotImplementedError("constrained / custom-generator initialisation is out of scope")
     options = options or {}
     if options.get("sample_around_best", False):
         raise NotImplementedError("sample_around_best is out of scope")
@@ -200,28 +190,59 @@ def gen_batch_initial_conditions(acq_function, bounds, q, num_restarts, raw_samp
             init_kwargs["alpha"] = options.get("alpha")
     else:
         init_func = initialize_q_batch
+    return seed, batch_limit, init_func, init_kwargs
+
+
+def select_initial_indices(init_func, Y_rnd: torch.Tensor, num_restarts: int, init_kwargs) -> Tuple[torch.Tensor, bool]:
+    """The Boltzmann selection of initializers.py:424-426 on the host values
+    (one 8 B-per-design copy, where the reference copies each chunk with
+    ``.cpu()``), drawing from the global CPU generator exactly as the reference
+    does.  ``init_func`` gets an index column in place of X: it reads only
+    X's shape and indexes it, so the generator calls and the picks are the
+    reference's.  Returns (indices into the raw designs, warned)."""
+    Yh = Y_rnd.detach().cpu()
+    n = Yh.shape[0]
+    with warnings.catch_warnings(record=True) as ws:
+        warnings.simplefilter("always", category=BadInitialCandidatesWarning)
+        idx = init_func(X=torch.arange(n).view(n, 1, 1), Y=Yh, n=num_restarts, **init_kwargs)
+    # recorded, not re-emitted: the reference only uses them to decide the retry
+    return idx.reshape(-1), any(issubclass(w.category, BadInitialCandidatesWarning) for w in ws)
+
+
+def gen_batch_initial_conditions(acq_function, bounds, q, num_restarts, raw_samples,
+                                 fixed_features=None, options=None, inequality_constraints=None,
+                                 equality_constraints=None, generator=None, fixed_X_fantasies=None,
+                                 **kwargs):
+    """optim/initializers.py:243-438: Sobol raw samples, forward-only evaluation
+    in chunks of init_batch_limit, Boltzmann selection; retried with up to 5x
+    the raw samples (seed + 1 each time) while the selection warns.
+
+    MI355X path (bounds on the GPU): the raw designs are generated on the
+    device (bo_sobol_box, bit-identical to draw_sobol_samples) and evaluated
+    there chunk by chunk; only the values cross to the host, once, for the
+    selection, which draws from the global CPU generator as the reference does
+    (so the picks are the reference's)."""
+    if inequality_constraints or equality_constraints or generator is not None \
+            or fixed_X_fantasies is not None:
+        raise NotImplementedError("constrained / custom-generator initialisation is out of scope")
+    seed, batch_limit, init_func, init_kwargs = init_options(acq_function, bounds, options)
     q = 1 if q is None else q
     factor, max_factor = 1, 5
     while factor < max_factor:
-        with warnings.catch_warnings(record=True) as ws:
-            warnings.simplefilter("always", category=BadInitialCandidatesWarning)
-            n = raw_samples * factor
-            X_rnd = draw_raw_samples(bounds, n, q, seed)
-            if fixed_features:
-                for k, v in fixed_features.items():
-                    X_rnd[..., k] = v
-            Y_rnd = evaluate_raw_samples(acq_function, X_rnd.to(bounds.device), batch_limit)
-            # Seeded selection (the reference draws it from the global RNG): every
-            # rank of optimize_acqf_sharded / every rerun picks reproducibly.
-            with _seeded(seed, Y_rnd.device):
-                ics = init_func(X=X_rnd.to(Y_rnd.device), Y=Y_rnd, n=num_restarts, **init_kwargs)
-            ics = ics.to(device=bounds.device)
-            if not any(issubclass(w.category, BadInitialCandidatesWarning) for w in ws):
-                return ics
-            if factor < max_factor:
-                factor += 1
-                if seed is not None:
-                    seed += 1
+        n = raw_samples * factor
+        X_rnd = draw_raw_samples(bounds, n, q, seed)
+        if fixed_features:
+            for k, v in fixed_features.items():
+                X_rnd[..., k] = v
+        Y_rnd = evaluate_raw_samples(acq_function, X_rnd.to(bounds.device), batch_limit)
+        idx, warned = select_initial_indices(init_func, Y_rnd, num_restarts, init_kwargs)
+        ics = X_rnd[idx.to(X_rnd.device)].to(device=bounds.device)
+        if not warned:
+            return ics
+        if factor < max_factor:
+            factor += 1
+            if seed is not None:
+                seed += 1
     warnings.warn("Unable to find non-zero acquisition function values - initial conditions "
                   "are being selected randomly.", BadInitialCandidatesWarning)
     return ics
@@ -360,6 +381,25 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     return cands, acq
 
 
+def generate_in_chunks(acq_function, ics, bounds, batch_limit, options, gen_candidates):
+    """_optimize_acqf_batch's loop over batch_limit chunks of the initial
+    conditions (optimize.py:335-365): (candidates, values, any
+    OptimizationWarning)."""
+    gen_options = {k: v for k, v in (options or {}).items() if k not in INIT_OPTION_KEYS}
+    cands, vals, warned = [], [], False
+    for chunk in ics.split(max(1, batch_limit)):
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always", category=OptimizationWarning)
+            c, v = gen_candidates(chunk, acq_function, lower_bounds=bounds[0],
+                                  upper_bounds=bounds[1], options=gen_options)
+        warned |= any(issubclass(x.category, OptimizationWarning) for x in w)
+        cands.append(c)
+        vals.append(v.reshape(-1))
+    if not cands:
+        return ics.clone(), ics.new_empty(0), False
+    return torch.cat(cands), torch.cat(vals), warned
+
+
 def optimize_acqf(acq_function, bounds, q, num_restarts, raw_samples=None, options=None,
                   batch_initial_conditions=None, return_best_only=True, gen_candidates=None,
                   sequential=False, retry_on_optimization_warning=True, **kwargs):
@@ -376,25 +416,15 @@ def optimize_acqf(acq_function, bounds, q, num_restarts, raw_samples=None, optio
         batch_initial_conditions = gen_batch_initial_conditions(
             acq_function, bounds, q, num_restarts, raw_samples, options=options)
     batch_limit = options.get("batch_limit", num_restarts)
-    gen_options = {k: v for k, v in options.items() if k not in INIT_OPTION_KEYS}
 
     def _run(ics):
-        cands, vals, ws = [], [], []
-        for chunk in ics.split(batch_limit):
-            with warnings.catch_warnings(record=True) as w:
-                warnings.simplefilter("always", category=OptimizationWarning)
-                c, v = gen_candidates(chunk, acq_function, lower_bounds=bounds[0],
-                                      upper_bounds=bounds[1], options=gen_options)
-            ws += w
-            cands.append(c)
-            vals.append(v)
-        return torch.cat(cands), torch.cat([v.reshape(-1) for v in vals]), ws
+        return generate_in_chunks(acq_function, ics, bounds, batch_limit, options, gen_candidates)
 
-    cands, vals, ws = _run(batch_initial_conditions)
-    if retry_on_optimization_warning and any(issubclass(w.category, OptimizationWarning) for w in ws):
+    cands, vals, warned = _run(batch_initial_conditions)
+    if retry_on_optimization_warning and warned:
         new_ics = gen_batch_initial_conditions(acq_function, bounds, q, num_restarts,
                                                raw_samples or num_restarts, options=options)
-        cands, vals, ws = _run(new_ics)
+        cands, vals, warned = _run(new_ics)
     if return_best_only:
         best = torch.argmax(vals.view(-1), dim=0)
         return cands[best], vals[best]

@@ -219,3 +219,25 @@ def neg_mll(train_X, train_y, lengthscale, noise, constant):
     prior = lognormal_log_prob(lengthscale, ls_loc, math.sqrt(3)).sum()
     prior = prior + lognormal_log_prob(noise.reshape(-1), -4.0, 1.0).sum()
     return -(ll + prior) / n
+
+
+def fit_scipy(train_X, train_y, x0, bounds, options=None):
+    """fit_gpytorch_mll_scipy (optim/fit.py:47-110 -> optim/core.py:55-140):
+    scipy L-BFGS-B over the flat parameter vector [noise, constant,
+    lengthscale_1..d] (the order of get_parameters_and_bounds for
+    SingleTaskGP), with bounds from the constraints and the closure's loss and
+    autograd gradient (neg_mll).  Returns the scipy OptimizeResult."""
+    import numpy as np
+    from scipy.optimize import minimize
+
+    def f(x):
+        noise = torch.tensor(float(x[0]), dtype=torch.float64, requires_grad=True)
+        c = torch.tensor(float(x[1]), dtype=torch.float64, requires_grad=True)
+        ls = torch.tensor(np.asarray(x[2:]), dtype=torch.float64, requires_grad=True)
+        loss = neg_mll(train_X, train_y, ls, noise, c)
+        loss.backward()
+        g = np.concatenate([[noise.grad.item(), c.grad.item()], ls.grad.numpy()])
+        return loss.item(), g
+
+    return minimize(f, np.asarray(x0, dtype=np.float64), jac=True, method="L-BFGS-B",
+                    bounds=bounds, options=options or {})

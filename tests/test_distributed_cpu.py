@@ -1,5 +1,7 @@
-"""Restart sharding over ranks (botorch_amd/distributed.py) with the gloo backend,
-world_size 2, on CPU: the only collective is the final argmax all-gather."""
+"""Restart sharding over ranks (botorch_amd/distributed.py) with the gloo backend
+on CPU, driving a GP-shaped acquisition (qEI on an exact GP, the oracle's CPU
+restatement standing in for the device path): W ranks return what one process
+returns, bit for bit, when the single process runs the same chunks."""
 import os
 import socket
 
@@ -10,16 +12,25 @@ import torch.multiprocessing as mp
 from botorch_amd.distributed import shard_range
 
 
-class _Bumps(torch.nn.Module):
-    """Multimodal CPU acquisition surrogate (sum over t-batches is separable,
-    like every acquisition function optimize_acqf drives)."""
+class _GPqEI(torch.nn.Module):
+    """qExpectedImprovement on a 48-point exact GP over Hartmann6 (fixed Sobol
+    base samples), differentiable in X on the CPU."""
+
+    def __init__(self, q=2, S=64):
+        super().__init__()
+        from botorch_amd.test_functions import Hartmann
+        from oracle.gp import ExactGPOracle, GPHyper
+        from oracle.sampling import draw_sobol_normal_samples, draw_sobol_samples
+        lo = torch.zeros(6, dtype=torch.float64)
+        X = draw_sobol_samples(lo, lo + 1, 48, 1, 0).squeeze(1)
+        Y = Hartmann(negate=True)(X).unsqueeze(-1)
+        self.orc = ExactGPOracle(X, Y, GPHyper(torch.full((6,), 0.35, dtype=torch.float64), 1e-3, 0.0))
+        self.Z = draw_sobol_normal_samples(q, S, 3)
+        self.best_f = float(Y.max()) - 0.2
 
     def forward(self, X):
-        X = X if X.dim() > 2 else X.unsqueeze(0)
-        c1 = torch.tensor([0.2, 0.7], dtype=X.dtype)
-        c2 = torch.tensor([0.8, 0.3], dtype=X.dtype)
-        f = (torch.exp(-20 * ((X - c1) ** 2).sum(-1)) + 1.3 * torch.exp(-30 * ((X - c2) ** 2).sum(-1)))
-        return f.sum(-1)
+        from oracle.acquisition import qei
+        return qei(self.orc, X, self.Z, self.best_f)
 
 
 def _free_port():
@@ -30,11 +41,17 @@ def _free_port():
     return port
 
 
+OPTS = {"seed": 5, "maxiter": 30}
+B, RAW, Q = 8, 64, 2
+
+
 def _worker(rank, ws, port, outdir, mode):
     import torch.distributed as dist
-    from botorch_amd.distributed import gather_argmax, optimize_acqf_sharded
+    from botorch_amd.distributed import (gather_argmax, gen_batch_initial_conditions_sharded,
+                                         optimize_acqf_sharded)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
         if mode == "argmax":
@@ -42,12 +59,21 @@ def _worker(rank, ws, port, outdir, mode):
             val = torch.tensor([2.0, 2.0, 1.0, 0.5][rank], dtype=torch.float64)
             cand = torch.full((3, 2), float(rank), dtype=torch.float64)
             best, bv, owner = gather_argmax(val, cand)
-            torch.save({"best": best, "val": bv, "owner": owner}, os.path.join(outdir, f"r{rank}.pt"))
+            out = {"best": best, "val": bv, "owner": owner}
         else:
-            bounds = torch.tensor([[0.0, 0.0], [1.0, 1.0]], dtype=torch.float64)
-            cand, val = optimize_acqf_sharded(_Bumps(), bounds, q=1, num_restarts=4, raw_samples=32,
-                                              options={"seed": 5, "maxiter": 50})
-            torch.save({"cand": cand, "val": val}, os.path.join(outdir, f"r{rank}.pt"))
+            acqf = _GPqEI(q=Q)
+            bounds = torch.stack([torch.zeros(6), torch.ones(6)]).to(torch.float64)
+            opts = dict(OPTS, batch_limit=B // ws, init_batch_limit=RAW // ws)
+            torch.manual_seed(123)
+            ics = gen_batch_initial_conditions_sharded(acqf, bounds, Q, B, RAW, options=opts)
+            torch.manual_seed(123)
+            cand, val = optimize_acqf_sharded(acqf, bounds, q=Q, num_restarts=B, raw_samples=RAW,
+                                              options=opts)
+            torch.manual_seed(123)
+            cands, vals = optimize_acqf_sharded(acqf, bounds, q=Q, num_restarts=B, raw_samples=RAW,
+                                                options=opts, return_best_only=False)
+            out = {"ics": ics, "cand": cand, "val": val, "cands": cands, "vals": vals}
+        torch.save(out, os.path.join(outdir, f"r{rank}.pt"))
     finally:
         dist.destroy_process_group()
 
@@ -75,18 +101,25 @@ def test_gather_argmax_ties_lowest_rank(tmp_path):
         assert torch.equal(o["best"], torch.zeros(3, 2, dtype=torch.float64))
 
 
-def test_optimize_acqf_sharded_matches_local_shards(tmp_path):
-    from botorch_amd.optim import optimize_acqf
-    outs = _run(2, "opt", tmp_path)
-    # every rank ends with the same global answer
-    assert torch.equal(outs[0]["cand"], outs[1]["cand"])
-    # ... which is the best of the two per-shard runs (seed + rank, half the work each)
-    bounds = torch.tensor([[0.0, 0.0], [1.0, 1.0]], dtype=torch.float64)
-    local = [optimize_acqf(_Bumps(), bounds, q=1, num_restarts=2, raw_samples=16,
-                           options={"seed": 5 + r, "maxiter": 50}) for r in range(2)]
-    best = max(range(2), key=lambda r: float(local[r][1]))
-    torch.testing.assert_close(outs[0]["cand"], local[best][0])
-    torch.testing.assert_close(outs[0]["val"].reshape(()), local[best][1].reshape(()))
-    # the global optimum of the surrogate is the taller bump
-    torch.testing.assert_close(outs[0]["cand"].reshape(-1), torch.tensor([0.8, 0.3], dtype=torch.float64),
-                               atol=1e-3, rtol=0)
+@pytest.mark.parametrize("ws", [2, 4])
+def test_sharded_optimize_acqf_equals_single_process(tmp_path, ws):
+    """W ranks vs one process running the same chunks (init_batch_limit =
+    raw / W, batch_limit = restarts / W): identical initial conditions, all
+    restarts' candidates and values, and the same argmax, bit for bit."""
+    from botorch_amd.optim import gen_batch_initial_conditions, optimize_acqf
+    outs = _run(ws, "opt", tmp_path)
+    acqf = _GPqEI(q=Q)
+    bounds = torch.stack([torch.zeros(6), torch.ones(6)]).to(torch.float64)
+    opts = dict(OPTS, batch_limit=B // ws, init_batch_limit=RAW // ws)
+    torch.manual_seed(123)
+    ics = gen_batch_initial_conditions(acqf, bounds, Q, B, RAW, options=opts)
+    torch.manual_seed(123)
+    cand, val = optimize_acqf(acqf, bounds, q=Q, num_restarts=B, raw_samples=RAW, options=opts)
+    torch.manual_seed(123)
+    cands, vals = optimize_acqf(acqf, bounds, q=Q, num_restarts=B, raw_samples=RAW, options=opts,
+                                return_best_only=False)
+    assert float(val) > 0
+    for o in outs:
+        assert torch.equal(o["ics"], ics)
+        assert torch.equal(o["cands"], cands) and torch.equal(o["vals"], vals)
+        assert torch.equal(o["cand"], cand) and torch.equal(o["val"].reshape(()), val.reshape(()))

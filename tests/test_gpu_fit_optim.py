@@ -103,7 +103,8 @@ def test_gen_batch_initial_conditions_on_device():
     on the device; the picks are raw designs and include the best one."""
     from botorch_amd.acquisition import qExpectedImprovement, qLogExpectedImprovement
     from botorch_amd.models import SingleTaskGP
-    from botorch_amd.optim import evaluate_raw_samples, gen_batch_initial_conditions
+    from botorch_amd.optim import (evaluate_raw_samples, gen_batch_initial_conditions, initialize_q_batch,
+                                   initialize_q_batch_nonneg)
     from botorch_amd.sampling import SobolQMCNormalSampler
     from botorch_amd.utils_sampling import draw_sobol_samples
     X, Y = _data(128)
@@ -111,6 +112,7 @@ def test_gen_batch_initial_conditions_on_device():
     bounds = torch.stack([torch.zeros(6), torch.ones(6)]).to(torch.float64).to(DEV)
     for cls, bf in ((qExpectedImprovement, Y.max().item() - 0.5), (qLogExpectedImprovement, Y.max().item())):
         acqf = cls(m, bf, sampler=SobolQMCNormalSampler(torch.Size([64]), seed=0))
+        torch.manual_seed(21)
         ics = gen_batch_initial_conditions(acqf, bounds, q=4, num_restarts=6, raw_samples=96,
                                            options={"seed": 3, "init_batch_limit": 40})
         assert ics.is_cuda and ics.shape == (6, 4, 6)
@@ -121,6 +123,11 @@ def test_gen_batch_initial_conditions_on_device():
         hits = [(raw == ic).all(-1).all(-1).nonzero().flatten().tolist() for ic in ics.cpu()]
         assert all(len(h) == 1 for h in hits)
         assert int(yr.argmax()) in [h[0] for h in hits]
+        # the reference's host selection on the same values and generator state
+        init = initialize_q_batch_nonneg if cls is qExpectedImprovement else initialize_q_batch
+        torch.manual_seed(21)
+        assert torch.equal(ics.cpu(), init(X=raw, Y=yr, n=6))
+        torch.manual_seed(21)
         again = gen_batch_initial_conditions(acqf, bounds, q=4, num_restarts=6, raw_samples=96,
                                              options={"seed": 3, "init_batch_limit": 40})
         assert torch.equal(ics, again)

@@ -74,6 +74,7 @@ def test_gen_batch_initial_conditions_host_path():
     def acqf(X):
         return -((X - 0.3) ** 2).sum((-1, -2))
 
+    torch.manual_seed(11)
     ics = gen_batch_initial_conditions(acqf, bounds, q=3, num_restarts=4, raw_samples=16,
                                        options={"seed": 7})
     raw = draw_sobol_samples(bounds, 16, 3, seed=7)
@@ -82,10 +83,28 @@ def test_gen_batch_initial_conditions_host_path():
     hits = [(raw == ic).all(-1).all(-1).nonzero().flatten().tolist() for ic in ics]
     assert all(len(h) == 1 for h in hits)
     assert int(acqf(raw).argmax()) in [h[0] for h in hits]
-    # reproducible under the seed
+    # the selection draws from the global CPU generator, as initializers.py:424-426:
+    # the same picks as the reference protocol (init_func on the raw designs)
+    torch.manual_seed(11)
+    ref = initialize_q_batch(X=raw, Y=acqf(raw), n=4)
+    assert torch.equal(ics, ref)
+    torch.manual_seed(11)
     again = gen_batch_initial_conditions(acqf, bounds, q=3, num_restarts=4, raw_samples=16,
                                          options={"seed": 7})
     assert torch.equal(ics, again)
+
+
+def test_select_initial_indices_nonneg_matches_reference_picks():
+    from botorch_amd.optim import select_initial_indices
+    g = torch.Generator().manual_seed(0)
+    X = torch.rand(64, 2, 3, generator=g, dtype=torch.float64)
+    Y = torch.rand(64, generator=g, dtype=torch.float64) - 0.3
+    for seed in range(5):
+        torch.manual_seed(seed)
+        ref = initialize_q_batch_nonneg(X=X, Y=Y, n=8)
+        torch.manual_seed(seed)
+        idx, warned = select_initial_indices(initialize_q_batch_nonneg, Y, 8, {})
+        assert not warned and torch.equal(X[idx], ref)
 
 
 def test_is_nonnegative_follows_reference_list():
