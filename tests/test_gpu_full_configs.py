@@ -60,16 +60,21 @@ def test_c3_qei_full_batch_matches_oracle(c3):
     from oracle.acquisition import qei
     from oracle.sampling import draw_sobol_normal_samples
     Xtr, Ytr, Xc, m, orc = c3
-    best_f = Ytr.max().item()
-    acqf = qExpectedImprovement(m, best_f, sampler=SobolQMCNormalSampler(torch.Size([S3]), seed=0))
-    with torch.no_grad():
-        v = acqf(Xc.to(DEV)).cpu()
-    assert v.shape == (B3,) and torch.isfinite(v).all()
     idx = torch.arange(0, B3, B3 // 64)                      # 64 t-batches, first to last
-    ref = qei(orc, Xc[idx], draw_sobol_normal_samples(Q3, S3, 0), best_f)
-    assert (ref > 0).sum() >= 16, "degenerate check: too few non-zero improvements"
-    torch.testing.assert_close(v[idx], ref, rtol=1e-2, atol=1e-8)
-    torch.testing.assert_close(v[idx], ref, rtol=1e-7, atol=1e-12)
+    Z = draw_sobol_normal_samples(Q3, S3, 0)
+    # best_f = max Y (the bench's): no Sobol candidate improves on the data at
+    # n = 4096, every value is exactly 0 on both sides; best_f 1.5 lower gives
+    # non-zero improvements to compare
+    for off, min_pos in ((0.0, 0), (1.5, 16)):
+        best_f = Ytr.max().item() - off
+        acqf = qExpectedImprovement(m, best_f, sampler=SobolQMCNormalSampler(torch.Size([S3]), seed=0))
+        with torch.no_grad():
+            v = acqf(Xc.to(DEV)).cpu()
+        assert v.shape == (B3,) and torch.isfinite(v).all()
+        ref = qei(orc, Xc[idx], Z, best_f)
+        assert (ref > 0).sum() >= min_pos, "degenerate check: too few non-zero improvements"
+        torch.testing.assert_close(v[idx], ref, rtol=1e-2, atol=1e-8)
+        torch.testing.assert_close(v[idx], ref, rtol=1e-7, atol=1e-12)
     # the posterior moments of the same t-batches (north_star: 1e-4 relative)
     post = m.posterior(Xc[idx].to(DEV))
     mr, cr = orc.posterior(Xc[idx])
@@ -85,7 +90,16 @@ def _prune_seed(k):
     return torch.randint(0, 1000000, (1,)).item()
 
 
-@pytest.mark.parametrize("ls,noise,r_expect", [(LS3, NOISE3, 1), (0.15, 0.5, 32)])
+def _near_best(Xtr, Ytr, b, q, scale, seed):
+    """b t-batches of q points scattered around the q best training points (so
+    the MC improvements over the baseline are not all zero)."""
+    g = torch.Generator().manual_seed(seed)
+    top = Xtr[Ytr.squeeze(-1).topk(q).indices]
+    return (top.unsqueeze(0) + scale * torch.randn(b, q, Xtr.shape[-1], generator=g,
+                                                   dtype=torch.float64)).clamp(0, 1)
+
+
+@pytest.mark.parametrize("ls,noise,r_expect", [(LS3, NOISE3, 1), (0.15, 0.5, 31)])
 def test_c3_qnei_pruned_full_batch_matches_oracle(ls, noise, r_expect):
     from botorch_amd.acquisition import qNoisyExpectedImprovement
     from botorch_amd.sampling import SobolQMCNormalSampler
@@ -108,10 +122,16 @@ def test_c3_qnei_pruned_full_batch_matches_oracle(ls, noise, r_expect):
     ref_acq = QNEIOracle(orc, kept_ref, S3, seed=0)
     torch.testing.assert_close(acqf._baseline_best_f.cpu(), ref_acq.best_f, rtol=1e-9, atol=1e-10)
     idx = torch.arange(0, B3, B3 // 32)
-    ref = ref_acq(Xc[idx])
+    # Sobol candidates (the bench's: nearly all values 0), then t-batches around
+    # the best training points (non-zero improvements)
+    Xn = _near_best(Xtr, Ytr, B3, Q3, 0.03, 1)
+    with torch.no_grad():
+        vn = acqf(Xn.to(DEV)).cpu()
+    for got, X in ((v, Xc), (vn, Xn)):
+        ref = ref_acq(X[idx])
+        torch.testing.assert_close(got[idx], ref, rtol=1e-2, atol=1e-8)
+        torch.testing.assert_close(got[idx], ref, rtol=1e-6, atol=1e-10)
     assert (ref > 0).sum() >= 8
-    torch.testing.assert_close(v[idx], ref, rtol=1e-2, atol=1e-8)
-    torch.testing.assert_close(v[idx], ref, rtol=1e-6, atol=1e-10)
 
 
 def test_c4_qehvi_full_config_matches_oracle(golden):
@@ -136,17 +156,24 @@ def test_c4_qehvi_full_config_matches_oracle(golden):
                                            sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
     u = torch.zeros(6, dtype=torch.float64)
     Xc = draw_sobol_samples(u, u + 1, b, q, 1)
-    with torch.no_grad():
-        v = acqf(Xc.to(DEV)).cpu()
-    assert v.shape == (b,) and torch.isfinite(v).all()
+    # Sobol candidates (most values 0 against 2048 points) and t-batches around
+    # the Pareto set (non-zero improvements)
+    g = torch.Generator().manual_seed(2)
+    P = X[torch.from_numpy(golden["dtlz2_pareto_mask"])]
+    pick = torch.randint(0, P.shape[0], (b, q), generator=g)
+    Xn = (P[pick] + 0.05 * torch.randn(b, q, 6, generator=g, dtype=torch.float64)).clamp(0, 1)
     idx = torch.tensor([0, 17, 40, 63, 64, 99, 111, 127])
     cl = torch.from_numpy(golden["dtlz2_cells_lower"])
     cu = torch.from_numpy(golden["dtlz2_cells_upper"])
     Zm = base_samples_multi_output(S, q, 3, 0)
-    ref = torch.cat([qehvi([p[1] for p in pairs], Xc[i:i + 1], Zm, cl, cu) for i in idx.tolist()])
-    assert (ref > 0).all()
-    torch.testing.assert_close(v[idx], ref, rtol=1e-2, atol=1e-8)
-    torch.testing.assert_close(v[idx], ref, rtol=1e-7, atol=1e-10)
+    for Xt in (Xc, Xn):
+        with torch.no_grad():
+            v = acqf(Xt.to(DEV)).cpu()
+        assert v.shape == (b,) and torch.isfinite(v).all()
+        ref = torch.cat([qehvi([p[1] for p in pairs], Xt[i:i + 1], Zm, cl, cu) for i in idx.tolist()])
+        torch.testing.assert_close(v[idx], ref, rtol=1e-2, atol=1e-8)
+        torch.testing.assert_close(v[idx], ref, rtol=1e-7, atol=1e-10)
+    assert (ref > 0).sum() >= 6
 
 
 def _oracle_loss_grad(X, Y, x):
