@@ -73,6 +73,8 @@ _SIGNATURES = {
                                   _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P]),
     "bo_chol_backward": (c_int, [c_int, c_int, _P, _P, _P, _P]),
     "bo_probe_potrf_phases": (c_int, [_P, c_int64, _P, _P, _P, _P]),
+    "bo_probe_chol_dag": (c_int, [_P, _P, c_int64, _P, _P, _P, _P, _P]),
+    "bo_chol_dag_tasks": (c_int, [c_int, _P, c_int]),
     "bo_kernel_grad": (c_int, [c_int, _P, c_int64, _P, c_int64, c_int, _P, c_double, _P, c_int64,
                                c_int, c_int, _P, _P]),
     "bo_mc_reduce": (c_int, [c_int, c_int, c_int, _P, c_double, _P, _P, _P]),

@@ -16,7 +16,9 @@
 // np = roundup(n, 128) with an identity pad, so the 128-wide diagonal blocks of
 // the right-looking factorisation never straddle the edge.
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "common.h"
@@ -24,6 +26,18 @@
 
 int bo_potrf_block128(double* A, int64_t lda, int64_t k0, double* Linv, int64_t ldi, int* info,
                       hipStream_t st);
+int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipStream_t st,
+                long long* trace = nullptr);
+
+// BO_CHOL_LEGACY=1 selects the launch-per-step look-ahead factorisation below
+// (kept for A/B timing) instead of the persistent task-DAG kernel (chol_dag.hip).
+static bool chol_legacy() {
+  static const bool legacy = [] {
+    const char* e = std::getenv("BO_CHOL_LEGACY");
+    return e && e[0] == '1';
+  }();
+  return legacy;
+}
 
 namespace {
 
@@ -162,6 +176,11 @@ struct SideStream {
   hipEvent_t bulk_done = nullptr;  // BULK_k done (side stream)
 };
 
+// Creation is guarded, and a legacy factorisation holds g_side_mu for its
+// whole enqueue sequence, so concurrent host callers never interleave record /
+// wait pairs on the shared events.
+static std::mutex g_side_mu;
+
 static SideStream* side_stream() {
   static SideStream per_dev[64];
   int dev = 0;
@@ -256,11 +275,23 @@ int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* 
   BO_CHECK_ARG(((uintptr_t)A & 15) == 0 && ((uintptr_t)Linv & 15) == 0,
                "bo_cholesky_inverse: buffers must be 16-B aligned");
   hipStream_t st = as_stream(stream);
+  if (!chol_legacy()) return bo_chol_dag(A, Linv, np, info, work, st);
+  std::lock_guard<std::mutex> side_lock(g_side_mu);
   SideStream* side = side_stream();
   if (!side) {
     bo_set_error("bo_cholesky_inverse: could not create the look-ahead stream/events");
     return BO_ERR_HIP;
   }
+  // every exit joins the side stream back into the caller's stream: no
+  // look-ahead work on A / work is left unordered behind a returned error
+  bool side_used = false;
+  auto join = [&](int status) {
+    if (side_used) {
+      (void)hipEventRecord(side->bulk_done, side->stream);
+      (void)hipStreamWaitEvent(st, side->bulk_done, 0);
+    }
+    return status;
+  };
   BO_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
   BO_HIP(hipMemsetAsync(Linv, 0, sizeof(double) * np * np, st));
   // Right-looking factorisation over 128-column panels with a one-panel
@@ -277,7 +308,7 @@ int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* 
   bool bulk_pending = false;
   for (int64_t K0 = 0, k = 0; K0 < np; K0 += NBO, ++k) {
     int s = bo_potrf_block128(A, np, K0, Linv, np, info, st);
-    if (s) return s;
+    if (s) return join(s);
     const int64_t rem = np - K0 - NBO;
     if (rem <= 0) break;
     double* W = Wbuf[k & 1];
@@ -285,8 +316,9 @@ int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* 
     const double* Dinv = Linv + K0 * np + K0;  // 128 x 128 lower
     s = bo_gemm_f64_impl(0, 1, (int)rem, NBO, NBO, 1.0, P, np, 0, Dinv, np, 0, 0.0, W, NBO, 0, 1,
                          BO_GEMM_B_UPPER, st);
-    if (s) return s;
+    if (s) return join(s);
     double* A22 = A + (K0 + NBO) * np + (K0 + NBO);
+    side_used = true;
     BO_HIP(hipEventRecord(side->solved, st));
     BO_HIP(hipStreamWaitEvent(side->stream, side->solved, 0));
     // Off the critical path (side stream, low priority): the solved panel goes
@@ -298,13 +330,13 @@ int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* 
       s = bo_gemm_f64_impl(0, 1, (int)(rem - NBO), (int)(rem - NBO), NBO, -1.0, W + NBO * NBO,
                            NBO, 0, W + NBO * NBO, NBO, 0, 1.0, A22 + NBO * np + NBO, np, 0, 1,
                            BO_GEMM_LOWER_C, side->stream);
-      if (s) return s;
+      if (s) return join(s);
     }
     if (bulk_pending) BO_HIP(hipStreamWaitEvent(st, side->bulk_done, 0));  // BULK_{k-1}
     // LA_k: the next panel column (all rem rows x 128 columns, lower on its diagonal block)
     s = bo_gemm_f64_impl(0, 1, (int)rem, NBO, NBO, -1.0, W, NBO, 0, W, NBO, 0, 1.0, A22, np, 0, 1,
                          BO_GEMM_LOWER_C, st);
-    if (s) return s;
+    if (s) return join(s);
     BO_HIP(hipEventRecord(side->bulk_done, side->stream));
     bulk_pending = true;
   }
@@ -385,6 +417,10 @@ int bo_gp_cache_build(int kind, const double* Xt, int64_t n, int d, const double
     if (s) return s;
     BO_HIP(hipMemcpyAsync(&info_h, info_dev, sizeof(int), hipMemcpyDeviceToHost, st));
     BO_HIP(hipStreamSynchronize(st));
+    if (info_h < 0) {
+      bo_set_error("bo_gp_cache_build: Cholesky task DAG timed out");
+      return BO_ERR_HIP;
+    }
     if (info_h == 0) break;
   }
   if (jitter_used) *jitter_used = jitter;
@@ -541,6 +577,10 @@ extern "C" int bo_cholesky_jitter(const double* A, int64_t n, double* L, double*
     if (s) return s;
     BO_HIP(hipMemcpyAsync(&info_h, info_dev, sizeof(int), hipMemcpyDeviceToHost, st));
     BO_HIP(hipStreamSynchronize(st));
+    if (info_h < 0) {
+      bo_set_error("bo_cholesky_jitter: Cholesky task DAG timed out");
+      return BO_ERR_HIP;
+    }
     if (info_h == 0) break;
   }
   if (jitter_used) *jitter_used = jitter;

@@ -1,0 +1,982 @@
+// Blocked Cholesky + triangular inverse of one n x n SPD matrix as ONE
+// persistent launch over a task DAG of 64 x 64 tiles (gfx950).
+//
+// Replaces, for the GP caches and the MLL closure (botorch/models/gpytorch.py:446
+// -> [G] DefaultPredictionStrategy; optim/closures/model_closures.py:171-184):
+//   L = cholesky(A) and X = L^{-1}  ([G] root_inv_decomposition's L^{-T},
+//   botorch/__init__.py:44).
+//
+// Why one launch: the factorisation is a chain of n/64 diagonal-tile steps.
+// Launched step by step (chol.hip's look-ahead path) every step pays kernel
+// launch gaps and cross-stream event waits on the critical path, and the
+// diagonal factor runs while most CUs idle.  Here every workgroup (one per CU)
+// pulls tasks from one queue in a fixed order in which every dependency of a
+// task precedes it; a task waits (bounded spin) on per-tile counters.  A task
+// is only ever claimed by a running workgroup, and every task it waits on was
+// claimed earlier, so the queue cannot deadlock (no co-residency assumption).
+//
+// Tasks (T = np / 64 tile rows; tile (i, j), i >= j; A holds the lower
+// triangle and is overwritten by L; Linv receives X):
+//   CRIT(k)            L_{k,k-1} = A_{k,k-1} D_{k-1}^T,  A_kk -= L_{k,k-1} L_{k,k-1}^T,
+//                      then L_kk = chol(A_kk) and D_k = L_kk^{-1} (one workgroup, LDS)
+//   TRSM(k, rows)      L_ik = A_ik D_k^T                 (i >= k + 2)
+//   COLUPD(j, k, rows) A_ij -= L_ik L_jk^T               (step k update of column j)
+//   XSTEP(j, k, rows)  X_kj = -D_k acc_kj (k > j; X_jj = D_j), then
+//                      acc_ij += L_ik X_kj for the rows i > k  (right-looking trtri)
+// Task order (host-built table): CRIT(0), CRIT(1), then per step k: TRSM(k,.),
+// the two COLUPD chunks CRIT(k+2) needs, CRIT(k+2), XSTEP(., k), the other
+// COLUPD chunks; finally the X_{T-1,j} finalisations.
+//
+// Cross-workgroup hand-off (MI355X_MICROARCH.md, inter-workgroup visibility; the
+// per-XCD L2s are not coherent): every tile byte another workgroup reads is
+// stored write-through (sc1 buffer stores), every storing wave drains
+// (s_waitcnt vmcnt(0)), a workgroup barrier, then ONE lane publishes the tile's
+// counter with an agent-scope atomic store; consumers poll that word with an
+// agent-scope (sc1) load and read the tiles with sc1 loads only (L1 bypassed),
+// one workgroup per CU (the 104 KB LDS footprint admits one).
+#include <algorithm>
+#include <map>
+#include <utility>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+constexpr int TB = 64;  // tile
+constexpr int LP = 68;  // LDS pitch in doubles (rows 16-B aligned)
+constexpr int CH = 8;   // tile rows per chunked task
+constexpr int NFLAG0 = 16;  // head counter, abort word, padding
+constexpr long long SPIN_TIMEOUT = 200000000;  // wall-clock ticks (100 MHz): 2 s
+
+enum : int { T_CRIT = 0, T_TRSM = 1, T_COLUPD = 2, T_XSTEP = 3 };
+
+typedef unsigned int u32;
+typedef u32 v2u __attribute__((ext_vector_type(2)));
+typedef u32 v4u __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+constexpr int SC1 = 16;  // cache-policy bit: write-through store / L1-bypassing load
+
+__device__ __forceinline__ rsrc_t make_rsrc(const double* p, u32 bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double2 ld16(rsrc_t r, u32 off) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, SC1));
+}
+__device__ __forceinline__ void st16(rsrc_t r, u32 off, double2 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, off, 0, SC1);
+}
+__device__ __forceinline__ double ld8(rsrc_t r, u32 off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, SC1));
+}
+__device__ __forceinline__ void st8(rsrc_t r, u32 off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), r, off, 0, SC1);
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), l);
+  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ double rsq_nr(double v) {
+  double r = __builtin_amdgcn_rsq(v);
+  r = r * fma(-0.5 * v * r, r, 1.5);
+  r = r * fma(-0.5 * v * r, r, 1.5);
+  return r;
+}
+
+struct Ctx {
+  rsrc_t rA, rI;
+  int np;
+  int tid, lane, wave, wm, wn;
+};
+
+// byte offset of element (r, c) of tile (ti, tj)
+__device__ __forceinline__ u32 toff(const Ctx& c, int ti, int tj, int r, int col) {
+  return (u32)((((u32)(ti * TB + r)) * (u32)c.np + (u32)(tj * TB + col)) * 8u);
+}
+
+// 64 x 64 tile -> LDS (pitch LP), 16-B sc1 loads, 8 per thread in flight.
+__device__ __forceinline__ void tile_to_lds(const Ctx& c, rsrc_t r, int ti, int tj, double* S) {
+  double2 v[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int e = c.tid + 256 * p;
+    v[p] = ld16(r, toff(c, ti, tj, e >> 5, (e & 31) * 2));
+  }
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int e = c.tid + 256 * p;
+    *reinterpret_cast<double2*>(S + (e >> 5) * LP + (e & 31) * 2) = v[p];
+  }
+}
+
+__device__ __forceinline__ void lds_to_tile(const Ctx& c, const double* S, rsrc_t r, int ti, int tj) {
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int e = c.tid + 256 * p;
+    st16(r, toff(c, ti, tj, e >> 5, (e & 31) * 2),
+         *reinterpret_cast<const double2*>(S + (e >> 5) * LP + (e & 31) * 2));
+  }
+}
+
+// Accumulator: each wave owns a 32 x 32 quadrant (2 x 2 MFMA tiles).
+struct Acc {
+  v4d t[2][2];
+};
+
+__device__ __forceinline__ void acc_zero(Acc& a) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) a.t[i][j] = v4d_zero();
+}
+
+__device__ __forceinline__ void acc_load(const Ctx& c, Acc& a, rsrc_t r, int ti, int tj) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        a.t[i][j][q] = ld8(r, toff(c, ti, tj, c.wm + 16 * i + mfma_row(c.lane, q),
+                                   c.wn + 16 * j + mfma_col(c.lane)));
+}
+
+__device__ __forceinline__ void acc_store(const Ctx& c, const Acc& a, rsrc_t r, int ti, int tj) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st8(r, toff(c, ti, tj, c.wm + 16 * i + mfma_row(c.lane, q), c.wn + 16 * j + mfma_col(c.lane)),
+            a.t[i][j][q]);
+}
+
+__device__ __forceinline__ void acc_to_lds(const Ctx& c, const Acc& a, double* S) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        S[(c.wm + 16 * i + mfma_row(c.lane, q)) * LP + c.wn + 16 * j + mfma_col(c.lane)] = a.t[i][j][q];
+}
+
+// acc += sgn * SA * op(SB), 64-deep; BT: op(SB) = SB^T, else SB.
+template <bool BT>
+__device__ __forceinline__ void acc_mma(const Ctx& c, Acc& a, const double* SA, const double* SB,
+                                        double sgn) {
+  const int r16 = c.lane & 15, kq = c.lane >> 4;
+#pragma unroll 4
+  for (int ks = 0; ks < 16; ++ks) {
+    const int k = 4 * ks + kq;
+    const double a0 = sgn * SA[(c.wm + r16) * LP + k];
+    const double a1 = sgn * SA[(c.wm + 16 + r16) * LP + k];
+    double b0, b1;
+    if (BT) {
+      b0 = SB[(c.wn + r16) * LP + k];
+      b1 = SB[(c.wn + 16 + r16) * LP + k];
+    } else {
+      b0 = SB[k * LP + c.wn + r16];
+      b1 = SB[k * LP + c.wn + 16 + r16];
+    }
+    a.t[0][0] = mfma_f64(a0, b0, a.t[0][0]);
+    a.t[0][1] = mfma_f64(a0, b1, a.t[0][1]);
+    a.t[1][0] = mfma_f64(a1, b0, a.t[1][0]);
+    a.t[1][1] = mfma_f64(a1, b1, a.t[1][1]);
+  }
+}
+
+// acc += sgn * SA * SB^T, 64-deep, operands read 16 B at a time: lane group kq
+// takes k = 8 s + 2 kq (first MFMA) and 8 s + 2 kq + 1 (second) -- the same k
+// permutation on both operands, so the sum is the same set of products.
+__device__ __forceinline__ void acc_mma_nt(const Ctx& c, Acc& a, const double* SA, const double* SB,
+                                           double sgn) {
+  const int r16 = c.lane & 15, kq = c.lane >> 4;
+  const double* pa0 = SA + (c.wm + r16) * LP + 2 * kq;
+  const double* pa1 = pa0 + 16 * LP;
+  const double* pb0 = SB + (c.wn + r16) * LP + 2 * kq;
+  const double* pb1 = pb0 + 16 * LP;
+  double2 a0 = *reinterpret_cast<const double2*>(pa0), a1 = *reinterpret_cast<const double2*>(pa1);
+  double2 b0 = *reinterpret_cast<const double2*>(pb0), b1 = *reinterpret_cast<const double2*>(pb1);
+#pragma unroll
+  for (int st = 0; st < 8; ++st) {
+    double2 na0, na1, nb0, nb1;
+    if (st < 7) {  // next k-pair in flight under this pair's MFMAs
+      na0 = *reinterpret_cast<const double2*>(pa0 + 8 * (st + 1));
+      na1 = *reinterpret_cast<const double2*>(pa1 + 8 * (st + 1));
+      nb0 = *reinterpret_cast<const double2*>(pb0 + 8 * (st + 1));
+      nb1 = *reinterpret_cast<const double2*>(pb1 + 8 * (st + 1));
+    }
+    a.t[0][0] = mfma_f64(sgn * a0.x, b0.x, a.t[0][0]);
+    a.t[0][1] = mfma_f64(sgn * a0.x, b1.x, a.t[0][1]);
+    a.t[1][0] = mfma_f64(sgn * a1.x, b0.x, a.t[1][0]);
+    a.t[1][1] = mfma_f64(sgn * a1.x, b1.x, a.t[1][1]);
+    a.t[0][0] = mfma_f64(sgn * a0.y, b0.y, a.t[0][0]);
+    a.t[0][1] = mfma_f64(sgn * a0.y, b1.y, a.t[0][1]);
+    a.t[1][0] = mfma_f64(sgn * a1.y, b0.y, a.t[1][0]);
+    a.t[1][1] = mfma_f64(sgn * a1.y, b1.y, a.t[1][1]);
+    if (st < 7) { a0 = na0; a1 = na1; b0 = nb0; b1 = nb1; }
+  }
+}
+
+// 64 x 64 tile -> LDS transposed (S[col][row]): the B operand of acc += L X
+// read in the 16-B pattern of acc_mma_nt.
+__device__ __forceinline__ void tile_to_lds_t(const Ctx& c, rsrc_t r, int ti, int tj, double* S) {
+  double2 v[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int e = c.tid + 256 * p;
+    v[p] = ld16(r, toff(c, ti, tj, e >> 5, (e & 31) * 2));
+  }
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int e = c.tid + 256 * p;
+    const int row = e >> 5, col = (e & 31) * 2;
+    S[col * LP + row] = v[p].x;
+    S[(col + 1) * LP + row] = v[p].y;
+  }
+}
+
+__device__ __forceinline__ void acc_to_lds_t(const Ctx& c, const Acc& a, double* S) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        S[(c.wn + 16 * j + mfma_col(c.lane)) * LP + c.wm + 16 * i + mfma_row(c.lane, q)] = a.t[i][j][q];
+}
+
+// ---- hand-off ---------------------------------------------------------------
+__device__ __forceinline__ u32 flag_load(const u32* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Every storing wave drains its sc1 stores, the workgroup meets, one lane
+// publishes the counter value.
+__device__ __forceinline__ void publish(const Ctx& c, u32* f, u32 val) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (c.tid == 0) __hip_atomic_store(f, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Thread 0 polls until f1 >= t1 and f2 >= t2 (bounded: timeout -> abort word);
+// the workgroup then proceeds together.  Returns false when aborted.
+__device__ __forceinline__ bool wait2(const Ctx& c, const u32* f1, u32 t1, const u32* f2, u32 t2,
+                                      u32* abortw, int* s_ok, long long* wacc = nullptr) {
+  if (c.tid == 0) {
+    int ok = 1;
+    if (flag_load(f1) < t1 || flag_load(f2) < t2) {
+      const long long t0 = wall_clock64();
+      for (;;) {
+        __builtin_amdgcn_s_sleep(1);
+        if (flag_load(f1) >= t1 && flag_load(f2) >= t2) break;
+        if (flag_load(abortw)) { ok = 0; break; }
+        if (wall_clock64() - t0 > SPIN_TIMEOUT) {
+          __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+      }
+      if (wacc) *wacc += wall_clock64() - t0;
+    }
+    *s_ok = ok;
+  }
+  __syncthreads();
+  const int ok = *s_ok;
+  __syncthreads();
+  return ok != 0;
+}
+
+// ---- the diagonal tile ------------------------------------------------------------
+// v broadcast from lane K of each 16-lane row (DPP row_newbcast on gfx950).
+template <int K>
+__device__ __forceinline__ double row_bcast(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(x & 0xffffffffll), 0x150 + K, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(x >> 32), 0x150 + K, 0xf, 0xf, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+template <int JJ, int M>
+__device__ __forceinline__ void col_update(double (&v)[16], double l) {
+  if constexpr (M > JJ) v[M] = fma(-l, row_bcast<M>(l), v[M]);
+}
+template <int JJ, int... M>
+__device__ __forceinline__ void col_updates(std::integer_sequence<int, M...>, double (&v)[16], double l) {
+  (col_update<JJ, M>(v, l), ...);
+}
+
+// Column JJ of the 16 x 16 diagonal-block factorisation (wave 0; lane = (group
+// g, row r), every group holds the whole block): pivot broadcast inside the
+// 16-lane row (DPP), the next pivot's column updated first.  Group 0 publishes
+// the column L[., JJ] and 1 / L_JJ,JJ to LDS, then the column counter, for the
+// inverse built concurrently on wave 1 (diag_inv_step).
+template <int JJ>
+__device__ __forceinline__ void diag_step(double (&v)[16], int r, int g, bool lane0, int& fail,
+                                          double* rinv, double* Lc, volatile int* cnt, int cbase) {
+  const double piv = row_bcast<JJ>(v[JJ]);
+  if (!(piv > 0.0) && fail == 0) fail = JJ + 1;
+  const double rr = rsq_nr(piv);
+  const double l = (r >= JJ) ? v[JJ] * rr : 0.0;  // L_{r,JJ} (r == JJ: sqrt(piv))
+  v[JJ] = l;
+  if (g == 0) Lc[JJ * 16 + r] = l;
+  if (lane0) {
+    rinv[JJ] = rr;
+    *cnt = cbase + JJ + 1;  // LDS writes of one wave land in order
+  }
+  col_updates<JJ>(std::make_integer_sequence<int, 16>{}, v, l);  // next pivot's column first
+}
+
+template <int... JJ>
+__device__ __forceinline__ void diag_steps(std::integer_sequence<int, JJ...>, double (&v)[16],
+                                           int r, int g, bool lane0, int& fail, double* rinv,
+                                           double* Lc, volatile int* cnt, int cbase) {
+  (diag_step<JJ>(v, r, g, lane0, fail, rinv, Lc, cnt, cbase), ...);
+}
+
+// Column JJ of the inverse of the diagonal block (wave 1, one column behind wave
+// 0): group g owns inverse columns 4 g .. 4 g + 3; row JJ is scaled by 1 / L_JJ,JJ
+// and eliminated from the rows below (forward substitution).
+template <int JJ>
+__device__ __forceinline__ void diag_inv_step(double (&x)[4], int r, const double* rinv,
+                                              const double* Lc, volatile int* cnt, int cbase) {
+  while (*cnt < cbase + JJ + 1) __builtin_amdgcn_s_sleep(0);
+  const double rr = rinv[JJ];
+  const double l = Lc[JJ * 16 + r];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double xs = (r == JJ) ? x[q] * rr : x[q];
+    const double sv = row_bcast<JJ>(xs);
+    x[q] = (r > JJ) ? fma(-l, sv, xs) : xs;
+  }
+}
+
+template <int... JJ>
+__device__ __forceinline__ void diag_inv_steps(std::integer_sequence<int, JJ...>, double (&x)[4],
+                                               int r, const double* rinv, const double* Lc,
+                                               volatile int* cnt, int cbase) {
+  (diag_inv_step<JJ>(x, r, rinv, Lc, cnt, cbase), ...);
+}
+
+// 16 x 16 MFMA tile: acc = sum_k A[k] op(B) over K = 16 * nk columns/rows from LDS.
+// A(m, k) = SA[m * LP + k]; BT: B(k, n) = SB[n * LP + k], else SB[k * LP + n].
+template <bool BT>
+__device__ __forceinline__ v4d mma16(const double* SA, const double* SB, int nk, int lane) {
+  v4d a = v4d_zero();
+  const int r16 = lane & 15, kq = lane >> 4;
+  for (int ks = 0; ks < 4 * nk; ++ks) {
+    const int k = 4 * ks + kq;
+    const double av = SA[r16 * LP + k];
+    const double bv = BT ? SB[r16 * LP + k] : SB[k * LP + r16];
+    a = mfma_f64(av, bv, a);
+  }
+  return a;
+}
+
+__device__ __forceinline__ void put16(double* D, v4d a, int lane, double scale) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) D[mfma_row(lane, q) * LP + mfma_col(lane)] = scale * a[q];
+}
+
+// S (64 x 64, lower part meaningful) -> L (lower, upper zeroed) in place, and
+// D = L^{-1} (lower, upper zero).  Four 16-column panels: wave 0 factors the
+// 16 x 16 diagonal block AND inverts it (pivots and columns broadcast inside
+// 16-lane rows by DPP), the panel below is solved against that inverse on the
+// MFMA, the trailing lower triangle takes the rank-16 update on the MFMA (wave
+// 0 updates the next diagonal block and goes on factoring it while the other
+// waves update the rest).  The inverse is then merged from the four block
+// inverses by recursive doubling, X21 = -X22 L21 X11 (16 -> 32 -> 64), on the
+// MFMA; the strictly-upper blocks of S serve as scratch for the products.
+__device__ void potrf_trtri64(const Ctx& c, double* S, double* D, double* rinv, int* info, int row0,
+                              double* Lc, volatile int* cnt, long long* ct = nullptr) {
+  for (int e = c.tid; e < TB * TB; e += 256) D[(e >> 6) * LP + (e & 63)] = 0.0;
+  if (c.tid == 0) *cnt = 0;
+  __syncthreads();
+  const int r = c.lane & 15, g = c.lane >> 4;
+  // diagonal block p (rows/cols 16 p ..): wave 0 factors it in place, wave 1
+  // builds its inverse into D
+  auto diag_block = [&](int p) {
+    const int c0 = 16 * p;
+    double* T = S + c0 * LP + c0;
+    if (c.wave == 0) {
+      double v[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v[m] = T[r * LP + m];
+      int fail = 0;  // first non-positive pivot of the block (1-based), uniform
+      diag_steps(std::make_integer_sequence<int, 16>{}, v, r, g, c.lane == 0, fail, rinv + c0,
+                 Lc + 256 * (p & 1), cnt, 16 * p);
+      if (fail && c.lane == 0) atomicCAS(info, 0, row0 + c0 + fail);
+      if (g == 0) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) T[r * LP + m] = (m <= r) ? v[m] : 0.0;
+      }
+    } else {  // wave 1
+      double x[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = (r == 4 * g + q) ? 1.0 : 0.0;
+      diag_inv_steps(std::make_integer_sequence<int, 16>{}, x, r, rinv + c0, Lc + 256 * (p & 1), cnt,
+                     16 * p);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) D[(c0 + r) * LP + c0 + 4 * g + q] = x[q];
+    }
+  };
+  if (c.wave < 2) diag_block(0);
+  __syncthreads();
+  if (ct && c.tid == 0) ct[4] = wall_clock64();
+#pragma unroll 1
+  for (int p = 0; p < 3; ++p) {
+    const int c0 = 16 * p;
+    // panel below: L_{ib,p} = A_{ib,p} D_pp^T, one 16 x 16 tile per wave
+    for (int ib = p + 1 + c.wave; ib < 4; ib += 4) {
+      double* T = S + 16 * ib * LP + c0;
+      const v4d a = mma16<true>(T, D + c0 * LP + c0, 1, c.lane);
+      put16(T, a, c.lane, 1.0);
+    }
+    __syncthreads();
+    // trailing update: tiles (ib, jb), p < jb <= ib; wave 0 takes (p+1, p+1)
+    // and factors it right away while wave 1 inverts it, waves 2, 3 update the
+    // rest
+    const int nt = 3 - p;
+    const int ntile = nt * (nt + 1) / 2;
+    if (c.wave == 0) {
+      const int c1 = c0 + 16;
+      double* T = S + c1 * LP + c1;
+      const v4d a = mma16<true>(S + c1 * LP + c0, S + c1 * LP + c0, 1, c.lane);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) T[mfma_row(c.lane, q) * LP + mfma_col(c.lane)] -= a[q];
+      diag_block(p + 1);
+    } else if (c.wave == 1) {
+      diag_block(p + 1);
+    } else {
+      for (int t = c.wave - 1; t < ntile; t += 2) {  // tiles 1.. (tile 0 = (p+1, p+1))
+        int tr = 0;
+        while ((tr + 1) * (tr + 2) / 2 <= t) ++tr;
+        const int tc = t - tr * (tr + 1) / 2;
+        const int r0 = c0 + 16 + 16 * tr, q0 = c0 + 16 + 16 * tc;
+        const v4d a = mma16<true>(S + r0 * LP + c0, S + q0 * LP + c0, 1, c.lane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) S[(r0 + mfma_row(c.lane, q)) * LP + q0 + mfma_col(c.lane)] -= a[q];
+      }
+    }
+    __syncthreads();
+  }
+  if (ct && c.tid == 0) ct[5] = wall_clock64();
+  // 16 -> 32: pairs (0, 1) and (2, 3) (waves 0, 1): X21 = -X22 (L21 X11)
+  if (c.wave < 2) {
+    const int b1 = 32 * c.wave, b2 = b1 + 16;
+    double* Tb = S + b1 * LP + b2;  // strictly-upper scratch
+    v4d a = mma16<false>(S + b2 * LP + b1, D + b1 * LP + b1, 1, c.lane);
+    put16(Tb, a, c.lane, 1.0);
+    a = mma16<false>(D + b2 * LP + b2, Tb, 1, c.lane);
+    put16(D + b2 * LP + b1, a, c.lane, -1.0);
+  }
+  __syncthreads();
+  // 32 -> 64: X21 (rows 32.., cols 0..31) = -X22 (L21 X11); one 16 x 16 tile per wave
+  {
+    const int ti = c.wave >> 1, tj = c.wave & 1;
+    double* Tb = S + 32;  // rows 0..31, cols 32..63: strictly upper
+    const v4d a = mma16<false>(S + (32 + 16 * ti) * LP, D + 16 * tj, 2, c.lane);
+    __syncthreads();  // the (masked-free) reads above precede the scratch writes of other waves
+    put16(Tb + 16 * ti * LP + 16 * tj, a, c.lane, 1.0);
+    __syncthreads();
+    const v4d b = mma16<false>(D + (32 + 16 * ti) * LP + 32, Tb + 16 * tj, 2, c.lane);
+    put16(D + (32 + 16 * ti) * LP + 16 * tj, b, c.lane, -1.0);
+  }
+  __syncthreads();
+  for (int e = c.tid; e < TB * TB; e += 256) {
+    const int rr = e >> 6, col = e & 63;
+    if (col > rr) S[rr * LP + col] = 0.0;
+  }
+  __syncthreads();
+}
+
+// ---- the bulk tasks: a chunk of tile rows i in [i0, i1) ----------------------------
+// KIND 0 TRSM    X0 <- A_ik,                   acc  = X0 X1^T  -> A_ik = L_ik, fL[i][k] = 1
+// KIND 1 COLUPD  X0 <- L_ik (X1 if i == j),    acc  = A_ij - X0 X1^T -> A_ij, fA[i][j] = k + 1
+// KIND 2 XSTEP   X0 <- L_ik,                   acc  = acc_ij + X0 X1 -> Linv_ij, fX[i][j] = k - j + 1
+// The next tile's operands are loaded into registers while this tile's MFMAs
+// run (when its inputs are already published; one poll by thread 0 decides).
+struct Flags {
+  u32 *fA, *fL, *fX, *fXd, *abortw;
+  int T;
+  __device__ __forceinline__ u32* at(u32* a, int i, int j) const { return a + i * T + j; }
+};
+
+template <int KIND>
+__device__ __forceinline__ void row_deps(const Flags& f, int i, int j, int k, const u32*& d1, u32& t1,
+                                         const u32*& d2, u32& t2) {
+  if (KIND == 0) { d1 = f.at(f.fA, i, k); t1 = (u32)k; d2 = d1; t2 = t1; }
+  else if (KIND == 1) { d1 = f.at(f.fL, i, k); t1 = 1u; d2 = f.at(f.fA, i, j); t2 = (u32)k; }
+  else { d1 = f.at(f.fL, i, k); t1 = 1u; d2 = f.at(f.fX, i, j); t2 = (u32)(k - j); }
+}
+
+template <int KIND>
+__device__ __forceinline__ void row_issue(const Ctx& c, int i, int j, int k, double2 (&pv)[8],
+                                          double (&pa)[16]) {
+  const int ti = i, tj = KIND == 0 ? k : k;
+  if (!(KIND == 1 && i == j)) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int e = c.tid + 256 * p;
+      pv[p] = ld16(c.rA, toff(c, ti, tj, e >> 5, (e & 31) * 2));
+    }
+  }
+  if (KIND == 1 || (KIND == 2 && k > j)) {
+    const rsrc_t r = KIND == 1 ? c.rA : c.rI;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          pa[8 * a + 4 * b + q] = ld8(r, toff(c, i, j, c.wm + 16 * a + mfma_row(c.lane, q),
+                                              c.wn + 16 * b + mfma_col(c.lane)));
+  }
+}
+
+template <int KIND>
+__device__ bool row_loop(const Ctx& c, const Flags& f, int k, int j, int i0, int i1, double* X0,
+                         const double* X1, int* s_ok, int* s_rdy, long long* wsum,
+                         long long* ph = nullptr) {
+  long long tA = 0;
+  double2 pv[8];
+  double pa[16];
+  Acc acc;
+  bool pre = false;
+  u32* pending = nullptr;  // flag of the previous tile, published once its stores drained
+  u32 pending_val = 0;
+  for (int i = i0; i < i1; ++i) {
+    const u32 *d1, *d2;
+    u32 t1, t2;
+    if (!pre) {
+      // never block while holding an unpublished row (a waiter could need it)
+      if (pending) {
+        publish(c, pending, pending_val);
+        pending = nullptr;
+      }
+      row_deps<KIND>(f, i, j, k, d1, t1, d2, t2);
+      if (!wait2(c, d1, t1, d2, t2, f.abortw, s_ok, wsum)) return false;
+      row_issue<KIND>(c, i, j, k, pv, pa);
+      // one round of polls over the rest of the chunk: rows whose inputs are
+      // already published get their operands prefetched without a poll
+      if (c.tid == 0) {
+        int mask = 0;
+        for (int ii = i + 1; ii < i1 && ii < i + 31; ++ii) {
+          row_deps<KIND>(f, ii, j, k, d1, t1, d2, t2);
+          if (flag_load(d1) >= t1 && flag_load(d2) >= t2) mask |= 1 << (ii - i);
+          else break;
+        }
+        s_rdy[i & 1] = mask;
+      }
+    }
+    if (ph && c.tid == 0) tA = wall_clock64();
+    const bool own_x0 = !(KIND == 1 && i == j);
+    if (own_x0) {
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        const int e = c.tid + 256 * p;
+        *reinterpret_cast<double2*>(X0 + (e >> 5) * LP + (e & 31) * 2) = pv[p];
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc.t[a][b][q] = (KIND == 1 || (KIND == 2 && k > j)) ? pa[8 * a + 4 * b + q] : 0.0;
+    __syncthreads();
+    const int mask = s_rdy[i & 1];
+    pre = (mask >> 1) & 1;
+    if (pre) row_issue<KIND>(c, i + 1, j, k, pv, pa);
+    long long tB = 0;
+    if (ph && c.tid == 0) { tB = wall_clock64(); ph[0] += tB - tA; }
+    if (KIND == 0) acc_mma_nt(c, acc, X0, X1, 1.0);
+    else if (KIND == 1) acc_mma_nt(c, acc, own_x0 ? X0 : X1, X1, -1.0);
+    else acc_mma_nt(c, acc, X0, X1, 1.0);  // X1 holds X_kj transposed
+    long long tC = 0;
+    if (ph && c.tid == 0) {
+      // MFMAs retire before the timestamp only through a dependent use
+      tC = wall_clock64();
+      ph[1] += tC - tB;
+    }
+    // publish the previous tile (its stores were issued one tile ago; the
+    // drain also covers the prefetch above, which has had the MFMAs' time)
+    // (and the barrier that keeps X0 until every wave's MFMAs have read it)
+    if (pending) {
+      publish(c, pending, pending_val);
+      pending = nullptr;
+    } else {
+      __syncthreads();
+    }
+    // next row's readiness in the other slot (its last readers passed this
+    // iteration's barrier)
+    if (c.tid == 0) s_rdy[(i + 1) & 1] = mask >> 1;
+    if (KIND == 2) acc_store(c, acc, c.rI, i, j);
+    else acc_store(c, acc, c.rA, i, KIND == 0 ? k : j);
+    u32* fl;
+    u32 val;
+    if (KIND == 0) { fl = f.at(f.fL, i, k); val = 1u; }
+    else if (KIND == 1) { fl = f.at(f.fA, i, j); val = (u32)(k + 1); }
+    else { fl = f.at(f.fX, i, j); val = (u32)(k - j + 1); }
+    if (i == i0) publish(c, fl, val);  // the first row of a chunk may be on the critical path
+    else { pending = fl; pending_val = val; }
+    if (ph && c.tid == 0) { ph[2] += wall_clock64() - tC; ph[3] += 1; }
+  }
+  if (pending) publish(c, pending, pending_val);
+  return true;
+}
+
+__global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, double* __restrict__ Linv,
+                                                       int np, int T, const int4* __restrict__ tasks,
+                                                       int ntasks, u32* __restrict__ flags,
+                                                       int* __restrict__ info,
+                                                       long long* __restrict__ trace) {
+  __shared__ __attribute__((aligned(16))) double X0[TB * LP];
+  __shared__ __attribute__((aligned(16))) double X1[TB * LP];
+  __shared__ __attribute__((aligned(16))) double X2[TB * LP];
+  __shared__ double rinv[TB];
+  __shared__ double Lcol[512];  // diagonal-block columns, double-buffered by block parity
+  __shared__ int s_cnt;
+  __shared__ int s_ok;
+  __shared__ int s_rdy[2];
+  __shared__ int s_task;
+
+  Ctx c;
+  c.np = np;
+  c.tid = threadIdx.x;
+  c.lane = c.tid & 63;
+  c.wave = c.tid >> 6;
+  c.wm = (c.wave >> 1) * 32;
+  c.wn = (c.wave & 1) * 32;
+  const u32 bytes = (u32)np * (u32)np * 8u;
+  c.rA = make_rsrc(A, bytes);
+  c.rI = make_rsrc(Linv, bytes);
+  u32* head = flags;
+  u32* abortw = flags + 1;
+  u32* fA = flags + NFLAG0;
+  u32* fL = fA + T * T;
+  u32* fX = fL + T * T;
+  u32* fXd = fX + T * T;
+#define F(arr, i, j) (arr + (i) * T + (j))
+  Flags fl;
+  fl.fA = fA; fl.fL = fL; fl.fX = fX; fl.fXd = fXd; fl.abortw = abortw; fl.T = T;
+
+  if (c.tid == 0) s_task = (int)__hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  int t = s_task;
+  __syncthreads();
+  Acc acc;
+  while (t < ntasks) {
+    const int4 tk = tasks[t];
+    const int type = tk.x & 0xff, fin = tk.x >> 8;
+    long long wsum = 0;
+    long long phs[4] = {0, 0, 0, 0};
+    long long* ph = trace ? phs : nullptr;
+    if (trace && c.tid == 0) trace[4 * t] = wall_clock64();
+    const int k = tk.y, j = tk.z, i0 = tk.w & 0xffff, i1 = tk.w >> 16;
+    bool ok = true;
+    if (type == T_CRIT) {
+      if (k > 0) {
+        ok = wait2(c, F(fA, k, k - 1), (u32)(k - 1), F(fL, k - 1, k - 1), 1u, abortw, &s_ok, &wsum);
+        if (ok) {
+          tile_to_lds(c, c.rA, k, k - 1, X0);
+          tile_to_lds(c, c.rI, k - 1, k - 1, X1);
+          __syncthreads();
+          acc_zero(acc);
+          acc_mma_nt(c, acc, X0, X1, 1.0);  // L_{k,k-1} = A_{k,k-1} D_{k-1}^T
+          acc_to_lds(c, acc, X2);
+          acc_store(c, acc, c.rA, k, k - 1);
+          publish(c, F(fL, k, k - 1), 1u);
+          ok = wait2(c, F(fA, k, k), (u32)(k - 1), F(fA, k, k), (u32)(k - 1), abortw, &s_ok, &wsum);
+        }
+        if (ok) {
+          acc_load(c, acc, c.rA, k, k);
+          acc_mma_nt(c, acc, X2, X2, -1.0);  // A_kk -= L L^T (step k - 1)
+          acc_to_lds(c, acc, X0);
+        }
+      } else {
+        tile_to_lds(c, c.rA, 0, 0, X0);
+      }
+      if (ok) {
+        __syncthreads();
+        long long* ct = trace ? trace + 4 * ntasks + 8 * k : nullptr;
+        if (ct && c.tid == 0) ct[0] = wall_clock64();
+        potrf_trtri64(c, X0, X1, rinv, info, k * TB, Lcol, &s_cnt, ct);
+        if (ct && c.tid == 0) ct[1] = wall_clock64();
+        if (ct && c.tid == 0) ct[2] = wall_clock64();
+        lds_to_tile(c, X0, c.rA, k, k);
+        lds_to_tile(c, X1, c.rI, k, k);
+        publish(c, F(fL, k, k), 1u);
+        if (ct && c.tid == 0) ct[3] = wall_clock64();
+      }
+    } else if (type == T_TRSM) {
+      ok = wait2(c, F(fL, k, k), 1u, F(fL, k, k), 1u, abortw, &s_ok, &wsum);
+      if (ok) tile_to_lds(c, c.rI, k, k, X1);  // D_k
+      if (ok) ok = row_loop<0>(c, fl, k, j, i0, i1, X0, X1, &s_ok, s_rdy, &wsum, ph);
+    } else if (type == T_COLUPD) {
+      ok = wait2(c, F(fL, j, k), 1u, F(fL, j, k), 1u, abortw, &s_ok, &wsum);
+      if (ok) tile_to_lds(c, c.rA, j, k, X1);  // L_jk
+      if (ok) ok = row_loop<1>(c, fl, k, j, i0, i1, X0, X1, &s_ok, s_rdy, &wsum, ph);
+    } else {  // T_XSTEP: column j of X at step k
+      if (k == j) {
+        ok = wait2(c, F(fL, k, k), 1u, F(fL, k, k), 1u, abortw, &s_ok, &wsum);
+        if (ok) tile_to_lds_t(c, c.rI, k, k, X1);  // X_kk = D_k (transposed)
+      } else if (fin) {
+        ok = wait2(c, F(fX, k, j), (u32)(k - j), F(fL, k, k), 1u, abortw, &s_ok, &wsum);
+        if (ok) {
+          tile_to_lds(c, c.rI, k, k, X0);  // D_k
+          tile_to_lds(c, c.rI, k, j, X2);  // acc_kj
+          __syncthreads();
+          acc_zero(acc);
+          acc_mma<false>(c, acc, X0, X2, -1.0);  // X_kj = -D_k acc_kj
+          acc_to_lds_t(c, acc, X1);
+          acc_store(c, acc, c.rI, k, j);
+          publish(c, F(fXd, k, j), 1u);
+        }
+      } else {
+        ok = wait2(c, F(fXd, k, j), 1u, F(fXd, k, j), 1u, abortw, &s_ok, &wsum);
+        if (ok) tile_to_lds_t(c, c.rI, k, j, X1);
+      }
+      if (ok && i0 < i1) {
+        __syncthreads();  // X1 (X_kj) complete before the row loop reads it
+        ok = row_loop<2>(c, fl, k, j, i0, i1, X0, X1, &s_ok, s_rdy, &wsum, ph);
+      }
+    }
+    if (trace && c.tid == 0) {
+      trace[4 * t + 1] = wall_clock64();
+      trace[4 * t + 3] = wsum;
+      long long* pt = trace + 4 * ntasks + 8 * T + 4 * t;
+      pt[0] = phs[0]; pt[1] = phs[1]; pt[2] = phs[2]; pt[3] = phs[3];
+      trace[4 * t + 2] = (long long)blockIdx.x | ((long long)tk.x << 16) | ((long long)k << 24) |
+                         ((long long)j << 40);
+    }
+    // claim the next task only now: a task claimed early would sit behind this
+    // one (a critical-path task claimed by a busy workgroup stalls the chain)
+    if (c.tid == 0)
+      s_task = ok ? (int)__hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                  : ntasks;
+    __syncthreads();
+    t = s_task;
+    __syncthreads();
+  }
+  if (c.tid == 0 && flag_load(abortw)) atomicExch(info, -1);
+#undef F
+}
+
+// ---- host: task table (cached per device and order) ------------------------------
+struct DagTable {
+  int4* dev = nullptr;
+  int n = 0;
+};
+
+void push_rows(std::vector<int4>& v, int type, int k, int j, int lo, int hi, bool first_fin) {
+  bool first = true;
+  for (int i0 = lo; i0 < hi; i0 += CH) {
+    const int i1 = i0 + CH < hi ? i0 + CH : hi;
+    v.push_back(make_int4(type | ((first && first_fin) ? 256 : 0), k, j, i0 | (i1 << 16)));
+    first = false;
+  }
+}
+
+// Queue order: the generation order above is a topological order of the task
+// DAG; it is re-sorted by bottom level (estimated time from the task's start to
+// the end of the run along its longest chain of dependants), which keeps a
+// topological order (every dependant has a strictly smaller bottom level) and
+// puts the diagonal chain and the tiles it waits on ahead of the bulk updates.
+std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
+  const int n = (int)v.size();
+  auto tix = [T](int i, int j) { return (size_t)i * T + j; };
+  std::vector<int> prodL((size_t)T * T, -1), prodXd((size_t)T * T, -1);
+  // version-indexed producers: A(i,j) after v updates (v = 1..j), X(i,j) after v
+  std::vector<std::vector<int>> prodA((size_t)T * T), prodX((size_t)T * T);
+  for (int t = 0; t < n; ++t) {
+    const int type = v[t].x & 0xff, fin = v[t].x >> 8, k = v[t].y, j = v[t].z;
+    const int i0 = v[t].w & 0xffff, i1 = v[t].w >> 16;
+    if (type == T_CRIT) {
+      prodL[tix(k, k)] = t;
+      if (k > 0) prodL[tix(k, k - 1)] = t;
+    } else if (type == T_TRSM) {
+      for (int i = i0; i < i1; ++i) prodL[tix(i, k)] = t;
+    } else if (type == T_COLUPD) {
+      for (int i = i0; i < i1; ++i) {
+        auto& pa = prodA[tix(i, j)];
+        if ((int)pa.size() < k + 2) pa.resize(k + 2, -1);
+        pa[k + 1] = t;
+      }
+    } else {
+      if (fin && k > j) prodXd[tix(k, j)] = t;
+      for (int i = i0; i < i1; ++i) {
+        auto& px = prodX[tix(i, j)];
+        if ((int)px.size() < k - j + 2) px.resize(k - j + 2, -1);
+        px[k - j + 1] = t;
+      }
+    }
+  }
+  auto verA = [&](int i, int j, int ver) {
+    const auto& pa = prodA[tix(i, j)];
+    return ver >= 1 && ver < (int)pa.size() ? pa[ver] : -1;
+  };
+  auto verX = [&](int i, int j, int ver) {
+    const auto& px = prodX[tix(i, j)];
+    return ver >= 1 && ver < (int)px.size() ? px[ver] : -1;
+  };
+  std::vector<std::vector<int>> deps(n);
+  std::vector<double> dur(n);
+  for (int t = 0; t < n; ++t) {
+    const int type = v[t].x & 0xff, fin = v[t].x >> 8, k = v[t].y, j = v[t].z;
+    const int i0 = v[t].w & 0xffff, i1 = v[t].w >> 16;
+    auto& d = deps[t];
+    const int rows = i1 - i0;
+    if (type == T_CRIT) {
+      if (k > 0) {
+        d.push_back(verA(k, k - 1, k - 1));
+        d.push_back(prodL[tix(k - 1, k - 1)]);
+        d.push_back(verA(k, k, k - 1));
+      }
+      dur[t] = 28.0;
+    } else if (type == T_TRSM) {
+      d.push_back(prodL[tix(k, k)]);
+      for (int i = i0; i < i1; ++i) d.push_back(verA(i, k, k));
+      dur[t] = 1.0 + 3.6 * rows;
+    } else if (type == T_COLUPD) {
+      d.push_back(prodL[tix(j, k)]);
+      for (int i = i0; i < i1; ++i) {
+        d.push_back(prodL[tix(i, k)]);
+        d.push_back(verA(i, j, k));
+      }
+      dur[t] = 2.0 + 3.6 * rows;
+    } else {
+      if (k == j) d.push_back(prodL[tix(k, k)]);
+      else if (fin) { d.push_back(verX(k, j, k - j)); d.push_back(prodL[tix(k, k)]); }
+      else d.push_back(prodXd[tix(k, j)]);
+      for (int i = i0; i < i1; ++i) {
+        d.push_back(prodL[tix(i, k)]);
+        d.push_back(verX(i, j, k - j));
+      }
+      dur[t] = 2.0 + 3.6 * rows + (fin && k > j ? 3.0 : 0.0);
+    }
+  }
+  // bottom levels, dependants first (reverse generation order is reverse topological)
+  std::vector<double> succ(n, 0.0), bl(n, 0.0);
+  for (int t = n - 1; t >= 0; --t) {
+    bl[t] = dur[t] + succ[t];
+    for (int dd : deps[t])
+      if (dd >= 0 && bl[t] > succ[dd]) succ[dd] = bl[t];
+  }
+  std::vector<int> idx(n);
+  for (int t = 0; t < n; ++t) idx[t] = t;
+  std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return bl[a] > bl[b]; });
+  std::vector<int4> out(n);
+  for (int t = 0; t < n; ++t) out[t] = v[idx[t]];
+  return out;
+}
+
+std::vector<int4> build_tasks(int T) {
+  std::vector<int4> v;
+  auto crit = [&](int k) { v.push_back(make_int4(T_CRIT, k, k, 0)); };
+  crit(0);
+  if (T > 1) crit(1);
+  for (int k = 0; k + 1 < T; ++k) {
+    push_rows(v, T_TRSM, k, k, k + 2, T, false);
+    // the two chunks CRIT(k + 2) waits on: tiles (k+2, k+1) and (k+2, k+2) at step k
+    const int c1 = (k + 2 + CH < T) ? k + 2 + CH : T;
+    if (k + 2 < T) {
+      v.push_back(make_int4(T_COLUPD, k, k + 1, (k + 2) | (c1 << 16)));
+      v.push_back(make_int4(T_COLUPD, k, k + 2, (k + 2) | (c1 << 16)));
+      crit(k + 2);
+    }
+    for (int j = 0; j <= k; ++j) push_rows(v, T_XSTEP, k, j, k + 1, T, true);
+    if (k + 2 < T) {
+      push_rows(v, T_COLUPD, k, k + 1, c1, T, false);
+      push_rows(v, T_COLUPD, k, k + 2, c1, T, false);
+    }
+    for (int j = k + 3; j < T; ++j) push_rows(v, T_COLUPD, k, j, j, T, false);
+  }
+  for (int j = 0; j + 1 < T; ++j) v.push_back(make_int4(T_XSTEP | 256, T - 1, j, 0));
+  return priority_order(v, T);
+}
+
+std::mutex g_tab_mu;
+std::map<std::pair<int, int>, DagTable> g_tabs;  // (device, T) -> table
+
+int dag_table(int T, DagTable** out) {
+  int dev = 0;
+  BO_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_tab_mu);
+  DagTable& tb = g_tabs[{dev, T}];
+  if (!tb.dev) {
+    const std::vector<int4> v = build_tasks(T);
+    int4* d = nullptr;
+    BO_HIP(hipMalloc(&d, sizeof(int4) * v.size()));
+    BO_HIP(hipMemcpy(d, v.data(), sizeof(int4) * v.size(), hipMemcpyHostToDevice));
+    tb.dev = d;
+    tb.n = (int)v.size();
+  }
+  *out = &tb;
+  return BO_OK;
+}
+
+}  // namespace
+
+// In-place L = chol(A) (lower) and Linv = L^{-1} as one persistent launch.
+// np % 64 == 0; work: >= (16 + 4 (np/64)^2) * 4 bytes of scratch for the
+// counters; *info as in bo_cholesky_inverse (-1: the task DAG timed out).
+int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipStream_t st,
+                long long* trace) {
+  BO_CHECK_ARG(np > 0 && np % TB == 0 && np <= 16384, "bo_chol_dag: order %lld", (long long)np);
+  const int T = (int)(np / TB);
+  DagTable* tb = nullptr;
+  int s = dag_table(T, &tb);
+  if (s) return s;
+  int dev = 0, cus = 0;
+  BO_HIP(hipGetDevice(&dev));
+  BO_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const size_t fbytes = ((size_t)(NFLAG0 + 4 * T * T) * 4 + 15) / 16 * 16;
+  BO_HIP(hipMemsetAsync(work, 0, fbytes, st));
+  BO_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
+  BO_HIP(hipMemsetAsync(Linv, 0, sizeof(double) * np * np, st));
+  const int grid = cus < tb->n ? cus : tb->n;
+  chol_dag_kernel<<<grid, 256, 0, st>>>(A, Linv, (int)np, T, tb->dev, tb->n, (u32*)work, info,
+                                          trace);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+// Timing probe of the task DAG (tools/trace_chol.py): trace receives, per task
+// in queue order, [start, end, packed (block, type, k, j)] in wall-clock ticks
+// (100 MHz); returns the task count through *ntasks (host int).
+extern "C" int bo_probe_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work,
+                                 long long* trace, int* ntasks, void* stream) {
+  BO_CHECK_ARG(np > 0 && np % TB == 0, "bo_probe_chol_dag: order");
+  DagTable* tb = nullptr;
+  int s = dag_table((int)(np / TB), &tb);
+  if (s) return s;
+  *ntasks = tb->n;
+  return bo_chol_dag(A, Linv, np, info, work, as_stream(stream), trace);
+}
+
+// The queue of the task DAG for T tile rows (host only, no device call): out
+// receives 4 ints per task (type | fin << 8, k, j, i0 | i1 << 16) in queue
+// order, up to cap tasks; returns the task count (tests/test_chol_dag_cpu.py
+// checks that every dependency precedes its task).
+extern "C" int bo_chol_dag_tasks(int T, int* out, int cap) {
+  if (T < 1) return 0;
+  const std::vector<int4> v = build_tasks(T);
+  const int n = (int)v.size();
+  for (int t = 0; t < n && t < cap; ++t) {
+    out[4 * t] = v[t].x;
+    out[4 * t + 1] = v[t].y;
+    out[4 * t + 2] = v[t].z;
+    out[4 * t + 3] = v[t].w;
+  }
+  return n;
+}

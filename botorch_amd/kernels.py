@@ -20,7 +20,20 @@ from . import _lib
 from ._lib import check, lib
 
 DP = 8  # padded input dimension of the fused posterior kernel
-KXT_MAX_BYTES = 4 << 30  # largest K*x^T workspace built per posterior call
+# Largest K*x^T workspace built per posterior call: 4 GiB, at most 1/16 of the
+# device's memory, overridable with BO_KXT_MAX_BYTES (above it the posterior
+# kernel evaluates the kernel rows between its MFMAs instead).
+KXT_MAX_BYTES = int(os.environ.get("BO_KXT_MAX_BYTES", 4 << 30))
+_KXT_CAP = {}
+
+
+def kxt_cap(device: torch.device) -> int:
+    """KXT_MAX_BYTES bounded by 1/16 of the device's total memory (cached per
+    device; no synchronisation)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _KXT_CAP:
+        _KXT_CAP[idx] = min(KXT_MAX_BYTES, torch.cuda.get_device_properties(idx).total_memory // 16)
+    return _KXT_CAP[idx]
 CHOLESKY_MAX_TRIES = 6  # botorch/__init__.py:47
 CHOLESKY_JITTER_F64 = 1e-8  # [G] linear_operator.settings.cholesky_jitter (double)
 
@@ -129,7 +142,10 @@ def cholesky_inverse(A: torch.Tensor):
     info = torch.zeros(1, dtype=torch.int32, device=dev)
     check(lib().bo_cholesky_inverse(_p(W), _p(Linv), _p(work), np_, _p(info), _stream(dev)),
           "cholesky_inverse")
-    return W[:n, :n], Linv[:n, :n], int(info.item())
+    status = int(info.item())
+    if status < 0:
+        raise RuntimeError("bo_cholesky_inverse: the Cholesky task DAG timed out")
+    return W[:n, :n], Linv[:n, :n], status
 
 
 @dataclass
@@ -231,7 +247,7 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
     (rq x nrows_pad) from the same pass -- on one-pass plans only; under a
     split-k plan pp.Cx is None and R^T is stored instead.  ``kxt``: build
     K*x^T first and read it in the posterior kernel (None: when it fits
-    KXT_MAX_BYTES)."""
+    kxt_cap)."""
     dev = _dev(X)
     B, q, d = X.shape
     if d != cache.d:
@@ -258,7 +274,7 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
     # the kernel there), within a memory cap
     Kt = None
     if kxt is None:
-        kxt = cache.np * nrows_pad * 8 <= KXT_MAX_BYTES
+        kxt = cache.np * nrows_pad * 8 <= kxt_cap(dev)
     if kxt:
         Kt = torch.empty(cache.np, nrows_pad, **f64)
         check(lib().bo_post_kxt(cache.kind, _p(Xq), B, q, d, _p(cache.Xt_scaled), cache.n,

@@ -71,6 +71,17 @@ int bo_probe_valu_f64(int waves, long long* out, void* stream);
 int bo_probe_potrf_phases(double* A, int64_t lda, double* Linv, int* info, long long* tsc,
                           void* stream);
 
+/* Task trace of the persistent Cholesky DAG (chol_dag.hip) on A (np x np,
+ * np % 64 == 0): trace (device, >= 4 x tasks + 8 x np/64 int64) gets per task [start, end,
+ * packed block/type/k/j, spin-wait ticks] (100 MHz); *ntasks (HOST int) the count. */
+int bo_probe_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work,
+                      long long* trace, int* ntasks, void* stream);
+
+/* Queue of the Cholesky task DAG for T = np/64 tile rows (HOST function, no
+ * device work): 4 ints per task (type | fin << 8, k, j, i0 | i1 << 16) into
+ * out (capacity cap tasks); returns the task count. */
+int bo_chol_dag_tasks(int T, int* out, int cap);
+
 /* Batched C = alpha op(A) op(B) + beta C on the fp64 matrix cores (strides sA,
  * sB, sC between batch members).  Building block of the Cholesky/inverse and
  * of the qNEI cross-covariance; replaces the dense torch.matmul calls inside

@@ -199,7 +199,11 @@ def test_post_partials_split_k(n, B, q, split):
         assert kc > 0  # C2 geometry (32 tiles) is planned as split-k
     one = kernels.post_partials(c, Xc, store_R=True, split=0)
     spl = kernels.post_partials(c, Xc, store_R=True, split=split)
-    for a, b in ((one.Spart, spl.Spart), (one.mpart, spl.mpart), (one.Rt, spl.Rt)):
+    # the split-k plan without the K*x^T buffer (kernel rows
+    # evaluated between the MFMAs) -- the path taken above the KXT cap
+    nok = kernels.post_partials(c, Xc, store_R=True, split=split, kxt=False)
+    for a, b in ((one.Spart, spl.Spart), (one.mpart, spl.mpart), (one.Rt, spl.Rt),
+                 (one.Spart, nok.Spart), (one.mpart, nok.mpart), (one.Rt, nok.Rt)):
         torch.testing.assert_close(b, a, rtol=1e-11, atol=1e-13)
     out = kernels.qmc_finalize(c, spl, _lib.QMC_POSTERIOR, orc.ymean.item(), orc.ystd.item())
     mean_r, cov_r = orc.posterior(Xc.cpu())

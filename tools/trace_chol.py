@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Task trace of the persistent Cholesky DAG (bo_probe_chol_dag): where the
+n = 4096 factorisation + inverse spends its time.  Prints the span, per-type
+task time sums, the CRIT(k) chain (start/end, gap to its predecessor) and the
+idle fraction of the workgroups.  BO_N overrides n."""
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from botorch_amd import kernels  # noqa: E402
+from botorch_amd._lib import check, lib  # noqa: E402
+from oracle.gp import covar  # noqa: E402
+
+TYPES = ["CRIT", "TRSM", "COLUPD", "XSTEP"]
+
+
+def main():
+    n = int(os.environ.get("BO_N", "4096"))
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(0)
+    X = torch.rand(n, 6, generator=g, dtype=torch.float64)
+    A0 = (covar(X, X, torch.full((6,), 0.5, dtype=torch.float64), x1_eq_x2=True)
+          + 1e-3 * torch.eye(n, dtype=torch.float64)).tril().to(dev)
+    np_ = kernels.padded_order(n)
+    A = torch.eye(np_, dtype=torch.float64, device=dev)
+    Linv = torch.empty_like(A)
+    work = torch.empty_like(A)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    trace = torch.zeros(8 * 40000 + 8 * 1024, dtype=torch.int64, device=dev)
+    nt = ctypes.c_int(0)
+    out = {}
+    for rep in range(3):
+        A[:n, :n] = A0
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        check(lib().bo_probe_chol_dag(kernels._p(A), kernels._p(Linv), np_, kernels._p(info),
+                                      kernels._p(work), kernels._p(trace), ctypes.byref(nt),
+                                      kernels._stream(dev)), "probe_chol_dag")
+        e1.record()
+        torch.cuda.synchronize()
+        out[f"ms_rep{rep}"] = e0.elapsed_time(e1)
+    ntask = nt.value
+    tr = trace[: 4 * ntask].view(ntask, 4).cpu()
+    st, en, pk, wt = tr[:, 0], tr[:, 1], tr[:, 2], tr[:, 3]
+    t0 = int(st.min())
+    typ = (pk >> 16) & 0xff
+    k = (pk >> 24) & 0xffff
+    j = (pk >> 40) & 0xffff
+    blk = pk & 0xffff
+    dur = (en - st).double() / 100.0  # us
+    out.update(n=n, info=int(info.item()), tasks=ntask, span_us=float(en.max() - t0) / 100.0)
+    out["per_type_us"] = {TYPES[t]: float(dur[typ == t].sum()) for t in range(4)}
+    out["per_type_count"] = {TYPES[t]: int((typ == t).sum()) for t in range(4)}
+    out["per_type_wait_us"] = {TYPES[t]: float(wt[typ == t].double().sum() / 100.0) for t in range(4)}
+    out["per_type_mean_us"] = {TYPES[t]: float(dur[typ == t].mean()) for t in range(4) if (typ == t).any()}
+    nblk = int(blk.max()) + 1
+    busy = float(dur.sum())
+    out["blocks"] = nblk
+    out["busy_frac"] = busy / (nblk * out["span_us"])
+    crit = (typ == 0).nonzero().flatten()
+    rows = []
+    prev_end = None
+    for idx in crit.tolist():
+        s_, e_ = (int(st[idx]) - t0) / 100.0, (int(en[idx]) - t0) / 100.0
+        rows.append([int(k[idx]), round(s_, 1), round(e_, 1), round(e_ - s_, 1),
+                     None if prev_end is None else round(e_ - prev_end, 1)])
+        prev_end = e_
+    out["crit_k_start_end_dur_step"] = rows
+    ct = trace[4 * ntask: 4 * ntask + 8 * (n // 64)].view(-1, 8).cpu()
+    ph = (ct[:, 1:4] - ct[:, 0:3]).double() / 100.0
+    out["crit_phase_us_mean"] = {"potrf": float(ph[:, 0].mean()), "trtri": float(ph[:, 1].mean()),
+                                 "store_publish": float(ph[:, 2].mean()),
+                                 "diag0": float(((ct[:, 4] - ct[:, 0]).double() / 100.0).mean()),
+                                 "loop3": float(((ct[:, 5] - ct[:, 4]).double() / 100.0).mean()),
+                                 "merges": float(((ct[:, 1] - ct[:, 5]).double() / 100.0).mean())}
+    pre = [(int(ct[kk, 0]) - int(st[i])) / 100.0 for kk, i in enumerate(crit.tolist())]
+    out["crit_pre_us_mean"] = sum(pre) / len(pre)
+    ph = trace[4 * ntask + 8 * (np_ // 64): 4 * ntask + 8 * (np_ // 64) + 4 * ntask].view(ntask, 4).cpu()
+    for t in (0, 1, 3):
+        sel = typ == t
+        tiles = max(1, int(ph[sel, 3].sum()))
+        out[f"{TYPES[t]}_per_tile_us"] = {"commit": float(ph[sel, 0].sum()) / 100.0 / tiles,
+                                          "mfma": float(ph[sel, 1].sum()) / 100.0 / tiles,
+                                          "store_publish": float(ph[sel, 2].sum()) / 100.0 / tiles,
+                                          "tiles": tiles}
+    # the last finishing tasks
+    last = torch.argsort(en, descending=True)[:8]
+    out["last_tasks"] = [[TYPES[int(typ[i])], int(k[i]), int(j[i]), round((int(st[i]) - t0) / 100.0, 1),
+                          round((int(en[i]) - t0) / 100.0, 1)] for i in last.tolist()]
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
