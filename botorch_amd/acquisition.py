@@ -166,7 +166,10 @@ class _FusedMC(torch.autograd.Function):
         out = kernels.qmc_finalize(cache, pp, mode, ymean, ystd, Z=Z, best_f=best_f,
                                    best_f_s=best_f_s, want_mean=need_grad, want_cov=False,
                                    want_L=need_grad, log_params=lp)
-        kernels._raise_not_psd(out["info"], out["jitter"], type(acqf).__name__)
+        if need_grad:  # the gradient needs a factored root: check now
+            kernels._raise_not_psd(out["info"], out["jitter"], type(acqf).__name__)
+        else:  # forward-only: checked one call later / at the caller's sync
+            kernels.raise_not_psd_deferred(out["info"], out["jitter"], type(acqf).__name__)
         if need_grad:
             ctx.cache, ctx.pp, ctx.ystd, ctx.mode = cache, pp, ystd, mode
             ctx.best_f, ctx.best_f_s, ctx.Z = best_f, best_f_s, Z

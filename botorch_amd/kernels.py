@@ -462,6 +462,63 @@ def post_backward(cache: GPCache, pp: PostPartials, W: Optional[WMat],
     return dX
 
 
+# Deferred ladder status (forward-only fused acquisitions): the status of call t
+# is copied to pinned host memory behind an event and checked at call t + 1, at
+# the driver's own synchronisation points (gen_candidates_scipy's loss.item(),
+# the raw-sample selection, optimize_acqf's return) or by check_ladder_status().
+# The host thus runs at most one forward ahead of the device instead of
+# draining the queue every call.  Failed t-batches carry NaN values meanwhile.
+# BO_SYNC_LADDER=1 restores the per-call check.
+SYNC_LADDER = os.environ.get("BO_SYNC_LADDER", "0") == "1"
+_LADDER_PENDING = {}
+_LADDER_PINNED = {}
+
+
+def check_ladder_status(device=None) -> None:
+    """Raise NotPSDError / warn NumericalWarning for a deferred ladder status
+    (waits for the forward that produced it); no-op when none is pending."""
+    keys = list(_LADDER_PENDING) if device is None else \
+        [torch.device(device).index if torch.device(device).index is not None
+         else torch.cuda.current_device()]
+    for idx in keys:
+        item = _LADDER_PENDING.pop(idx, None)
+        if item is None:
+            continue
+        pinned, ev, what = item
+        ev.synchronize()
+        _ladder_outcome(float(pinned[0]), float(pinned[1]), what)
+
+
+def _ladder_outcome(info_max: float, jitter_max: float, what: str) -> None:
+    if info_max > 0:
+        from .exceptions import NotPSDError
+        raise NotPSDError(f"{what}: matrix not positive definite after repeatedly adding "
+                          f"jitter up to {CHOLESKY_JITTER_F64 * 10 ** (CHOLESKY_MAX_TRIES - 1):.1e}")
+    if jitter_max > 0:
+        import warnings
+        from .exceptions import NumericalWarning
+        warnings.warn(f"A not p.d., added jitter of {jitter_max:.1e} to the diagonal", NumericalWarning)
+
+
+def raise_not_psd_deferred(info: torch.Tensor, jitter: torch.Tensor, what: str) -> None:
+    """_raise_not_psd without the per-call device-to-host synchronisation."""
+    if SYNC_LADDER or info.numel() == 0:
+        return _raise_not_psd(info, jitter, what)
+    dev = info.device
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    check_ladder_status(dev)  # the previous call's status (one forward behind)
+    packed = torch.empty(2, dtype=torch.float64, device=dev)
+    check(lib().bo_ladder_status(_p(info.contiguous()), _p(jitter.contiguous()), info.numel(),
+                                 _p(packed), _stream(dev)), "ladder_status")
+    pinned = _LADDER_PINNED.get(idx)
+    if pinned is None:
+        pinned = _LADDER_PINNED[idx] = torch.empty(2, dtype=torch.float64, pin_memory=True)
+    pinned.copy_(packed, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    _LADDER_PENDING[idx] = (pinned, ev, what)
+
+
 def _raise_not_psd(info: torch.Tensor, jitter: torch.Tensor, what: str):
     """Host check of a batched ladder (one D2H read, as [G] psd_safe_cholesky's
     torch.any(info)); warns like [G] when jitter was added."""

@@ -15,7 +15,6 @@ from __future__ import annotations
 import math
 import time
 import warnings
-from contextlib import contextmanager
 from typing import Any, Callable, Dict, Optional, Tuple
 
 import numpy as np
@@ -133,18 +132,12 @@ def is_nonnegative(acq_function) -> bool:
 _is_nonnegative = is_nonnegative
 
 
-@contextmanager
-def _seeded(seed, device):
-    """manual_seed(seed) for the CPU and, when used, the current GPU generator,
-    restoring both afterwards (utils/sampling.py:40-63 extended to the device)."""
-    if seed is None:
-        yield
-        return
-    devices = [device.index if device.index is not None else torch.cuda.current_device()] \
-        if device.type == "cuda" else []
-    with torch.random.fork_rng(devices=devices):
-        torch.manual_seed(seed)
-        yield
+def _check_deferred(X) -> None:
+    """Surface a deferred jitter-ladder failure of the fused forward-only path
+    at the driver's own synchronisation point (kernels.raise_not_psd_deferred)."""
+    if X.is_cuda:
+        from . import kernels
+        kernels.check_ladder_status(X.device)
 
 
 def draw_raw_samples(bounds, n, q, seed=None):
@@ -201,6 +194,7 @@ def select_initial_indices(init_func, Y_rnd: torch.Tensor, num_restarts: int, in
     X's shape and indexes it, so the generator calls and the picks are the
     reference's.  Returns (indices into the raw designs, warned)."""
     Yh = Y_rnd.detach().cpu()
+    _check_deferred(Y_rnd)
     n = Yh.shape[0]
     with warnings.catch_warnings(record=True) as ws:
         warnings.simplefilter("always", category=BadInitialCandidatesWarning)
@@ -273,6 +267,7 @@ def gen_candidates_scipy(initial_conditions, acquisition_function, lower_bounds=
         X = torch.from_numpy(x).to(initial_conditions).view(shapeX).contiguous().requires_grad_(True)
         loss = -acquisition_function(X).sum()
         grad = torch.autograd.grad(loss, X)[0].contiguous().view(-1).cpu().numpy()
+        _check_deferred(X)
         if np.isnan(grad).any():
             raise RuntimeError(f"{np.isnan(grad).sum()} elements of the {x.size} element gradient "
                                "array `gradf` are NaN. This often indicates numerical issues.")
@@ -281,7 +276,9 @@ def gen_candidates_scipy(initial_conditions, acquisition_function, lower_bounds=
     def f_only(x):
         X = torch.from_numpy(x).to(initial_conditions).view(shapeX).contiguous()
         with torch.no_grad():
-            return -acquisition_function(X).sum().item()
+            val = -acquisition_function(X).sum().item()
+        _check_deferred(X)
+        return val
 
     t0 = time.monotonic()
     res = minimize(f_np_wrapper if with_grad else f_only, x0, method=method, jac=with_grad,
@@ -425,6 +422,7 @@ def optimize_acqf(acq_function, bounds, q, num_restarts, raw_samples=None, optio
         new_ics = gen_batch_initial_conditions(acq_function, bounds, q, num_restarts,
                                                raw_samples or num_restarts, options=options)
         cands, vals, warned = _run(new_ics)
+    _check_deferred(cands)
     if return_best_only:
         best = torch.argmax(vals.view(-1), dim=0)
         return cands[best], vals[best]

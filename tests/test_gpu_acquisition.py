@@ -451,3 +451,28 @@ def test_post_w_full_size_matches_gemm():
     assert W.kmajor
     Wg = kernels.gemm(pp.Rt, cache.U, transA=True, transB=True, flags=_lib.GEMM_B_LOWER)
     torch.testing.assert_close(W.t.T, Wg, rtol=1e-10, atol=1e-10)
+
+
+def test_qei_forward_only_ladder_status_is_deferred():
+    """Forward-only fused qEI: the jitter-ladder status is read one call later
+    (or at check_ladder_status / the optimiser's sync), not in the call; the
+    warning of a jittered q x q root still reaches the caller."""
+    import warnings
+    from botorch_amd import kernels
+    from botorch_amd.acquisition import qExpectedImprovement
+    from botorch_amd.exceptions import NumericalWarning
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    X, Y, m, orc = _setup(n=64, noise=1e-4)
+    m.likelihood.noise = torch.tensor([1e-12], dtype=torch.float64)
+    m.eval()
+    acqf = qExpectedImprovement(m, Y.max().item(), sampler=SobolQMCNormalSampler(torch.Size([32]), seed=0))
+    Xd = X[:3].unsqueeze(1).repeat(1, 2, 1).to(DEV)  # duplicated rows at training points: singular
+    kernels.check_ladder_status()
+    with warnings.catch_warnings(record=True) as ws:
+        warnings.simplefilter("always")
+        with torch.no_grad():
+            v = acqf(Xd)
+        assert not any(issubclass(w.category, NumericalWarning) for w in ws)
+        kernels.check_ladder_status()
+        assert any(issubclass(w.category, NumericalWarning) for w in ws)
+    assert torch.isfinite(v).all()
