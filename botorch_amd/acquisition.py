@@ -152,40 +152,29 @@ class MCAcquisitionFunction(AcquisitionFunction):
         return _ensemble_mean(self.model, self._sample_reduction(self._q_reduction(acqval)))
 
 
-class _FusedMC(torch.autograd.Function):
-    """qEI / qNEI value of B t-batches as one autograd node on the gfx950 path."""
-
-    @staticmethod
-    def forward(ctx, X3, acqf, mode, best_f, best_f_s, Z):
-        model = acqf.model
-        cache = model.prediction_cache()
-        ymean, ystd = model.outcome_stats()
-        need_grad = ctx.needs_input_grad[0]
-        pp = kernels.post_partials(cache, X3.detach(), store_R=need_grad)
-        lp = getattr(acqf, "_log_params", None)
-        out = kernels.qmc_finalize(cache, pp, mode, ymean, ystd, Z=Z, best_f=best_f,
-                                   best_f_s=best_f_s, want_mean=need_grad, want_cov=False,
-                                   want_L=need_grad, log_params=lp)
-        if need_grad:  # the gradient needs a factored root: check now
-            kernels._raise_not_psd(out["info"], out["jitter"], type(acqf).__name__)
-        else:  # forward-only: checked one call later / at the caller's sync
-            kernels.raise_not_psd_deferred(out["info"], out["jitter"], type(acqf).__name__)
-        if need_grad:
-            ctx.cache, ctx.pp, ctx.ystd, ctx.mode = cache, pp, ystd, mode
-            ctx.best_f, ctx.best_f_s, ctx.Z = best_f, best_f_s, Z
-            ctx.lp, ctx.acq = lp, out["acq"].detach().clone()
-            ctx.mean, ctx.L = out["mean"], out["L"]
-            ctx.W = kernels.w_matrix(cache, pp)
-        return out["acq"]
-
-    @staticmethod
-    def backward(ctx, dacq):
-        dmean, dcov = kernels.qmc_backward(ctx.mode, ctx.mean, ctx.L, ctx.Z, dacq.contiguous(),
-                                           ctx.best_f, ctx.best_f_s, acq_fwd=ctx.acq,
-                                           log_params=ctx.lp)
-        dX = kernels.post_backward(ctx.cache, ctx.pp, ctx.W, dmean, dcov, ctx.ystd)
-        return dX, None, None, None, None, None
-
+def _fused_mc(X3: torch.Tensor, acqf, mode: int, best_f: float, best_f_s, Z: torch.Tensor):
+    """qEI / qLogEI value of B t-batches on the gfx950 fused path through
+    bo::qmc_acq (one torch.ops call; its registered backward gives dX).  The
+    jitter-ladder status is checked now when a gradient follows (the root must
+    have factored), else one call later (kernels.raise_not_psd_deferred)."""
+    from . import ops  # noqa: F401  (torch.ops.bo registration)
+    model = acqf.model
+    cache = model.prediction_cache()
+    ymean, ystd = model.outcome_stats()
+    need_grad = torch.is_grad_enabled() and X3.requires_grad
+    lp = getattr(acqf, "_log_params", None)
+    fat, tau_relu, tau_max = lp if lp is not None else (True, 1.0, 1.0)
+    outs = torch.ops.bo.qmc_acq(
+        X3, cache.Xt, cache.Xt_scaled, cache.U, cache.Linv, cache.beta, cache.alpha,
+        cache.lengthscale, Z, best_f_s, int(cache.kind), int(mode), float(cache.outputscale),
+        float(cache.constant), float(ymean), float(ystd), float(best_f), bool(fat),
+        float(tau_relu), float(tau_max), bool(need_grad))
+    acq, jit, info = outs[0], outs[6], outs[7]
+    if need_grad:
+        kernels._raise_not_psd(info, jit, type(acqf).__name__)
+    else:
+        kernels.raise_not_psd_deferred(info, jit, type(acqf).__name__)
+    return acq
 
 def _ensemble_mean(model, acq: torch.Tensor) -> torch.Tensor:
     """Average over the MCMC batch of ensemble models (utils/transforms.py:289-293)."""
@@ -215,7 +204,7 @@ class qExpectedImprovement(MCAcquisitionFunction):
         if self._fused_eligible(X) and self.best_f.numel() == 1:
             sampler = self._ensure_sampler()
             Z = sampler.base_samples_2d(q, X.device)
-            acq = _FusedMC.apply(X3, self, _lib.QMC_QEI, float(self.best_f), None, Z)
+            acq = _fused_mc(X3, self, _lib.QMC_QEI, float(self.best_f), None, Z)
             return acq.reshape(batch)
         if (getattr(self.model, "_is_fully_bayesian", False) and X.is_cuda and not self._log
                 and type(self.objective) is IdentityMCObjective and self.posterior_transform is None
@@ -831,7 +820,7 @@ class qLogExpectedImprovement(qExpectedImprovement):
         if self._fused_eligible(X) and self.best_f.numel() == 1:
             sampler = self._ensure_sampler()
             Z = sampler.base_samples_2d(q, X.device)
-            acq = _FusedMC.apply(X.reshape(-1, q, d), self, _lib.QMC_QLOGEI, float(self.best_f),
+            acq = _fused_mc(X.reshape(-1, q, d), self, _lib.QMC_QLOGEI, float(self.best_f),
                                  None, Z)
             return acq.reshape(batch)
         return self._generic_forward(X)
@@ -899,7 +888,8 @@ class _FusedQEHVI(torch.autograd.Function):
         Z = sampler.base_samples_2d(q * len(models), X3.device)
         lo, hi = acqf._cells(X3.device)
         mean, L = torch.stack(means), torch.stack(Ls)
-        acq = kernels.qehvi(mean, L, Z, lo, hi)
+        from . import ops  # noqa: F401  (torch.ops.bo registration)
+        acq = torch.ops.bo.qehvi(mean, L, Z, lo, hi)
         if need_grad:
             ctx.saved, ctx.mean, ctx.L, ctx.Z, ctx.cells = saved, mean, L, Z, (lo, hi)
         return acq

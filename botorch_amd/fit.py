@@ -90,18 +90,16 @@ class _Layout:
             m.covar_module.outputscale = float(x[2 + self.d])
 
 
-def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout):
-    """Loss = -(log N(y | c, K + s2 I) + log priors) / n and its gradient."""
-    layout.set(x)
-    Xt = model.train_inputs[0]
-    y = model.train_targets
+def mll_terms(Xt: torch.Tensor, y: torch.Tensor, ls_t: torch.Tensor, noise: float, const: float,
+              os_: float, kind: int):
+    """Data term of [G] ExactMarginalLogLikelihood, ll = log N(y | c, K + s2 I)
+    (no priors, not divided by n), and d ll / d [noise, constant,
+    lengthscale_1..d, outputscale] (bo::mll's implementation)."""
     n, d = Xt.shape
-    noise, const = x[0], x[1]
-    ls = x[2:2 + d]
-    os_ = x[2 + d] if layout.has_os else 1.0
     dev = Xt.device
+    ls = ls_t.detach().cpu().numpy().astype(np.float64) if torch.is_tensor(ls_t) else np.asarray(ls_t)
     ls_t = torch.as_tensor(ls, dtype=torch.float64, device=dev)
-    cache = kernels.build_gp_cache(Xt, y, ls_t, noise, const, kind=model.kind, outputscale=os_,
+    cache = kernels.build_gp_cache(Xt, y, ls_t, noise, const, kind=kind, outputscale=os_,
                                    check_nan=False)  # checked once in fit_gpytorch_mll_scipy
     # A^{-1} = U U^T: lower triangle only, triangular operands (n^3/3 flops).
     Ainv = torch.empty(cache.np, cache.np, dtype=torch.float64, device=dev)
@@ -110,19 +108,40 @@ def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout):
                             0, kernels._p(cache.U), cache.np, 0, 0.0, kernels._p(Ainv), cache.np, 0,
                             1, _lib.GEMM_LOWER_C | _lib.GEMM_A_UPPER | _lib.GEMM_B_LOWER, st), "Ainv")
     part = torch.empty(n, d + 5, dtype=torch.float64, device=dev)
-    check(lib().bo_mll_terms(model.kind, kernels._p(Xt.contiguous()), n, d, kernels._p(ls_t), os_,
+    check(lib().bo_mll_terms(kind, kernels._p(Xt.contiguous()), n, d, kernels._p(ls_t), os_,
                              kernels._p(cache.L), kernels._p(Ainv), cache.np,
                              kernels._p(cache.alpha), kernels._p(cache.beta), kernels._p(part), st),
           "mll_terms")
     s = part.sum(dim=0).cpu().numpy()
     quad, logdet_half, sum_alpha = s[d + 3], s[d + 2], s[d + 4]
     ll = -0.5 * quad - logdet_half - 0.5 * n * math.log(2 * math.pi)
-    g = np.zeros_like(x)
+    g = np.zeros(d + 3)
     g[0] = 0.5 * s[d]                       # d ll / d noise
     g[1] = sum_alpha                        # d ll / d constant
     g[2:2 + d] = 0.5 * s[:d] / ls ** 3      # d ll / d lengthscale
+    g[2 + d] = 0.5 * s[d + 1]               # d ll / d outputscale
+    return float(ll), g
+
+
+def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout):
+    """Loss = -(log N(y | c, K + s2 I) + log priors) / n and its gradient: the
+    data term through bo::mll (torch.ops), the LogNormal priors on the host."""
+    from . import ops  # noqa: F401  (registers torch.ops.bo)
+    layout.set(x)
+    Xt = model.train_inputs[0]
+    y = model.train_targets
+    n, d = Xt.shape
+    noise, const = x[0], x[1]
+    ls = x[2:2 + d]
+    os_ = x[2 + d] if layout.has_os else 1.0
+    ls_t = torch.as_tensor(ls, dtype=torch.float64, device=Xt.device)
+    llt, gt = torch.ops.bo.mll(Xt, y, ls_t, float(noise), float(const), float(os_), int(model.kind))
+    ll = float(llt.item())
+    gall = gt.cpu().numpy()
+    g = np.zeros_like(x)
+    g[: 2 + d] = gall[: 2 + d]
     if layout.has_os:
-        g[2 + d] = 0.5 * s[d + 1]
+        g[2 + d] = gall[2 + d]
     pv, pg = _prior_terms(model.likelihood.noise_prior, np.array([noise]))
     ll += pv
     g[0] += pg[0]

@@ -341,14 +341,10 @@ def sobol_engine_state(dim: int, seed: int):
 
 def sobol_normal(dim: int, n: int, seed: int, device, skip: int = 0) -> torch.Tensor:
     """n x dim scrambled-Sobol N(0,1) samples generated on the device."""
+    from . import ops  # noqa: F401  (torch.ops.bo registration)
     state, shift = sobol_engine_state(dim, seed)
-    state = state.to(device)
-    shift = shift.to(device)
-    out = torch.empty(n, dim, dtype=torch.float64, device=device)
-    first_f32 = int(torch.get_default_dtype() == torch.float32)
-    check(lib().bo_sobol_normal(_p(state), _p(shift), dim, n, skip, first_f32, _p(out),
-                                _stream(torch.device(device))), "sobol_normal")
-    return out
+    first_f32 = torch.get_default_dtype() == torch.float32
+    return torch.ops.bo.sobol_normal(state.to(device), shift.to(device), n, skip, first_f32)
 
 
 def sobol_box(bounds: torch.Tensor, n: int, q: int, seed: Optional[int]) -> torch.Tensor:

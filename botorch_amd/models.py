@@ -295,9 +295,16 @@ class SingleTaskGP(Model):
         from . import kernels
         key = self._key()
         if self._cache is None or self._cache_key != key:
+            from . import ops  # noqa: F401  (torch.ops.bo registration)
             ls, os_, noise, c = self.hyper()
-            self._cache = kernels.build_gp_cache(self.train_inputs[0], self.train_targets, ls,
-                                                 noise, c, kind=self.kind, outputscale=os_)
+            Xt = self.train_inputs[0].contiguous()
+            L, Linv, U, beta, alpha, Xs, jit = torch.ops.bo.gp_cache(
+                Xt, self.train_targets.contiguous(), ls.contiguous(), float(os_), float(noise),
+                float(c), int(self.kind))
+            n, d = Xt.shape
+            self._cache = kernels.GPCache(self.kind, n, d, U.shape[0], Xt, Xs, ls.contiguous(),
+                                          float(os_), float(noise), float(c), L, Linv, U, beta,
+                                          alpha, 0.0)
             self._cache_key = key
         return self._cache
 

@@ -36,8 +36,15 @@ from . import _lib, kernels
 F64 = torch.float64
 
 
-def _geometry(B: int, q: int, n: int):
-    return kernels.geometry(B, q, n)  # host arithmetic in the library (no device work)
+def _geometry(B, q, n):
+    """bo_post_geometry restated for symbolic shapes (the fake implementations
+    run under tracing): (Qp, nrows_pad, nC) of B t-batches of q <= 16 points
+    against n training points -- 16-row t-batch tiles padded to 128 rows,
+    128-column training tiles."""
+    Qp = 1
+    while Qp < q:
+        Qp *= 2
+    return Qp, ((B * Qp + 127) // 128) * 128, (n + 127) // 128
 
 
 def _padded(n: int) -> int:
@@ -55,7 +62,7 @@ def _cache_from(Xt, Xt_scaled, lengthscale, U, beta, alpha, kind, outputscale, c
 
 
 def _pp_from(B, q, n, Xq, Spart, mpart, Rt) -> kernels.PostPartials:
-    Qp, nrows_pad, nC = _geometry(B, q, n)
+    Qp, nrows_pad, nC = kernels.geometry(B, q, n)
     return kernels.PostPartials(B, q, Qp, nrows_pad, nC, Xq, Spart, mpart,
                                 Rt if Rt.numel() else None)
 
@@ -174,10 +181,11 @@ def qmc_finalize(Spart: Tensor, mpart: Tensor, Xq: Tensor, Z: Optional[Tensor],
     out = kernels.qmc_finalize(c, pp, mode, ymean, ystd, Z=Z, best_f=best_f, best_f_s=best_f_s,
                                want_mean=True, want_cov=True, want_L=True,
                                log_params=(fat, tau_relu, tau_max))
-    e = Xq.new_empty(0)
-    return (out["acq"] if out["acq"] is not None else e, out["mean"], out["cov"], out["L"],
-            out["info"] if out["info"] is not None else e.to(torch.int32),
-            out["jitter"] if out["jitter"] is not None else e)
+    def e(dtype=F64):
+        return Xq.new_empty(0, dtype=dtype)
+    return (out["acq"] if out["acq"] is not None else e(), out["mean"], out["cov"], out["L"],
+            out["info"] if out["info"] is not None else e(torch.int32),
+            out["jitter"] if out["jitter"] is not None else e())
 
 
 @qmc_finalize.register_fake
@@ -202,16 +210,16 @@ def gp_posterior(X: Tensor, Xt: Tensor, Xt_scaled: Tensor, U: Tensor, Linv: Tens
     c = _cache_from(Xt, Xt_scaled, lengthscale, U, beta, alpha, kind, outputscale, constant, Linv)
     pp = kernels.post_partials(c, X, store_R=need_grad)
     out = kernels.qmc_finalize(c, pp, _lib.QMC_POSTERIOR, ymean, ystd)
-    e = X.new_empty(0, dtype=F64)
     if not need_grad:
-        return out["mean"], out["cov"], e, e, e
+        return (out["mean"], out["cov"], X.new_empty(0, dtype=F64), X.new_empty(0, dtype=F64),
+                X.new_empty(0, dtype=F64))
     W = kernels.w_matrix(c, pp)
     Wt = W.t if W.kmajor else W.t.T.contiguous()  # stored k-major (np x B Qp) either way
     return out["mean"], out["cov"], pp.Xq, pp.Rt, Wt
 
 
 @gp_posterior.register_fake
-def _(X, Xt, Xt_scaled, U, beta_l, Linv, alpha, lengthscale, kind, outputscale, constant, ymean,
+def _(X, Xt, Xt_scaled, U, Linv, beta, alpha, lengthscale, kind, outputscale, constant, ymean,
       ystd, need_grad):
     B, q, _ = X.shape
     mk = lambda *s: X.new_empty(*s, dtype=F64)  # noqa: E731
@@ -245,17 +253,18 @@ def _post_setup(ctx, inputs, output):
         need_grad = inputs
     _, _, Xq, Rt, Wt = output
     ctx.save_for_backward(Xq, Rt, Wt, Xt, Xt_scaled, alpha, lengthscale)
-    ctx.meta = (kind, outputscale, ystd, X.shape[1])
+    ctx.meta = (kind, outputscale, ystd, X.shape[0], X.shape[1])
 
 
 def _post_bwd(ctx, dmean, dcov, *_):
     Xq, Rt, Wt, Xt, Xt_scaled, alpha, lengthscale = ctx.saved_tensors
-    kind, outputscale, ystd, q = ctx.meta
+    kind, outputscale, ystd, B, q = ctx.meta
     if Rt.numel() == 0:
         raise RuntimeError("bo::gp_posterior was called with need_grad=False")
-    B = Xq.new_empty(0).shape  # placeholder for symmetry
     if dmean is None:
-        dmean = torch.zeros(Wt.shape[1], dtype=F64, device=Wt.device)[:0]
+        dmean = Wt.new_zeros(B, q)
+    if dcov is None:
+        dcov = Wt.new_zeros(B, q, q)
     dX = torch.ops.bo.gp_posterior_backward(dmean, dcov, Xq, Rt, Wt, Xt, Xt_scaled, alpha,
                                             lengthscale, kind, outputscale, ystd, q)
     return (dX,) + (None,) * 13
@@ -281,9 +290,9 @@ def qmc_acq(X: Tensor, Xt: Tensor, Xt_scaled: Tensor, U: Tensor, Linv: Tensor, b
     out = kernels.qmc_finalize(c, pp, mode, ymean, ystd, Z=Z, best_f=best_f, best_f_s=best_f_s,
                                want_mean=need_grad, want_cov=False, want_L=need_grad,
                                log_params=(fat, tau_relu, tau_max))
-    e = X.new_empty(0, dtype=F64)
     if not need_grad:
-        return out["acq"], e, e, e, e, e, out["jitter"], out["info"]
+        e = [X.new_empty(0, dtype=F64) for _ in range(5)]
+        return out["acq"], e[0], e[1], e[2], e[3], e[4], out["jitter"], out["info"]
     W = kernels.w_matrix(c, pp)
     Wt = W.t if W.kmajor else W.t.T.contiguous()
     return out["acq"], out["mean"], out["L"], pp.Xq, pp.Rt, Wt, out["jitter"], out["info"]

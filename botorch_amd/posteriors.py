@@ -20,30 +20,18 @@ def _fused_ok(q: int, d: int) -> bool:
     return q <= FUSED_QMAX and d <= kernels.DP
 
 
-class _PosteriorMoments(torch.autograd.Function):
-    """(mean', Sigma') of B t-batches of q points, outcome space."""
-
-    @staticmethod
-    def forward(ctx, X3, model):
-        cache = model.prediction_cache()
-        ymean, ystd = model.outcome_stats()
-        need_grad = ctx.needs_input_grad[0]
-        pp = kernels.post_partials(cache, X3.detach(), store_R=need_grad)
-        out = kernels.qmc_finalize(cache, pp, _lib.QMC_POSTERIOR, ymean, ystd)
-        if need_grad:
-            ctx.cache, ctx.pp, ctx.ystd = cache, pp, ystd
-            ctx.W = kernels.w_matrix(cache, pp)
-        return out["mean"], out["cov"]
-
-    @staticmethod
-    def backward(ctx, dmean, dcov):
-        pp = ctx.pp
-        if dmean is None:
-            dmean = torch.zeros(pp.B, pp.q, dtype=torch.float64, device=ctx.W.device)
-        if dcov is None:
-            dcov = torch.zeros(pp.B, pp.q, pp.q, dtype=torch.float64, device=ctx.W.device)
-        dX = kernels.post_backward(ctx.cache, pp, ctx.W, dmean, dcov, ctx.ystd)
-        return dX, None
+def _fused_moments(X3: torch.Tensor, model):
+    """(mean', Sigma') of B t-batches of q <= 16 points (outcome space) through
+    bo::gp_posterior, differentiable w.r.t. X3 (the op's registered backward)."""
+    from . import ops  # noqa: F401  (torch.ops.bo registration)
+    cache = model.prediction_cache()
+    ymean, ystd = model.outcome_stats()
+    need_grad = torch.is_grad_enabled() and X3.requires_grad
+    mean, cov, _, _, _ = torch.ops.bo.gp_posterior(
+        X3, cache.Xt, cache.Xt_scaled, cache.U, cache.Linv, cache.beta, cache.alpha,
+        cache.lengthscale, int(cache.kind), float(cache.outputscale), float(cache.constant),
+        float(ymean), float(ystd), bool(need_grad))
+    return mean, cov
 
 
 class _GeneralMoments(torch.autograd.Function):
@@ -140,7 +128,7 @@ def posterior_moments(model, X: torch.Tensor):
     if not _fused_ok(q, d):
         mean, cov = _GeneralMoments.apply(X3, model)
     else:
-        mean, cov = _PosteriorMoments.apply(X3, model)
+        mean, cov = _fused_moments(X3, model)
     return mean.reshape(*batch, q), cov.reshape(*batch, q, q)
 
 

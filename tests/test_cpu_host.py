@@ -57,3 +57,28 @@ def test_split_plan_geometry():
     assert kernels.split_plan(1, 1, 4096)[0] == 256
     assert kernels.split_plan(128, 8, 2048)[0] == 128
     assert kernels.split_plan(64, 8, 100)[0] == 0         # nothing to split
+
+
+def test_custom_ops_registered_with_meta_shapes():
+    """torch.ops.bo.* exist and their fake (meta) implementations give the
+    shapes the device kernels produce -- no device needed."""
+    import torch
+    from botorch_amd import ops
+    for name in ops.OPS:
+        assert hasattr(torch.ops.bo, name), name
+    meta = dict(device="meta", dtype=torch.float64)
+    n, d, B, q = 300, 6, 5, 4
+    Xt, y, ls = torch.empty(n, d, **meta), torch.empty(n, **meta), torch.empty(d, **meta)
+    L, Linv, U, beta, alpha, Xs, jit = torch.ops.bo.gp_cache(Xt, y, ls, 1.0, 1e-3, 0.0, 0)
+    assert L.shape == U.shape == (384, 384) and Xs.shape == (n, 8) and jit.shape == (1,)
+    X = torch.empty(B, q, d, **meta)
+    mean, cov, Xq, Rt, Wt = torch.ops.bo.gp_posterior(X, Xt, Xs, U, Linv, beta, alpha, ls, 0, 1.0,
+                                                      0.0, 0.0, 1.0, True)
+    assert mean.shape == (B, q) and cov.shape == (B, q, q)
+    assert Xq.shape == (128, 8) and Rt.shape == (384, 128) and Wt.shape == (384, 128)
+    Z = torch.empty(64, q, **meta)
+    outs = torch.ops.bo.qmc_acq(X, Xt, Xs, U, Linv, beta, alpha, ls, Z, None, 0, 1, 1.0, 0.0, 0.0,
+                                1.0, 0.5, True, 1.0, 1.0, False)
+    assert outs[0].shape == (B,) and outs[7].dtype == torch.int32
+    Sp, mp, Xq2, Rt2 = torch.ops.bo.post_partials(X, Xt, Xs, U, beta, ls, 0, 1.0, False)
+    assert Sp.shape == (3, 8, 16, 16) and mp.shape == (3, 128) and Rt2.numel() == 0
