@@ -19,7 +19,7 @@ RBF, MATERN52 = 0, 1
 GEMM_LOWER_C, GEMM_A_LOWER, GEMM_B_UPPER, GEMM_A_UPPER, GEMM_B_LOWER = 1, 2, 4, 8, 16
 QMC_POSTERIOR, QMC_QEI, QMC_QNEI, QMC_CHOL, QMC_QLOGEI, QMC_QLOGNEI = 0, 1, 2, 3, 4, 5
 LOG_MODES = (QMC_QLOGEI, QMC_QLOGNEI)
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _P = c_void_p  # device pointers travel as void*
 
@@ -93,6 +93,98 @@ _SIGNATURES = {
                                  _P]),
 }
 
+
+
+# ---- parameter-struct entry points (ABI 9): ctypes mirrors of the C records ----------
+from ctypes import Structure, c_uint32, sizeof  # noqa: E402
+
+c_int32 = ctypes.c_int32
+_D = ctypes.c_void_p  # device pointer field
+
+
+class _Args(Structure):
+    """Base of the ABI-9 argument records: fills struct_size / abi_version and
+    maps torch tensors (or None) of pointer fields to their data pointers."""
+
+    def __init__(self, **kw):
+        super().__init__()
+        self.struct_size = sizeof(self)
+        self.abi_version = ABI_VERSION
+        self._keep = []
+        for k, v in kw.items():
+            if hasattr(v, "data_ptr"):
+                self._keep.append(v)
+                v = v.data_ptr()
+            setattr(self, k, v)
+
+
+_HDR = [("struct_size", c_uint32), ("abi_version", c_uint32)]
+
+
+class PostPartialsArgs(_Args):
+    _fields_ = _HDR + [("kind", c_int32), ("B", c_int32), ("q", c_int32), ("d", c_int32),
+                       ("Xq", _D), ("Xt_scaled", _D), ("n", c_int64), ("U", _D), ("ldu", c_int64),
+                       ("beta", _D), ("outputscale", c_double), ("Spart", _D), ("mpart", _D),
+                       ("Rt", _D), ("kc_len", c_int32), ("rq", c_int32), ("work", _D),
+                       ("Qc", _D), ("ldq", c_int64), ("Cx", _D), ("Kt", _D)]
+
+
+class QmcFinalizeArgs(_Args):
+    _fields_ = _HDR + [("kind", c_int32), ("mode", c_int32), ("B", c_int32), ("q", c_int32),
+                       ("Xq", _D), ("Spart", _D), ("mpart", _D), ("n", c_int64),
+                       ("outputscale", c_double), ("constant", c_double), ("ymean", c_double),
+                       ("ystd", c_double), ("Z", _D), ("S", c_int32), ("max_tries", c_int32),
+                       ("best_f", c_double), ("best_f_s", _D), ("jitter0", c_double),
+                       ("acq", _D), ("mean_out", _D), ("cov_out", _D), ("L_out", _D),
+                       ("info_out", _D), ("jitter_out", _D), ("Tm", _D), ("r", c_int32),
+                       ("fat", c_int32), ("ldT", c_int64), ("F", _D), ("ldF", c_int64),
+                       ("tau_relu", c_double), ("tau_max", c_double)]
+
+
+class QmcBackwardArgs(_Args):
+    _fields_ = _HDR + [("mode", c_int32), ("B", c_int32), ("q", c_int32), ("S", c_int32),
+                       ("mean", _D), ("Lq", _D), ("Z", _D), ("best_f", c_double),
+                       ("best_f_s", _D), ("F", _D), ("ldF", c_int64), ("dacq", _D),
+                       ("dmean", _D), ("dcov", _D), ("dF", _D), ("acq_fwd", _D),
+                       ("fat", c_int32), ("_pad", c_int32), ("tau_relu", c_double),
+                       ("tau_max", c_double)]
+
+
+class PostBackwardArgs(_Args):
+    _fields_ = _HDR + [("kind", c_int32), ("B", c_int32), ("q", c_int32), ("d", c_int32),
+                       ("Xq", _D), ("Xt_scaled", _D), ("n", c_int64), ("W", _D), ("ldw", c_int64),
+                       ("alpha", _D), ("dmean", _D), ("dcov", _D), ("E", _D), ("lde", c_int64),
+                       ("lengthscale", _D), ("outputscale", c_double), ("ystd", c_double),
+                       ("accumulate", c_int32), ("w_kmajor", c_int32), ("dX", _D)]
+
+
+class QehviArgs(_Args):
+    _fields_ = _HDR + [("B", c_int32), ("q", c_int32), ("m", c_int32), ("S", c_int32),
+                       ("mean", _D), ("L", _D), ("Z", _D), ("cell_lo", _D), ("cell_hi", _D),
+                       ("K", c_int32), ("Qp", c_int32), ("cell_stride", c_int64), ("F", _D),
+                       ("ldF", c_int64), ("sF", c_int64), ("acq", _D), ("dacq", _D),
+                       ("dmean", _D), ("dL", _D), ("dF", _D)]
+
+
+class LbfgsStepArgs(_Args):
+    _fields_ = _HDR + [("B", c_int32), ("n", c_int32), ("m", c_int32), ("_pad", c_int32),
+                       ("x", _D), ("f", _D), ("g", _D), ("xt", _D), ("ft", _D), ("gt", _D),
+                       ("d", _D), ("alpha", _D), ("S", _D), ("Y", _D), ("rho", _D),
+                       ("hcount", _D), ("hhead", _D), ("status", _D), ("nacc", _D),
+                       ("lower", _D), ("upper", _D), ("c1", c_double), ("ftol", c_double),
+                       ("pgtol", c_double), ("min_alpha", c_double)]
+
+
+for _name, _cls in (("bo_post_partials_v", PostPartialsArgs), ("bo_qmc_finalize_v", QmcFinalizeArgs),
+                    ("bo_qmc_backward_v", QmcBackwardArgs), ("bo_post_backward_v", PostBackwardArgs),
+                    ("bo_qehvi_v", QehviArgs), ("bo_qehvi_backward_v", QehviArgs),
+                    ("bo_lbfgs_step_v", LbfgsStepArgs)):
+    _SIGNATURES[_name] = (c_int, [POINTER(_cls), _P])
+_SIGNATURES["bo_struct_size"] = (c_int64, [ctypes.c_char_p])
+ARG_RECORDS = {"BoPostPartialsArgs": PostPartialsArgs, "BoQmcFinalizeArgs": QmcFinalizeArgs,
+               "BoQmcBackwardArgs": QmcBackwardArgs, "BoPostBackwardArgs": PostBackwardArgs,
+               "BoQehviArgs": QehviArgs, "BoLbfgsStepArgs": LbfgsStepArgs}
+
 _lib = None
 
 
@@ -116,6 +208,9 @@ def lib():
         if handle.bo_version() != ABI_VERSION:
             raise NativeLibraryMissing(
                 f"{LIB_PATH} has ABI {handle.bo_version()}, expected {ABI_VERSION}: rebuild with `make`")
+        for cname, rec in ARG_RECORDS.items():  # record layouts agree with the C header
+            if handle.bo_struct_size(cname.encode()) != sizeof(rec):
+                raise NativeLibraryMissing(f"{cname}: ctypes layout differs from the library's")
         _lib = handle
     return _lib
 

@@ -1,0 +1,93 @@
+// Parameter-struct entry points of the C ABI (include/botorch_amd.h, ABI 9):
+// each validates the struct header and forwards to the positional function.
+// Host code only (g++): no device work of its own.
+#include <cstdio>
+#include <string>
+
+#include "../../include/botorch_amd.h"
+
+void bo_set_error(const char* fmt, ...);
+
+namespace {
+
+template <class T>
+bool header_ok(const T* a, const char* name) {
+  if (!a) {
+    bo_set_error("%s: null argument struct", name);
+    return false;
+  }
+  if (a->struct_size != sizeof(T) || a->abi_version != BO_ABI_VERSION) {
+    bo_set_error("%s: struct size %u / ABI %u, library expects %zu / %d", name, a->struct_size,
+                 a->abi_version, sizeof(T), BO_ABI_VERSION);
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bo_post_partials_v(const BoPostPartialsArgs* a, void* stream) {
+  if (!header_ok(a, "bo_post_partials_v")) return BO_ERR_ARG;
+  return bo_post_partials(a->kind, a->Xq, a->B, a->q, a->d, a->Xt_scaled, a->n, a->U, a->ldu,
+                          a->beta, a->outputscale, a->Spart, a->mpart, a->Rt, a->kc_len, a->work,
+                          a->Qc, a->rq, a->ldq, a->Cx, a->Kt, stream);
+}
+
+int bo_qmc_finalize_v(const BoQmcFinalizeArgs* a, void* stream) {
+  if (!header_ok(a, "bo_qmc_finalize_v")) return BO_ERR_ARG;
+  return bo_qmc_finalize(a->kind, a->mode, a->B, a->q, a->Xq, a->Spart, a->mpart, a->n,
+                         a->outputscale, a->constant, a->ymean, a->ystd, a->Z, a->S, a->best_f,
+                         a->best_f_s, a->max_tries, a->jitter0, a->acq, a->mean_out, a->cov_out,
+                         a->L_out, a->info_out, a->jitter_out, a->Tm, a->r, a->ldT, a->F, a->ldF,
+                         a->fat, a->tau_relu, a->tau_max, stream);
+}
+
+int bo_qmc_backward_v(const BoQmcBackwardArgs* a, void* stream) {
+  if (!header_ok(a, "bo_qmc_backward_v")) return BO_ERR_ARG;
+  return bo_qmc_backward(a->mode, a->B, a->q, a->mean, a->Lq, a->Z, a->S, a->best_f, a->best_f_s,
+                         a->F, a->ldF, a->dacq, a->dmean, a->dcov, a->dF, a->acq_fwd, a->fat,
+                         a->tau_relu, a->tau_max, stream);
+}
+
+int bo_post_backward_v(const BoPostBackwardArgs* a, void* stream) {
+  if (!header_ok(a, "bo_post_backward_v")) return BO_ERR_ARG;
+  return bo_post_backward(a->kind, a->B, a->q, a->d, a->Xq, a->Xt_scaled, a->n, a->W, a->ldw,
+                          a->alpha, a->dmean, a->dcov, a->E, a->lde, a->lengthscale,
+                          a->outputscale, a->ystd, a->accumulate, a->dX, a->w_kmajor, stream);
+}
+
+int bo_qehvi_v(const BoQehviArgs* a, void* stream) {
+  if (!header_ok(a, "bo_qehvi_v")) return BO_ERR_ARG;
+  return bo_qehvi(a->B, a->q, a->m, a->mean, a->L, a->Z, a->S, a->cell_lo, a->cell_hi, a->K,
+                  a->cell_stride, a->F, a->ldF, a->sF, a->Qp, a->acq, stream);
+}
+
+int bo_qehvi_backward_v(const BoQehviArgs* a, void* stream) {
+  if (!header_ok(a, "bo_qehvi_backward_v")) return BO_ERR_ARG;
+  return bo_qehvi_backward(a->B, a->q, a->m, a->mean, a->L, a->Z, a->S, a->cell_lo, a->cell_hi,
+                           a->K, a->cell_stride, a->F, a->ldF, a->sF, a->Qp, a->dacq, a->dmean,
+                           a->dL, a->dF, stream);
+}
+
+int bo_lbfgs_step_v(const BoLbfgsStepArgs* a, void* stream) {
+  if (!header_ok(a, "bo_lbfgs_step_v")) return BO_ERR_ARG;
+  return bo_lbfgs_step(a->B, a->n, a->m, a->x, a->f, a->g, a->xt, a->ft, a->gt, a->d, a->alpha,
+                       a->S, a->Y, a->rho, a->hcount, a->hhead, a->status, a->nacc, a->lower,
+                       a->upper, a->c1, a->ftol, a->pgtol, a->min_alpha, stream);
+}
+
+}  // extern "C"
+
+// sizeof of each argument record (HOST, for bindings to verify their layouts).
+extern "C" int64_t bo_struct_size(const char* name) {
+  const std::string s = name ? name : "";
+  if (s == "BoPostPartialsArgs") return sizeof(BoPostPartialsArgs);
+  if (s == "BoQmcFinalizeArgs") return sizeof(BoQmcFinalizeArgs);
+  if (s == "BoQmcBackwardArgs") return sizeof(BoQmcBackwardArgs);
+  if (s == "BoPostBackwardArgs") return sizeof(BoPostBackwardArgs);
+  if (s == "BoQehviArgs") return sizeof(BoQehviArgs);
+  if (s == "BoLbfgsStepArgs") return sizeof(BoLbfgsStepArgs);
+  return -1;
+}

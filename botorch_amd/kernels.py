@@ -287,13 +287,13 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
         Rt = torch.empty(nC * 128, nrows_pad, **f64)  # the caller forms the cross term from R^T
     if TIMING_HOOK is not None:
         TIMING_HOOK("post_partials_begin")
-    check(lib().bo_post_partials(cache.kind, _p(Xq), B, q, d, _p(cache.Xt_scaled), cache.n,
-                                 _p(cache.U), cache.np, _p(cache.beta), cache.outputscale,
-                                 _p(Spart), _p(mpart), _p(Rt), kc_len, _p(work),
-                                 _p(cross if Cx is not None else None),
-                                 cross.shape[0] if Cx is not None else 0,
-                                 cross.shape[1] if Cx is not None else 0, _p(Cx), _p(Kt), st),
-          "post_partials")
+    a = _lib.PostPartialsArgs(kind=cache.kind, B=B, q=q, d=d, Xq=Xq, Xt_scaled=cache.Xt_scaled,
+                              n=cache.n, U=cache.U, ldu=cache.np, beta=cache.beta,
+                              outputscale=cache.outputscale, Spart=Spart, mpart=mpart, Rt=Rt,
+                              kc_len=kc_len, work=work, Qc=cross if Cx is not None else None,
+                              rq=cross.shape[0] if Cx is not None else 0,
+                              ldq=cross.shape[1] if Cx is not None else 0, Cx=Cx, Kt=Kt)
+    check(lib().bo_post_partials_v(ctypes.byref(a), st), "post_partials")
     if TIMING_HOOK is not None:
         TIMING_HOOK("post_partials_end")
     return PostPartials(B, q, Qp, nrows_pad, nC, Xq, Spart, mpart, Rt,
@@ -321,14 +321,17 @@ def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd
     S = Z.shape[0] if Z is not None else 0
     if Z is not None:
         Z = Z.reshape(S, q).contiguous()
-    check(lib().bo_qmc_finalize(cache.kind, mode, B, q, _p(pp.Xq), _p(pp.Spart), _p(pp.mpart),
-                                cache.n, cache.outputscale, cache.constant, float(ymean),
-                                float(ystd), _p(Z), S, float(best_f), _p(best_f_s), max_tries,
-                                jitter0, _p(acq), _p(mean), _p(cov), _p(L), _p(info), _p(jit),
-                                _p(T), T.shape[0] if T is not None else 0,
-                                T.shape[1] if T is not None else 0, _p(F),
-                                F.shape[1] if F is not None else 0, int(bool(fat)),
-                                float(tau_relu), float(tau_max), _stream(dev)), "qmc_finalize")
+    a = _lib.QmcFinalizeArgs(kind=cache.kind, mode=mode, B=B, q=q, Xq=pp.Xq, Spart=pp.Spart,
+                             mpart=pp.mpart, n=cache.n, outputscale=cache.outputscale,
+                             constant=cache.constant, ymean=float(ymean), ystd=float(ystd), Z=Z,
+                             S=S, max_tries=max_tries, best_f=float(best_f), best_f_s=best_f_s,
+                             jitter0=jitter0, acq=acq, mean_out=mean, cov_out=cov, L_out=L,
+                             info_out=info, jitter_out=jit, Tm=T,
+                             r=T.shape[0] if T is not None else 0, fat=int(bool(fat)),
+                             ldT=T.shape[1] if T is not None else 0, F=F,
+                             ldF=F.shape[1] if F is not None else 0, tau_relu=float(tau_relu),
+                             tau_max=float(tau_max))
+    check(lib().bo_qmc_finalize_v(ctypes.byref(a), _stream(dev)), "qmc_finalize")
     return dict(acq=acq, mean=mean, cov=cov, L=L, info=info, jitter=jit)
 
 
@@ -419,11 +422,13 @@ def qmc_backward(mode: int, mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor
     fat, tau_relu, tau_max = log_params if log_params is not None else (1, 1.0, 1.0)
     if acq_fwd is not None:
         acq_fwd = acq_fwd.contiguous()
-    check(lib().bo_qmc_backward(mode, B, q, _p(mean), _p(L), _p(Z.reshape(S, q).contiguous()), S,
-                                float(best_f), _p(best_f_s), _p(F),
-                                F.shape[1] if F is not None else 0, _p(dacq.contiguous()),
-                                _p(dmean), _p(dcov), _p(dF), _p(acq_fwd), int(bool(fat)),
-                                float(tau_relu), float(tau_max), _stream(dev)), "qmc_backward")
+    a = _lib.QmcBackwardArgs(mode=mode, B=B, q=q, S=S, mean=mean, Lq=L,
+                             Z=Z.reshape(S, q).contiguous(), best_f=float(best_f),
+                             best_f_s=best_f_s, F=F, ldF=F.shape[1] if F is not None else 0,
+                             dacq=dacq.contiguous(), dmean=dmean, dcov=dcov, dF=dF,
+                             acq_fwd=acq_fwd, fat=int(bool(fat)), tau_relu=float(tau_relu),
+                             tau_max=float(tau_max))
+    check(lib().bo_qmc_backward_v(ctypes.byref(a), _stream(dev)), "qmc_backward")
     if F is not None:
         return dmean, dcov, dF
     return dmean, dcov
@@ -448,13 +453,15 @@ def post_backward(cache: GPCache, pp: PostPartials, W: Optional[WMat],
     kmajor = W is not None and W.kmajor
     W = cont(W.t) if W is not None else None
     E, dmean, dcov = cont(E), cont(dmean), cont(dcov)
-    check(lib().bo_post_backward(cache.kind, pp.B, pp.q, cache.d, _p(pp.Xq),
-                                 _p(Xt_scaled if other else cache.Xt_scaled),
-                                 n if other else cache.n, _p(W), W.shape[1] if W is not None else 0,
-                                 None if other else _p(cache.alpha), _p(dmean), _p(dcov), _p(E),
-                                 E.shape[1] if E is not None else 0, _p(cache.lengthscale),
-                                 cache.outputscale, float(ystd), int(acc), _p(dX),
-                                 int(kmajor), _stream(dev)), "post_backward")
+    a = _lib.PostBackwardArgs(kind=cache.kind, B=pp.B, q=pp.q, d=cache.d, Xq=pp.Xq,
+                              Xt_scaled=Xt_scaled if other else cache.Xt_scaled,
+                              n=n if other else cache.n, W=W,
+                              ldw=W.shape[1] if W is not None else 0,
+                              alpha=None if other else cache.alpha, dmean=dmean, dcov=dcov, E=E,
+                              lde=E.shape[1] if E is not None else 0,
+                              lengthscale=cache.lengthscale, outputscale=cache.outputscale,
+                              ystd=float(ystd), accumulate=int(acc), w_kmajor=int(kmajor), dX=dX)
+    check(lib().bo_post_backward_v(ctypes.byref(a), _stream(dev)), "post_backward")
     return dX
 
 
@@ -685,12 +692,12 @@ def qehvi(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor, cell_lo: torch.T
     K, cstride = _cells_layout(cell_lo, S)
     acq = torch.empty(B, dtype=torch.float64, device=dev)
     Fc = F.contiguous() if F is not None else None
-    check(lib().bo_qehvi(B, q, m, _p(mean.contiguous()), _p(L.contiguous()),
-                         _p(Z.reshape(S, q * m).contiguous()), S, _p(cell_lo.contiguous()),
-                         _p(cell_hi.contiguous()), K, cstride, _p(Fc),
-                         Fc.shape[-1] if Fc is not None else 0,
-                         Fc.shape[-1] * S if Fc is not None else 0, Qp, _p(acq), _stream(dev)),
-          "qehvi")
+    a = _lib.QehviArgs(B=B, q=q, m=m, S=S, mean=mean.contiguous(), L=L.contiguous(),
+                       Z=Z.reshape(S, q * m).contiguous(), cell_lo=cell_lo.contiguous(),
+                       cell_hi=cell_hi.contiguous(), K=K, Qp=Qp, cell_stride=cstride, F=Fc,
+                       ldF=Fc.shape[-1] if Fc is not None else 0,
+                       sF=Fc.shape[-1] * S if Fc is not None else 0, acq=acq)
+    check(lib().bo_qehvi_v(ctypes.byref(a), _stream(dev)), "qehvi")
     return acq
 
 
@@ -706,13 +713,13 @@ def qehvi_backward(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor, cell_lo
     dL = torch.empty(m, B, q, q, dtype=torch.float64, device=dev)
     Fc = F.contiguous() if F is not None else None
     dF = torch.zeros_like(Fc) if Fc is not None else None
-    check(lib().bo_qehvi_backward(B, q, m, _p(mean.contiguous()), _p(L.contiguous()),
-                                  _p(Z.reshape(S, q * m).contiguous()), S,
-                                  _p(cell_lo.contiguous()), _p(cell_hi.contiguous()), K, cstride,
-                                  _p(Fc), Fc.shape[-1] if Fc is not None else 0,
-                                  Fc.shape[-1] * S if Fc is not None else 0, Qp,
-                                  _p(dacq.contiguous()), _p(dmean), _p(dL), _p(dF),
-                                  _stream(dev)), "qehvi_backward")
+    a = _lib.QehviArgs(B=B, q=q, m=m, S=S, mean=mean.contiguous(), L=L.contiguous(),
+                       Z=Z.reshape(S, q * m).contiguous(), cell_lo=cell_lo.contiguous(),
+                       cell_hi=cell_hi.contiguous(), K=K, Qp=Qp, cell_stride=cstride, F=Fc,
+                       ldF=Fc.shape[-1] if Fc is not None else 0,
+                       sF=Fc.shape[-1] * S if Fc is not None else 0, dacq=dacq.contiguous(),
+                       dmean=dmean, dL=dL, dF=dF)
+    check(lib().bo_qehvi_backward_v(ctypes.byref(a), _stream(dev)), "qehvi_backward")
     if F is not None:
         return dmean, dL, dF
     return dmean, dL

@@ -329,7 +329,9 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
 
     ``maxiter`` bounds the function evaluations per restart (scipy's own
     ``maxfun`` analogue); returns (candidates b x q x d, acq values b)."""
-    from . import kernels
+    import ctypes
+
+    from . import _lib, kernels
     from ._lib import check, lib
     if fixed_features:
         raise NotImplementedError("fixed_features is not supported by the device optimiser")
@@ -360,10 +362,12 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
         (gt,) = torch.autograd.grad(ft.sum(), Xt)
         ft = ft.detach().reshape(-1).to(torch.float64).contiguous()
         gt = gt.reshape(st.B, st.n).to(torch.float64).contiguous()
-        check(lib().bo_lbfgs_step(st.B, st.n, m, P(st.x), P(st.f), P(st.g), P(st.xt), P(ft), P(gt),
-                                  P(st.d), P(st.alpha), P(st.S), P(st.Y), P(st.rho), P(st.hcount),
-                                  P(st.hhead), P(st.status), P(st.nacc), P(lo), P(hi), 1e-4, ftol,
-                                  pgtol, 1e-12, stream), "lbfgs_step")
+        a = _lib.LbfgsStepArgs(B=st.B, n=st.n, m=m, x=st.x, f=st.f, g=st.g, xt=st.xt, ft=ft, gt=gt,
+                               d=st.d, alpha=st.alpha, S=st.S, Y=st.Y, rho=st.rho,
+                               hcount=st.hcount, hhead=st.hhead, status=st.status, nacc=st.nacc,
+                               lower=lo, upper=hi, c1=1e-4, ftol=ftol, pgtol=pgtol,
+                               min_alpha=1e-12)
+        check(lib().bo_lbfgs_step_v(ctypes.byref(a), stream), "lbfgs_step")
         if (it + 1) % check_every == 0 or it == maxiter:
             if bool((st.status > 0).all()):
                 break

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 8
+#define BO_ABI_VERSION 9
 
 /* status codes */
 #define BO_OK 0
@@ -406,6 +406,122 @@ int bo_nd_partition_host(const double* Y, int64_t S, int64_t n, int m, const dou
 int bo_sobol_box(const int64_t* state, const int64_t* shift, int dim, int64_t n, int64_t skip,
                  int first_f32, const double* lower, const double* range, int d, double* out,
                  void* stream);
+
+/* ---- Parameter-struct entry points (ABI 9) ------------------------------------
+ * The widest calls above also take one struct of named fields, so a binding
+ * declares a record instead of a positional list of 20-33 arguments.  Every
+ * struct opens with struct_size = sizeof(struct) and abi_version =
+ * BO_ABI_VERSION; a mismatch returns BO_ERR_ARG (never a misread field).  Field
+ * meanings are those of the positional function named in each comment; each
+ * _v function forwards to it. */
+#define BO_STRUCT_HEADER \
+  uint32_t struct_size;  \
+  uint32_t abi_version
+
+typedef struct BoPostPartialsArgs { /* bo_post_partials */
+  BO_STRUCT_HEADER;
+  int32_t kind, B, q, d;
+  const double* Xq;
+  const double* Xt_scaled;
+  int64_t n;
+  const double* U;
+  int64_t ldu;
+  const double* beta;
+  double outputscale;
+  double *Spart, *mpart, *Rt;
+  int32_t kc_len, rq;
+  double* work;
+  const double* Qc;
+  int64_t ldq;
+  double* Cx;
+  const double* Kt;
+} BoPostPartialsArgs;
+int bo_post_partials_v(const BoPostPartialsArgs* a, void* stream);
+
+typedef struct BoQmcFinalizeArgs { /* bo_qmc_finalize */
+  BO_STRUCT_HEADER;
+  int32_t kind, mode, B, q;
+  const double *Xq, *Spart, *mpart;
+  int64_t n;
+  double outputscale, constant, ymean, ystd;
+  const double* Z;
+  int32_t S, max_tries;
+  double best_f;
+  const double* best_f_s;
+  double jitter0;
+  double *acq, *mean_out, *cov_out, *L_out;
+  int* info_out;
+  double* jitter_out;
+  const double* Tm;
+  int32_t r, fat;
+  int64_t ldT;
+  const double* F;
+  int64_t ldF;
+  double tau_relu, tau_max;
+} BoQmcFinalizeArgs;
+int bo_qmc_finalize_v(const BoQmcFinalizeArgs* a, void* stream);
+
+typedef struct BoQmcBackwardArgs { /* bo_qmc_backward */
+  BO_STRUCT_HEADER;
+  int32_t mode, B, q, S;
+  const double *mean, *Lq, *Z;
+  double best_f;
+  const double *best_f_s, *F;
+  int64_t ldF;
+  const double* dacq;
+  double *dmean, *dcov, *dF;
+  const double* acq_fwd;
+  int32_t fat, _pad;
+  double tau_relu, tau_max;
+} BoQmcBackwardArgs;
+int bo_qmc_backward_v(const BoQmcBackwardArgs* a, void* stream);
+
+typedef struct BoPostBackwardArgs { /* bo_post_backward */
+  BO_STRUCT_HEADER;
+  int32_t kind, B, q, d;
+  const double *Xq, *Xt_scaled;
+  int64_t n;
+  const double* W;
+  int64_t ldw;
+  const double *alpha, *dmean, *dcov, *E;
+  int64_t lde;
+  const double* lengthscale;
+  double outputscale, ystd;
+  int32_t accumulate, w_kmajor;
+  double* dX;
+} BoPostBackwardArgs;
+int bo_post_backward_v(const BoPostBackwardArgs* a, void* stream);
+
+typedef struct BoQehviArgs { /* bo_qehvi and bo_qehvi_backward (d* fields: backward only) */
+  BO_STRUCT_HEADER;
+  int32_t B, q, m, S;
+  const double *mean, *L, *Z, *cell_lo, *cell_hi;
+  int32_t K, Qp;
+  int64_t cell_stride;
+  const double* F;
+  int64_t ldF, sF;
+  double* acq;
+  const double* dacq;
+  double *dmean, *dL, *dF;
+} BoQehviArgs;
+int bo_qehvi_v(const BoQehviArgs* a, void* stream);
+int bo_qehvi_backward_v(const BoQehviArgs* a, void* stream);
+
+typedef struct BoLbfgsStepArgs { /* bo_lbfgs_step */
+  BO_STRUCT_HEADER;
+  int32_t B, n, m, _pad;
+  double *x, *f, *g, *xt;
+  const double *ft, *gt;
+  double *d, *alpha, *S, *Y, *rho;
+  int *hcount, *hhead, *status, *nacc;
+  const double *lower, *upper;
+  double c1, ftol, pgtol, min_alpha;
+} BoLbfgsStepArgs;
+int bo_lbfgs_step_v(const BoLbfgsStepArgs* a, void* stream);
+
+/* HOST: sizeof the named record ("BoPostPartialsArgs", ...), -1 if unknown --
+ * lets a binding check its declared layout once at load time. */
+int64_t bo_struct_size(const char* name);
 
 #ifdef __cplusplus
 }

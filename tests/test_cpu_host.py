@@ -39,7 +39,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(handle, s), s
     assert set(syms) == set(_lib.exported_symbols()), set(syms) ^ set(_lib.exported_symbols())
     lib = _lib.lib()
-    assert lib.bo_version() == _lib.ABI_VERSION == 8
+    assert lib.bo_version() == _lib.ABI_VERSION == 9
     assert lib.bo_padded_order(4096) == 4096 and lib.bo_padded_order(20) == 128
 
 
@@ -82,3 +82,23 @@ def test_custom_ops_registered_with_meta_shapes():
     assert outs[0].shape == (B,) and outs[7].dtype == torch.int32
     Sp, mp, Xq2, Rt2 = torch.ops.bo.post_partials(X, Xt, Xs, U, beta, ls, 0, 1.0, False)
     assert Sp.shape == (3, 8, 16, 16) and mp.shape == (3, 128) and Rt2.numel() == 0
+
+
+def test_arg_records_match_c_layout():
+    """ABI-9 parameter records: the ctypes layouts equal the C header's sizeof,
+    the header fields are filled, and a wrong abi_version / struct_size is
+    refused with an error code before anything is launched."""
+    import ctypes
+    from botorch_amd import _lib
+    lib = _lib.lib()
+    for cname, rec in _lib.ARG_RECORDS.items():
+        assert lib.bo_struct_size(cname.encode()) == ctypes.sizeof(rec), cname
+        r = rec()
+        assert r.struct_size == ctypes.sizeof(rec) and r.abi_version == _lib.ABI_VERSION
+    assert lib.bo_struct_size(b"NoSuchStruct") < 0
+    a = _lib.PostPartialsArgs(B=1, q=1, d=1)
+    a.abi_version = 8
+    assert lib.bo_post_partials_v(ctypes.byref(a), None) != 0
+    a = _lib.LbfgsStepArgs(B=1, n=1, m=1)
+    a.struct_size = 8
+    assert lib.bo_lbfgs_step_v(ctypes.byref(a), None) != 0
