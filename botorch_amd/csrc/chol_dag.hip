@@ -33,7 +33,7 @@
 // (s_waitcnt vmcnt(0)), a workgroup barrier, then ONE lane publishes the tile's
 // counter with an agent-scope atomic store; consumers poll that word with an
 // agent-scope (sc1) load and read the tiles with sc1 loads only (L1 bypassed),
-// one workgroup per CU (the 104 KB LDS footprint admits one).
+// one workgroup per CU.
 #include <algorithm>
 #include <map>
 #include <utility>
@@ -56,6 +56,10 @@ typedef unsigned int u32;
 typedef u32 v2u __attribute__((ext_vector_type(2)));
 typedef u32 v4u __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+// the diagonal block's column counter: an explicit LDS pointer, so polls and
+// updates are ds_read / ds_write (a generic volatile pointer becomes a flat
+// access with a full vmcnt drain per column)
+typedef volatile __attribute__((address_space(3))) int lds_cnt_t;
 
 constexpr int SC1 = 16;  // cache-policy bit: write-through store / L1-bypassing load
 
@@ -147,6 +151,8 @@ __device__ __forceinline__ void acc_load(const Ctx& c, Acc& a, rsrc_t r, int ti,
                                    c.wn + 16 * j + mfma_col(c.lane)));
 }
 
+// (8-B accesses in the MFMA layout: 16-B ones after a lane-pair exchange
+// measured slower, 2.38 -> 2.47 ms at n = 4096)
 __device__ __forceinline__ void acc_store(const Ctx& c, const Acc& a, rsrc_t r, int ti, int tj) {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -321,7 +327,7 @@ __device__ __forceinline__ void col_updates(std::integer_sequence<int, M...>, do
 // inverse built concurrently on wave 1 (diag_inv_step).
 template <int JJ>
 __device__ __forceinline__ void diag_step(double (&v)[16], int r, int g, bool lane0, int& fail,
-                                          double* rinv, double* Lc, volatile int* cnt, int cbase) {
+                                          double* rinv, double* Lc, lds_cnt_t* cnt, int cbase) {
   const double piv = row_bcast<JJ>(v[JJ]);
   if (!(piv > 0.0) && fail == 0) fail = JJ + 1;
   const double rr = rsq_nr(piv);
@@ -338,7 +344,7 @@ __device__ __forceinline__ void diag_step(double (&v)[16], int r, int g, bool la
 template <int... JJ>
 __device__ __forceinline__ void diag_steps(std::integer_sequence<int, JJ...>, double (&v)[16],
                                            int r, int g, bool lane0, int& fail, double* rinv,
-                                           double* Lc, volatile int* cnt, int cbase) {
+                                           double* Lc, lds_cnt_t* cnt, int cbase) {
   (diag_step<JJ>(v, r, g, lane0, fail, rinv, Lc, cnt, cbase), ...);
 }
 
@@ -347,7 +353,7 @@ __device__ __forceinline__ void diag_steps(std::integer_sequence<int, JJ...>, do
 // and eliminated from the rows below (forward substitution).
 template <int JJ>
 __device__ __forceinline__ void diag_inv_step(double (&x)[4], int r, const double* rinv,
-                                              const double* Lc, volatile int* cnt, int cbase) {
+                                              const double* Lc, lds_cnt_t* cnt, int cbase) {
   while (*cnt < cbase + JJ + 1) __builtin_amdgcn_s_sleep(0);
   const double rr = rinv[JJ];
   const double l = Lc[JJ * 16 + r];
@@ -362,7 +368,7 @@ __device__ __forceinline__ void diag_inv_step(double (&x)[4], int r, const doubl
 template <int... JJ>
 __device__ __forceinline__ void diag_inv_steps(std::integer_sequence<int, JJ...>, double (&x)[4],
                                                int r, const double* rinv, const double* Lc,
-                                               volatile int* cnt, int cbase) {
+                                               lds_cnt_t* cnt, int cbase) {
   (diag_inv_step<JJ>(x, r, rinv, Lc, cnt, cbase), ...);
 }
 
@@ -396,7 +402,7 @@ __device__ __forceinline__ void put16(double* D, v4d a, int lane, double scale) 
 // inverses by recursive doubling, X21 = -X22 L21 X11 (16 -> 32 -> 64), on the
 // MFMA; the strictly-upper blocks of S serve as scratch for the products.
 __device__ void potrf_trtri64(const Ctx& c, double* S, double* D, double* rinv, int* info, int row0,
-                              double* Lc, volatile int* cnt, long long* ct = nullptr) {
+                              double* Lc, lds_cnt_t* cnt, long long* ct = nullptr) {
   for (int e = c.tid; e < TB * TB; e += 256) D[(e >> 6) * LP + (e & 63)] = 0.0;
   if (c.tid == 0) *cnt = 0;
   __syncthreads();
@@ -521,12 +527,11 @@ __device__ __forceinline__ void row_deps(const Flags& f, int i, int j, int k, co
 template <int KIND>
 __device__ __forceinline__ void row_issue(const Ctx& c, int i, int j, int k, double2 (&pv)[8],
                                           double (&pa)[16]) {
-  const int ti = i, tj = KIND == 0 ? k : k;
   if (!(KIND == 1 && i == j)) {
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
       const int e = c.tid + 256 * p;
-      pv[p] = ld16(c.rA, toff(c, ti, tj, e >> 5, (e & 31) * 2));
+      pv[p] = ld16(c.rA, toff(c, i, k, e >> 5, (e & 31) * 2));
     }
   }
   if (KIND == 1 || (KIND == 2 && k > j)) {
@@ -642,7 +647,6 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
                                                        long long* __restrict__ trace) {
   __shared__ __attribute__((aligned(16))) double X0[TB * LP];
   __shared__ __attribute__((aligned(16))) double X1[TB * LP];
-  __shared__ __attribute__((aligned(16))) double X2[TB * LP];
   __shared__ double rinv[TB];
   __shared__ double Lcol[512];  // diagonal-block columns, double-buffered by block parity
   __shared__ int s_cnt;
@@ -693,14 +697,16 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
           __syncthreads();
           acc_zero(acc);
           acc_mma_nt(c, acc, X0, X1, 1.0);  // L_{k,k-1} = A_{k,k-1} D_{k-1}^T
-          acc_to_lds(c, acc, X2);
+          __syncthreads();                  // every wave's reads of X0 done
+          acc_to_lds(c, acc, X0);
           acc_store(c, acc, c.rA, k, k - 1);
           publish(c, F(fL, k, k - 1), 1u);
           ok = wait2(c, F(fA, k, k), (u32)(k - 1), F(fA, k, k), (u32)(k - 1), abortw, &s_ok, &wsum);
         }
         if (ok) {
           acc_load(c, acc, c.rA, k, k);
-          acc_mma_nt(c, acc, X2, X2, -1.0);  // A_kk -= L L^T (step k - 1)
+          acc_mma_nt(c, acc, X0, X0, -1.0);  // A_kk -= L L^T (step k - 1)
+          __syncthreads();
           acc_to_lds(c, acc, X0);
         }
       } else {
@@ -710,7 +716,7 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
         __syncthreads();
         long long* ct = trace ? trace + 4 * ntasks + 8 * k : nullptr;
         if (ct && c.tid == 0) ct[0] = wall_clock64();
-        potrf_trtri64(c, X0, X1, rinv, info, k * TB, Lcol, &s_cnt, ct);
+        potrf_trtri64(c, X0, X1, rinv, info, k * TB, Lcol, (lds_cnt_t*)&s_cnt, ct);
         if (ct && c.tid == 0) ct[1] = wall_clock64();
         if (ct && c.tid == 0) ct[2] = wall_clock64();
         lds_to_tile(c, X0, c.rA, k, k);
@@ -734,10 +740,11 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
         ok = wait2(c, F(fX, k, j), (u32)(k - j), F(fL, k, k), 1u, abortw, &s_ok, &wsum);
         if (ok) {
           tile_to_lds(c, c.rI, k, k, X0);  // D_k
-          tile_to_lds(c, c.rI, k, j, X2);  // acc_kj
+          tile_to_lds(c, c.rI, k, j, X1);  // acc_kj
           __syncthreads();
           acc_zero(acc);
-          acc_mma<false>(c, acc, X0, X2, -1.0);  // X_kj = -D_k acc_kj
+          acc_mma<false>(c, acc, X0, X1, -1.0);  // X_kj = -D_k acc_kj
+          __syncthreads();
           acc_to_lds_t(c, acc, X1);
           acc_store(c, acc, c.rI, k, j);
           publish(c, F(fXd, k, j), 1u);
@@ -944,6 +951,8 @@ int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipS
   BO_HIP(hipMemsetAsync(work, 0, fbytes, st));
   BO_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
   BO_HIP(hipMemsetAsync(Linv, 0, sizeof(double) * np * np, st));
+  // one workgroup per CU: two per CU (74 KB of LDS each fits) measured slower,
+  // 2.35 -> 2.97 ms at n = 4096 -- the sc1 tile traffic, not latency, is the limit
   const int grid = cus < tb->n ? cus : tb->n;
   chol_dag_kernel<<<grid, 256, 0, st>>>(A, Linv, (int)np, T, tb->dev, tb->n, (u32*)work, info,
                                           trace);

@@ -22,16 +22,25 @@
 // materialised (C3: 268 MB saved per forward).
 //
 // Small problems (C2: 8 column tiles x 4 row tiles = 32 workgroups for 256
-// CUs) run split-k: each column tile's triangular k-range is cut into chunks,
-// every (chunk, column tile, row tile) is a workgroup that writes its partial
-// R^T accumulators to a workspace, and post_splitk_reduce_kernel sums the
-// chunks in chunk order (deterministic) and runs the same epilogue.
+// CUs; a rank's b = 64 share of C3: 256 tiles of very unequal triangular
+// k-ranges) run split: a host-built segment table gives every workgroup a list
+// of (tile, k-range) segments.  The stream-K plan cuts the concatenated
+// k-steps of all tiles (heaviest column tile first, row tiles inner) into one
+// equal share per resident slot, so no slot idles behind the longest column
+// tile; the uniform plan cuts every tile into chunks of kc_len.  A segment
+// that covers its whole tile runs the epilogue itself; the others write their
+// partial R^T accumulators to a workspace and post_splitk_reduce_kernel sums
+// each tile's chunks in k order (deterministic) and runs the same epilogue.
 //
 // Test rows are laid out per t-batch: row b*Qp + a, a < q, Qp = q rounded up
 // to a power of two <= 16, so every t-batch sits inside one 16-row MFMA tile.
 #include "common.h"
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
 
 namespace {
 
@@ -131,9 +140,9 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     const double* __restrict__ Xq, int nrows, const double* __restrict__ Xt, int n,
     const double* __restrict__ U, int64_t ldu, const double* __restrict__ beta,
     double outputscale, int nC, int nI, double* __restrict__ Spart, double* __restrict__ mpart,
-    double* __restrict__ Rt, int kc_len, double* __restrict__ work,
-    const double* __restrict__ Qc, int rq, int64_t ldq, double* __restrict__ Cx,
-    const double* __restrict__ Kt, int grouped) {
+    double* __restrict__ Rt, const int4* __restrict__ segs, const int* __restrict__ wg_off,
+    double* __restrict__ work, const double* __restrict__ Qc, int rq, int64_t ldq,
+    double* __restrict__ Cx, const double* __restrict__ Kt, int grouped) {
   // Two LDS stages: while the MFMAs consume stage t, the U rows of step t+1
   // are in flight to registers and this thread evaluates its 8 kernel values
   // of step t+1 between the MFMAs (VALU work hidden under the matrix pipe);
@@ -142,18 +151,9 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   __shared__ __attribute__((aligned(16))) double Ks[2][PK][PLD];
 
   const int bid = blockIdx.x;
-  int ci, ii, kc = 0, kbeg = 0, kend;
+  int ci = 0, ii = 0, kbeg = 0, kend = 0;
   if constexpr (SPLIT) {
-    // Split-k: block -> (column tile, chunk, row tile), row tiles fastest so
-    // neighbouring blocks read the same U chunk.
-    const int nk = (n + kc_len - 1) / kc_len;
-    ii = bid % nI;
-    const int rest = bid / nI;
-    kc = rest % nk;
-    ci = rest / nk;
-    if (ci >= nC || kc >= splitk_chunks(ci, n, kc_len)) return;
-    kbeg = kc * kc_len;
-    kend = min(min(n, ci * PC + PC), kbeg + kc_len);
+    // segments come from the table below
   } else if (grouped) {
     // Grouped XCD schedule (nC, nI multiples of 8): consecutive block ids are
     // dealt round-robin over the 8 XCDs, so block b and b+8 share an L2.  The
@@ -195,6 +195,24 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     ci = nC - 1 - ci;
     kbeg = ci * PC;
     kend = n;
+  }
+  // Split plans: this workgroup's segments (uniform control flow: every
+  // thread walks the same list; the last k-step's barrier frees the LDS
+  // stages before the next segment's prologue writes them).
+  int sbeg = 0, send = 1;
+  if constexpr (SPLIT) {
+    sbeg = wg_off[bid];
+    send = wg_off[bid + 1];
+  }
+  for (int sidx = sbeg; sidx < send; ++sidx) {
+  int chunk = -1;
+  if constexpr (SPLIT) {
+    const int4 sg = segs[sidx];
+    ci = sg.x & 0xffff;
+    ii = sg.x >> 16;
+    kbeg = sg.y;
+    kend = sg.z;
+    chunk = sg.w;  // -1: the segment covers its whole tile
   }
   const int c0 = ci * PC;
   const int i0 = ii * PI;
@@ -352,14 +370,12 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
       }
   }
 
-  if constexpr (SPLIT) {
+  if (SPLIT && chunk >= 0) {
     // Partial R^T of this chunk: register-major, lane-minor per 16-row tile,
     // so every store instruction writes 512 contiguous bytes.
-    const int64_t chunk = splitk_base(ci, n, kc_len) + kc;
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-      const int rt = ii * (PI / 16) + wave * 2 + it;
-      double* w = work + (chunk * (nI * (PI / 16)) + rt) * kTileDoubles + lane;
+      double* w = work + ((int64_t)chunk * (PI / 16) + wave * 2 + it) * kTileDoubles + lane;
 #pragma unroll
       for (int ct = 0; ct < 8; ++ct)
 #pragma unroll
@@ -382,7 +398,7 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
             Rt[(int64_t)c * nrows_pad + i] = acc[ct][it][r];
           }
     }
-    if constexpr (LOWERK) return;  // W^T only
+    if constexpr (!LOWERK) {  // LOWERK: W^T only
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       v4d P = v4d_zero();
@@ -406,7 +422,9 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
       m += __shfl_xor(m, 32);
       if (lane < 16) mpart[(int64_t)ci * nrows_pad + row0 + lane] = m;
     }
+    }
   }
+  }  // segments
 }
 
 // K*x^T once per call: Kt[k][i] = outputscale k(x_i, x_k), zero for k >= n
@@ -434,24 +452,22 @@ __global__ __launch_bounds__(256) void kxt_build_kernel(const double* __restrict
   }
 }
 
-// Split-k reduction: one wave per (column tile, 16-row tile) sums the chunk
-// partials in chunk order and runs the epilogue.
+// Split reduction: one wave per 16-row tile of every tile split over several
+// chunks (red: column tile, row tile, first chunk, chunk count) sums the
+// chunk partials in k order and runs the epilogue.
 __global__ __launch_bounds__(64) void post_splitk_reduce_kernel(
-    const double* __restrict__ work, int n, int nC, int nI, int kc_len,
+    const double* __restrict__ work, const int4* __restrict__ red, int n, int nI,
     const double* __restrict__ beta, double* __restrict__ Spart, double* __restrict__ mpart,
     double* __restrict__ Rt) {
-  const int nrows16 = nI * (PI / 16);
-  const int rt = blockIdx.x % nrows16;
-  const int ci = blockIdx.x / nrows16;
-  if (ci >= nC) return;
+  const int4 r4 = red[blockIdx.x / (PI / 16)];
+  const int sub = blockIdx.x % (PI / 16);
+  const int ci = r4.x, rt = r4.y * (PI / 16) + sub;
   const int lane = threadIdx.x;
-  const int nk = splitk_chunks(ci, n, kc_len);
-  const int64_t base = splitk_base(ci, n, kc_len);
   v4d acc[8];
 #pragma unroll
   for (int ct = 0; ct < 8; ++ct) acc[ct] = v4d_zero();
-  for (int kc = 0; kc < nk; ++kc) {
-    const double* w = work + ((base + kc) * nrows16 + rt) * kTileDoubles + lane;
+  for (int c = r4.z; c < r4.z + r4.w; ++c) {
+    const double* w = work + ((int64_t)c * (PI / 16) + sub) * kTileDoubles + lane;
 #pragma unroll
     for (int ct = 0; ct < 8; ++ct)
 #pragma unroll
@@ -475,6 +491,106 @@ __global__ void prepare_rows_kernel(const double* __restrict__ X, int B, int q, 
   double v = 0.0;
   if (b < B && a < q && t < d) v = X[(b * q + a) * d + t] / ls[t];
   Xq[idx] = v;
+}
+
+// ---- split plans (host) ----------------------------------------------------------
+// Segment (ci | ii << 16, kbeg, kend, chunk or -1) lists per workgroup, and the
+// reduction list of the tiles split over several chunks.
+struct SplitPlan {
+  std::vector<int4> segs, red;
+  std::vector<int> wg_off;
+  int nchunks = 0, max_segs = 0;
+  int64_t max_steps = 0;  // k-steps of the busiest workgroup
+};
+
+// kc_len > 0: uniform chunks of kc_len; kc_len < 0: stream-K over `slots`.
+SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots) {
+  struct Seg { int ci, ii, kb, ke; };
+  std::vector<std::vector<Seg>> wg;
+  auto kfull = [n](int ci) { return std::min(n, ci * PC + PC); };
+  if (kc_len > 0) {
+    for (int ci = nC - 1; ci >= 0; --ci)
+      for (int kb = 0; kb < kfull(ci); kb += kc_len)
+        for (int ii = 0; ii < nI; ++ii) wg.push_back({Seg{ci, ii, kb, std::min(kfull(ci), kb + kc_len)}});
+  } else {
+    int64_t total = 0;
+    for (int ci = 0; ci < nC; ++ci) total += (int64_t)nI * ceil_div(kfull(ci), PK);
+    const int64_t W = std::max<int64_t>(1, std::min<int64_t>(slots, total / 16));
+    const int64_t share = ceil_div(total, W);
+    wg.resize((size_t)ceil_div(total, share));
+    int64_t pos = 0;
+    for (int ci = nC - 1; ci >= 0; --ci)
+      for (int ii = 0; ii < nI; ++ii) {
+        const int L = (int)ceil_div(kfull(ci), PK);
+        int s0 = 0;
+        while (s0 < L) {
+          const int64_t w = pos / share;
+          const int take = (int)std::min<int64_t>(L - s0, (w + 1) * share - pos);
+          wg[(size_t)w].push_back(Seg{ci, ii, s0 * PK, std::min(kfull(ci), (s0 + take) * PK)});
+          s0 += take;
+          pos += take;
+        }
+      }
+  }
+  // chunk numbers: the segments of every split tile, in k order
+  std::map<std::pair<int, int>, std::vector<std::pair<int, int>>> tiles;  // -> (wg, idx) in k order
+  for (int w = 0; w < (int)wg.size(); ++w)
+    for (int j = 0; j < (int)wg[w].size(); ++j) tiles[{wg[w][j].ci, wg[w][j].ii}].push_back({w, j});
+  std::vector<std::vector<int>> chunk_of(wg.size());
+  for (size_t w = 0; w < wg.size(); ++w) chunk_of[w].assign(wg[w].size(), -1);
+  SplitPlan p;
+  for (auto& kv : tiles) {
+    auto& lst = kv.second;
+    std::sort(lst.begin(), lst.end(), [&](const std::pair<int, int>& a, const std::pair<int, int>& b) {
+      return wg[a.first][a.second].kb < wg[b.first][b.second].kb;
+    });
+    if (lst.size() == 1) continue;  // whole tile in one segment: epilogue in place
+    p.red.push_back(make_int4(kv.first.first, kv.first.second, p.nchunks, (int)lst.size()));
+    for (auto& e : lst) chunk_of[e.first][e.second] = p.nchunks++;
+  }
+  p.wg_off.push_back(0);
+  for (size_t w = 0; w < wg.size(); ++w) {
+    int64_t steps = 0;
+    for (size_t j = 0; j < wg[w].size(); ++j) {
+      const Seg& g = wg[w][j];
+      p.segs.push_back(make_int4(g.ci | (g.ii << 16), g.kb, g.ke, chunk_of[w][j]));
+      steps += ceil_div(g.ke - g.kb, PK);
+    }
+    p.wg_off.push_back((int)p.segs.size());
+    p.max_segs = std::max(p.max_segs, (int)wg[w].size());
+    p.max_steps = std::max(p.max_steps, steps);
+  }
+  return p;
+}
+
+struct DevPlan {
+  int4 *segs = nullptr, *red = nullptr;
+  int* wg_off = nullptr;
+  int W = 0, nred = 0, nchunks = 0;
+};
+std::mutex g_plan_mu;
+std::map<std::tuple<int, int, int, int, int, int>, DevPlan> g_plans;  // (dev, nC, nI, n, kc, slots)
+
+int device_plan(int nC, int nI, int n, int kc_len, DevPlan** out) {
+  int dev = 0;
+  BO_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  DevPlan& dp = g_plans[std::make_tuple(dev, nC, nI, n, kc_len, kSlots)];
+  if (!dp.wg_off) {
+    const SplitPlan p = build_split_plan(nC, nI, n, kc_len, kSlots);
+    BO_HIP(hipMalloc(&dp.segs, sizeof(int4) * std::max<size_t>(1, p.segs.size())));
+    BO_HIP(hipMalloc(&dp.red, sizeof(int4) * std::max<size_t>(1, p.red.size())));
+    BO_HIP(hipMalloc(&dp.wg_off, sizeof(int) * p.wg_off.size()));
+    BO_HIP(hipMemcpy(dp.segs, p.segs.data(), sizeof(int4) * p.segs.size(), hipMemcpyHostToDevice));
+    if (!p.red.empty())
+      BO_HIP(hipMemcpy(dp.red, p.red.data(), sizeof(int4) * p.red.size(), hipMemcpyHostToDevice));
+    BO_HIP(hipMemcpy(dp.wg_off, p.wg_off.data(), sizeof(int) * p.wg_off.size(), hipMemcpyHostToDevice));
+    dp.W = (int)p.wg_off.size() - 1;
+    dp.nred = (int)p.red.size();
+    dp.nchunks = p.nchunks;
+  }
+  *out = &dp;
+  return BO_OK;
 }
 
 }  // namespace
@@ -504,24 +620,51 @@ int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len,
   // Cost model in k-step units (measured on MI355X, tools/tune_split.py):
   //  one pass: the heaviest-first schedule ends at max(total steps / slots,
   //            longest column tile) plus a per-workgroup overhead per round;
-  //  split-k:  every round of workgroups lasts one chunk (kc / 16 steps) plus
-  //            the overhead, plus the reduction launch.  Ties go to the
-  //            shorter chunk.
+  //  stream-K: the busiest workgroup's k-steps plus the overhead of each of
+  //            its segments, plus the reduction launch.
   const int64_t steps = nI * splitk_base(nC, (int)n, PK);
   const int64_t longest = splitk_chunks(nC - 1, (int)n, PK);
   const int64_t one_pass = std::max(ceil_div(steps, slots), longest) +
                            kWgOverheadSteps * ceil_div((int64_t)nC * nI, slots);
-  int64_t best_cost = one_pass;
-  for (int kc = 64; kc <= 1024; kc *= 2) {
-    if (kc >= n) break;
-    const int64_t wgs = nI * splitk_base(nC, (int)n, kc);
-    const int64_t cost = ceil_div(wgs, slots) * (kc / PK + kWgOverheadSteps) + kReduceSteps;
-    if (cost < best_cost) {
-      best_cost = cost;
-      *kc_len = kc;
-    }
+  const SplitPlan p = build_split_plan(nC, (int)nI, (int)n, -1, slots);
+  const int64_t sk = p.max_steps + (int64_t)kWgOverheadSteps * p.max_segs + kReduceSteps;
+  if (sk < one_pass) {
+    *kc_len = -1;
+    *work_elems = (int64_t)p.nchunks * PI * PC;
   }
-  if (*kc_len) *work_elems = splitk_base(nC, (int)n, *kc_len) * nrows_pad * PC;
+  return BO_OK;
+}
+
+int bo_post_split_work(int64_t B, int q, int64_t n, int kc_len, int64_t* work_elems) {
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  *work_elems = 0;
+  if (kc_len == 0 || nrows_pad == 0) return BO_OK;
+  const SplitPlan p = build_split_plan(nC, nrows_pad / PI, (int)n, kc_len, kSlots);
+  *work_elems = (int64_t)p.nchunks * PI * PC;
+  return BO_OK;
+}
+
+// The segment table of a plan (host only, tests): up to cap segments as 4 ints
+// (ci | ii << 16, kbeg, kend, chunk or -1) and up to wcap + 1 workgroup
+// offsets; *nseg / *nwg receive the sizes.
+int bo_post_split_table(int64_t B, int q, int64_t n, int kc_len, int* segs, int cap, int* wg_off,
+                        int wcap, int* nseg, int* nwg) {
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  BO_CHECK_ARG(kc_len != 0 && nrows_pad > 0, "bo_post_split_table: a split plan of a non-empty batch");
+  const SplitPlan p = build_split_plan(nC, nrows_pad / PI, (int)n, kc_len, kSlots);
+  *nseg = (int)p.segs.size();
+  *nwg = (int)p.wg_off.size() - 1;
+  for (int i = 0; i < *nseg && i < cap; ++i) {
+    segs[4 * i] = p.segs[i].x;
+    segs[4 * i + 1] = p.segs[i].y;
+    segs[4 * i + 2] = p.segs[i].z;
+    segs[4 * i + 3] = p.segs[i].w;
+  }
+  for (int i = 0; i <= *nwg && i <= wcap; ++i) wg_off[i] = p.wg_off[i];
   return BO_OK;
 }
 
@@ -587,8 +730,8 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
                (long long)ldu);
   if (B == 0) return BO_OK;  // no t-batches: nothing to launch
   const bool pre = Kt != nullptr;
-  BO_CHECK_ARG(kc_len == 0 || (kc_len > 0 && kc_len % PK == 0 && work != nullptr),
-               "split-k chunk %d must be a positive multiple of %d with a workspace", kc_len, PK);
+  BO_CHECK_ARG(kc_len == 0 || kc_len == -1 || (kc_len > 0 && kc_len % PK == 0),
+               "split chunk %d must be 0, -1 (stream-K) or a positive multiple of %d", kc_len, PK);
   int Qp, nrows_pad, nC;
   int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
   if (s) return s;
@@ -599,18 +742,27 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
   // Grouped 8 x 8 super-tile schedule where the grid divides (C3: 2.68 -> 2.49 ms,
   // HBM 4.5 -> 3.7 GB per launch against the per-column-tile order).
   const int grouped = kc_len == 0 && nC % 8 == 0 && nI % 8 == 0;
-  const int64_t blocks = kc_len > 0 ? (int64_t)nC * ceil_div(n, kc_len) * nI
+  DevPlan* plan = nullptr;
+  if (kc_len != 0) {
+    s = device_plan(nC, nI, (int)n, kc_len, &plan);
+    if (s) return s;
+    BO_CHECK_ARG(plan->nchunks == 0 || work != nullptr, "split plan needs a workspace of %lld doubles",
+                 (long long)plan->nchunks * PI * PC);
+  }
+  const int64_t blocks = kc_len != 0 ? plan->W
                          : grouped  ? 512 * (int64_t)ceil_div((nC / 8) * (nI / 8), 8)
                                     : 8 * ceil_div(nC, 8) * (int64_t)nI;
+  const int4* segs = plan ? plan->segs : nullptr;
+  const int* wg_off = plan ? plan->wg_off : nullptr;
   hipStream_t st = as_stream(stream);
   // One instantiation per active input dimension (the padded coordinates
   // beyond d are zero, so fewer distance terms are exact, not approximate).
 #define BO_POST_GO(KIND, ND, SPL, CRS, PRE_)                                                \
   post_partials_kernel<KIND, ND, SPL, CRS, PRE_><<<(unsigned)blocks, 256, 0, st>>>(          \
       Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,    \
-      kc_len, work, Qc, rq, ldq, Cx, Kt, grouped)
+      segs, wg_off, work, Qc, rq, ldq, Cx, Kt, grouped)
 #define BO_POST_LAUNCH(KIND, ND)                                                            \
-  if (kc_len > 0) {                                                                         \
+  if (kc_len != 0) {                                                                        \
     if (pre) BO_POST_GO(KIND, ND, true, false, true);                                       \
     else BO_POST_GO(KIND, ND, true, false, false);                                          \
   } else if (Qc != nullptr) {                                                               \
@@ -639,9 +791,9 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
 #undef BO_POST_LAUNCH
 #undef BO_POST_GO
   BO_LAUNCH_CHECK();
-  if (kc_len > 0) {
-    post_splitk_reduce_kernel<<<(unsigned)(nC * (nrows_pad / 16)), 64, 0, st>>>(
-        work, (int)n, nC, nI, kc_len, beta, Spart, mpart, Rt);
+  if (plan && plan->nred > 0) {
+    post_splitk_reduce_kernel<<<(unsigned)(plan->nred * (PI / 16)), 64, 0, st>>>(
+        work, plan->red, (int)n, nI, beta, Spart, mpart, Rt);
     BO_LAUNCH_CHECK();
   }
   return BO_OK;
@@ -664,8 +816,8 @@ int bo_post_w(const double* Linv, int64_t ldl, const double* Rt, int B, int q, i
   const int64_t blocks = 512 * (int64_t)ceil_div((nC / 8) * (nI / 8), 8);
   post_partials_kernel<BO_RBF, 1, false, false, true, true><<<(unsigned)blocks, 256, 0,
                                                                 as_stream(stream)>>>(
-      Rt, 0, Rt, (int)n, Linv, ldl, nullptr, 0.0, nC, nI, nullptr, nullptr, Wt, 0,
-      nullptr, nullptr, 0, 0, nullptr, Rt, 1);
+      Rt, 0, Rt, (int)n, Linv, ldl, nullptr, 0.0, nC, nI, nullptr, nullptr, Wt, nullptr,
+      nullptr, nullptr, nullptr, 0, 0, nullptr, Rt, 1);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

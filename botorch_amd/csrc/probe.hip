@@ -18,7 +18,11 @@ __global__ void probe_kernel(double* out) {
   }
 }
 // Peak-rate probe: every wave issues `iters` x 8 independent back-to-back
-// v_mfma_f64_16x16x4_f64 (operands in registers), 4 waves per CU-slot.
+// v_mfma_f64_16x16x4_f64 (operands in registers), 4 waves per CU-slot.  The
+// MFMAs are inline asm on VGPR accumulators: written as builtins, the compiler
+// copied all 8 accumulators VGPR -> AGPR -> VGPR around every iteration (128
+// moves per 8 MFMAs), which capped the round-1 probe at 47 TF/s.  Dependent
+// MFMAs are 8 apart (8 x 16 passes), beyond any srcC hazard window.
 __global__ __launch_bounds__(256) void rate_kernel(int iters, double* out) {
   const int lane = threadIdx.x & 63;
   double a = 1.0 + 1e-3 * lane, b = 1.0 - 1e-3 * lane;
@@ -27,8 +31,10 @@ __global__ __launch_bounds__(256) void rate_kernel(int iters, double* out) {
   for (int j = 0; j < 8; ++j) acc[j] = v4d_zero();
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = mfma_f64(a, b, acc[j]);
+    for (int j = 0; j < 8; ++j)
+      asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(acc[j]) : "v"(a), "v"(b));
   }
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");  // last MFMAs retire before the reads
   double s = 0.0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];

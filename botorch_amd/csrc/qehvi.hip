@@ -24,6 +24,7 @@ constexpr int THREADS = 256;
 constexpr int QMAX = 12;
 constexpr int MMAX = 4;
 constexpr int LDS_SAMPLES_DOUBLES = 6144;  // 48 KiB of samples per pass
+constexpr int GROUP = 16;                  // lanes per sample in the backward
 
 // Optional extensions used by qNEHVI (cached baseline root, per-sample box
 // decompositions): cstride > 0 gives every sample its own K cells
@@ -126,8 +127,8 @@ __global__ __launch_bounds__(THREADS) void qehvi_kernel(
 // term sign * prod_t mn_t, the derivative w.r.t. f[s][p*][t] is
 // sign * prod_{t' != t} mn_t' where p* = argmin_{p in T} f_pt and the min is
 // not the cell's upper bound (min(u, .) passes no gradient to f there; a
-// clamped-at-lower term is zero with zero gradient).  df accumulates in LDS
-// (ds_add_f64), then dmean_t[p] = sum_s df[s][p][t] and
+// clamped-at-lower term is zero with zero gradient).  df[s] is summed by one
+// 16-lane group over the cells in a fixed order (no atomics), then dmean_t[p] = sum_s df[s][p][t] and
 // dL_t[p][j] = sum_s df[s][p][t] Z[s][j m + t] (j <= p), scaled by dacq / S.
 template <int M>
 __global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
@@ -152,74 +153,80 @@ __global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
     for (int e = tid; e < ns * per_sample; e += THREADS) {
       const int s = e / per_sample;
       f[e] = sample_value<M>(B, b, q, (e / M) % q, e % M, s0 + s, mean, L, Z, ex);
-      df[e] = 0.0;
     }
     __syncthreads();
-    for (int e = tid; e < ns * K; e += THREADS) {
-      const int s = e / K;
-      const int k = e % K;
-      double l[M], u[M];
-      const int64_t co = (int64_t)(s0 + s) * ex.cstride + (int64_t)k * M;
-#pragma unroll
-      for (int t = 0; t < M; ++t) {
-        l[t] = lo[co + t];
-        u[t] = hi[co + t];
-      }
+    // GROUP consecutive lanes share one sample: lane g of the group takes the
+    // cells k = g, g + GROUP, ...; the group's partial gradients reduce in a
+    // fixed butterfly, so df (and every gradient) is bitwise reproducible
+    for (int s = tid / GROUP; s < ns; s += THREADS / GROUP) {
       const double* fs = f + s * per_sample;
-      double a[QMAX][M];
-      unsigned act = 0;
-#pragma unroll
-      for (int p = 0; p < QMAX; ++p) {
-        bool ok = p < q;
-#pragma unroll
-        for (int t = 0; t < M; ++t) {
-          const double v = p < q ? fmin(u[t], fs[p * M + t]) - l[t] : 0.0;
-          a[p][t] = v;
-          ok = ok && (v > 0.0);
-        }
-        if (ok) act |= 1u << p;
-      }
       double gacc[QMAX][M];
 #pragma unroll
       for (int p = 0; p < QMAX; ++p)
 #pragma unroll
         for (int t = 0; t < M; ++t) gacc[p][t] = 0.0;
-      for (unsigned sub = act; sub; sub = (sub - 1) & act) {
-        double mn[M];
-        int am[M];
+      for (int k = tid % GROUP; k < K; k += GROUP) {
+        double l[M], u[M];
+        const int64_t co = (int64_t)(s0 + s) * ex.cstride + (int64_t)k * M;
 #pragma unroll
         for (int t = 0; t < M; ++t) {
-          mn[t] = INFINITY;
-          am[t] = 0;
+          l[t] = lo[co + t];
+          u[t] = hi[co + t];
         }
+        double a[QMAX][M];
+        unsigned act = 0;
 #pragma unroll
-        for (int p = 0; p < QMAX; ++p)
-          if (sub & (1u << p))
+        for (int p = 0; p < QMAX; ++p) {
+          bool ok = p < q;
 #pragma unroll
-            for (int t = 0; t < M; ++t)
-              if (a[p][t] < mn[t]) {
-                mn[t] = a[p][t];
-                am[t] = p;
-              }
-        const double sg = (__popc(sub) & 1) ? 1.0 : -1.0;
+          for (int t = 0; t < M; ++t) {
+            const double v = p < q ? fmin(u[t], fs[p * M + t]) - l[t] : 0.0;
+            a[p][t] = v;
+            ok = ok && (v > 0.0);
+          }
+          if (ok) act |= 1u << p;
+        }
+        for (unsigned sub = act; sub; sub = (sub - 1) & act) {
+          double mn[M];
+          int am[M];
 #pragma unroll
-        for (int t = 0; t < M; ++t) {
-          double o = sg;
-#pragma unroll
-          for (int t2 = 0; t2 < M; ++t2)
-            if (t2 != t) o *= mn[t2];
-          // the min reaches f only where f < u (else the upper bound is active)
+          for (int t = 0; t < M; ++t) {
+            mn[t] = INFINITY;
+            am[t] = 0;
+          }
 #pragma unroll
           for (int p = 0; p < QMAX; ++p)
-            if (p == am[t] && fs[p * M + t] < u[t]) gacc[p][t] += o;
+            if (sub & (1u << p))
+#pragma unroll
+              for (int t = 0; t < M; ++t)
+                if (a[p][t] < mn[t]) {
+                  mn[t] = a[p][t];
+                  am[t] = p;
+                }
+          const double sg = (__popc(sub) & 1) ? 1.0 : -1.0;
+#pragma unroll
+          for (int t = 0; t < M; ++t) {
+            double o = sg;
+#pragma unroll
+            for (int t2 = 0; t2 < M; ++t2)
+              if (t2 != t) o *= mn[t2];
+            // the min reaches f only where f < u (else the upper bound is active)
+#pragma unroll
+            for (int p = 0; p < QMAX; ++p)
+              if (p == am[t] && fs[p * M + t] < u[t]) gacc[p][t] += o;
+          }
         }
       }
-      if (act) {
 #pragma unroll
-        for (int p = 0; p < QMAX; ++p)
+      for (int p = 0; p < QMAX; ++p) {
+        if (p >= q) break;
 #pragma unroll
-          for (int t = 0; t < M; ++t)
-            if (p < q && gacc[p][t] != 0.0) atomicAdd(&df[s * per_sample + p * M + t], gacc[p][t]);
+        for (int t = 0; t < M; ++t) {
+          double v = gacc[p][t];
+#pragma unroll
+          for (int o = GROUP / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, GROUP);
+          if (tid % GROUP == 0) df[s * per_sample + p * M + t] = v;
+        }
       }
     }
     __syncthreads();

@@ -231,7 +231,8 @@ def geometry(B: int, q: int, n: int):
 
 
 def split_plan(B: int, q: int, n: int, slots: int = 0):
-    """(kc_len, workspace doubles) of the split-k posterior; kc_len = 0: one pass."""
+    """(kc_len, workspace doubles) of the posterior plan; kc_len = 0: one pass,
+    -1: stream-K."""
     kc, we = ctypes.c_int(), ctypes.c_int64()
     check(lib().bo_post_split_plan(B, q, n, slots, ctypes.byref(kc), ctypes.byref(we)),
           "post_split_plan")
@@ -242,7 +243,8 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
                   split: Optional[int] = None, cross: Optional[torch.Tensor] = None,
                   kxt: Optional[bool] = None) -> PostPartials:
     """Column-tile partials of R R^T and R beta for X (B x q x d).  ``split``:
-    None = the library's plan, 0 = never split-k, k > 0 = chunks of k rows.
+    None = the library's plan, 0 = one pass, k > 0 = chunks of k rows,
+    -1 = stream-K (equal k-step shares over the resident slots).
     ``cross`` (rq <= 16 rows x >= n): also return pp.Cx = cross K*x^T
     (rq x nrows_pad) from the same pass -- on one-pass plans only; under a
     split-k plan pp.Cx is None and R^T is stored instead.  ``kxt``: build
@@ -263,10 +265,11 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
     Rt = torch.empty(nC * 128, nrows_pad, **f64) if store_R else None
     if split is None:
         kc_len, work_elems = split_plan(B, q, cache.n)
-    elif split > 0:
+    elif split != 0:
         kc_len = int(split)
-        nk = [-(-min(cache.n, (c + 1) * 128) // kc_len) for c in range(nC)]
-        work_elems = sum(nk) * nrows_pad * 128
+        we = ctypes.c_int64()
+        check(lib().bo_post_split_work(B, q, cache.n, kc_len, ctypes.byref(we)), "post_split_work")
+        work_elems = we.value
     else:
         kc_len, work_elems = 0, 0
     work = torch.empty(work_elems, **f64) if kc_len else None

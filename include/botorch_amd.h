@@ -204,9 +204,11 @@ int bo_prepare_rows(const double* X, int B, int q, int d, const double* lengthsc
  * training inputs; U: >= np x np with leading dim ldu; beta: n.
  * Spart: nC x (nrows_pad/16) x 16 x 16,  mpart: nC x nrows_pad.
  * Rt (nullable, gradient path): R^T, (nC*128) x nrows_pad.
- * kc_len > 0 runs split-k (chunks of kc_len training rows, then a reduction
- * in chunk order) with `work` >= work_elems doubles from bo_post_split_plan;
- * kc_len = 0: one workgroup per (column tile, row tile), work unused.
+ * kc_len = 0: one workgroup per (column tile, row tile), work unused;
+ * kc_len > 0: split (every tile cut into chunks of kc_len training rows);
+ * kc_len = -1: stream-K (the tiles' k-steps cut into one equal share per
+ * resident slot).  Split plans reduce each cut tile's chunks in k order, with
+ * `work` >= the work_elems of bo_post_split_plan / bo_post_split_work.
  * Qc (nullable, one-pass only): rq <= 16 rows (leading dim ldq >= n) whose
  * products with K*x are returned as nC column-tile partials
  * Cx[ci] (nC x rq x nrows_pad; sum over ci = Qc K*x^T) -- the
@@ -235,12 +237,20 @@ int bo_post_kxt(int kind, const double* Xq, int B, int q, int d, const double* X
 int bo_post_w(const double* Linv, int64_t ldl, const double* Rt, int B, int q, int64_t n,
               double* Wt, void* stream);
 
-/* Split-k plan of bo_post_partials (host pointers): the chunk length in
- * {64, ..., 1024} (or 0 = one pass) that minimises a k-step cost model of the
- * triangular grid over `slots` resident workgroups (slots <= 0: 512 = 256 CUs
- * x 2), and the workspace size in doubles. */
+/* Plan of bo_post_partials (host pointers): kc_len = 0 (one pass) or -1
+ * (stream-K), whichever a k-step cost model of the triangular grid over
+ * `slots` resident workgroups (slots <= 0: 512 = 256 CUs x 2) rates faster,
+ * and the workspace size in doubles. */
 int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len,
                        int64_t* work_elems);
+/* Workspace doubles of bo_post_partials under a given kc_len (0, -1 or a
+ * chunk length). */
+int bo_post_split_work(int64_t B, int q, int64_t n, int kc_len, int64_t* work_elems);
+/* The segment table of a split plan (host only; tests): up to cap segments as
+ * 4 ints (ci | ii << 16, kbeg, kend, chunk or -1 = whole tile in place) and
+ * up to wcap + 1 per-workgroup offsets; *nseg, *nwg receive the sizes. */
+int bo_post_split_table(int64_t B, int q, int64_t n, int kc_len, int* segs, int cap, int* wg_off,
+                        int wcap, int* nseg, int* nwg);
 
 /* Finalise the posterior of each t-batch and (mode != POSTERIOR) run the
  * fused q x q psd_safe_cholesky + reparameterised sampling + MC reduction:

@@ -4,6 +4,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -44,19 +45,67 @@ def test_library_exports_every_header_symbol():
 
 
 def test_split_plan_geometry():
-    """Host-side split-k plan of bo_post_partials (no GPU call); the choices
-    below are the measured optima of tools/tune_split.py on MI355X."""
+    """Host-side plan of bo_post_partials (no GPU call): one pass where the
+    tile grid fills the slots, stream-K where the triangular tiles are too few
+    or too unequal."""
     from botorch_amd import kernels
     assert kernels.split_plan(512, 16, 4096)[0] == 0      # C3: 2048 tiles, one pass
-    kc, work = kernels.split_plan(64, 8, 1024)            # C2: 8 x 4 tiles
-    assert kc == 64
-    # workspace = non-empty chunks x padded rows x 128 columns
-    nk = sum(-(-min(1024, (c + 1) * 128) // kc) for c in range(8))
-    assert work == nk * 512 * 128
-    assert kernels.split_plan(64, 16, 4096)[0] == 256     # 256 unbalanced tiles
-    assert kernels.split_plan(1, 1, 4096)[0] == 256
-    assert kernels.split_plan(128, 8, 2048)[0] == 128
+    assert kernels.split_plan(64, 8, 1024)[0] == -1       # C2: 8 x 4 tiles
+    assert kernels.split_plan(64, 16, 4096)[0] == -1      # a rank's b = 64 share of C3
+    assert kernels.split_plan(1, 1, 4096)[0] == -1
     assert kernels.split_plan(64, 8, 100)[0] == 0         # nothing to split
+
+
+def _split_table(B, q, n, kc):
+    import ctypes
+    import numpy as np
+    from botorch_amd import _lib
+    ns, nw = ctypes.c_int(), ctypes.c_int()
+    _lib.check(_lib.lib().bo_post_split_table(B, q, n, kc, None, 0, None, -1, ctypes.byref(ns),
+                                              ctypes.byref(nw)), "split_table")
+    segs = np.zeros((ns.value, 4), dtype=np.int32)
+    off = np.zeros(nw.value + 1, dtype=np.int32)
+    _lib.check(_lib.lib().bo_post_split_table(B, q, n, kc, segs.ctypes.data, ns.value,
+                                              off.ctypes.data, nw.value, ctypes.byref(ns),
+                                              ctypes.byref(nw)), "split_table")
+    return segs, off
+
+
+@pytest.mark.parametrize("B,q,n,kc", [(64, 16, 4096, -1), (64, 8, 1024, -1), (9, 5, 513, -1),
+                                      (64, 8, 1024, 64), (20, 3, 1000, 128), (1, 1, 4096, -1)])
+def test_split_table_covers_every_tile_once(B, q, n, kc):
+    """Every (column tile, row tile) k-range [0, min(n, 128 (ci + 1))) is
+    covered exactly once by the segments; chunk numbers are dense, in k order
+    within a tile, -1 exactly for whole-tile segments; stream-K shares differ
+    by at most one tile boundary's rounding."""
+    import numpy as np
+    from botorch_amd import kernels
+    Qp, nrows_pad, nC = kernels.geometry(B, q, n)
+    nI = nrows_pad // 128
+    segs, off = _split_table(B, q, n, kc)
+    tiles = {}
+    for ci_ii, kb, ke, ch in segs.tolist():
+        tiles.setdefault((ci_ii & 0xffff, ci_ii >> 16), []).append((kb, ke, ch))
+    assert len(tiles) == nC * nI
+    chunks = []
+    for (ci, ii), lst in tiles.items():
+        lst.sort()
+        assert lst[0][0] == 0 and lst[-1][1] == min(n, 128 * (ci + 1))
+        assert all(a[1] == b[0] for a, b in zip(lst, lst[1:]))
+        assert all(kb % 16 == 0 and ke > kb for kb, ke, _ in lst)
+        if len(lst) == 1:
+            assert lst[0][2] == -1
+        else:
+            cs = [c for _, _, c in lst]
+            assert cs == list(range(cs[0], cs[0] + len(cs)))
+            chunks += cs
+    assert sorted(chunks) == list(range(len(chunks)))
+    assert off[0] == 0 and off[-1] == len(segs) and np.all(np.diff(off) >= 1)
+    if kc == -1:
+        steps = [sum(-(-(ke - kb) // 16) for _, kb, ke, _ in segs[off[w]:off[w + 1]].tolist())
+                 for w in range(len(off) - 1)]
+        assert len(steps) <= 512
+        assert max(steps) - min(steps[:-1] or steps) <= len(steps) and max(steps) <= -(-sum(steps) // len(steps)) + 1
 
 
 def test_custom_ops_registered_with_meta_shapes():

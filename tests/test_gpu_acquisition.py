@@ -282,6 +282,10 @@ def test_qehvi_gradient_matches_oracle(golden, B, q, S):
     torch.testing.assert_close(v.detach().cpu(), ref.detach(), rtol=1e-7, atol=1e-10)
     assert go.abs().max() > 0
     torch.testing.assert_close(gd.cpu(), go, rtol=1e-5, atol=1e-8)
+    # the backward reduces per sample in a fixed order: bitwise reproducible
+    for _ in range(2):
+        (g2,) = torch.autograd.grad(acqf(Xd).sum(), Xd)
+        assert torch.equal(g2, gd)
 
 
 @pytest.mark.parametrize("d,M,q", [(50, 16, 4), (10, 3, 2)])

@@ -185,9 +185,11 @@ def test_posterior_matches_oracle(n, B, q):
 
 
 @pytest.mark.parametrize("n,B,q,split", [(1024, 64, 8, None), (1024, 64, 8, 64), (1000, 20, 3, 128),
-                                         (513, 9, 5, 256), (300, 33, 16, 64)])
+                                         (513, 9, 5, 256), (300, 33, 16, 64), (4096, 64, 16, None),
+                                         (1000, 20, 3, -1), (300, 33, 16, -1), (2048, 40, 16, -1)])
 def test_post_partials_split_k(n, B, q, split):
-    """Split-k (chunked k-range + ordered reduction) against the one-pass kernel
+    """Split plans (uniform chunks, or stream-K shares of the concatenated
+    k-steps; ordered reduction of each cut tile) against the one-pass kernel
     and the oracle: same Spart / mpart / R^T up to fp64 summation order."""
     from botorch_amd import kernels, _lib
     X, Y, orc, h = _oracle_model(n)
@@ -196,7 +198,7 @@ def test_post_partials_split_k(n, B, q, split):
     Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64).to(DEV)
     kc, _ = kernels.split_plan(B, q, n)
     if split is None:
-        assert kc > 0  # C2 geometry (32 tiles) is planned as split-k
+        assert kc == -1  # C2 geometry (32 tiles) and a rank's b = 64 share of C3: stream-K
     one = kernels.post_partials(c, Xc, store_R=True, split=0)
     spl = kernels.post_partials(c, Xc, store_R=True, split=split)
     # the split-k plan without the K*x^T buffer (kernel rows
