@@ -50,8 +50,6 @@ constexpr int PK = 16;    // k-step
 constexpr int PLD = 144;  // LDS row pitch (doubles): 2 x 144 dwords = 32 mod 64 banks
 constexpr int DP = 8;     // padded input dimension held in registers
 constexpr int kSlots = 512;            // resident workgroups: 256 CUs x 2 (launch bounds)
-constexpr int kWgOverheadSteps = 4;    // prologue + epilogue of a workgroup, in k-steps
-constexpr int kReduceSteps = 3;        // the split-k reduction launch, in k-steps
 constexpr int kTileDoubles = 32 * 64;  // one 16-row x 128-column R^T tile
 
 // One kernel value k(x_i, x_k) from scaled coordinates (0 beyond n / invalid rows).
@@ -513,24 +511,34 @@ SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots) {
       for (int kb = 0; kb < kfull(ci); kb += kc_len)
         for (int ii = 0; ii < nI; ++ii) wg.push_back({Seg{ci, ii, kb, std::min(kfull(ci), kb + kc_len)}});
   } else {
-    int64_t total = 0;
-    for (int ci = 0; ci < nC; ++ci) total += (int64_t)nI * ceil_div(kfull(ci), PK);
-    const int64_t W = std::max<int64_t>(1, std::min<int64_t>(slots, total / 16));
-    const int64_t share = ceil_div(total, W);
-    wg.resize((size_t)ceil_div(total, share));
-    int64_t pos = 0;
-    for (int ci = nC - 1; ci >= 0; --ci)
-      for (int ii = 0; ii < nI; ++ii) {
+    // One lane of workgroups per row tile ii, each lane cutting the same
+    // sequence (column tiles heaviest first, k ascending) into equal shares:
+    // workgroup j of every lane covers the same k-steps of the same column
+    // tiles, so the nI workgroups of one j read the same U slices at the same
+    // time; they are placed on one XCD (block b: XCD b % 8, slot b / 8) so
+    // those slices are fetched into its L2 once.
+    int64_t lane_total = 0;
+    for (int ci = 0; ci < nC; ++ci) lane_total += ceil_div(kfull(ci), PK);
+    const int64_t per_lane =
+        std::max<int64_t>(1, std::min<int64_t>(std::max(1, slots / nI), lane_total / 16));
+    const int64_t share = ceil_div(lane_total, per_lane);
+    const int64_t jn = ceil_div(lane_total, share);  // workgroups used per lane
+    wg.resize((size_t)(ceil_div(jn, 8) * 8 * nI));
+    for (int ii = 0; ii < nI; ++ii) {
+      int64_t pos = 0;
+      for (int ci = nC - 1; ci >= 0; --ci) {
         const int L = (int)ceil_div(kfull(ci), PK);
         int s0 = 0;
         while (s0 < L) {
-          const int64_t w = pos / share;
-          const int take = (int)std::min<int64_t>(L - s0, (w + 1) * share - pos);
-          wg[(size_t)w].push_back(Seg{ci, ii, s0 * PK, std::min(kfull(ci), (s0 + take) * PK)});
+          const int64_t j = pos / share;
+          const int take = (int)std::min<int64_t>(L - s0, (j + 1) * share - pos);
+          const int64_t b = ((j / 8) * nI + ii) * 8 + (j % 8);
+          wg[(size_t)b].push_back(Seg{ci, ii, s0 * PK, std::min(kfull(ci), (s0 + take) * PK)});
           s0 += take;
           pos += take;
         }
       }
+    }
   }
   // chunk numbers: the segments of every split tile, in k order
   std::map<std::pair<int, int>, std::vector<std::pair<int, int>>> tiles;  // -> (wg, idx) in k order
@@ -617,18 +625,16 @@ int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len,
   *kc_len = 0;
   *work_elems = 0;
   if (nI == 0) return BO_OK;  // no t-batches
-  // Cost model in k-step units (measured on MI355X, tools/tune_split.py):
-  //  one pass: the heaviest-first schedule ends at max(total steps / slots,
-  //            longest column tile) plus a per-workgroup overhead per round;
-  //  stream-K: the busiest workgroup's k-steps plus the overhead of each of
-  //            its segments, plus the reduction launch.
+  // Stream-K wherever the one-pass grid is imbalance-bound: fewer than four
+  // tiles per slot (the heaviest-first rounds cannot even out the triangular
+  // k-ranges) and at least one k-step per slot to share.  Measured at n = 4096,
+  // q = 16 (tools/time_posterior.py, us, one pass -> stream-K): b = 64
+  // 1026 -> 411, 128 1033 -> 693, 256 1552 -> 1261, 512 (2048 tiles) 2403 ->
+  // 2432 (the grouped 8 x 8 super-tile schedule keeps its edge there).
   const int64_t steps = nI * splitk_base(nC, (int)n, PK);
-  const int64_t longest = splitk_chunks(nC - 1, (int)n, PK);
-  const int64_t one_pass = std::max(ceil_div(steps, slots), longest) +
-                           kWgOverheadSteps * ceil_div((int64_t)nC * nI, slots);
-  const SplitPlan p = build_split_plan(nC, (int)nI, (int)n, -1, slots);
-  const int64_t sk = p.max_steps + (int64_t)kWgOverheadSteps * p.max_segs + kReduceSteps;
-  if (sk < one_pass) {
+  const int64_t tiles = (int64_t)nC * nI;
+  if (tiles < 4 * (int64_t)slots && steps >= slots) {
+    const SplitPlan p = build_split_plan(nC, (int)nI, (int)n, -1, slots);
     *kc_len = -1;
     *work_elems = (int64_t)p.nchunks * PI * PC;
   }

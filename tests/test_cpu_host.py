@@ -100,12 +100,15 @@ def test_split_table_covers_every_tile_once(B, q, n, kc):
             assert cs == list(range(cs[0], cs[0] + len(cs)))
             chunks += cs
     assert sorted(chunks) == list(range(len(chunks)))
-    assert off[0] == 0 and off[-1] == len(segs) and np.all(np.diff(off) >= 1)
+    assert off[0] == 0 and off[-1] == len(segs) and np.all(np.diff(off) >= 0)
     if kc == -1:
+        # one lane of equal shares per row tile: every non-empty workgroup but
+        # the last of each lane has the same k-step count
         steps = [sum(-(-(ke - kb) // 16) for _, kb, ke, _ in segs[off[w]:off[w + 1]].tolist())
                  for w in range(len(off) - 1)]
-        assert len(steps) <= 512
-        assert max(steps) - min(steps[:-1] or steps) <= len(steps) and max(steps) <= -(-sum(steps) // len(steps)) + 1
+        busy = sorted(s for s in steps if s > 0)
+        assert len(steps) <= 512 + 8 * nI
+        assert sum(1 for s in busy if s != busy[-1]) <= nI
 
 
 def test_custom_ops_registered_with_meta_shapes():

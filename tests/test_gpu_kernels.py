@@ -204,9 +204,11 @@ def test_post_partials_split_k(n, B, q, split):
     # the split-k plan without the K*x^T buffer (kernel rows
     # evaluated between the MFMAs) -- the path taken above the KXT cap
     nok = kernels.post_partials(c, Xc, store_R=True, split=split, kxt=False)
+    # fp64 summation order only: atol grows with the k-range summed (n)
+    atol = 1e-13 * max(1.0, n / 1024)
     for a, b in ((one.Spart, spl.Spart), (one.mpart, spl.mpart), (one.Rt, spl.Rt),
                  (one.Spart, nok.Spart), (one.mpart, nok.mpart), (one.Rt, nok.Rt)):
-        torch.testing.assert_close(b, a, rtol=1e-11, atol=1e-13)
+        torch.testing.assert_close(b, a, rtol=1e-11, atol=atol)
     out = kernels.qmc_finalize(c, spl, _lib.QMC_POSTERIOR, orc.ymean.item(), orc.ystd.item())
     mean_r, cov_r = orc.posterior(Xc.cpu())
     torch.testing.assert_close(out["mean"].cpu(), mean_r, rtol=1e-4, atol=1e-8)
