@@ -64,6 +64,8 @@ _SIGNATURES = {
     "bo_post_split_plan": (c_int, [c_int64, c_int, c_int64, c_int, POINTER(c_int),
                                    POINTER(c_int64)]),
     "bo_post_split_work": (c_int, [c_int64, c_int, c_int64, c_int, POINTER(c_int64)]),
+    "bo_ainv_work": (c_int, [c_int64, POINTER(c_int64)]),
+    "bo_ainv": (c_int, [_P, c_int64, c_int64, _P, _P, _P]),
     "bo_post_split_table": (c_int, [c_int64, c_int, c_int64, c_int, _P, c_int, _P, c_int,
                                     POINTER(c_int), POINTER(c_int)]),
     "bo_qmc_finalize": (c_int, [c_int, c_int, c_int, c_int, _P, _P, _P, c_int64, c_double,

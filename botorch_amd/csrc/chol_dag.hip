@@ -561,6 +561,7 @@ __device__ bool row_loop(const Ctx& c, const Flags& f, int k, int j, int i0, int
   for (int i = i0; i < i1; ++i) {
     const u32 *d1, *d2;
     u32 t1, t2;
+    if (ph && c.tid == 0) ph[4] += pre ? 1 : 0;
     if (!pre) {
       // never block while holding an unpublished row (a waiter could need it)
       if (pending) {
@@ -582,7 +583,11 @@ __device__ bool row_loop(const Ctx& c, const Flags& f, int k, int j, int i0, int
         s_rdy[i & 1] = mask;
       }
     }
-    if (ph && c.tid == 0) tA = wall_clock64();
+    if (ph && c.tid == 0) {
+      tA = wall_clock64();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // traced runs: time the operand arrival
+      ph[5] += wall_clock64() - tA;
+    }
     const bool own_x0 = !(KIND == 1 && i == j);
     if (own_x0) {
 #pragma unroll
@@ -683,7 +688,7 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
     const int4 tk = tasks[t];
     const int type = tk.x & 0xff, fin = tk.x >> 8;
     long long wsum = 0;
-    long long phs[4] = {0, 0, 0, 0};
+    long long phs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long* ph = trace ? phs : nullptr;
     if (trace && c.tid == 0) trace[4 * t] = wall_clock64();
     const int k = tk.y, j = tk.z, i0 = tk.w & 0xffff, i1 = tk.w >> 16;
@@ -761,8 +766,8 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
     if (trace && c.tid == 0) {
       trace[4 * t + 1] = wall_clock64();
       trace[4 * t + 3] = wsum;
-      long long* pt = trace + 4 * ntasks + 8 * T + 4 * t;
-      pt[0] = phs[0]; pt[1] = phs[1]; pt[2] = phs[2]; pt[3] = phs[3];
+      long long* pt = trace + 4 * ntasks + 8 * T + 8 * t;
+      for (int e = 0; e < 8; ++e) pt[e] = phs[e];
       trace[4 * t + 2] = (long long)blockIdx.x | ((long long)tk.x << 16) | ((long long)k << 24) |
                          ((long long)j << 40);
     }

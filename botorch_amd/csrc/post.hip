@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     ci = nC - 1 - pos;
     kend = min(n, ci * PC + PC);
   }
-  if constexpr (LOWERK) {
+  if constexpr (LOWERK && !SPLIT) {
     // W^T = L^{-T} R^T (bo_post_w): column tile ci reads k in [128 ci, n),
     // so the heaviest tiles are the SMALLEST ci -- mirror the schedule's order.
     ci = nC - 1 - ci;
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(64) void post_splitk_reduce_kernel(
       for (int r = 0; r < 4; ++r) acc[ct][r] += w[(ct * 4 + r) * 64];
   }
   if (Rt != nullptr) post_store_rt(acc, ci, rt * 16, lane, nI, Rt);
-  post_epilogue(acc, ci, rt * 16, lane, n, beta, nI, Spart, mpart);
+  if (Spart != nullptr) post_epilogue(acc, ci, rt * 16, lane, n, beta, nI, Spart, mpart);
 }
 
 // Scatter X (B x q x d) into the padded, lengthscale-scaled row layout
@@ -502,11 +502,42 @@ struct SplitPlan {
 };
 
 // kc_len > 0: uniform chunks of kc_len; kc_len < 0: stream-K over `slots`.
-SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots) {
+// ainv: the tiles of A^{-1} = L^{-T} L^{-1} (bo_ainv): column tiles ci >= row
+// tiles ii, k-range [128 ci, n).
+SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, bool ainv = false) {
   struct Seg { int ci, ii, kb, ke; };
   std::vector<std::vector<Seg>> wg;
   auto kfull = [n](int ci) { return std::min(n, ci * PC + PC); };
-  if (kc_len > 0) {
+  if (ainv) {
+    // Stream-K per row tile (lane ii holds column tiles ci = nC-1 .. ii, the
+    // shortest k-ranges first); every lane gets workgroups in proportion to
+    // its k-steps so the shares come out equal.
+    std::vector<int64_t> lane(nI, 0);
+    int64_t total = 0;
+    for (int ii = 0; ii < nI; ++ii) {
+      for (int ci = ii; ci < nC; ++ci) lane[ii] += ceil_div(n - ci * PC, PK);
+      total += lane[ii];
+    }
+    // sum over lanes of ceil(lane / share) <= total / share + nI <= slots
+    const int64_t share = std::max<int64_t>(16, ceil_div(total, std::max(1, slots - nI)));
+    for (int ii = 0; ii < nI; ++ii) {
+      const size_t base = wg.size();
+      int64_t pos = 0;
+      for (int ci = nC - 1; ci >= ii; --ci) {
+        const int L = (int)ceil_div(n - ci * PC, PK);
+        int s0 = 0;
+        while (s0 < L) {
+          const int64_t j = pos / share;
+          if (base + (size_t)j >= wg.size()) wg.resize(base + (size_t)j + 1);
+          const int take = (int)std::min<int64_t>(L - s0, (j + 1) * share - pos);
+          wg[base + (size_t)j].push_back(Seg{ci, ii, ci * PC + s0 * PK,
+                                             std::min(n, ci * PC + (s0 + take) * PK)});
+          s0 += take;
+          pos += take;
+        }
+      }
+    }
+  } else if (kc_len > 0) {
     for (int ci = nC - 1; ci >= 0; --ci)
       for (int kb = 0; kb < kfull(ci); kb += kc_len)
         for (int ii = 0; ii < nI; ++ii) wg.push_back({Seg{ci, ii, kb, std::min(kfull(ci), kb + kc_len)}});
@@ -577,15 +608,15 @@ struct DevPlan {
   int W = 0, nred = 0, nchunks = 0;
 };
 std::mutex g_plan_mu;
-std::map<std::tuple<int, int, int, int, int, int>, DevPlan> g_plans;  // (dev, nC, nI, n, kc, slots)
+std::map<std::tuple<int, int, int, int, int, int>, DevPlan> g_plans;  // (dev, nC, nI, n, kc, ainv)
 
-int device_plan(int nC, int nI, int n, int kc_len, DevPlan** out) {
+int device_plan(int nC, int nI, int n, int kc_len, DevPlan** out, bool ainv = false) {
   int dev = 0;
   BO_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_plan_mu);
-  DevPlan& dp = g_plans[std::make_tuple(dev, nC, nI, n, kc_len, kSlots)];
+  DevPlan& dp = g_plans[std::make_tuple(dev, nC, nI, n, kc_len, ainv ? 1 : 0)];
   if (!dp.wg_off) {
-    const SplitPlan p = build_split_plan(nC, nI, n, kc_len, kSlots);
+    const SplitPlan p = build_split_plan(nC, nI, n, kc_len, kSlots, ainv);
     BO_HIP(hipMalloc(&dp.segs, sizeof(int4) * std::max<size_t>(1, p.segs.size())));
     BO_HIP(hipMalloc(&dp.red, sizeof(int4) * std::max<size_t>(1, p.red.size())));
     BO_HIP(hipMalloc(&dp.wg_off, sizeof(int) * p.wg_off.size()));
@@ -825,6 +856,39 @@ int bo_post_w(const double* Linv, int64_t ldl, const double* Rt, int B, int q, i
       Rt, 0, Rt, (int)n, Linv, ldl, nullptr, 0.0, nC, nI, nullptr, nullptr, Wt, nullptr,
       nullptr, nullptr, nullptr, 0, 0, nullptr, Rt, 1);
   BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+// A^{-1} = L^{-T} L^{-1} (lower tiles: Ainv[r][c] for tile row >= tile column)
+// from L^{-1} (np x np, ld = np, identity pad): the posterior kernel's lower
+// k-range MFMA tiles with L^{-1} as both operands, under a stream-K plan (the
+// k-ranges [128 ci, n) are very unequal), partial tiles reduced in k order.
+int bo_ainv_work(int64_t n, int64_t* work_elems) {
+  const int nC = (int)ceil_div(n, PC);
+  const SplitPlan p = build_split_plan(nC, nC, (int)n, -1, kSlots, true);
+  *work_elems = (int64_t)p.nchunks * PI * PC;
+  return BO_OK;
+}
+
+int bo_ainv(const double* Linv, int64_t ld, int64_t n, double* Ainv, double* work, void* stream) {
+  const int nC = (int)ceil_div(n, PC);
+  BO_CHECK_ARG(n > 0 && ld == (int64_t)nC * PC, "bo_ainv: ld %lld must be n rounded up to %d",
+               (long long)ld, PC);
+  DevPlan* plan = nullptr;
+  int s = device_plan(nC, nC, (int)n, -1, &plan, true);
+  if (s) return s;
+  BO_CHECK_ARG(plan->nchunks == 0 || work != nullptr, "bo_ainv needs a workspace of %lld doubles",
+               (long long)plan->nchunks * PI * PC);
+  hipStream_t st = as_stream(stream);
+  post_partials_kernel<BO_RBF, 1, true, false, true, true><<<(unsigned)plan->W, 256, 0, st>>>(
+      Linv, 0, Linv, (int)n, Linv, ld, nullptr, 0.0, nC, nC, nullptr, nullptr, Ainv, plan->segs,
+      plan->wg_off, work, nullptr, 0, 0, nullptr, Linv, 0);
+  BO_LAUNCH_CHECK();
+  if (plan->nred > 0) {
+    post_splitk_reduce_kernel<<<(unsigned)(plan->nred * (PI / 16)), 64, 0, st>>>(
+        work, plan->red, (int)n, nC, nullptr, nullptr, nullptr, Ainv);
+    BO_LAUNCH_CHECK();
+  }
   return BO_OK;
 }
 

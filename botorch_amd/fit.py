@@ -7,7 +7,7 @@ constraints, optim/utils/model_utils.py:69-109) and the closure
 optim/closures/model_closures.py:171-184 (-[G] ExactMarginalLogLikelihood).
 
 Each closure call: kernel matrix + blocked MFMA Cholesky with the jitter ladder
-+ explicit inverse (bo_gp_cache_build), A^{-1} = U U^T (triangular MFMA GEMM),
++ explicit inverse (bo_gp_cache_build), A^{-1} = L^{-T} L^{-1} (bo_ainv),
 one pass of bo_mll_terms; the host reads back n x (d+5) row sums and forms
 the loss and its exact gradient (plus the LogNormal prior terms).
 """
@@ -101,12 +101,10 @@ def mll_terms(Xt: torch.Tensor, y: torch.Tensor, ls_t: torch.Tensor, noise: floa
     ls_t = torch.as_tensor(ls, dtype=torch.float64, device=dev)
     cache = kernels.build_gp_cache(Xt, y, ls_t, noise, const, kind=kind, outputscale=os_,
                                    check_nan=False)  # checked once in fit_gpytorch_mll_scipy
-    # A^{-1} = U U^T: lower triangle only, triangular operands (n^3/3 flops).
-    Ainv = torch.empty(cache.np, cache.np, dtype=torch.float64, device=dev)
+    # A^{-1} = L^{-T} L^{-1}, lower tiles (n^3/3 flops on the posterior kernel's
+    # MFMA tiles, stream-K over the unequal k-ranges)
+    Ainv = kernels.ainv(cache)
     st = kernels._stream(dev)
-    check(lib().bo_gemm_f64(0, 1, cache.np, cache.np, cache.np, 1.0, kernels._p(cache.U), cache.np,
-                            0, kernels._p(cache.U), cache.np, 0, 0.0, kernels._p(Ainv), cache.np, 0,
-                            1, _lib.GEMM_LOWER_C | _lib.GEMM_A_UPPER | _lib.GEMM_B_LOWER, st), "Ainv")
     part = torch.empty(n, d + 5, dtype=torch.float64, device=dev)
     check(lib().bo_mll_terms(kind, kernels._p(Xt.contiguous()), n, d, kernels._p(ls_t), os_,
                              kernels._p(cache.L), kernels._p(Ainv), cache.np,

@@ -230,6 +230,18 @@ def geometry(B: int, q: int, n: int):
     return Qp.value, nrows.value, nC.value
 
 
+def ainv(cache: "GPCache") -> torch.Tensor:
+    """A^{-1} = L^{-T} L^{-1} (np x np; the lower tiles -- tile row >= tile
+    column, diagonal tiles whole -- are written) by bo_ainv."""
+    dev = cache.Linv.device
+    out = torch.empty(cache.np, cache.np, dtype=torch.float64, device=dev)
+    we = ctypes.c_int64()
+    check(lib().bo_ainv_work(cache.n, ctypes.byref(we)), "ainv_work")
+    work = torch.empty(max(1, we.value), dtype=torch.float64, device=dev)
+    check(lib().bo_ainv(_p(cache.Linv), cache.np, cache.n, _p(out), _p(work), _stream(dev)), "ainv")
+    return out
+
+
 def split_plan(B: int, q: int, n: int, slots: int = 0):
     """(kc_len, workspace doubles) of the posterior plan; kc_len = 0: one pass,
     -1: stream-K."""

@@ -246,6 +246,14 @@ int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len,
 /* Workspace doubles of bo_post_partials under a given kc_len (0, -1 or a
  * chunk length). */
 int bo_post_split_work(int64_t B, int q, int64_t n, int kc_len, int64_t* work_elems);
+/* A^{-1} = L^{-T} L^{-1} for the MLL gradient (replaces the U U^T GEMM of
+ * fit.py's closure, optim/closures/model_closures.py:171-184 -> [G]
+ * ExactMarginalLogLikelihood backward): Linv np x np (ld = np = n rounded up
+ * to 128, identity pad), Ainv np x np receives the lower tiles (tile row >=
+ * tile column; diagonal tiles whole).  work >= bo_ainv_work doubles. */
+int bo_ainv_work(int64_t n, int64_t* work_elems);
+int bo_ainv(const double* Linv, int64_t ld, int64_t n, double* Ainv, double* work, void* stream);
+
 /* The segment table of a split plan (host only; tests): up to cap segments as
  * 4 ints (ci | ii << 16, kbeg, kend, chunk or -1 = whole tile in place) and
  * up to wcap + 1 per-workgroup offsets; *nseg, *nwg receive the sizes. */

@@ -349,3 +349,25 @@ def test_posterior_full_c3_matches_oracle():
     oe = kernels.qmc_finalize(c, pe, _lib.QMC_POSTERIOR, orc.ymean.item(), orc.ystd.item())
     torch.testing.assert_close(out["mean"], oe["mean"], rtol=1e-11, atol=1e-12)
     torch.testing.assert_close(out["cov"], oe["cov"], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("n", [37, 300, 1000, 4096])
+def test_ainv_lower_tiles(n):
+    """bo_ainv: A^{-1} = L^{-T} L^{-1} on the stream-K posterior tiles equals
+    the GEMM of the cached inverse on every lower 128 x 128 tile (the part the
+    MLL gradient reads), and the oracle's inverse at small n."""
+    from botorch_amd import kernels
+    X, Y, orc, h = _oracle_model(n)
+    c = _device_cache(X, Y, h, orc)
+    Ai = kernels.ainv(c)
+    Li = c.Linv
+    ref = Li.T @ Li
+    tiles = torch.arange(n, device=Ai.device) // 128
+    low = tiles.view(-1, 1) >= tiles.view(1, -1)  # the n x n block (the pad is not summed)
+    Ai, ref = Ai[:n, :n], ref[:n, :n]
+    torch.testing.assert_close(Ai[low], ref[low], rtol=1e-10, atol=1e-10 * float(ref.abs().max()))
+    if n <= 1000:  # the oracle's (K + s2 I)^{-1} = L^{-T} L^{-1}
+        want = orc.LinvT @ orc.LinvT.T
+        lown = low.cpu()
+        torch.testing.assert_close(Ai.cpu()[lown], want[lown], rtol=1e-7,
+                                   atol=1e-9 * float(want.abs().max()))

@@ -80,13 +80,15 @@ def main():
                                  "merges": float(((ct[:, 1] - ct[:, 5]).double() / 100.0).mean())}
     pre = [(int(ct[kk, 0]) - int(st[i])) / 100.0 for kk, i in enumerate(crit.tolist())]
     out["crit_pre_us_mean"] = sum(pre) / len(pre)
-    ph = trace[4 * ntask + 8 * (np_ // 64): 4 * ntask + 8 * (np_ // 64) + 4 * ntask].view(ntask, 4).cpu()
-    for t in (0, 1, 3):
+    ph = trace[4 * ntask + 8 * (np_ // 64): 4 * ntask + 8 * (np_ // 64) + 8 * ntask].view(ntask, 8).cpu()
+    for t in (0, 1, 2, 3):
         sel = typ == t
         tiles = max(1, int(ph[sel, 3].sum()))
         out[f"{TYPES[t]}_per_tile_us"] = {"commit": float(ph[sel, 0].sum()) / 100.0 / tiles,
+                                          "of_which_operand_wait": float(ph[sel, 5].sum()) / 100.0 / tiles,
                                           "mfma": float(ph[sel, 1].sum()) / 100.0 / tiles,
                                           "store_publish": float(ph[sel, 2].sum()) / 100.0 / tiles,
+                                          "prefetched_frac": float(ph[sel, 4].sum()) / tiles,
                                           "tiles": tiles}
     # the last finishing tasks
     last = torch.argsort(en, descending=True)[:8]
