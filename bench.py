@@ -74,6 +74,29 @@ def pmc_traffic(kernel="post_partials_kernel<0, 6, false, false, true, false>"):
     return e.get("hbm_bytes"), os.path.relpath(files[-1], ROOT)
 
 
+def mfma_f64_ceiling(dev):
+    """On-box fp64 MFMA ceiling, TFLOP/s: bo_probe_mfma_f64_rate (8 independent
+    v_mfma_f64_16x16x4f64 chains per wave, 2048 workgroups = 8 waves per SIMD,
+    operands in registers) timed with HIP events on its launch stream."""
+    import ctypes
+    from botorch_amd import _lib
+    out = torch.zeros(1, dtype=torch.float64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    blocks, iters = 2048, 2000
+    _lib.check(_lib.lib().bo_probe_mfma_f64_rate(blocks, 10, ctypes.c_void_p(out.data_ptr()),
+                                                 ctypes.c_void_p(st.cuda_stream)), "probe")
+    best = 0.0
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        _lib.check(_lib.lib().bo_probe_mfma_f64_rate(blocks, iters, ctypes.c_void_p(out.data_ptr()),
+                                                     ctypes.c_void_p(st.cuda_stream)), "probe")
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        best = max(best, blocks * 4 * iters * 8 * 2048 / (e0.elapsed_time(e1) * 1e-3) / 1e12)
+    return best
+
+
 def cpu_cores():
     """Host cores this process may use: the affinity mask, capped by
     OMP_NUM_THREADS (the GPU box grants a 16-core share of a larger host)."""
@@ -554,6 +577,7 @@ def main():
     fl = flops_post_partials(r1 - r0, Q, N_TRAIN)
     achieved = fl / (kern_avg_ms * 1e-3) / 1e12
     peak = 78.6  # MI355X dense FP64 matrix TFLOP/s (MI355X_MICROARCH.md / SURVEY.md 8(d))
+    peak_box = mfma_f64_ceiling(dev)
     traffic, traffic_src = pmc_traffic()
 
     # forward + backward (the optimize_acqf call pattern, gen.py:194-222)
@@ -612,7 +636,9 @@ def main():
                        "parallelism": f"restart-sharded x{ws}"},
             "roofline": {"bound": "mfma", "kernel": "post_partials_kernel",
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": traffic,
+                         "frac": achieved / peak, "peak_measured": peak_box,
+                         "frac_of_measured": achieved / peak_box if peak_box else None,
+                         "traffic": traffic,
                          "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "kernel_ms": kern_avg_ms, "flops_per_launch": fl},
             "cpu_baseline": cpu,
