@@ -81,6 +81,10 @@ int bo_probe_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work
  * device work): 4 ints per task (type | fin << 8, k, j, i0 | i1 << 16) into
  * out (capacity cap tasks); returns the task count. */
 int bo_chol_dag_tasks(int T, int* out, int cap);
+/* Timing probe (tools/probe_diag16.py): s_memtime ticks per 16 x 16 diagonal
+ * factor + inverse on one wave, out[0..2] = DPP / readlane broadcasts / DPP
+ * factor only; sink: one double of scratch. */
+int bo_probe_diag16(long long* out, double* sink, void* stream);
 
 /* Batched C = alpha op(A) op(B) + beta C on the fp64 matrix cores (strides sA,
  * sB, sC between batch members).  Building block of the Cholesky/inverse and
