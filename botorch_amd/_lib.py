@@ -65,6 +65,8 @@ _SIGNATURES = {
                                    POINTER(c_int64)]),
     "bo_post_split_work": (c_int, [c_int64, c_int, c_int64, c_int, POINTER(c_int64)]),
     "bo_ainv_work": (c_int, [c_int64, POINTER(c_int64)]),
+    "bo_post_w_work": (c_int, [c_int, c_int, c_int64, POINTER(c_int), POINTER(c_int64)]),
+    "bo_post_w_split": (c_int, [_P, c_int64, _P, c_int, c_int, c_int64, _P, _P, _P]),
     "bo_probe_diag16": (c_int, [_P, _P, _P]),
     "bo_ainv": (c_int, [_P, c_int64, c_int64, _P, _P, _P]),
     "bo_post_split_table": (c_int, [c_int64, c_int, c_int64, c_int, _P, c_int, _P, c_int,

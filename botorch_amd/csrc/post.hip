@@ -502,12 +502,20 @@ struct SplitPlan {
 };
 
 // kc_len > 0: uniform chunks of kc_len; kc_len < 0: stream-K over `slots`.
-// ainv: the tiles of A^{-1} = L^{-T} L^{-1} (bo_ainv): column tiles ci >= row
-// tiles ii, k-range [128 ci, n).
-SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, bool ainv = false) {
+// mode PLAN_POST: posterior tiles, k-range [0, min(n, 128 ci + 128));
+// PLAN_AINV: the tiles of A^{-1} = L^{-T} L^{-1} (bo_ainv), column tiles ci >=
+// row tiles ii, k-range [128 ci, n); PLAN_LOWER: every tile, k-range
+// [128 ci, n) (W^T = L^{-T} R^T, bo_post_w).
+enum { PLAN_POST = 0, PLAN_AINV = 1, PLAN_LOWER = 2 };
+SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, int mode = PLAN_POST) {
   struct Seg { int ci, ii, kb, ke; };
   std::vector<std::vector<Seg>> wg;
   auto kfull = [n](int ci) { return std::min(n, ci * PC + PC); };
+  const bool ainv = mode == PLAN_AINV;
+  // k-range of column tile ci, and the column tiles heaviest first
+  auto kbeg_of = [&](int ci) { return mode == PLAN_POST ? 0 : ci * PC; };
+  auto kend_of = [&](int ci) { return mode == PLAN_POST ? kfull(ci) : n; };
+  auto ci_at = [&](int t) { return mode == PLAN_POST ? nC - 1 - t : t; };
   if (ainv) {
     // Stream-K per row tile (lane ii holds column tiles ci = nC-1 .. ii, the
     // shortest k-ranges first); every lane gets workgroups in proportion to
@@ -538,9 +546,11 @@ SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, bool ai
       }
     }
   } else if (kc_len > 0) {
-    for (int ci = nC - 1; ci >= 0; --ci)
-      for (int kb = 0; kb < kfull(ci); kb += kc_len)
-        for (int ii = 0; ii < nI; ++ii) wg.push_back({Seg{ci, ii, kb, std::min(kfull(ci), kb + kc_len)}});
+    for (int t = 0; t < nC; ++t) {
+      const int ci = ci_at(t);
+      for (int kb = kbeg_of(ci); kb < kend_of(ci); kb += kc_len)
+        for (int ii = 0; ii < nI; ++ii) wg.push_back({Seg{ci, ii, kb, std::min(kend_of(ci), kb + kc_len)}});
+    }
   } else {
     // One lane of workgroups per row tile ii, each lane cutting the same
     // sequence (column tiles heaviest first, k ascending) into equal shares:
@@ -549,22 +559,23 @@ SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, bool ai
     // time; they are placed on one XCD (block b: XCD b % 8, slot b / 8) so
     // those slices are fetched into its L2 once.
     int64_t lane_total = 0;
-    for (int ci = 0; ci < nC; ++ci) lane_total += ceil_div(kfull(ci), PK);
+    for (int ci = 0; ci < nC; ++ci) lane_total += ceil_div(kend_of(ci) - kbeg_of(ci), PK);
     const int64_t per_lane =
-        std::max<int64_t>(1, std::min<int64_t>(std::max(1, slots / nI), lane_total / 16));
+        std::max<int64_t>(1, std::min<int64_t>(std::max(1, slots / nI), lane_total / 4));
     const int64_t share = ceil_div(lane_total, per_lane);
     const int64_t jn = ceil_div(lane_total, share);  // workgroups used per lane
     wg.resize((size_t)(ceil_div(jn, 8) * 8 * nI));
     for (int ii = 0; ii < nI; ++ii) {
       int64_t pos = 0;
-      for (int ci = nC - 1; ci >= 0; --ci) {
-        const int L = (int)ceil_div(kfull(ci), PK);
+      for (int t = 0; t < nC; ++t) {
+        const int ci = ci_at(t), kb0 = kbeg_of(ci), ke0 = kend_of(ci);
+        const int L = (int)ceil_div(ke0 - kb0, PK);
         int s0 = 0;
         while (s0 < L) {
           const int64_t j = pos / share;
           const int take = (int)std::min<int64_t>(L - s0, (j + 1) * share - pos);
           const int64_t b = ((j / 8) * nI + ii) * 8 + (j % 8);
-          wg[(size_t)b].push_back(Seg{ci, ii, s0 * PK, std::min(kfull(ci), (s0 + take) * PK)});
+          wg[(size_t)b].push_back(Seg{ci, ii, kb0 + s0 * PK, std::min(ke0, kb0 + (s0 + take) * PK)});
           s0 += take;
           pos += take;
         }
@@ -608,15 +619,15 @@ struct DevPlan {
   int W = 0, nred = 0, nchunks = 0;
 };
 std::mutex g_plan_mu;
-std::map<std::tuple<int, int, int, int, int, int>, DevPlan> g_plans;  // (dev, nC, nI, n, kc, ainv)
+std::map<std::tuple<int, int, int, int, int, int>, DevPlan> g_plans;  // (dev, nC, nI, n, kc, mode)
 
-int device_plan(int nC, int nI, int n, int kc_len, DevPlan** out, bool ainv = false) {
+int device_plan(int nC, int nI, int n, int kc_len, DevPlan** out, int mode = PLAN_POST) {
   int dev = 0;
   BO_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_plan_mu);
-  DevPlan& dp = g_plans[std::make_tuple(dev, nC, nI, n, kc_len, ainv ? 1 : 0)];
+  DevPlan& dp = g_plans[std::make_tuple(dev, nC, nI, n, kc_len, mode)];
   if (!dp.wg_off) {
-    const SplitPlan p = build_split_plan(nC, nI, n, kc_len, kSlots, ainv);
+    const SplitPlan p = build_split_plan(nC, nI, n, kc_len, kSlots, mode);
     BO_HIP(hipMalloc(&dp.segs, sizeof(int4) * std::max<size_t>(1, p.segs.size())));
     BO_HIP(hipMalloc(&dp.red, sizeof(int4) * std::max<size_t>(1, p.red.size())));
     BO_HIP(hipMalloc(&dp.wg_off, sizeof(int) * p.wg_off.size()));
@@ -859,13 +870,61 @@ int bo_post_w(const double* Linv, int64_t ldl, const double* Rt, int B, int q, i
   return BO_OK;
 }
 
+// W^T = L^{-T} R^T under a stream-K plan (the k-ranges [128 ci, n) are very
+// unequal; grids below four tiles per slot).  *kc_len = -1 and the workspace
+// when the plan applies, else 0 (use bo_post_w or a GEMM).
+int bo_post_w_work(int B, int q, int64_t n, int* kc_len, int64_t* work_elems) {
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  const int nI = nrows_pad / PI;
+  *kc_len = 0;
+  *work_elems = 0;
+  int64_t steps = 0;
+  for (int ci = 0; ci < nC; ++ci) steps += (int64_t)nI * ceil_div(n - ci * PC, PK);
+  if (nI > 0 && (int64_t)nC * nI < 4 * (int64_t)kSlots && steps >= kSlots) {
+    const SplitPlan p = build_split_plan(nC, nI, (int)n, -1, kSlots, PLAN_LOWER);
+    *kc_len = -1;
+    *work_elems = (int64_t)p.nchunks * PI * PC;
+  }
+  return BO_OK;
+}
+
+int bo_post_w_split(const double* Linv, int64_t ldl, const double* Rt, int B, int q, int64_t n,
+                    double* Wt, double* work, void* stream) {
+  BO_CHECK_ARG(ldl % 2 == 0 && ldl >= ceil_div(n, PC) * PC, "L^{-1} leading dim %lld too small",
+               (long long)ldl);
+  if (B == 0) return BO_OK;
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  const int nI = nrows_pad / PI;
+  if (nI == 0) return BO_OK;
+  DevPlan* plan = nullptr;
+  s = device_plan(nC, nI, (int)n, -1, &plan, PLAN_LOWER);
+  if (s) return s;
+  BO_CHECK_ARG(plan->nchunks == 0 || work != nullptr, "bo_post_w_split needs a workspace of %lld doubles",
+               (long long)plan->nchunks * PI * PC);
+  hipStream_t st = as_stream(stream);
+  post_partials_kernel<BO_RBF, 1, true, false, true, true><<<(unsigned)plan->W, 256, 0, st>>>(
+      Rt, 0, Rt, (int)n, Linv, ldl, nullptr, 0.0, nC, nI, nullptr, nullptr, Wt, plan->segs,
+      plan->wg_off, work, nullptr, 0, 0, nullptr, Rt, 0);
+  BO_LAUNCH_CHECK();
+  if (plan->nred > 0) {
+    post_splitk_reduce_kernel<<<(unsigned)(plan->nred * (PI / 16)), 64, 0, st>>>(
+        work, plan->red, (int)n, nI, nullptr, nullptr, nullptr, Wt);
+    BO_LAUNCH_CHECK();
+  }
+  return BO_OK;
+}
+
 // A^{-1} = L^{-T} L^{-1} (lower tiles: Ainv[r][c] for tile row >= tile column)
 // from L^{-1} (np x np, ld = np, identity pad): the posterior kernel's lower
 // k-range MFMA tiles with L^{-1} as both operands, under a stream-K plan (the
 // k-ranges [128 ci, n) are very unequal), partial tiles reduced in k order.
 int bo_ainv_work(int64_t n, int64_t* work_elems) {
   const int nC = (int)ceil_div(n, PC);
-  const SplitPlan p = build_split_plan(nC, nC, (int)n, -1, kSlots, true);
+  const SplitPlan p = build_split_plan(nC, nC, (int)n, -1, kSlots, PLAN_AINV);
   *work_elems = (int64_t)p.nchunks * PI * PC;
   return BO_OK;
 }
@@ -875,7 +934,7 @@ int bo_ainv(const double* Linv, int64_t ld, int64_t n, double* Ainv, double* wor
   BO_CHECK_ARG(n > 0 && ld == (int64_t)nC * PC, "bo_ainv: ld %lld must be n rounded up to %d",
                (long long)ld, PC);
   DevPlan* plan = nullptr;
-  int s = device_plan(nC, nC, (int)n, -1, &plan, true);
+  int s = device_plan(nC, nC, (int)n, -1, &plan, PLAN_AINV);
   if (s) return s;
   BO_CHECK_ARG(plan->nchunks == 0 || work != nullptr, "bo_ainv needs a workspace of %lld doubles",
                (long long)plan->nchunks * PI * PC);

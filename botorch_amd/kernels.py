@@ -396,16 +396,25 @@ class WMat:
 
 
 def w_matrix(cache: GPCache, pp: PostPartials, post_w: Optional[bool] = None) -> WMat:
-    """W = R L^{-1} = K*x (K + s2 I)^{-1}, from the stored R^T.  Grids of 8 x 8
-    super-tiles: W^T = L^{-T} R^T on the posterior kernel's MFMA tiles
-    (bo_post_w); otherwise the GEMM W[i][k] = sum_c R[i][c] U[k][c] (U = L^{-T}
-    upper -> op(B) zero below c < k).  ``post_w``: None = bo_post_w when its
-    grid fills the 512 resident slots (C3: 2048 workgroups; C4's 128 run
-    faster as 64 x 64 GEMM tiles), True = whenever the grid allows it."""
+    """W = R L^{-1} = K*x (K + s2 I)^{-1}, from the stored R^T, as W^T =
+    L^{-T} R^T on the posterior kernel's MFMA tiles: under a stream-K plan
+    below four tiles per slot (bo_post_w_split), one pass on grids of 8 x 8
+    super-tiles (bo_post_w); otherwise the GEMM W[i][k] = sum_c R[i][c] U[k][c]
+    (U = L^{-T} upper -> op(B) zero below c < k).  ``post_w``: None = the plan
+    above, True = bo_post_w whenever the grid allows it, False = the GEMM."""
     if pp.Rt is None:
         raise RuntimeError("post_partials(store_R=True) is required for gradients")
     dev = pp.Rt.device
     nI = pp.nrows_pad // 128
+    kc, we = ctypes.c_int(), ctypes.c_int64()
+    check(lib().bo_post_w_work(pp.B, pp.q, cache.n, ctypes.byref(kc), ctypes.byref(we)), "post_w_work")
+    if post_w is None and kc.value == -1:
+        # stream-K W^T: grids below four tiles per slot (b <= 256 at n = 4096, C4)
+        Wt = torch.empty(cache.np, pp.nrows_pad, dtype=torch.float64, device=dev)
+        work = torch.empty(max(1, we.value), dtype=torch.float64, device=dev)
+        check(lib().bo_post_w_split(_p(cache.Linv), cache.np, _p(pp.Rt), pp.B, pp.q, cache.n, _p(Wt),
+                                    _p(work), _stream(dev)), "post_w_split")
+        return WMat(Wt, True)
     if post_w is None:
         post_w = pp.nC * nI >= 512
     if post_w and pp.nC % 8 == 0 and nI % 8 == 0:

@@ -240,6 +240,13 @@ int bo_post_kxt(int kind, const double* Xq, int B, int q, int d, const double* X
  * super-tiles (the caller then uses bo_gemm_f64). */
 int bo_post_w(const double* Linv, int64_t ldl, const double* Rt, int B, int q, int64_t n,
               double* Wt, void* stream);
+/* The same W^T under a stream-K plan (grids below four tiles per resident
+ * slot, where the k-ranges [128 c, n) leave the one-pass grid imbalanced; no
+ * super-tile condition).  bo_post_w_work: *kc_len = -1 and the workspace
+ * doubles when the plan applies, else *kc_len = 0. */
+int bo_post_w_work(int B, int q, int64_t n, int* kc_len, int64_t* work_elems);
+int bo_post_w_split(const double* Linv, int64_t ldl, const double* Rt, int B, int q, int64_t n,
+                    double* Wt, double* work, void* stream);
 
 /* Plan of bo_post_partials (host pointers): kc_len = 0 (one pass) or -1
  * (stream-K), whichever a k-step cost model of the triangular grid over

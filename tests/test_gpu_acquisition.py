@@ -480,3 +480,26 @@ def test_qei_forward_only_ladder_status_is_deferred():
         kernels.check_ladder_status()
         assert any(issubclass(w.category, NumericalWarning) for w in ws)
     assert torch.isfinite(v).all()
+
+
+@pytest.mark.parametrize("n,B,q", [(4096, 64, 16), (1000, 64, 8), (2048, 128, 8)])
+def test_post_w_stream_k_matches_gemm(n, B, q):
+    """Stream-K W^T = L^{-T} R^T (bo_post_w_split, the default below four tiles
+    per slot) against the triangular GEMM route, and post_backward through it
+    against the GEMM's W."""
+    from botorch_amd import _lib, kernels
+    X, Y, m, orc = _setup(n=n)
+    g = torch.Generator().manual_seed(n + B)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64)
+    cache = m.prediction_cache()
+    pp = kernels.post_partials(cache, Xc.to(DEV), store_R=True)
+    W = kernels.w_matrix(cache, pp)
+    assert W.kmajor  # the stream-K plan applies at these grids
+    Wg = kernels.gemm(pp.Rt, cache.U, transA=True, transB=True, flags=_lib.GEMM_B_LOWER)
+    atol = 1e-11 * max(1.0, n / 1024)
+    torch.testing.assert_close(W.t.T[:, :n], Wg[:, :n], rtol=1e-10, atol=atol)
+    dmean = torch.randn(B, q, generator=g, dtype=torch.float64).to(DEV)
+    dcov = torch.randn(B, q, q, generator=g, dtype=torch.float64).to(DEV)
+    dx_k = kernels.post_backward(cache, pp, W, dmean, dcov, 0.7)
+    dx_r = kernels.post_backward(cache, pp, kernels.WMat(Wg, False), dmean, dcov, 0.7)
+    torch.testing.assert_close(dx_k, dx_r, rtol=1e-9, atol=1e-11)

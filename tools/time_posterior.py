@@ -22,11 +22,16 @@ def main():
     ls = torch.full((d,), 0.4, dtype=torch.float64, device=dev)
     cache = kernels.build_gp_cache(X, y, ls, 1e-3, 0.0)
     out = {}
-    for B in (64, 128, 256, 512):
+    Xs = torch.rand(1024, d, generator=g, dtype=torch.float64).to(dev)
+    ys = torch.randn(1024, generator=g, dtype=torch.float64).to(dev)
+    c2 = kernels.build_gp_cache(Xs, ys, ls, 1e-3, 0.0)
+    for B, q, cache in ((64, 16, cache), (128, 16, cache), (256, 16, cache), (512, 16, cache),
+                        (64, 8, c2)):
+        n = cache.n
         Xc = torch.rand(B, q, d, generator=g, dtype=torch.float64).to(dev)
         plan = kernels.split_plan(B, q, n)[0]
         row = {"plan": plan}
-        for name, split in (("auto", None), ("one_pass", 0), ("stream_k", -1)):
+        for name, split in (("auto", None), ("one_pass", 0), ("stream_k", -1), ("kc64", 64)):
             ts = []
             for rep in range(23):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -38,7 +43,7 @@ def main():
                     ts.append(e0.elapsed_time(e1) * 1e3)
             ts.sort()
             row[name] = round(ts[len(ts) // 2], 1)
-        out[B] = row
+        out[f"n{n}_b{B}_q{q}"] = row
     print(json.dumps(out))
 
 
