@@ -231,6 +231,22 @@ def other_configs(dev, cpu=True):
         t = _gpu_time(lambda: acqf(Xd), steps=20, warmup=3)
     e = {"config": "C2 qEI n=1024 d=6 q=8 S=256 b=64", "gpu_evals_per_s": q * S * b / t,
          "gpu_ms": 1e3 * t}
+    # the same forward (and forward + backward) captured once as a HIP graph and
+    # replayed (botorch_amd.graphs; values bit-equal to the eager call)
+    from botorch_amd.graphs import GraphedAcquisition
+    ga = GraphedAcquisition(acqf, Xd)
+    tg = _gpu_time(lambda: ga(Xd), steps=50, warmup=5)
+    Xg = Xd.clone().requires_grad_(True)
+
+    def c2_fb():
+        v = acqf(Xg)
+        torch.autograd.grad(v.sum(), Xg)
+
+    tfb = _gpu_time(c2_fb, steps=20, warmup=3)
+    gab = GraphedAcquisition(acqf, Xd, with_grad=True)
+    tgb = _gpu_time(lambda: gab(Xd), steps=50, warmup=5)
+    e.update(graphed_ms=1e3 * tg, graphed_evals_per_s=q * S * b / tg, fwd_bwd_ms=1e3 * tfb,
+             graphed_fwd_bwd_ms=1e3 * tgb)
     if cpu:
         orc = ExactGPOracle(X, Y, GPHyper(torch.full((6,), LENGTHSCALE, dtype=f64), NOISE, 0.0))
         Z = base_samples_single_output(S, q, 0)
@@ -311,10 +327,15 @@ def other_configs(dev, cpu=True):
         return initialize_q_batch_nonneg(Xr, Yr, b).to(dev)
 
     t_host = _gpu_time(host_protocol, steps=5, warmup=1)
+    # the reference default (no init_batch_limit): all 2048 raw designs in one
+    # forward launch
+    t_one = _gpu_time(lambda: gen_batch_initial_conditions(acq_ei, bounds_d, q, b, raw,
+                                                           options={"seed": 0}), steps=5, warmup=1)
     out["C3_init"] = {"config": "C3 gen_batch_initial_conditions: qEI, 2048 raw x q=16, 512 restarts, "
-                                "S=512, init_batch_limit=512",
+                                "S=512, init_batch_limit=512 (and unlimited: one launch)",
                       "device_ms": 1e3 * t_dev, "host_roundtrip_ms": 1e3 * t_host,
-                      "raw_evals_per_s": raw * q * S / t_dev}
+                      "device_one_launch_ms": 1e3 * t_one,
+                      "raw_evals_per_s": raw * q * S / min(t_dev, t_one)}
     acqf = qLogNoisyExpectedImprovement(m, X.to(dev), sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0),
                                         prune_baseline=True)
     with torch.no_grad():

@@ -1,0 +1,99 @@
+"""HIP-graph capture of an acquisition evaluation (hard
+part 6: launch-bound inner loops).
+
+A fused qEI / qLogEI forward (and, with ``with_grad``, its backward) issues a
+fixed sequence of launches for a fixed X shape: prepare_rows, the K*x^T build,
+the posterior kernel (+ its split reduction), the finalisation, and the
+ladder-status reduction.  At small shapes (C2: 64 t-batches, n = 1024) the
+host-side dispatch of that sequence costs as much as the kernels.
+``GraphedAcquisition`` captures it once with ``torch.cuda.graph`` on the
+caller's device and replays it: a call copies X into the captured input
+buffer, replays the graph and returns the captured outputs.
+
+The reference has no counterpart (it evaluates eagerly through gpytorch); the
+values are the eager path's, bit for bit (tests/test_gpu_graphs.py).  The
+jitter-ladder status of a replay is kept on the device and checked at the next
+call (``check_each_call``) or by ``check_status()`` (the same deferral as the
+eager forward-only path, kernels.raise_not_psd_deferred; the device optimiser
+checks it at its own status reads only).
+
+Constraints of capture: the model's caches, the Sobol base samples and the
+split plans must exist before capture (two eager warm-up calls build them),
+and the model must not change between replays (a changed model raises).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import kernels
+
+
+class GraphedAcquisition:
+    """Callable wrapper: ``GraphedAcquisition(acqf, X_example)(X)`` equals
+    ``acqf(X)`` for X of X_example's shape; with ``with_grad`` it returns
+    ``(acq, dacq_sum/dX)`` (the gradient ``gen_candidates_*`` needs)."""
+
+    def __init__(self, acqf, X_example: torch.Tensor, with_grad: bool = False, warmup: int = 2,
+                 check_each_call: bool = True):
+        if not X_example.is_cuda:
+            raise RuntimeError("GraphedAcquisition captures ROCm device work")
+        self.acqf = acqf
+        self.with_grad = with_grad
+        self.check_each_call = check_each_call
+        self.dev = X_example.device
+        self.X = X_example.detach().clone()
+        self._model_key = self._key()
+        side = torch.cuda.Stream(self.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._body()
+        torch.cuda.current_stream(self.dev).wait_stream(side)
+        kernels.check_ladder_status(self.dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with kernels.capturing(self.dev):
+            with torch.cuda.graph(self.graph):
+                self.out = self._body()
+        self._status = kernels.take_captured_status(self.dev)
+        self._pending = False
+
+    def _key(self):
+        m = getattr(self.acqf, "model", None)
+        return m._key() if m is not None and hasattr(m, "_key") else None
+
+    def _body(self):
+        if self.with_grad:
+            Xg = self.X.requires_grad_(True)
+            v = self.acqf(Xg)
+            (g,) = torch.autograd.grad(v.sum(), Xg)
+            self.X.requires_grad_(False)
+            return v.detach(), g
+        with torch.no_grad():
+            return self.acqf(self.X)
+
+    def check_status(self) -> None:
+        """Raise NotPSDError / warn for the last replay's jitter ladder."""
+        if self._pending and self._status is not None:
+            self._pending = False
+            packed, what = self._status
+            vals = packed.cpu()
+            kernels._ladder_outcome(float(vals[0]), float(vals[1]), what)
+
+    def __call__(self, X: torch.Tensor):
+        if X.shape != self.X.shape:
+            raise ValueError(f"captured for X of shape {tuple(self.X.shape)}, got {tuple(X.shape)}")
+        if self._key() != self._model_key:
+            raise RuntimeError("the model changed since capture; build a new GraphedAcquisition")
+        if self.check_each_call:
+            self.check_status()  # the previous replay's ladder (one call behind)
+        self.X.copy_(X.detach())
+        self.graph.replay()
+        self._pending = True
+        return self.out
+
+
+def graphed(acqf, X_example: torch.Tensor, with_grad: bool = False) -> Optional[GraphedAcquisition]:
+    """GraphedAcquisition(acqf, X_example, with_grad)."""
+    return GraphedAcquisition(acqf, X_example, with_grad=with_grad)

@@ -527,8 +527,51 @@ def _ladder_outcome(info_max: float, jitter_max: float, what: str) -> None:
         warnings.warn(f"A not p.d., added jitter of {jitter_max:.1e} to the diagonal", NumericalWarning)
 
 
+# Graph capture (graphs.GraphedAcquisition): inside capturing(dev) the ladder
+# status is reduced into a device buffer that the graph owns and is read by
+# the wrapper after a replay -- no host read, pinned copy or event in the graph.
+_CAPTURE = {}
+
+
+class capturing:
+    """Context of a HIP-graph capture on ``device`` (see _CAPTURE)."""
+
+    def __init__(self, device):
+        d = torch.device(device)
+        self.idx = d.index if d.index is not None else torch.cuda.current_device()
+
+    def __enter__(self):
+        _CAPTURE[self.idx] = None
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+def take_captured_status(device):
+    """(packed status tensor, what) written by the captured forward, or None."""
+    d = torch.device(device)
+    idx = d.index if d.index is not None else torch.cuda.current_device()
+    return _CAPTURE.pop(idx, None)
+
+
+def _capture_status(info: torch.Tensor, jitter: torch.Tensor, what: str) -> bool:
+    dev = info.device
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _CAPTURE:
+        return False
+    packed = torch.zeros(2, dtype=torch.float64, device=dev)
+    if info.numel():
+        check(lib().bo_ladder_status(_p(info.contiguous()), _p(jitter.contiguous()), info.numel(),
+                                     _p(packed), _stream(dev)), "ladder_status")
+    _CAPTURE[idx] = (packed, what)
+    return True
+
+
 def raise_not_psd_deferred(info: torch.Tensor, jitter: torch.Tensor, what: str) -> None:
     """_raise_not_psd without the per-call device-to-host synchronisation."""
+    if _capture_status(info, jitter, what):
+        return
     if SYNC_LADDER or info.numel() == 0:
         return _raise_not_psd(info, jitter, what)
     dev = info.device
@@ -549,7 +592,7 @@ def raise_not_psd_deferred(info: torch.Tensor, jitter: torch.Tensor, what: str) 
 def _raise_not_psd(info: torch.Tensor, jitter: torch.Tensor, what: str):
     """Host check of a batched ladder (one D2H read, as [G] psd_safe_cholesky's
     torch.any(info)); warns like [G] when jitter was added."""
-    if info.numel() == 0:
+    if info.numel() == 0 or _capture_status(info, jitter, what):
         return
     packed = torch.empty(2, dtype=torch.float64, device=info.device)
     check(lib().bo_ladder_status(_p(info.contiguous()), _p(jitter.contiguous()), info.numel(),

@@ -325,7 +325,9 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     ``ftol`` / ``gtol``) on the GPU.  One evaluation = one batched forward +
     backward of the acquisition at all trial points + one bo_lbfgs_step launch;
     the iterate, gradient and history never leave HBM, and the host reads the
-    (B,) status vector only every ``check_every`` evaluations.
+    (B,) status vector only every ``check_every`` evaluations.  ``use_graph``
+    (default True): the evaluation is captured once as a HIP graph and
+    replayed (botorch_amd.graphs), where the acquisition allows capture.
 
     ``maxiter`` bounds the function evaluations per restart (scipy's own
     ``maxfun`` analogue); returns (candidates b x q x d, acq values b)."""
@@ -355,13 +357,30 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
           else torch.full((st.n,), math.inf, dtype=torch.float64, device=X0.device))
     stream = kernels._stream(X0.device)
     P = kernels._p
+    # one evaluation (forward + backward at all trial points) as a HIP graph
+    # replay where the acquisition allows capture (the fused qEI / qLogEI
+    # paths); the eager autograd evaluation otherwise
+    ga = None
+    if options.get("use_graph", True):
+        from .graphs import GraphedAcquisition
+        try:
+            ga = GraphedAcquisition(acquisition_function, st.xt.view(shapeX), with_grad=True,
+                                    warmup=1, check_each_call=False)
+        except RuntimeError:  # capture refused (e.g. a generic route with host reads)
+            ga = None
+            torch.cuda.synchronize(X0.device)
     t0 = time.monotonic()
     for it in range(maxiter + 1):
-        Xt = st.xt.view(shapeX).detach().requires_grad_(True)
-        ft = -acquisition_function(Xt)
-        (gt,) = torch.autograd.grad(ft.sum(), Xt)
-        ft = ft.detach().reshape(-1).to(torch.float64).contiguous()
-        gt = gt.reshape(st.B, st.n).to(torch.float64).contiguous()
+        if ga is not None:
+            v, g = ga(st.xt.view(shapeX))
+            ft = (-v).reshape(-1).to(torch.float64).contiguous()
+            gt = (-g).reshape(st.B, st.n).to(torch.float64).contiguous()
+        else:
+            Xt = st.xt.view(shapeX).detach().requires_grad_(True)
+            ft = -acquisition_function(Xt)
+            (gt,) = torch.autograd.grad(ft.sum(), Xt)
+            ft = ft.detach().reshape(-1).to(torch.float64).contiguous()
+            gt = gt.reshape(st.B, st.n).to(torch.float64).contiguous()
         a = _lib.LbfgsStepArgs(B=st.B, n=st.n, m=m, x=st.x, f=st.f, g=st.g, xt=st.xt, ft=ft, gt=gt,
                                d=st.d, alpha=st.alpha, S=st.S, Y=st.Y, rho=st.rho,
                                hcount=st.hcount, hhead=st.hhead, status=st.status, nacc=st.nacc,
@@ -369,6 +388,8 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
                                min_alpha=1e-12)
         check(lib().bo_lbfgs_step_v(ctypes.byref(a), stream), "lbfgs_step")
         if (it + 1) % check_every == 0 or it == maxiter:
+            if ga is not None:
+                ga.check_status()
             if bool((st.status > 0).all()):
                 break
             if timeout_sec is not None and time.monotonic() - t0 > timeout_sec:
