@@ -48,6 +48,8 @@ constexpr int TB = 64;  // tile
 constexpr int LP = 68;  // LDS pitch in doubles (rows 16-B aligned)
 constexpr int CH = 8;   // tile rows per chunked task
 constexpr int NFLAG0 = 16;  // head counter, abort word, padding
+constexpr int GB = 3;       // steps per batched column update (LDS: X0 + GB operand tiles)
+constexpr int CHB = 8;      // tile rows per batched task (4 measured slower: 2.11 vs 2.00 ms)
 constexpr long long SPIN_TIMEOUT = 200000000;  // wall-clock ticks (100 MHz): 2 s
 
 enum : int { T_CRIT = 0, T_TRSM = 1, T_COLUPD = 2, T_XSTEP = 3 };
@@ -668,6 +670,113 @@ __device__ bool row_loop(const Ctx& c, const Flags& f, int k, int j, int i0, int
   return true;
 }
 
+// Batched column update: A_ij -= sum_{k in [kb, kb + nk)} L_ik L_jk^T for the
+// rows of the chunk, the L_jk of the batch resident in LDS (XB[g]).  A_ij is
+// loaded and stored once per batch instead of once per step: per tile update
+// the HBM traffic falls from 96 KB (A operand + A_ij in + A_ij out) to
+// 32 + 64 / nk KB -- the hand-off traffic, not the MFMAs, bounds the bulk.
+// KIND 1: A_ij -= sum_k L_ik L_jk^T (fA[i][j] = kb + nk);
+// KIND 2: acc_ij += sum_k L_ik X_kj (X_kj transposed in XB; fX[i][j] = kb + nk - j).
+template <int KIND>
+__device__ bool batched_update(const Ctx& c, const Flags& f, int kb, int nk, int j, int i0, int i1,
+                               double* X0, double* XB0, double* XB1, double* XB2, int* s_ok,
+                               int* s_rdy, long long* wsum, long long* ph = nullptr) {
+  auto XB = [&](int g) { return g == 0 ? XB0 : (g == 1 ? XB1 : XB2); };
+  const rsrc_t rc = KIND == 1 ? c.rA : c.rI;                      // C tile in / out
+  u32* const fC = KIND == 1 ? f.fA : f.fX;                        // its version flags
+  const u32 v0 = KIND == 1 ? (u32)kb : (u32)(kb - j);             // version before / after
+  const u32 v1 = v0 + (u32)nk;
+  const double sgn = KIND == 1 ? -1.0 : 1.0;
+  double2 pv[8];
+  double pa[16];
+  Acc acc;
+  bool pre = false;
+  const int ke = kb + nk;
+  auto issue_a = [&](int i, int k) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int e = c.tid + 256 * p;
+      pv[p] = ld16(c.rA, toff(c, i, k, e >> 5, (e & 31) * 2));
+    }
+  };
+  auto issue_c = [&](int i) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          pa[8 * a + 4 * b + q] = ld8(rc, toff(c, i, j, c.wm + 16 * a + mfma_row(c.lane, q),
+                                               c.wn + 16 * b + mfma_col(c.lane)));
+  };
+  for (int i = i0; i < i1; ++i) {
+    long long tA = 0;
+    if (ph && c.tid == 0) ph[4] += pre ? 1 : 0;
+    if (!pre) {
+      if (!wait2(c, f.at(f.fL, i, ke - 1), 1u, f.at(fC, i, j), v0, f.abortw, s_ok, wsum))
+        return false;
+      issue_c(i);
+      if (KIND == 2 || i != j) issue_a(i, kb);
+      if (c.tid == 0) {
+        int mask = 0;
+        for (int ii = i + 1; ii < i1 && ii < i + 31; ++ii) {
+          if (flag_load(f.at(f.fL, ii, ke - 1)) >= 1u && flag_load(f.at(fC, ii, j)) >= v0)
+            mask |= 1 << (ii - i);
+          else
+            break;
+        }
+        s_rdy[i & 1] = mask;
+      }
+    }
+    if (ph && c.tid == 0) tA = wall_clock64();
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc.t[a][b][q] = pa[8 * a + 4 * b + q];
+    __syncthreads();  // s_rdy
+    const int mask = s_rdy[i & 1];
+    const bool next = (mask >> 1) & 1;
+    long long tB = 0, tm = 0;
+    for (int g = 0; g < nk; ++g) {
+      const bool own = KIND == 2 || i != j;  // COLUPD's diagonal tile: the A operand is XB(g)
+      if (own) {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+          const int e = c.tid + 256 * p;
+          *reinterpret_cast<double2*>(X0 + (e >> 5) * LP + (e & 31) * 2) = pv[p];
+        }
+        __syncthreads();
+      }
+      // the next operand tile (this row's next step, or the next row's first
+      // step and C) in flight under this step's MFMAs
+      if (g + 1 < nk) {
+        if (KIND == 2 || i != j) issue_a(i, kb + g + 1);
+      } else if (next) {
+        issue_c(i + 1);
+        if (KIND == 2 || i + 1 != j) issue_a(i + 1, kb);
+      }
+      if (ph && c.tid == 0) tB = wall_clock64();
+      acc_mma_nt(c, acc, own ? X0 : XB(g), XB(g), sgn);
+      if (ph && c.tid == 0) tm += wall_clock64() - tB;
+      __syncthreads();  // X0 free for the next step's operand
+    }
+    pre = next;
+    if (c.tid == 0) s_rdy[(i + 1) & 1] = mask >> 1;
+    long long tC = 0;
+    if (ph && c.tid == 0) {
+      tC = wall_clock64();
+      ph[1] += tm;
+      ph[0] += tC - tA - tm;
+    }
+    acc_store(c, acc, rc, i, j);
+    publish(c, f.at(fC, i, j), v1);
+    if (ph && c.tid == 0) { ph[2] += wall_clock64() - tC; ph[3] += nk; }
+  }
+  return true;
+}
+
 __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, double* __restrict__ Linv,
                                                        int np, int T, const int4* __restrict__ tasks,
                                                        int ntasks, u32* __restrict__ flags,
@@ -675,6 +784,8 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
                                                        long long* __restrict__ trace) {
   __shared__ __attribute__((aligned(16))) double X0[TB * LP];
   __shared__ __attribute__((aligned(16))) double X1[TB * LP];
+  __shared__ __attribute__((aligned(16))) double X2[TB * LP];  // batched update operands
+  __shared__ __attribute__((aligned(16))) double X3[TB * LP];
   __shared__ double rinv[TB];
   __shared__ int s_ok;
   __shared__ int s_rdy[2];
@@ -707,7 +818,7 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
   Acc acc;
   while (t < ntasks) {
     const int4 tk = tasks[t];
-    const int type = tk.x & 0xff, fin = tk.x >> 8;
+    const int type = tk.x & 0xff, fin = (tk.x >> 8) & 0xff, nk = tk.x >> 16;
     long long wsum = 0;
     long long phs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long* ph = trace ? phs : nullptr;
@@ -754,10 +865,28 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
       ok = wait2(c, F(fL, k, k), 1u, F(fL, k, k), 1u, abortw, &s_ok, &wsum);
       if (ok) tile_to_lds(c, c.rI, k, k, X1);  // D_k
       if (ok) ok = row_loop<0>(c, fl, k, j, i0, i1, X0, X1, &s_ok, s_rdy, &wsum, ph);
+    } else if (type == T_COLUPD && nk > 1) {
+      ok = wait2(c, F(fL, j, k + nk - 1), 1u, F(fL, j, k + nk - 1), 1u, abortw, &s_ok, &wsum);
+      if (ok) {
+        for (int g = 0; g < nk; ++g)  // L_jk of the batch
+          tile_to_lds(c, c.rA, j, k + g, g == 0 ? X1 : (g == 1 ? X2 : X3));
+        __syncthreads();
+        ok = batched_update<1>(c, fl, k, nk, j, i0, i1, X0, X1, X2, X3, &s_ok, s_rdy, &wsum, ph);
+      }
     } else if (type == T_COLUPD) {
       ok = wait2(c, F(fL, j, k), 1u, F(fL, j, k), 1u, abortw, &s_ok, &wsum);
       if (ok) tile_to_lds(c, c.rA, j, k, X1);  // L_jk
       if (ok) ok = row_loop<1>(c, fl, k, j, i0, i1, X0, X1, &s_ok, s_rdy, &wsum, ph);
+    } else if (nk > 1) {  // T_XSTEP, batched: the far rows of steps k .. k + nk - 1
+      const int kl = k + nk - 1;  // X_{k..kl, j} final once X_{kl, j} is
+      if (kl == j) ok = wait2(c, F(fL, j, j), 1u, F(fL, j, j), 1u, abortw, &s_ok, &wsum);
+      else ok = wait2(c, F(fXd, kl, j), 1u, F(fXd, kl, j), 1u, abortw, &s_ok, &wsum);
+      if (ok) {
+        for (int g = 0; g < nk; ++g)  // X_kj transposed (X_jj = D_j)
+          tile_to_lds_t(c, c.rI, k + g, j, g == 0 ? X1 : (g == 1 ? X2 : X3));
+        __syncthreads();
+        ok = batched_update<2>(c, fl, k, nk, j, i0, i1, X0, X1, X2, X3, &s_ok, s_rdy, &wsum, ph);
+      }
     } else {  // T_XSTEP: column j of X at step k
       if (k == j) {
         ok = wait2(c, F(fL, k, k), 1u, F(fL, k, k), 1u, abortw, &s_ok, &wsum);
@@ -811,10 +940,11 @@ struct DagTable {
   int n = 0;
 };
 
-void push_rows(std::vector<int4>& v, int type, int k, int j, int lo, int hi, bool first_fin) {
+void push_rows(std::vector<int4>& v, int type, int k, int j, int lo, int hi, bool first_fin,
+               int ch = CH) {
   bool first = true;
-  for (int i0 = lo; i0 < hi; i0 += CH) {
-    const int i1 = i0 + CH < hi ? i0 + CH : hi;
+  for (int i0 = lo; i0 < hi; i0 += ch) {
+    const int i1 = i0 + ch < hi ? i0 + ch : hi;
     v.push_back(make_int4(type | ((first && first_fin) ? 256 : 0), k, j, i0 | (i1 << 16)));
     first = false;
   }
@@ -832,7 +962,8 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
   // version-indexed producers: A(i,j) after v updates (v = 1..j), X(i,j) after v
   std::vector<std::vector<int>> prodA((size_t)T * T), prodX((size_t)T * T);
   for (int t = 0; t < n; ++t) {
-    const int type = v[t].x & 0xff, fin = v[t].x >> 8, k = v[t].y, j = v[t].z;
+    const int type = v[t].x & 0xff, fin = (v[t].x >> 8) & 0xff, k = v[t].y, j = v[t].z;
+    const int nk = std::max(1, v[t].x >> 16);
     const int i0 = v[t].w & 0xffff, i1 = v[t].w >> 16;
     if (type == T_CRIT) {
       prodL[tix(k, k)] = t;
@@ -842,15 +973,15 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
     } else if (type == T_COLUPD) {
       for (int i = i0; i < i1; ++i) {
         auto& pa = prodA[tix(i, j)];
-        if ((int)pa.size() < k + 2) pa.resize(k + 2, -1);
-        pa[k + 1] = t;
+        if ((int)pa.size() < k + nk + 1) pa.resize(k + nk + 1, -1);
+        pa[k + nk] = t;
       }
     } else {
       if (fin && k > j) prodXd[tix(k, j)] = t;
       for (int i = i0; i < i1; ++i) {
         auto& px = prodX[tix(i, j)];
-        if ((int)px.size() < k - j + 2) px.resize(k - j + 2, -1);
-        px[k - j + 1] = t;
+        if ((int)px.size() < k + nk - j + 1) px.resize(k + nk - j + 1, -1);
+        px[k + nk - j] = t;
       }
     }
   }
@@ -865,7 +996,8 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
   std::vector<std::vector<int>> deps(n);
   std::vector<double> dur(n);
   for (int t = 0; t < n; ++t) {
-    const int type = v[t].x & 0xff, fin = v[t].x >> 8, k = v[t].y, j = v[t].z;
+    const int type = v[t].x & 0xff, fin = (v[t].x >> 8) & 0xff, k = v[t].y, j = v[t].z;
+    const int nk = std::max(1, v[t].x >> 16);
     const int i0 = v[t].w & 0xffff, i1 = v[t].w >> 16;
     auto& d = deps[t];
     const int rows = i1 - i0;
@@ -881,12 +1013,20 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
       for (int i = i0; i < i1; ++i) d.push_back(verA(i, k, k));
       dur[t] = 1.0 + 3.6 * rows;
     } else if (type == T_COLUPD) {
-      d.push_back(prodL[tix(j, k)]);
+      d.push_back(prodL[tix(j, k + nk - 1)]);
       for (int i = i0; i < i1; ++i) {
-        d.push_back(prodL[tix(i, k)]);
+        d.push_back(prodL[tix(i, k + nk - 1)]);
         d.push_back(verA(i, j, k));
       }
-      dur[t] = 2.0 + 3.6 * rows;
+      dur[t] = 2.0 + (nk > 1 ? 2.6 * nk + 1.0 : 3.6) * rows;
+    } else if (nk > 1) {
+      const int kl = k + nk - 1;
+      d.push_back(kl == j ? prodL[tix(j, j)] : prodXd[tix(kl, j)]);
+      for (int i = i0; i < i1; ++i) {
+        d.push_back(prodL[tix(i, kl)]);
+        d.push_back(verX(i, j, k - j));
+      }
+      dur[t] = 2.0 + (2.6 * nk + 1.0) * rows;
     } else {
       if (k == j) d.push_back(prodL[tix(k, k)]);
       else if (fin) { d.push_back(verX(k, j, k - j)); d.push_back(prodL[tix(k, k)]); }
@@ -927,12 +1067,39 @@ std::vector<int4> build_tasks(int T) {
       v.push_back(make_int4(T_COLUPD, k, k + 2, (k + 2) | (c1 << 16)));
       crit(k + 2);
     }
-    for (int j = 0; j <= k; ++j) push_rows(v, T_XSTEP, k, j, k + 1, T, true);
+    // column j of X at step k: the near rows (k, ke) of the aligned batch
+    // [kb, ke) one step at a time (X_kj's finalisation rides on the first
+    // chunk, or is a task of its own); at the batch's last step, one batched
+    // update of the far rows [ke, T) over all its steps
+    for (int j = 0; j <= k; ++j) {
+      const int kb = j + ((k - j) / GB) * GB, ke = std::min(kb + GB, T);
+      if (k + 1 < ke) push_rows(v, T_XSTEP, k, j, k + 1, ke, true);
+      else if (k > j) v.push_back(make_int4(T_XSTEP | 256, k, j, 0));
+      if (k == ke - 1 && ke < T) {
+        const size_t first = v.size();
+        push_rows(v, T_XSTEP, kb, j, ke, T, false, CHB);
+        for (size_t t = first; t < v.size(); ++t) v[t].x |= (ke - kb) << 16;
+      }
+    }
     if (k + 2 < T) {
       push_rows(v, T_COLUPD, k, k + 1, c1, T, false);
       push_rows(v, T_COLUPD, k, k + 2, c1, T, false);
     }
-    for (int j = k + 3; j < T; ++j) push_rows(v, T_COLUPD, k, j, j, T, false);
+    // columns j >= k + 3 at step k: the steps of an aligned batch [kb, kb + GB)
+    // that lies wholly at or below j - 3 go in one batched task at the batch's
+    // last step (A_ij loaded / stored once per batch); the rest one per step
+    for (int j = k + 3; j < T; ++j) {
+      const int kb = (k / GB) * GB;
+      if (GB > 1 && kb + GB - 1 <= j - 3) {
+        if (k == kb + GB - 1) {
+          const size_t first = v.size();
+          push_rows(v, T_COLUPD, kb, j, j, T, false, CHB);
+          for (size_t t = first; t < v.size(); ++t) v[t].x |= GB << 16;
+        }
+      } else {
+        push_rows(v, T_COLUPD, k, j, j, T, false);
+      }
+    }
   }
   for (int j = 0; j + 1 < T; ++j) v.push_back(make_int4(T_XSTEP | 256, T - 1, j, 0));
   return priority_order(v, T);
@@ -1011,7 +1178,7 @@ extern "C" int bo_probe_diag16(long long* out, double* sink, void* stream) {
 }
 
 // The queue of the task DAG for T tile rows (host only, no device call): out
-// receives 4 ints per task (type | fin << 8, k, j, i0 | i1 << 16) in queue
+// receives 4 ints per task (type | fin << 8 | nk << 16, k, j, i0 | i1 << 16) in queue
 // order, up to cap tasks; returns the task count (tests/test_chol_dag_cpu.py
 // checks that every dependency precedes its task).
 extern "C" int bo_chol_dag_tasks(int T, int* out, int cap) {

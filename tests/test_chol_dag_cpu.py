@@ -18,8 +18,8 @@ def _queue(T):
     m = lib().bo_chol_dag_tasks(T, buf.ctypes.data_as(ctypes.c_void_p), n)
     assert m == n
     q = buf.reshape(n, 4)
-    return [(int(x) & 0xFF, int(x) >> 8, int(k), int(j), int(w) & 0xFFFF, int(w) >> 16)
-            for x, k, j, w in q]
+    return [(int(x) & 0xFF, (int(x) >> 8) & 0xFF, int(k), int(j), int(w) & 0xFFFF, int(w) >> 16,
+             max(1, int(x) >> 16)) for x, k, j, w in q]
 
 
 @pytest.mark.parametrize("T", [1, 2, 3, 5, 16, 64])
@@ -29,7 +29,7 @@ def test_queue_is_topological_and_complete(T):
     A = {}                    # (i, j) -> updates applied
     X = {}                    # (i, j) -> updates applied to X's accumulator
     Xd = set()                # finalised X tiles (k > j)
-    for type_, fin, k, j, i0, i1 in q:
+    for type_, fin, k, j, i0, i1, nk in q:
         if type_ == T_CRIT:
             if k > 0:
                 assert A.get((k, k - 1), 0) >= k - 1 and (k - 1, k - 1) in L
@@ -42,11 +42,17 @@ def test_queue_is_topological_and_complete(T):
             for i in range(i0, i1):
                 assert A.get((i, k), 0) >= k and (i, k) not in L
                 L.add((i, k))
-        elif type_ == T_COLUPD:
-            assert (j, k) in L
+        elif type_ == T_COLUPD:  # steps k .. k + nk - 1 (nk > 1: a batched update)
+            assert all((j, kk) in L for kk in range(k, k + nk))
             for i in range(i0, i1):
-                assert (i, k) in L and A.get((i, j), 0) == k
-                A[(i, j)] = k + 1
+                assert all((i, kk) in L for kk in range(k, k + nk)) and A.get((i, j), 0) == k
+                A[(i, j)] = k + nk
+        elif nk > 1:  # XSTEP, batched: steps k .. k + nk - 1 on far rows
+            assert all((kk, j) in Xd or (kk == j and (j, j) in L) for kk in range(k, k + nk))
+            for i in range(i0, i1):
+                assert i >= k + nk
+                assert all((i, kk) in L for kk in range(k, k + nk)) and X.get((i, j), 0) == k - j
+                X[(i, j)] = k + nk - j
         else:
             if k == j:
                 assert (k, k) in L
