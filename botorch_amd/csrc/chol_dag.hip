@@ -827,24 +827,29 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
     bool ok = true;
     if (type == T_CRIT) {
       if (k > 0) {
-        ok = wait2(c, F(fA, k, k - 1), (u32)(k - 1), F(fL, k - 1, k - 1), 1u, abortw, &s_ok, &wsum);
+        // the bulk's inputs (A_{k,k-1}, A_kk at version k-1) are usually ready
+        // before D_{k-1}: load them while the previous diagonal step runs, so
+        // only D_{k-1}'s load, two tile products and the L_{k,k-1} hand-off
+        // stay on the chain
+        Acc akk;
+        ok = wait2(c, F(fA, k, k - 1), (u32)(k - 1), F(fA, k, k), (u32)(k - 1), abortw, &s_ok, &wsum);
         if (ok) {
           tile_to_lds(c, c.rA, k, k - 1, X0);
+          acc_load(c, akk, c.rA, k, k);
+          ok = wait2(c, F(fL, k - 1, k - 1), 1u, F(fL, k - 1, k - 1), 1u, abortw, &s_ok, &wsum);
+        }
+        if (ok) {
           tile_to_lds(c, c.rI, k - 1, k - 1, X1);
           __syncthreads();
           acc_zero(acc);
           acc_mma_nt(c, acc, X0, X1, 1.0);  // L_{k,k-1} = A_{k,k-1} D_{k-1}^T
           __syncthreads();                  // every wave's reads of X0 done
           acc_to_lds(c, acc, X0);
-          acc_store(c, acc, c.rA, k, k - 1);
-          publish(c, F(fL, k, k - 1), 1u);
-          ok = wait2(c, F(fA, k, k), (u32)(k - 1), F(fA, k, k), (u32)(k - 1), abortw, &s_ok, &wsum);
-        }
-        if (ok) {
-          acc_load(c, acc, c.rA, k, k);
-          acc_mma_nt(c, acc, X0, X0, -1.0);  // A_kk -= L L^T (step k - 1)
-          __syncthreads();
-          acc_to_lds(c, acc, X0);
+          acc_store(c, acc, c.rA, k, k - 1);  // in flight under the update below
+          __syncthreads();                    // X0 = L_{k,k-1} complete
+          acc_mma_nt(c, akk, X0, X0, -1.0);   // A_kk -= L L^T (step k - 1)
+          publish(c, F(fL, k, k - 1), 1u);    // (its barrier also frees X0)
+          acc_to_lds(c, akk, X0);
         }
       } else {
         tile_to_lds(c, c.rA, 0, 0, X0);

@@ -90,6 +90,27 @@ def main():
                                           "store_publish": float(ph[sel, 2].sum()) / 100.0 / tiles,
                                           "prefetched_frac": float(ph[sel, 4].sum()) / tiles,
                                           "tiles": tiles}
+    # the tasks that touch the last tile row after the second-to-last CRIT
+    # (what the final diagonal step waited on)
+    import numpy as np
+    nq = lib().bo_chol_dag_tasks(np_ // 64, None, 0)
+    qb = np.zeros(4 * nq, dtype=np.int32)
+    lib().bo_chol_dag_tasks(np_ // 64, qb.ctypes.data_as(ctypes.c_void_p), nq)
+    qb = qb.reshape(nq, 4)
+    T = np_ // 64
+    crit_end = {int(k[i]): int(en[i]) for i in crit.tolist()}
+    t62 = crit_end.get(T - 2, int(en.max()))
+    tail = []
+    for t in range(ntask):
+        x, kk, jj, w = (int(v) for v in qb[t])
+        i0, i1 = w & 0xFFFF, w >> 16
+        if int(en[t]) > t62 - 3000 and (i1 > T - 1 or (x & 0xFF) == 0):
+            tail.append([TYPES[x & 0xFF], kk, jj, i0, i1, max(1, x >> 16), (x >> 8) & 0xFF,
+                         round((int(st[t]) - t0) / 100.0, 1), round((int(en[t]) - t0) / 100.0, 1),
+                         int(blk[t])])
+    tail.sort(key=lambda r: r[7])
+    out["tail_tasks_type_k_j_i0_i1_nk_fin_start_end_block"] = [r for r in tail if r[0] != "XSTEP"] + \
+        [r for r in tail if r[0] == "XSTEP"][-8:]
     # the last finishing tasks
     last = torch.argsort(en, descending=True)[:8]
     out["last_tasks"] = [[TYPES[int(typ[i])], int(k[i]), int(j[i]), round((int(st[i]) - t0) / 100.0, 1),
