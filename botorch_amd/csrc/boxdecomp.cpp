@@ -182,7 +182,7 @@ Cells partition(const double* Y, int64_t n, int m, const double* ref) {
 extern "C" int bo_nd_partition_host(const double* Y, int64_t S, int64_t n, int m,
                                     const double* ref, int64_t K_cap, int64_t* K_out,
                                     double* cell_lo, double* cell_hi, int nthreads) {
-  if (S < 0 || n < 0 || m < 2 || !Y || !ref || !K_out) {
+  if (S < 0 || n < 0 || m < 2 || (!Y && S * n > 0) || !ref || !K_out) {
     bo_set_error("bo_nd_partition_host: bad arguments (S %lld, n %lld, m %d)", (long long)S,
                  (long long)n, m);
     return BO_ERR_ARG;
