@@ -293,6 +293,12 @@ class SingleTaskGP(Model):
     def prediction_cache(self):
         """Device caches of [G] exact prediction; rebuilt on any change."""
         from . import kernels
+        from .settings import propagate_grads
+        if propagate_grads.on() and (self.train_inputs[0].requires_grad or self.train_targets.requires_grad):
+            from .exceptions import UnsupportedError
+            raise UnsupportedError(
+                "settings.propagate_grads: posterior gradients to the training data are not "
+                "supported (the prediction caches are built without a backward to them)")
         key = self._key()
         if self._cache is None or self._cache_key != key:
             from . import ops  # noqa: F401  (torch.ops.bo registration)

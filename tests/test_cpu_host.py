@@ -154,3 +154,23 @@ def test_arg_records_match_c_layout():
     a = _lib.LbfgsStepArgs(B=1, n=1, m=1)
     a.struct_size = 8
     assert lib.bo_lbfgs_step_v(ctypes.byref(a), None) != 0
+
+
+def test_settings_flags_mirror_reference():
+    """settings.py:16-77 switch semantics; propagate_grads with training data
+    that require grad raises (no silent detach) before any device work."""
+    from botorch_amd import settings
+    from botorch_amd.exceptions import UnsupportedError
+    from botorch_amd.models import SingleTaskGP
+    assert settings.propagate_grads.off() and settings.validate_input_scaling.on()
+    with settings.propagate_grads(True):
+        assert settings.propagate_grads.on()
+        with settings.propagate_grads(False):
+            assert settings.propagate_grads.off()
+        assert settings.propagate_grads.on()
+    assert settings.propagate_grads.off()
+    X = torch.rand(8, 2, dtype=torch.float64, requires_grad=True)
+    m = SingleTaskGP(X, torch.rand(8, 1, dtype=torch.float64)).eval()
+    with settings.propagate_grads(True):
+        with pytest.raises(UnsupportedError):
+            m.prediction_cache()
