@@ -58,6 +58,10 @@ typedef unsigned int u32;
 typedef u32 v2u __attribute__((ext_vector_type(2)));
 typedef u32 v4u __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+// the diagonal block's column counter: an explicit LDS pointer, so polls and
+// updates are ds_read / ds_write (a generic volatile pointer becomes a flat
+// access with a full vmcnt drain per column)
+typedef volatile __attribute__((address_space(3))) int lds_cnt_t;
 
 constexpr int SC1 = 16;  // cache-policy bit: write-through store / L1-bypassing load
 
@@ -318,24 +322,57 @@ __device__ __forceinline__ void col_updates(std::integer_sequence<int, M...>, do
   (col_update<JJ, M>(v, l), ...);
 }
 
-// Column JJ of the 16 x 16 diagonal-block factorisation AND inverse (one wave;
-// lane = (group g, row r), every group holds the whole block in v[16] and
-// inverse columns 4 g .. 4 g + 3 in x[4]): pivot broadcast inside the 16-lane
-// row (DPP), the next pivot's column updated first; the inverse's forward
-// substitution step JJ uses the fresh column l = L[., JJ] and 1 / L_JJ,JJ
-// straight from registers -- two independent dependency chains in one
-// instruction stream instead of a second wave one column behind behind an
-// LDS counter (whose poll / read round trips set the pace).
+template <int JJ, int M>
+__device__ __forceinline__ void col_update_lds(double (&v)[16], double l, const double* Lj) {
+  if constexpr (M > JJ + 1) v[M] = fma(-l, Lj[M], v[M]);
+}
+template <int JJ, int... M>
+__device__ __forceinline__ void col_updates_lds(std::integer_sequence<int, M...>, double (&v)[16],
+                                                double l, const double* Lj) {
+  (col_update_lds<JJ, M>(v, l, Lj), ...);
+}
+
+// Column JJ of the 16 x 16 diagonal-block factorisation (wave 0; lane = (group
+// g, row r), every group holds the whole block): pivot broadcast inside the
+// 16-lane row (DPP).  Group 0 publishes the column L[., JJ] and 1 / L_JJ,JJ to
+// LDS, then the column counter, for the inverse built concurrently on wave 1
+// (diag_inv_step).  The next pivot's column takes its factor through DPP (the
+// chain); the other columns read L[M, JJ] back from that LDS copy -- one
+// uniform-address read per value instead of two DPP moves: the step is bound
+// by the wave's instruction issue, not by the chain.
 template <int JJ>
-__device__ __forceinline__ void diag_step(double (&v)[16], double (&x)[4], int r, bool lane0,
-                                          int& fail, double* rinv) {
+__device__ __forceinline__ void diag_step(double (&v)[16], int r, int g, bool lane0, int& fail,
+                                          double* rinv, double* Lc, lds_cnt_t* cnt, int cbase) {
   const double piv = row_bcast<JJ>(v[JJ]);
   if (!(piv > 0.0) && fail == 0) fail = JJ + 1;
   const double rr = rsq_nr(piv);
   const double l = (r >= JJ) ? v[JJ] * rr : 0.0;  // L_{r,JJ} (r == JJ: sqrt(piv))
   v[JJ] = l;
-  if (lane0) rinv[JJ] = rr;
-  col_updates<JJ>(std::make_integer_sequence<int, 16>{}, v, l);  // next pivot's column first
+  if (g == 0) Lc[JJ * 16 + r] = l;
+  if (lane0) {
+    rinv[JJ] = rr;
+    *cnt = cbase + JJ + 1;  // LDS writes of one wave land in order
+  }
+  if constexpr (JJ + 1 < 16) v[JJ + 1] = fma(-l, row_bcast<JJ + 1>(l), v[JJ + 1]);
+  col_updates_lds<JJ>(std::make_integer_sequence<int, 16>{}, v, l, Lc + JJ * 16);
+}
+
+template <int... JJ>
+__device__ __forceinline__ void diag_steps(std::integer_sequence<int, JJ...>, double (&v)[16],
+                                           int r, int g, bool lane0, int& fail, double* rinv,
+                                           double* Lc, lds_cnt_t* cnt, int cbase) {
+  (diag_step<JJ>(v, r, g, lane0, fail, rinv, Lc, cnt, cbase), ...);
+}
+
+// Column JJ of the inverse of the diagonal block (wave 1, one column behind wave
+// 0): group g owns inverse columns 4 g .. 4 g + 3; row JJ is scaled by 1 / L_JJ,JJ
+// and eliminated from the rows below (forward substitution).
+template <int JJ>
+__device__ __forceinline__ void diag_inv_step(double (&x)[4], int r, const double* rinv,
+                                              const double* Lc, lds_cnt_t* cnt, int cbase) {
+  while (*cnt < cbase + JJ + 1) __builtin_amdgcn_s_sleep(0);
+  const double rr = rinv[JJ];
+  const double l = Lc[JJ * 16 + r];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const double xs = (r == JJ) ? x[q] * rr : x[q];
@@ -345,10 +382,10 @@ __device__ __forceinline__ void diag_step(double (&v)[16], double (&x)[4], int r
 }
 
 template <int... JJ>
-__device__ __forceinline__ void diag_steps(std::integer_sequence<int, JJ...>, double (&v)[16],
-                                           double (&x)[4], int r, bool lane0, int& fail,
-                                           double* rinv) {
-  (diag_step<JJ>(v, x, r, lane0, fail, rinv), ...);
+__device__ __forceinline__ void diag_inv_steps(std::integer_sequence<int, JJ...>, double (&x)[4],
+                                               int r, const double* rinv, const double* Lc,
+                                               lds_cnt_t* cnt, int cbase) {
+  (diag_inv_step<JJ>(x, r, rinv, Lc, cnt, cbase), ...);
 }
 
 // ---- timing probe of the 16 x 16 diagonal step (tools/probe_diag16.py) ----------
@@ -438,31 +475,39 @@ __device__ __forceinline__ void put16(double* D, v4d a, int lane, double scale) 
 // inverses by recursive doubling, X21 = -X22 L21 X11 (16 -> 32 -> 64), on the
 // MFMA; the strictly-upper blocks of S serve as scratch for the products.
 __device__ void potrf_trtri64(const Ctx& c, double* S, double* D, double* rinv, int* info, int row0,
-                              long long* ct = nullptr) {
+                              double* Lc, lds_cnt_t* cnt, long long* ct = nullptr) {
   for (int e = c.tid; e < TB * TB; e += 256) D[(e >> 6) * LP + (e & 63)] = 0.0;
   __syncthreads();
   const int r = c.lane & 15, g = c.lane >> 4;
-  // diagonal block p (rows/cols 16 p ..): wave 0 factors it in place and
+  if (c.tid == 0) *cnt = 0;
+  // diagonal block p (rows/cols 16 p ..): wave 0 factors it in place, wave 1
   // builds its inverse into D
   auto diag_block = [&](int p) {
     const int c0 = 16 * p;
     double* T = S + c0 * LP + c0;
-    double v[16], x[4];
+    if (c.wave == 0) {
+      double v[16];
 #pragma unroll
-    for (int m = 0; m < 16; ++m) v[m] = T[r * LP + m];
+      for (int m = 0; m < 16; ++m) v[m] = T[r * LP + m];
+      int fail = 0;  // first non-positive pivot of the block (1-based), uniform
+      diag_steps(std::make_integer_sequence<int, 16>{}, v, r, g, c.lane == 0, fail, rinv + c0,
+                 Lc + 256 * (p & 1), cnt, 16 * p);
+      if (fail && c.lane == 0) atomicCAS(info, 0, row0 + c0 + fail);
+      if (g == 0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) x[q] = (r == 4 * g + q) ? 1.0 : 0.0;
-    int fail = 0;  // first non-positive pivot of the block (1-based), uniform
-    diag_steps(std::make_integer_sequence<int, 16>{}, v, x, r, c.lane == 0, fail, rinv + c0);
-    if (fail && c.lane == 0) atomicCAS(info, 0, row0 + c0 + fail);
-    if (g == 0) {
+        for (int m = 0; m < 16; ++m) T[r * LP + m] = (m <= r) ? v[m] : 0.0;
+      }
+    } else {  // wave 1
+      double x[4];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) T[r * LP + m] = (m <= r) ? v[m] : 0.0;
+      for (int q = 0; q < 4; ++q) x[q] = (r == 4 * g + q) ? 1.0 : 0.0;
+      diag_inv_steps(std::make_integer_sequence<int, 16>{}, x, r, rinv + c0, Lc + 256 * (p & 1), cnt,
+                     16 * p);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) D[(c0 + r) * LP + c0 + 4 * g + q] = x[q];
     }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) D[(c0 + r) * LP + c0 + 4 * g + q] = x[q];
   };
-  if (c.wave == 0) diag_block(0);
+  if (c.wave < 2) diag_block(0);
   __syncthreads();
   if (ct && c.tid == 0) ct[4] = wall_clock64();
 #pragma unroll 1
@@ -476,7 +521,8 @@ __device__ void potrf_trtri64(const Ctx& c, double* S, double* D, double* rinv, 
     }
     __syncthreads();
     // trailing update: tiles (ib, jb), p < jb <= ib; wave 0 takes (p+1, p+1)
-    // and factors + inverts it right away, waves 1-3 update the rest
+    // and factors it right away while wave 1 inverts it, waves 2, 3 update the
+    // rest
     const int nt = 3 - p;
     const int ntile = nt * (nt + 1) / 2;
     if (c.wave == 0) {
@@ -486,8 +532,10 @@ __device__ void potrf_trtri64(const Ctx& c, double* S, double* D, double* rinv, 
 #pragma unroll
       for (int q = 0; q < 4; ++q) T[mfma_row(c.lane, q) * LP + mfma_col(c.lane)] -= a[q];
       diag_block(p + 1);
+    } else if (c.wave == 1) {
+      diag_block(p + 1);
     } else {
-      for (int t = c.wave; t < ntile; t += 3) {  // tiles 1.. (tile 0 = (p+1, p+1))
+      for (int t = c.wave - 1; t < ntile; t += 2) {  // tiles 1.. (tile 0 = (p+1, p+1))
         int tr = 0;
         while ((tr + 1) * (tr + 2) / 2 <= t) ++tr;
         const int tc = t - tr * (tr + 1) / 2;
@@ -787,6 +835,8 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
   __shared__ __attribute__((aligned(16))) double X2[TB * LP];  // batched update operands
   __shared__ __attribute__((aligned(16))) double X3[TB * LP];
   __shared__ double rinv[TB];
+  __shared__ double Lcol[512];  // diagonal-block columns, double-buffered by block parity
+  __shared__ int s_cnt;
   __shared__ int s_ok;
   __shared__ int s_rdy[2];
   __shared__ int s_task;
@@ -858,7 +908,7 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
         __syncthreads();
         long long* ct = trace ? trace + 4 * ntasks + 8 * k : nullptr;
         if (ct && c.tid == 0) ct[0] = wall_clock64();
-        potrf_trtri64(c, X0, X1, rinv, info, k * TB, ct);
+        potrf_trtri64(c, X0, X1, rinv, info, k * TB, Lcol, (lds_cnt_t*)&s_cnt, ct);
         if (ct && c.tid == 0) ct[1] = wall_clock64();
         if (ct && c.tid == 0) ct[2] = wall_clock64();
         lds_to_tile(c, X0, c.rA, k, k);
