@@ -514,12 +514,21 @@ def main():
     args = ap.parse_args()
 
     ws, rank, local = _dist_env()
+    # BO_BENCH_REHEARSE=1: every rank on cuda:0 over gloo -- a one-GPU rehearsal
+    # of the multi-rank code path (barriers, max over ranks, rank-0 report);
+    # never the measured configuration
+    rehearse = os.environ.get("BO_BENCH_REHEARSE", "0") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if ws > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from botorch_amd import kernels
     from botorch_amd.acquisition import qExpectedImprovement
