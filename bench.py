@@ -455,6 +455,48 @@ def other_configs(dev, cpu=True):
     return out
 
 
+def time_cholesky(Xtr, dev, reps=10):
+    """Standalone n x n Cholesky + triangular inverse (bo_cholesky_inverse, the
+    persistent task DAG) on the C3 kernel matrix ("standalone
+    n x n Cholesky ms and MFMA %"): HIP events on the launch stream around the
+    launch alone (the input copy excluded), median of ``reps``; flops n^3/3
+    (factor) + n^3/3 (inverse)."""
+    import ctypes
+    from botorch_amd import kernels
+    from botorch_amd._lib import check, lib
+    X = Xtr.to(dev) / LENGTHSCALE
+    n = X.shape[0]
+    # the RBF kernel matrix of the C3 training set (plain torch input preparation)
+    A0 = torch.exp(-0.5 * torch.cdist(X, X) ** 2) + NOISE * torch.eye(n, dtype=torch.float64, device=dev)
+    np_ = kernels.padded_order(n)
+    base = torch.eye(np_, dtype=torch.float64, device=dev)
+    base[:n, :n] = torch.tril(A0)
+    W = torch.empty_like(base)
+    Linv = torch.empty_like(base)
+    work = torch.empty_like(base)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream(dev)
+    ts = []
+    for r in range(reps + 2):
+        W.copy_(base)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        check(lib().bo_cholesky_inverse(kernels._p(W), kernels._p(Linv), kernels._p(work), np_,
+                                        kernels._p(info), ctypes.c_void_p(st.cuda_stream)), "chol")
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        if r >= 2:
+            ts.append(e0.elapsed_time(e1))
+    if int(info.item()) != 0:
+        raise RuntimeError(f"bench Cholesky: info {int(info.item())}")
+    ts.sort()
+    ms = ts[len(ts) // 2]
+    fl = 2.0 * n ** 3 / 3.0
+    return {"n": n, "ms": ms, "flops": fl, "tflops": fl / (ms * 1e-3) / 1e12,
+            "frac_of_spec": fl / (ms * 1e-3) / 1e12 / 78.6,
+            "note": "factor + inverse, one persistent task-DAG launch, input in HBM"}
+
+
 def time_gp_fit(Xtr, Ytr, dev, cpu=True):
     """GP-fit half of the metric: fit_gpytorch_mll (L-BFGS-B, exact MLL + gradient on
     the device) from BoTorch's default initialisation, n=4096, d=6.  CPU side: one
@@ -636,6 +678,7 @@ def main():
                                     "projected_value": Q * RESTARTS * MC / tW}
     gp_fit = None
     extra = None
+    chol = time_cholesky(Xtr, dev) if rank == 0 else None
     if rank == 0 and ws == 1 and not args.no_extra:
         extra = other_configs(dev, cpu=not args.no_cpu_baseline)
     if rank == 0 and not args.no_fit:
@@ -674,6 +717,7 @@ def main():
             "cpu_baseline": cpu,
             "fwd_bwd": fwd_bwd,
             "strong_scaling_projection": strong_proj,
+            "cholesky": chol,
             "gp_fit": gp_fit,
             "other_configs": extra,
         }
