@@ -670,12 +670,18 @@ def main():
         # the per-rank shard of the strong split, timed on this GPU (projection)
         strong_proj = {"note": "projection: the C3 qEI step at b = 512/W restarts on one GPU, "
                                "collectives excluded; value = 512*q*S / step time"}
+        from botorch_amd.graphs import GraphedAcquisition
         for W in (1, 2, 4, 8):
             Xs = Xd[: RESTARTS // W]
             with torch.no_grad():
                 tW = _gpu_time(lambda: acqf(Xs), steps=10, warmup=2)
+            gW = GraphedAcquisition(acqf, Xs)  # the same forward replayed as a HIP graph
+            tG = _gpu_time(lambda: gW(Xs), steps=10, warmup=2)
             strong_proj[f"W{W}"] = {"restarts_per_gpu": RESTARTS // W, "ms": 1e3 * tW,
-                                    "projected_value": Q * RESTARTS * MC / tW}
+                                    "projected_value": Q * RESTARTS * MC / tW,
+                                    "ms_graphed": 1e3 * tG,
+                                    "projected_value_graphed": Q * RESTARTS * MC / tG}
+            del gW
     gp_fit = None
     extra = None
     chol = time_cholesky(Xtr, dev) if rank == 0 else None
