@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import collections
 import ctypes
+import functools
 import math
 import os
 from dataclasses import dataclass
@@ -58,7 +59,11 @@ def _p(t: Optional[torch.Tensor]):
 
 
 def _stream(device: torch.device):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """The caller's current HIP stream on ``device`` (raw handle; the same
+    stream torch.cuda.current_stream(device) wraps, without building the
+    Python stream object on every launch)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(idx))
 
 
 def _dev(*tensors: torch.Tensor) -> torch.device:
@@ -223,6 +228,7 @@ class PostPartials:
     Cx: Optional[torch.Tensor] = None  # cross K*x^T (rq x nrows_pad), fused cross term
 
 
+@functools.lru_cache(maxsize=256)
 def geometry(B: int, q: int, n: int):
     Qp, nrows, nC = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     check(lib().bo_post_geometry(B, q, n, ctypes.byref(Qp), ctypes.byref(nrows),
@@ -242,6 +248,7 @@ def ainv(cache: "GPCache") -> torch.Tensor:
     return out
 
 
+@functools.lru_cache(maxsize=256)
 def split_plan(B: int, q: int, n: int, slots: int = 0):
     """(kc_len, workspace doubles) of the posterior plan; kc_len = 0: one pass,
     -1: stream-K."""
@@ -577,14 +584,17 @@ def raise_not_psd_deferred(info: torch.Tensor, jitter: torch.Tensor, what: str) 
     dev = info.device
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     check_ladder_status(dev)  # the previous call's status (one forward behind)
-    packed = torch.empty(2, dtype=torch.float64, device=dev)
+    # one device word pair, one pinned pair and one event per device, reused:
+    # call t's status is read (after its event) before call t+1 writes them
+    bufs = _LADDER_PINNED.get(idx)
+    if bufs is None:
+        bufs = _LADDER_PINNED[idx] = (torch.empty(2, dtype=torch.float64, device=dev),
+                                      torch.empty(2, dtype=torch.float64, pin_memory=True),
+                                      torch.cuda.Event())
+    packed, pinned, ev = bufs
     check(lib().bo_ladder_status(_p(info.contiguous()), _p(jitter.contiguous()), info.numel(),
                                  _p(packed), _stream(dev)), "ladder_status")
-    pinned = _LADDER_PINNED.get(idx)
-    if pinned is None:
-        pinned = _LADDER_PINNED[idx] = torch.empty(2, dtype=torch.float64, pin_memory=True)
     pinned.copy_(packed, non_blocking=True)
-    ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
     _LADDER_PENDING[idx] = (pinned, ev, what)
 
