@@ -53,6 +53,9 @@ _SIGNATURES = {
     "bo_gp_cache_build": (c_int, [c_int, _P, c_int64, c_int, _P, c_double, c_double, c_double,
                                   _P, _P, _P, _P, _P, _P, c_int, c_double, POINTER(c_double),
                                   _P, _P]),
+    "bo_gp_cache_build_fixed": (c_int, [c_int, _P, c_int64, c_int, _P, c_double, _P, c_double,
+                                        _P, _P, _P, _P, _P, _P, c_int, c_double,
+                                        POINTER(c_double), _P, _P]),
     "bo_post_geometry": (c_int, [c_int64, c_int, c_int64, POINTER(c_int), POINTER(c_int),
                                  POINTER(c_int)]),
     "bo_prepare_rows": (c_int, [_P, c_int, c_int, c_int, _P, _P, _P]),

@@ -166,6 +166,14 @@ __global__ void scale_inputs_kernel(const double* __restrict__ X, int64_t n, int
   Xs[idx] = (t < d) ? (X[i * d + t] - (center ? center[t] : 0.0)) / ls[t] : 0.0;
 }
 
+// A[i][i] += v[i], i < n: the observed noise variances of a fixed-noise
+// likelihood on the kernel matrix's diagonal.
+__global__ void add_diag_kernel(double* __restrict__ A, int64_t ld, int64_t n,
+                                const double* __restrict__ v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) A[i * ld + i] += v[i];
+}
+
 }  // namespace
 
 // Look-ahead stream of the blocked Cholesky (one per device, created on first
@@ -398,11 +406,16 @@ int bo_scale_inputs(const double* X, int64_t n, int d, const double* lengthscale
   return BO_OK;
 }
 
-int bo_gp_cache_build(int kind, const double* Xt, int64_t n, int d, const double* lengthscale,
-                      double outputscale, double noise, double constant, const double* y,
-                      double* L, double* Linv, double* U, double* beta, double* alpha,
-                      int max_tries, double jitter0, double* jitter_used, int* info_dev,
-                      void* stream) {
+}  // extern "C"
+
+// Shared body of bo_gp_cache_build (homoskedastic noise) and
+// bo_gp_cache_build_fixed (noise_vec: one observed variance per point).
+static int gp_cache_build_impl(int kind, const double* Xt, int64_t n, int d,
+                               const double* lengthscale, double outputscale, double noise,
+                               const double* noise_vec, double constant, const double* y,
+                               double* L, double* Linv, double* U, double* beta, double* alpha,
+                               int max_tries, double jitter0, double* jitter_used, int* info_dev,
+                               void* stream) {
   BO_CHECK_ARG(n > 0 && d > 0, "bo_gp_cache_build: empty training set");
   hipStream_t st = as_stream(stream);
   const int64_t np = bo_padded_order(n);
@@ -413,6 +426,10 @@ int bo_gp_cache_build(int kind, const double* Xt, int64_t n, int d, const double
     int s = bo_covar_matrix(kind, Xt, n, Xt, n, d, lengthscale, outputscale, noise + jitter, 1,
                             L, np, np, np, stream);
     if (s) return s;
+    if (noise_vec) {
+      add_diag_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(L, np, n, noise_vec);
+      BO_LAUNCH_CHECK();
+    }
     s = bo_cholesky_inverse(L, Linv, U, np, info_dev, stream);
     if (s) return s;
     BO_HIP(hipMemcpyAsync(&info_h, info_dev, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -434,6 +451,29 @@ int bo_gp_cache_build(int kind, const double* Xt, int64_t n, int d, const double
   s = bo_gemv(Linv, np, n, y, constant, beta, stream);  // beta = L^{-1} (y - c)
   if (s) return s;
   return bo_gemv(U, np, n, beta, 0.0, alpha, stream);   // alpha = L^{-T} beta
+}
+
+extern "C" {
+
+int bo_gp_cache_build(int kind, const double* Xt, int64_t n, int d, const double* lengthscale,
+                      double outputscale, double noise, double constant, const double* y,
+                      double* L, double* Linv, double* U, double* beta, double* alpha,
+                      int max_tries, double jitter0, double* jitter_used, int* info_dev,
+                      void* stream) {
+  return gp_cache_build_impl(kind, Xt, n, d, lengthscale, outputscale, noise, nullptr, constant,
+                             y, L, Linv, U, beta, alpha, max_tries, jitter0, jitter_used,
+                             info_dev, stream);
+}
+
+int bo_gp_cache_build_fixed(int kind, const double* Xt, int64_t n, int d,
+                            const double* lengthscale, double outputscale,
+                            const double* noise_vec, double constant, const double* y, double* L,
+                            double* Linv, double* U, double* beta, double* alpha, int max_tries,
+                            double jitter0, double* jitter_used, int* info_dev, void* stream) {
+  BO_CHECK_ARG(noise_vec != nullptr, "bo_gp_cache_build_fixed: noise_vec is NULL");
+  return gp_cache_build_impl(kind, Xt, n, d, lengthscale, outputscale, 0.0, noise_vec, constant,
+                             y, L, Linv, U, beta, alpha, max_tries, jitter0, jitter_used,
+                             info_dev, stream);
 }
 
 }  // extern "C"

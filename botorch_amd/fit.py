@@ -25,7 +25,7 @@ from scipy.optimize import minimize
 from . import _lib, kernels
 from ._lib import check, lib
 from .exceptions import NotPSDError, OptimizationWarning
-from .models import LogNormalPrior, ScaleKernel, SingleTaskGP
+from .models import FixedNoiseGaussianLikelihood, LogNormalPrior, ScaleKernel, SingleTaskGP
 
 
 class ExactMarginalLogLikelihood:
@@ -60,41 +60,108 @@ def _prior_terms(prior: Optional[LogNormalPrior], x: np.ndarray):
 
 class _Layout:
     """Flat parameter vector <-> model hyperparameters (order of
-    get_parameters_and_bounds: noise, constant, lengthscales[, outputscale])."""
+    get_parameters_and_bounds: noise, constant, lengthscales[, outputscale];
+    a fixed-noise likelihood has no noise entry)."""
 
     def __init__(self, model: SingleTaskGP):
         self.model = model
         self.d = model.train_inputs[0].shape[-1]
+        self.fixed = isinstance(model.likelihood, FixedNoiseGaussianLikelihood)
+        self.o = 0 if self.fixed else 1  # offset of the constant
         self.has_os = isinstance(model.covar_module, ScaleKernel)
         base = model.covar_module.base_kernel if self.has_os else model.covar_module
         self.base = base
-        lo = [model.likelihood.noise_lower, -np.inf] + [base.lengthscale_lower] * self.d
+        lo = ([] if self.fixed else [model.likelihood.noise_lower]) + [-np.inf]
+        lo += [base.lengthscale_lower] * self.d
         if self.has_os:
             lo.append(0.0)
         self.bounds = [(None if not np.isfinite(l) else l, None) for l in lo]
+        # (name, start, size) segments, the order above
+        self.segments = ([] if self.fixed else [("noise", 0, 1)]) + [
+            ("constant", self.o, 1), ("lengthscale", self.o + 1, self.d)] + (
+            [("outputscale", self.o + 1 + self.d, 1)] if self.has_os else [])
+        self.size = self.o + 1 + self.d + (1 if self.has_os else 0)
 
     def get(self) -> np.ndarray:
         m = self.model
-        v = [float(m.likelihood.noise.detach()), float(m.mean_module.constant.detach())]
+        v = [] if self.fixed else [float(m.likelihood.noise.detach())]
+        v.append(float(m.mean_module.constant.detach()))
         v += self.base.lengthscale.detach().reshape(-1).cpu().tolist()
         if self.has_os:
             v.append(float(m.covar_module.outputscale.detach()))
         return np.asarray(v, dtype=np.float64)
 
     def set(self, x: np.ndarray) -> None:
-        m = self.model
-        m.likelihood.noise = torch.tensor([float(x[0])], dtype=torch.float64)
-        m.mean_module.constant = float(x[1])
-        self.base.lengthscale = torch.as_tensor(x[2:2 + self.d]).reshape(1, -1)
+        m, o = self.model, self.o
+        if not self.fixed:
+            m.likelihood.noise = torch.tensor([float(x[0])], dtype=torch.float64)
+        m.mean_module.constant = float(x[o])
+        self.base.lengthscale = torch.as_tensor(x[o + 1:o + 1 + self.d]).reshape(1, -1)
         if self.has_os:
-            m.covar_module.outputscale = float(x[2 + self.d])
+            m.covar_module.outputscale = float(x[o + 1 + self.d])
+
+    def value_and_grad(self, x: np.ndarray):
+        return mll_value_and_grad(self.model, x, self)
+
+    def sample_priors(self, gen: torch.Generator) -> None:
+        _sample_all_priors(self.model, self, gen)
 
 
-def mll_terms(Xt: torch.Tensor, y: torch.Tensor, ls_t: torch.Tensor, noise: float, const: float,
+class _MultiLayout:
+    """The m members of a multi-output SingleTaskGP as one flat vector in the
+    batched model's parameter order (each parameter's m entries together:
+    noise_1..m, constant_1..m, lengthscale m x d, outputscale_1..m).  The loss
+    is the sum of the members' losses (the closure's Tensor.sum reducer over
+    the batched MLL, optim/closures/model_closures.py:171-184), so one
+    L-BFGS-B runs over all of them jointly, as the reference's does."""
+
+    def __init__(self, model: SingleTaskGP):
+        self.model = model
+        self.parts = [_Layout(mm) for mm in model.models]
+        p0, L = self.parts[0], self.parts[0].size
+        self.perm = np.asarray([t * L + start + j for _, start, size in p0.segments
+                                for t in range(len(self.parts)) for j in range(size)])
+        self.bounds = [b for p in self.parts for b in p.bounds]
+        self.bounds = [self.bounds[i] for i in self.perm]
+        self.size = L * len(self.parts)
+
+    def _split(self, x: np.ndarray):
+        cat = np.empty(self.size)
+        cat[self.perm] = x
+        L = self.parts[0].size
+        return [cat[t * L:(t + 1) * L] for t in range(len(self.parts))]
+
+    def get(self) -> np.ndarray:
+        return np.concatenate([p.get() for p in self.parts])[self.perm]
+
+    def set(self, x: np.ndarray) -> None:
+        for p, v in zip(self.parts, self._split(x)):
+            p.set(v)
+
+    def value_and_grad(self, x: np.ndarray):
+        loss, grads = 0.0, []
+        for p, v in zip(self.parts, self._split(x)):
+            lt, gt = p.value_and_grad(v)
+            loss += lt
+            grads.append(gt)
+        return loss, np.concatenate(grads)[self.perm]
+
+    def sample_priors(self, gen: torch.Generator) -> None:
+        for p in self.parts:
+            p.sample_priors(gen)
+
+
+def _layout(model):
+    return _MultiLayout(model) if getattr(model, "_is_multi_output", False) else _Layout(model)
+
+
+def mll_terms(Xt: torch.Tensor, y: torch.Tensor, ls_t: torch.Tensor, noise, const: float,
               os_: float, kind: int):
     """Data term of [G] ExactMarginalLogLikelihood, ll = log N(y | c, K + s2 I)
     (no priors, not divided by n), and d ll / d [noise, constant,
-    lengthscale_1..d, outputscale] (bo::mll's implementation)."""
+    lengthscale_1..d, outputscale] (bo::mll's implementation).  ``noise`` may
+    be an n-vector (fixed-noise likelihood: K + diag(noise); its gradient
+    entry is then meaningless)."""
     n, d = Xt.shape
     dev = Xt.device
     ls = ls_t.detach().cpu().numpy().astype(np.float64) if torch.is_tensor(ls_t) else np.asarray(ls_t)
@@ -123,43 +190,50 @@ def mll_terms(Xt: torch.Tensor, y: torch.Tensor, ls_t: torch.Tensor, noise: floa
 
 def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout):
     """Loss = -(log N(y | c, K + s2 I) + log priors) / n and its gradient: the
-    data term through bo::mll (torch.ops), the LogNormal priors on the host."""
+    data term through bo::mll (torch.ops), the LogNormal priors on the host.
+    Fixed noise: K + diag(observed variances), no noise entry or prior."""
     from . import ops  # noqa: F401  (registers torch.ops.bo)
     layout.set(x)
     Xt = model.train_inputs[0]
     y = model.train_targets
     n, d = Xt.shape
-    noise, const = x[0], x[1]
-    ls = x[2:2 + d]
-    os_ = x[2 + d] if layout.has_os else 1.0
+    o = layout.o
+    noise = 0.0 if layout.fixed else x[0]
+    nv = model.likelihood.noise if layout.fixed else None
+    const = x[o]
+    ls = x[o + 1:o + 1 + d]
+    os_ = x[o + 1 + d] if layout.has_os else 1.0
     ls_t = torch.as_tensor(ls, dtype=torch.float64, device=Xt.device)
-    llt, gt = torch.ops.bo.mll(Xt, y, ls_t, float(noise), float(const), float(os_), int(model.kind))
+    llt, gt = torch.ops.bo.mll(Xt, y, ls_t, float(noise), float(const), float(os_),
+                               int(model.kind), nv)
     ll = float(llt.item())
     gall = gt.cpu().numpy()
     g = np.zeros_like(x)
-    g[: 2 + d] = gall[: 2 + d]
+    if not layout.fixed:
+        g[0] = gall[0]
+        pv, pg = _prior_terms(model.likelihood.noise_prior, np.array([noise]))
+        ll += pv
+        g[0] += pg[0]
+    g[o:o + 1 + d] = gall[1:2 + d]
     if layout.has_os:
-        g[2 + d] = gall[2 + d]
-    pv, pg = _prior_terms(model.likelihood.noise_prior, np.array([noise]))
-    ll += pv
-    g[0] += pg[0]
+        g[o + 1 + d] = gall[2 + d]
     pv, pg = _prior_terms(layout.base.lengthscale_prior, ls)
     ll += pv
-    g[2:2 + d] += pg
+    g[o + 1:o + 1 + d] += pg
     return -ll / n, -g / n
 
 
 def fit_gpytorch_mll_scipy(mll: ExactMarginalLogLikelihood, method="L-BFGS-B", options=None,
                            callback=None, timeout_sec=None):
     model = mll.model
-    layout = _Layout(model)
+    layout = _layout(model)
     x0 = layout.get()
     if torch.isnan(model.train_inputs[0]).any() or torch.isnan(model.train_targets).any():
         from .exceptions import NanError
         raise NanError("training data contains NaN")
 
     def f(x):
-        return mll_value_and_grad(model, x, layout)
+        return layout.value_and_grad(x)
 
     res = minimize(f, x0, jac=True, method=method, bounds=layout.bounds, options=options or {},
                    callback=callback)
@@ -173,15 +247,15 @@ def fit_gpytorch_mll_scipy(mll: ExactMarginalLogLikelihood, method="L-BFGS-B", o
 def _sample_all_priors(model: SingleTaskGP, layout: _Layout, gen: torch.Generator):
     """sample_all_priors: draw free hyperparameters from their priors."""
     x = layout.get()
-    base = layout.base
-    if model.likelihood.noise_prior is not None:
+    base, o = layout.base, layout.o
+    if not layout.fixed and model.likelihood.noise_prior is not None:
         p = model.likelihood.noise_prior
         x[0] = max(math.exp(p.loc + p.scale * torch.randn(1, generator=gen).item()),
                    model.likelihood.noise_lower)
     if base.lengthscale_prior is not None:
         p = base.lengthscale_prior
         z = torch.randn(layout.d, generator=gen, dtype=torch.float64).numpy()
-        x[2:2 + layout.d] = np.maximum(np.exp(p.loc + p.scale * z), base.lengthscale_lower)
+        x[o + 1:o + 1 + layout.d] = np.maximum(np.exp(p.loc + p.scale * z), base.lengthscale_lower)
     layout.set(x)
 
 
@@ -191,13 +265,13 @@ def fit_gpytorch_mll(mll: ExactMarginalLogLikelihood, optimizer_kwargs=None, max
     optimizer_kwargs = optimizer_kwargs or {}
     model = mll.model
     mll.train()
-    layout = _Layout(model)
+    layout = _layout(model)
     gen = torch.Generator().manual_seed(0)
     ckpt = layout.get()
     for attempt in range(1, max_attempts + 1):
         if attempt > 1:
             layout.set(ckpt)
-            _sample_all_priors(model, layout, gen)
+            layout.sample_priors(gen)
         try:
             with warnings.catch_warnings(record=True) as ws:
                 warnings.simplefilter("always", category=OptimizationWarning)

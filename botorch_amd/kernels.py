@@ -197,10 +197,22 @@ def build_gp_cache(Xt, y, lengthscale, noise, constant, kind=_lib.RBF, outputsca
     jit = ctypes.c_double(0.0)
     ls = lengthscale.detach().reshape(-1).contiguous()
     st = _stream(dev)
-    check(lib().bo_gp_cache_build(kind, _p(Xt), n, d, _p(ls), float(outputscale), float(noise),
-                                  float(constant), _p(y.contiguous()), _p(L), _p(Linv), _p(U),
-                                  _p(beta), _p(alpha), max_tries, jitter0, ctypes.byref(jit),
-                                  _p(info), st), "gp_cache_build")
+    if torch.is_tensor(noise) and noise.numel() > 1:
+        # fixed-noise likelihood: one observed variance per training point
+        nv = noise.detach().reshape(-1).to(**f64).contiguous()
+        if nv.numel() != n:
+            raise ValueError(f"fixed noise has {nv.numel()} entries for {n} training points")
+        check(lib().bo_gp_cache_build_fixed(kind, _p(Xt), n, d, _p(ls), float(outputscale),
+                                            _p(nv), float(constant), _p(y.contiguous()), _p(L),
+                                            _p(Linv), _p(U), _p(beta), _p(alpha), max_tries,
+                                            jitter0, ctypes.byref(jit), _p(info), st),
+              "gp_cache_build_fixed")
+        noise = float(nv.mean())
+    else:
+        check(lib().bo_gp_cache_build(kind, _p(Xt), n, d, _p(ls), float(outputscale),
+                                      float(noise), float(constant), _p(y.contiguous()), _p(L),
+                                      _p(Linv), _p(U), _p(beta), _p(alpha), max_tries, jitter0,
+                                      ctypes.byref(jit), _p(info), st), "gp_cache_build")
     if jit.value > 0:
         import warnings
         from .exceptions import NumericalWarning

@@ -134,6 +134,21 @@ class GaussianLikelihood(nn.Module):
             self.raw_noise.copy_(torch.as_tensor(v, dtype=torch.float64).reshape(1))
 
 
+class FixedNoiseGaussianLikelihood(nn.Module):
+    """Observed per-point noise variances ([G] FixedNoiseGaussianLikelihood with
+    learn_additional_noise=False), the likelihood SingleTaskGP builds from
+    train_Yvar (botorch/models/gp_regression.py:187-194).  Nothing is learned:
+    ``noise`` is a buffer, there is no prior, and the MLL's K + s2 I becomes
+    K + diag(noise)."""
+
+    noise_prior = None
+    noise_lower = 0.0
+
+    def __init__(self, noise: torch.Tensor):
+        super().__init__()
+        self.register_buffer("noise", torch.as_tensor(noise, dtype=torch.float64).reshape(-1).clone())
+
+
 class ConstantMean(nn.Module):
     def __init__(self):
         super().__init__()
@@ -194,6 +209,28 @@ class Standardize(nn.Module):
         return self.means + self.stdvs * Y, (self.stdvs.pow(2) * Yvar if Yvar is not None else None)
 
 
+class _StackedView:
+    """Read-only view of one module of a multi-output SingleTaskGP's members,
+    stacking an attribute over the outputs in the reference's batched shapes
+    (likelihood.noise m x 1, covar_module.lengthscale m x 1 x d,
+    mean_module.constant m)."""
+
+    def __init__(self, members, name: str):
+        object.__setattr__(self, "_mods", [getattr(mm, name) for mm in members])
+
+    def __getattr__(self, attr):
+        vals = [getattr(mod, attr) for mod in self._mods]
+        if all(torch.is_tensor(v) for v in vals):
+            return torch.stack([v.detach() for v in vals])
+        if all(isinstance(v, (int, float)) for v in vals):
+            return torch.tensor(vals, dtype=torch.float64)
+        return vals
+
+    def __setattr__(self, attr, value):
+        raise AttributeError("set the hyperparameters of a multi-output SingleTaskGP through "
+                             "model.models[t]")
+
+
 class Model(nn.Module):
     """Abstract model with BoTorch's ``posterior`` contract (models/model.py:82-117)."""
 
@@ -232,36 +269,106 @@ class SingleTaskGP(Model):
                  train_Yvar: Optional[torch.Tensor] = None, likelihood=None, covar_module=None,
                  mean_module=None, outcome_transform="DEFAULT", input_transform=None):
         super().__init__()
-        if train_Yvar is not None:
-            raise UnsupportedError("fixed-noise models are not on the accelerated path")
         if input_transform is not None:
             raise UnsupportedError("input transforms are not on the accelerated path")
-        if train_X.dim() != 2 or train_Y.dim() != 2 or train_Y.shape[-1] != 1:
-            raise UnsupportedError("SingleTaskGP here takes train_X n x d and train_Y n x 1")
+        if train_X.dim() != 2 or train_Y.dim() != 2 or train_X.shape[0] != train_Y.shape[0]:
+            raise UnsupportedError("SingleTaskGP here takes train_X n x d and train_Y n x m")
+        if train_Yvar is not None and train_Yvar.shape != train_Y.shape:
+            raise ValueError(f"train_Yvar of shape {tuple(train_Yvar.shape)} does not match "
+                             f"train_Y of shape {tuple(train_Y.shape)}")
         train_X = train_X.to(torch.float64)
         train_Y = train_Y.to(torch.float64)
+        from .exceptions import InputDataError
         if torch.isnan(train_X).any() or torch.isnan(train_Y).any():
-            from .exceptions import InputDataError
             raise InputDataError("Input data contains NaN values.")
+        if train_Yvar is not None:
+            train_Yvar = train_Yvar.to(torch.float64)
+            if torch.isnan(train_Yvar).any():
+                raise InputDataError("Input data contains NaN values.")
+            if (train_Yvar < 0).any():  # models/utils/assorted.py validate_input_scaling
+                raise InputDataError("Input data contains negative variances.")
+        if train_Y.shape[-1] > 1:
+            self._init_multi_output(train_X, train_Y, train_Yvar, likelihood, covar_module,
+                                    mean_module, outcome_transform)
+            return
         if outcome_transform == "DEFAULT":
             outcome_transform = Standardize(m=1)
         if outcome_transform is not None:
             outcome_transform.train()
-            train_Y_tf, _ = outcome_transform(train_Y)
+            train_Y_tf, train_Yvar_tf = outcome_transform(train_Y, train_Yvar)
             self.outcome_transform = outcome_transform
         else:
-            train_Y_tf = train_Y
+            train_Y_tf, train_Yvar_tf = train_Y, train_Yvar
         self._check_scaling(train_X, train_Y_tf)
         self.train_inputs = (train_X,)
         self.train_targets = train_Y_tf.squeeze(-1)
         self._raw_train_Y = train_Y
         d = train_X.shape[-1]
+        if likelihood is None and train_Yvar_tf is not None:
+            likelihood = FixedNoiseGaussianLikelihood(train_Yvar_tf.squeeze(-1))
         self.likelihood = likelihood if likelihood is not None else get_gaussian_likelihood_with_lognormal_prior()
         self.mean_module = mean_module if mean_module is not None else ConstantMean()
         self.covar_module = covar_module if covar_module is not None else get_covar_module_with_dim_scaled_prior(d)
         self._cache = None
         self._cache_key = None
         self.to(train_X.device)
+
+    def _init_multi_output(self, train_X, train_Y, train_Yvar, likelihood, covar_module,
+                           mean_module, outcome_transform):
+        """m > 1 outputs: the reference's batched multi-output model
+        (models/gpytorch.py:327-355 BatchedMultiOutputGPyTorchModel, batch shape
+        [m] of independent GPs with their own hyperparameters) as m single-output
+        members sharing train_X.  Standardize(m) standardises each column on its
+        own, so each member's Standardize(1) holds exactly its column's
+        statistics; the posterior is the members' block-diagonal joint (the
+        from_batch_mvn MTMVN), which the ModelListGP routes (qEHVI / qNEHVI /
+        scalarised qEI) consume through ``models``; fit_gpytorch_mll minimises
+        the summed loss jointly over all members' parameters."""
+        m = train_Y.shape[-1]
+        if likelihood is not None or covar_module is not None or mean_module is not None:
+            raise UnsupportedError("custom modules of a multi-output SingleTaskGP (batched "
+                                   "modules) are not on the accelerated path")
+        if outcome_transform == "DEFAULT":
+            outcome_transform = Standardize(m=m)
+        if outcome_transform is not None and not (isinstance(outcome_transform, Standardize)
+                                                  and outcome_transform._m == m):
+            raise UnsupportedError("a multi-output SingleTaskGP takes Standardize(m) or no "
+                                   "outcome transform here")
+        if outcome_transform is not None:
+            # statistics of the full n x m Y (the reference's reduction), each
+            # member then holds its column of them
+            outcome_transform.train()
+            Y_tf, Yvar_tf = outcome_transform(train_Y, train_Yvar)
+            outcome_transform.eval()
+            self.outcome_transform = outcome_transform
+        else:
+            Y_tf, Yvar_tf = train_Y, train_Yvar
+        members = []
+        for t in range(m):
+            mm = SingleTaskGP(train_X, Y_tf[:, t:t + 1],
+                              None if Yvar_tf is None else Yvar_tf[:, t:t + 1],
+                              outcome_transform=None)
+            if outcome_transform is not None:
+                col = Standardize(m=1, min_stdv=outcome_transform._min_stdv)
+                col.means = outcome_transform.means[..., t:t + 1].clone()
+                col.stdvs = outcome_transform.stdvs[..., t:t + 1].clone()
+                col._is_trained = True
+                col.eval()
+                mm.outcome_transform = col
+                mm._raw_train_Y = train_Y[:, t:t + 1]
+            members.append(mm)
+        self.models = nn.ModuleList(members)
+        self._num_outputs = m
+        for name in ("likelihood", "covar_module", "mean_module"):
+            setattr(self, name, _StackedView(members, name))
+        self.train_inputs = (train_X,)
+        self.train_targets = torch.stack([mm.train_targets for mm in members])  # m x n
+        self._cache = None
+        self._cache_key = None
+
+    @property
+    def _is_multi_output(self) -> bool:
+        return self._num_outputs > 1
 
     @staticmethod
     def _check_scaling(X, Y):
@@ -276,9 +383,11 @@ class SingleTaskGP(Model):
         return self.covar_module.kind
 
     def hyper(self):
+        if self._is_multi_output:
+            raise UnsupportedError("hyper() of a multi-output SingleTaskGP: use model.models[t]")
         ls = self.covar_module.lengthscale.detach().reshape(-1)
         os_ = float(self.covar_module.outputscale.detach()) if isinstance(self.covar_module, ScaleKernel) else 1.0
-        return ls, os_, float(self.likelihood.noise.detach()), float(self.mean_module.constant.detach())
+        return ls, os_, float(self.likelihood.noise.detach().mean()), float(self.mean_module.constant.detach())
 
     def train(self, mode: bool = True):
         if mode:
@@ -286,13 +395,22 @@ class SingleTaskGP(Model):
             self._cache_key = None
         return super().train(mode)
 
+    @property
+    def batch_shape(self) -> torch.Size:
+        return torch.Size([])
+
     def _key(self):
+        if self._is_multi_output:
+            return tuple(mm._key() for mm in self.models)
         ps = [self.train_inputs[0], self.train_targets] + list(self.parameters())
         return tuple((p.data_ptr(), p._version) for p in ps)
 
     def prediction_cache(self):
         """Device caches of [G] exact prediction; rebuilt on any change."""
         from . import kernels
+        if self._is_multi_output:
+            raise UnsupportedError("a multi-output SingleTaskGP keeps one cache per output "
+                                   "(model.models[t].prediction_cache())")
         from .settings import propagate_grads
         if propagate_grads.on() and (self.train_inputs[0].requires_grad or self.train_targets.requires_grad):
             from .exceptions import UnsupportedError
@@ -304,9 +422,10 @@ class SingleTaskGP(Model):
             from . import ops  # noqa: F401  (torch.ops.bo registration)
             ls, os_, noise, c = self.hyper()
             Xt = self.train_inputs[0].contiguous()
+            nv = self.likelihood.noise if isinstance(self.likelihood, FixedNoiseGaussianLikelihood) else None
             L, Linv, U, beta, alpha, Xs, jit = torch.ops.bo.gp_cache(
                 Xt, self.train_targets.contiguous(), ls.contiguous(), float(os_), float(noise),
-                float(c), int(self.kind))
+                float(c), int(self.kind), nv)
             n, d = Xt.shape
             self._cache = kernels.GPCache(self.kind, n, d, U.shape[0], Xt, Xs, ls.contiguous(),
                                           float(os_), float(noise), float(c), L, Linv, U, beta,
@@ -316,8 +435,13 @@ class SingleTaskGP(Model):
 
     def posterior(self, X: torch.Tensor, output_indices=None, observation_noise=False,
                   posterior_transform=None):
-        """botorch/models/gpytorch.py:405-466."""
-        from .posteriors import GPyTorchPosterior
+        """botorch/models/gpytorch.py:405-466 (m > 1: :327-355)."""
+        from .posteriors import GPyTorchPosterior, PosteriorList
+        if self._is_multi_output:
+            idx = output_indices if output_indices is not None else range(self._num_outputs)
+            post = PosteriorList(*[self.models[i].posterior(X, observation_noise=observation_noise)
+                                   for i in idx])
+            return post if posterior_transform is None else posterior_transform(post)
         if output_indices not in (None, [0]):
             raise UnsupportedError("single-output model")
         self.eval()

@@ -89,16 +89,19 @@ def _(state, shift, n, skip, first_f32):
 # ---- bo::gp_cache --------------------------------------------------------------------------
 @torch.library.custom_op("bo::gp_cache", mutates_args=(), device_types="cuda")
 def gp_cache(Xt: Tensor, y: Tensor, lengthscale: Tensor, outputscale: float, noise: float,
-             constant: float, kind: int) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
-    """(L, L^{-1}, U = L^{-T}: np x np; beta, alpha: n; Xt_scaled: n x 8; jitter: 1)."""
-    c = kernels.build_gp_cache(Xt, y, lengthscale, noise, constant, kind=kind,
+             constant: float, kind: int, noise_vec: Optional[Tensor] = None
+             ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """(L, L^{-1}, U = L^{-T}: np x np; beta, alpha: n; Xt_scaled: n x 8; jitter: 1).
+    noise_vec (n): a fixed-noise likelihood's observed variances (noise ignored)."""
+    c = kernels.build_gp_cache(Xt, y, lengthscale, noise if noise_vec is None else noise_vec,
+                               constant, kind=kind,
                                outputscale=outputscale)
     jit = torch.full((1,), c.jitter, dtype=F64, device=Xt.device)
     return c.L, c.Linv, c.U, c.beta, c.alpha, c.Xt_scaled, jit
 
 
 @gp_cache.register_fake
-def _(Xt, y, lengthscale, outputscale, noise, constant, kind):
+def _(Xt, y, lengthscale, outputscale, noise, constant, kind, noise_vec=None):
     n = Xt.shape[0]
     np_ = _padded(n)
     mk = lambda *s: Xt.new_empty(*s, dtype=F64)  # noqa: E731
@@ -398,19 +401,22 @@ qehvi.register_autograd(_qehvi_bwd, setup_context=_qehvi_setup)
 # ---- bo::mll -----------------------------------------------------------------------------------
 @torch.library.custom_op("bo::mll", mutates_args=(), device_types="cuda")
 def mll(Xt: Tensor, y: Tensor, lengthscale: Tensor, noise: float, constant: float,
-        outputscale: float, kind: int) -> Tuple[Tensor, Tensor]:
+        outputscale: float, kind: int, noise_vec: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
     """Data term of the exact marginal log likelihood, log N(y | c, K + s2 I)
     (no priors, not divided by n), and its gradient w.r.t. [noise, constant,
     lengthscale_1..d, (outputscale)]: one Cholesky + inverse (task DAG), the
-    triangular A^{-1} = U U^T and one bo_mll_terms pass."""
+    triangular A^{-1} = U U^T and one bo_mll_terms pass.  noise_vec (n): a
+    fixed-noise likelihood (K + diag(noise_vec); the noise entry of the
+    gradient is then meaningless and unused)."""
     from .fit import mll_terms
-    val, grad = mll_terms(Xt, y, lengthscale, noise, constant, outputscale, kind)
+    val, grad = mll_terms(Xt, y, lengthscale, noise if noise_vec is None else noise_vec,
+                          constant, outputscale, kind)
     return (torch.tensor([val], dtype=F64, device=Xt.device),
             torch.as_tensor(grad, dtype=F64).to(Xt.device))
 
 
 @mll.register_fake
-def _(Xt, y, lengthscale, noise, constant, outputscale, kind):
+def _(Xt, y, lengthscale, noise, constant, outputscale, kind, noise_vec=None):
     d = Xt.shape[1]
     return Xt.new_empty(1, dtype=F64), Xt.new_empty(d + 3, dtype=F64)
 

@@ -177,7 +177,9 @@ class GPyTorchPosterior:
         mean, cov = posterior_moments(model, X)
         if observation_noise is True:
             _, ystd = model.outcome_stats()
-            noise = model.likelihood.noise.reshape(()) * ystd * ystd
+            # homoskedastic: the one noise level; fixed noise: the mean of the
+            # observed variances (models/gpytorch.py _apply_noise, FixedNoise case)
+            noise = model.likelihood.noise.mean() * ystd * ystd
             cov = cov + noise * torch.eye(cov.shape[-1], dtype=cov.dtype, device=cov.device)
         elif torch.is_tensor(observation_noise):
             cov = cov + torch.diag_embed(observation_noise.squeeze(-1))

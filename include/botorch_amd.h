@@ -190,6 +190,15 @@ int bo_gp_cache_build(int kind, const double* Xt, int64_t n, int d, const double
                       double* L, double* Linv, double* U, double* beta, double* alpha,
                       int max_tries, double jitter0, double* jitter_used, int* info_dev,
                       void* stream);
+/* The same caches under a fixed-noise likelihood (SingleTaskGP with train_Yvar,
+ * botorch/models/gp_regression.py:187-194 -> [G] FixedNoiseGaussianLikelihood):
+ * K + diag(noise_vec), noise_vec: n observed variances (device, standardised
+ * like the targets), then the same jitter ladder. */
+int bo_gp_cache_build_fixed(int kind, const double* Xt, int64_t n, int d,
+                            const double* lengthscale, double outputscale,
+                            const double* noise_vec, double constant, const double* y, double* L,
+                            double* Linv, double* U, double* beta, double* alpha, int max_tries,
+                            double jitter0, double* jitter_used, int* info_dev, void* stream);
 
 /* Geometry of the fused posterior kernels for B t-batches of q points (1 <= q
  * <= 16) over n training points: Qp = q rounded up to a power of two,

@@ -115,7 +115,7 @@ def standardize_fit(Y: torch.Tensor, min_stdv: float = 1e-8):
 class GPHyper:
     """SingleTaskGP hyperparameters (transform=None constraints: raw == value)."""
     lengthscale: torch.Tensor  # (d,)
-    noise: float
+    noise: float  # or an (n,) tensor: a fixed-noise likelihood's variances, K + diag(noise)
     constant: float
     outputscale: float = 1.0
     kind: int = RBF
@@ -198,13 +198,16 @@ def lognormal_log_prob(x, loc, scale):
     return -((lx - loc) ** 2) / (2 * scale ** 2) - math.log(scale) - 0.5 * math.log(2 * math.pi) - lx
 
 
-def neg_mll(train_X, train_y, lengthscale, noise, constant):
+def neg_mll(train_X, train_y, lengthscale, noise, constant, fixed_noise: bool = False):
     """Loss of botorch's exact-MLL closure (optim/closures/model_closures.py:171-184).
 
     [G] ExactMarginalLogLikelihood: (log N(y | c, K + s2 I) + sum of prior
     log-probs) / n, negated; priors = LogNormal(sqrt2 + ln(d)/2, sqrt3) on each
     lengthscale and LogNormal(-4, 1) on the noise (gpytorch_modules.py:74-127).
     Differentiable (autograd) in lengthscale, noise, constant.
+    fixed_noise: ``noise`` is the n observed variances of a fixed-noise
+    likelihood ([G] FixedNoiseGaussianLikelihood, gp_regression.py:187-194):
+    K + diag(noise), no noise prior.
     """
     n, d = train_X.shape
     K = covar(train_X, train_X, lengthscale, RBF, 1.0, x1_eq_x2=True)
@@ -217,7 +220,8 @@ def neg_mll(train_X, train_y, lengthscale, noise, constant):
     ll = -0.5 * (inv_quad + logdet + n * math.log(2 * math.pi))
     ls_loc = math.sqrt(2) + 0.5 * math.log(d)
     prior = lognormal_log_prob(lengthscale, ls_loc, math.sqrt(3)).sum()
-    prior = prior + lognormal_log_prob(noise.reshape(-1), -4.0, 1.0).sum()
+    if not fixed_noise:
+        prior = prior + lognormal_log_prob(noise.reshape(-1), -4.0, 1.0).sum()
     return -(ll + prior) / n
 
 

@@ -1,0 +1,185 @@
+"""SingleTaskGP with train_Yvar (fixed-noise likelihood) and with m > 1 outputs
+(the batched multi-output model), on the device path, against the oracle
+(reference: botorch/models/gp_regression.py:130-217, models/gpytorch.py:327-466,
+[G] FixedNoiseGaussianLikelihood; optim/closures/model_closures.py:171-184)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _data(n, m=1, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.rand(n, 4, generator=g, dtype=torch.float64)
+    cols = [torch.sin(3 * X[:, 0] + t) + X[:, 1] * (t + 1) - X[:, 2] ** 2 for t in range(m)]
+    Y = torch.stack(cols, dim=-1) + 0.05 * torch.randn(n, m, generator=g, dtype=torch.float64)
+    Yvar = 1e-3 + 0.02 * torch.rand(n, m, generator=g, dtype=torch.float64)
+    return X, Y, Yvar
+
+
+def test_fixed_noise_mll_value_and_grad_match_oracle():
+    from botorch_amd.fit import _Layout, mll_value_and_grad
+    from botorch_amd.models import FixedNoiseGaussianLikelihood, SingleTaskGP
+    from oracle.gp import neg_mll, standardize_fit
+    X, Y, Yvar = _data(300)
+    m = SingleTaskGP(X.to(DEV), Y.to(DEV), Yvar.to(DEV))
+    assert isinstance(m.likelihood, FixedNoiseGaussianLikelihood)
+    lay = _Layout(m)
+    assert lay.fixed and len(lay.get()) == 1 + 4  # constant + lengthscales, no noise
+    x = np.array([0.1, 0.4, 0.5, 0.6, 0.7])
+    val, grad = mll_value_and_grad(m, x, lay)
+    mu, sd = standardize_fit(Y)
+    y = ((Y - mu) / sd).squeeze(-1)
+    nv = (Yvar / sd ** 2).squeeze(-1)  # Standardize transforms Yvar (outcome.py:253-307)
+    ls = torch.tensor(x[1:], requires_grad=True)
+    c = torch.tensor(x[0], requires_grad=True)
+    loss = neg_mll(X, y, ls, nv, c, fixed_noise=True)
+    loss.backward()
+    ref_g = np.concatenate([[c.grad.item()], ls.grad.numpy()])
+    assert abs(val - loss.item()) < 1e-9 * max(1.0, abs(loss.item()))
+    np.testing.assert_allclose(grad, ref_g, rtol=1e-6, atol=1e-9)
+
+
+def test_fixed_noise_posterior_matches_oracle():
+    from botorch_amd.models import SingleTaskGP
+    from oracle.gp import ExactGPOracle, GPHyper, standardize_fit
+    X, Y, Yvar = _data(200, seed=1)
+    m = SingleTaskGP(X.to(DEV), Y.to(DEV), Yvar.to(DEV))
+    m.covar_module.lengthscale = torch.tensor([[0.5, 0.6, 0.7, 0.8]], dtype=torch.float64)
+    m.mean_module.constant = 0.2
+    m.eval()
+    _, sd = standardize_fit(Y)
+    orc = ExactGPOracle(X, Y, GPHyper(torch.tensor([0.5, 0.6, 0.7, 0.8], dtype=torch.float64),
+                                      (Yvar / sd ** 2).squeeze(-1), 0.2))
+    Xc = torch.rand(5, 3, 4, generator=torch.Generator().manual_seed(3), dtype=torch.float64)
+    post = m.posterior(Xc.to(DEV))
+    mean_ref, cov_ref = orc.posterior(Xc)
+    torch.testing.assert_close(post.mean.squeeze(-1).cpu(), mean_ref, rtol=1e-9, atol=1e-10)
+    torch.testing.assert_close(post.distribution.covariance_matrix.cpu(), cov_ref, rtol=1e-8,
+                               atol=1e-10)
+    # observation_noise=True: the mean observed variance (models/gpytorch.py _apply_noise)
+    pn = m.posterior(Xc.to(DEV), observation_noise=True)
+    extra = float((Yvar / sd ** 2).mean()) * float(sd) ** 2
+    torch.testing.assert_close(pn.distribution.covariance_matrix.cpu(),
+                               cov_ref + extra * torch.eye(3, dtype=torch.float64),
+                               rtol=1e-8, atol=1e-10)
+
+
+def test_fixed_noise_fit_matches_oracle_optimum():
+    """fit_gpytorch_mll over (constant, lengthscales) vs scipy L-BFGS-B on the
+    oracle's fixed-noise loss from the same start: same optimum."""
+    from scipy.optimize import minimize
+
+    from botorch_amd.fit import ExactMarginalLogLikelihood, _Layout, fit_gpytorch_mll
+    from botorch_amd.models import SingleTaskGP
+    from oracle.gp import neg_mll, standardize_fit
+    X, Y, Yvar = _data(150, seed=2)
+    m = SingleTaskGP(X.to(DEV), Y.to(DEV), Yvar.to(DEV))
+    lay = _Layout(m)
+    x0 = lay.get()
+    fit_gpytorch_mll(ExactMarginalLogLikelihood(m.likelihood, m))
+    x1 = lay.get()
+    mu, sd = standardize_fit(Y)
+    y = ((Y - mu) / sd).squeeze(-1)
+    nv = (Yvar / sd ** 2).squeeze(-1)
+
+    def f(x):
+        c = torch.tensor(float(x[0]), requires_grad=True)
+        ls = torch.tensor(np.asarray(x[1:]), requires_grad=True)
+        loss = neg_mll(X, y, ls, nv, c, fixed_noise=True)
+        loss.backward()
+        return loss.item(), np.concatenate([[c.grad.item()], ls.grad.numpy()])
+
+    ref = minimize(f, x0, jac=True, method="L-BFGS-B", bounds=lay.bounds)
+    assert f(x1)[0] <= ref.fun + 1e-6 * abs(ref.fun)
+    np.testing.assert_allclose(x1, ref.x, rtol=2e-3, atol=2e-3)
+
+
+def _multi(n=120, m=3, seed=4, yvar=False):
+    from botorch_amd.models import SingleTaskGP
+    X, Y, Yvar = _data(n, m, seed)
+    mdl = SingleTaskGP(X.to(DEV), Y.to(DEV), Yvar.to(DEV) if yvar else None)
+    singles = [SingleTaskGP(X.to(DEV), Y[:, t:t + 1].to(DEV),
+                            Yvar[:, t:t + 1].to(DEV) if yvar else None) for t in range(m)]
+    for t in range(m):
+        ls = torch.tensor([[0.4 + 0.1 * t, 0.6, 0.7, 0.9]], dtype=torch.float64)
+        for mm in (mdl.models[t], singles[t]):
+            mm.covar_module.lengthscale = ls
+            mm.mean_module.constant = 0.1 * t
+            if not yvar:
+                mm.likelihood.noise = torch.tensor([1e-3 * (t + 1)], dtype=torch.float64)
+    return X, Y, mdl.eval(), [s.eval() for s in singles]
+
+
+def test_multi_output_shapes_and_posterior():
+    X, Y, mdl, singles = _multi()
+    assert mdl.num_outputs == 3
+    assert mdl.likelihood.noise.shape == (3, 1)
+    assert mdl.covar_module.lengthscale.shape == (3, 1, 4)
+    assert mdl.mean_module.constant.shape == (3,)
+    assert mdl.train_targets.shape == (3, 120)
+    torch.testing.assert_close(mdl.outcome_transform.means.cpu(), Y.mean(0, keepdim=True))
+    Xc = torch.rand(4, 5, 4, generator=torch.Generator().manual_seed(0), dtype=torch.float64).to(DEV)
+    post = mdl.posterior(Xc)
+    assert post.mean.shape == (4, 5, 3)
+    for t in range(3):
+        ps = singles[t].posterior(Xc)
+        # the members hold the full-Y Standardize statistics, the singles their
+        # own column's (equal up to the reduction order)
+        torch.testing.assert_close(post.mean[..., t], ps.mean[..., 0], rtol=1e-12, atol=1e-13)
+    sub = mdl.posterior(Xc, output_indices=[2])
+    assert torch.equal(sub.mean[..., 0], post.mean[..., 2])
+
+
+def test_multi_output_qehvi_equals_model_list():
+    """The batched model's posterior is the from_batch_mvn block-diagonal joint,
+    the same as a ModelListGP's (one q*m Sobol draw either way): qEHVI values
+    and gradients agree (to the last bits of the Standardize statistics)."""
+    from botorch_amd.acquisition import qExpectedHypervolumeImprovement
+    from botorch_amd.models import ModelListGP
+    from botorch_amd.multi_objective import FastNondominatedPartitioning
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    X, Y, mdl, singles = _multi(m=2)
+    ref_point = (Y.min(0).values - 0.1).tolist()
+    part = FastNondominatedPartitioning(torch.tensor(ref_point, dtype=torch.float64), Y)
+    vals, grads = [], []
+    for model in (mdl, ModelListGP(*singles)):
+        acqf = qExpectedHypervolumeImprovement(model, ref_point, part,
+                                               sampler=SobolQMCNormalSampler(torch.Size([64]), seed=1))
+        Xc = torch.rand(6, 3, 4, generator=torch.Generator().manual_seed(1),
+                        dtype=torch.float64).to(DEV).requires_grad_(True)
+        v = acqf(Xc)
+        (g,) = torch.autograd.grad(v.sum(), Xc)
+        vals.append(v.detach())
+        grads.append(g)
+    torch.testing.assert_close(vals[0], vals[1], rtol=1e-11, atol=1e-13)
+    torch.testing.assert_close(grads[0], grads[1], rtol=1e-9, atol=1e-11)
+
+
+@pytest.mark.parametrize("yvar", [False, True])
+def test_multi_output_joint_fit(yvar):
+    """The summed loss over the members, one L-BFGS-B in the batched model's
+    parameter order: the joint value is the sum of the members' values and the
+    joint optimum is each member's own optimum (the loss is separable)."""
+    from botorch_amd.fit import ExactMarginalLogLikelihood, _Layout, _layout, fit_gpytorch_mll
+    _, _, mdl, singles = _multi(n=100, m=2, seed=5, yvar=yvar)
+    lay = _layout(mdl)
+    x0 = lay.get()
+    v0, g0 = lay.value_and_grad(x0)
+    parts = [_Layout(s).value_and_grad(_Layout(s).get()) for s in singles]
+    assert abs(v0 - sum(p[0] for p in parts)) < 1e-12 * max(1.0, abs(v0))
+    np.testing.assert_allclose(np.sort(g0), np.sort(np.concatenate([p[1] for p in parts])),
+                               rtol=1e-12, atol=1e-15)
+    fit_gpytorch_mll(ExactMarginalLogLikelihood(mdl.likelihood, mdl))
+    v1, _ = lay.value_and_grad(lay.get())
+    assert v1 < v0
+    tot = 0.0
+    for s in singles:
+        fit_gpytorch_mll(ExactMarginalLogLikelihood(s.likelihood, s))
+        sl = _Layout(s)
+        tot += sl.value_and_grad(sl.get())[0]
+    # one joint L-BFGS-B over 2 x 6 parameters stops on the summed loss's
+    # tolerance, the separate fits on their own: the same optimum to ~1e-4
+    assert abs(v1 - tot) < 2e-4 * max(1.0, abs(tot))
