@@ -92,6 +92,9 @@ _SIGNATURES = {
     "bo_sobol_normal": (c_int, [_P, _P, c_int, c_int64, c_int64, c_int, _P, _P]),
     "bo_lbfgs_step": (c_int, [c_int, c_int, c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P, _P, c_double, c_double, c_double, c_double, _P]),
+    "bo_lbfgsb_step": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double, _P,
+                               _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "bo_lbfgsb_layout": (c_int, [_P]),
     "bo_nd_partition_host": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, POINTER(c_int64), _P,
                                      _P, c_int]),
     "bo_sobol_box": (c_int, [_P, _P, c_int, c_int64, c_int64, c_int, _P, _P, c_int, _P, _P]),
@@ -186,15 +189,24 @@ class LbfgsStepArgs(_Args):
                        ("pgtol", c_double), ("min_alpha", c_double)]
 
 
+class LbfgsbArgs(_Args):
+    _fields_ = _HDR + [("B", c_int32), ("n", c_int32), ("m", c_int32), ("maxls", c_int32),
+                       ("maxiter", c_int32), ("maxfun", c_int32), ("ftol", c_double),
+                       ("pgtol", c_double), ("lower", _D), ("upper", _D), ("xt", _D), ("ft", _D),
+                       ("gt", _D), ("v", _D), ("iv", _D), ("ws", _D), ("wy", _D), ("mat", _D),
+                       ("ds", _D), ("is_", _D)]
+
+
 for _name, _cls in (("bo_post_partials_v", PostPartialsArgs), ("bo_qmc_finalize_v", QmcFinalizeArgs),
                     ("bo_qmc_backward_v", QmcBackwardArgs), ("bo_post_backward_v", PostBackwardArgs),
                     ("bo_qehvi_v", QehviArgs), ("bo_qehvi_backward_v", QehviArgs),
-                    ("bo_lbfgs_step_v", LbfgsStepArgs)):
+                    ("bo_lbfgs_step_v", LbfgsStepArgs), ("bo_lbfgsb_step_v", LbfgsbArgs)):
     _SIGNATURES[_name] = (c_int, [POINTER(_cls), _P])
 _SIGNATURES["bo_struct_size"] = (c_int64, [ctypes.c_char_p])
 ARG_RECORDS = {"BoPostPartialsArgs": PostPartialsArgs, "BoQmcFinalizeArgs": QmcFinalizeArgs,
                "BoQmcBackwardArgs": QmcBackwardArgs, "BoPostBackwardArgs": PostBackwardArgs,
-               "BoQehviArgs": QehviArgs, "BoLbfgsStepArgs": LbfgsStepArgs}
+               "BoQehviArgs": QehviArgs, "BoLbfgsStepArgs": LbfgsStepArgs,
+               "BoLbfgsbArgs": LbfgsbArgs}
 
 _lib = None
 

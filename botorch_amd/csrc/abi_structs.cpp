@@ -78,6 +78,13 @@ int bo_lbfgs_step_v(const BoLbfgsStepArgs* a, void* stream) {
                        a->upper, a->c1, a->ftol, a->pgtol, a->min_alpha, stream);
 }
 
+int bo_lbfgsb_step_v(const BoLbfgsbArgs* a, void* stream) {
+  if (!header_ok(a, "bo_lbfgsb_step_v")) return BO_ERR_ARG;
+  return bo_lbfgsb_step(a->B, a->n, a->m, a->maxls, a->maxiter, a->maxfun, a->ftol, a->pgtol,
+                        a->lower, a->upper, a->xt, a->ft, a->gt, a->v, a->iv, a->ws, a->wy, a->mat,
+                        a->ds, a->is, stream);
+}
+
 }  // extern "C"
 
 // sizeof of each argument record (HOST, for bindings to verify their layouts).
@@ -89,5 +96,6 @@ extern "C" int64_t bo_struct_size(const char* name) {
   if (s == "BoPostBackwardArgs") return sizeof(BoPostBackwardArgs);
   if (s == "BoQehviArgs") return sizeof(BoQehviArgs);
   if (s == "BoLbfgsStepArgs") return sizeof(BoLbfgsStepArgs);
+  if (s == "BoLbfgsbArgs") return sizeof(BoLbfgsbArgs);
   return -1;
 }

@@ -1,0 +1,102 @@
+// Device-resident multi-start L-BFGS-B: one 64-lane wave per restart runs the
+// reverse-communication state machine of lbfgsb_core.h (scipy 1.15's L-BFGS-B,
+// the optimiser of botorch's gen_candidates_scipy, botorch/generation/gen.py:
+// 194-267) for one function evaluation per launch.
+//
+// The caller evaluates -acq and its gradient at every restart's trial point xt
+// (one batched forward + backward of the fused acquisition kernels) and
+// launches bo_lbfgsb_step, which consumes them and writes the next trial
+// points.  Iterate, gradient, the compact-form memory (S, Y ring; SY, SS and
+// the Cholesky factor of theta SS + L D^-1 L^T) and the line-search state stay
+// in HBM between launches; the host reads only the status vector, every few
+// evaluations.  Vector work (dot products over n = q d, the Cauchy breakpoint
+// search, the free-set products of formk) is spread over the wave's lanes; the
+// 2m x 2m algebra runs on lane 0 in LDS.  A restart that has stopped keeps
+// xt = x, so it costs nothing but its slot in the batched evaluation.
+#include "common.h"
+
+#define BO_HD __device__
+#include "lbfgsb_core.h"
+
+namespace {
+
+struct WaveCtx {
+  static constexpr int NL = 64;
+  int lane;
+  __device__ void sync() { __syncthreads(); }
+  __device__ double sum(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+  }
+  __device__ double max(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+  }
+  __device__ double min(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+  }
+  __device__ void argmin(double& v, int& i) {  // ties to the smallest index
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(v, o);
+      const int oi = __shfl_xor(i, o);
+      if (ov < v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
+      }
+    }
+  }
+};
+
+__global__ __launch_bounds__(64) void lbfgsb_kernel(bolb::Problem P, double* __restrict__ xt,
+                                                    const double* __restrict__ ft,
+                                                    const double* __restrict__ gt,
+                                                    double* __restrict__ v, int* __restrict__ iv,
+                                                    double* __restrict__ ws,
+                                                    double* __restrict__ wy,
+                                                    double* __restrict__ mat,
+                                                    double* __restrict__ ds, int* __restrict__ is) {
+  __shared__ bolb::Shared S;
+  const long b = blockIdx.x;
+  const long n = P.n, m = P.m;
+  bolb::Restart R{xt + b * n,
+                  ft[b],
+                  gt + b * n,
+                  v + b * bolb::V_COUNT * n,
+                  iv + b * bolb::IV_COUNT * n,
+                  ws + b * m * n,
+                  wy + b * m * n,
+                  mat + b * bolb::NMAT * bolb::MMAX * bolb::MMAX,
+                  ds + b * bolb::DSLOTS,
+                  is + b * bolb::ISLOTS};
+  WaveCtx c{(int)threadIdx.x};
+  bolb::Step<WaveCtx> st(c, P, R, S);
+  st.run();
+}
+
+}  // namespace
+
+extern "C" int bo_lbfgsb_layout(int* out) {
+  out[0] = bolb::V_COUNT;
+  out[1] = bolb::IV_COUNT;
+  out[2] = bolb::NMAT * bolb::MMAX * bolb::MMAX;
+  out[3] = bolb::DSLOTS;
+  out[4] = bolb::ISLOTS;
+  out[5] = bolb::MMAX;
+  return BO_OK;
+}
+
+extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int maxfun, double ftol,
+                              double pgtol, const double* lower, const double* upper, double* xt,
+                              const double* ft, const double* gt, double* v, int* iv, double* ws,
+                              double* wy, double* mat, double* ds, int* is, void* stream) {
+  BO_CHECK_ARG(B >= 0 && n >= 1 && m >= 1 && m <= bolb::MMAX && maxls >= 1,
+               "bo_lbfgsb_step: B=%d n=%d m=%d (1..%d) maxls=%d", B, n, m, bolb::MMAX, maxls);
+  BO_CHECK_ARG(lower && upper && xt && ft && gt && v && iv && ws && wy && mat && ds && is,
+               "bo_lbfgsb_step: null buffer");
+  if (B == 0) return BO_OK;
+  bolb::Problem P{n, m, maxls, maxiter, maxfun, ftol, pgtol, lower, upper};
+  lbfgsb_kernel<<<B, 64, 0, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws, wy, mat, ds, is);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}

@@ -12,6 +12,7 @@ the final argmax/gather is one all-reduce.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import time
 import warnings
@@ -316,29 +317,87 @@ class _LBFGSState:
         self.nacc = torch.zeros(B, **i32)
 
 
+class _LBFGSBState:
+    """Device buffers of the multi-start L-BFGS-B (bo_lbfgsb_step): zeroed
+    state = "start at xt"."""
+
+    def __init__(self, X0: torch.Tensor, m: int):
+        from ._lib import lib
+        lay = (ctypes.c_int * 6)()
+        lib().bo_lbfgsb_layout(lay)
+        nv, niv, nmat, nd, ni, mmax = list(lay)
+        if not 1 <= m <= mmax:
+            raise ValueError(f"maxcor={m}: the device L-BFGS-B keeps at most {mmax} pairs")
+        B, n = X0.shape[0], X0[0].numel()
+        f64 = dict(dtype=torch.float64, device=X0.device)
+        i32 = dict(dtype=torch.int32, device=X0.device)
+        self.B, self.n, self.m = B, n, m
+        self.xt = X0.reshape(B, n).to(torch.float64).clone()
+        self.v = torch.zeros(B, nv, n, **f64)
+        self.iv = torch.zeros(B, niv, n, **i32)
+        self.ws = torch.zeros(B, m, n, **f64)
+        self.wy = torch.zeros(B, m, n, **f64)
+        self.mat = torch.zeros(B, nmat, **f64)
+        self.ds = torch.zeros(B, nd, **f64)
+        self.is_ = torch.zeros(B, ni, **i32)
+
+    @property
+    def x(self):
+        return self.v[:, 0]
+
+    @property
+    def status(self):
+        return self.is_[:, 1]
+
+    @property
+    def nit(self):
+        return self.is_[:, 10]
+
+    @property
+    def f(self):
+        return self.ds[:, 0]
+
+
+LBFGSB_STATUS = {0: "running", 1: "CONVERGENCE: NORM OF PROJECTED GRADIENT <= PGTOL",
+                 2: "CONVERGENCE: RELATIVE REDUCTION OF F <= FACTR*EPSMCH",
+                 3: "ABNORMAL: LINE SEARCH FAILED",
+                 4: "STOP: TOTAL NO. OF ITERATIONS REACHED LIMIT",
+                 5: "STOP: TOTAL NO. OF F,G EVALUATIONS EXCEEDS LIMIT",
+                 6: "ERROR: NON-FINITE VALUE OR LINE-SEARCH INPUT"}
+
+
 def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds=None,
                           upper_bounds=None, options=None, fixed_features=None, timeout_sec=None,
                           **kwargs):
     """Device-resident replacement of gen_candidates_scipy (generation/gen.py:
-    46-298): every restart runs its own projected
-    L-BFGS (history ``maxcor``, Armijo backtracking, scipy's default
-    ``ftol`` / ``gtol``) on the GPU.  One evaluation = one batched forward +
-    backward of the acquisition at all trial points + one bo_lbfgs_step launch;
-    the iterate, gradient and history never leave HBM, and the host reads the
-    (B,) status vector only every ``check_every`` evaluations.  ``use_graph``
-    (default True): the evaluation is captured once as a HIP graph and
-    replayed (botorch_amd.graphs), where the acquisition allows capture.
+    46-298).
 
-    ``maxiter`` bounds the function evaluations per restart (scipy's own
-    ``maxfun`` analogue); returns (candidates b x q x d, acq values b)."""
-    import ctypes
+    ``algorithm="lbfgsb"`` (default): every restart runs scipy 1.15's L-BFGS-B
+    (generalized Cauchy point, subspace minimisation, More-Thuente line search;
+    csrc/lbfgsb_core.h) on the GPU with scipy's options ``maxcor`` / ``ftol`` /
+    ``gtol`` / ``maxls`` / ``maxiter`` / ``maxfun`` and their defaults.  A
+    restart's trial points are scipy's on the same objective; the reference
+    runs ONE L-BFGS-B over the sum of the restarts' objectives, so its
+    iterates equal these at b = 1 and differ (same stationary points) at b > 1.
+    ``algorithm="projected"``: the round-1 projected L-BFGS with Armijo
+    backtracking (``maxiter`` bounds its evaluations).
 
+    One evaluation = one batched forward + backward of the acquisition at all
+    trial points + one step launch; iterates, gradients and histories never
+    leave HBM and the host reads the status vector every ``check_every``
+    evaluations.  ``use_graph`` (default True): the evaluation is captured once
+    as a HIP graph and replayed (botorch_amd.graphs) where the acquisition
+    allows capture.  Returns (candidates b x q x d, acq values b); an
+    OptimizationWarning is raised for restarts that end abnormally, as
+    gen_candidates_scipy does for scipy's failures."""
     from . import _lib, kernels
     from ._lib import check, lib
     if fixed_features:
         raise NotImplementedError("fixed_features is not supported by the device optimiser")
     options = dict(options or {})
-    maxiter = int(options.get("maxiter", 200))
+    algorithm = options.get("algorithm", "lbfgsb")
+    if algorithm not in ("lbfgsb", "projected"):
+        raise ValueError(f"algorithm={algorithm!r}: 'lbfgsb' or 'projected'")
     m = int(options.get("maxcor", 10))
     ftol = float(options.get("ftol", 1e7 * np.finfo(float).eps))  # scipy factr 1e7
     pgtol = float(options.get("gtol", 1e-5))
@@ -347,8 +406,17 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     if not X0.is_cuda:
         raise RuntimeError("gen_candidates_device runs on ROCm device tensors")
     shapeX = X0.shape
-    st = _LBFGSState(X0, m)
-    d = shapeX[-1]
+    lbfgsb = algorithm == "lbfgsb"
+    if lbfgsb:
+        maxiter = int(options.get("maxiter", 2000))  # gen_candidates_scipy's default
+        maxfun = int(options.get("maxfun", 15000))
+        maxls = int(options.get("maxls", 20))
+        max_evals = maxfun + maxls + 1
+        st = _LBFGSBState(X0, m)
+    else:
+        maxiter = int(options.get("maxiter", 200))
+        max_evals = maxiter + 1
+        st = _LBFGSState(X0, m)
     lo = (torch.as_tensor(lower_bounds, dtype=torch.float64, device=X0.device).expand(shapeX[-2:])
           .reshape(-1).contiguous() if lower_bounds is not None
           else torch.full((st.n,), -math.inf, dtype=torch.float64, device=X0.device))
@@ -356,7 +424,6 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
           .reshape(-1).contiguous() if upper_bounds is not None
           else torch.full((st.n,), math.inf, dtype=torch.float64, device=X0.device))
     stream = kernels._stream(X0.device)
-    P = kernels._p
     # one evaluation (forward + backward at all trial points) as a HIP graph
     # replay where the acquisition allows capture (the fused qEI / qLogEI
     # paths); the eager autograd evaluation otherwise
@@ -370,7 +437,8 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
             ga = None
             torch.cuda.synchronize(X0.device)
     t0 = time.monotonic()
-    for it in range(maxiter + 1):
+    it = 0
+    for it in range(max_evals):
         if ga is not None:
             v, g = ga(st.xt.view(shapeX))
             ft = (-v).reshape(-1).to(torch.float64).contiguous()
@@ -381,13 +449,20 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
             (gt,) = torch.autograd.grad(ft.sum(), Xt)
             ft = ft.detach().reshape(-1).to(torch.float64).contiguous()
             gt = gt.reshape(st.B, st.n).to(torch.float64).contiguous()
-        a = _lib.LbfgsStepArgs(B=st.B, n=st.n, m=m, x=st.x, f=st.f, g=st.g, xt=st.xt, ft=ft, gt=gt,
-                               d=st.d, alpha=st.alpha, S=st.S, Y=st.Y, rho=st.rho,
-                               hcount=st.hcount, hhead=st.hhead, status=st.status, nacc=st.nacc,
-                               lower=lo, upper=hi, c1=1e-4, ftol=ftol, pgtol=pgtol,
-                               min_alpha=1e-12)
-        check(lib().bo_lbfgs_step_v(ctypes.byref(a), stream), "lbfgs_step")
-        if (it + 1) % check_every == 0 or it == maxiter:
+        if lbfgsb:
+            a = _lib.LbfgsbArgs(B=st.B, n=st.n, m=m, maxls=maxls, maxiter=maxiter, maxfun=maxfun,
+                                ftol=ftol, pgtol=pgtol, lower=lo, upper=hi, xt=st.xt, ft=ft, gt=gt,
+                                v=st.v, iv=st.iv, ws=st.ws, wy=st.wy, mat=st.mat, ds=st.ds,
+                                is_=st.is_)
+            check(lib().bo_lbfgsb_step_v(ctypes.byref(a), stream), "lbfgsb_step")
+        else:
+            a = _lib.LbfgsStepArgs(B=st.B, n=st.n, m=m, x=st.x, f=st.f, g=st.g, xt=st.xt, ft=ft,
+                                   gt=gt, d=st.d, alpha=st.alpha, S=st.S, Y=st.Y, rho=st.rho,
+                                   hcount=st.hcount, hhead=st.hhead, status=st.status,
+                                   nacc=st.nacc, lower=lo, upper=hi, c1=1e-4, ftol=ftol,
+                                   pgtol=pgtol, min_alpha=1e-12)
+            check(lib().bo_lbfgs_step_v(ctypes.byref(a), stream), "lbfgs_step")
+        if (it + 1) % check_every == 0 or it == max_evals - 1:
             if ga is not None:
                 ga.check_status()
             if bool((st.status > 0).all()):
@@ -398,6 +473,12 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     cands = columnwise_clamp(cands, lower_bounds, upper_bounds)
     with torch.no_grad():
         acq = acquisition_function(cands)
+    if lbfgsb:
+        bad = (st.status == 3) | (st.status == 6)
+        if bool(bad.any()):
+            codes = sorted({int(s) for s in st.status[bad].tolist()})
+            warnings.warn(f"Optimization failed on the device for {int(bad.sum())} restart(s): "
+                          + "; ".join(LBFGSB_STATUS[c_] for c_ in codes), OptimizationWarning)
     gen_candidates_device.last_state = st
     gen_candidates_device.last_evals = it + 1
     return cands, acq

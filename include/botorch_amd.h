@@ -423,6 +423,28 @@ int bo_lbfgs_step(int B, int n, int m, double* x, double* f, double* g, double* 
                   const double* lower, const double* upper, double c1, double ftol,
                   double pgtol, double min_alpha, void* stream);
 
+/* One function evaluation of the device-resident multi-start L-BFGS-B: scipy
+ * 1.15's L-BFGS-B (generalized Cauchy point, subspace minimisation with the
+ * v3.0 projection, More-Thuente line search; the optimiser of
+ * gen_candidates_scipy, botorch/generation/gen.py:252-267) as a reverse-
+ * communication state machine, one 64-lane wave per restart.  The caller
+ * writes ft (B) / gt (B x n) = objective and gradient at the trial points xt
+ * (B x n); the call advances every restart to its next evaluation and
+ * overwrites xt.  Zeroed state (v, iv, ws, wy, mat, ds, is) means "start at
+ * xt".  ftol / pgtol / maxls / maxiter / maxfun are scipy's options of the same
+ * names (m = maxcor <= 20).  Per restart: v = V x n doubles, iv = IV x n ints,
+ * ws / wy = m x n, mat = MAT doubles, ds = DS doubles, is = IS ints, with
+ * (V, IV, MAT, DS, IS) from bo_lbfgsb_layout; is[1] is the status (0 running,
+ * 1 projected gradient <= pgtol, 2 relative reduction <= ftol, 3 abnormal line
+ * search, 4 maxiter, 5 maxfun, 6 error), is[10] the iterations, ds[0] f and
+ * v[0..n) x. */
+int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int maxfun, double ftol,
+                   double pgtol, const double* lower, const double* upper, double* xt,
+                   const double* ft, const double* gt, double* v, int* iv, double* ws, double* wy,
+                   double* mat, double* ds, int* is, void* stream);
+/* HOST: out[0..5] = V, IV, MAT, DS, IS, maximum m. */
+int bo_lbfgsb_layout(int* out);
+
 /* HOST function (plain host pointers; no GPU involved): exact non-dominated
  * box decompositions of S point sets Y (S x n x m, maximisation) w.r.t. ref (m),
  * FastNondominatedPartitioning per set (botorch/utils/multi_objective/
@@ -556,6 +578,20 @@ typedef struct BoLbfgsStepArgs { /* bo_lbfgs_step */
   double c1, ftol, pgtol, min_alpha;
 } BoLbfgsStepArgs;
 int bo_lbfgs_step_v(const BoLbfgsStepArgs* a, void* stream);
+
+typedef struct BoLbfgsbArgs { /* bo_lbfgsb_step */
+  BO_STRUCT_HEADER;
+  int32_t B, n, m, maxls, maxiter, maxfun;
+  double ftol, pgtol;
+  const double *lower, *upper;
+  double* xt;
+  const double *ft, *gt;
+  double* v;
+  int* iv;
+  double *ws, *wy, *mat, *ds;
+  int* is;
+} BoLbfgsbArgs;
+int bo_lbfgsb_step_v(const BoLbfgsbArgs* a, void* stream);
 
 /* HOST: sizeof the named record ("BoPostPartialsArgs", ...), -1 if unknown --
  * lets a binding check its declared layout once at load time. */

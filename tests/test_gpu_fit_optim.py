@@ -206,7 +206,7 @@ def test_device_lbfgs_qei_reaches_scipy_values():
         v0 = acqf(ics)
     assert (vd >= v0 - 1e-12).all()
     st = gen_candidates_device.last_state
-    assert (st.nacc.cpu() > 0).any()
+    assert (st.nit.cpu() > 0).any()
 
 
 def test_fit_rejects_nan_training_data():

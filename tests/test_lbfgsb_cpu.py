@@ -1,0 +1,122 @@
+"""The L-BFGS-B state machine of botorch_amd/csrc/lbfgsb_core.h (host build,
+tests/host/lbfgsb_host.cpp) against scipy 1.15's L-BFGS-B -- the optimiser
+botorch's gen_candidates_scipy calls (botorch/generation/gen.py:252-267).
+
+scipy is the oracle here: every point it evaluates (start, then each
+line-search trial) is recorded and the state machine must request the same
+points in the same order, stop with the same iteration count and return the
+same x.  The gfx950 kernel runs this code with 64 lanes
+(tests/test_gpu_lbfgsb.py)."""
+import numpy as np
+import pytest
+import torch
+
+from tests.lbfgsb_harness import HostLbfgsb, build_host, scipy_trials
+
+
+def _rosen(x):
+    f = np.sum(100.0 * (x[1:] - x[:-1] ** 2) ** 2 + (1 - x[:-1]) ** 2)
+    g = np.zeros_like(x)
+    g[:-1] += -400 * x[:-1] * (x[1:] - x[:-1] ** 2) - 2 * (1 - x[:-1])
+    g[1:] += 200 * (x[1:] - x[:-1] ** 2)
+    return f, g
+
+
+def _quad(A, b):
+    return lambda x: (0.5 * x @ A @ x - b @ x, A @ x - b)
+
+
+def _hartmann_batch(q):
+    from botorch_amd.test_functions import Hartmann
+    H = Hartmann(negate=False)
+
+    def fg(x):
+        X = torch.tensor(x.reshape(q, 6), requires_grad=True)
+        f = H(X).sum()
+        (g,) = torch.autograd.grad(f, X)
+        return f.item(), g.reshape(-1).numpy().astype(np.float64)
+    return fg
+
+
+def _compare(fg, x0, lo, hi, atol_pts=1e-9, **opt):
+    bounds = None if lo is None else list(zip(lo, hi))
+    sp, res = scipy_trials(fg, x0, bounds, **opt)
+    kw = dict(m=opt.get("maxcor", 10), maxiter=opt.get("maxiter", 15000), lower=lo, upper=hi)
+    hp, x, f, status, nit = HostLbfgsb(len(x0), **kw).run(fg, x0)
+    assert len(hp) == len(sp), (len(hp), len(sp))
+    for i, (a, b) in enumerate(zip(sp, hp)):
+        np.testing.assert_allclose(b, a, atol=atol_pts, rtol=0, err_msg=f"trial point {i}")
+    assert nit == res.nit
+    np.testing.assert_allclose(x, res.x, atol=atol_pts, rtol=0)
+    np.testing.assert_allclose(f, res.fun, rtol=1e-12, atol=1e-14)
+    msg = str(res.message)
+    expect = {1: "PROJECTED GRADIENT", 2: "RELATIVE REDUCTION", 4: "ITERATIONS REACHED LIMIT"}
+    assert expect[status] in msg, (status, msg)
+    return len(sp)
+
+
+def test_layout_matches_device_library():
+    import ctypes
+    from botorch_amd import _lib
+    host, dev = (ctypes.c_int * 6)(), (ctypes.c_int * 6)()
+    build_host().bo_lbfgsb_host_layout(host)
+    _lib.lib().bo_lbfgsb_layout(dev)
+    assert list(host) == list(dev)
+
+
+def test_box_rosenbrock_trial_points():
+    rng = np.random.default_rng(0)
+    n = 10
+    _compare(_rosen, rng.uniform(-1, 1, n), np.full(n, -1.5), np.full(n, 0.8))
+
+
+def test_unconstrained_rosenbrock_trial_points():
+    """No bounds: the Cauchy search is skipped once memory exists (mainlb's
+    `.not. cnstnd` branch).  Near the optimum the summation order of the dot
+    products shows after ~60 evaluations, so the points are compared there."""
+    rng = np.random.default_rng(0)
+    x0 = rng.uniform(-1, 1, 10)
+    sp, res = scipy_trials(_rosen, x0, None)
+    hp, x, f, status, nit = HostLbfgsb(10).run(_rosen, x0)
+    assert len(hp) == len(sp) and nit == res.nit and status == 2
+    for a, b in zip(sp[:50], hp[:50]):
+        np.testing.assert_allclose(b, a, atol=1e-9, rtol=0)
+    np.testing.assert_allclose(x, res.x, atol=1e-8)
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_quadratic_with_active_bounds(mixed):
+    rng = np.random.default_rng(0)
+    M = rng.standard_normal((12, 12))
+    A = M @ M.T + np.eye(12)
+    b = rng.standard_normal(12) * 5
+    if mixed:  # one-sided and absent bounds (nbd 0 / 1 / 3)
+        lo = np.full(12, -np.inf)
+        lo[:4] = 0.0
+        hi = np.full(12, np.inf)
+        hi[4:8] = 0.2
+        x0 = rng.uniform(0, 0.1, 12)
+    else:
+        lo, hi = np.zeros(12), np.ones(12)
+        x0 = rng.uniform(0, 1, 12)
+    _compare(_quad(A, b), x0, lo, hi)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_hartmann_batches_like_gen_candidates(seed):
+    """q x 6 Hartmann restarts in [0, 1]: many breakpoints, maxcor 3 / 5 / 10
+    (ring wrap-around) and the maxiter stop."""
+    rng = np.random.default_rng(100 + seed)
+    q = int(rng.integers(1, 5))
+    m = int(rng.choice([3, 5, 10]))
+    maxiter = int(rng.choice([5, 50, 200]))
+    n = 6 * q
+    _compare(_hartmann_batch(q), rng.uniform(0, 1, n), np.zeros(n), np.ones(n), atol_pts=1e-8,
+             maxcor=m, maxiter=maxiter)
+
+
+def test_start_at_stationary_point():
+    """A start whose projected gradient is already <= pgtol stops at once."""
+    hp, x, f, status, nit = HostLbfgsb(3, lower=np.zeros(3), upper=np.ones(3)).run(
+        lambda x: (float(np.sum((x - 0.5) ** 2)), 2 * (x - 0.5)), np.full(3, 0.5))
+    assert status == 1 and nit == 0 and len(hp) == 1
