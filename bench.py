@@ -359,15 +359,24 @@ def other_configs(dev, cpu=True):
         acq_o = qExpectedImprovement(mm, bfv, sampler=SobolQMCNormalSampler(torch.Size([SS]), seed=0))
         bnd = unit(6).to(dev)
         res = {}
-        for gname, gen in (("scipy", gen_candidates_scipy), ("device", gen_candidates_device)):
-            opts = {"seed": 0, "maxiter": 100}
+        for gname, gen, extra in (("scipy", gen_candidates_scipy, {}),
+                                  ("device", gen_candidates_device, {"algorithm": "lbfgsb"}),
+                                  ("device_projected", gen_candidates_device,
+                                   {"algorithm": "projected"})):
+            opts = {"seed": 0, "maxiter": 100, **extra}
             optimize_acqf(acq_o, bnd, qq, bb, raw_n, options=opts, gen_candidates=gen)  # warm-up
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             cand, val = optimize_acqf(acq_o, bnd, qq, bb, raw_n, options=opts, gen_candidates=gen)
             torch.cuda.synchronize()
             res[gname] = {"ms": 1e3 * (time.perf_counter() - t0), "best_acq": float(val)}
-        res["device_evals"] = int(gen_candidates_device.last_evals)
+            if gen is gen_candidates_device:
+                res[gname]["evals"] = int(gen_candidates_device.last_evals)
+                if extra["algorithm"] == "lbfgsb":
+                    stl = gen_candidates_device.last_state
+                    res[gname]["max_nit"] = int(stl.nit.max())
+                    u, cnt = torch.unique(stl.status.cpu(), return_counts=True)
+                    res[gname]["status_counts"] = {str(int(k)): int(v) for k, v in zip(u, cnt)}
         out[f"{tag}_optimize_acqf"] = {
             "config": f"{tag} optimize_acqf qEI q={qq} S={SS} restarts={bb} raw={raw_n} maxiter=100",
             **res, "speedup": res["scipy"]["ms"] / res["device"]["ms"]}

@@ -15,6 +15,12 @@
 // xt = x, so it costs nothing but its slot in the batched evaluation.
 #include "common.h"
 
+// No multiply-add contraction: scipy's L-BFGS-B rounds every product and sum
+// separately, and a fused a*b+c flips borderline line-search tests (measured:
+// one restart in 16 took another trial point after 14 evaluations).  The step
+// is latency-bound scalar work; the FMAs saved nothing.
+#pragma clang fp contract(off)
+
 #define BO_HD __device__
 #include "lbfgsb_core.h"
 

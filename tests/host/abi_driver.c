@@ -164,7 +164,10 @@ static int gpu_checks(void) {
       const double sol = fmin(fmax(target[i], 0.0), 1.0);
       err = fmax(err, fabs(x[b * N + i] - sol));
     }
-  if (err > 1e-8) FAIL("max |x - clamp(target)| = %g", err);
+  /* stopped by pgtol = 1e-5 or the relative reduction test: |x - x*| <= ~1e-5 */
+  for (int b = 0; b < B; ++b)
+    if (is[b * NIS + 1] != 1 && is[b * NIS + 1] != 2) FAIL("restart %d status %d", b, is[b * NIS + 1]);
+  if (err > 1e-4) FAIL("max |x - clamp(target)| = %g", err);
   printf("ok gpu lbfgsb: %d restarts, %d evaluations, max err %.2e\n", B, evals, err);
   hipFree(d_lo); hipFree(d_hi); hipFree(d_xt); hipFree(d_ft); hipFree(d_gt); hipFree(d_v);
   hipFree(d_iv); hipFree(d_ws); hipFree(d_wy); hipFree(d_mat); hipFree(d_ds); hipFree(d_is);

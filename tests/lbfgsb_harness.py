@@ -29,15 +29,14 @@ def build_host():
     if not os.path.exists(HOST_SO) or any(os.path.getmtime(s) > os.path.getmtime(HOST_SO)
                                           for s in _SRC):
         os.makedirs(os.path.dirname(HOST_SO), exist_ok=True)
-        subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", HOST_SO, _SRC[0]],
-                       check=True)
+        subprocess.run(["g++", "-O2", "-std=c++20", "-fPIC", "-shared", "-pthread", "-o", HOST_SO,
+                        _SRC[0]], check=True)
     lib = ctypes.CDLL(HOST_SO)
     P = ctypes.c_void_p
-    lib.bo_lbfgsb_host_step.restype = ctypes.c_int
-    lib.bo_lbfgsb_host_step.argtypes = [ctypes.c_int] * 5 + [ctypes.c_double] * 2 + [P, P, P,
-                                                                                      ctypes.c_double,
-                                                                                      P, P, P, P, P,
-                                                                                      P, P, P]
+    for fn in (lib.bo_lbfgsb_host_step, lib.bo_lbfgsb_host_step_lanes):
+        fn.restype = ctypes.c_int
+        fn.argtypes = ([ctypes.c_int] * 5 + [ctypes.c_double] * 2 + [P, P, P, ctypes.c_double]
+                       + [P] * 8)
     return lib
 
 
@@ -62,11 +61,13 @@ def scipy_trials(fun_and_grad, x0, bounds, maxiter=15000, maxcor=10, ftol=2.2204
 
 
 class HostLbfgsb:
-    """One restart of the host build; ``run`` returns (trial points, x, f, status, nit)."""
+    """One restart of the host build; ``run`` returns (trial points, x, f, status, nit).
+    ``lanes=True``: the 64-thread emulation of the kernel's wave."""
 
     def __init__(self, n, m=10, maxls=20, maxiter=15000, maxfun=15000,
-                 ftol=2.2204460492503131e-09, gtol=1e-05, lower=None, upper=None):
+                 ftol=2.2204460492503131e-09, gtol=1e-05, lower=None, upper=None, lanes=False):
         self.lib = build_host()
+        self._step = self.lib.bo_lbfgsb_host_step_lanes if lanes else self.lib.bo_lbfgsb_host_step
         lay = (ctypes.c_int * 6)()
         self.lib.bo_lbfgsb_host_layout(lay)
         nv, niv, nmat, nd, ni, _ = list(lay)
@@ -85,7 +86,7 @@ class HostLbfgsb:
     def step(self, xt, f, g):
         maxls, maxiter, maxfun, ftol, gtol = self.cfg
         g = np.ascontiguousarray(g, np.float64)
-        return self.lib.bo_lbfgsb_host_step(
+        return self._step(
             self.n, self.m, maxls, maxiter, maxfun, ftol, gtol, _p(self.lower), _p(self.upper),
             _p(xt), float(f), _p(g), _p(self.v), _p(self.iv), _p(self.ws), _p(self.wy),
             _p(self.mat), _p(self.ds), _p(self.is_))

@@ -120,3 +120,20 @@ def test_start_at_stationary_point():
     hp, x, f, status, nit = HostLbfgsb(3, lower=np.zeros(3), upper=np.ones(3)).run(
         lambda x: (float(np.sum((x - 0.5) ** 2)), 2 * (x - 0.5)), np.full(3, 0.5))
     assert status == 1 and nit == 0 and len(hp) == 1
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_wave_emulation_equals_scipy(seed):
+    """The 64-thread emulation of the kernel's wave (a barrier per sync, the
+    kernel's xor-butterfly reductions, NaN-poisoned shared record per call):
+    lane-parallel mistakes of the device build show here on the CPU."""
+    rng = np.random.default_rng(200 + seed)
+    q = 2
+    n = 6 * q
+    x0 = rng.uniform(0, 1, n)
+    fg = _hartmann_batch(q)
+    sp, res = scipy_trials(fg, x0, list(zip(np.zeros(n), np.ones(n))))
+    hp, x, f, status, nit = HostLbfgsb(n, lower=np.zeros(n), upper=np.ones(n), lanes=True).run(fg, x0)
+    assert len(hp) == len(sp) and nit == res.nit
+    for a, b in zip(sp, hp):
+        np.testing.assert_allclose(b, a, atol=1e-9, rtol=0)
