@@ -30,6 +30,7 @@ struct WaveCtx {
   static constexpr int NL = 64;
   int lane;
   __device__ void sync() { __syncthreads(); }
+  __device__ unsigned long long clock() { return wall_clock64(); }
   __device__ double sum(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
@@ -77,10 +78,17 @@ __global__ __launch_bounds__(64) void lbfgsb_kernel(bolb::Problem P, double* __r
                   is + b * bolb::ISLOTS};
   WaveCtx c{(int)threadIdx.x};
   bolb::Step<WaveCtx> st(c, P, R, S);
-  st.run();
+  st.run(P.prof ? P.prof + b * bolb::PROF_SLOTS : nullptr);
 }
 
 }  // namespace
+
+// phase clocks of the next launches (tools/prof_lbfgsb.py), B x PROF_SLOTS, or null
+static unsigned long long* g_lbfgsb_prof = nullptr;
+extern "C" int bo_lbfgsb_set_profile(unsigned long long* prof) {
+  g_lbfgsb_prof = prof;
+  return BO_OK;
+}
 
 extern "C" int bo_lbfgsb_layout(int* out) {
   out[0] = bolb::V_COUNT;
@@ -101,7 +109,7 @@ extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int m
   BO_CHECK_ARG(lower && upper && xt && ft && gt && v && iv && ws && wy && mat && ds && is,
                "bo_lbfgsb_step: null buffer");
   if (B == 0) return BO_OK;
-  bolb::Problem P{n, m, maxls, maxiter, maxfun, ftol, pgtol, lower, upper};
+  bolb::Problem P{n, m, maxls, maxiter, maxfun, ftol, pgtol, lower, upper, g_lbfgsb_prof};
   lbfgsb_kernel<<<B, 64, 0, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws, wy, mat, ds, is);
   BO_LAUNCH_CHECK();
   return BO_OK;

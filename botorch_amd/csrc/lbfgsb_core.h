@@ -70,7 +70,9 @@ struct Problem {
   double pgtol;  // scipy's gtol
   const double* lower;  // n; -inf / +inf for a missing bound
   const double* upper;
+  unsigned long long* prof;  // optional per-restart phase clocks (PROF_SLOTS each), or null
 };
+constexpr int PROF_SLOTS = 8;  // load, cauchy, freev, formk, cmprlb, subsm, line search, store
 
 struct Restart {   // global buffers of one restart
   double* xt;      // trial point (in: where f, g were evaluated; out: next point)
@@ -365,6 +367,15 @@ struct Step {
     iwhere = R.iv + (long)IV_WHERE * n;
     index = R.iv + (long)IV_INDEX * n;
     cnstnd = boxed = false;
+  }
+
+  unsigned long long tprev = 0;
+  unsigned long long* prof = nullptr;  // this restart's PROF_SLOTS clocks
+  BO_HD void tick(int phase) {  // attribute the time since the last tick to `phase`
+    if (!prof) return;
+    const unsigned long long now = c.clock();
+    if (c.lane == 0) prof[phase] += now - tprev;
+    tprev = now;
   }
 
   BO_HD double lo(int i) const { return P.lower[i]; }
@@ -849,14 +860,24 @@ struct Step {
         if (c.lane == 0) S.i[I_NFREE] = n;
         c.sync();
       } else {
-        if (cauchy()) {
+        tick(6);
+        const int info = cauchy();
+        tick(1);
+        if (info) {
           refresh();
           continue;
         }
         freev();
+        tick(2);
       }
       if (S.i[I_NFREE] != 0 && S.i[I_COL] != 0) {
-        if (formk() || cmprlb(unconstrained) || subsm()) {
+        int info = formk();
+        tick(3);
+        if (!info) info = cmprlb(unconstrained);
+        tick(4);
+        if (!info) info = subsm();
+        tick(5);
+        if (info) {
           refresh();
           continue;
         }
@@ -991,7 +1012,9 @@ struct Step {
   }
 
   // ---- the call: consume f, g at xt; run to the next evaluation ----
-  BO_HD void run() {
+  BO_HD void run(unsigned long long* prof_b) {
+    prof = prof_b;
+    if (prof) tprev = c.clock();
     // load the persistent record
     for (int k = c.lane; k < DSLOTS; k += C::NL) S.d[k] = R.ds[k];
     for (int k = c.lane; k < ISLOTS; k += C::NL) S.i[k] = R.is[k];
@@ -1021,6 +1044,7 @@ struct Step {
       if (!(gi - gi == 0.0)) finite = 0.0;
     }
     finite = c.min(finite);
+    tick(0);
     if (phase == PH_START) {
       for (int i = c.lane; i < n; i += C::NL) {
         x[i] = R.xt[i];
@@ -1108,6 +1132,7 @@ struct Step {
       }
     }
     c.sync();
+    tick(6);
     if (S.i[I_PHASE] == PH_STOP)
       for (int i = c.lane; i < n; i += C::NL) R.xt[i] = x[i];
     for (int k = c.lane; k < DSLOTS; k += C::NL) R.ds[k] = S.d[k];
@@ -1117,6 +1142,7 @@ struct Step {
       R.mat[MMAX * MMAX + k] = S.ss[k];
       R.mat[2 * MMAX * MMAX + k] = S.wt[k];
     }
+    tick(7);
   }
 };
 

@@ -444,6 +444,10 @@ int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int maxfun, doub
                    double* mat, double* ds, int* is, void* stream);
 /* HOST: out[0..5] = V, IV, MAT, DS, IS, maximum m. */
 int bo_lbfgsb_layout(int* out);
+/* Profiling aid: subsequent bo_lbfgsb_step launches add each restart's phase
+ * times (wall-clock ticks: load, Cauchy point, free set, formk, cmprlb, subsm,
+ * line search + update, store) into prof (B x 8, device memory); NULL stops. */
+int bo_lbfgsb_set_profile(unsigned long long* prof);
 
 /* HOST function (plain host pointers; no GPU involved): exact non-dominated
  * box decompositions of S point sets Y (S x n x m, maximisation) w.r.t. ref (m),

@@ -12,6 +12,7 @@ struct HostCtx {
   static constexpr int NL = 1;
   int lane = 0;
   void sync() {}
+  unsigned long long clock() { return 0; }
   double sum(double v) { return v; }
   double max(double v) { return v; }
   double min(double v) { return v; }
@@ -26,11 +27,11 @@ extern "C" int bo_lbfgsb_host_step(int n, int m, int maxls, int maxiter, int max
   if (n < 1 || m < 1 || m > bolb::MMAX) return -1;
   static bolb::Shared S;
   memset(&S, 0xff, sizeof S);  // LDS holds garbage at a kernel's start: NaN everywhere
-  bolb::Problem P{n, m, maxls, maxiter, maxfun, tol, pgtol, lower, upper};
+  bolb::Problem P{n, m, maxls, maxiter, maxfun, tol, pgtol, lower, upper, nullptr};
   bolb::Restart R{xt, ft, gt, v, iv, ws, wy, mat, ds, is};
   HostCtx c;
   bolb::Step<HostCtx> st(c, P, R, S);
-  st.run();
+  st.run(nullptr);
   return is[bolb::I_STATUS];
 }
 
@@ -63,6 +64,7 @@ struct LaneCtx {
   int lane;
   LaneShared* sh;
   void sync() { sh->bar.arrive_and_wait(); }
+  unsigned long long clock() { return 0; }
   template <class Op>
   double butterfly(double v, Op op) {
     for (int o = 32; o > 0; o >>= 1) {
@@ -102,14 +104,14 @@ extern "C" int bo_lbfgsb_host_step_lanes(int n, int m, int maxls, int maxiter, i
   static bolb::Shared S;
   memset(&S, 0xff, sizeof S);
   LaneShared sh;
-  bolb::Problem P{n, m, maxls, maxiter, maxfun, tol, pgtol, lower, upper};
+  bolb::Problem P{n, m, maxls, maxiter, maxfun, tol, pgtol, lower, upper, nullptr};
   bolb::Restart R{xt, ft, gt, v, iv, ws, wy, mat, ds, is};
   std::vector<std::thread> th;
   for (int l = 0; l < 64; ++l)
     th.emplace_back([&, l] {
       LaneCtx c{l, &sh};
       bolb::Step<LaneCtx> st(c, P, R, S);
-      st.run();
+      st.run(nullptr);
     });
   for (auto& t : th) t.join();
   return is[bolb::I_STATUS];
