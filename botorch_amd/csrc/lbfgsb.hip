@@ -55,6 +55,18 @@ struct WaveCtx {
   }
 };
 
+// Bytes of LDS a restart's working set takes (vectors, int vectors, S / Y ring).
+inline size_t staged_bytes(int n, int m) {
+  return sizeof(double) * ((size_t)bolb::V_COUNT * n + 2 * (size_t)m * n) +
+         sizeof(int) * (size_t)bolb::IV_COUNT * n;
+}
+constexpr size_t STAGE_LIMIT = 64 * 1024 - sizeof(bolb::Shared);  // dynamic LDS budget
+
+// One wave per restart.  With `staged`, the restart's vectors and ring are
+// copied into LDS for the launch (coalesced, once) and back at the end: every
+// dot product, breakpoint scan and formk product then reads LDS instead of
+// chaining dependent HBM / L2 loads, which set the duration of the slowest
+// restart (the launch's duration).
 __global__ __launch_bounds__(64) void lbfgsb_kernel(bolb::Problem P, double* __restrict__ xt,
                                                     const double* __restrict__ ft,
                                                     const double* __restrict__ gt,
@@ -62,31 +74,70 @@ __global__ __launch_bounds__(64) void lbfgsb_kernel(bolb::Problem P, double* __r
                                                     double* __restrict__ ws,
                                                     double* __restrict__ wy,
                                                     double* __restrict__ mat,
-                                                    double* __restrict__ ds, int* __restrict__ is) {
+                                                    double* __restrict__ ds, int* __restrict__ is,
+                                                    int staged) {
   __shared__ bolb::Shared S;
+  extern __shared__ double lds_dyn[];
   const long b = blockIdx.x;
   const long n = P.n, m = P.m;
+  const int lane = threadIdx.x;
+  double* gv = v + b * bolb::V_COUNT * n;
+  int* giv = iv + b * bolb::IV_COUNT * n;
+  double* gws = ws + b * m * n;
+  double* gwy = wy + b * m * n;
   bolb::Restart R{xt + b * n,
                   ft[b],
                   gt + b * n,
-                  v + b * bolb::V_COUNT * n,
-                  iv + b * bolb::IV_COUNT * n,
-                  ws + b * m * n,
-                  wy + b * m * n,
+                  gv,
+                  giv,
+                  gws,
+                  gwy,
                   mat + b * bolb::NMAT * bolb::MMAX * bolb::MMAX,
                   ds + b * bolb::DSLOTS,
                   is + b * bolb::ISLOTS};
-  WaveCtx c{(int)threadIdx.x};
+  const long nv = bolb::V_COUNT * n, nr = m * n, ni = bolb::IV_COUNT * n;
+  if (staged) {
+    double* lv = lds_dyn;
+    double* lws = lv + nv;
+    double* lwy = lws + nr;
+    int* liv = reinterpret_cast<int*>(lwy + nr);
+    for (long k = lane; k < nv; k += 64) lv[k] = gv[k];
+    for (long k = lane; k < nr; k += 64) {
+      lws[k] = gws[k];
+      lwy[k] = gwy[k];
+    }
+    for (long k = lane; k < ni; k += 64) liv[k] = giv[k];
+    __syncthreads();
+    R.v = lv;
+    R.ws = lws;
+    R.wy = lwy;
+    R.iv = liv;
+  }
+  WaveCtx c{lane};
   bolb::Step<WaveCtx> st(c, P, R, S);
   st.run(P.prof ? P.prof + b * bolb::PROF_SLOTS : nullptr);
+  if (staged) {
+    __syncthreads();
+    for (long k = lane; k < nv; k += 64) gv[k] = R.v[k];
+    for (long k = lane; k < nr; k += 64) {
+      gws[k] = R.ws[k];
+      gwy[k] = R.wy[k];
+    }
+    for (long k = lane; k < ni; k += 64) giv[k] = R.iv[k];
+  }
 }
 
 }  // namespace
 
 // phase clocks of the next launches (tools/prof_lbfgsb.py), B x PROF_SLOTS, or null
 static unsigned long long* g_lbfgsb_prof = nullptr;
+static int g_lbfgsb_unstaged = 0;  // 1: keep the working set in HBM (A/B timing)
 extern "C" int bo_lbfgsb_set_profile(unsigned long long* prof) {
   g_lbfgsb_prof = prof;
+  return BO_OK;
+}
+extern "C" int bo_lbfgsb_set_staging(int on) {
+  g_lbfgsb_unstaged = !on;
   return BO_OK;
 }
 
@@ -110,7 +161,10 @@ extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int m
                "bo_lbfgsb_step: null buffer");
   if (B == 0) return BO_OK;
   bolb::Problem P{n, m, maxls, maxiter, maxfun, ftol, pgtol, lower, upper, g_lbfgsb_prof};
-  lbfgsb_kernel<<<B, 64, 0, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws, wy, mat, ds, is);
+  const size_t bytes = staged_bytes(n, m);
+  const int staged = bytes <= STAGE_LIMIT && !g_lbfgsb_unstaged;
+  lbfgsb_kernel<<<B, 64, staged ? bytes : 0, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws, wy,
+                                                                  mat, ds, is, staged);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

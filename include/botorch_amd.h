@@ -448,6 +448,9 @@ int bo_lbfgsb_layout(int* out);
  * times (wall-clock ticks: load, Cauchy point, free set, formk, cmprlb, subsm,
  * line search + update, store) into prof (B x 8, device memory); NULL stops. */
 int bo_lbfgsb_set_profile(unsigned long long* prof);
+/* Timing aid: 0 keeps every restart's working set in HBM; 1 (default) stages it
+ * in LDS for each launch when it fits (8 (10 + 2m) n + 8 n bytes <= ~40 KB). */
+int bo_lbfgsb_set_staging(int on);
 
 /* HOST function (plain host pointers; no GPU involved): exact non-dominated
  * box decompositions of S point sets Y (S x n x m, maximisation) w.r.t. ref (m),

@@ -4,6 +4,7 @@
 evaluation kernels it sits between."""
 import os
 import sys
+import time
 
 import torch
 
@@ -29,21 +30,27 @@ for n, q, S, b, raw in ((1024, 8, 256, 64, 512), (4096, 16, 512, 128, 1024)):
     m.eval()
     acqf = qExpectedImprovement(m, float(Y.max()) - 0.3,
                                 sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
-    prof = torch.zeros(b, 8, dtype=torch.int64, device=dev)
-    for it in range(2):
-        if it == 1:  # phase clocks of the second run (100 MHz wall clock)
-            torch.cuda.synchronize()
-            lib().bo_lbfgsb_set_profile(prof.data_ptr())
-        c, v = optimize_acqf(acqf, unit.to(dev), q, b, raw, options={"seed": 0, "maxiter": 100},
-                             gen_candidates=gen_candidates_device)
-    torch.cuda.synchronize()
-    lib().bo_lbfgsb_set_profile(None)
-    ev = gen_candidates_device.last_evals
-    tot = prof.double().cpu() * 0.01 / ev  # 100 MHz wall clock -> us per launch, per restart
-    names = ["load", "cauchy", "freev", "formk", "cmprlb", "subsm", "linesearch+update", "store"]
-    worst = int(tot.sum(1).argmax())
-    print(f"n={n} q={q} b={b}: best {float(v):.8f}, evals {ev}; us per launch, restart mean: "
-          + ", ".join(f"{k} {x:.2f}" for k, x in zip(names, tot.mean(0).tolist()))
-          + f"; total mean {tot.sum(1).mean():.2f}, slowest restart {tot.sum(1).max():.2f} ("
-          + ", ".join(f"{k} {x:.2f}" for k, x in zip(names, tot[worst].tolist())) + ")",
-          flush=True)
+    for staged in (1, 0, 1):
+        lib().bo_lbfgsb_set_staging(staged)
+        prof = torch.zeros(b, 8, dtype=torch.int64, device=dev)
+        for it in range(2):
+            if it == 1:  # phase clocks of the second run (100 MHz wall clock)
+                torch.cuda.synchronize()
+                lib().bo_lbfgsb_set_profile(prof.data_ptr())
+                t0 = time.perf_counter()
+            c, v = optimize_acqf(acqf, unit.to(dev), q, b, raw, options={"seed": 0, "maxiter": 100},
+                                 gen_candidates=gen_candidates_device)
+        torch.cuda.synchronize()
+        wall = 1e3 * (time.perf_counter() - t0)
+        lib().bo_lbfgsb_set_profile(None)
+        ev = gen_candidates_device.last_evals
+        tot = prof.double().cpu() * 0.01 / ev  # 100 MHz wall clock -> us per launch, per restart
+        names = ["load", "cauchy", "freev", "formk", "cmprlb", "subsm", "linesearch+update",
+                 "store"]
+        worst = int(tot.sum(1).argmax())
+        print(f"n={n} q={q} b={b} staged={staged}: optimize_acqf {wall:.1f} ms, best {float(v):.8f},"
+              f" evals {ev}; us per launch, restart mean: "
+              + ", ".join(f"{k} {x:.2f}" for k, x in zip(names, tot.mean(0).tolist()))
+              + f"; total mean {tot.sum(1).mean():.2f}, slowest restart {tot.sum(1).max():.2f} ("
+              + ", ".join(f"{k} {x:.2f}" for k, x in zip(names, tot[worst].tolist())) + ")",
+              flush=True)
