@@ -501,9 +501,44 @@ def time_cholesky(Xtr, dev, reps=10):
     ts.sort()
     ms = ts[len(ts) // 2]
     fl = 2.0 * n ** 3 / 3.0
-    return {"n": n, "ms": ms, "flops": fl, "tflops": fl / (ms * 1e-3) / 1e12,
-            "frac_of_spec": fl / (ms * 1e-3) / 1e12 / 78.6,
-            "note": "factor + inverse, one persistent task-DAG launch, input in HBM"}
+    out = {"n": n, "ms": ms, "flops": fl, "tflops": fl / (ms * 1e-3) / 1e12,
+           "frac_of_spec": fl / (ms * 1e-3) / 1e12 / 78.6,
+           "note": "factor + inverse, one persistent task-DAG launch, input in HBM"}
+    # batched: nb independent factor + inverse problems in one launch
+    # (bo_cholesky_inverse_batched), the shapes of the path's multi-model fits
+    # and caches: C4's ModelListGP(3) at n = 2048, multi-output models at C3's n
+    batched = []
+    for nb, nn in ((3, 2048), (4, 4096), (8, 4096)):
+        npb = kernels.padded_order(nn)
+        Bb = torch.eye(npb, dtype=torch.float64, device=dev).repeat(nb, 1, 1)
+        for m in range(nb):  # the C3 kernel matrix scaled per member (distinct SPD inputs)
+            Bb[m, :nn, :nn] = torch.tril(A0[:nn, :nn]) * (1.0 + 0.1 * m)
+        Wb, Lb = torch.empty_like(Bb), torch.empty_like(Bb)
+        T = npb // 64
+        wk = torch.empty((16 + 4 * nb * T * T + 3) // 4 * 2, dtype=torch.float64, device=dev)
+        ib = torch.zeros(nb, dtype=torch.int32, device=dev)
+        tb = []
+        for r in range(reps + 2):
+            Wb.copy_(Bb)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            check(lib().bo_cholesky_inverse_batched(kernels._p(Wb), kernels._p(Lb), kernels._p(wk),
+                                                    nb, npb, kernels._p(ib),
+                                                    ctypes.c_void_p(st.cuda_stream)), "chol_b")
+            e1.record(st)
+            torch.cuda.synchronize(dev)
+            if r >= 2:
+                tb.append(e0.elapsed_time(e1))
+        if any(int(v) != 0 for v in ib.tolist()):
+            raise RuntimeError(f"bench batched Cholesky: info {ib.tolist()}")
+        tb.sort()
+        msb = tb[len(tb) // 2]
+        flb = nb * 2.0 * nn ** 3 / 3.0
+        batched.append({"nb": nb, "n": nn, "ms": msb, "tflops": flb / (msb * 1e-3) / 1e12,
+                        "frac_of_spec": flb / (msb * 1e-3) / 1e12 / 78.6})
+        del Bb, Wb, Lb
+    out["batched"] = batched
+    return out
 
 
 def time_gp_fit(Xtr, Ytr, dev, cpu=True):

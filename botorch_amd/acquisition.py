@@ -29,6 +29,7 @@ from .objective import (ConstrainedMCObjective, GenericMCObjective, IdentityMCOb
                         MCAcquisitionObjective, MCObjective, compute_best_feasible_objective,
                         compute_feasibility_indicator, compute_smoothed_feasibility_indicator,
                         repeat_to_match_aug_dim)
+from .models import prime_prediction_caches
 from .posteriors import FUSED_QMAX
 from .sampling import MCSampler, ShapeOnlyPosterior, SobolQMCNormalSampler, get_sampler
 
@@ -873,6 +874,7 @@ class _FusedQEHVI(torch.autograd.Function):
         need_grad = ctx.needs_input_grad[0]
         q = X3.shape[-2]
         means, Ls, saved = [], [], []
+        prime_prediction_caches(models)
         for mm in models:
             cache = mm.prediction_cache()
             ymean, ystd = mm.outcome_stats()
@@ -1037,6 +1039,7 @@ class _FusedQNEHVI(torch.autograd.Function):
         q = X3.shape[-2]
         means, Ls, Fs, saved = [], [], [], []
         pp = None
+        prime_prediction_caches(models)
         for t, mm in enumerate(models):
             cache = mm.prediction_cache()
             ymean, ystd = mm.outcome_stats()

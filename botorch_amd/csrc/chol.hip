@@ -27,7 +27,7 @@
 int bo_potrf_block128(double* A, int64_t lda, int64_t k0, double* Linv, int64_t ldi, int* info,
                       hipStream_t st);
 int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipStream_t st,
-                long long* trace = nullptr);
+                long long* trace = nullptr, int nb = 1);
 
 // BO_CHOL_LEGACY=1 selects the launch-per-step look-ahead factorisation below
 // (kept for A/B timing) instead of the persistent task-DAG kernel (chol_dag.hip).
@@ -274,6 +274,16 @@ int bo_gemm_f64(int ta, int tb, int M, int N, int K, double alpha, const double*
                 int64_t ldc, int64_t sC, int batch, int flags, void* stream) {
   return bo_gemm_f64_impl(ta, tb, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
                           batch, flags, as_stream(stream));
+}
+
+int bo_cholesky_inverse_batched(double* A, double* Linv, double* work, int nb, int64_t np,
+                                int* info, void* stream) {
+  BO_CHECK_ARG(nb >= 1 && nb <= 128 && np > 0 && np % NBO == 0,
+               "bo_cholesky_inverse_batched: %d matrices of order %lld (1..128, multiple of %d)",
+               nb, (long long)np, NBO);
+  BO_CHECK_ARG(((uintptr_t)A & 15) == 0 && ((uintptr_t)Linv & 15) == 0,
+               "bo_cholesky_inverse_batched: buffers must be 16-B aligned");
+  return bo_chol_dag(A, Linv, np, info, work, as_stream(stream), nullptr, nb);
 }
 
 int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* info,

@@ -825,11 +825,15 @@ __device__ bool batched_update(const Ctx& c, const Flags& f, int kb, int nk, int
   return true;
 }
 
+// nb > 1: nb independent matrices (A + m * np^2, Linv + m * np^2, info[m], flag
+// block m) share the launch; each task names its matrix in bits 9-15 of x, and
+// the queue interleaves the matrices' own queues, so one matrix's diagonal
+// chain runs while the others' bulk updates fill the CUs.
 __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, double* __restrict__ Linv,
                                                        int np, int T, const int4* __restrict__ tasks,
                                                        int ntasks, u32* __restrict__ flags,
                                                        int* __restrict__ info,
-                                                       long long* __restrict__ trace) {
+                                                       long long* __restrict__ trace, int nb) {
   __shared__ __attribute__((aligned(16))) double X0[TB * LP];
   __shared__ __attribute__((aligned(16))) double X1[TB * LP];
   __shared__ __attribute__((aligned(16))) double X2[TB * LP];  // batched update operands
@@ -853,6 +857,7 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
   c.rI = make_rsrc(Linv, bytes);
   u32* head = flags;
   u32* abortw = flags + 1;
+  const int fstride = 4 * T * T;  // flag words per matrix
   u32* fA = flags + NFLAG0;
   u32* fL = fA + T * T;
   u32* fX = fL + T * T;
@@ -860,6 +865,8 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
 #define F(arr, i, j) (arr + (i) * T + (j))
   Flags fl;
   fl.fA = fA; fl.fL = fL; fl.fX = fX; fl.fXd = fXd; fl.abortw = abortw; fl.T = T;
+  int cur = 0;          // matrix of the buffer resources / flags above
+  int* minfo = info;
 
   if (c.tid == 0) s_task = (int)__hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
@@ -868,7 +875,20 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
   Acc acc;
   while (t < ntasks) {
     const int4 tk = tasks[t];
-    const int type = tk.x & 0xff, fin = (tk.x >> 8) & 0xff, nk = tk.x >> 16;
+    const int type = tk.x & 0xff, fin = (tk.x >> 8) & 1, nk = tk.x >> 16;
+    const int mid = (tk.x >> 9) & 0x7f;
+    if (mid != cur) {  // rebind to matrix mid
+      cur = mid;
+      const size_t off = (size_t)mid * (size_t)np * (size_t)np;
+      c.rA = make_rsrc(A + off, bytes);
+      c.rI = make_rsrc(Linv + off, bytes);
+      fA = flags + NFLAG0 + (size_t)mid * fstride;
+      fL = fA + T * T;
+      fX = fL + T * T;
+      fXd = fX + T * T;
+      fl.fA = fA; fl.fL = fL; fl.fX = fX; fl.fXd = fXd;
+      minfo = info + mid;
+    }
     long long wsum = 0;
     long long phs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long* ph = trace ? phs : nullptr;
@@ -908,7 +928,7 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
         __syncthreads();
         long long* ct = trace ? trace + 4 * ntasks + 8 * k : nullptr;
         if (ct && c.tid == 0) ct[0] = wall_clock64();
-        potrf_trtri64(c, X0, X1, rinv, info, k * TB, Lcol, (lds_cnt_t*)&s_cnt, ct);
+        potrf_trtri64(c, X0, X1, rinv, minfo, k * TB, Lcol, (lds_cnt_t*)&s_cnt, ct);
         if (ct && c.tid == 0) ct[1] = wall_clock64();
         if (ct && c.tid == 0) ct[2] = wall_clock64();
         lds_to_tile(c, X0, c.rA, k, k);
@@ -985,7 +1005,8 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
     t = s_task;
     __syncthreads();
   }
-  if (c.tid == 0 && flag_load(abortw)) atomicExch(info, -1);
+  if (c.tid == 0 && flag_load(abortw))
+    for (int m = 0; m < nb; ++m) atomicExch(info + m, -1);
 #undef F
 }
 
@@ -1160,16 +1181,30 @@ std::vector<int4> build_tasks(int T) {
   return priority_order(v, T);
 }
 
-std::mutex g_tab_mu;
-std::map<std::pair<int, int>, DagTable> g_tabs;  // (device, T) -> table
+// nb matrices: the single queue repeated per matrix (id in bits 9-15 of x),
+// interleaved task by task.  Each matrix's tasks keep their order, and a task
+// only waits on tasks of its own matrix, so every dependency still precedes
+// its task in the merged queue.
+std::vector<int4> build_tasks_batched(int T, int nb) {
+  const std::vector<int4> one = build_tasks(T);
+  if (nb == 1) return one;
+  std::vector<int4> v;
+  v.reserve(one.size() * nb);
+  for (const int4& t : one)
+    for (int m = 0; m < nb; ++m) v.push_back(make_int4(t.x | (m << 9), t.y, t.z, t.w));
+  return v;
+}
 
-int dag_table(int T, DagTable** out) {
+std::mutex g_tab_mu;
+std::map<std::tuple<int, int, int>, DagTable> g_tabs;  // (device, T, nb) -> table
+
+int dag_table(int T, DagTable** out, int nb = 1) {
   int dev = 0;
   BO_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_tab_mu);
-  DagTable& tb = g_tabs[{dev, T}];
+  DagTable& tb = g_tabs[std::make_tuple(dev, T, nb)];
   if (!tb.dev) {
-    const std::vector<int4> v = build_tasks(T);
+    const std::vector<int4> v = build_tasks_batched(T, nb);
     int4* d = nullptr;
     BO_HIP(hipMalloc(&d, sizeof(int4) * v.size()));
     BO_HIP(hipMemcpy(d, v.data(), sizeof(int4) * v.size(), hipMemcpyHostToDevice));
@@ -1182,28 +1217,31 @@ int dag_table(int T, DagTable** out) {
 
 }  // namespace
 
-// In-place L = chol(A) (lower) and Linv = L^{-1} as one persistent launch.
-// np % 64 == 0; work: >= (16 + 4 (np/64)^2) * 4 bytes of scratch for the
-// counters; *info as in bo_cholesky_inverse (-1: the task DAG timed out).
+// In-place L = chol(A) (lower) and Linv = L^{-1} as one persistent launch, for
+// nb matrices stored back to back (np x np each).  np % 64 == 0; work: >=
+// (16 + 4 nb (np/64)^2) * 4 bytes of scratch for the counters; info[m] as in
+// bo_cholesky_inverse (-1: the task DAG timed out).
 int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipStream_t st,
-                long long* trace) {
+                long long* trace, int nb) {
   BO_CHECK_ARG(np > 0 && np % TB == 0 && np <= 16384, "bo_chol_dag: order %lld", (long long)np);
+  BO_CHECK_ARG(nb >= 1 && nb <= 128 && (trace == nullptr || nb == 1),
+               "bo_chol_dag: batch %d (1..128; traced launches single)", nb);
   const int T = (int)(np / TB);
   DagTable* tb = nullptr;
-  int s = dag_table(T, &tb);
+  int s = dag_table(T, &tb, nb);
   if (s) return s;
   int dev = 0, cus = 0;
   BO_HIP(hipGetDevice(&dev));
   BO_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const size_t fbytes = ((size_t)(NFLAG0 + 4 * T * T) * 4 + 15) / 16 * 16;
+  const size_t fbytes = ((size_t)(NFLAG0 + (size_t)nb * 4 * T * T) * 4 + 15) / 16 * 16;
   BO_HIP(hipMemsetAsync(work, 0, fbytes, st));
-  BO_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
-  BO_HIP(hipMemsetAsync(Linv, 0, sizeof(double) * np * np, st));
+  BO_HIP(hipMemsetAsync(info, 0, sizeof(int) * nb, st));
+  BO_HIP(hipMemsetAsync(Linv, 0, sizeof(double) * np * np * nb, st));
   // one workgroup per CU: two per CU (74 KB of LDS each fits) measured slower,
   // 2.35 -> 2.97 ms at n = 4096 -- the sc1 tile traffic, not latency, is the limit
   const int grid = cus < tb->n ? cus : tb->n;
   chol_dag_kernel<<<grid, 256, 0, st>>>(A, Linv, (int)np, T, tb->dev, tb->n, (u32*)work, info,
-                                          trace);
+                                          trace, nb);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
@@ -1218,7 +1256,7 @@ extern "C" int bo_probe_chol_dag(double* A, double* Linv, int64_t np, int* info,
   int s = dag_table((int)(np / TB), &tb);
   if (s) return s;
   *ntasks = tb->n;
-  return bo_chol_dag(A, Linv, np, info, work, as_stream(stream), trace);
+  return bo_chol_dag(A, Linv, np, info, work, as_stream(stream), trace, 1);
 }
 
 // Cycles (s_memtime ticks) per 16 x 16 diagonal factor + inverse on one wave:

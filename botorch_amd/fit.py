@@ -139,9 +139,25 @@ class _MultiLayout:
             p.set(v)
 
     def value_and_grad(self, x: np.ndarray):
+        """All members' K + s2 I factorised in ONE batched DAG launch
+        (kernels.build_gp_caches; bit-identical to per-member builds), then
+        each member's A^{-1}, data term and priors."""
+        xs = self._split(x)
+        caches = [None] * len(self.parts)
+        if not any(p.fixed for p in self.parts):
+            specs = []
+            for p, v in zip(self.parts, xs):
+                mm = p.model
+                noise, const, ls, os_ = _hyper_of(mm, v, p)
+                specs.append(dict(Xt=mm.train_inputs[0], y=mm.train_targets,
+                                  lengthscale=torch.as_tensor(ls, dtype=torch.float64,
+                                                              device=mm.train_inputs[0].device),
+                                  noise=float(noise), constant=float(const), kind=int(mm.kind),
+                                  outputscale=float(os_)))
+            caches = kernels.build_gp_caches(specs, check_nan=False)
         loss, grads = 0.0, []
-        for p, v in zip(self.parts, self._split(x)):
-            lt, gt = p.value_and_grad(v)
+        for p, v, cache in zip(self.parts, xs, caches):
+            lt, gt = mll_value_and_grad(p.model, v, p, cache=cache)
             loss += lt
             grads.append(gt)
         return loss, np.concatenate(grads)[self.perm]
@@ -156,18 +172,20 @@ def _layout(model):
 
 
 def mll_terms(Xt: torch.Tensor, y: torch.Tensor, ls_t: torch.Tensor, noise, const: float,
-              os_: float, kind: int):
+              os_: float, kind: int, cache=None):
     """Data term of [G] ExactMarginalLogLikelihood, ll = log N(y | c, K + s2 I)
     (no priors, not divided by n), and d ll / d [noise, constant,
     lengthscale_1..d, outputscale] (bo::mll's implementation).  ``noise`` may
     be an n-vector (fixed-noise likelihood: K + diag(noise); its gradient
-    entry is then meaningless)."""
+    entry is then meaningless).  ``cache``: the caches of exactly these
+    hyperparameters, already built (the batched multi-output closure)."""
     n, d = Xt.shape
     dev = Xt.device
     ls = ls_t.detach().cpu().numpy().astype(np.float64) if torch.is_tensor(ls_t) else np.asarray(ls_t)
     ls_t = torch.as_tensor(ls, dtype=torch.float64, device=dev)
-    cache = kernels.build_gp_cache(Xt, y, ls_t, noise, const, kind=kind, outputscale=os_,
-                                   check_nan=False)  # checked once in fit_gpytorch_mll_scipy
+    if cache is None:
+        cache = kernels.build_gp_cache(Xt, y, ls_t, noise, const, kind=kind, outputscale=os_,
+                                       check_nan=False)  # checked once in fit_gpytorch_mll_scipy
     # A^{-1} = L^{-T} L^{-1}, lower tiles (n^3/3 flops on the posterior kernel's
     # MFMA tiles, stream-K over the unequal k-ranges)
     Ainv = kernels.ainv(cache)
@@ -188,10 +206,19 @@ def mll_terms(Xt: torch.Tensor, y: torch.Tensor, ls_t: torch.Tensor, noise, cons
     return float(ll), g
 
 
-def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout):
+def _hyper_of(model: SingleTaskGP, x: np.ndarray, layout: _Layout):
+    d = model.train_inputs[0].shape[1]
+    o = layout.o
+    noise = 0.0 if layout.fixed else x[0]
+    return noise, x[o], x[o + 1:o + 1 + d], (x[o + 1 + d] if layout.has_os else 1.0)
+
+
+def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout, cache=None):
     """Loss = -(log N(y | c, K + s2 I) + log priors) / n and its gradient: the
     data term through bo::mll (torch.ops), the LogNormal priors on the host.
-    Fixed noise: K + diag(observed variances), no noise entry or prior."""
+    Fixed noise: K + diag(observed variances), no noise entry or prior.
+    ``cache``: prebuilt caches at x (the batched multi-output closure); the
+    data term then comes from fit.mll_terms on them directly."""
     from . import ops  # noqa: F401  (registers torch.ops.bo)
     layout.set(x)
     Xt = model.train_inputs[0]
@@ -204,10 +231,14 @@ def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout):
     ls = x[o + 1:o + 1 + d]
     os_ = x[o + 1 + d] if layout.has_os else 1.0
     ls_t = torch.as_tensor(ls, dtype=torch.float64, device=Xt.device)
-    llt, gt = torch.ops.bo.mll(Xt, y, ls_t, float(noise), float(const), float(os_),
-                               int(model.kind), nv)
-    ll = float(llt.item())
-    gall = gt.cpu().numpy()
+    if cache is not None:
+        ll, gall = mll_terms(Xt, y, ls_t, float(noise), float(const), float(os_), int(model.kind),
+                             cache=cache)
+    else:
+        llt, gt = torch.ops.bo.mll(Xt, y, ls_t, float(noise), float(const), float(os_),
+                                   int(model.kind), nv)
+        ll = float(llt.item())
+        gall = gt.cpu().numpy()
     g = np.zeros_like(x)
     if not layout.fixed:
         g[0] = gall[0]

@@ -226,6 +226,96 @@ def build_gp_cache(Xt, y, lengthscale, noise, constant, kind=_lib.RBF, outputsca
                    float(constant), L, Linv, U, beta, alpha, jit.value)
 
 
+def cholesky_inverse_batched(As: torch.Tensor):
+    """L = chol(A_m), Linv = L^{-1} of nb SPD matrices (nb x n x n) in ONE
+    persistent DAG launch (bo_cholesky_inverse_batched; bit-identical to nb
+    cholesky_inverse calls).  Returns (L, Linv, info list)."""
+    dev = _dev(As)
+    nb, n = As.shape[0], As.shape[-1]
+    np_ = padded_order(n)
+    W = torch.eye(np_, dtype=torch.float64, device=dev).repeat(nb, 1, 1)
+    W[:, :n, :n] = torch.tril(As)
+    Linv = torch.empty_like(W)
+    T = np_ // 64
+    work = torch.empty((16 + 4 * nb * T * T + 3) // 4 * 2, dtype=torch.float64, device=dev)
+    info = torch.zeros(nb, dtype=torch.int32, device=dev)
+    check(lib().bo_cholesky_inverse_batched(_p(W), _p(Linv), _p(work), nb, np_, _p(info),
+                                            _stream(dev)), "cholesky_inverse_batched")
+    status = info.cpu().tolist()
+    if any(s_ < 0 for s_ in status):
+        raise RuntimeError("bo_cholesky_inverse_batched: the Cholesky task DAG timed out")
+    return W[:, :n, :n], Linv[:, :n, :n], status
+
+
+def build_gp_caches(specs, check_nan: bool = True):
+    """GPCaches of several exact GPs whose training sets pad to one order (the
+    outputs of a batched multi-output SingleTaskGP, a ModelListGP's members):
+    their covariances are built side by side and factorised in ONE
+    bo_cholesky_inverse_batched launch, with one status read-back for all.  A
+    member whose first factorisation fails runs the jitter ladder on its own
+    (build_gp_cache: the reference's psd_safe_cholesky sequence from jitter 0).
+    Results are bit-identical to build_gp_cache per member.  specs: dicts of
+    build_gp_cache's arguments (Xt, y, lengthscale, noise, constant, kind,
+    outputscale); fixed-noise members or unequal orders fall back to
+    build_gp_cache per member."""
+    specs = list(specs)
+    if not specs:
+        return []
+    nps = {padded_order(sp["Xt"].shape[0]) for sp in specs}
+    fixed = any(torch.is_tensor(sp["noise"]) and sp["noise"].numel() > 1 for sp in specs)
+    if len(specs) == 1 or len(nps) != 1 or fixed or len(specs) > 128:
+        return [build_gp_cache(check_nan=check_nan, **sp) for sp in specs]
+    dev = _dev(specs[0]["Xt"])
+    np_ = nps.pop()
+    nb = len(specs)
+    f64 = dict(dtype=torch.float64, device=dev)
+    Lb = torch.empty(nb, np_, np_, **f64)
+    Linvb = torch.empty(nb, np_, np_, **f64)
+    T = np_ // 64
+    work = torch.empty((16 + 4 * nb * T * T + 3) // 4 * 2, **f64)
+    info = torch.zeros(nb, dtype=torch.int32, device=dev)
+    st = _stream(dev)
+    prep = []
+    for m, sp in enumerate(specs):
+        Xt = sp["Xt"].contiguous()
+        y = sp["y"].contiguous()
+        n, d = Xt.shape
+        if check_nan and (torch.isnan(Xt).any() or torch.isnan(y).any()):
+            from .exceptions import NanError
+            raise NanError("training data contains NaN")
+        ls = sp["lengthscale"].detach().reshape(-1).to(**f64).contiguous()
+        kind = sp.get("kind", _lib.RBF)
+        os_ = float(sp.get("outputscale", 1.0))
+        check(lib().bo_covar_matrix(kind, _p(Xt), n, _p(Xt), n, d, _p(ls), os_, float(sp["noise"]),
+                                    1, _p(Lb[m]), np_, np_, np_, st), "covar_matrix")
+        prep.append((Xt, y, ls, kind, os_, n, d))
+    check(lib().bo_cholesky_inverse_batched(_p(Lb), _p(Linvb), _p(work), nb, np_, _p(info), st),
+          "cholesky_inverse_batched")
+    status = info.cpu().tolist()  # the one read-back for all members
+    if any(s_ < 0 for s_ in status):
+        raise RuntimeError("bo_cholesky_inverse_batched: the Cholesky task DAG timed out")
+    out = []
+    for m, (sp, (Xt, y, ls, kind, os_, n, d)) in enumerate(zip(specs, prep)):
+        if status[m] != 0:  # not p.d. without jitter: the member's own ladder
+            out.append(build_gp_cache(check_nan=False, **sp))
+            continue
+        L, Linv = Lb[m], Linvb[m]
+        U = torch.empty(np_, np_, **f64)
+        beta = torch.empty(n, **f64)
+        alpha = torch.empty(n, **f64)
+        c = float(sp["constant"])
+        check(lib().bo_transpose(_p(Linv), _p(U), np_, np_, st), "transpose")
+        check(lib().bo_gemv(_p(Linv), np_, n, _p(y), c, _p(beta), st), "gemv")
+        check(lib().bo_gemv(_p(U), np_, n, _p(beta), 0.0, _p(alpha), st), "gemv")
+        Xs = torch.empty(n, DP, **f64)
+        if d <= DP:
+            check(lib().bo_scale_inputs(_p(Xt), n, d, _p(ls), ctypes.c_void_p(0), DP, _p(Xs), st),
+                  "scale_inputs")
+        out.append(GPCache(kind, n, d, np_, Xt, Xs, ls, os_, float(sp["noise"]), c, L, Linv, U,
+                           beta, alpha, 0.0))
+    return out
+
+
 @dataclass
 class PostPartials:
     B: int

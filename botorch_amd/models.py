@@ -439,6 +439,7 @@ class SingleTaskGP(Model):
         from .posteriors import GPyTorchPosterior, PosteriorList
         if self._is_multi_output:
             idx = output_indices if output_indices is not None else range(self._num_outputs)
+            prime_prediction_caches([self.models[i] for i in idx])
             post = PosteriorList(*[self.models[i].posterior(X, observation_noise=observation_noise)
                                    for i in idx])
             return post if posterior_transform is None else posterior_transform(post)
@@ -449,6 +450,43 @@ class SingleTaskGP(Model):
         if posterior_transform is not None:
             return posterior_transform(post)
         return post
+
+
+def prime_prediction_caches(models) -> None:
+    """Build the stale prediction caches of several single-output exact GPs
+    (a ModelListGP's members, the outputs of a multi-output SingleTaskGP, the
+    SAAS ensemble's members) with ONE batched factorisation
+    (kernels.build_gp_caches: the members' K + s2 I in one persistent DAG
+    launch, one status read-back); each model.prediction_cache() then returns
+    its cache without a launch.  The caches are bit-identical to the
+    per-model builds; fixed-noise members and unequal orders keep the
+    per-model path."""
+    from . import kernels
+    from .settings import propagate_grads
+    stale = []
+    for mm in models:
+        if not isinstance(mm, SingleTaskGP) or mm._is_multi_output:
+            continue
+        if isinstance(mm.likelihood, FixedNoiseGaussianLikelihood):
+            continue
+        if propagate_grads.on() and (mm.train_inputs[0].requires_grad
+                                     or mm.train_targets.requires_grad):
+            continue  # prediction_cache raises the reference's error
+        key = mm._key()
+        if mm._cache is not None and mm._cache_key == key:
+            continue
+        stale.append((mm, key))
+    if len(stale) < 2:
+        return
+    specs = []
+    for mm, _ in stale:
+        ls, os_, noise, c = mm.hyper()
+        specs.append(dict(Xt=mm.train_inputs[0].contiguous(), y=mm.train_targets.contiguous(),
+                          lengthscale=ls.contiguous(), noise=float(noise), constant=float(c),
+                          kind=int(mm.kind), outputscale=float(os_)))
+    for (mm, key), cache in zip(stale, kernels.build_gp_caches(specs)):
+        mm._cache = cache
+        mm._cache_key = key
 
 
 class ModelListGP(Model):
@@ -463,6 +501,7 @@ class ModelListGP(Model):
     def posterior(self, X, output_indices=None, observation_noise=False, posterior_transform=None):
         from .posteriors import PosteriorList
         idx = output_indices if output_indices is not None else range(len(self.models))
+        prime_prediction_caches([self.models[i] for i in idx])
         post = PosteriorList(*[self.models[i].posterior(X, observation_noise=observation_noise) for i in idx])
         if posterior_transform is not None:
             return posterior_transform(post)
@@ -542,6 +581,7 @@ class SaasFullyBayesianSingleTaskGP(Model):
         """The members' prediction caches stacked for the batched ensemble path:
         U (M x n x n, each L_m^{-T}), alpha (M x n), lengthscale (M x d),
         outputscale (M), constant (M); rebuilt whenever a member's cache is."""
+        prime_prediction_caches(self._members)
         caches = [m.prediction_cache() for m in self._members]
         key = tuple(id(c) for c in caches)
         if self._ens is None or self._ens_key != key:

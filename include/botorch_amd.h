@@ -128,6 +128,17 @@ int bo_covar_batched(int kind, const double* X1, int64_t s1o, int64_t s1i, int n
 int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* info,
                         void* stream);
 
+/* nb independent bo_cholesky_inverse problems in ONE persistent launch: A and
+ * Linv hold nb np x np matrices back to back, info nb device ints, work >=
+ * (16 + 4 nb (np/64)^2) * 4 bytes.  The matrices' task queues are interleaved,
+ * so one matrix's diagonal chain overlaps the others' MFMA updates.  Results
+ * are bit-identical to nb separate calls.  Replaces the per-output
+ * factorisations of a batched multi-output GP ([G] batched
+ * psd_safe_cholesky over the output batch, models/gpytorch.py:327-355) and of
+ * a ModelListGP's members (models/model_list_gp_regression.py). */
+int bo_cholesky_inverse_batched(double* A, double* Linv, double* work, int nb, int64_t np,
+                                int* info, void* stream);
+
 /* psd_safe_cholesky of one n x n matrix ([G] linear_operator, the ladder of
  * botorch/__init__.py:47): factor A + jitter I for jitter = 0, jitter0,
  * 10 jitter0, ... (max_tries increments).  L, Linv, work: np x np (identity

@@ -145,3 +145,20 @@ def test_projected_algorithm_still_available():
     assert c.shape == ics.shape and (c >= 0).all() and (c <= 1).all()
     with torch.no_grad():
         assert (v >= acqf(ics) - 1e-12).all()
+
+
+def test_restart_shards_reproduce_the_whole_batch():
+    """Per-restart L-BFGS-B makes the restart sharding of
+    distributed.optimize_acqf_sharded exact: the halves a 2-rank job optimises
+    return the candidates of the whole batch (the reference's joint L-BFGS-B
+    couples the restarts through one line search, so sharding it would change
+    its iterates)."""
+    from botorch_amd.optim import gen_candidates_device
+    acqf, bounds, ics = _qei_setup()
+    c_all, v_all = gen_candidates_device(ics, acqf, bounds[0], bounds[1])
+    halves = [gen_candidates_device(ics[s], acqf, bounds[0], bounds[1])
+              for s in (slice(0, 4), slice(4, 8))]
+    c_sh = torch.cat([h[0] for h in halves])
+    v_sh = torch.cat([h[1] for h in halves])
+    torch.testing.assert_close(c_sh, c_all, atol=1e-8, rtol=0)
+    torch.testing.assert_close(v_sh, v_all, atol=1e-12, rtol=1e-10)
