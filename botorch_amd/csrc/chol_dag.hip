@@ -42,6 +42,8 @@
 
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int TB = 64;  // tile
@@ -1185,13 +1187,30 @@ std::vector<int4> build_tasks(int T) {
 // interleaved task by task.  Each matrix's tasks keep their order, and a task
 // only waits on tasks of its own matrix, so every dependency still precedes
 // its task in the merged queue.
+// Matrix m's queue is offset by m * stagger * (queue length) / nb positions
+// (merge key: own position + offset, ties to the lower matrix), so one
+// matrix's chain-bound tail overlaps the next one's update-heavy opening
+// instead of all matrices opening together.
 std::vector<int4> build_tasks_batched(int T, int nb) {
   const std::vector<int4> one = build_tasks(T);
   if (nb == 1) return one;
+  double stagger = 0.0;
+  if (const char* e = getenv("BO_CHOL_BATCH_STAGGER")) stagger = atof(e);
+  const double shift = stagger * (double)one.size() / nb;
+  std::vector<std::pair<double, int4>> keyed;
+  keyed.reserve(one.size() * nb);
+  for (size_t i = 0; i < one.size(); ++i)
+    for (int m = 0; m < nb; ++m) {
+      const int4& t = one[i];
+      keyed.push_back({(double)i + m * shift, make_int4(t.x | (m << 9), t.y, t.z, t.w)});
+    }
+  std::stable_sort(keyed.begin(), keyed.end(),
+                   [](const std::pair<double, int4>& a, const std::pair<double, int4>& b) {
+                     return a.first < b.first;
+                   });
   std::vector<int4> v;
-  v.reserve(one.size() * nb);
-  for (const int4& t : one)
-    for (int m = 0; m < nb; ++m) v.push_back(make_int4(t.x | (m << 9), t.y, t.z, t.w));
+  v.reserve(keyed.size());
+  for (const auto& kv : keyed) v.push_back(kv.second);
   return v;
 }
 
