@@ -874,9 +874,9 @@ class _FusedQEHVI(torch.autograd.Function):
         need_grad = ctx.needs_input_grad[0]
         q = X3.shape[-2]
         means, Ls, saved = [], [], []
-        prime_prediction_caches(models)
-        for mm in models:
-            cache = mm.prediction_cache()
+        keys = prime_prediction_caches(models)
+        for mm, key in zip(models, keys):
+            cache = mm.prediction_cache(key=key)
             ymean, ystd = mm.outcome_stats()
             pp = kernels.post_partials(cache, X3.detach(), store_R=need_grad)
             out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
@@ -1039,9 +1039,9 @@ class _FusedQNEHVI(torch.autograd.Function):
         q = X3.shape[-2]
         means, Ls, Fs, saved = [], [], [], []
         pp = None
-        prime_prediction_caches(models)
+        keys = prime_prediction_caches(models)
         for t, mm in enumerate(models):
-            cache = mm.prediction_cache()
+            cache = mm.prediction_cache(key=keys[t])
             ymean, ystd = mm.outcome_stats()
             pp = kernels.post_partials(cache, X3.detach(), store_R=need_grad,
                                        cross=acqf._roots[t].Q_b)

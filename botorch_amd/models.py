@@ -405,8 +405,9 @@ class SingleTaskGP(Model):
         ps = [self.train_inputs[0], self.train_targets] + list(self.parameters())
         return tuple((p.data_ptr(), p._version) for p in ps)
 
-    def prediction_cache(self):
-        """Device caches of [G] exact prediction; rebuilt on any change."""
+    def prediction_cache(self, key=None):
+        """Device caches of [G] exact prediction; rebuilt on any change.
+        ``key``: this model's _key(), when the caller has just computed it."""
         from . import kernels
         if self._is_multi_output:
             raise UnsupportedError("a multi-output SingleTaskGP keeps one cache per output "
@@ -417,7 +418,8 @@ class SingleTaskGP(Model):
             raise UnsupportedError(
                 "settings.propagate_grads: posterior gradients to the training data are not "
                 "supported (the prediction caches are built without a backward to them)")
-        key = self._key()
+        if key is None:
+            key = self._key()
         if self._cache is None or self._cache_key != key:
             from . import ops  # noqa: F401  (torch.ops.bo registration)
             ls, os_, noise, c = self.hyper()
@@ -452,7 +454,7 @@ class SingleTaskGP(Model):
         return post
 
 
-def prime_prediction_caches(models) -> None:
+def prime_prediction_caches(models):
     """Build the stale prediction caches of several single-output exact GPs
     (a ModelListGP's members, the outputs of a multi-output SingleTaskGP, the
     SAAS ensemble's members) with ONE batched factorisation
@@ -460,11 +462,14 @@ def prime_prediction_caches(models) -> None:
     launch, one status read-back); each model.prediction_cache() then returns
     its cache without a launch.  The caches are bit-identical to the
     per-model builds; fixed-noise members and unequal orders keep the
-    per-model path."""
+    per-model path.  Returns each model's version key (None where not
+    computed), for prediction_cache(key=...): one key computation per model
+    and forward."""
     from . import kernels
     from .settings import propagate_grads
-    stale = []
+    stale, keys = [], []
     for mm in models:
+        keys.append(None)
         if not isinstance(mm, SingleTaskGP) or mm._is_multi_output:
             continue
         if isinstance(mm.likelihood, FixedNoiseGaussianLikelihood):
@@ -472,12 +477,12 @@ def prime_prediction_caches(models) -> None:
         if propagate_grads.on() and (mm.train_inputs[0].requires_grad
                                      or mm.train_targets.requires_grad):
             continue  # prediction_cache raises the reference's error
-        key = mm._key()
+        key = keys[-1] = mm._key()
         if mm._cache is not None and mm._cache_key == key:
             continue
         stale.append((mm, key))
     if len(stale) < 2:
-        return
+        return keys
     specs = []
     for mm, _ in stale:
         ls, os_, noise, c = mm.hyper()
@@ -487,6 +492,7 @@ def prime_prediction_caches(models) -> None:
     for (mm, key), cache in zip(stale, kernels.build_gp_caches(specs)):
         mm._cache = cache
         mm._cache_key = key
+    return keys
 
 
 class ModelListGP(Model):
@@ -581,8 +587,8 @@ class SaasFullyBayesianSingleTaskGP(Model):
         """The members' prediction caches stacked for the batched ensemble path:
         U (M x n x n, each L_m^{-T}), alpha (M x n), lengthscale (M x d),
         outputscale (M), constant (M); rebuilt whenever a member's cache is."""
-        prime_prediction_caches(self._members)
-        caches = [m.prediction_cache() for m in self._members]
+        keys = prime_prediction_caches(self._members)
+        caches = [m.prediction_cache(key=k) for m, k in zip(self._members, keys)]
         key = tuple(id(c) for c in caches)
         if self._ens is None or self._ens_key != key:
             n = caches[0].n
