@@ -468,14 +468,14 @@ def prime_prediction_caches(models):
     from . import kernels
     from .settings import propagate_grads
     stale, keys = [], []
+    pg = propagate_grads.on()
     for mm in models:
         keys.append(None)
         if not isinstance(mm, SingleTaskGP) or mm._is_multi_output:
             continue
         if isinstance(mm.likelihood, FixedNoiseGaussianLikelihood):
             continue
-        if propagate_grads.on() and (mm.train_inputs[0].requires_grad
-                                     or mm.train_targets.requires_grad):
+        if pg and (mm.train_inputs[0].requires_grad or mm.train_targets.requires_grad):
             continue  # prediction_cache raises the reference's error
         key = keys[-1] = mm._key()
         if mm._cache is not None and mm._cache_key == key:
