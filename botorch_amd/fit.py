@@ -101,7 +101,10 @@ class _Layout:
             m.covar_module.outputscale = float(x[o + 1 + self.d])
 
     def value_and_grad(self, x: np.ndarray):
-        return mll_value_and_grad(self.model, x, self)
+        # the closure reads x, not the module: the parameters are written once,
+        # at the optimum (fit_gpytorch_mll_scipy), not per evaluation (four
+        # constrained-parameter writes = a dozen small host-to-device copies)
+        return mll_value_and_grad(self.model, x, self, sync_model=False)
 
     def sample_priors(self, gen: torch.Generator) -> None:
         _sample_all_priors(self.model, self, gen)
@@ -157,7 +160,7 @@ class _MultiLayout:
             caches = kernels.build_gp_caches(specs, check_nan=False)
         loss, grads = 0.0, []
         for p, v, cache in zip(self.parts, xs, caches):
-            lt, gt = mll_value_and_grad(p.model, v, p, cache=cache)
+            lt, gt = mll_value_and_grad(p.model, v, p, cache=cache, sync_model=False)
             loss += lt
             grads.append(gt)
         return loss, np.concatenate(grads)[self.perm]
@@ -183,19 +186,43 @@ def mll_terms(Xt: torch.Tensor, y: torch.Tensor, ls_t: torch.Tensor, noise, cons
     dev = Xt.device
     ls = ls_t.detach().cpu().numpy().astype(np.float64) if torch.is_tensor(ls_t) else np.asarray(ls_t)
     ls_t = torch.as_tensor(ls, dtype=torch.float64, device=dev)
-    if cache is None:
+    fixed = torch.is_tensor(noise) and noise.numel() > 1
+    info = None
+    if cache is None and not fixed:
+        # optimistic: the jitter-free factorisation and everything after it are
+        # enqueued at once; its status comes back with the MLL sums (one
+        # device-to-host transfer per closure instead of two)
+        cache, info = kernels.build_gp_cache_optimistic(Xt, y, ls_t, float(noise), const,
+                                                        kind=kind, outputscale=os_)
+    elif cache is None:
         cache = kernels.build_gp_cache(Xt, y, ls_t, noise, const, kind=kind, outputscale=os_,
                                        check_nan=False)  # checked once in fit_gpytorch_mll_scipy
-    # A^{-1} = L^{-T} L^{-1}, lower tiles (n^3/3 flops on the posterior kernel's
-    # MFMA tiles, stream-K over the unequal k-ranges)
-    Ainv = kernels.ainv(cache)
-    st = kernels._stream(dev)
-    part = torch.empty(n, d + 5, dtype=torch.float64, device=dev)
-    check(lib().bo_mll_terms(kind, kernels._p(Xt.contiguous()), n, d, kernels._p(ls_t), os_,
-                             kernels._p(cache.L), kernels._p(Ainv), cache.np,
-                             kernels._p(cache.alpha), kernels._p(cache.beta), kernels._p(part), st),
-          "mll_terms")
-    s = part.sum(dim=0).cpu().numpy()
+
+    def _sums(cache, info):
+        # A^{-1} = L^{-T} L^{-1}, lower tiles (n^3/3 flops on the posterior
+        # kernel's MFMA tiles, stream-K over the unequal k-ranges)
+        Ainv = kernels.ainv(cache)
+        st = kernels._stream(dev)
+        part = torch.empty(n, d + 5, dtype=torch.float64, device=dev)
+        check(lib().bo_mll_terms(kind, kernels._p(Xt.contiguous()), n, d, kernels._p(ls_t), os_,
+                                 kernels._p(cache.L), kernels._p(Ainv), cache.np,
+                                 kernels._p(cache.alpha), kernels._p(cache.beta), kernels._p(part),
+                                 st), "mll_terms")
+        sums = part.sum(dim=0)
+        if info is not None:
+            sums = torch.cat([sums, info.to(torch.float64)])
+        return sums.cpu().numpy()
+
+    s = _sums(cache, info)
+    if info is not None:
+        status = int(s[-1])
+        s = s[:-1]
+        if status < 0:
+            raise RuntimeError("bo_cholesky_inverse: the Cholesky task DAG timed out")
+        if status != 0:  # not p.d. without jitter: the ladder, then the sums again
+            cache = kernels.build_gp_cache(Xt, y, ls_t, noise, const, kind=kind, outputscale=os_,
+                                           check_nan=False)
+            s = _sums(cache, None)
     quad, logdet_half, sum_alpha = s[d + 3], s[d + 2], s[d + 4]
     ll = -0.5 * quad - logdet_half - 0.5 * n * math.log(2 * math.pi)
     g = np.zeros(d + 3)
@@ -213,14 +240,18 @@ def _hyper_of(model: SingleTaskGP, x: np.ndarray, layout: _Layout):
     return noise, x[o], x[o + 1:o + 1 + d], (x[o + 1 + d] if layout.has_os else 1.0)
 
 
-def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout, cache=None):
+def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout, cache=None,
+                       sync_model: bool = True):
     """Loss = -(log N(y | c, K + s2 I) + log priors) / n and its gradient: the
     data term through bo::mll (torch.ops), the LogNormal priors on the host.
     Fixed noise: K + diag(observed variances), no noise entry or prior.
     ``cache``: prebuilt caches at x (the batched multi-output closure); the
-    data term then comes from fit.mll_terms on them directly."""
+    data term then comes from fit.mll_terms on them directly.  ``sync_model``
+    (default True): also write x into the model's parameters, as the
+    reference's closure leaves them."""
     from . import ops  # noqa: F401  (registers torch.ops.bo)
-    layout.set(x)
+    if sync_model:
+        layout.set(x)
     Xt = model.train_inputs[0]
     y = model.train_targets
     n, d = Xt.shape
@@ -230,11 +261,14 @@ def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout, cach
     const = x[o]
     ls = x[o + 1:o + 1 + d]
     os_ = x[o + 1 + d] if layout.has_os else 1.0
-    ls_t = torch.as_tensor(ls, dtype=torch.float64, device=Xt.device)
-    if cache is not None:
-        ll, gall = mll_terms(Xt, y, ls_t, float(noise), float(const), float(os_), int(model.kind),
-                             cache=cache)
+    if cache is not None or not sync_model:
+        # the fit's own closure: bo::mll's implementation with the host
+        # lengthscales (no device-to-host read of them)
+        ll, gall = mll_terms(Xt, y, np.asarray(ls, dtype=np.float64),
+                             nv if nv is not None else float(noise), float(const), float(os_),
+                             int(model.kind), cache=cache)
     else:
+        ls_t = torch.as_tensor(ls, dtype=torch.float64, device=Xt.device)
         llt, gt = torch.ops.bo.mll(Xt, y, ls_t, float(noise), float(const), float(os_),
                                    int(model.kind), nv)
         ll = float(llt.item())

@@ -247,6 +247,44 @@ def cholesky_inverse_batched(As: torch.Tensor):
     return W[:, :n, :n], Linv[:, :n, :n], status
 
 
+def build_gp_cache_optimistic(Xt, y, lengthscale, noise: float, constant: float, kind=_lib.RBF,
+                              outputscale=1.0):
+    """The first (jitter-free) attempt of build_gp_cache, enqueued without a
+    status read-back: returns (cache, info) with info a device int that the
+    caller reads together with its own results (the MLL closure: one
+    device-to-host transfer per evaluation).  info != 0 means K + s2 I was not
+    p.d. without jitter and the cache is invalid: the caller then reruns
+    build_gp_cache, whose ladder starts from jitter 0 as the reference's
+    psd_safe_cholesky does."""
+    dev = _dev(Xt, y, lengthscale)
+    Xt = Xt.contiguous()
+    y = y.contiguous()
+    n, d = Xt.shape
+    np_ = padded_order(n)
+    f64 = dict(dtype=torch.float64, device=dev)
+    L = torch.empty(np_, np_, **f64)
+    Linv = torch.empty(np_, np_, **f64)
+    U = torch.empty(np_, np_, **f64)  # the DAG's counters, then L^{-T}
+    beta = torch.empty(n, **f64)
+    alpha = torch.empty(n, **f64)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    ls = lengthscale.detach().reshape(-1).to(**f64).contiguous()
+    st = _stream(dev)
+    check(lib().bo_covar_matrix(kind, _p(Xt), n, _p(Xt), n, d, _p(ls), float(outputscale),
+                                float(noise), 1, _p(L), np_, np_, np_, st), "covar_matrix")
+    check(lib().bo_cholesky_inverse(_p(L), _p(Linv), _p(U), np_, _p(info), st), "cholesky_inverse")
+    check(lib().bo_transpose(_p(Linv), _p(U), np_, np_, st), "transpose")
+    check(lib().bo_gemv(_p(Linv), np_, n, _p(y), float(constant), _p(beta), st), "gemv")
+    check(lib().bo_gemv(_p(U), np_, n, _p(beta), 0.0, _p(alpha), st), "gemv")
+    Xs = torch.empty(n, DP, **f64)
+    if d <= DP:
+        check(lib().bo_scale_inputs(_p(Xt), n, d, _p(ls), ctypes.c_void_p(0), DP, _p(Xs), st),
+              "scale_inputs")
+    cache = GPCache(kind, n, d, np_, Xt, Xs, ls, float(outputscale), float(noise),
+                    float(constant), L, Linv, U, beta, alpha, 0.0)
+    return cache, info
+
+
 def build_gp_caches(specs, check_nan: bool = True):
     """GPCaches of several exact GPs whose training sets pad to one order (the
     outputs of a batched multi-output SingleTaskGP, a ModelListGP's members):

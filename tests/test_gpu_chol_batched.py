@@ -94,3 +94,36 @@ def test_multi_output_closure_and_posterior_use_the_batched_caches():
             mm.train_inputs[0], mm.train_targets, ls, noise, cst, kind=mm.kind, outputscale=os_)
         assert torch.equal(c.U, ref.U) and torch.equal(c.alpha, ref.alpha)
     assert post.mean.shape[-1] == 3
+
+
+@pytest.mark.parametrize("singular", [False, True])
+def test_optimistic_mll_closure_matches_the_ladder_path(singular):
+    """fit.mll_terms enqueues the jitter-free factorisation and reads its status
+    with the MLL sums; a K + s2 I that is not p.d. without jitter falls back to
+    build_gp_cache's ladder and must give exactly the ladder path's terms."""
+    import numpy as np
+    from botorch_amd import kernels
+    from botorch_amd.fit import mll_terms
+    g = torch.Generator().manual_seed(3)
+    X = torch.rand(300, 6, generator=g, dtype=torch.float64)
+    if singular:
+        X[150:] = X[:150]  # duplicated points
+    y = torch.sin(X.sum(-1))
+    Xd, yd = X.to(DEV), y.to(DEV)
+    ls = torch.full((6,), 0.4, dtype=torch.float64, device=DEV)
+    noise = 0.0 if singular else 1e-3
+    ll, grad = mll_terms(Xd, yd, ls, noise, 0.1, 1.3, 0)
+    with pytest.warns(Warning) if singular else _nullcontext():
+        ref_cache = kernels.build_gp_cache(Xd, yd, ls, noise, 0.1, outputscale=1.3)
+    assert (ref_cache.jitter > 0) == singular
+    ll2, grad2 = mll_terms(Xd, yd, ls, noise, 0.1, 1.3, 0, cache=ref_cache)
+    assert ll == ll2
+    np.testing.assert_array_equal(grad, grad2)
+
+
+class _nullcontext:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
