@@ -50,6 +50,7 @@ _SIGNATURES = {
     "bo_covar_blocks": (c_int, [c_int, _P, c_int64, c_int, c_int, _P, c_double, c_double, _P,
                                 _P]),
     "bo_gemv": (c_int, [_P, c_int64, c_int64, _P, c_double, _P, _P]),
+    "bo_gemv_tri": (c_int, [_P, c_int64, c_int64, _P, c_double, _P, c_int, _P]),
     "bo_scale_inputs": (c_int, [_P, c_int64, c_int, _P, _P, c_int, _P, _P]),
     "bo_gp_cache_build": (c_int, [c_int, _P, c_int64, c_int, _P, c_double, c_double, c_double,
                                   _P, _P, _P, _P, _P, _P, c_int, c_double, POINTER(c_double),

@@ -274,8 +274,9 @@ def build_gp_cache_optimistic(Xt, y, lengthscale, noise: float, constant: float,
                                 float(noise), 1, _p(L), np_, np_, np_, st), "covar_matrix")
     check(lib().bo_cholesky_inverse(_p(L), _p(Linv), _p(U), np_, _p(info), st), "cholesky_inverse")
     check(lib().bo_transpose(_p(Linv), _p(U), np_, np_, st), "transpose")
-    check(lib().bo_gemv(_p(Linv), np_, n, _p(y), float(constant), _p(beta), st), "gemv")
-    check(lib().bo_gemv(_p(U), np_, n, _p(beta), 0.0, _p(alpha), st), "gemv")
+    check(lib().bo_gemv_tri(_p(Linv), np_, n, _p(y), float(constant), _p(beta), 1, st),
+          "gemv_tri")
+    check(lib().bo_gemv_tri(_p(U), np_, n, _p(beta), 0.0, _p(alpha), 2, st), "gemv_tri")
     Xs = torch.empty(n, DP, **f64)
     if d <= DP:
         check(lib().bo_scale_inputs(_p(Xt), n, d, _p(ls), ctypes.c_void_p(0), DP, _p(Xs), st),
@@ -343,8 +344,8 @@ def build_gp_caches(specs, check_nan: bool = True):
         alpha = torch.empty(n, **f64)
         c = float(sp["constant"])
         check(lib().bo_transpose(_p(Linv), _p(U), np_, np_, st), "transpose")
-        check(lib().bo_gemv(_p(Linv), np_, n, _p(y), c, _p(beta), st), "gemv")
-        check(lib().bo_gemv(_p(U), np_, n, _p(beta), 0.0, _p(alpha), st), "gemv")
+        check(lib().bo_gemv_tri(_p(Linv), np_, n, _p(y), c, _p(beta), 1, st), "gemv_tri")
+        check(lib().bo_gemv_tri(_p(U), np_, n, _p(beta), 0.0, _p(alpha), 2, st), "gemv_tri")
         Xs = torch.empty(n, DP, **f64)
         if d <= DP:
             check(lib().bo_scale_inputs(_p(Xt), n, d, _p(ls), ctypes.c_void_p(0), DP, _p(Xs), st),

@@ -179,6 +179,11 @@ int bo_transpose(const double* A, double* B, int64_t n, int64_t ld, void* stream
 /* y[i] = sum_k M[i][k] (x[k] - xshift), i, k < n. */
 int bo_gemv(const double* M, int64_t ld, int64_t n, const double* x, double xshift, double* y,
             void* stream);
+/* bo_gemv for a triangular M (uplo 1: lower, 2: upper), reading only the
+ * triangle; bit-identical to bo_gemv on the same (zero-filled) matrix.  The
+ * cache builds' beta = L^{-1}(y - c) and alpha = L^{-T} beta. */
+int bo_gemv_tri(const double* M, int64_t ld, int64_t n, const double* x, double xshift, double* y,
+                int uplo, void* stream);
 
 /* Xs[i][t] = (X[i][t] - center[t]) / lengthscale[t] for t < d, 0 for d <= t < dp
  * (center may be NULL). */

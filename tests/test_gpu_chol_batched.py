@@ -127,3 +127,42 @@ class _nullcontext:
 
     def __exit__(self, *a):
         return False
+
+
+@pytest.mark.parametrize("uplo", [1, 2])
+def test_gemv_tri_bit_identical_to_gemv(uplo):
+    from botorch_amd import kernels
+    from botorch_amd._lib import lib
+    g = torch.Generator().manual_seed(5)
+    n, ld = 1000, 1024
+    M = torch.randn(ld, ld, generator=g, dtype=torch.float64)
+    M = (torch.tril(M) if uplo == 1 else torch.triu(M)).to(DEV)
+    x = torch.randn(ld, generator=g, dtype=torch.float64).to(DEV)
+    y0 = torch.empty(n, dtype=torch.float64, device=DEV)
+    y1 = torch.empty_like(y0)
+    st = kernels._stream(DEV)
+    assert lib().bo_gemv(kernels._p(M), ld, n, kernels._p(x), 0.25, kernels._p(y0), st) == 0
+    assert lib().bo_gemv_tri(kernels._p(M), ld, n, kernels._p(x), 0.25, kernels._p(y1), uplo,
+                             st) == 0
+    assert torch.equal(y0, y1)
+    torch.testing.assert_close(y1.cpu(), (M[:n, :n] @ (x[:n] - 0.25)).cpu(), rtol=1e-12,
+                               atol=1e-12)
+
+
+def test_covar_matrix_against_torch():
+    from botorch_amd import kernels
+    from botorch_amd._lib import lib
+    g = torch.Generator().manual_seed(6)
+    n, d, np_ = 700, 6, 768
+    X = torch.rand(n, d, generator=g, dtype=torch.float64)
+    ls = torch.rand(d, generator=g, dtype=torch.float64) + 0.2
+    K = torch.empty(np_, np_, dtype=torch.float64, device=DEV)
+    Xd, lsd = X.to(DEV), ls.to(DEV)
+    assert lib().bo_covar_matrix(0, kernels._p(Xd), n, kernels._p(Xd), n, d, kernels._p(lsd), 1.7,
+                                 0.01, 1, kernels._p(K), np_, np_, np_, kernels._stream(DEV)) == 0
+    Xs = X / ls
+    ref = 1.7 * torch.exp(-0.5 * torch.cdist(Xs, Xs) ** 2) + 0.01 * torch.eye(n, dtype=torch.float64)
+    Kc = K.cpu()
+    torch.testing.assert_close(Kc[:n, :n], torch.tril(ref), rtol=1e-12, atol=1e-13)
+    torch.testing.assert_close(Kc[n:, n:], torch.eye(np_ - n, dtype=torch.float64))
+    assert float(Kc[:n, n:].abs().max()) == 0.0
