@@ -47,49 +47,63 @@ constexpr int NBO = 128; // panel width = diagonal block of potrf.hip
 // leading dimension ldk, over a `rows x cols` padded extent (identity pad).
 // mode bit 1: zero the strict upper triangle (Cholesky input).
 constexpr int CM_DMAX = 256;  // dimensions staged in LDS by covar_matrix_kernel
+constexpr int CM_ROWS = 8;    // rows per workgroup
 
+// K[i][j] = outputscale * k(x_i, x_j) (+ diag_add on i == j), row-major with
+// leading dimension ldk, over a `rows x cols` padded extent (identity pad).
+// mode bit 1: zero the strict upper triangle (Cholesky input).
+// A workgroup takes CM_ROWS rows x 256 columns: the rows' inputs and the
+// reciprocal lengthscales sit in LDS (one divide per dimension per workgroup),
+// each thread reuses its column's input for all CM_ROWS rows, and each row's
+// 256 values leave as one 2 KB coalesced store.  (One row per workgroup with
+// per-element divides: 80 us for the n = 4096 Cholesky input.)
 template <int KIND>
 __global__ __launch_bounds__(256) void covar_matrix_kernel(
     const double* __restrict__ X1, int64_t n1, const double* __restrict__ X2, int64_t n2,
     int d, const double* __restrict__ ls, double outputscale, double diag_add, int mode,
     double* __restrict__ K, int64_t ldk, int64_t rows, int64_t cols) {
-  // the row's inputs and the reciprocal lengthscales in LDS: one divide per
-  // dimension per workgroup instead of d per element (the divides were most
-  // of the kernel: 80 us for the n = 4096 Cholesky input)
-  __shared__ double invl[CM_DMAX], xi[CM_DMAX];
+  __shared__ double invl[CM_DMAX], xi[CM_ROWS][CM_DMAX];
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t i = blockIdx.y;
-  const bool lds = d <= CM_DMAX;
-  if (lds) {
-    for (int t = threadIdx.x; t < d; t += blockDim.x) {
-      invl[t] = 1.0 / ls[t];
-      xi[t] = i < n1 ? X1[i * d + t] : 0.0;
-    }
-    __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.y * CM_ROWS;
+  for (int t = threadIdx.x; t < d; t += blockDim.x) invl[t] = 1.0 / ls[t];
+  __syncthreads();
+  for (int e = threadIdx.x; e < CM_ROWS * d; e += blockDim.x) {
+    const int r = e / d, t = e - r * d;
+    xi[r][t] = (i0 + r < n1) ? X1[(i0 + r) * d + t] * invl[t] : 0.0;
   }
-  if (j >= cols || i >= rows) return;
-  double v;
-  if (i >= n1 || j >= n2) {
-    v = (i == j) ? 1.0 : 0.0;
-  } else if ((mode & 1) && j > i) {
-    v = 0.0;
-  } else {
-    double d2 = 0.0;
-    if (lds) {
-      for (int t = 0; t < d; ++t) {
-        const double diff = (xi[t] - X2[j * d + t]) * invl[t];
-        d2 = fma(diff, diff, d2);
+  __syncthreads();
+  if (j >= cols) return;
+  const bool jv = j < n2;
+  double d2[CM_ROWS];
+#pragma unroll
+  for (int r = 0; r < CM_ROWS; ++r) d2[r] = 0.0;
+  // rows of this workgroup that need a kernel value at column j
+  const bool any = jv && i0 < n1 && !((mode & 1) && j > i0 + CM_ROWS - 1);
+  if (any) {
+    for (int t = 0; t < d; ++t) {
+      const double v = X2[j * d + t] * invl[t];
+#pragma unroll
+      for (int r = 0; r < CM_ROWS; ++r) {
+        const double diff = xi[r][t] - v;
+        d2[r] = fma(diff, diff, d2[r]);
       }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < CM_ROWS; ++r) {
+    const int64_t i = i0 + r;
+    if (i >= rows) break;
+    double val;
+    if (i >= n1 || !jv) {
+      val = (i == j) ? 1.0 : 0.0;
+    } else if ((mode & 1) && j > i) {
+      val = 0.0;
     } else {
-      for (int t = 0; t < d; ++t) {
-        const double diff = (X1[i * d + t] - X2[j * d + t]) / ls[t];
-        d2 = fma(diff, diff, d2);
-      }
+      val = outputscale * kernel_from_d2<KIND>(d2[r]);
+      if (i == j) val += diag_add;
     }
-    v = outputscale * kernel_from_d2<KIND>(d2);
-    if (i == j) v += diag_add;
+    K[i * ldk + j] = val;
   }
-  K[i * ldk + j] = v;
 }
 
 // Two-level batched covariance: batch z = o * inner + i reads its inputs at
@@ -269,9 +283,10 @@ int bo_covar_matrix(int kind, const double* X1, int64_t n1, const double* X2, in
                     int d, const double* lengthscale, double outputscale, double diag_add,
                     int mode, double* K, int64_t ldk, int64_t rows, int64_t cols, void* stream) {
   BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bo_covar_matrix: bad kind %d", kind);
-  BO_CHECK_ARG(d > 0 && ldk >= cols && rows >= n1 && cols >= n2, "bo_covar_matrix: bad shape");
+  BO_CHECK_ARG(d > 0 && d <= CM_DMAX && ldk >= cols && rows >= n1 && cols >= n2,
+               "bo_covar_matrix: bad shape (d = %d, at most %d)", d, CM_DMAX);
   if (rows == 0 || cols == 0) return BO_OK;
-  dim3 grid((unsigned)ceil_div(cols, 256), (unsigned)rows);
+  dim3 grid((unsigned)ceil_div(cols, 256), (unsigned)ceil_div(rows, CM_ROWS));
   hipStream_t st = as_stream(stream);
   if (kind == BO_RBF)
     covar_matrix_kernel<BO_RBF><<<grid, 256, 0, st>>>(X1, n1, X2, n2, d, lengthscale, outputscale, diag_add, mode, K, ldk, rows, cols);

