@@ -21,7 +21,9 @@
 // is latency-bound scalar work; the FMAs saved nothing.
 #pragma clang fp contract(off)
 
-#define BO_HD __device__
+// everything inlined into the kernel: a call keeps `this` (Step, Restart) on the
+// stack, and every field access becomes a scratch load (374 of them)
+#define BO_HD __device__ __attribute__((always_inline))
 #include "lbfgsb_core.h"
 
 namespace {

@@ -110,6 +110,7 @@ BO_HD inline int dpofa(double* a, int ld, int n) {
     double s = 0.0;
     for (int k = 0; k < j; ++k) {
       double t = a[k + j * ld];
+      #pragma unroll 4
       for (int i = 0; i < k; ++i) t -= a[i + k * ld] * a[i + j * ld];
       t /= a[k + k * ld];
       a[k + j * ld] = t;
@@ -128,6 +129,7 @@ BO_HD inline int dtrsl_t(const double* t, int ld, int n, double* b) {
   b[0] /= t[0];
   for (int j = 1; j < n; ++j) {
     double s = 0.0;
+    #pragma unroll 4
     for (int i = 0; i < j; ++i) s += t[i + j * ld] * b[i];
     b[j] = (b[j] - s) / t[j + j * ld];
   }
@@ -140,6 +142,7 @@ BO_HD inline int dtrsl_n(const double* t, int ld, int n, double* b) {
   b[n - 1] /= t[(n - 1) + (n - 1) * ld];
   for (int j = n - 2; j >= 0; --j) {
     const double temp = -b[j + 1];
+    #pragma unroll 4
     for (int i = 0; i <= j; ++i) b[i] += temp * t[i + (j + 1) * ld];
     b[j] /= t[j + j * ld];
   }
@@ -151,6 +154,7 @@ BO_HD inline int bmv(const double* sy, const double* wt, int col, const double* 
   p[col] = v[col];
   for (int i = 1; i < col; ++i) {
     double sum = 0.0;
+    #pragma unroll 4
     for (int k = 0; k < i; ++k) sum += sy[i + k * MMAX] * v[k] / sy[k + k * MMAX];
     p[col + i] = v[col + i] + sum;
   }
@@ -162,6 +166,7 @@ BO_HD inline int bmv(const double* sy, const double* wt, int col, const double* 
   for (int i = 0; i < col; ++i) p[i] = -p[i] / sqrt(sy[i + i * MMAX]);
   for (int i = 0; i < col; ++i) {
     double sum = 0.0;
+    #pragma unroll 4
     for (int k = i + 1; k < col; ++k) sum += sy[k + i * MMAX] * p[col + k] / sy[i + i * MMAX];
     p[i] += sum;
   }
@@ -173,6 +178,7 @@ BO_HD inline int formt(double* wt, const double* sy, const double* ss, int col, 
   for (int i = 1; i < col; ++i)
     for (int j = i; j < col; ++j) {
       double ddum = 0.0;
+      #pragma unroll 4
       for (int k = 0; k < i; ++k) ddum += sy[i + k * MMAX] * sy[j + k * MMAX] / sy[k + k * MMAX];
       wt[i + j * MMAX] = ddum + theta * ss[i + j * MMAX];
     }
@@ -651,20 +657,24 @@ struct Step {
       double s = 0.0;
       if (kind == 0) {  // Y' ZZ' Y
         const double *a = WY(i), *b = WY(j);
+        #pragma unroll 8  // loads issue ahead; the sum keeps its order
         for (int k = 0; k < nfree; ++k) s += a[index[k]] * b[index[k]];
         double v = s / theta;
         if (i == j) v += S.sy[i + i * MMAX];
         S.wn[j + i * M2] = v;
       } else if (kind == 1) {  // S' AA' S
         const double *a = WS(i), *b = WS(j);
+        #pragma unroll 8  // loads issue ahead; the sum keeps its order
         for (int k = nfree; k < n; ++k) s += a[index[k]] * b[index[k]];
         S.wn[(col + j) + (col + i) * M2] = s * theta;
       } else {  // L_a (i > j, active) / R_z (i <= j, free) of S' . Y
         const double *a = WS(i), *b = WY(j);
         if (i > j) {
+          #pragma unroll 8  // loads issue ahead; the sum keeps its order
           for (int k = nfree; k < n; ++k) s += a[index[k]] * b[index[k]];
           S.wn[j + (col + i) * M2] = -s;
         } else {
+          #pragma unroll 8  // loads issue ahead; the sum keeps its order
           for (int k = 0; k < nfree; ++k) s += a[index[k]] * b[index[k]];
           S.wn[j + (col + i) * M2] = s;
         }
@@ -678,6 +688,7 @@ struct Step {
         for (int is = col; is < 2 * col; ++is)
           for (int js = is; js < 2 * col; ++js) {
             double s = 0.0;
+            #pragma unroll 4
             for (int k = 0; k < col; ++k) s += S.wn[k + is * M2] * S.wn[k + js * M2];
             S.wn[is + js * M2] += s;
           }
