@@ -455,18 +455,25 @@ class SingleTaskGP(Model):
 
 
 def prime_prediction_caches(models):
-    """Build the stale prediction caches of several single-output exact GPs
+    """Build the missing prediction caches of several single-output exact GPs
     (a ModelListGP's members, the outputs of a multi-output SingleTaskGP, the
     SAAS ensemble's members) with ONE batched factorisation
     (kernels.build_gp_caches: the members' K + s2 I in one persistent DAG
     launch, one status read-back); each model.prediction_cache() then returns
-    its cache without a launch.  The caches are bit-identical to the
+    its cache without a launch.  When every model already holds a cache this
+    returns at once (a stale cache, after new hyperparameters, is rebuilt by
+    its own prediction_cache()).  The caches are bit-identical to the
     per-model builds; fixed-noise members and unequal orders keep the
     per-model path.  Returns each model's version key (None where not
     computed), for prediction_cache(key=...): one key computation per model
     and forward."""
     from . import kernels
     from .settings import propagate_grads
+    if all(getattr(mm, "_cache", None) is not None for mm in models):
+        # every model has a cache: a stale one (new hyperparameters) is rebuilt
+        # by its own prediction_cache(); this keeps the per-forward host cost
+        # of the common case (all fresh) at one attribute read per model
+        return [None] * len(models)
     stale, keys = [], []
     pg = propagate_grads.on()
     for mm in models:
