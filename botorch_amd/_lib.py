@@ -97,7 +97,7 @@ _SIGNATURES = {
     "bo_lbfgsb_step": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double, _P,
                                _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "bo_lbfgsb_layout": (c_int, [_P]),
-    "bo_lbfgsb_set_profile": (c_int, [_P]),
+    "bo_lbfgsb_set_profile": (c_int, [_P, c_int]),
     "bo_lbfgsb_set_staging": (c_int, [c_int]),
     "bo_nd_partition_host": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, POINTER(c_int64), _P,
                                      _P, c_int]),

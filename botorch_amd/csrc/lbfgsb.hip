@@ -15,6 +15,8 @@
 // xt = x, so it costs nothing but its slot in the batched evaluation.
 #include "common.h"
 
+#include <atomic>
+
 // No multiply-add contraction: scipy's L-BFGS-B rounds every product and sum
 // separately, and a fused a*b+c flips borderline line-search tests (measured:
 // one restart in 16 took another trial point after 14 evaluations).  The step
@@ -132,14 +134,18 @@ __global__ __launch_bounds__(64) void lbfgsb_kernel(bolb::Problem P, double* __r
 }  // namespace
 
 // phase clocks of the next launches (tools/prof_lbfgsb.py), B x PROF_SLOTS, or null
-static unsigned long long* g_lbfgsb_prof = nullptr;
-static int g_lbfgsb_unstaged = 0;  // 1: keep the working set in HBM (A/B timing)
-extern "C" int bo_lbfgsb_set_profile(unsigned long long* prof) {
-  g_lbfgsb_prof = prof;
+// (profiling aids: atomics, so a setter on one thread never tears a launch's read)
+static std::atomic<unsigned long long*> g_lbfgsb_prof{nullptr};
+static std::atomic<int> g_lbfgsb_prof_cap{0};   // restarts the buffer holds
+static std::atomic<int> g_lbfgsb_unstaged{0};   // 1: keep the working set in HBM (A/B timing)
+extern "C" int bo_lbfgsb_set_profile(unsigned long long* prof, int capacity) {
+  BO_CHECK_ARG(capacity >= 0, "bo_lbfgsb_set_profile: capacity %d", capacity);
+  g_lbfgsb_prof_cap.store(prof ? capacity : 0);
+  g_lbfgsb_prof.store(prof);
   return BO_OK;
 }
 extern "C" int bo_lbfgsb_set_staging(int on) {
-  g_lbfgsb_unstaged = !on;
+  g_lbfgsb_unstaged.store(!on);
   return BO_OK;
 }
 
@@ -162,9 +168,11 @@ extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int m
   BO_CHECK_ARG(lower && upper && xt && ft && gt && v && iv && ws && wy && mat && ds && is,
                "bo_lbfgsb_step: null buffer");
   if (B == 0) return BO_OK;
-  bolb::Problem P{n, m, maxls, maxiter, maxfun, ftol, pgtol, lower, upper, g_lbfgsb_prof};
+  // profile only launches the buffer can hold (B x PROF_SLOTS clocks)
+  unsigned long long* prof = B <= g_lbfgsb_prof_cap.load() ? g_lbfgsb_prof.load() : nullptr;
+  bolb::Problem P{n, m, maxls, maxiter, maxfun, ftol, pgtol, lower, upper, prof};
   const size_t bytes = staged_bytes(n, m);
-  const int staged = bytes <= STAGE_LIMIT && !g_lbfgsb_unstaged;
+  const int staged = bytes <= STAGE_LIMIT && !g_lbfgsb_unstaged.load();
   lbfgsb_kernel<<<B, 64, staged ? bytes : 0, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws, wy,
                                                                   mat, ds, is, staged);
   BO_LAUNCH_CHECK();

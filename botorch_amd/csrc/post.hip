@@ -51,6 +51,9 @@ constexpr int PLD = 144;  // LDS row pitch (doubles): 2 x 144 dwords = 32 mod 64
 constexpr int DP = 8;     // padded input dimension held in registers
 constexpr int kSlots = 512;            // resident workgroups: 256 CUs x 2 (launch bounds)
 constexpr int kTileDoubles = 32 * 64;  // one 16-row x 128-column R^T tile
+#ifndef KXT_K
+#define KXT_K 16  // training points per thread of kxt_build_kernel
+#endif
 
 // One kernel value k(x_i, x_k) from scaled coordinates (0 beyond n / invalid rows).
 template <int KIND, int ND>
@@ -437,14 +440,14 @@ __global__ __launch_bounds__(256) void kxt_build_kernel(const double* __restrict
                                                         int np, int nrows_pad, double outputscale,
                                                         double* __restrict__ Kt) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  const int k0 = blockIdx.y * 16;
+  const int k0 = blockIdx.y * KXT_K;
   const bool iv = i < nrows;
   double xi[ND];
 #pragma unroll
   for (int t = 0; t < ND; ++t) xi[t] = iv ? Xq[(int64_t)i * DP + t] : 0.0;
   if (i >= nrows_pad) return;
 #pragma unroll 4
-  for (int kk = 0; kk < 16; ++kk) {
+  for (int kk = 0; kk < KXT_K; ++kk) {
     const int k = k0 + kk;
     if (k < np) Kt[(int64_t)k * nrows_pad + i] = eval_kernel_row<KIND, ND>(xi, Xt, n, k, outputscale, iv);
   }
@@ -741,7 +744,7 @@ int bo_post_kxt(int kind, const double* Xq, int B, int q, int d, const double* X
   const int np = nC * PC;
   const int nrows = B * Qp;
   hipStream_t st = as_stream(stream);
-  const dim3 grid((unsigned)ceil_div(nrows_pad, 256), (unsigned)(np / 16));
+  const dim3 grid((unsigned)ceil_div(nrows_pad, 256), (unsigned)ceil_div(np, KXT_K));
 #define BO_KXT(KIND, ND)                                                                   \
   kxt_build_kernel<KIND, ND><<<grid, 256, 0, st>>>(Xq, nrows, Xt_scaled, (int)n, np, nrows_pad, \
                                                    outputscale, Kt)

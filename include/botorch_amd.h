@@ -460,10 +460,11 @@ int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int maxfun, doub
                    double* mat, double* ds, int* is, void* stream);
 /* HOST: out[0..5] = V, IV, MAT, DS, IS, maximum m. */
 int bo_lbfgsb_layout(int* out);
-/* Profiling aid: subsequent bo_lbfgsb_step launches add each restart's phase
- * times (wall-clock ticks: load, Cauchy point, free set, formk, cmprlb, subsm,
- * line search + update, store) into prof (B x 8, device memory); NULL stops. */
-int bo_lbfgsb_set_profile(unsigned long long* prof);
+/* Profiling aid: subsequent bo_lbfgsb_step launches of at most `capacity`
+ * restarts add each restart's phase times (wall-clock ticks: load, Cauchy
+ * point, free set, formk, cmprlb, subsm, line search + update, store) into prof
+ * (capacity x 8, device memory); larger launches are not profiled; NULL stops. */
+int bo_lbfgsb_set_profile(unsigned long long* prof, int capacity);
 /* Timing aid: 0 keeps every restart's working set in HBM; 1 (default) stages it
  * in LDS for each launch when it fits (8 (10 + 2m) n + 8 n bytes <= ~40 KB). */
 int bo_lbfgsb_set_staging(int on);

@@ -36,13 +36,13 @@ for n, q, S, b, raw in ((1024, 8, 256, 64, 512), (4096, 16, 512, 128, 1024)):
         for it in range(2):
             if it == 1:  # phase clocks of the second run (100 MHz wall clock)
                 torch.cuda.synchronize()
-                lib().bo_lbfgsb_set_profile(prof.data_ptr())
+                lib().bo_lbfgsb_set_profile(prof.data_ptr(), b)
                 t0 = time.perf_counter()
             c, v = optimize_acqf(acqf, unit.to(dev), q, b, raw, options={"seed": 0, "maxiter": 100},
                                  gen_candidates=gen_candidates_device)
         torch.cuda.synchronize()
         wall = 1e3 * (time.perf_counter() - t0)
-        lib().bo_lbfgsb_set_profile(None)
+        lib().bo_lbfgsb_set_profile(None, 0)
         ev = gen_candidates_device.last_evals
         tot = prof.double().cpu() * 0.01 / ev  # 100 MHz wall clock -> us per launch, per restart
         names = ["load", "cauchy", "freev", "formk", "cmprlb", "subsm", "linesearch+update",
