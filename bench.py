@@ -361,6 +361,8 @@ def other_configs(dev, cpu=True):
         res = {}
         for gname, gen, extra in (("scipy", gen_candidates_scipy, {}),
                                   ("device", gen_candidates_device, {"algorithm": "lbfgsb"}),
+                                  ("device_compaction", gen_candidates_device,
+                                   {"algorithm": "lbfgsb", "compact": True}),
                                   ("device_projected", gen_candidates_device,
                                    {"algorithm": "projected"})):
             opts = {"seed": 0, "maxiter": 100, **extra}
@@ -373,6 +375,7 @@ def other_configs(dev, cpu=True):
             if gen is gen_candidates_device:
                 res[gname]["evals"] = int(gen_candidates_device.last_evals)
                 if extra["algorithm"] == "lbfgsb":
+                    res[gname]["shrinks"] = list(gen_candidates_device.last_shrinks)
                     stl = gen_candidates_device.last_state
                     res[gname]["max_nit"] = int(stl.nit.max())
                     u, cnt = torch.unique(stl.status.cpu(), return_counts=True)

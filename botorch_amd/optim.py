@@ -341,6 +341,21 @@ class _LBFGSBState:
         self.ds = torch.zeros(B, nd, **f64)
         self.is_ = torch.zeros(B, ni, **i32)
 
+    _FIELDS = ("xt", "v", "iv", "ws", "wy", "mat", "ds", "is_")
+
+    def take(self, idx: torch.Tensor) -> "_LBFGSBState":
+        """The restarts idx as a compact state (copies; each restart's state is
+        self-contained, so the compact batch continues exactly)."""
+        sub = object.__new__(_LBFGSBState)
+        sub.B, sub.n, sub.m = int(idx.numel()), self.n, self.m
+        for f in self._FIELDS:
+            setattr(sub, f, getattr(self, f).index_select(0, idx).contiguous())
+        return sub
+
+    def put(self, idx: torch.Tensor, sub: "_LBFGSBState") -> None:
+        for f in self._FIELDS:
+            getattr(self, f).index_copy_(0, idx, getattr(sub, f))
+
     @property
     def x(self):
         return self.v[:, 0]
@@ -387,7 +402,12 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     leave HBM and the host reads the status vector every ``check_every``
     evaluations.  ``use_graph`` (default True): the evaluation is captured once
     as a HIP graph and replayed (botorch_amd.graphs) where the acquisition
-    allows capture.  Returns (candidates b x q x d, acq values b); an
+    allows capture.  ``compact`` (L-BFGS-B): at a status read
+    where at most half of the batch is still running (and at least
+    ``compact_min`` restarts have stopped), the running restarts continue as a
+    smaller batch (their states gathered, the graph re-captured for the new
+    shape), so stopped restarts no longer take slots in the evaluations.
+    Returns (candidates b x q x d, acq values b); an
     OptimizationWarning is raised for restarts that end abnormally, as
     gen_candidates_scipy does for scipy's failures."""
     from . import _lib, kernels
@@ -401,7 +421,7 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     m = int(options.get("maxcor", 10))
     ftol = float(options.get("ftol", 1e7 * np.finfo(float).eps))  # scipy factr 1e7
     pgtol = float(options.get("gtol", 1e-5))
-    check_every = int(options.get("check_every", 8))
+    check_every = int(options.get("check_every", 4 if algorithm == "lbfgsb" else 8))
     X0 = columnwise_clamp(initial_conditions, lower_bounds, upper_bounds).detach()
     if not X0.is_cuda:
         raise RuntimeError("gen_candidates_device runs on ROCm device tensors")
@@ -427,15 +447,24 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     # one evaluation (forward + backward at all trial points) as a HIP graph
     # replay where the acquisition allows capture (the fused qEI / qLogEI
     # paths); the eager autograd evaluation otherwise
-    ga = None
-    if options.get("use_graph", True):
+    use_graph = bool(options.get("use_graph", True))
+    compact = lbfgsb and bool(options.get("compact", False))
+    compact_min = int(options.get("compact_min", 8))
+
+    def _graph(state, shape):
+        if not use_graph:
+            return None
         from .graphs import GraphedAcquisition
         try:
-            ga = GraphedAcquisition(acquisition_function, st.xt.view(shapeX), with_grad=True,
-                                    warmup=1, check_each_call=False)
+            return GraphedAcquisition(acquisition_function, state.xt.view(shape), with_grad=True,
+                                      warmup=1, check_each_call=False)
         except RuntimeError:  # capture refused (e.g. a generic route with host reads)
-            ga = None
             torch.cuda.synchronize(X0.device)
+            return None
+
+    ga = _graph(st, shapeX)
+    full, active = st, None   # the whole batch; rows of `full` that `st` holds
+    shrinks = []
     t0 = time.monotonic()
     it = 0
     for it in range(max_evals):
@@ -465,10 +494,28 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
         if (it + 1) % check_every == 0 or it == max_evals - 1:
             if ga is not None:
                 ga.check_status()
-            if bool((st.status > 0).all()):
+            running = st.status <= 0  # 0 running; -1: the projected path's first call
+            n_run = int(running.sum())
+            if n_run == 0:
                 break
             if timeout_sec is not None and time.monotonic() - t0 > timeout_sec:
                 break
+            if compact and 2 * n_run <= st.B and st.B - n_run >= compact_min:
+                keep = running.nonzero().flatten()
+                if active is None:
+                    rows, sub = keep, st.take(keep)
+                else:
+                    rows = active.index_select(0, keep)
+                    full.put(active, st)
+                    sub = full.take(rows)
+                active, st = rows, sub
+                shrinks.append((it + 1, st.B))
+                shapeX = torch.Size((st.B,) + tuple(shapeX[1:]))
+                ga = _graph(st, shapeX)
+    if active is not None:
+        full.put(active, st)
+        st = full
+        shapeX = X0.shape
     cands = st.x.view(shapeX).to(initial_conditions.dtype)
     cands = columnwise_clamp(cands, lower_bounds, upper_bounds)
     with torch.no_grad():
@@ -481,6 +528,7 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
                           + "; ".join(LBFGSB_STATUS[c_] for c_ in codes), OptimizationWarning)
     gen_candidates_device.last_state = st
     gen_candidates_device.last_evals = it + 1
+    gen_candidates_device.last_shrinks = shrinks  # (evaluation, restarts kept)
     return cands, acq
 
 

@@ -162,3 +162,19 @@ def test_restart_shards_reproduce_the_whole_batch():
     v_sh = torch.cat([h[1] for h in halves])
     torch.testing.assert_close(c_sh, c_all, atol=1e-8, rtol=0)
     torch.testing.assert_close(v_sh, v_all, atol=1e-12, rtol=1e-10)
+
+
+def test_restart_compaction_is_exact():
+    """Stopped restarts leave the batch (their states set aside, the graph
+    re-captured for the smaller shape): every restart ends where it ends
+    without compaction."""
+    from botorch_amd.optim import gen_candidates_device
+    acqf, bounds, ics = _qei_setup()
+    c0, v0 = gen_candidates_device(ics, acqf, bounds[0], bounds[1], options={"compact": False})
+    s0 = gen_candidates_device.last_state.status.clone()
+    c1, v1 = gen_candidates_device(ics, acqf, bounds[0], bounds[1],
+                                   options={"compact": True, "compact_min": 1, "check_every": 2})
+    assert gen_candidates_device.last_shrinks, "no compaction happened"
+    assert torch.equal(gen_candidates_device.last_state.status, s0)
+    torch.testing.assert_close(c1, c0, atol=1e-8, rtol=0)
+    torch.testing.assert_close(v1, v0, atol=1e-12, rtol=1e-10)
