@@ -361,8 +361,8 @@ def other_configs(dev, cpu=True):
         res = {}
         for gname, gen, extra in (("scipy", gen_candidates_scipy, {}),
                                   ("device", gen_candidates_device, {"algorithm": "lbfgsb"}),
-                                  ("device_compaction", gen_candidates_device,
-                                   {"algorithm": "lbfgsb", "compact": True}),
+                                  ("device_no_compaction", gen_candidates_device,
+                                   {"algorithm": "lbfgsb", "compact": False}),
                                   ("device_projected", gen_candidates_device,
                                    {"algorithm": "projected"})):
             opts = {"seed": 0, "maxiter": 100, **extra}
