@@ -178,3 +178,32 @@ def test_restart_compaction_is_exact():
     assert torch.equal(gen_candidates_device.last_state.status, s0)
     torch.testing.assert_close(c1, c0, atol=1e-8, rtol=0)
     torch.testing.assert_close(v1, v0, atol=1e-12, rtol=1e-10)
+
+
+def test_kernel_unconstrained_and_fixed_variables():
+    """The kernel on the unconstrained branch (no bounds: the Cauchy search is
+    skipped once memory exists) and on fixed variables (l == u)."""
+    from tests.test_lbfgsb_cpu import _quad
+    rng = np.random.default_rng(0)
+    x0 = rng.uniform(-1, 1, 10)
+    inf = np.full(10, np.inf)
+    trials, x, f, status, nit = _drive([_rosen], x0[None], -inf, inf)
+    sp, res = scipy_trials(_rosen, x0, None)
+    assert len(trials[0]) == len(sp) and nit[0] == res.nit
+    for a, b in zip(sp[:50], trials[0][:50]):
+        np.testing.assert_allclose(b, a, atol=1e-9, rtol=0)
+    np.testing.assert_allclose(x[0], res.x, atol=1e-8, rtol=0)
+    rng = np.random.default_rng(11)
+    n = 10
+    M = rng.standard_normal((n, n))
+    A = M @ M.T + np.eye(n)
+    bb = rng.standard_normal(n) * 4
+    lo = np.array([0.3, 0.3, 0, 0, -np.inf, -np.inf, 0, -1, -np.inf, 0.5])
+    hi = np.array([0.3, 0.3, 1, 1, np.inf, 0.0, np.inf, 1, np.inf, 0.5])
+    x0 = np.clip(rng.uniform(-0.5, 0.5, n), lo, hi)
+    fg = _quad(A, bb)
+    trials, x, f, status, nit = _drive([fg], x0[None], lo, hi)
+    sp, res = scipy_trials(fg, x0, list(zip(lo, hi)))
+    assert len(trials[0]) == len(sp) and nit[0] == res.nit
+    np.testing.assert_allclose(x[0], res.x, atol=1e-10, rtol=0)
+    assert x[0][0] == 0.3 and x[0][1] == 0.3 and x[0][9] == 0.5

@@ -137,3 +137,17 @@ def test_wave_emulation_equals_scipy(seed):
     assert len(hp) == len(sp) and nit == res.nit
     for a, b in zip(sp, hp):
         np.testing.assert_allclose(b, a, atol=1e-9, rtol=0)
+
+
+def test_fixed_variables_and_mixed_bounds():
+    """l == u variables (scipy's iwhere = 3: never move) beside two-sided,
+    one-sided and absent bounds."""
+    rng = np.random.default_rng(11)
+    n = 10
+    M = rng.standard_normal((n, n))
+    A = M @ M.T + np.eye(n)
+    b = rng.standard_normal(n) * 4
+    lo = np.array([0.3, 0.3, 0, 0, -np.inf, -np.inf, 0, -1, -np.inf, 0.5])
+    hi = np.array([0.3, 0.3, 1, 1, np.inf, 0.0, np.inf, 1, np.inf, 0.5])
+    x0 = np.clip(rng.uniform(-0.5, 0.5, n), lo, hi)
+    _compare(_quad(A, b), x0, lo, hi)
