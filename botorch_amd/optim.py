@@ -408,7 +408,8 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     restarts continue as a smaller batch (their states gathered, the graph
     re-captured for the new shape), so stopped restarts no longer take slots
     in the evaluations; "auto" does so only when an evaluation has cost at
-    least ``compact_eval_ms`` (1 ms) on average.
+    least ``compact_eval_ms`` (2 ms) on average, and then also defers the
+    first graph capture to the first status read.
     Returns (candidates b x q x d, acq values b); an
     OptimizationWarning is raised for restarts that end abnormally, as
     gen_candidates_scipy does for scipy's failures."""
@@ -454,8 +455,9 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     compact_min = int(options.get("compact_min", 8))
     # "auto": shrink only when an evaluation costs at least this much (the
     # re-capture of the graph costs a few evaluations' worth: measured C3
-    # 55 -> 35 ms, C2 9.1 -> 14.5 ms with an unconditional shrink)
-    compact_eval_ms = float(options.get("compact_eval_ms", 1.0))
+    # 55 -> 35 ms, C2 9.1 -> 14.5 ms with an unconditional shrink; eager C3
+    # evaluations take 2.5-3 ms, C2 ones 0.7-1.2 ms)
+    compact_eval_ms = float(options.get("compact_eval_ms", 2.0))
 
     def _graph(state, shape):
         if not use_graph:
@@ -468,7 +470,11 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
             torch.cuda.synchronize(X0.device)
             return None
 
-    ga = _graph(st, shapeX)
+    # expensive evaluations (the auto-compaction regime): the first capture
+    # waits for the first status read, where the batch usually shrinks and is
+    # captured at its new shape anyway; cheap ones are captured at once
+    defer = use_graph and compact == "auto"
+    ga = None if defer else _graph(st, shapeX)
     full, active = st, None   # the whole batch; rows of `full` that `st` holds
     shrinks = []
     t0 = time.monotonic()
@@ -497,6 +503,11 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
                                    nacc=st.nacc, lower=lo, upper=hi, c1=1e-4, ftol=ftol,
                                    pgtol=pgtol, min_alpha=1e-12)
             check(lib().bo_lbfgs_step_v(ctypes.byref(a), stream), "lbfgs_step")
+        if defer and it == 0:
+            torch.cuda.synchronize(X0.device)  # one eager evaluation timed
+            if 1e3 * (time.monotonic() - t0) < compact_eval_ms:
+                defer = False
+                ga = _graph(st, shapeX)
         if (it + 1) % check_every == 0 or it == max_evals - 1:
             if ga is not None:
                 ga.check_status()
@@ -519,6 +530,10 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
                 active, st = rows, sub
                 shrinks.append((it + 1, st.B))
                 shapeX = torch.Size((st.B,) + tuple(shapeX[1:]))
+                ga = _graph(st, shapeX)
+                defer = False
+            elif defer:
+                defer = False
                 ga = _graph(st, shapeX)
     if active is not None:
         full.put(active, st)
