@@ -474,6 +474,7 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     # waits for the first status read, where the batch usually shrinks and is
     # captured at its new shape anyway; cheap ones are captured at once
     defer = use_graph and compact == "auto"
+    expensive = False  # the first evaluation took >= compact_eval_ms
     ga = None if defer else _graph(st, shapeX)
     full, active = st, None   # the whole batch; rows of `full` that `st` holds
     shrinks = []
@@ -505,7 +506,8 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
             check(lib().bo_lbfgs_step_v(ctypes.byref(a), stream), "lbfgs_step")
         if defer and it == 0:
             torch.cuda.synchronize(X0.device)  # one eager evaluation timed
-            if 1e3 * (time.monotonic() - t0) < compact_eval_ms:
+            expensive = 1e3 * (time.monotonic() - t0) >= compact_eval_ms
+            if not expensive:
                 defer = False
                 ga = _graph(st, shapeX)
         if (it + 1) % check_every == 0 or it == max_evals - 1:
@@ -517,8 +519,8 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
                 break
             if timeout_sec is not None and time.monotonic() - t0 > timeout_sec:
                 break
-            shrink = compact is True or (
-                compact == "auto" and 1e3 * (time.monotonic() - t0) / (it + 1) >= compact_eval_ms)
+            shrink = compact is True or (compact == "auto" and (
+                expensive or 1e3 * (time.monotonic() - t0) / (it + 1) >= compact_eval_ms))
             if shrink and 2 * n_run <= st.B and st.B - n_run >= compact_min:
                 keep = running.nonzero().flatten()
                 if active is None:
