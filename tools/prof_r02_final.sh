@@ -12,7 +12,7 @@ bash tools/gpu_run.sh test smoke || exit $?
 timeout -k 10 700 python3 bench.py > $O/bench_default.log 2>&1 || exit $?
 echo "bench: $(grep -c '^{' $O/bench_default.log) line(s)"
 B="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra --no-bwd"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_fwd -o run -- $B --no-fit > $O/stats_fwd.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_fwd -o run -- python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-extra --no-bwd --no-fit > $O/stats_fwd.log 2>&1 || exit $?
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_fit -o run -- $B > $O/stats_fit.log 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $B --no-fit > $O/fetch.log 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $B --no-fit > $O/write.log 2>&1 || exit $?
