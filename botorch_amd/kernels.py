@@ -295,14 +295,15 @@ def build_gp_caches(specs, check_nan: bool = True):
     (build_gp_cache: the reference's psd_safe_cholesky sequence from jitter 0).
     Results are bit-identical to build_gp_cache per member.  specs: dicts of
     build_gp_cache's arguments (Xt, y, lengthscale, noise, constant, kind,
-    outputscale); fixed-noise members or unequal orders fall back to
-    build_gp_cache per member."""
+    outputscale); fixed-noise members, unequal orders or members on different
+    devices fall back to build_gp_cache per member."""
     specs = list(specs)
     if not specs:
         return []
     nps = {padded_order(sp["Xt"].shape[0]) for sp in specs}
+    devs = {sp["Xt"].device for sp in specs}
     fixed = any(torch.is_tensor(sp["noise"]) and sp["noise"].numel() > 1 for sp in specs)
-    if len(specs) == 1 or len(nps) != 1 or fixed or len(specs) > 128:
+    if len(specs) == 1 or len(nps) != 1 or len(devs) != 1 or fixed or len(specs) > 128:
         return [build_gp_cache(check_nan=check_nan, **sp) for sp in specs]
     dev = _dev(specs[0]["Xt"])
     np_ = nps.pop()
