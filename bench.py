@@ -61,6 +61,14 @@ def flops_post_partials(B, q, n):
     return B * q * n * n + 2 * B * q * q * n + 2 * B * q * n
 
 
+def post_partials_bytes(B, q, n):
+    """Algorithmic HBM bytes of one post_partials launch: K*x^T read once
+    (B q n doubles), the upper triangle of U = L^{-T} read once (n^2/2
+    doubles), the per-strip partials written (n/128 strips x B x 16 x 16 +
+    B q doubles)."""
+    return 8 * (B * q * n + n * n // 2 + (n // 128) * (B * 256 + B * q))
+
+
 def pmc_traffic(kernel="post_partials_kernel<0, 6, false, false, true, false>"):
     """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 PMC
     summary (profiles/rNN/pmc_summary.json, written by tools/pmc_summary.py from
@@ -588,36 +596,150 @@ def time_gp_fit(Xtr, Ytr, dev, cpu=True):
     return out
 
 
+def _launch_ranks(n: int) -> int:
+    """``--gpus N`` without torchrun's environment: start the N ranks (one
+    process per GPU) under torch.distributed.run as a CHILD process -- this
+    process has not touched the GPU -- and return its exit code."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def timed_steps(step, steps, warmup, dist, sync, dev=None):
+    """W untimed steps, then exactly K timed steps bracketed by a barrier +
+    device sync on both sides; the MAX over ranks of the elapsed time (one
+    all-reduce on ``dev``, the device the process group reduces on)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def rehearse_cpu(args, ws, rank):
+    """BO_BENCH_REHEARSE=cpu: the multi-rank launch, the restart split, the
+    collectives and rank 0's report over gloo on the CPU, with a stub in place
+    of the acquisition forward (no GPU, no kernels: it measures nothing, the
+    line says so).  Exercised by tests/test_bench_launch_cpu.py."""
+    import torch.distributed as tdist
+    from botorch_amd.distributed import allgather_rows, shard_range
+    dist = None
+    if ws > 1:
+        tdist.init_process_group("gloo")
+        dist = tdist
+    strong = ws > 1 and not args.weak
+    r0, r1 = shard_range(RESTARTS, ws, rank) if strong else (0, RESTARTS)
+    best = torch.empty(1, dtype=torch.float64)
+
+    def step():
+        acq = torch.zeros(r1 - r0, dtype=torch.float64)   # stub of acqf(X[r0:r1])
+        if strong:
+            torch.amax(allgather_rows(acq, RESTARTS), dim=0, keepdim=True, out=best)
+        else:
+            torch.amax(acq, dim=0, keepdim=True, out=best)
+            if dist is not None:
+                dist.all_reduce(best, op=dist.ReduceOp.MAX)
+
+    elapsed = timed_steps(step, args.steps, args.warmup, dist, lambda: None)
+    if dist is not None:
+        assert dist.get_world_size() == args.gpus
+    if rank == 0:
+        print(json.dumps({"metric": "acq-evals/sec (q x restarts x MC), qEI forward",
+                          "value": None, "unit": "acq-evals/s", "n_gpus": ws,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": 1e3 * elapsed / args.steps,
+                          "scaling": "strong" if strong else "weak",
+                          "rehearsal": "cpu stub: launch, split and collectives only",
+                          "config": {"restarts_per_gpu": r1 - r0,
+                                     "parallelism": f"restart-sharded x{ws}"}}), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def verify_step(acqf, Xd, r0, Xtr, Ytr, Xc_local, best_f, k=8):
+    """Outside the timed region, on rank 0: the timed forward's values at k
+    t-batches spread over this rank's slice against the CPU restatement
+    (oracle/, the checker), at the MC bar of north_star (1e-2) and at 1e-7."""
+    from oracle.acquisition import qei
+    from oracle.gp import ExactGPOracle, GPHyper
+    from oracle.sampling import draw_sobol_normal_samples
+    b = Xd.shape[0]
+    idx = torch.linspace(0, b - 1, k).round().long()
+    with torch.no_grad():
+        got = acqf(Xd).cpu()[idx]
+    h = GPHyper(torch.full((D,), LENGTHSCALE, dtype=torch.float64), NOISE, CONSTANT)
+    ref = qei(ExactGPOracle(Xtr, Ytr, h), Xc_local[idx], draw_sobol_normal_samples(Q, MC, 0), best_f)
+    err = ((got - ref).abs() / ref.abs().clamp_min(1e-12)).max().item()
+    ok = bool(torch.allclose(got, ref, rtol=1e-7, atol=1e-12))
+    if not (ok and (ref > 0).all()):
+        raise SystemExit(f"bench: the timed forward disagrees with the oracle: {got} vs {ref}")
+    return {"t_batches": [int(r0 + i) for i in idx], "max_rel_err": err,
+            "min_value": float(ref.min()), "rtol": 1e-7}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="number of GPUs (ranks); without torchrun's env, N > 1 launches them")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fit", action="store_true", help="skip the GP-fit half of the metric")
     ap.add_argument("--no-bwd", action="store_true", help="skip the forward+backward timing")
-    ap.add_argument("--strong", action="store_true",
-                    help="shard the 512 restarts over the ranks (strong scaling)")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: each rank its own 512 restarts (weak scaling) as the headline")
+    ap.add_argument("--strong", action="store_true", help=argparse.SUPPRESS)  # the N > 1 default
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the other section-8 configurations (C2, C3 qNEI, C4, C5)")
     args = ap.parse_args()
-
+    if args.gpus is None:
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_launch_ranks(args.gpus))
     ws, rank, local = _dist_env()
+    if ws != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={ws}")
+    rehearse = os.environ.get("BO_BENCH_REHEARSE", "0")
+    if rehearse == "cpu":
+        return rehearse_cpu(args, ws, rank)
     # BO_BENCH_REHEARSE=1: every rank on cuda:0 over gloo -- a one-GPU rehearsal
     # of the multi-rank code path (barriers, max over ranks, rank-0 report);
     # never the measured configuration
-    rehearse = os.environ.get("BO_BENCH_REHEARSE", "0") == "1"
-    if rehearse:
+    if rehearse == "1":
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if ws > 1:
         import torch.distributed as dist
-        if rehearse:
+        if rehearse == "1":
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == args.gpus
+    # N > 1: the headline is north_star's C3 split -- ONE global draw of 512
+    # restarts sharded over the ranks (strong scaling); --weak: 512 per rank
+    strong = ws > 1 and not args.weak
 
     from botorch_amd import kernels
     from botorch_amd.acquisition import qExpectedImprovement
@@ -626,13 +748,17 @@ def main():
 
     from botorch_amd.distributed import allgather_rows, shard_range
     r0, r1 = 0, RESTARTS
-    if args.strong:  # one global draw, each rank its contiguous slice
-        Xtr, Ytr, Xc = build_problem(dev, RESTARTS, seed_offset=0)
+    Xtr, Ytr, Xc_all = build_problem(dev, RESTARTS, seed_offset=0)
+    Xc = Xc_all
+    if strong:  # one global draw, each rank its contiguous slice
         r0, r1 = shard_range(RESTARTS, ws, rank)
-        Xc = Xc[r0:r1]
-    else:
-        Xtr, Ytr, Xc = build_problem(dev, RESTARTS, seed_offset=rank)
-    best_f = Ytr.max().item()
+        Xc = Xc_all[r0:r1]
+    elif ws > 1:
+        Xc = build_problem(dev, RESTARTS, seed_offset=rank)[2]
+    # best_f 1.5 below the data maximum: with best_f =
+    # max Y no Sobol candidate improves on 4096 observations and every value
+    # would be exactly 0; the work per step does not depend on it
+    best_f = Ytr.max().item() - 1.5
     model = SingleTaskGP(Xtr.to(dev), Ytr.to(dev))
     model.covar_module.lengthscale = torch.full((1, D), LENGTHSCALE, dtype=torch.float64)
     model.likelihood.noise = torch.tensor([NOISE], dtype=torch.float64)
@@ -655,10 +781,10 @@ def main():
     kernels.TIMING_HOOK = hook
     best = torch.empty(1, dtype=torch.float64, device=dev)
 
-    def step(i=None):
+    def step():
         with torch.no_grad():
             acq = acqf(Xd)
-        if args.strong:
+        if strong:
             allv = allgather_rows(acq, RESTARTS)   # every rank: all 512 values
             torch.amax(allv, dim=0, keepdim=True, out=best)
             return allv
@@ -667,30 +793,17 @@ def main():
             dist.all_reduce(best, op=dist.ReduceOp.MAX)
         return acq
 
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+    # warm-up outside the event window, then the timed K steps
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
     timing[0] = True
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed = timed_steps(step, args.steps, 0, dist, sync, dev)
+    timing[0] = False
     ms_step = 1e3 * elapsed / args.steps
-    evals_per_step = Q * RESTARTS * MC * (1 if args.strong else ws)
+    evals_per_step = Q * RESTARTS * MC * (1 if strong else ws)
     value = evals_per_step * args.steps / elapsed
 
-    timing[0] = False
     kern_ms = sorted(a.elapsed_time(b) for a, b in zip(ev["post_partials_begin"], ev["post_partials_end"]))
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
     fl = flops_post_partials(r1 - r0, Q, N_TRAIN)
@@ -698,6 +811,23 @@ def main():
     peak = 78.6  # MI355X dense FP64 matrix TFLOP/s (MI355X_MICROARCH.md / SURVEY.md 8(d))
     peak_box = mfma_f64_ceiling(dev)
     traffic, traffic_src = pmc_traffic()
+    alg_bytes = post_partials_bytes(r1 - r0, Q, N_TRAIN)
+
+    weak = None
+    if strong:
+        # the weak line beside it: each rank its own 512 restarts (seed 1 + rank)
+        Xw = build_problem(dev, RESTARTS, seed_offset=rank)[2].to(dev)
+
+        def step_weak():
+            with torch.no_grad():
+                acq = acqf(Xw)
+            torch.amax(acq, dim=0, keepdim=True, out=best)
+            dist.all_reduce(best, op=dist.ReduceOp.MAX)
+
+        ew = timed_steps(step_weak, args.steps, args.warmup, dist, sync, dev)
+        weak = {"value": Q * RESTARTS * MC * ws * args.steps / ew,
+                "ms_per_step": 1e3 * ew / args.steps, "restarts_per_gpu": RESTARTS,
+                "note": "each rank its own 512 restarts, one all-reduce(MAX) per step"}
 
     # forward + backward (the optimize_acqf call pattern, gen.py:194-222)
     Xg = Xd.clone().requires_grad_(True)
@@ -731,6 +861,7 @@ def main():
             del gW
     gp_fit = None
     extra = None
+    check = None
     chol = time_cholesky(Xtr, dev) if rank == 0 else None
     if rank == 0 and ws == 1 and not args.no_extra:
         extra = other_configs(dev, cpu=not args.no_cpu_baseline)
@@ -738,8 +869,11 @@ def main():
         gp_fit = time_gp_fit(Xtr, Ytr, dev, cpu=(not args.no_cpu_baseline and ws == 1))
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and ws == 1:
-            cpu = cpu_baseline(Xtr, Ytr, Xc, best_f)
+        if not args.no_cpu_baseline:
+            # the CPU leg: the oracle checks the timed forward, then (N = 1) is timed
+            check = verify_step(acqf, Xd, r0, Xtr, Ytr, Xc, best_f)
+            if ws == 1:
+                cpu = cpu_baseline(Xtr, Ytr, Xc, best_f)
         line = {
             "metric": "acq-evals/sec (q x restarts x MC), qEI forward",
             "value": value,
@@ -749,15 +883,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: Hartmann6 on Sobol(seed 0) training inputs, "
-                    + ("Sobol(seed 1) candidates, rank slice" if args.strong
+                    + ("Sobol(seed 1) candidates, rank slice" if strong
                        else "Sobol(seed 1+rank) candidates"),
             "config": {"workload": ("C3 qEI forward: SingleTaskGP n=4096 d=6, q=16, "
-                                    + ("512 restarts sharded over the GPUs" if args.strong
-                                       else "512 restarts/GPU") + ", 512 Sobol MC samples"),
+                                    + ("512 restarts sharded over the GPUs" if strong
+                                       else "512 restarts/GPU") + ", 512 Sobol MC samples, "
+                                    "best_f = max(Y) - 1.5"),
                        "n": N_TRAIN, "d": D, "q": Q, "restarts_per_gpu": r1 - r0, "mc": MC,
                        "parallelism": f"restart-sharded x{ws}"},
             "roofline": {"bound": "mfma", "kernel": "post_partials_kernel",
@@ -766,8 +901,12 @@ def main():
                          "frac_of_measured": achieved / peak_box if peak_box else None,
                          "traffic": traffic,
                          "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                         "algorithmic_bytes": alg_bytes,
+                         "traffic_ratio": traffic / alg_bytes if traffic else None,
                          "kernel_ms": kern_avg_ms, "flops_per_launch": fl},
             "cpu_baseline": cpu,
+            "check": check,
+            "weak": weak,
             "fwd_bwd": fwd_bwd,
             "strong_scaling_projection": strong_proj,
             "cholesky": chol,

@@ -1197,3 +1197,72 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
         X3 = X.reshape(-1, q, d)
         acq = _FusedQNEHVI.apply(X3, self)
         return acq.reshape(batch) + self._prev_nehvi.to(acq)
+
+
+class FixedFeatureAcquisitionFunction(AcquisitionFunction):
+    """acquisition/fixed_feature.py:54-200: the base acquisition over the full
+    d-dim input, evaluated on X of dim d' = d - d_f with the ``columns`` filled
+    from ``values``.  The optimisers use it to drop fixed features from the
+    search space (generation/utils.py:102-196).  Filling the columns is one
+    concatenation and one column gather on the device, so the fused forward of
+    the base acquisition (and its HIP-graph capture) is unchanged."""
+
+    def __init__(self, acq_function: AcquisitionFunction, d: int, columns: List[int], values):
+        nn.Module.__init__(self)
+        self.acq_func = acq_function
+        self.d = d
+        if torch.is_tensor(values):
+            vals = values.detach().clone()
+        else:
+            # python numbers are fp64 (fixed_feature.py:25-37); tensors keep shape
+            single = all(torch.is_tensor(v) and v.dtype == torch.float32 for v in values)
+            dtype = torch.float32 if single else torch.float64
+            dev = next((v.device for v in values if torch.is_tensor(v) and v.is_cuda),
+                       torch.device("cpu"))
+            parts = []
+            for v in values:
+                t = torch.tensor([float(v)], dtype=dtype) if not torch.is_tensor(v) else (
+                    v.detach().clone().reshape(1) if v.ndim == 0 else v.detach().clone())
+                parts.append(t.to(dtype=dtype, device=dev))
+            vals = torch.cat(torch.broadcast_tensors(*parts), dim=-1)
+        self.register_buffer("values", vals)
+        # column i of X_full: from X (free) or from the appended values (fixed)
+        d_f = vals.shape[-1]
+        cols = set(columns)
+        free = iter(range(d - d_f))
+        fixed = iter(range(d - d_f, d))
+        self._selector = [next(fixed) if i in cols else next(free) for i in range(d)]
+
+    @property
+    def model(self):
+        return self.acq_func.model
+
+    @property
+    def X_pending(self):
+        try:
+            return self.acq_func.X_pending
+        except AttributeError:
+            raise ValueError(f"Base acquisition function {type(self.acq_func).__name__} does not "
+                             "have an `X_pending` attribute.")
+
+    @X_pending.setter
+    def X_pending(self, X_pending):
+        if "acq_func" not in self._modules:  # AcquisitionFunction.__init__ is skipped
+            return
+        self.acq_func.X_pending = (self._construct_X_full(X_pending) if X_pending is not None
+                                   else None)
+
+    def set_X_pending(self, X_pending=None) -> None:
+        self.acq_func.set_X_pending(self._construct_X_full(X_pending) if X_pending is not None
+                                    else None)
+
+    def _construct_X_full(self, X: torch.Tensor) -> torch.Tensor:
+        d_prime, d_f = X.shape[-1], self.values.shape[-1]
+        if d_prime + d_f != self.d:
+            raise ValueError(f"Feature dimension d' ({d_prime}) of input must be "
+                             f"d - d_f ({self.d - d_f}).")
+        vals = self.values.to(X).expand(*X.shape[:-1], d_f)
+        return torch.cat([X, vals], dim=-1)[..., self._selector]
+
+    def forward(self, X: torch.Tensor) -> torch.Tensor:
+        return self.acq_func(self._construct_X_full(X))

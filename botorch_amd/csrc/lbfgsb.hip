@@ -16,6 +16,7 @@
 #include "common.h"
 
 #include <atomic>
+#include <mutex>
 
 // No multiply-add contraction: scipy's L-BFGS-B rounds every product and sum
 // separately, and a fused a*b+c flips borderline line-search tests (measured:
@@ -133,16 +134,24 @@ __global__ __launch_bounds__(64) void lbfgsb_kernel(bolb::Problem P, double* __r
 
 }  // namespace
 
-// phase clocks of the next launches (tools/prof_lbfgsb.py), B x PROF_SLOTS, or null
-// (profiling aids: atomics, so a setter on one thread never tears a launch's read)
-static std::atomic<unsigned long long*> g_lbfgsb_prof{nullptr};
-static std::atomic<int> g_lbfgsb_prof_cap{0};   // restarts the buffer holds
+// phase clocks of the next launches (tools/prof_lbfgsb.py), B x PROF_SLOTS, or null.
+// The buffer and its capacity change together under one mutex, so a launch on
+// another thread reads a consistent pair (never a new capacity with the old,
+// smaller buffer).
+static std::mutex g_lbfgsb_prof_mu;
+static unsigned long long* g_lbfgsb_prof = nullptr;
+static int g_lbfgsb_prof_cap = 0;               // restarts the buffer holds
 static std::atomic<int> g_lbfgsb_unstaged{0};   // 1: keep the working set in HBM (A/B timing)
 extern "C" int bo_lbfgsb_set_profile(unsigned long long* prof, int capacity) {
   BO_CHECK_ARG(capacity >= 0, "bo_lbfgsb_set_profile: capacity %d", capacity);
-  g_lbfgsb_prof_cap.store(prof ? capacity : 0);
-  g_lbfgsb_prof.store(prof);
+  std::lock_guard<std::mutex> lk(g_lbfgsb_prof_mu);
+  g_lbfgsb_prof = prof;
+  g_lbfgsb_prof_cap = prof ? capacity : 0;
   return BO_OK;
+}
+static unsigned long long* lbfgsb_profile_for(int B) {
+  std::lock_guard<std::mutex> lk(g_lbfgsb_prof_mu);
+  return B <= g_lbfgsb_prof_cap ? g_lbfgsb_prof : nullptr;
 }
 extern "C" int bo_lbfgsb_set_staging(int on) {
   g_lbfgsb_unstaged.store(!on);
@@ -169,7 +178,7 @@ extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int m
                "bo_lbfgsb_step: null buffer");
   if (B == 0) return BO_OK;
   // profile only launches the buffer can hold (B x PROF_SLOTS clocks)
-  unsigned long long* prof = B <= g_lbfgsb_prof_cap.load() ? g_lbfgsb_prof.load() : nullptr;
+  unsigned long long* prof = lbfgsb_profile_for(B);
   bolb::Problem P{n, m, maxls, maxiter, maxfun, ftol, pgtol, lower, upper, prof};
   const size_t bytes = staged_bytes(n, m);
   const int staged = bytes <= STAGE_LIMIT && !g_lbfgsb_unstaged.load();

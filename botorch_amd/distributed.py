@@ -158,7 +158,7 @@ def optimize_acqf_sharded(acq_function, bounds, q: int, num_restarts: int,
     def _run(ics):
         c, v, warned = generate_in_chunks(acq_function, ics[r0:r1], bounds, batch_limit, options,
                                           gen_candidates)
-        flag = torch.tensor([float(warned)], dtype=torch.float64, device=ics.device)
+        flag = torch.tensor([float(bool(warned))], dtype=torch.float64, device=ics.device)
         if ws > 1:
             dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
         return c, v, bool(flag.item())

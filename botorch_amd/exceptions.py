@@ -39,3 +39,23 @@ class OptimizationWarning(BotorchWarning):
 
 class InputDataWarning(BotorchWarning):
     pass
+
+
+class ModelFittingError(Exception):
+    """botorch/exceptions/errors.py ModelFittingError: every fit attempt of
+    fit_gpytorch_mll failed (fit.py:255-259)."""
+
+
+class OptimizationTimeoutError(BotorchError):
+    """botorch/exceptions/errors.py OptimizationTimeoutError: raised inside the
+    scipy callback when ``timeout_sec`` is exceeded (optim/utils/timeout.py:49-53)
+    and turned into a "timed out" OptimizeResult by minimize_with_timeout."""
+
+    def __init__(self, *args, current_x=None, runtime: float = 0.0):
+        super().__init__(*args)
+        self.current_x = current_x
+        self.runtime = runtime
+
+
+class BadInitialCandidatesWarning(RuntimeWarning):
+    """botorch/exceptions/warnings.py BadInitialCandidatesWarning."""

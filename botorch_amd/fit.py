@@ -13,9 +13,13 @@ the loss and its exact gradient (plus the LogNormal prior terms).
 """
 from __future__ import annotations
 
+import logging
 import math
+import re
 import time
 import warnings
+from dataclasses import dataclass
+from enum import Enum, auto
 from typing import Optional
 
 import numpy as np
@@ -24,8 +28,10 @@ from scipy.optimize import minimize
 
 from . import _lib, kernels
 from ._lib import check, lib
-from .exceptions import NotPSDError, OptimizationWarning
+from .exceptions import NotPSDError, OptimizationWarning, UnsupportedError
 from .models import FixedNoiseGaussianLikelihood, LogNormalPrior, ScaleKernel, SingleTaskGP
+
+logger = logging.getLogger("botorch_amd")
 
 
 class ExactMarginalLogLikelihood:
@@ -106,9 +112,6 @@ class _Layout:
         # constrained-parameter writes = a dozen small host-to-device copies)
         return mll_value_and_grad(self.model, x, self, sync_model=False)
 
-    def sample_priors(self, gen: torch.Generator) -> None:
-        _sample_all_priors(self.model, self, gen)
-
 
 class _MultiLayout:
     """The m members of a multi-output SingleTaskGP as one flat vector in the
@@ -164,10 +167,6 @@ class _MultiLayout:
             loss += lt
             grads.append(gt)
         return loss, np.concatenate(grads)[self.perm]
-
-    def sample_priors(self, gen: torch.Generator) -> None:
-        for p in self.parts:
-            p.sample_priors(gen)
 
 
 def _layout(model):
@@ -288,66 +287,294 @@ def mll_value_and_grad(model: SingleTaskGP, x: np.ndarray, layout: _Layout, cach
     return -ll / n, -g / n
 
 
-def fit_gpytorch_mll_scipy(mll: ExactMarginalLogLikelihood, method="L-BFGS-B", options=None,
-                           callback=None, timeout_sec=None):
+class OptimizationStatus(int, Enum):
+    """optim/core.py:39-43."""
+    RUNNING = auto()
+    SUCCESS = auto()
+    FAILURE = auto()
+    STOPPED = auto()
+
+
+@dataclass
+class OptimizationResult:
+    """optim/core.py:46-52."""
+    step: int
+    fval: float
+    status: OptimizationStatus
+    runtime: Optional[float] = None
+    message: Optional[str] = None
+
+
+# optim/core.py:34-36 matches the iteration / evaluation limit messages of
+# scipy <= 1.14's Fortran L-BFGS-B ("TOTAL NO. of ITERATIONS REACHED LIMIT",
+# "TOTAL NO. of f AND g EVALUATIONS EXCEEDS LIMIT").  scipy 1.15 (installed
+# here) spells them "TOTAL NO. OF ITERATIONS REACHED LIMIT" and "TOTAL NO. OF
+# F,G EVALUATIONS EXCEEDS LIMIT", which the reference's case-sensitive pattern
+# misses (a maxiter stop would then count as a failed fit).  Both spellings are
+# matched here: the reference's intent with the scipy the box has.
+LBFGSB_MAXITER_MAXFUN_REGEX = re.compile(
+    r"TOTAL NO\. OF (ITERATIONS REACHED LIMIT|F AND G EVALUATIONS EXCEEDS LIMIT|"
+    r"F,G EVALUATIONS EXCEEDS LIMIT)", re.IGNORECASE)
+
+
+def _param_bounds_by_name(layout):
+    """get_parameters_and_bounds names (optim/utils/model_utils.py:69-109) of
+    the single-output layout's segments."""
+    return {"likelihood.noise_covar.raw_noise": "noise", "mean_module.raw_constant": "constant",
+            "covar_module.raw_lengthscale": "lengthscale",
+            "covar_module.base_kernel.raw_lengthscale": "lengthscale",
+            "covar_module.raw_outputscale": "outputscale"}
+
+
+def _apply_user_bounds(layout, bounds) -> list:
+    """fit_gpytorch_mll_scipy's ``bounds`` dict (updating the defaults,
+    optim/fit.py:83-84) onto the flat vector's scipy bounds."""
+    out = list(layout.bounds)
+    if not bounds:
+        return out
+    if isinstance(layout, _MultiLayout):
+        raise UnsupportedError("user bounds for a multi-output SingleTaskGP fit")
+    names = _param_bounds_by_name(layout)
+    segs = {name: (start, size) for name, start, size in layout.segments}
+    for pname, (lo, hi) in bounds.items():
+        seg = names.get(pname)
+        if seg is None or seg not in segs:
+            raise UnsupportedError(f"bounds for unknown parameter {pname!r}")
+        start, size = segs[seg]
+        for j in range(start, start + size):
+            out[j] = (lo, hi)
+    return out
+
+
+def fit_gpytorch_mll_scipy(mll: ExactMarginalLogLikelihood, parameters=None, bounds=None,
+                           closure=None, closure_kwargs=None, method="L-BFGS-B", options=None,
+                           callback=None, timeout_sec=None) -> OptimizationResult:
+    """optim/fit.py:47-110 + optim/core.py:55-140: L-BFGS-B over the flat
+    hyperparameter vector, the closure being the device MLL (value and exact
+    gradient from bo::mll), bounded by ``timeout_sec``; the parameters are
+    written at the optimum; an OptimizationWarning when the run did not end in
+    SUCCESS.  ``callback(parameters, OptimizationResult)`` is called after
+    each iteration as the reference's wrapped callback does.  ``parameters`` /
+    ``closure``: the device closure is the only one on this path (a custom
+    torch closure raises UnsupportedError)."""
+    if parameters is not None or closure is not None or closure_kwargs:
+        raise UnsupportedError("custom parameters / closures: the MLL closure here is the "
+                               "device one (bo::mll)")
+    from .optim import minimize_with_timeout
+    t0 = time.monotonic()
     model = mll.model
     layout = _layout(model)
     x0 = layout.get()
     if torch.isnan(model.train_inputs[0]).any() or torch.isnan(model.train_targets).any():
         from .exceptions import NanError
         raise NanError("training data contains NaN")
+    wrapped = None
+    if callback is not None:
+        step = [0]
 
-    def f(x):
-        return layout.value_and_grad(x)
+        def wrapped(x):
+            step[0] += 1
+            res = OptimizationResult(step=step[0], fval=float(layout.value_and_grad(x)[0]),
+                                     status=OptimizationStatus.RUNNING,
+                                     runtime=time.monotonic() - t0)
+            return callback(dict(model.named_parameters()), res)
 
-    res = minimize(f, x0, jac=True, method=method, bounds=layout.bounds, options=options or {},
-                   callback=callback)
-    layout.set(res.x)
-    if not res.success:
-        warnings.warn(f"`scipy_minimize` terminated with status {res.status}, displaying original "
-                      f"message from `scipy.optimize.minimize`: {res.message}", OptimizationWarning)
-    return res
+    raw = minimize_with_timeout(layout.value_and_grad, x0, jac=True, method=method,
+                                bounds=_apply_user_bounds(layout, bounds), options=options or {},
+                                callback=wrapped, timeout_sec=timeout_sec)
+    layout.set(raw.x)
+    msg = raw.message if isinstance(raw.message, str) else raw.message.decode("ascii")
+    if raw.success:
+        status = OptimizationStatus.SUCCESS
+    elif LBFGSB_MAXITER_MAXFUN_REGEX.search(msg) or "Optimization timed out after" in msg:
+        status = OptimizationStatus.STOPPED
+    else:
+        status = OptimizationStatus.FAILURE
+    result = OptimizationResult(step=int(getattr(raw, "nit", 0)), fval=float(raw.fun),
+                                status=status, runtime=time.monotonic() - t0, message=msg)
+    if status != OptimizationStatus.SUCCESS:
+        warnings.warn(f"`scipy_minimize` terminated with status {status}, displaying original "
+                      f"message from `scipy.optimize.minimize`: {msg}", OptimizationWarning)
+    return result
 
 
-def _sample_all_priors(model: SingleTaskGP, layout: _Layout, gen: torch.Generator):
-    """sample_all_priors: draw free hyperparameters from their priors."""
-    x = layout.get()
-    base, o = layout.base, layout.o
-    if not layout.fixed and model.likelihood.noise_prior is not None:
-        p = model.likelihood.noise_prior
-        x[0] = max(math.exp(p.loc + p.scale * torch.randn(1, generator=gen).item()),
-                   model.likelihood.noise_lower)
+def _sample_prior_values(prior: LogNormalPrior, shape, device) -> torch.Tensor:
+    """[G] LogNormalPrior.sample(shape) in fp64 on the model's device:
+    exp(torch.normal(loc, scale)) from the global generator of that device."""
+    loc = torch.full(shape, prior.loc, dtype=torch.float64, device=device)
+    scale = torch.full(shape, prior.scale, dtype=torch.float64, device=device)
+    with torch.no_grad():
+        return torch.normal(loc, scale).exp()
+
+
+def sample_all_priors(model) -> None:
+    """optim/utils/model_utils.py:153-193 sample_all_priors: each free
+    hyperparameter with a prior gets a draw of its own shape, in the order of
+    [G] named_priors (the module's own priors, then its children's in
+    registration order: likelihood noise, then the covariance module -- a
+    ScaleKernel's outputscale before its base kernel's lengthscale).  The
+    draws come from the global generator of the parameters' device, as the
+    reference's do; the constraints have ``transform=None``, so a draw is set
+    as is (L-BFGS-B clips it into the bounds)."""
+    if getattr(model, "_is_multi_output", False):
+        members = list(model.models)
+        dev = model.train_inputs[0].device
+        m, d = len(members), model.train_inputs[0].shape[-1]
+        # the batched model (batch shape [m]) draws each prior once, m-wide
+        p = members[0].likelihood.noise_prior
+        if p is not None and not isinstance(members[0].likelihood, FixedNoiseGaussianLikelihood):
+            v = _sample_prior_values(p, (m, 1), dev)
+            for t, mm in enumerate(members):
+                mm.likelihood.noise = v[t]
+        ck = members[0].covar_module
+        if isinstance(ck, ScaleKernel) and ck.outputscale_prior is not None:
+            v = _sample_prior_values(ck.outputscale_prior, (m,), dev)
+            for t, mm in enumerate(members):
+                mm.covar_module.outputscale = float(v[t])
+        base = ck.base_kernel if isinstance(ck, ScaleKernel) else ck
+        if base.lengthscale_prior is not None:
+            v = _sample_prior_values(base.lengthscale_prior, (m, 1, d), dev)
+            for t, mm in enumerate(members):
+                b = mm.covar_module.base_kernel if isinstance(mm.covar_module, ScaleKernel) \
+                    else mm.covar_module
+                b.lengthscale = v[t]
+        return
+    dev = model.train_inputs[0].device
+    lik = model.likelihood
+    if not isinstance(lik, FixedNoiseGaussianLikelihood) and lik.noise_prior is not None:
+        lik.noise = _sample_prior_values(lik.noise_prior, (1,), dev)
+    ck = model.covar_module
+    if isinstance(ck, ScaleKernel) and ck.outputscale_prior is not None:
+        ck.outputscale = float(_sample_prior_values(ck.outputscale_prior, (), dev))
+    base = ck.base_kernel if isinstance(ck, ScaleKernel) else ck
     if base.lengthscale_prior is not None:
-        p = base.lengthscale_prior
-        z = torch.randn(layout.d, generator=gen, dtype=torch.float64).numpy()
-        x[o + 1:o + 1 + layout.d] = np.maximum(np.exp(p.loc + p.scale * z), base.lengthscale_lower)
-    layout.set(x)
+        base.lengthscale = _sample_prior_values(base.lengthscale_prior,
+                                                tuple(base.lengthscale.shape), dev)
 
 
-def fit_gpytorch_mll(mll: ExactMarginalLogLikelihood, optimizer_kwargs=None, max_attempts=5,
-                     **kwargs) -> ExactMarginalLogLikelihood:
-    """botorch/fit.py:75-258 (_fit_fallback)."""
-    optimizer_kwargs = optimizer_kwargs or {}
+def _debug_warn(w) -> bool:
+    return bool(LBFGSB_MAXITER_MAXFUN_REGEX.search(str(w.message)))
+
+
+def _rethrow_warn(w) -> bool:
+    if not issubclass(w.category, OptimizationWarning):
+        return True
+    return "Optimization timed out after" in str(w.message)
+
+
+def DEFAULT_WARNING_HANDLER(w) -> bool:
+    """fit.py:51-71 (_warning_handler_template with _debug_warn / _rethrow_warn):
+    True when the warning is resolved -- iteration / evaluation limits are
+    logged, non-optimisation warnings and timeouts are re-emitted -- False when
+    it should trigger a retry."""
+    if _debug_warn(w):
+        logger.debug(str(w.message))
+        return True
+    if _rethrow_warn(w):
+        warnings.warn_explicit(str(w.message), w.category, w.filename, w.lineno)
+        return True
+    return False
+
+
+class SumMarginalLogLikelihood:
+    """[G] SumMarginalLogLikelihood(likelihood, ModelListGP): one exact MLL per
+    member."""
+
+    def __init__(self, likelihood, model):
+        self.likelihood = likelihood
+        self.model = model
+        self.mlls = [ExactMarginalLogLikelihood(mm.likelihood, mm) for mm in model.models]
+
+    def train(self):
+        self.model.train()
+        return self
+
+    def eval(self):
+        self.model.eval()
+        return self
+
+    @property
+    def training(self):
+        return any(m.training for m in self.mlls)
+
+
+def fit_gpytorch_mll(mll, closure=None, optimizer=None, closure_kwargs=None,
+                     optimizer_kwargs=None, **kwargs):
+    """botorch/fit.py:75-113: dispatch on the MLL type -- a
+    SumMarginalLogLikelihood over a ModelListGP fits each member (_fit_list,
+    fit.py:262-283), anything else goes to _fit_fallback."""
+    if optimizer is not None:
+        kwargs["optimizer"] = optimizer
+    if isinstance(mll, SumMarginalLogLikelihood):
+        mll.train()
+        for sub in mll.mlls:
+            fit_gpytorch_mll(sub, closure=closure, closure_kwargs=closure_kwargs,
+                             optimizer_kwargs=optimizer_kwargs, **kwargs)
+        return mll.eval() if not mll.training else mll
+    return _fit_fallback(mll, closure=closure, closure_kwargs=closure_kwargs,
+                         optimizer_kwargs=optimizer_kwargs, **kwargs)
+
+
+def _fit_fallback(mll, *, closure=None, optimizer=fit_gpytorch_mll_scipy, closure_kwargs=None,
+                  optimizer_kwargs=None, max_attempts: int = 5,
+                  pick_best_of_all_attempts: bool = False,
+                  warning_handler=DEFAULT_WARNING_HANDLER,
+                  caught_exception_types=(NotPSDError,), **ignore):
+    """botorch/fit.py:116-259.  Each attempt starts from the state the fit was
+    called with (the rollback of module_rollback_ctx); attempts after the first
+    resample the priors from the global generator first.  Warnings the
+    ``warning_handler`` does not resolve are re-emitted and make the attempt a
+    failure; exceptions of ``caught_exception_types`` are logged and count as
+    failed attempts.  The first successful attempt is kept, or with
+    ``pick_best_of_all_attempts`` the successful attempt of largest MLL.  When
+    no attempt succeeded: ModelFittingError, with the model back at its
+    starting state and in train mode."""
+    from .exceptions import ModelFittingError
+    from .settings import debug
+    if closure is not None or closure_kwargs:
+        raise UnsupportedError("custom closures: the MLL closure here is the device one "
+                               "(bo::mll)")
+    optimizer_kwargs = {} if optimizer_kwargs is None else optimizer_kwargs
     model = mll.model
     mll.train()
     layout = _layout(model)
-    gen = torch.Generator().manual_seed(0)
-    ckpt = layout.get()
+    ckpt = layout.get()   # module_rollback_ctx's checkpoint
+    best_mll, best_x = -math.inf, None
     for attempt in range(1, max_attempts + 1):
+        layout.set(ckpt)
         if attempt > 1:
-            layout.set(ckpt)
-            layout.sample_priors(gen)
+            sample_all_priors(model)
         try:
-            with warnings.catch_warnings(record=True) as ws:
+            with warnings.catch_warnings(record=True) as wlist, debug(True):
                 warnings.simplefilter("always", category=OptimizationWarning)
-                fit_gpytorch_mll_scipy(mll, **optimizer_kwargs)
-            bad = [w for w in ws if issubclass(w.category, OptimizationWarning)
-                   and "ITERATIONS REACHED LIMIT" not in str(w.message).upper()
-                   and "timed out" not in str(w.message)]
-            if not bad:
+                result = optimizer(mll, closure=None, **optimizer_kwargs)
+            success = True
+            for w in wlist:
+                if not warning_handler(w):
+                    warnings.warn_explicit(str(w.message), w.category, w.filename, w.lineno)
+                    success = False
+            if success and not pick_best_of_all_attempts:
                 return mll.eval()
-        except NotPSDError:
-            pass
+            if success:
+                cur = -float(result.fval)
+                if cur > best_mll:
+                    best_mll, best_x = cur, layout.get()
+                    logger.debug(f"Fit attempt #{attempt}: New best MLL: {best_mll}.")
+                else:
+                    logger.debug(f"Fit attempt #{attempt}: Current MLL {cur} did not beat best "
+                                 f"MLL so far {best_mll}.")
+            mll.train()
+            if not success:
+                logger.debug(f"Fit attempt #{attempt} of {max_attempts} triggered retry policy"
+                             f"{'.' if attempt == max_attempts else '; retrying...'}")
+        except caught_exception_types as err:
+            logger.debug(f"Fit attempt #{attempt} of {max_attempts} failed with exception:\n{err}")
+    if best_x is not None:
+        layout.set(best_x)
+        return mll.eval()
     layout.set(ckpt)
-    warnings.warn("All attempts to fit the model have failed.", OptimizationWarning)
-    return mll
+    mll.train()
+    msg = "All attempts to fit the model have failed."
+    if debug.off():
+        msg += " For more information, try enabling botorch.settings.debug mode."
+    raise ModelFittingError(msg)

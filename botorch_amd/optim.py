@@ -13,6 +13,7 @@ the final argmax/gather is one all-reduce.
 from __future__ import annotations
 
 import ctypes
+import logging
 import math
 import time
 import warnings
@@ -22,16 +23,14 @@ import numpy as np
 import torch
 from scipy.optimize import minimize
 
-from .exceptions import OptimizationWarning
+from .exceptions import BadInitialCandidatesWarning, OptimizationWarning
 from .utils_sampling import draw_sobol_samples, manual_seed
+
+logger = logging.getLogger("botorch_amd")  # botorch/logging.py: quiet unless configured
 
 INIT_OPTION_KEYS = {"alpha", "batch_limit", "eta", "init_batch_limit", "nonnegative", "n_burnin",
                     "sample_around_best", "sample_around_best_sigma",
                     "sample_around_best_prob_perturb", "seed", "thinning"}
-
-
-class BadInitialCandidatesWarning(RuntimeWarning):
-    pass
 
 
 def columnwise_clamp(X, lower=None, upper=None, raise_on_violation=False):
@@ -171,8 +170,6 @@ def init_options(acq_function, bounds, options):
         raise NotImplementedError("Currently only finite values in `bounds` are supported for "
                                   "generating initial conditions for optimization.")
     options = options or {}
-    if options.get("sample_around_best", False):
-        raise NotImplementedError("sample_around_best is out of scope")
     seed = options.get("seed")
     batch_limit = options.get("init_batch_limit", options.get("batch_limit"))
     init_kwargs = {}
@@ -204,31 +201,206 @@ def select_initial_indices(init_func, Y_rnd: torch.Tensor, num_restarts: int, in
     return idx.reshape(-1), any(issubclass(w.category, BadInitialCandidatesWarning) for w in ws)
 
 
+def fix_features(X: torch.Tensor, fixed_features=None) -> torch.Tensor:
+    """optim/utils/acquisition_utils.py:66-93: columns with a value are set to
+    it (zero gradient); columns mapped to None are detached."""
+    if fixed_features is None:
+        return X
+    cols = list(X.unbind(dim=-1))
+    for k, v in fixed_features.items():
+        cols[k] = cols[k].detach() if v is None else torch.full_like(cols[k], v)
+    return torch.stack(cols, dim=-1)
+
+
+def _normalize(X, bounds):
+    return (X - bounds[0]) / (bounds[1] - bounds[0])
+
+
+def _unnormalize(X, bounds):
+    return X * (bounds[1] - bounds[0]) + bounds[0]
+
+
+def _std_normal_cdf(x):
+    return 0.5 * (1 + torch.erf(x / math.sqrt(2)))
+
+
+def _std_normal_icdf(p):
+    return torch.erfinv(2 * p - 1) * math.sqrt(2)
+
+
+def sample_truncated_normal_perturbations(X, n_discrete_points, sigma, bounds, qmc=True):
+    """optim/initializers.py:1145-1193: N(X, sigma^2 I) truncated to the unit
+    cube by the inverse CDF, in normalised coordinates."""
+    X = _normalize(X, bounds)
+    d = X.shape[1]
+    if X.shape[0] > 1:
+        X = X[torch.randint(X.shape[0], (n_discrete_points,), device=X.device)]
+    if qmc:
+        unit = torch.zeros(2, d, dtype=X.dtype, device=X.device)
+        unit[1] = 1
+        u = draw_sobol_samples(bounds=unit, n=n_discrete_points, q=1).squeeze(1)
+    else:
+        u = torch.rand((n_discrete_points, d), dtype=X.dtype, device=X.device)
+    lo_cdf = _std_normal_cdf(-X / sigma)
+    hi_cdf = _std_normal_cdf((1 - X) / sigma)
+    pert = _std_normal_icdf(lo_cdf + u * (hi_cdf - lo_cdf)) * sigma
+    return _unnormalize((X + pert).clamp(0.0, 1.0), bounds)
+
+
+def sample_perturbed_subset_dims(X, bounds, n_discrete_points, sigma=1e-1, qmc=True,
+                                 prob_perturb=None):
+    """optim/initializers.py:1196-1269: perturb a random subset of the
+    dimensions (each with probability min(20/d, 1); a row that drew none gets
+    ceil(d p) of them)."""
+    if bounds.ndim != 2 or X.ndim != 2:
+        raise ValueError("bounds must be 2 x d and X must be n x d")
+    d = bounds.shape[-1]
+    if prob_perturb is None:
+        prob_perturb = min(20.0 / d, 1.0)
+    if X.shape[0] == 1:
+        X_cand = X.repeat(n_discrete_points, 1)
+    else:
+        X_cand = X[torch.randint(X.shape[0], (n_discrete_points,), device=X.device)]
+    pert = sample_truncated_normal_perturbations(X_cand, n_discrete_points, sigma, bounds, qmc)
+    mask = torch.rand(n_discrete_points, d, dtype=bounds.dtype, device=bounds.device) <= prob_perturb
+    none = (~mask).all(dim=-1).nonzero()
+    template = torch.zeros(d, dtype=mask.dtype, device=mask.device)
+    template[:math.ceil(d * prob_perturb)] = True
+    for row in none:
+        mask[row] = template[torch.randperm(d, device=bounds.device)]
+    X_cand[mask] = pert[mask]
+    return X_cand
+
+
+def get_X_baseline(acq_function):
+    """optim/utils/acquisition_utils.py:96-135: the acquisition's X_baseline,
+    else the model's training inputs (None if neither)."""
+    Xb = getattr(acq_function, "X_baseline", None)
+    if Xb is None:
+        model = getattr(acq_function, "model", None)
+        if model is None:
+            return None
+        ti = getattr(model, "train_inputs", None)
+        if ti is None and hasattr(model, "models"):
+            ti = getattr(model.models[0], "train_inputs", None)
+        if ti is None:
+            return None
+        Xb = ti[0]
+    while Xb is not None and Xb.ndim > 2:
+        Xb = Xb[0]
+    return Xb if Xb is not None and Xb.shape[0] > 0 else None
+
+
+def sample_points_around_best(acq_function, n_discrete_points, sigma, bounds, best_pct=5.0,
+                              subset_sigma=1e-1, prob_perturb=None):
+    """optim/initializers.py:1040-1142: the best_pct % best baseline points by
+    posterior mean (or the Pareto set of a multi-output objective), perturbed;
+    None without baseline points."""
+    from .exceptions import BotorchWarning
+    X = get_X_baseline(acq_function)
+    if X is None:
+        return None
+    with torch.no_grad():
+        try:
+            mean = acq_function.model.posterior(X).mean
+        except AttributeError:
+            warnings.warn("Failed to sample around previous best points.", BotorchWarning)
+            return None
+        while mean.ndim > 2:
+            mean = mean.mean(dim=0)
+        try:
+            f_pred = acq_function.objective(mean)
+        except (AttributeError, TypeError):
+            f_pred = mean
+        if hasattr(acq_function, "maximize") and not acq_function.maximize:
+            f_pred = -f_pred
+        constraints = getattr(acq_function, "constraints", None)
+        if constraints is not None:
+            neg_violation = -torch.stack([c(mean).clamp_min(0.0) for c in constraints],
+                                         dim=-1).sum(dim=-1)
+            feas = neg_violation == 0
+            if feas.any():
+                f_pred[~feas] = float("-inf")
+            else:
+                f_pred = neg_violation
+        if f_pred.ndim == mean.ndim and f_pred.shape[-1] > 1:
+            from .multi_objective import is_non_dominated
+            best_X = X[is_non_dominated(f_pred)]
+        else:
+            if f_pred.shape[-1] == 1:
+                f_pred = f_pred.squeeze(-1)
+            n_best = max(1, round(X.shape[0] * best_pct / 100))
+            best_X = X[torch.topk(f_pred, n_best).indices.view(-1)]
+    subset = best_X.shape[-1] >= 20 or prob_perturb is not None
+    n_tn = n_discrete_points // 2 if subset else n_discrete_points
+    out = sample_truncated_normal_perturbations(best_X, n_tn, sigma, bounds)
+    if subset:
+        sub = sample_perturbed_subset_dims(best_X, bounds, n_discrete_points - n_tn, sigma,
+                                           prob_perturb=prob_perturb)
+        out = torch.cat([out, sub], dim=0)
+        out = out[torch.randperm(out.shape[0], device=X.device)]
+    return out
+
+
+SOBOL_MAXDIM = 21201  # torch.quasirandom.SobolEngine.MAXDIM
+
+
 def gen_batch_initial_conditions(acq_function, bounds, q, num_restarts, raw_samples,
                                  fixed_features=None, options=None, inequality_constraints=None,
-                                 equality_constraints=None, generator=None, fixed_X_fantasies=None,
-                                 **kwargs):
-    """optim/initializers.py:243-438: Sobol raw samples, forward-only evaluation
-    in chunks of init_batch_limit, Boltzmann selection; retried with up to 5x
-    the raw samples (seed + 1 each time) while the selection warns.
+                                 equality_constraints=None, generator=None, fixed_X_fantasies=None):
+    """optim/initializers.py:243-438: Sobol raw samples (or ``generator(n, q,
+    seed)``; uniform draws past SobolEngine.MAXDIM), optionally joined by
+    points sampled around the incumbents, features fixed, forward-only
+    evaluation in chunks of init_batch_limit, Boltzmann selection; retried with
+    up to 5x the raw samples (seed + 1 each time) while the selection warns.
 
     MI355X path (bounds on the GPU): the raw designs are generated on the
     device (bo_sobol_box, bit-identical to draw_sobol_samples) and evaluated
     there chunk by chunk; only the values cross to the host, once, for the
     selection, which draws from the global CPU generator as the reference does
-    (so the picks are the reference's)."""
-    if inequality_constraints or equality_constraints or generator is not None \
-            or fixed_X_fantasies is not None:
-        raise NotImplementedError("constrained / custom-generator initialisation is out of scope")
+    (so the picks are the reference's).  Linear constraints need the
+    reference's polytope sampler (utils/sampling.py HitAndRun), which is not on
+    this path: they raise UnsupportedError."""
+    from .exceptions import UnsupportedError
+    if inequality_constraints or equality_constraints:
+        raise UnsupportedError("linear parameter constraints are not supported by this "
+                               "initialiser (the reference's polytope sampler is out of scope)")
+    options = options or {}
+    sample_around_best = options.get("sample_around_best", False)
+    if sample_around_best and generator:
+        raise UnsupportedError("Option 'sample_around_best' is not supported when custom "
+                               "generator is be used.")
     seed, batch_limit, init_func, init_kwargs = init_options(acq_function, bounds, options)
     q = 1 if q is None else q
+    d = bounds.shape[-1]
     factor, max_factor = 1, 5
     while factor < max_factor:
         n = raw_samples * factor
-        X_rnd = draw_raw_samples(bounds, n, q, seed)
-        if fixed_features:
-            for k, v in fixed_features.items():
-                X_rnd[..., k] = v
+        if generator is not None:
+            X_rnd = generator(n, q, seed)
+        elif d * q <= SOBOL_MAXDIM:
+            X_rnd = draw_raw_samples(bounds, n, q, seed)
+        else:
+            b_cpu = bounds.cpu()
+            with manual_seed(seed):
+                u = torch.rand(n, q, d, dtype=bounds.dtype)
+            X_rnd = b_cpu[0] + (b_cpu[1] - b_cpu[0]) * u
+        if sample_around_best:
+            X_best = sample_points_around_best(
+                acq_function, n_discrete_points=n * q,
+                sigma=options.get("sample_around_best_sigma", 1e-3), bounds=bounds,
+                subset_sigma=options.get("sample_around_best_subset_sigma", 1e-1),
+                prob_perturb=options.get("sample_around_best_prob_perturb"))
+            if X_best is not None:
+                X_rnd = torch.cat([X_rnd, X_best.view(n, q, d).to(X_rnd)], dim=0)
+        X_rnd = fix_features(X_rnd, fixed_features)
+        if fixed_X_fantasies is not None:
+            if fixed_X_fantasies.shape[-1] != X_rnd.shape[-1]:
+                raise ValueError("`fixed_X_fantasies` and `bounds` must both have the same "
+                                 f"trailing dimension `d`, but have {fixed_X_fantasies.shape[-1]} "
+                                 f"and {X_rnd.shape[-1]}, respectively.")
+            fx = fixed_X_fantasies.to(X_rnd)
+            X_rnd = torch.cat([X_rnd, fx.unsqueeze(0).expand(X_rnd.shape[0], *fx.shape)], dim=-2)
         Y_rnd = evaluate_raw_samples(acq_function, X_rnd.to(bounds.device), batch_limit)
         idx, warned = select_initial_indices(init_func, Y_rnd, num_restarts, init_kwargs)
         ics = X_rnd[idx.to(X_rnd.device)].to(device=bounds.device)
@@ -243,24 +415,113 @@ def gen_batch_initial_conditions(acq_function, bounds, q, num_restarts, raw_samp
     return ics
 
 
+def minimize_with_timeout(fun, x0, args=(), method=None, jac=None, bounds=None, constraints=(),
+                          tol=None, callback=None, options=None, timeout_sec=None):
+    """optim/utils/timeout.py:19-108: scipy.optimize.minimize whose callback
+    raises once ``timeout_sec`` has passed; the iterate it held is returned as
+    an unsuccessful result with the message "Optimization timed out after
+    <s> seconds." (status 1, as L-BFGS-B's maxiter stop)."""
+    from scipy.optimize import OptimizeResult
+    from .exceptions import OptimizationTimeoutError
+    wrapped = callback
+    if timeout_sec is not None:
+        t0 = time.monotonic()
+        n_it = [0]
+
+        def wrapped(xk, *extra):
+            runtime = time.monotonic() - t0
+            n_it[0] += 1
+            if runtime > timeout_sec:
+                raise OptimizationTimeoutError(current_x=xk, runtime=runtime)
+            if callback is not None:
+                return callback(xk, *extra)
+            return False
+    try:
+        kw = dict(method=method, jac=jac, bounds=bounds, tol=tol, callback=wrapped,
+                  options=options)
+        if constraints:
+            kw["constraints"] = constraints
+        return minimize(fun, x0, args=args, **kw)
+    except OptimizationTimeoutError as e:
+        fval = fun(e.current_x, *args)
+        fval = fval[0] if isinstance(fval, tuple) else fval
+        return OptimizeResult(fun=fval, x=e.current_x, nit=n_it[0], success=False, status=1,
+                              message=f"Optimization timed out after {e.runtime} seconds.")
+
+
+def _process_scipy_result(res, options) -> None:
+    """generation/gen.py:458-493: the iteration limit, the evaluation limit and
+    a timeout are logged, not warned; any other unsuccessful exit warns
+    OptimizationWarning (which makes optimize_acqf retry)."""
+    if "success" not in res.keys() or "status" not in res.keys():
+        warnings.warn("Optimization failed within `scipy.optimize.minimize` with no status "
+                      "returned to `res.`", OptimizationWarning)
+    elif not res.success:
+        msg = str(res.message)
+        if ("ITERATIONS REACHED LIMIT" in msg or "Iteration limit reached" in msg
+                or "EVALUATIONS EXCEEDS LIMIT" in msg or "Optimization timed out after" in msg):
+            logger.info("`scipy.minimize` exited: %s (maxiter %s, maxfun %s)", msg,
+                        options.get("maxiter"), options.get("maxfun"))
+        else:
+            warnings.warn(f"Optimization failed within `scipy.optimize.minimize` with status "
+                          f"{res.status} and message {msg}.", OptimizationWarning)
+
+
+def _without_fixed_features(fixed_features, acquisition_function, initial_conditions,
+                            lower_bounds, upper_bounds):
+    """generation/utils.py:102-196 without constraints: the base acquisition
+    wrapped so that it takes only the free columns, and the initial conditions
+    and bounds restricted to them."""
+    from .acquisition import FixedFeatureAcquisitionFunction
+    keys = sorted(fixed_features)
+    vals = [initial_conditions[..., [k]] if fixed_features[k] is None else fixed_features[k]
+            for k in keys]
+    d = initial_conditions.shape[-1]
+    ff = FixedFeatureAcquisitionFunction(acquisition_function, d=d, columns=keys, values=vals)
+    free = sorted(set(range(d)) - set(keys))
+    ics = initial_conditions[..., free]
+    if torch.is_tensor(lower_bounds):
+        lower_bounds = lower_bounds[..., free]
+    if torch.is_tensor(upper_bounds):
+        upper_bounds = upper_bounds[..., free]
+    return ff, ics, lower_bounds, upper_bounds
+
+
+def _reject_constraints(inequality_constraints, equality_constraints,
+                        nonlinear_inequality_constraints) -> None:
+    if inequality_constraints or equality_constraints or nonlinear_inequality_constraints:
+        from .exceptions import UnsupportedError
+        raise UnsupportedError("parameter constraints (SLSQP / trust-constr candidate "
+                               "generation) are not supported on this path")
+
+
 def gen_candidates_scipy(initial_conditions, acquisition_function, lower_bounds=None,
-                         upper_bounds=None, options=None, fixed_features=None,
-                         timeout_sec=None, **kwargs):
-    """generation/gen.py:46-298 (box constraints, L-BFGS-B, with_grad)."""
+                         upper_bounds=None, inequality_constraints=None, equality_constraints=None,
+                         nonlinear_inequality_constraints=None, options=None, fixed_features=None,
+                         timeout_sec=None):
+    """generation/gen.py:46-298 (box constraints, L-BFGS-B): fixed features
+    are removed from the search space (gen.py:124-175), the run is bounded by
+    ``timeout_sec`` (minimize_with_timeout, gen.py:252-267) and its exit is
+    resolved by _process_scipy_result (gen.py:268).  Linear and nonlinear
+    constraints raise UnsupportedError."""
+    _reject_constraints(inequality_constraints, equality_constraints,
+                        nonlinear_inequality_constraints)
     options = dict(options or {})
     options = {**options, "maxiter": options.get("maxiter", 2000)}
+    if fixed_features:
+        ff, ics, lo, hi = _without_fixed_features(fixed_features, acquisition_function,
+                                                  initial_conditions, lower_bounds, upper_bounds)
+        c, acq = gen_candidates_scipy(ics, ff, lo, hi, options=options, timeout_sec=timeout_sec)
+        return ff._construct_X_full(c), acq
     clamped = columnwise_clamp(initial_conditions, lower_bounds, upper_bounds)
     shapeX = clamped.shape
     x0 = clamped.detach().reshape(-1).cpu().numpy()
-    d = shapeX[-1]
     lb = (torch.as_tensor(lower_bounds).expand(shapeX).reshape(-1).cpu().numpy()
           if lower_bounds is not None else np.full(x0.shape, -np.inf))
     ub = (torch.as_tensor(upper_bounds).expand(shapeX).reshape(-1).cpu().numpy()
           if upper_bounds is not None else np.full(x0.shape, np.inf))
     scipy_bounds = list(zip(lb, ub))
-    with_grad = options.pop("with_grad", True)
-    method = options.pop("method", "L-BFGS-B")
-    callback = options.pop("callback", None)
+    with_grad = options.get("with_grad", True)
 
     def f_np_wrapper(x: np.ndarray):
         if np.isnan(x).any():
@@ -281,12 +542,13 @@ def gen_candidates_scipy(initial_conditions, acquisition_function, lower_bounds=
         _check_deferred(X)
         return val
 
-    t0 = time.monotonic()
-    res = minimize(f_np_wrapper if with_grad else f_only, x0, method=method, jac=with_grad,
-                   bounds=scipy_bounds, callback=callback, options=options)
-    if not res.success and "ITERATIONS REACHED LIMIT" not in str(res.message):
-        warnings.warn(f"Optimization failed within `scipy.optimize.minimize` with status "
-                      f"{res.status} and message {res.message}.", OptimizationWarning)
+    res = minimize_with_timeout(f_np_wrapper if with_grad else f_only, x0,
+                                method=options.get("method", "L-BFGS-B"), jac=with_grad,
+                                bounds=scipy_bounds, callback=options.get("callback", None),
+                                options={k: v for k, v in options.items()
+                                         if k not in ("method", "callback", "with_grad")},
+                                timeout_sec=timeout_sec)
+    _process_scipy_result(res, options)
     candidates = torch.from_numpy(res.x).to(initial_conditions).reshape(shapeX)
     clamped = columnwise_clamp(candidates, lower_bounds, upper_bounds, raise_on_violation=True)
     with torch.no_grad():
@@ -381,9 +643,34 @@ LBFGSB_STATUS = {0: "running", 1: "CONVERGENCE: NORM OF PROJECTED GRADIENT <= PG
                  6: "ERROR: NON-FINITE VALUE OR LINE-SEARCH INPUT"}
 
 
+def _eval_flops(acquisition_function, B: int, q: int):
+    """Deterministic cost of one forward + backward of a GP acquisition at B
+    t-batches of q points: 2 x B q' n^2 (the two triangular n x n contractions,
+    R = K*x L^-T and its backward W), summed over the GP members (a
+    ModelListGP's outputs, a SAAS ensemble), q' = q + pending (+ r baseline
+    rows for the cached-root qNEI).  None when there is no GP to estimate."""
+    acq = acquisition_function
+    while hasattr(acq, "acq_func"):  # FixedFeatureAcquisitionFunction
+        acq = acq.acq_func
+    model = getattr(acq, "model", None)
+    if model is None:
+        return None
+    members = list(getattr(model, "models", None) or [model])
+    qq = q + (0 if getattr(acq, "X_pending", None) is None else int(acq.X_pending.shape[-2]))
+    total = 0.0
+    for mm in members:
+        ti = getattr(mm, "train_inputs", None)
+        if ti is None:
+            return None
+        n = int(ti[0].shape[-2])
+        total += 2.0 * B * qq * n * n * max(1, int(getattr(mm, "num_mcmc_samples", 1) or 1))
+    return total
+
+
 def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds=None,
-                          upper_bounds=None, options=None, fixed_features=None, timeout_sec=None,
-                          **kwargs):
+                          upper_bounds=None, inequality_constraints=None,
+                          equality_constraints=None, nonlinear_inequality_constraints=None,
+                          options=None, fixed_features=None, timeout_sec=None):
     """Device-resident replacement of gen_candidates_scipy (generation/gen.py:
     46-298).
 
@@ -407,16 +694,31 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     running (and at least ``compact_min`` restarts have stopped), the running
     restarts continue as a smaller batch (their states gathered, the graph
     re-captured for the new shape), so stopped restarts no longer take slots
-    in the evaluations; "auto" does so only when an evaluation has cost at
-    least ``compact_eval_ms`` (2 ms) on average, and then also defers the
-    first graph capture to the first status read.
+    in the evaluations; "auto" does so only for expensive evaluations --
+    decided once, before the first evaluation, from the acquisition's
+    deterministic cost estimate (forward + backward GP flops 2 B q' n^2 against
+    ``compact_flops``, default 1e10: C3's 128 restarts shrink, C2's 64 do not;
+    the minimum of two timed evaluations against ``compact_eval_ms`` only when
+    the acquisition has no GP model to estimate) -- and then also defers the
+    first graph capture to the first status read.  The shrunken batch runs the
+    same per-restart L-BFGS-B, but its evaluations take the split plan of the
+    smaller batch, so f and g are summed in another order (equal to ~1e-15
+    relative, not bit for bit): a compacted run is deterministic from run to
+    run and box to box, and equal to the uncompacted one to rounding.
     Returns (candidates b x q x d, acq values b); an
     OptimizationWarning is raised for restarts that end abnormally, as
     gen_candidates_scipy does for scipy's failures."""
     from . import _lib, kernels
     from ._lib import check, lib
-    if fixed_features:
-        raise NotImplementedError("fixed_features is not supported by the device optimiser")
+    _reject_constraints(inequality_constraints, equality_constraints,
+                        nonlinear_inequality_constraints)
+    if fixed_features:  # the search space without them (generation/utils.py:102-196)
+        ff, ics, lo_b, hi_b = _without_fixed_features(fixed_features, acquisition_function,
+                                                      initial_conditions, lower_bounds,
+                                                      upper_bounds)
+        c, acq = gen_candidates_device(ics, ff, lo_b, hi_b, options=options,
+                                       timeout_sec=timeout_sec)
+        return ff._construct_X_full(c), acq
     options = dict(options or {})
     algorithm = options.get("algorithm", "lbfgsb")
     if algorithm not in ("lbfgsb", "projected"):
@@ -453,11 +755,16 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     use_graph = bool(options.get("use_graph", True))
     compact = options.get("compact", "auto") if lbfgsb else False
     compact_min = int(options.get("compact_min", 8))
-    # "auto": shrink only when an evaluation costs at least this much (the
-    # re-capture of the graph costs a few evaluations' worth: measured C3
-    # 55 -> 35 ms, C2 9.1 -> 14.5 ms with an unconditional shrink; eager C3
-    # evaluations take 2.5-3 ms, C2 ones 0.7-1.2 ms)
+    # "auto": shrink only expensive evaluations (the re-capture of the graph
+    # costs a few evaluations' worth: measured C3 55 -> 35 ms, C2 9.1 -> 14.5 ms
+    # with an unconditional shrink; eager C3 evaluations take 2.5-3 ms, C2 ones
+    # 0.7-1.2 ms)
     compact_eval_ms = float(options.get("compact_eval_ms", 2.0))
+    est = _eval_flops(acquisition_function, shapeX[0], shapeX[-2])
+    expensive = (compact == "auto" and est is not None
+                 and est >= float(options.get("compact_flops", 1e10)))
+    timed = compact == "auto" and est is None  # no estimate: time two evaluations
+    eval_ms = []
 
     def _graph(state, shape):
         if not use_graph:
@@ -473,8 +780,7 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     # expensive evaluations (the auto-compaction regime): the first capture
     # waits for the first status read, where the batch usually shrinks and is
     # captured at its new shape anyway; cheap ones are captured at once
-    defer = use_graph and compact == "auto"
-    expensive = False  # the first evaluation took >= compact_eval_ms
+    defer = use_graph and (expensive or timed)
     ga = None if defer else _graph(st, shapeX)
     full, active = st, None   # the whole batch; rows of `full` that `st` holds
     shrinks = []
@@ -504,12 +810,16 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
                                    nacc=st.nacc, lower=lo, upper=hi, c1=1e-4, ftol=ftol,
                                    pgtol=pgtol, min_alpha=1e-12)
             check(lib().bo_lbfgs_step_v(ctypes.byref(a), stream), "lbfgs_step")
-        if defer and it == 0:
-            torch.cuda.synchronize(X0.device)  # one eager evaluation timed
-            expensive = 1e3 * (time.monotonic() - t0) >= compact_eval_ms
-            if not expensive:
-                defer = False
-                ga = _graph(st, shapeX)
+        if timed and it < 2:
+            torch.cuda.synchronize(X0.device)  # two eager evaluations timed, the min kept
+            eval_ms.append(1e3 * (time.monotonic() - (t0 if it == 0 else t_prev)))
+            t_prev = time.monotonic()
+            if it == 1:
+                timed = False
+                expensive = min(eval_ms) >= compact_eval_ms
+                if not expensive and defer:
+                    defer = False
+                    ga = _graph(st, shapeX)
         if (it + 1) % check_every == 0 or it == max_evals - 1:
             if ga is not None:
                 ga.check_status()
@@ -519,8 +829,7 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
                 break
             if timeout_sec is not None and time.monotonic() - t0 > timeout_sec:
                 break
-            shrink = compact is True or (compact == "auto" and (
-                expensive or 1e3 * (time.monotonic() - t0) / (it + 1) >= compact_eval_ms))
+            shrink = compact is True or (compact == "auto" and expensive)
             if shrink and 2 * n_run <= st.B and st.B - n_run >= compact_min:
                 keep = running.nonzero().flatten()
                 if active is None:
@@ -557,52 +866,163 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     return cands, acq
 
 
-def generate_in_chunks(acq_function, ics, bounds, batch_limit, options, gen_candidates):
+def generate_in_chunks(acq_function, ics, bounds, batch_limit, options, gen_candidates,
+                       fixed_features=None, timeout_sec=None):
     """_optimize_acqf_batch's loop over batch_limit chunks of the initial
-    conditions (optimize.py:335-365): (candidates, values, any
-    OptimizationWarning)."""
+    conditions (optimize.py:277-326): ``timeout_sec`` is shared evenly by the
+    chunks, an all-infinite bound is passed as None.  Returns (candidates,
+    values, the OptimizationWarnings the chunks raised)."""
     gen_options = {k: v for k, v in (options or {}).items() if k not in INIT_OPTION_KEYS}
-    cands, vals, warned = [], [], False
-    for chunk in ics.split(max(1, batch_limit)):
+    chunks = ics.split(max(1, batch_limit))
+    t_chunk = timeout_sec / len(chunks) if timeout_sec is not None and len(chunks) else None
+    lo = None if bounds[0].isinf().all() else bounds[0]
+    hi = None if bounds[1].isinf().all() else bounds[1]
+    cands, vals, opt_ws = [], [], []
+    for chunk in chunks:
         with warnings.catch_warnings(record=True) as w:
             warnings.simplefilter("always", category=OptimizationWarning)
-            c, v = gen_candidates(chunk, acq_function, lower_bounds=bounds[0],
-                                  upper_bounds=bounds[1], options=gen_options)
-        warned |= any(issubclass(x.category, OptimizationWarning) for x in w)
+            c, v = gen_candidates(chunk, acq_function, lower_bounds=lo, upper_bounds=hi,
+                                  options=gen_options, fixed_features=fixed_features,
+                                  timeout_sec=t_chunk)
+        opt_ws += [x for x in w if issubclass(x.category, OptimizationWarning)]
+        for x in w:  # everything else is passed on, as the reference's recorder does not
+            if not issubclass(x.category, OptimizationWarning):
+                warnings.warn_explicit(x.message, x.category, x.filename, x.lineno)
         cands.append(c)
-        vals.append(v.reshape(-1))
+        vals.append(v)
     if not cands:
-        return ics.clone(), ics.new_empty(0), False
-    return torch.cat(cands), torch.cat(vals), warned
+        return ics.clone(), ics.new_empty(0), opt_ws
+    if vals[0].ndim == 0:
+        return torch.cat(cands), torch.stack(vals), opt_ws
+    return torch.cat(cands), torch.cat(vals).flatten(), opt_ws
 
 
-def optimize_acqf(acq_function, bounds, q, num_restarts, raw_samples=None, options=None,
-                  batch_initial_conditions=None, return_best_only=True, gen_candidates=None,
-                  sequential=False, retry_on_optimization_warning=True, **kwargs):
-    """optim/optimize.py:397-543 -> _optimize_acqf_batch (:246-394): raw-sample
-    initialisation, batch_limit chunks through gen_candidates_scipy, one retry
-    on OptimizationWarning, argmax over restarts."""
-    if sequential:
-        raise NotImplementedError("sequential greedy optimisation is out of scope")
+def _validate_optimize_inputs(bounds, raw_samples, batch_initial_conditions, ic_generator,
+                              inequality_constraints) -> None:
+    """OptimizeAcqfInputs.__post_init__ (optimize.py:94-128)."""
+    if inequality_constraints is None and not (bounds.ndim == 2 and bounds.shape[0] == 2):
+        raise ValueError(f"bounds should be a `2 x d` tensor, current shape: {list(bounds.shape)}.")
+    d = bounds.shape[1]
+    if batch_initial_conditions is not None:
+        shp = batch_initial_conditions.shape
+        if len(shp) not in (2, 3):
+            raise ValueError("batch_initial_conditions must be 2-dimensional or 3-dimensional. "
+                             f"Its shape is {shp}.")
+        if shp[-1] != d:
+            raise ValueError(f"batch_initial_conditions.shape[-1] must be {d}. The shape is {shp}.")
+    elif ic_generator is None and raw_samples is None:
+        raise ValueError("Must specify `raw_samples` when `batch_initial_conditions` is None`.")
+
+
+def _optimize_acqf_batch(acq_function, bounds, q, num_restarts, raw_samples, options,
+                         fixed_features, post_processing_func, batch_initial_conditions,
+                         return_best_only, gen_candidates, ic_generator, timeout_sec,
+                         retry_on_optimization_warning, ic_gen_kwargs):
+    """optimize.py:246-394."""
     options = options or {}
-    gen_candidates = gen_candidates or gen_candidates_scipy
-    if batch_initial_conditions is None:
-        if raw_samples is None:
-            raise ValueError("Must specify `raw_samples` when `batch_initial_conditions` is None`.")
-        batch_initial_conditions = gen_batch_initial_conditions(
-            acq_function, bounds, q, num_restarts, raw_samples, options=options)
+    provided = batch_initial_conditions is not None
+    ic_gen = ic_generator or gen_batch_initial_conditions
+
+    def _ics():
+        return ic_gen(acq_function=acq_function, bounds=bounds, q=q, num_restarts=num_restarts,
+                      raw_samples=raw_samples, fixed_features=fixed_features, options=options,
+                      **ic_gen_kwargs)
+
+    ics = batch_initial_conditions if provided else _ics()
     batch_limit = options.get("batch_limit", num_restarts)
 
-    def _run(ics):
-        return generate_in_chunks(acq_function, ics, bounds, batch_limit, options, gen_candidates)
+    def _run(x0):
+        return generate_in_chunks(acq_function, x0, bounds, batch_limit, options, gen_candidates,
+                                  fixed_features=fixed_features, timeout_sec=timeout_sec)
 
-    cands, vals, warned = _run(batch_initial_conditions)
-    if retry_on_optimization_warning and warned:
-        new_ics = gen_batch_initial_conditions(acq_function, bounds, q, num_restarts,
-                                               raw_samples or num_restarts, options=options)
-        cands, vals, warned = _run(new_ics)
+    cands, vals, ws = _run(ics)
+    if ws and retry_on_optimization_warning:
+        msgs = [str(w.message) for w in ws]
+        if provided:
+            warnings.warn(f"Optimization failed in `gen_candidates_scipy` with the following "
+                          f"warning(s):\n{msgs}\nBecause you specified `batch_initial_conditions`, "
+                          "optimization will not be retried with new initial conditions and will "
+                          "proceed with the current solution. Suggested remediation: Try again "
+                          "with different `batch_initial_conditions`, or don't provide "
+                          "`batch_initial_conditions.`", RuntimeWarning)
+        else:
+            warnings.warn(f"Optimization failed in `gen_candidates_scipy` with the following "
+                          f"warning(s):\n{msgs}\nTrying again with a new set of initial "
+                          "conditions.", RuntimeWarning)
+            cands, vals, ws = _run(_ics())
+            if ws:
+                warnings.warn("Optimization failed on the second try, after generating a new set "
+                              "of initial conditions.", RuntimeWarning)
+    if post_processing_func is not None:
+        cands = post_processing_func(cands)
+        with torch.no_grad():
+            vals = torch.cat([acq_function(c) for c in cands.split(batch_limit, dim=0)], dim=0)
     _check_deferred(cands)
     if return_best_only:
         best = torch.argmax(vals.view(-1), dim=0)
         return cands[best], vals[best]
     return cands, vals
+
+
+def optimize_acqf(acq_function, bounds, q, num_restarts, raw_samples=None, options=None,
+                  inequality_constraints=None, equality_constraints=None,
+                  nonlinear_inequality_constraints=None, fixed_features=None,
+                  post_processing_func=None, batch_initial_conditions=None,
+                  return_best_only=True, gen_candidates=None, sequential=False, *,
+                  ic_generator=None, timeout_sec=None, return_full_tree=False,
+                  retry_on_optimization_warning=True, **ic_gen_kwargs):
+    """optim/optimize.py:397-564: the all-fixed shortcut (:140-159), sequential
+    greedy q (:202-243) or the joint batch (:246-394) -- raw-sample
+    initialisation, batch_limit chunks through ``gen_candidates`` (default
+    gen_candidates_scipy; gen_candidates_device is the device-resident one)
+    with fixed features and the timeout split over the chunks, one retry on
+    OptimizationWarning, post-processing, argmax over restarts.
+
+    Linear / nonlinear parameter constraints raise UnsupportedError (they need
+    SLSQP and the reference's polytope sampler, not on this path); every other
+    argument has the reference's meaning.  ``return_full_tree`` only matters
+    for one-shot acquisitions, which are not on this path."""
+    from .exceptions import UnsupportedError
+    _reject_constraints(inequality_constraints, equality_constraints,
+                        nonlinear_inequality_constraints)
+    gen_candidates = gen_candidates or gen_candidates_scipy
+    _validate_optimize_inputs(bounds, raw_samples, batch_initial_conditions, ic_generator,
+                              inequality_constraints)
+    if fixed_features is not None and len(fixed_features) == bounds.shape[-1]:
+        X = torch.tensor([fixed_features[i] for i in range(bounds.shape[-1])],
+                         device=bounds.device, dtype=bounds.dtype)
+        X = X.expand(q, *X.shape)
+        with torch.no_grad():
+            return X, acq_function(X)
+    args = dict(acq_function=acq_function, bounds=bounds, q=q, num_restarts=num_restarts,
+                raw_samples=raw_samples, options=options, fixed_features=fixed_features,
+                post_processing_func=post_processing_func,
+                batch_initial_conditions=batch_initial_conditions,
+                return_best_only=return_best_only, gen_candidates=gen_candidates,
+                ic_generator=ic_generator, timeout_sec=timeout_sec,
+                retry_on_optimization_warning=retry_on_optimization_warning,
+                ic_gen_kwargs=ic_gen_kwargs)
+    if not (sequential and q > 1):
+        return _optimize_acqf_batch(**args)
+    # _validate_sequential_inputs (optimize.py:162-199), then q greedy picks
+    if batch_initial_conditions is not None:
+        raise UnsupportedError("`batch_initial_conditions` is not supported for sequential "
+                               "optimization. Either avoid specifying `batch_initial_conditions` "
+                               "to use the custom initializer or use the `ic_generator` kwarg to "
+                               "generate initial conditions for the case of nonlinear inequality "
+                               "constraints.")
+    if not return_best_only:
+        raise NotImplementedError("`return_best_only=False` only supported for joint optimization.")
+    args.update(q=1, batch_initial_conditions=None, return_best_only=True,
+                timeout_sec=timeout_sec / q if timeout_sec is not None else None)
+    base_pending = acq_function.X_pending
+    picks, values = [], []
+    for _ in range(q):
+        c, v = _optimize_acqf_batch(**args)
+        picks.append(c)
+        values.append(v)
+        cands = torch.cat(picks, dim=-2)
+        acq_function.set_X_pending(torch.cat([base_pending, cands], dim=-2)
+                                   if base_pending is not None else cands)
+    acq_function.set_X_pending(base_pending)
+    return cands, torch.stack(values)

@@ -164,20 +164,36 @@ def test_restart_shards_reproduce_the_whole_batch():
     torch.testing.assert_close(v_sh, v_all, atol=1e-12, rtol=1e-10)
 
 
-def test_restart_compaction_is_exact():
+def test_restart_compaction_matches_and_is_deterministic():
     """Stopped restarts leave the batch (their states set aside, the graph
     re-captured for the smaller shape): every restart ends where it ends
-    without compaction."""
-    from botorch_amd.optim import gen_candidates_device
+    without compaction, to rounding (the smaller batch's evaluations take
+    another split plan, so f and g are summed in another order); a compacted
+    run repeats bit for bit, and "auto" decides from the deterministic cost
+    estimate (C3-sized qEI shrinks, a small one does not)."""
+    from botorch_amd.optim import _eval_flops, gen_candidates_device
     acqf, bounds, ics = _qei_setup()
     c0, v0 = gen_candidates_device(ics, acqf, bounds[0], bounds[1], options={"compact": False})
     s0 = gen_candidates_device.last_state.status.clone()
-    c1, v1 = gen_candidates_device(ics, acqf, bounds[0], bounds[1],
-                                   options={"compact": True, "compact_min": 1, "check_every": 2})
-    assert gen_candidates_device.last_shrinks, "no compaction happened"
+    opts = {"compact": True, "compact_min": 1, "check_every": 2}
+    c1, v1 = gen_candidates_device(ics, acqf, bounds[0], bounds[1], options=opts)
+    sh = list(gen_candidates_device.last_shrinks)
+    assert sh, "no compaction happened"
     assert torch.equal(gen_candidates_device.last_state.status, s0)
     torch.testing.assert_close(c1, c0, atol=1e-8, rtol=0)
     torch.testing.assert_close(v1, v0, atol=1e-12, rtol=1e-10)
+    c2, v2 = gen_candidates_device(ics, acqf, bounds[0], bounds[1], options=opts)
+    assert gen_candidates_device.last_shrinks == sh
+    assert torch.equal(c2, c1) and torch.equal(v2, v1)
+    n = acqf.model.train_inputs[0].shape[0]
+    q = ics.shape[-2]
+    assert _eval_flops(acqf, ics.shape[0], q) == 2.0 * ics.shape[0] * q * n * n
+    gen_candidates_device(ics, acqf, bounds[0], bounds[1], options={"compact_flops": 1.0,
+                                                                     "compact_min": 1})
+    assert gen_candidates_device.last_shrinks  # "auto" with a tiny threshold shrinks
+    gen_candidates_device(ics, acqf, bounds[0], bounds[1], options={"compact_flops": 1e30,
+                                                                     "compact_min": 1})
+    assert not gen_candidates_device.last_shrinks
 
 
 def test_kernel_unconstrained_and_fixed_variables():

@@ -116,3 +116,23 @@ def test_logei_known_answers_batch(route):
     v = f(samples, -1.0).exp()
     assert 1.999 <= v[0].item() <= 2.0 + TAU_RELU + TAU_MAX
     assert 1.0 <= v[1].item() <= 1.0 + TAU_RELU + TAU_MAX
+
+
+def test_anchored_reductions_infinite_slices():
+    """safe_math.py:149-187's contract for infinite maxima: a +inf entry
+    makes the slice +inf (gradient only to it), an all -inf slice stays -inf,
+    finite slices are the plain logsumexp with softmax gradients."""
+    from botorch_amd.safe_math import fatmax, logmeanexp, logsumexp
+    x = torch.tensor([[math.inf, 1.0, 2.0], [-math.inf, -math.inf, -math.inf], [0.5, 1.5, -2.0]],
+                     dtype=torch.float64, requires_grad=True)
+    v = logsumexp(x, dim=-1)
+    assert v[0].item() == math.inf and v[1].item() == -math.inf
+    torch.testing.assert_close(v[2], torch.logsumexp(x[2].detach(), dim=0))
+    (g,) = torch.autograd.grad(v[[0, 2]].sum(), x)
+    torch.testing.assert_close(g[0], torch.tensor([1.0, 0.0, 0.0], dtype=torch.float64))
+    torch.testing.assert_close(g[2], torch.softmax(x[2].detach(), dim=0))
+    assert torch.isfinite(fatmax(x[2:], dim=-1, tau=0.1)).all()
+    assert fatmax(x[:1], dim=-1).item() == math.inf
+    y = torch.randn(4, 5, 3, dtype=torch.float64)
+    torch.testing.assert_close(logmeanexp(y, dim=(0, 1)),
+                               torch.logsumexp(y, dim=(0, 1)) - math.log(20))
