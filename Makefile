@@ -12,8 +12,21 @@ CXX ?= g++
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -pthread -Wall
 HDR := $(wildcard botorch_amd/csrc/*.h) include/botorch_amd.h
 LIB := botorch_amd/libbotorch_amd.so
+# the torch operators (TORCH_LIBRARY): host C++ against torch's ROCm headers,
+# linked to the kernel library
+TORCH_DIR ?= $(shell python3 -c "import os, torch; print(os.path.dirname(torch.__file__))")
+TORCH_LIB := botorch_amd/libbotorch_amd_torch.so
+TORCH_SRC := $(wildcard botorch_amd/csrc/torch/*.cpp)
+TORCH_FLAGS := -O2 -std=c++17 -fPIC -shared -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 \
+               -I$(TORCH_DIR)/include -I$(TORCH_DIR)/include/torch/csrc/api/include \
+               -I/opt/rocm/include -Wall -Wno-unused-function
 
-all: $(LIB)
+all: $(LIB) $(TORCH_LIB)
+
+$(TORCH_LIB): $(TORCH_SRC) include/botorch_amd.h $(LIB)
+	$(CXX) $(TORCH_FLAGS) $(TORCH_SRC) -o $@ -Lbotorch_amd -lbotorch_amd \
+	  -L$(TORCH_DIR)/lib -ltorch -ltorch_cpu -lc10 -lc10_hip -ltorch_hip \
+	  -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(TORCH_DIR)/lib
 
 build/%.o: botorch_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
@@ -28,6 +41,6 @@ $(LIB): $(OBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(OBJ) -pthread -o $@
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(TORCH_LIB)
 
 .PHONY: all clean

@@ -242,6 +242,27 @@ def lib():
     return _lib
 
 
+TORCH_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libbotorch_amd_torch.so")
+_torch_ops_loaded = False
+
+
+def torch_ops():
+    """Load (once) the TORCH_LIBRARY operators of csrc/torch/bo_torch.cpp
+    (libbotorch_amd_torch.so: torch.ops.bo.qmc_acq_native, ladder_defer,
+    ladder_poll, post_timing[_read]); raise loudly if absent."""
+    global _torch_ops_loaded
+    if not _torch_ops_loaded:
+        lib()  # the kernel library it links against (and its ABI check)
+        if not os.path.exists(TORCH_LIB_PATH):
+            raise NativeLibraryMissing(
+                f"{TORCH_LIB_PATH} not found: build it with `make` (or __graft_entry__.build()).")
+        import torch
+        torch.ops.load_library(TORCH_LIB_PATH)
+        _torch_ops_loaded = True
+    import torch
+    return torch.ops.bo
+
+
 def exported_symbols():
     return list(_SIGNATURES)
 

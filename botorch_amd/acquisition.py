@@ -165,6 +165,20 @@ def _fused_mc(X3: torch.Tensor, acqf, mode: int, best_f: float, best_f_s, Z: tor
     need_grad = torch.is_grad_enabled() and X3.requires_grad
     lp = getattr(acqf, "_log_params", None)
     fat, tau_relu, tau_max = lp if lp is not None else (True, 1.0, 1.0)
+    dev = X3.device
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if X3.dtype != torch.float64:  # the model computes in fp64; the value returns in X's dtype
+        return _fused_mc(X3.to(torch.float64), acqf, mode, best_f, best_f_s, Z).to(X3.dtype)
+    if not need_grad and not kernels.SYNC_LADDER and idx not in kernels._CAPTURE:
+        # eager forward-only: ONE native call issues the whole chain and defers
+        # the ladder status (the previous call's is returned and acted on here)
+        outs = _lib.torch_ops().qmc_acq_native(
+            X3.contiguous(), cache.Xt_scaled, cache.U, cache.Linv, cache.beta, cache.lengthscale,
+            Z, best_f_s, int(cache.kind), int(mode), int(cache.n), float(cache.outputscale),
+            float(cache.constant), float(ymean), float(ystd), float(best_f), bool(fat),
+            float(tau_relu), float(tau_max), False, kernels.kxt_cap(dev), True)
+        kernels.ladder_prev_outcome(outs[8], idx, type(acqf).__name__)
+        return outs[0]
     outs = torch.ops.bo.qmc_acq(
         X3, cache.Xt, cache.Xt_scaled, cache.U, cache.Linv, cache.beta, cache.alpha,
         cache.lengthscale, Z, best_f_s, int(cache.kind), int(mode), float(cache.outputscale),

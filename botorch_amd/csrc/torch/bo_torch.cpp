@@ -1,0 +1,325 @@
+// PyTorch-ROCm operators of the fused MC-acquisition forward, in C++.
+//
+// the hot path is bound as PyTorch custom ops registered with
+// TORCH_LIBRARY.  One call of bo::qmc_acq_native issues the whole fused qEI /
+// qLogEI / posterior chain of acquisition/monte_carlo.py:253-289 (+ logei.py:
+// 137-234) for B t-batches -- rows prepared, K*x^T built, the R = K*x L^-T
+// contraction with its R R^T / R beta epilogue, the per-t-batch finalisation
+// with the jitter ladder and the MC reduction, and (with need_grad) the
+// backward's W^T -- on the caller's current HIP stream, with the buffers from
+// torch's caching allocator and no Python between the launches.  The kernels
+// are the C ABI of include/botorch_amd.h (libbotorch_amd.so); this library
+// adds only the host sequence, so the ctypes binding (botorch_amd/_lib.py)
+// and these ops drive the same code.
+//
+// The jitter-ladder status of a forward-only call is deferred, as [G]
+// psd_safe_cholesky's host check would otherwise synchronise every call: the
+// status is reduced on the device and copied to pinned host memory behind an
+// event, and read one call later (or at the driver's own sync, bo::ladder_poll)
+// -- two slots per device, so reading call t-1's status never waits on call t.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
+#include <torch/library.h>
+
+#include <array>
+#include <mutex>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "../../../include/botorch_amd.h"
+
+namespace {
+
+void ck(int rc, const char* what) {
+  TORCH_CHECK(rc == BO_OK, "botorch_amd ", what, ": ", bo_last_error());
+}
+void hk(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "botorch_amd ", what, ": ", hipGetErrorString(e));
+}
+const double* cp(const at::Tensor& t) { return t.defined() && t.numel() ? t.data_ptr<double>() : nullptr; }
+double* mp(const at::Tensor& t) { return t.defined() && t.numel() ? t.data_ptr<double>() : nullptr; }
+
+void check_f64(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "bo::qmc_acq_native: ", name, " must be a ROCm device tensor");
+  TORCH_CHECK(t.scalar_type() == at::kDouble, "bo::qmc_acq_native: ", name, " must be fp64");
+  TORCH_CHECK(t.is_contiguous(), "bo::qmc_acq_native: ", name, " must be contiguous");
+}
+
+// ---- deferred ladder status ---------------------------------------------------------
+struct Slot {
+  double* host = nullptr;   // pinned [info_max, jitter_max]
+  double* dev = nullptr;    // device [info_max, jitter_max]
+  hipEvent_t ev = nullptr;
+};
+struct DeviceLadder {
+  std::array<Slot, 2> slot;
+  int pending = -1;  // slot of the forward whose status is still unread
+};
+std::mutex g_ladder_mu;
+std::unordered_map<int, DeviceLadder> g_ladder;
+
+DeviceLadder& ladder_for(int dev) {
+  auto& L = g_ladder[dev];
+  if (!L.slot[0].host) {
+    for (auto& s : L.slot) {
+      hk(hipHostMalloc(reinterpret_cast<void**>(&s.host), 2 * sizeof(double), hipHostMallocDefault),
+         "hipHostMalloc");
+      hk(hipMalloc(reinterpret_cast<void**>(&s.dev), 2 * sizeof(double)), "hipMalloc");
+      hk(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
+    }
+  }
+  return L;
+}
+
+// [has_status, info_max, jitter_max] of the pending slot (waits for it), and
+// clears it.  Caller holds g_ladder_mu.
+at::Tensor take_pending(DeviceLadder& L) {
+  auto out = at::zeros({3}, at::TensorOptions().dtype(at::kDouble));
+  if (L.pending >= 0) {
+    Slot& s = L.slot[L.pending];
+    hk(hipEventSynchronize(s.ev), "hipEventSynchronize");
+    auto* o = out.data_ptr<double>();
+    o[0] = 1.0;
+    o[1] = s.host[0];
+    o[2] = s.host[1];
+    L.pending = -1;
+  }
+  return out;
+}
+
+// Enqueue this call's status into a free slot, then return (and clear) the
+// previous call's.
+at::Tensor defer_status(const at::Tensor& info, const at::Tensor& jitter, void* stream, int dev) {
+  std::lock_guard<std::mutex> lk(g_ladder_mu);
+  auto& L = ladder_for(dev);
+  const int prev = L.pending;
+  const int mine = prev == 0 ? 1 : 0;
+  Slot& s = L.slot[mine];
+  ck(bo_ladder_status(info.data_ptr<int>(), jitter.data_ptr<double>(), info.numel(), s.dev, stream),
+     "ladder_status");
+  hk(hipMemcpyAsync(s.host, s.dev, 2 * sizeof(double), hipMemcpyDeviceToHost,
+                    static_cast<hipStream_t>(stream)), "hipMemcpyAsync");
+  hk(hipEventRecord(s.ev, static_cast<hipStream_t>(stream)), "hipEventRecord");
+  auto out = take_pending(L);  // the previous forward's (enqueued long before)
+  L.pending = mine;
+  return out;
+}
+
+// ---- post_partials launch timing (bench.py: HIP events around the launch) ------------
+std::mutex g_time_mu;
+bool g_time_on = false;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_time_ev;
+
+hipEvent_t timing_event(void* stream) {
+  hipEvent_t e;
+  hk(hipEventCreate(&e), "hipEventCreate");
+  hk(hipEventRecord(e, static_cast<hipStream_t>(stream)), "hipEventRecord");
+  return e;
+}
+
+// ---- the fused forward ------------------------------------------------------------------
+std::vector<at::Tensor> qmc_acq_native(
+    const at::Tensor& X, const at::Tensor& Xt_scaled, const at::Tensor& U, const at::Tensor& Linv,
+    const at::Tensor& beta, const at::Tensor& lengthscale, const at::Tensor& Z,
+    const c10::optional<at::Tensor>& best_f_s, int64_t kind, int64_t mode, int64_t n,
+    double outputscale, double constant, double ymean, double ystd, double best_f, bool fat,
+    double tau_relu, double tau_max, bool need_grad, int64_t kxt_cap, bool defer_ladder) {
+  check_f64(X, "X");
+  check_f64(Xt_scaled, "Xt_scaled");
+  check_f64(U, "U");
+  check_f64(beta, "beta");
+  check_f64(lengthscale, "lengthscale");
+  check_f64(Z, "Z");
+  TORCH_CHECK(X.dim() == 3, "bo::qmc_acq_native: X must be B x q x d");
+  const int B = static_cast<int>(X.size(0)), q = static_cast<int>(X.size(1)),
+            d = static_cast<int>(X.size(2));
+  TORCH_CHECK(Xt_scaled.size(0) == n && lengthscale.numel() == d,
+              "bo::qmc_acq_native: model and X disagree (n, d)");
+  TORCH_CHECK(Z.dim() == 2 && Z.size(1) == q, "bo::qmc_acq_native: Z must be S x q");
+  if (need_grad) check_f64(Linv, "Linv");
+  const int dev = X.device().index();
+  void* st = c10::hip::getCurrentHIPStream(dev).stream();
+  auto f64 = X.options().dtype(at::kDouble);
+  const int64_t np = U.size(0);
+
+  int Qp = 0, nrows = 0, nC = 0;
+  ck(bo_post_geometry(B, q, n, &Qp, &nrows, &nC), "post_geometry");
+  auto Xq = at::empty({nrows, 8}, f64);
+  auto Spart = at::empty({nC, nrows / 16, 16, 16}, f64);
+  auto mpart = at::empty({nC, nrows}, f64);
+  ck(bo_prepare_rows(X.data_ptr<double>(), B, q, d, lengthscale.data_ptr<double>(),
+                     Xq.data_ptr<double>(), st), "prepare_rows");
+  at::Tensor Rt = need_grad ? at::empty({int64_t(nC) * 128, nrows}, f64) : at::Tensor();
+  int kc = 0;
+  int64_t we = 0;
+  ck(bo_post_split_plan(B, q, n, 0, &kc, &we), "post_split_plan");
+  at::Tensor work = kc ? at::empty({std::max<int64_t>(we, 1)}, f64) : at::Tensor();
+  at::Tensor Kt;
+  if (np * int64_t(nrows) * 8 <= kxt_cap) {
+    Kt = at::empty({np, nrows}, f64);
+    ck(bo_post_kxt(int(kind), Xq.data_ptr<double>(), B, q, d, Xt_scaled.data_ptr<double>(), n,
+                   outputscale, Kt.data_ptr<double>(), st), "post_kxt");
+  }
+  BoPostPartialsArgs pa{};
+  pa.struct_size = sizeof(pa);
+  pa.abi_version = BO_ABI_VERSION;
+  pa.kind = int(kind);
+  pa.B = B;
+  pa.q = q;
+  pa.d = d;
+  pa.Xq = Xq.data_ptr<double>();
+  pa.Xt_scaled = Xt_scaled.data_ptr<double>();
+  pa.n = n;
+  pa.U = U.data_ptr<double>();
+  pa.ldu = np;
+  pa.beta = beta.data_ptr<double>();
+  pa.outputscale = outputscale;
+  pa.Spart = Spart.data_ptr<double>();
+  pa.mpart = mpart.data_ptr<double>();
+  pa.Rt = mp(Rt);
+  pa.kc_len = kc;
+  pa.work = mp(work);
+  pa.Kt = cp(Kt);
+  hipEvent_t t0 = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_time_mu);
+    if (g_time_on) t0 = timing_event(st);
+  }
+  ck(bo_post_partials_v(&pa, st), "post_partials");
+  if (t0) {
+    std::lock_guard<std::mutex> lk(g_time_mu);
+    g_time_ev.emplace_back(t0, timing_event(st));
+  }
+
+  auto acq = at::empty({B}, f64);
+  auto info = at::empty({B}, X.options().dtype(at::kInt));
+  auto jit = at::empty({B}, f64);
+  at::Tensor mean = need_grad ? at::empty({B, q}, f64) : at::empty({0}, f64);
+  at::Tensor L = need_grad ? at::empty({B, q, q}, f64) : at::empty({0}, f64);
+  const at::Tensor bfs = best_f_s.has_value() ? best_f_s->contiguous() : at::Tensor();
+  BoQmcFinalizeArgs fa{};
+  fa.struct_size = sizeof(fa);
+  fa.abi_version = BO_ABI_VERSION;
+  fa.kind = int(kind);
+  fa.mode = int(mode);
+  fa.B = B;
+  fa.q = q;
+  fa.Xq = Xq.data_ptr<double>();
+  fa.Spart = Spart.data_ptr<double>();
+  fa.mpart = mpart.data_ptr<double>();
+  fa.n = n;
+  fa.outputscale = outputscale;
+  fa.constant = constant;
+  fa.ymean = ymean;
+  fa.ystd = ystd;
+  fa.Z = Z.data_ptr<double>();
+  fa.S = static_cast<int32_t>(Z.size(0));
+  fa.max_tries = 6;        // botorch/__init__.py:47 (cholesky_max_tries)
+  fa.best_f = best_f;
+  fa.best_f_s = cp(bfs);
+  fa.jitter0 = 1e-8;       // [G] cholesky_jitter, double
+  fa.acq = acq.data_ptr<double>();
+  fa.mean_out = mp(mean);
+  fa.L_out = mp(L);
+  fa.info_out = info.data_ptr<int>();
+  fa.jitter_out = jit.data_ptr<double>();
+  fa.fat = fat ? 1 : 0;
+  fa.tau_relu = tau_relu;
+  fa.tau_max = tau_max;
+  ck(bo_qmc_finalize_v(&fa, st), "qmc_finalize");
+
+  at::Tensor Wt = at::empty({0}, f64);
+  if (need_grad) {
+    // W^T = L^-T R^T: stream-K below four tiles per slot, the 8 x 8
+    // super-tile grid where it fills the chip, the structured GEMM otherwise
+    // (kernels.w_matrix)
+    int wkc = 0;
+    int64_t wwe = 0;
+    ck(bo_post_w_work(B, q, n, &wkc, &wwe), "post_w_work");
+    const int nI = nrows / 128;
+    if (wkc == -1) {
+      Wt = at::empty({np, nrows}, f64);
+      auto ww = at::empty({std::max<int64_t>(wwe, 1)}, f64);
+      ck(bo_post_w_split(Linv.data_ptr<double>(), np, Rt.data_ptr<double>(), B, q, n,
+                         Wt.data_ptr<double>(), ww.data_ptr<double>(), st), "post_w_split");
+    } else if (int64_t(nC) * nI >= 512 && nC % 8 == 0 && nI % 8 == 0) {
+      Wt = at::empty({np, nrows}, f64);
+      ck(bo_post_w(Linv.data_ptr<double>(), np, Rt.data_ptr<double>(), B, q, n,
+                   Wt.data_ptr<double>(), st), "post_w");
+    } else {
+      auto W = at::empty({nrows, np}, f64);
+      ck(bo_gemm_f64(1, 1, nrows, int(np), nC * 128, 1.0, Rt.data_ptr<double>(), nrows, 0,
+                     U.data_ptr<double>(), np, 0, 0.0, W.data_ptr<double>(), np, 0, 1,
+                     BO_GEMM_B_LOWER, st), "w_matrix");
+      Wt = W.t().contiguous();
+    }
+  }
+  at::Tensor prev = at::zeros({3}, at::TensorOptions().dtype(at::kDouble));
+  if (defer_ladder && B > 0) prev = defer_status(info, jit, st, dev);
+  if (!need_grad) {
+    Xq = at::empty({0}, f64);
+    Rt = at::empty({0}, f64);
+  }
+  return {acq, mean, L, Xq, Rt, Wt, jit, info, prev};
+}
+
+at::Tensor ladder_defer(const at::Tensor& info, const at::Tensor& jitter) {
+  TORCH_CHECK(info.is_cuda() && info.scalar_type() == at::kInt && info.is_contiguous(),
+              "bo::ladder_defer: info must be a contiguous int32 device tensor");
+  TORCH_CHECK(jitter.is_cuda() && jitter.scalar_type() == at::kDouble && jitter.is_contiguous(),
+              "bo::ladder_defer: jitter must be a contiguous fp64 device tensor");
+  if (info.numel() == 0) return at::zeros({3}, at::TensorOptions().dtype(at::kDouble));
+  const int dev = info.device().index();
+  return defer_status(info, jitter, c10::hip::getCurrentHIPStream(dev).stream(), dev);
+}
+
+at::Tensor ladder_poll(int64_t device) {
+  std::lock_guard<std::mutex> lk(g_ladder_mu);
+  auto it = g_ladder.find(static_cast<int>(device));
+  if (it == g_ladder.end()) return at::zeros({3}, at::TensorOptions().dtype(at::kDouble));
+  return take_pending(it->second);
+}
+
+void post_timing(bool on) {
+  std::lock_guard<std::mutex> lk(g_time_mu);
+  g_time_on = on;
+}
+
+// Durations (ms) of the timed post_partials launches since the last read;
+// waits for the last one.
+at::Tensor post_timing_read() {
+  std::lock_guard<std::mutex> lk(g_time_mu);
+  auto out = at::empty({int64_t(g_time_ev.size())}, at::TensorOptions().dtype(at::kDouble));
+  auto* o = out.data_ptr<double>();
+  for (size_t i = 0; i < g_time_ev.size(); ++i) {
+    float ms = 0.f;
+    hk(hipEventSynchronize(g_time_ev[i].second), "hipEventSynchronize");
+    hk(hipEventElapsedTime(&ms, g_time_ev[i].first, g_time_ev[i].second), "hipEventElapsedTime");
+    o[i] = ms;
+    hk(hipEventDestroy(g_time_ev[i].first), "hipEventDestroy");
+    hk(hipEventDestroy(g_time_ev[i].second), "hipEventDestroy");
+  }
+  g_time_ev.clear();
+  return out;
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(bo, m) {
+  m.def("qmc_acq_native(Tensor X, Tensor Xt_scaled, Tensor U, Tensor Linv, Tensor beta, "
+        "Tensor lengthscale, Tensor Z, Tensor? best_f_s, int kind, int mode, int n, "
+        "float outputscale, float constant, float ymean, float ystd, float best_f, bool fat, "
+        "float tau_relu, float tau_max, bool need_grad, int kxt_cap, bool defer_ladder) "
+        "-> Tensor[]");
+  m.def("ladder_defer(Tensor info, Tensor jitter) -> Tensor");
+  m.def("ladder_poll(int device) -> Tensor", &ladder_poll);
+  m.def("post_timing(bool on) -> ()", &post_timing);
+  m.def("post_timing_read() -> Tensor", &post_timing_read);
+}
+
+TORCH_LIBRARY_IMPL(bo, CUDA, m) {
+  m.impl("qmc_acq_native", &qmc_acq_native);
+  m.impl("ladder_defer", &ladder_defer);
+}

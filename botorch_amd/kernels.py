@@ -646,23 +646,38 @@ def post_backward(cache: GPCache, pp: PostPartials, W: Optional[WMat],
 # draining the queue every call.  Failed t-batches carry NaN values meanwhile.
 # BO_SYNC_LADDER=1 restores the per-call check.
 SYNC_LADDER = os.environ.get("BO_SYNC_LADDER", "0") == "1"
-_LADDER_PENDING = {}
-_LADDER_PINNED = {}
+# The deferred status itself lives in the native operators (bo::ladder_defer /
+# bo::ladder_poll, csrc/torch/bo_torch.cpp: two pinned slots + events per
+# device); here only the name of the acquisition whose status is pending.
+_LADDER_WHAT = {}
+
+
+def _dev_index(device) -> int:
+    d = torch.device(device)
+    return d.index if d.index is not None else torch.cuda.current_device()
+
+
+def ladder_prev_outcome(status: torch.Tensor, idx: int, what: str) -> None:
+    """Act on the previous deferred status [has, info_max, jitter_max] that a
+    native call returned, and record ``what`` as the name of the new pending
+    one."""
+    prev_what = _LADDER_WHAT.get(idx, what)
+    _LADDER_WHAT[idx] = what
+    has, info_max, jitter_max = status.tolist()
+    if has:
+        _ladder_outcome(info_max, jitter_max, prev_what)
 
 
 def check_ladder_status(device=None) -> None:
     """Raise NotPSDError / warn NumericalWarning for a deferred ladder status
     (waits for the forward that produced it); no-op when none is pending."""
-    keys = list(_LADDER_PENDING) if device is None else \
-        [torch.device(device).index if torch.device(device).index is not None
-         else torch.cuda.current_device()]
+    ops = _lib.torch_ops()
+    keys = list(_LADDER_WHAT) if device is None else [_dev_index(device)]
     for idx in keys:
-        item = _LADDER_PENDING.pop(idx, None)
-        if item is None:
-            continue
-        pinned, ev, what = item
-        ev.synchronize()
-        _ladder_outcome(float(pinned[0]), float(pinned[1]), what)
+        has, info_max, jitter_max = ops.ladder_poll(idx).tolist()
+        what = _LADDER_WHAT.pop(idx, "acquisition")
+        if has:
+            _ladder_outcome(info_max, jitter_max, what)
 
 
 def _ladder_outcome(info_max: float, jitter_max: float, what: str) -> None:
@@ -723,22 +738,9 @@ def raise_not_psd_deferred(info: torch.Tensor, jitter: torch.Tensor, what: str) 
         return
     if SYNC_LADDER or info.numel() == 0:
         return _raise_not_psd(info, jitter, what)
-    dev = info.device
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    check_ladder_status(dev)  # the previous call's status (one forward behind)
-    # one device word pair, one pinned pair and one event per device, reused:
-    # call t's status is read (after its event) before call t+1 writes them
-    bufs = _LADDER_PINNED.get(idx)
-    if bufs is None:
-        bufs = _LADDER_PINNED[idx] = (torch.empty(2, dtype=torch.float64, device=dev),
-                                      torch.empty(2, dtype=torch.float64, pin_memory=True),
-                                      torch.cuda.Event())
-    packed, pinned, ev = bufs
-    check(lib().bo_ladder_status(_p(info.contiguous()), _p(jitter.contiguous()), info.numel(),
-                                 _p(packed), _stream(dev)), "ladder_status")
-    pinned.copy_(packed, non_blocking=True)
-    ev.record(torch.cuda.current_stream(dev))
-    _LADDER_PENDING[idx] = (pinned, ev, what)
+    # this call's status is enqueued, the previous call's read (one forward behind)
+    prev = _lib.torch_ops().ladder_defer(info.contiguous(), jitter.contiguous())
+    ladder_prev_outcome(prev, _dev_index(info.device), what)
 
 
 def _raise_not_psd(info: torch.Tensor, jitter: torch.Tensor, what: str):

@@ -437,8 +437,12 @@ class SingleTaskGP(Model):
 
     def posterior(self, X: torch.Tensor, output_indices=None, observation_noise=False,
                   posterior_transform=None):
-        """botorch/models/gpytorch.py:405-466 (m > 1: :327-355)."""
+        """botorch/models/gpytorch.py:405-466 (m > 1: :327-355).  The model
+        computes in fp64: X of another floating dtype is promoted (the
+        gradient flows back through the cast)."""
         from .posteriors import GPyTorchPosterior, PosteriorList
+        if X.dtype != torch.float64:
+            X = X.to(torch.float64)
         if self._is_multi_output:
             idx = output_indices if output_indices is not None else range(self._num_outputs)
             prime_prediction_caches([self.models[i] for i in idx])

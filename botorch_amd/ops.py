@@ -288,17 +288,14 @@ def qmc_acq(X: Tensor, Xt: Tensor, Xt_scaled: Tensor, U: Tensor, Linv: Tensor, b
     Sobol samples and the qEI / qLogEI reduction, one launch each.  With
     need_grad also (mean, L, Xq, R^T, W^T) for the registered backward; the last
     output is the ladder status tensor (info)."""
-    c = _cache_from(Xt, Xt_scaled, lengthscale, U, beta, alpha, kind, outputscale, constant, Linv)
-    pp = kernels.post_partials(c, X, store_R=need_grad)
-    out = kernels.qmc_finalize(c, pp, mode, ymean, ystd, Z=Z, best_f=best_f, best_f_s=best_f_s,
-                               want_mean=need_grad, want_cov=False, want_L=need_grad,
-                               log_params=(fat, tau_relu, tau_max))
-    if not need_grad:
-        e = [X.new_empty(0, dtype=F64) for _ in range(5)]
-        return out["acq"], e[0], e[1], e[2], e[3], e[4], out["jitter"], out["info"]
-    W = kernels.w_matrix(c, pp)
-    Wt = W.t if W.kmajor else W.t.T.contiguous()
-    return out["acq"], out["mean"], out["L"], pp.Xq, pp.Rt, Wt, out["jitter"], out["info"]
+    # the whole host sequence is one native call (csrc/torch/bo_torch.cpp)
+    n = Xt.shape[0]
+    out = _lib.torch_ops().qmc_acq_native(
+        X.contiguous(), Xt_scaled, U, Linv, beta, lengthscale, Z.reshape(-1, X.shape[1]).contiguous(),
+        best_f_s, kind, mode, n, outputscale, constant, ymean, ystd, best_f, fat, tau_relu, tau_max,
+        need_grad, kernels.kxt_cap(X.device), False)
+    acq, mean, L, Xq, Rt, Wt, jit, info, _ = out
+    return acq, mean, L, Xq, Rt, Wt, jit, info
 
 
 @qmc_acq.register_fake

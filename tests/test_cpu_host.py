@@ -174,3 +174,20 @@ def test_settings_flags_mirror_reference():
     with settings.propagate_grads(True):
         with pytest.raises(UnsupportedError):
             m.prediction_cache()
+
+
+def test_native_torch_operators_load():
+    """The TORCH_LIBRARY operators (csrc/torch/bo_torch.cpp) load on the host
+    and declare their schemas; the ladder poll of a device that never
+    deferred anything reports no status (no device needed)."""
+    import torch
+    from botorch_amd import _lib
+    ops = _lib.torch_ops()
+    for name in ("qmc_acq_native", "ladder_defer", "ladder_poll", "post_timing",
+                 "post_timing_read"):
+        assert hasattr(ops, name), name
+    schema = str(torch.ops.bo.qmc_acq_native.default._schema)
+    assert "bool need_grad" in schema and "Tensor[]" in schema
+    assert torch.ops.bo.ladder_poll(7).tolist() == [0.0, 0.0, 0.0]
+    torch.ops.bo.post_timing(False)
+    assert torch.ops.bo.post_timing_read().numel() == 0
