@@ -37,6 +37,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -153,8 +154,28 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
 
   const int bid = blockIdx.x;
   int ci = 0, ii = 0, kbeg = 0, kend = 0;
+  int ci_long = 0, ci_short = 0;  // paired schedule: the workgroup's two column tiles
   if constexpr (SPLIT) {
     // segments come from the table below
+  } else if (grouped == 2) {
+    // Paired super-tiles (nC a multiple of 16): the grouped schedule below,
+    // but every workgroup runs a LONG column tile and then its SHORT partner
+    // of the mirrored column group (cg and nC/8 - 1 - cg), ci_long + ci_short
+    // = nC - 1, so every workgroup does nC + 1 k-blocks: the triangular
+    // k-ranges even out inside each workgroup instead of across the launch's
+    // tail (the heaviest-first grouped order still lost ~7% there).  The 8
+    // workgroups sharing a row tile and the 8 sharing a column tile stay on
+    // one XCD in both halves.
+    const int xcd = bid & 7;
+    const int slot = bid >> 3;
+    const int t = (slot >> 6) * 8 + xcd;
+    const int w = slot & 63;
+    const int nIG = nI >> 3;
+    const int p = t / nIG;
+    if (p >= (nC >> 4)) return;
+    ci_long = ((nC >> 3) - 1 - p) * 8 + 7 - (w & 7);
+    ci_short = p * 8 + (w & 7);
+    ii = (t % nIG) * 8 + (w >> 3);
   } else if (grouped) {
     // Grouped XCD schedule (nC, nI multiples of 8): consecutive block ids are
     // dealt round-robin over the 8 XCDs, so block b and b+8 share an L2.  The
@@ -190,7 +211,7 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     ci = nC - 1 - pos;
     kend = min(n, ci * PC + PC);
   }
-  if constexpr (LOWERK && !SPLIT) {
+  if (LOWERK && !SPLIT && grouped != 2) {
     // W^T = L^{-T} R^T (bo_post_w): column tile ci reads k in [128 ci, n),
     // so the heaviest tiles are the SMALLEST ci -- mirror the schedule's order.
     ci = nC - 1 - ci;
@@ -204,9 +225,21 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   if constexpr (SPLIT) {
     sbeg = wg_off[bid];
     send = wg_off[bid + 1];
+  } else {
+    if (grouped == 2) send = 2;
   }
   for (int sidx = sbeg; sidx < send; ++sidx) {
   int chunk = -1;
+  if (!SPLIT && grouped == 2) {
+    ci = sidx == 0 ? ci_long : ci_short;
+    kbeg = 0;
+    kend = min(n, ci * PC + PC);
+    if constexpr (LOWERK) {
+      ci = nC - 1 - ci;
+      kbeg = ci * PC;
+      kend = n;
+    }
+  }
   if constexpr (SPLIT) {
     const int4 sg = segs[sidx];
     ci = sg.x & 0xffff;
@@ -492,6 +525,15 @@ __global__ void prepare_rows_kernel(const double* __restrict__ X, int B, int q, 
   double v = 0.0;
   if (b < B && a < q && t < d) v = X[(b * q + a) * d + t] / ls[t];
   Xq[idx] = v;
+}
+
+// Paired super-tile schedule switch (default on; BO_POST_PAIRED=0: off), read once.
+static bool paired_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("BO_POST_PAIRED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 // ---- split plans (host) ----------------------------------------------------------
@@ -792,7 +834,10 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
   BO_CHECK_ARG(d >= 1 && d <= DP, "fused posterior kernel supports 1 <= d <= %d", DP);
   // Grouped 8 x 8 super-tile schedule where the grid divides (C3: 2.68 -> 2.49 ms,
   // HBM 4.5 -> 3.7 GB per launch against the per-column-tile order).
-  const int grouped = kc_len == 0 && nC % 8 == 0 && nI % 8 == 0;
+  // Paired where the column groups pair up (nC % 16 == 0; BO_POST_PAIRED=0
+  // keeps the unpaired grouped order for A/B timing).
+  const int grouped = (kc_len == 0 && nC % 8 == 0 && nI % 8 == 0)
+                          ? ((nC % 16 == 0 && paired_enabled()) ? 2 : 1) : 0;
   DevPlan* plan = nullptr;
   if (kc_len != 0) {
     s = device_plan(nC, nI, (int)n, kc_len, &plan);
@@ -800,9 +845,10 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
     BO_CHECK_ARG(plan->nchunks == 0 || work != nullptr, "split plan needs a workspace of %lld doubles",
                  (long long)plan->nchunks * PI * PC);
   }
-  const int64_t blocks = kc_len != 0 ? plan->W
-                         : grouped  ? 512 * (int64_t)ceil_div((nC / 8) * (nI / 8), 8)
-                                    : 8 * ceil_div(nC, 8) * (int64_t)nI;
+  const int64_t blocks = kc_len != 0    ? plan->W
+                         : grouped == 2 ? 512 * (int64_t)ceil_div((nC / 16) * (nI / 8), 8)
+                         : grouped      ? 512 * (int64_t)ceil_div((nC / 8) * (nI / 8), 8)
+                                        : 8 * ceil_div(nC, 8) * (int64_t)nI;
   const int4* segs = plan ? plan->segs : nullptr;
   const int* wg_off = plan ? plan->wg_off : nullptr;
   hipStream_t st = as_stream(stream);
@@ -864,11 +910,13 @@ int bo_post_w(const double* Linv, int64_t ldl, const double* Rt, int B, int q, i
     bo_set_error("bo_post_w: %d column x %d row tiles do not form 8 x 8 super-tiles", nC, nI);
     return BO_ERR_ARG;
   }
-  const int64_t blocks = 512 * (int64_t)ceil_div((nC / 8) * (nI / 8), 8);
+  const int grouped = (nC % 16 == 0 && paired_enabled()) ? 2 : 1;
+  const int64_t blocks = grouped == 2 ? 512 * (int64_t)ceil_div((nC / 16) * (nI / 8), 8)
+                                      : 512 * (int64_t)ceil_div((nC / 8) * (nI / 8), 8);
   post_partials_kernel<BO_RBF, 1, false, false, true, true><<<(unsigned)blocks, 256, 0,
                                                                 as_stream(stream)>>>(
       Rt, 0, Rt, (int)n, Linv, ldl, nullptr, 0.0, nC, nI, nullptr, nullptr, Wt, nullptr,
-      nullptr, nullptr, nullptr, 0, 0, nullptr, Rt, 1);
+      nullptr, nullptr, nullptr, 0, 0, nullptr, Rt, grouped);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
