@@ -40,7 +40,25 @@ build/%.o: botorch_amd/csrc/%.cpp $(HDR)
 $(LIB): $(OBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(OBJ) -pthread -o $@
 
-clean:
-	rm -rf build $(LIB) $(TORCH_LIB)
+# development probes (tools/bo_tools.h): the same sources with -DBO_TOOLS, into
+# a tools-only library the tools/ scripts load; never part of the product
+TOOLS_LIB := tools/libbotorch_amd_tools.so
+TOOLS_OBJ := $(patsubst botorch_amd/csrc/%.hip,build/tools/%.o,$(SRC)) $(patsubst botorch_amd/csrc/%.cpp,build/tools/%.o,$(CPPSRC))
 
-.PHONY: all clean
+build/tools/%.o: botorch_amd/csrc/%.hip $(HDR)
+	@mkdir -p build/tools
+	$(HIPCC) $(HIPFLAGS) -DBO_TOOLS -c $< -o $@
+
+build/tools/%.o: botorch_amd/csrc/%.cpp $(HDR)
+	@mkdir -p build/tools
+	$(CXX) $(CXXFLAGS) -DBO_TOOLS -c $< -o $@
+
+tools: $(TOOLS_LIB)
+
+$(TOOLS_LIB): $(TOOLS_OBJ)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(TOOLS_OBJ) -pthread -o $@
+
+clean:
+	rm -rf build $(LIB) $(TORCH_LIB) $(TOOLS_LIB)
+
+.PHONY: all clean tools

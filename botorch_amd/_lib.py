@@ -29,7 +29,6 @@ _SIGNATURES = {
     "bo_version": (c_int, []),
     "bo_probe_mfma_f64_layout": (c_int, [_P, _P]),
     "bo_probe_mfma_f64_rate": (c_int, [c_int, c_int, _P, _P]),
-    "bo_probe_valu_f64": (c_int, [c_int, _P, _P]),
     "bo_gemm_f64": (c_int, [c_int, c_int, c_int, c_int, c_int, c_double, _P, c_int64, c_int64,
                             _P, c_int64, c_int64, c_double, _P, c_int64, c_int64, c_int, c_int,
                             _P]),
@@ -72,7 +71,9 @@ _SIGNATURES = {
     "bo_ainv_work": (c_int, [c_int64, POINTER(c_int64)]),
     "bo_post_w_work": (c_int, [c_int, c_int, c_int64, POINTER(c_int), POINTER(c_int64)]),
     "bo_post_w_split": (c_int, [_P, c_int64, _P, c_int, c_int, c_int64, _P, _P, _P]),
-    "bo_probe_diag16": (c_int, [_P, _P, _P]),
+    "bo_post_w_dx_work": (c_int, [c_int, c_int, c_int64, POINTER(c_int64)]),
+    "bo_post_w_dx": (c_int, [c_int, _P, c_int64, _P, c_int, c_int, c_int, c_int64, _P, _P, _P, _P,
+                             _P, _P, c_double, c_double, _P, _P, _P]),
     "bo_ainv": (c_int, [_P, c_int64, c_int64, _P, _P, _P]),
     "bo_post_split_table": (c_int, [c_int64, c_int, c_int64, c_int, _P, c_int, _P, c_int,
                                     POINTER(c_int), POINTER(c_int)]),
@@ -85,8 +86,6 @@ _SIGNATURES = {
     "bo_qehvi_backward": (c_int, [c_int, c_int, c_int, _P, _P, _P, c_int, _P, _P, c_int, c_int64,
                                   _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P]),
     "bo_chol_backward": (c_int, [c_int, c_int, _P, _P, _P, _P]),
-    "bo_probe_potrf_phases": (c_int, [_P, c_int64, _P, _P, _P, _P]),
-    "bo_probe_chol_dag": (c_int, [_P, _P, c_int64, _P, _P, _P, _P, _P]),
     "bo_chol_dag_tasks": (c_int, [c_int, _P, c_int]),
     "bo_kernel_grad": (c_int, [c_int, _P, c_int64, _P, c_int64, c_int, _P, c_double, _P, c_int64,
                                c_int, c_int, _P, _P]),

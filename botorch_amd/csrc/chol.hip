@@ -24,24 +24,12 @@
 #include "common.h"
 #include "gemm.h"
 
-int bo_potrf_block128(double* A, int64_t lda, int64_t k0, double* Linv, int64_t ldi, int* info,
-                      hipStream_t st);
 int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipStream_t st,
                 long long* trace = nullptr, int nb = 1);
 
-// BO_CHOL_LEGACY=1 selects the launch-per-step look-ahead factorisation below
-// (kept for A/B timing) instead of the persistent task-DAG kernel (chol_dag.hip).
-static bool chol_legacy() {
-  static const bool legacy = [] {
-    const char* e = std::getenv("BO_CHOL_LEGACY");
-    return e && e[0] == '1';
-  }();
-  return legacy;
-}
-
 namespace {
 
-constexpr int NBO = 128; // panel width = diagonal block of potrf.hip
+constexpr int NBO = 128; // padded matrix order granule (n rounded up to 128)
 
 // K[i][j] = outputscale * k(x_i, x_j) (+ diag_add on i == j), row-major with
 // leading dimension ldk, over a `rows x cols` padded extent (identity pad).
@@ -230,37 +218,6 @@ __global__ void add_diag_kernel(double* __restrict__ A, int64_t ld, int64_t n,
 
 }  // namespace
 
-// Look-ahead stream of the blocked Cholesky (one per device, created on first
-// use and kept for the process lifetime) and its two ordering events.
-struct SideStream {
-  hipStream_t stream = nullptr;
-  hipEvent_t solved = nullptr;     // panel solve of step k done (caller's stream)
-  hipEvent_t bulk_done = nullptr;  // BULK_k done (side stream)
-};
-
-// Creation is guarded, and a legacy factorisation holds g_side_mu for its
-// whole enqueue sequence, so concurrent host callers never interleave record /
-// wait pairs on the shared events.
-static std::mutex g_side_mu;
-
-static SideStream* side_stream() {
-  static SideStream per_dev[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  SideStream& s = per_dev[dev];
-  if (!s.stream) {
-    // Lowest priority: the bulk trailing updates only fill CUs the critical
-    // path (diagonal block, panel solve, look-ahead column) leaves idle.
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
-    if (hipStreamCreateWithPriority(&s.stream, hipStreamNonBlocking, least) != hipSuccess)
-      return nullptr;
-    if (hipEventCreateWithFlags(&s.solved, hipEventDisableTiming) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&s.bulk_done, hipEventDisableTiming) != hipSuccess) return nullptr;
-  }
-  return &s;
-}
-
 // ---------------------------------------------------------------------------
 thread_local char g_err[512];
 void bo_set_error(const char* fmt, ...) {
@@ -347,102 +304,7 @@ int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* 
                (long long)np, NBO);
   BO_CHECK_ARG(((uintptr_t)A & 15) == 0 && ((uintptr_t)Linv & 15) == 0,
                "bo_cholesky_inverse: buffers must be 16-B aligned");
-  hipStream_t st = as_stream(stream);
-  if (!chol_legacy()) return bo_chol_dag(A, Linv, np, info, work, st);
-  std::lock_guard<std::mutex> side_lock(g_side_mu);
-  SideStream* side = side_stream();
-  if (!side) {
-    bo_set_error("bo_cholesky_inverse: could not create the look-ahead stream/events");
-    return BO_ERR_HIP;
-  }
-  // every exit joins the side stream back into the caller's stream: no
-  // look-ahead work on A / work is left unordered behind a returned error
-  bool side_used = false;
-  auto join = [&](int status) {
-    if (side_used) {
-      (void)hipEventRecord(side->bulk_done, side->stream);
-      (void)hipStreamWaitEvent(st, side->bulk_done, 0);
-    }
-    return status;
-  };
-  BO_HIP(hipMemsetAsync(info, 0, sizeof(int), st));
-  BO_HIP(hipMemsetAsync(Linv, 0, sizeof(double) * np * np, st));
-  // Right-looking factorisation over 128-column panels with a one-panel
-  // look-ahead.  Step k on the caller's stream: the diagonal block is factored
-  // AND inverted by one workgroup in LDS (potrf.hip); the panel below is solved
-  // as one MFMA GEMM against that inverse (into W_k, copied back into A); the
-  // NEXT panel column takes its rank-128 update (LA_k) so step k+1 can start.
-  // The bulk of the trailing update (BULK_k: columns beyond the next panel)
-  // runs on the side stream, overlapping the next diagonal factorisation.
-  // Ordering: BULK_k waits for the solve of step k; LA_{k+1} (same columns as
-  // BULK_k) waits for BULK_k; W alternates between two halves of `work`
-  // (BULK_k's input is only overwritten by the solve of step k+2, after LA_{k+1}).
-  double* Wbuf[2] = {work, work + np * NBO};
-  bool bulk_pending = false;
-  for (int64_t K0 = 0, k = 0; K0 < np; K0 += NBO, ++k) {
-    int s = bo_potrf_block128(A, np, K0, Linv, np, info, st);
-    if (s) return join(s);
-    const int64_t rem = np - K0 - NBO;
-    if (rem <= 0) break;
-    double* W = Wbuf[k & 1];
-    double* P = A + (K0 + NBO) * np + K0;       // rem x 128 panel
-    const double* Dinv = Linv + K0 * np + K0;  // 128 x 128 lower
-    s = bo_gemm_f64_impl(0, 1, (int)rem, NBO, NBO, 1.0, P, np, 0, Dinv, np, 0, 0.0, W, NBO, 0, 1,
-                         BO_GEMM_B_UPPER, st);
-    if (s) return join(s);
-    double* A22 = A + (K0 + NBO) * np + (K0 + NBO);
-    side_used = true;
-    BO_HIP(hipEventRecord(side->solved, st));
-    BO_HIP(hipStreamWaitEvent(side->stream, side->solved, 0));
-    // Off the critical path (side stream, low priority): the solved panel goes
-    // back into A (read again only by the inverse phase), then BULK_k: rows /
-    // cols >= K0 + 256, lower triangle, from rows NBO.. of W.
-    BO_HIP(hipMemcpy2DAsync(P, sizeof(double) * np, W, sizeof(double) * NBO,
-                            sizeof(double) * NBO, rem, hipMemcpyDeviceToDevice, side->stream));
-    if (rem > NBO) {
-      s = bo_gemm_f64_impl(0, 1, (int)(rem - NBO), (int)(rem - NBO), NBO, -1.0, W + NBO * NBO,
-                           NBO, 0, W + NBO * NBO, NBO, 0, 1.0, A22 + NBO * np + NBO, np, 0, 1,
-                           BO_GEMM_LOWER_C, side->stream);
-      if (s) return join(s);
-    }
-    if (bulk_pending) BO_HIP(hipStreamWaitEvent(st, side->bulk_done, 0));  // BULK_{k-1}
-    // LA_k: the next panel column (all rem rows x 128 columns, lower on its diagonal block)
-    s = bo_gemm_f64_impl(0, 1, (int)rem, NBO, NBO, -1.0, W, NBO, 0, W, NBO, 0, 1.0, A22, np, 0, 1,
-                         BO_GEMM_LOWER_C, st);
-    if (s) return join(s);
-    BO_HIP(hipEventRecord(side->bulk_done, side->stream));
-    bulk_pending = true;
-  }
-  if (bulk_pending) BO_HIP(hipStreamWaitEvent(st, side->bulk_done, 0));
-  // Triangular inverse by recursive doubling over the inverted diagonal
-  // blocks:  [L11 0; L21 L22]^{-1} = [X11 0; -X22 L21 X11  X22].
-  for (int64_t sz = NBO; sz < np; sz *= 2) {
-    const int64_t stride = 2 * sz;
-    const int64_t full = np / stride;          // pairs with a full-size second block
-    const int64_t tail_r2 = full * stride + sz;  // second block start of a ragged pair
-    for (int pass = 0; pass < 2; ++pass) {
-      int64_t npairs, r1, t;
-      if (pass == 0) { npairs = full; r1 = 0; t = sz; }
-      else {
-        if (tail_r2 >= np) break;
-        npairs = 1; r1 = full * stride; t = np - tail_r2;
-      }
-      if (npairs == 0) continue;
-      const int64_t r2 = r1 + sz;
-      const int64_t sBlk = stride * (np + 1);  // diagonal step between pairs
-      // T = L21 * X11     (t x sz)
-      int s = bo_gemm_f64_impl(0, 0, (int)t, (int)sz, (int)sz, 1.0, A + r2 * np + r1, np, sBlk,
-                               Linv + r1 * np + r1, np, sBlk, 0.0, work, sz, t * sz, (int)npairs,
-                               BO_GEMM_B_LOWER, st);
-      if (s) return s;
-      // X21 = -X22 * T     (t x sz)
-      s = bo_gemm_f64_impl(0, 0, (int)t, (int)sz, (int)t, -1.0, Linv + r2 * np + r2, np, sBlk,
-                           work, sz, t * sz, 0.0, Linv + r2 * np + r1, np, sBlk, (int)npairs,
-                           BO_GEMM_A_LOWER, st);
-      if (s) return s;
-    }
-  }
-  return BO_OK;
+  return bo_chol_dag(A, Linv, np, info, work, as_stream(stream));
 }
 
 int bo_transpose(const double* A, double* B, int64_t n, int64_t ld, void* stream) {

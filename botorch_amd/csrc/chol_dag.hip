@@ -1268,6 +1268,7 @@ int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipS
 // Timing probe of the task DAG (tools/trace_chol.py): trace receives, per task
 // in queue order, [start, end, packed (block, type, k, j)] in wall-clock ticks
 // (100 MHz); returns the task count through *ntasks (host int).
+#ifdef BO_TOOLS  // development probes (tools/bo_tools.h), not the product ABI
 extern "C" int bo_probe_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work,
                                  long long* trace, int* ntasks, void* stream) {
   BO_CHECK_ARG(np > 0 && np % TB == 0, "bo_probe_chol_dag: order");
@@ -1288,6 +1289,7 @@ extern "C" int bo_probe_diag16(long long* out, double* sink, void* stream) {
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
+#endif  // BO_TOOLS
 
 // The queue of the task DAG for T tile rows (host only, no device call): out
 // receives 4 ints per task (type | fin << 8 | nk << 16, k, j, i0 | i1 << 16) in queue

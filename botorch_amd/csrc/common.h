@@ -58,6 +58,18 @@ __device__ __forceinline__ double kernel_from_d2(double d2) {
   }
 }
 
+// dk(x_i, x_k)/dx_i (scaled coordinates), as a factor g with dk = g * (x_i - x_k).
+template <int KIND>
+__device__ __forceinline__ double dkernel_factor(double d2, double outputscale) {
+  if (KIND == BO_RBF) {
+    return -outputscale * exp(-0.5 * d2);
+  } else {
+    const double r = sqrt(fmax(d2, 0.0));
+    const double s5r = 2.23606797749978969641 * r;
+    return -outputscale * (5.0 / 3.0) * (1.0 + s5r) * exp(-s5r);
+  }
+}
+
 void bo_set_error(const char* fmt, ...);
 
 #define BO_CHECK_ARG(cond, ...)        \

@@ -25,18 +25,6 @@ constexpr int SMAX = 4096;  // samples staged in LDS per pass (winner masks)
 
 enum { MODE_QEI = 1, MODE_QNEI = 2, MODE_QLOGEI = 4, MODE_QLOGNEI = 5 };
 
-// dk(x_i, x_k)/dx_i (scaled coordinates), as a factor g with dk = g * (x_i - x_k).
-template <int KIND>
-__device__ __forceinline__ double dkernel_factor(double d2, double outputscale) {
-  if (KIND == BO_RBF) {
-    return -outputscale * exp(-0.5 * d2);
-  } else {
-    const double r = sqrt(fmax(d2, 0.0));
-    const double s5r = 2.23606797749978969641 * r;
-    return -outputscale * (5.0 / 3.0) * (1.0 + s5r) * exp(-s5r);
-  }
-}
-
 // qNEI (cached root): the samples carry the baseline term F[s][row] =
 // (Z_base T)[s][row] (row = b * Qp + a); its cotangent dF (same layout) is the
 // winner weight, from which the host forms dT = Z_base^T dF.

@@ -137,14 +137,28 @@ __device__ __forceinline__ void post_epilogue(const v4d (&acc)[8], int ci, int r
   if (lane < 16) mpart[(int64_t)ci * nrows_pad + row0 + lane] = m;
 }
 
-template <int KIND, int ND, bool SPLIT, bool CROSS, bool PRE = false, bool LOWERK = false>
+// Fused posterior-backward epilogue of the LOWERK (W^T) tiles (bo_post_w_dx):
+// what the dX reduction needs besides the W tile itself.
+struct FusedDx {
+  const double* dmean;  // B x q (standardised-space scale applied here: ystd)
+  const double* dcov;   // B x q x q
+  const double* alpha;  // n
+  const double* Xq;     // nrows_pad x 8 test rows (scaled)
+  const double* Xt;     // n x 8 training rows (scaled)
+  double ystd, outputscale;
+  int B, q, Qp;
+  double* part;         // nC x nrows_pad x 8 partial dX (scaled coordinates)
+};
+
+template <int KIND, int ND, bool SPLIT, bool CROSS, bool PRE = false, bool LOWERK = false,
+          bool FUSEDX = false>
 __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     const double* __restrict__ Xq, int nrows, const double* __restrict__ Xt, int n,
     const double* __restrict__ U, int64_t ldu, const double* __restrict__ beta,
     double outputscale, int nC, int nI, double* __restrict__ Spart, double* __restrict__ mpart,
     double* __restrict__ Rt, const int4* __restrict__ segs, const int* __restrict__ wg_off,
     double* __restrict__ work, const double* __restrict__ Qc, int rq, int64_t ldq,
-    double* __restrict__ Cx, const double* __restrict__ Kt, int grouped) {
+    double* __restrict__ Cx, const double* __restrict__ Kt, int grouped, FusedDx fx = FusedDx{}) {
   // Two LDS stages: while the MFMAs consume stage t, the U rows of step t+1
   // are in flight to registers and this thread evaluates its 8 kernel values
   // of step t+1 between the MFMAs (VALU work hidden under the matrix pipe);
@@ -360,7 +374,8 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
         b[it] = PRE ? bc[it][ks] : Ks[cur][kr][wave * 32 + it * 16 + (lane & 15)];   \
       _Pragma("unroll") for (int ct = 0; ct < 8; ++ct)                              \
         _Pragma("unroll") for (int it = 0; it < 2; ++it)                            \
-          acc[ct][it] = mfma_f64(a[ct], b[it], acc[ct][it]);                         \
+          acc[ct][it] = FUSEDX ? mfma_f64(b[it], a[ct], acc[ct][it])                \
+                               : mfma_f64(a[ct], b[it], acc[ct][it]);                \
       XMFMA                                                                          \
       if (!PRE) {                                                                    \
         kv[2 * ks] = BO_KVAL(knext + kh * 8 + 2 * ks);                              \
@@ -404,7 +419,115 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
       }
   }
 
-  if (SPLIT && chunk >= 0) {
+  if constexpr (FUSEDX) {
+    // The operands were swapped in the k-loop, so acc[ct][it] holds W = R L^-1
+    // itself: lane l, register r: test row i = row16 + (l >> 4) + 4 r,
+    // training point c = c0 + 16 ct + (l & 15).  Per 16-row tile:
+    //   (G W)[a][c] = sum_j G[a][j] W[j][c]: 4 MFMAs per 16 x 16 block, the W
+    //   accumulator register being the B operand as it stands (j = (l >> 4) +
+    //   4 r) and G (block-diagonal over the tile's t-batches, G_b = s^2
+    //   (dcov_b + dcov_b^T)) the A operand;
+    //   dK*x[a][c] = s dmean[a] alpha[c] - (G W)[a][c]  (post_backward's D),
+    //   dX[a][t] += dK*x[a][c] dk(x_a, x_c)/dx_a,t summed over this tile's 128
+    //   training points -> part[ci][a][t] (scaled coordinates; the reduction
+    //   over ci, the K** term and the 1 / lengthscale are post_dx_reduce's).
+    // W itself is never written.
+    const int ncol = lane & 15, grp = lane >> 4;
+    const double s2 = fx.ystd * fx.ystd;
+    const int nrows_pad = nI * PI;
+    // the tile's 128 training rows (+ alpha) and 128 test rows, staged in the
+    // (now free) U stages: the epilogue then holds only G, the G W block and
+    // the dX sums in registers beside the W accumulators
+    double* xc_s = &Us[0][0][0];       // 128 x 8
+    double* al_s = xc_s + PC * DP;     // 128
+    double* xa_s = al_s + PC;          // 128 x 8
+    for (int e = tid; e < PC * DP; e += 256) {
+      const int c = c0 + e / DP;
+      xc_s[e] = c < n ? fx.Xt[(int64_t)c * DP + (e % DP)] : 0.0;
+      xa_s[e] = fx.Xq[(int64_t)i0 * DP + e];
+    }
+    if (tid < PC) al_s[tid] = (c0 + tid) < n ? fx.alpha[c0 + tid] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int row16 = i0 + wave * 32 + it * 16;
+      const int rl = wave * 32 + it * 16;  // row16 - i0
+      double ga[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ra = row16 + ncol, rj = row16 + grp + 4 * r;
+        const int ba = ra / fx.Qp, bj = rj / fx.Qp;
+        const int aa = ra - ba * fx.Qp, jj = rj - bj * fx.Qp;
+        ga[r] = (ba == bj && ba < fx.B && aa < fx.q && jj < fx.q)
+                    ? s2 * (fx.dcov[((int64_t)ba * fx.q + aa) * fx.q + jj] +
+                            fx.dcov[((int64_t)ba * fx.q + jj) * fx.q + aa])
+                    : 0.0;
+      }
+      double dmu[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ra = row16 + grp + 4 * r;
+        const int b = ra / fx.Qp, aa = ra - b * fx.Qp;
+        dmu[r] = (b < fx.B && aa < fx.q) ? fx.ystd * fx.dmean[(int64_t)b * fx.q + aa] : 0.0;
+      }
+      // two rows of the lane's four at a time (the G W block is recomputed per
+      // half: 4 more MFMAs, fewer live registers beside the W accumulators)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        double dx[2][ND];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+          for (int t = 0; t < ND; ++t) dx[rr][t] = 0.0;
+#pragma unroll
+        for (int ct = 0; ct < 8; ++ct) {
+          v4d gw = v4d_zero();
+#pragma unroll
+          for (int r = 0; r < 4; ++r) gw = mfma_f64(ga[r], acc[ct][it][r], gw);
+          const int cl = ct * 16 + ncol;  // training row within the tile
+          const double al = al_s[cl];
+          const bool cv = c0 + cl < n;
+#pragma unroll
+          for (int rr = 0; rr < 2; ++rr) {
+            const int r = 2 * h + rr;
+            const double D = cv ? fma(dmu[r], al, -gw[r]) : 0.0;
+            const double* xa = xa_s + (rl + grp + 4 * r) * DP;
+            const double* xc = xc_s + cl * DP;
+            double diff[ND];
+            double d2 = 0.0;
+#pragma unroll
+            for (int t = 0; t < ND; ++t) {
+              diff[t] = xa[t] - xc[t];
+              d2 = fma(diff[t], diff[t], d2);
+            }
+            const double f = D * dkernel_factor<KIND>(d2, fx.outputscale);
+#pragma unroll
+            for (int t = 0; t < ND; ++t) dx[rr][t] = fma(f, diff[t], dx[rr][t]);
+          }
+        }
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+          for (int t = 0; t < ND; ++t) {
+            double v = dx[rr][t];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            dx[rr][t] = v;
+          }
+        if (ncol == 0) {
+#pragma unroll
+          for (int rr = 0; rr < 2; ++rr) {
+            double* o = fx.part + ((int64_t)ci * nrows_pad + row16 + grp + 4 * (2 * h + rr)) * DP;
+#pragma unroll
+            for (int t = 0; t < ND; ++t) o[t] = dx[rr][t];
+          }
+        }
+      }
+    }
+    __syncthreads();  // the next segment's prologue rewrites the U stages
+  } else if (SPLIT && chunk >= 0) {
     // Partial R^T of this chunk: register-major, lane-minor per 16-row tile,
     // so every store instruction writes 512 contiguous bytes.
 #pragma unroll
@@ -509,6 +632,38 @@ __global__ __launch_bounds__(64) void post_splitk_reduce_kernel(
   }
   if (Rt != nullptr) post_store_rt(acc, ci, rt * 16, lane, nI, Rt);
   if (Spart != nullptr) post_epilogue(acc, ci, rt * 16, lane, n, beta, nI, Spart, mpart);
+}
+
+// dX of the fused posterior backward (bo_post_w_dx): the per-column-tile
+// partials summed in column-tile order (deterministic), the K** term of the
+// q x q blocks (post_backward_kernel's), and the 1 / lengthscale of the
+// scaled coordinates.  One workgroup per t-batch, one thread per (a, t).
+template <int KIND>
+__global__ __launch_bounds__(256) void post_dx_reduce_kernel(
+    const double* __restrict__ part, int nC, int nrows_pad, int q, int Qp, int d,
+    const double* __restrict__ Xq, const double* __restrict__ dcov,
+    const double* __restrict__ ls, double outputscale, double ystd, double* __restrict__ dX) {
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (tid >= q * d) return;
+  const int a = tid / d, t = tid - (tid / d) * d;
+  const int64_t row = (int64_t)b * Qp + a;
+  double s = 0.0;
+  for (int ci = 0; ci < nC; ++ci) s += part[((int64_t)ci * nrows_pad + row) * DP + t];
+  const double s2 = ystd * ystd;
+  for (int c = 0; c < q; ++c) {
+    if (c == a) continue;
+    const int64_t rc = (int64_t)b * Qp + c;
+    double d2 = 0.0;
+#pragma unroll
+    for (int u = 0; u < DP; ++u) {
+      const double df = Xq[row * DP + u] - Xq[rc * DP + u];
+      d2 = fma(df, df, d2);
+    }
+    const double g = s2 * (dcov[((int64_t)b * q + a) * q + c] + dcov[((int64_t)b * q + c) * q + a]);
+    s = fma(g * dkernel_factor<KIND>(d2, outputscale), Xq[row * DP + t] - Xq[rc * DP + t], s);
+  }
+  dX[((int64_t)b * q + a) * d + t] = s / ls[t];
 }
 
 // Scatter X (B x q x d) into the padded, lengthscale-scaled row layout
@@ -720,6 +875,11 @@ int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len,
   // 2432 (the grouped 8 x 8 super-tile schedule keeps its edge there).
   const int64_t steps = nI * splitk_base(nC, (int)n, PK);
   const int64_t tiles = (int64_t)nC * nI;
+  // The paired one-pass grid (nC % 16 == 0, equal work per workgroup) already
+  // fills the slots from two tiles per slot: b = 256 at n = 4096 measured 1134
+  // (paired one pass) vs 1266 us (stream-K) (profiles/r03/time_posterior_paired.json).
+  const bool paired = nC % 16 == 0 && nI % 8 == 0 && paired_enabled();
+  if (paired && tiles >= 2 * (int64_t)slots) return BO_OK;
   if (tiles < 4 * (int64_t)slots && steps >= slots) {
     const SplitPlan p = build_split_plan(nC, (int)nI, (int)n, -1, slots);
     *kc_len = -1;
@@ -921,6 +1081,70 @@ int bo_post_w(const double* Linv, int64_t ldl, const double* Rt, int B, int q, i
   return BO_OK;
 }
 
+// The posterior backward with W = R L^{-1} never stored (bo_post_w_dx): the
+// one-pass W tiles of bo_post_w with the dK*x -> dX reduction fused into their
+// epilogue, then post_dx_reduce.  Applies where bo_post_w's one-pass grid does
+// (no stream-K plan, 8 x 8 super-tiles); elsewhere *work_elems = 0.
+int bo_post_w_dx_work(int B, int q, int64_t n, int64_t* work_elems) {
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  *work_elems = 0;
+  const int nI = nrows_pad / PI;
+  int kc = 0;
+  int64_t we = 0;
+  s = bo_post_w_work(B, q, n, &kc, &we);
+  if (s) return s;
+  if (nI > 0 && kc == 0 && nC % 8 == 0 && nI % 8 == 0)
+    *work_elems = (int64_t)nC * nrows_pad * DP;
+  return BO_OK;
+}
+
+int bo_post_w_dx(int kind, const double* Linv, int64_t ldl, const double* Rt, int B, int q, int d,
+                 int64_t n, const double* Xq, const double* Xt_scaled, const double* alpha,
+                 const double* dmean, const double* dcov, const double* lengthscale,
+                 double outputscale, double ystd, double* work, double* dX, void* stream) {
+  BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
+  BO_CHECK_ARG(d >= 1 && d <= DP && q >= 1 && q <= 16, "bo_post_w_dx: q=%d d=%d", q, d);
+  BO_CHECK_ARG(ldl % 2 == 0 && ldl >= ceil_div(n, PC) * PC, "L^{-1} leading dim %lld too small",
+               (long long)ldl);
+  BO_CHECK_ARG(Linv && Rt && Xq && Xt_scaled && alpha && dmean && dcov && lengthscale && work && dX,
+               "bo_post_w_dx: null buffer");
+  if (B == 0) return BO_OK;
+  int64_t we = 0;
+  int s = bo_post_w_dx_work(B, q, n, &we);
+  if (s) return s;
+  if (we == 0) {
+    bo_set_error("bo_post_w_dx: no one-pass W grid at B=%d q=%d n=%lld (use bo_post_w_split)", B,
+                 q, (long long)n);
+    return BO_ERR_ARG;
+  }
+  int Qp, nrows_pad, nC;
+  s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  const int nI = nrows_pad / PI;
+  const int grouped = (nC % 16 == 0 && paired_enabled()) ? 2 : 1;
+  const int64_t blocks = grouped == 2 ? 512 * (int64_t)ceil_div((nC / 16) * (nI / 8), 8)
+                                      : 512 * (int64_t)ceil_div((nC / 8) * (nI / 8), 8);
+  FusedDx fx{dmean, dcov, alpha, Xq, Xt_scaled, ystd, outputscale, B, q, Qp, work};
+  hipStream_t st = as_stream(stream);
+#define BO_WDX(KIND, ND)                                                                     \
+  post_partials_kernel<KIND, ND, false, false, true, true, true><<<(unsigned)blocks, 256, 0, st>>>( \
+      Rt, 0, Rt, (int)n, Linv, ldl, nullptr, 0.0, nC, nI, nullptr, nullptr, nullptr, nullptr,   \
+      nullptr, nullptr, nullptr, 0, 0, nullptr, Rt, grouped, fx);                             \
+  BO_LAUNCH_CHECK();                                                                         \
+  post_dx_reduce_kernel<KIND><<<(unsigned)B, 256, 0, st>>>(work, nC, nrows_pad, q, Qp, d, Xq, \
+                                                          dcov, lengthscale, outputscale, ystd, dX)
+  if (kind == BO_RBF) {
+    if (d == 6) { BO_WDX(BO_RBF, 6); } else { BO_WDX(BO_RBF, 8); }
+  } else {
+    if (d == 6) { BO_WDX(BO_MATERN52, 6); } else { BO_WDX(BO_MATERN52, 8); }
+  }
+#undef BO_WDX
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
 // W^T = L^{-T} R^T under a stream-K plan (the k-ranges [128 ci, n) are very
 // unequal; grids below four tiles per slot).  *kc_len = -1 and the workspace
 // when the plan applies, else 0 (use bo_post_w or a GEMM).
@@ -933,6 +1157,8 @@ int bo_post_w_work(int B, int q, int64_t n, int* kc_len, int64_t* work_elems) {
   *work_elems = 0;
   int64_t steps = 0;
   for (int ci = 0; ci < nC; ++ci) steps += (int64_t)nI * ceil_div(n - ci * PC, PK);
+  const bool paired = nC % 16 == 0 && nI % 8 == 0 && paired_enabled();  // as bo_post_split_plan
+  if (paired && (int64_t)nC * nI >= 2 * (int64_t)kSlots) return BO_OK;
   if (nI > 0 && (int64_t)nC * nI < 4 * (int64_t)kSlots && steps >= kSlots) {
     const SplitPlan p = build_split_plan(nC, nI, (int)n, -1, kSlots, PLAN_LOWER);
     *kc_len = -1;

@@ -40,6 +40,7 @@ __global__ __launch_bounds__(256) void rate_kernel(int iters, double* out) {
   for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
   if (s == 12345.678) out[0] = s;  // keep live
 }
+#ifdef BO_TOOLS
 // fp64 VALU latency / issue probe (one workgroup of `waves` waves; wave 0
 // lane 0 records s_memtime ticks): out[0] = ticks for 256 dependent v_fma_f64,
 // out[1] = ticks for 256 x 8 independent v_fma_f64 (8 chains), out[2] =
@@ -90,13 +91,16 @@ __global__ void valu_probe_kernel(double seed, long long* out) {
   }
   if (a + r + acc == 1234.5) out[4] = 1;
 }
+#endif  // BO_TOOLS
 }  // namespace
 
+#ifdef BO_TOOLS  // development probe (tools/bo_tools.h), not the product ABI
 extern "C" int bo_probe_valu_f64(int waves, long long* out, void* stream) {
   valu_probe_kernel<<<1, 64 * waves, 0, as_stream(stream)>>>(1.5, out);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
+#endif  // BO_TOOLS
 
 // flops = blocks * 4 waves * iters * 8 * 2048
 extern "C" int bo_probe_mfma_f64_rate(int blocks, int iters, double* out, void* stream) {

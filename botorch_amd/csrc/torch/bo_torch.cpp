@@ -230,32 +230,9 @@ std::vector<at::Tensor> qmc_acq_native(
   fa.tau_max = tau_max;
   ck(bo_qmc_finalize_v(&fa, st), "qmc_finalize");
 
+  // (the backward's W = R L^-1 is formed by qmc_acq_backward_native, fused
+  // into its dX reduction where the grid allows: nothing of it is stored here)
   at::Tensor Wt = at::empty({0}, f64);
-  if (need_grad) {
-    // W^T = L^-T R^T: stream-K below four tiles per slot, the 8 x 8
-    // super-tile grid where it fills the chip, the structured GEMM otherwise
-    // (kernels.w_matrix)
-    int wkc = 0;
-    int64_t wwe = 0;
-    ck(bo_post_w_work(B, q, n, &wkc, &wwe), "post_w_work");
-    const int nI = nrows / 128;
-    if (wkc == -1) {
-      Wt = at::empty({np, nrows}, f64);
-      auto ww = at::empty({std::max<int64_t>(wwe, 1)}, f64);
-      ck(bo_post_w_split(Linv.data_ptr<double>(), np, Rt.data_ptr<double>(), B, q, n,
-                         Wt.data_ptr<double>(), ww.data_ptr<double>(), st), "post_w_split");
-    } else if (int64_t(nC) * nI >= 512 && nC % 8 == 0 && nI % 8 == 0) {
-      Wt = at::empty({np, nrows}, f64);
-      ck(bo_post_w(Linv.data_ptr<double>(), np, Rt.data_ptr<double>(), B, q, n,
-                   Wt.data_ptr<double>(), st), "post_w");
-    } else {
-      auto W = at::empty({nrows, np}, f64);
-      ck(bo_gemm_f64(1, 1, nrows, int(np), nC * 128, 1.0, Rt.data_ptr<double>(), nrows, 0,
-                     U.data_ptr<double>(), np, 0, 0.0, W.data_ptr<double>(), np, 0, 1,
-                     BO_GEMM_B_LOWER, st), "w_matrix");
-      Wt = W.t().contiguous();
-    }
-  }
   at::Tensor prev = at::zeros({3}, at::TensorOptions().dtype(at::kDouble));
   if (defer_ladder && B > 0) prev = defer_status(info, jit, st, dev);
   if (!need_grad) {
@@ -263,6 +240,108 @@ std::vector<at::Tensor> qmc_acq_native(
     Rt = at::empty({0}, f64);
   }
   return {acq, mean, L, Xq, Rt, Wt, jit, info, prev};
+}
+
+// dX of qmc_acq_native (the registered autograd formula of bo::qmc_acq): the
+// reduction + sampling + q x q Cholesky backward (bo_qmc_backward), then the
+// posterior backward -- W = R L^-1 formed tile by tile and reduced into dX in
+// the same launch (bo_post_w_dx) where the one-pass grid applies, else W^T by
+// the stream-K / structured-GEMM route and bo_post_backward.
+at::Tensor qmc_acq_backward_native(
+    const at::Tensor& dacq, const at::Tensor& acq, const at::Tensor& mean, const at::Tensor& L,
+    const at::Tensor& Z, const c10::optional<at::Tensor>& best_f_s, const at::Tensor& Xq,
+    const at::Tensor& Rt, const at::Tensor& Linv, const at::Tensor& U, const at::Tensor& Xt_scaled,
+    const at::Tensor& alpha, const at::Tensor& lengthscale, int64_t kind, int64_t mode, int64_t d,
+    int64_t n, double outputscale, double ystd, double best_f, bool fat, double tau_relu,
+    double tau_max) {
+  for (const auto* t : {&mean, &L, &Z, &Xq, &Rt, &Linv, &U, &Xt_scaled, &alpha, &lengthscale})
+    check_f64(*t, "backward operand");
+  const int B = static_cast<int>(mean.size(0)), q = static_cast<int>(mean.size(1));
+  const int dev = mean.device().index();
+  void* st = c10::hip::getCurrentHIPStream(dev).stream();
+  auto f64 = mean.options();
+  const int64_t np = U.size(0);
+  auto dX = at::empty({B, q, d}, f64);
+  if (B == 0) return dX;
+  auto dmean = at::empty({B, q}, f64);
+  auto dcov = at::empty({B, q, q}, f64);
+  const at::Tensor da = dacq.to(at::kDouble).contiguous();
+  const at::Tensor af = acq.contiguous();
+  const at::Tensor bfs = best_f_s.has_value() ? best_f_s->contiguous() : at::Tensor();
+  BoQmcBackwardArgs qa{};
+  qa.struct_size = sizeof(qa);
+  qa.abi_version = BO_ABI_VERSION;
+  qa.mode = int(mode);
+  qa.B = B;
+  qa.q = q;
+  qa.S = static_cast<int32_t>(Z.size(0));
+  qa.mean = mean.data_ptr<double>();
+  qa.Lq = L.data_ptr<double>();
+  qa.Z = Z.data_ptr<double>();
+  qa.best_f = best_f;
+  qa.best_f_s = cp(bfs);
+  qa.dacq = da.data_ptr<double>();
+  qa.dmean = dmean.data_ptr<double>();
+  qa.dcov = dcov.data_ptr<double>();
+  qa.acq_fwd = af.data_ptr<double>();
+  qa.fat = fat ? 1 : 0;
+  qa.tau_relu = tau_relu;
+  qa.tau_max = tau_max;
+  ck(bo_qmc_backward_v(&qa, st), "qmc_backward");
+
+  int64_t wdx = 0;
+  ck(bo_post_w_dx_work(B, q, n, &wdx), "post_w_dx_work");
+  if (wdx > 0) {
+    auto work = at::empty({wdx}, f64);
+    ck(bo_post_w_dx(int(kind), Linv.data_ptr<double>(), np, Rt.data_ptr<double>(), B, q, int(d), n,
+                    Xq.data_ptr<double>(), Xt_scaled.data_ptr<double>(), alpha.data_ptr<double>(),
+                    dmean.data_ptr<double>(), dcov.data_ptr<double>(),
+                    lengthscale.data_ptr<double>(), outputscale, ystd, work.data_ptr<double>(),
+                    dX.data_ptr<double>(), st), "post_w_dx");
+    return dX;
+  }
+  int Qp = 0, nrows = 0, nC = 0;
+  ck(bo_post_geometry(B, q, n, &Qp, &nrows, &nC), "post_geometry");
+  int wkc = 0;
+  int64_t wwe = 0;
+  ck(bo_post_w_work(B, q, n, &wkc, &wwe), "post_w_work");
+  at::Tensor W;
+  bool kmajor = true;
+  if (wkc == -1) {
+    W = at::empty({np, nrows}, f64);
+    auto ww = at::empty({std::max<int64_t>(wwe, 1)}, f64);
+    ck(bo_post_w_split(Linv.data_ptr<double>(), np, Rt.data_ptr<double>(), B, q, n,
+                       W.data_ptr<double>(), ww.data_ptr<double>(), st), "post_w_split");
+  } else {
+    W = at::empty({nrows, np}, f64);
+    kmajor = false;
+    ck(bo_gemm_f64(1, 1, nrows, int(np), nC * 128, 1.0, Rt.data_ptr<double>(), nrows, 0,
+                   U.data_ptr<double>(), np, 0, 0.0, W.data_ptr<double>(), np, 0, 1,
+                   BO_GEMM_B_LOWER, st), "w_matrix");
+  }
+  BoPostBackwardArgs pb{};
+  pb.struct_size = sizeof(pb);
+  pb.abi_version = BO_ABI_VERSION;
+  pb.kind = int(kind);
+  pb.B = B;
+  pb.q = q;
+  pb.d = int(d);
+  pb.Xq = Xq.data_ptr<double>();
+  pb.Xt_scaled = Xt_scaled.data_ptr<double>();
+  pb.n = n;
+  pb.W = W.data_ptr<double>();
+  pb.ldw = W.size(1);
+  pb.alpha = alpha.data_ptr<double>();
+  pb.dmean = dmean.data_ptr<double>();
+  pb.dcov = dcov.data_ptr<double>();
+  pb.lengthscale = lengthscale.data_ptr<double>();
+  pb.outputscale = outputscale;
+  pb.ystd = ystd;
+  pb.accumulate = 0;
+  pb.w_kmajor = kmajor ? 1 : 0;
+  pb.dX = dX.data_ptr<double>();
+  ck(bo_post_backward_v(&pb, st), "post_backward");
+  return dX;
 }
 
 at::Tensor ladder_defer(const at::Tensor& info, const at::Tensor& jitter) {
@@ -313,6 +392,10 @@ TORCH_LIBRARY_FRAGMENT(bo, m) {
         "float outputscale, float constant, float ymean, float ystd, float best_f, bool fat, "
         "float tau_relu, float tau_max, bool need_grad, int kxt_cap, bool defer_ladder) "
         "-> Tensor[]");
+  m.def("qmc_acq_backward_native(Tensor dacq, Tensor acq, Tensor mean, Tensor L, Tensor Z, "
+        "Tensor? best_f_s, Tensor Xq, Tensor Rt, Tensor Linv, Tensor U, Tensor Xt_scaled, "
+        "Tensor alpha, Tensor lengthscale, int kind, int mode, int d, int n, float outputscale, "
+        "float ystd, float best_f, bool fat, float tau_relu, float tau_max) -> Tensor");
   m.def("ladder_defer(Tensor info, Tensor jitter) -> Tensor");
   m.def("ladder_poll(int device) -> Tensor", &ladder_poll);
   m.def("post_timing(bool on) -> ()", &post_timing);
@@ -321,5 +404,6 @@ TORCH_LIBRARY_FRAGMENT(bo, m) {
 
 TORCH_LIBRARY_IMPL(bo, CUDA, m) {
   m.impl("qmc_acq_native", &qmc_acq_native);
+  m.impl("qmc_acq_backward_native", &qmc_acq_backward_native);
   m.impl("ladder_defer", &ladder_defer);
 }

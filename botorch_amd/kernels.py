@@ -579,6 +579,28 @@ def w_matrix(cache: GPCache, pp: PostPartials, post_w: Optional[bool] = None) ->
     return WMat(W, False)
 
 
+def post_w_dx(cache: GPCache, pp: PostPartials, dmean: torch.Tensor, dcov: torch.Tensor,
+              ystd: float) -> Optional[torch.Tensor]:
+    """dX of the posterior moments' cotangents with W = R L^{-1} reduced into
+    dX tile by tile (bo_post_w_dx; W never stored); None where the one-pass
+    grid does not apply (then w_matrix + post_backward)."""
+    if pp.Rt is None:
+        raise RuntimeError("post_partials(store_R=True) is required for gradients")
+    dev = pp.Rt.device
+    we = ctypes.c_int64()
+    check(lib().bo_post_w_dx_work(pp.B, pp.q, cache.n, ctypes.byref(we)), "post_w_dx_work")
+    if we.value == 0:
+        return None
+    work = torch.empty(we.value, dtype=torch.float64, device=dev)
+    dX = torch.empty(pp.B, pp.q, cache.d, dtype=torch.float64, device=dev)
+    check(lib().bo_post_w_dx(cache.kind, _p(cache.Linv), cache.np, _p(pp.Rt), pp.B, pp.q, cache.d,
+                             cache.n, _p(pp.Xq), _p(cache.Xt_scaled), _p(cache.alpha),
+                             _p(dmean.contiguous()), _p(dcov.contiguous()), _p(cache.lengthscale),
+                             cache.outputscale, float(ystd), _p(work), _p(dX), _stream(dev)),
+          "post_w_dx")
+    return dX
+
+
 def qmc_backward(mode: int, mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor,
                  dacq: torch.Tensor, best_f: float = 0.0,
                  best_f_s: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,

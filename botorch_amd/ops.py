@@ -286,8 +286,9 @@ def qmc_acq(X: Tensor, Xt: Tensor, Xt_scaled: Tensor, U: Tensor, Linv: Tensor, b
     """MC acquisition value (B) of B t-batches on the fused path: posterior
     partials, finalisation with the per-member jitter ladder, reparameterised
     Sobol samples and the qEI / qLogEI reduction, one launch each.  With
-    need_grad also (mean, L, Xq, R^T, W^T) for the registered backward; the last
-    output is the ladder status tensor (info)."""
+    need_grad also (mean, L, Xq, R^T) for the registered backward (the W^T slot
+    stays empty: the backward forms W itself); the last output is the ladder
+    status tensor (info)."""
     # the whole host sequence is one native call (csrc/torch/bo_torch.cpp)
     n = Xt.shape[0]
     out = _lib.torch_ops().qmc_acq_native(
@@ -308,47 +309,46 @@ def _(X, Xt, Xt_scaled, U, Linv, beta, alpha, lengthscale, Z, best_f_s, kind, mo
         return mk(B), mk(0), mk(0), mk(0), mk(0), mk(0), mk(B), info
     Qp, nrows_pad, nC = _geometry(B, q, Xt.shape[0])
     return (mk(B), mk(B, q), mk(B, q, q), mk(nrows_pad, kernels.DP), mk(nC * 128, nrows_pad),
-            mk(U.shape[0], nrows_pad), mk(B), info)
+            mk(0), mk(B), info)
 
 
 @torch.library.custom_op("bo::qmc_acq_backward", mutates_args=(), device_types="cuda")
 def qmc_acq_backward(dacq: Tensor, acq: Tensor, mean: Tensor, L: Tensor, Z: Tensor,
-                     best_f_s: Optional[Tensor], Xq: Tensor, Rt: Tensor, Wt: Tensor, Xt: Tensor,
-                     Xt_scaled: Tensor, alpha: Tensor, lengthscale: Tensor, kind: int, mode: int,
-                     outputscale: float, ystd: float, best_f: float, fat: bool, tau_relu: float,
-                     tau_max: float) -> Tensor:
+                     best_f_s: Optional[Tensor], Xq: Tensor, Rt: Tensor, Linv: Tensor, U: Tensor,
+                     Xt: Tensor, Xt_scaled: Tensor, alpha: Tensor, lengthscale: Tensor, kind: int,
+                     mode: int, outputscale: float, ystd: float, best_f: float, fat: bool,
+                     tau_relu: float, tau_max: float) -> Tensor:
     """dX of qmc_acq: the reduction + sampling + q x q Cholesky backward
-    (bo_qmc_backward), then dK*x through dk/dx (bo_post_backward)."""
-    B, q = mean.shape
-    dmean, dcov = kernels.qmc_backward(mode, mean, L, Z, dacq.contiguous(), best_f=best_f,
-                                       best_f_s=best_f_s, acq_fwd=acq,
-                                       log_params=(fat, tau_relu, tau_max))
-    c = _cache_from(Xt, Xt_scaled, lengthscale, Wt, alpha, alpha, kind, outputscale, 0.0)
-    pp = _pp_from(B, q, Xt.shape[0], Xq, Xq, Xq, Rt)
-    return kernels.post_backward(c, pp, kernels.WMat(Wt, True), dmean, dcov, ystd)
+    (bo_qmc_backward), then the posterior backward with W = R L^-1 reduced into
+    dX as it is formed (bo_post_w_dx) -- one native call
+    (bo::qmc_acq_backward_native)."""
+    return _lib.torch_ops().qmc_acq_backward_native(
+        dacq.contiguous(), acq, mean, L, Z.reshape(-1, mean.shape[1]).contiguous(), best_f_s, Xq,
+        Rt, Linv, U, Xt_scaled, alpha, lengthscale, kind, mode, Xt.shape[1], Xt.shape[0],
+        outputscale, ystd, best_f, fat, tau_relu, tau_max)
 
 
 @qmc_acq_backward.register_fake
-def _(dacq, acq, mean, L, Z, best_f_s, Xq, Rt, Wt, Xt, Xt_scaled, alpha, lengthscale, kind, mode,
-      outputscale, ystd, best_f, fat, tau_relu, tau_max):
+def _(dacq, acq, mean, L, Z, best_f_s, Xq, Rt, Linv, U, Xt, Xt_scaled, alpha, lengthscale, kind,
+      mode, outputscale, ystd, best_f, fat, tau_relu, tau_max):
     return mean.new_empty(mean.shape[0], mean.shape[1], Xt.shape[1])
 
 
 def _acq_setup(ctx, inputs, output):
     (X, Xt, Xt_scaled, U, Linv, beta, alpha, lengthscale, Z, best_f_s, kind, mode, outputscale,
      constant, ymean, ystd, best_f, fat, tau_relu, tau_max, need_grad) = inputs
-    acq, mean, L, Xq, Rt, Wt, _, _ = output
-    ctx.save_for_backward(acq, mean, L, Z, Xq, Rt, Wt, Xt, Xt_scaled, alpha, lengthscale)
+    acq, mean, L, Xq, Rt, _, _, _ = output
+    ctx.save_for_backward(acq, mean, L, Z, Xq, Rt, Linv, U, Xt, Xt_scaled, alpha, lengthscale)
     ctx.best_f_s = best_f_s
     ctx.meta = (kind, mode, outputscale, ystd, best_f, fat, tau_relu, tau_max)
 
 
 def _acq_bwd(ctx, dacq, *_):
-    acq, mean, L, Z, Xq, Rt, Wt, Xt, Xt_scaled, alpha, lengthscale = ctx.saved_tensors
+    acq, mean, L, Z, Xq, Rt, Linv, U, Xt, Xt_scaled, alpha, lengthscale = ctx.saved_tensors
     if Rt.numel() == 0:
         raise RuntimeError("bo::qmc_acq was called with need_grad=False")
     kind, mode, outputscale, ystd, best_f, fat, tau_relu, tau_max = ctx.meta
-    dX = torch.ops.bo.qmc_acq_backward(dacq, acq, mean, L, Z, ctx.best_f_s, Xq, Rt, Wt, Xt,
+    dX = torch.ops.bo.qmc_acq_backward(dacq, acq, mean, L, Z, ctx.best_f_s, Xq, Rt, Linv, U, Xt,
                                        Xt_scaled, alpha, lengthscale, kind, mode, outputscale,
                                        ystd, best_f, fat, tau_relu, tau_max)
     return (dX,) + (None,) * 20

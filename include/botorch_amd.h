@@ -55,36 +55,22 @@ extern "C" {
 const char* bo_last_error(void);
 int bo_version(void);
 
-/* Hardware probe of the fp64 MFMA accumulator map; out: 64 x 8 doubles. */
+/* Hardware probe of the fp64 MFMA accumulator map; out: 64 x 8 doubles (the
+ * layout the kernels assume, checked by tests/test_gpu_kernels.py).  The
+ * timing/trace probes of the development tools are not part of this ABI: they
+ * live in tools/bo_tools.h (tools/libbotorch_amd_tools.so, `make tools`). */
 int bo_probe_mfma_f64_layout(double* out, void* stream);
 
 /* Peak-rate probe: `blocks` x 256 threads, each wave issuing iters x 8
  * independent fp64 MFMAs (2048 flop each).  out: 1 double (kept live). */
 int bo_probe_mfma_f64_rate(int blocks, int iters, double* out, void* stream);
-/* fp64 VALU / LDS latency probe (tools/probe_rate.py): out[0..3] = s_memtime
- * ticks of 256 dependent FMAs, 256 x 8 independent FMAs, 64 rsq+2NR chains,
- * 256 dependent LDS reads, with `waves` waves in the workgroup. */
-int bo_probe_valu_f64(int waves, long long* out, void* stream);
 
-/* Phase-timing probe of the 128-block Cholesky kernel (potrf.hip) on the
- * leading block of A (lda even, >= 128): 16 s_memtime stamps into tsc. */
-int bo_probe_potrf_phases(double* A, int64_t lda, double* Linv, int* info, long long* tsc,
-                          void* stream);
 
-/* Task trace of the persistent Cholesky DAG (chol_dag.hip) on A (np x np,
- * np % 64 == 0): trace (device, >= 4 x tasks + 8 x np/64 int64) gets per task [start, end,
- * packed block/type/k/j, spin-wait ticks] (100 MHz); *ntasks (HOST int) the count. */
-int bo_probe_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work,
-                      long long* trace, int* ntasks, void* stream);
 
 /* Queue of the Cholesky task DAG for T = np/64 tile rows (HOST function, no
  * device work): 4 ints per task (type | fin << 8, k, j, i0 | i1 << 16) into
  * out (capacity cap tasks); returns the task count. */
 int bo_chol_dag_tasks(int T, int* out, int cap);
-/* Timing probe (tools/probe_diag16.py): s_memtime ticks per 16 x 16 diagonal
- * factor + inverse on one wave, out[0..2] = DPP / readlane broadcasts / DPP
- * factor only; sink: one double of scratch. */
-int bo_probe_diag16(long long* out, double* sink, void* stream);
 
 /* Batched C = alpha op(A) op(B) + beta C on the fp64 matrix cores (strides sA,
  * sB, sC between batch members).  Building block of the Cholesky/inverse and
@@ -272,6 +258,22 @@ int bo_post_w(const double* Linv, int64_t ldl, const double* Rt, int B, int q, i
 int bo_post_w_work(int B, int q, int64_t n, int* kc_len, int64_t* work_elems);
 int bo_post_w_split(const double* Linv, int64_t ldl, const double* Rt, int B, int q, int64_t n,
                     double* Wt, double* work, void* stream);
+
+/* The posterior backward without W: dX (B x q x d) of the posterior moments'
+ * cotangents (dmean B x q, dcov B x q x q, standardised by ystd as in
+ * bo_post_backward) from bo_post_partials' stored R^T and L^{-1}: the one-pass
+ * W^T = L^{-T} R^T tiles of bo_post_w with the reduction dK*x = s dmean alpha^T
+ * - G W (G_b = s^2 (dcov_b + dcov_b^T)) -> dX fused into their epilogue, W
+ * never written; then the K** term and 1 / lengthscale (generation/gen.py:
+ * 194-222 -> autograd through [G] exact prediction).
+ * work >= bo_post_w_dx_work doubles (nC x nrows_pad x 8 partials); a zero
+ * size means the one-pass grid does not apply (stream-K plans: use
+ * bo_post_w_split + bo_post_backward) and bo_post_w_dx returns BO_ERR_ARG. */
+int bo_post_w_dx_work(int B, int q, int64_t n, int64_t* work_elems);
+int bo_post_w_dx(int kind, const double* Linv, int64_t ldl, const double* Rt, int B, int q, int d,
+                 int64_t n, const double* Xq, const double* Xt_scaled, const double* alpha,
+                 const double* dmean, const double* dcov, const double* lengthscale,
+                 double outputscale, double ystd, double* work, double* dX, void* stream);
 
 /* Plan of bo_post_partials (host pointers): kc_len = 0 (one pass) or -1
  * (stream-K), whichever a k-step cost model of the triangular grid over

@@ -503,3 +503,31 @@ def test_post_w_stream_k_matches_gemm(n, B, q):
     dx_k = kernels.post_backward(cache, pp, W, dmean, dcov, 0.7)
     dx_r = kernels.post_backward(cache, pp, kernels.WMat(Wg, False), dmean, dcov, 0.7)
     torch.testing.assert_close(dx_k, dx_r, rtol=1e-9, atol=1e-11)
+
+
+@pytest.mark.parametrize("n,B,q,kind", [(2048, 1024, 16, 0), (2048, 2048, 8, 0), (2048, 2048, 6, 1),
+                                        (4096, 256, 16, 0)])
+def test_post_w_dx_fused_matches_w_route(n, B, q, kind):
+    """bo_post_w_dx (W = R L^-1 reduced into dX inside the W tiles' epilogue,
+    W never stored) against W^T from the triangular GEMM + bo_post_backward,
+    on one-pass grids (>= 1024 paired tiles): q = 16 (one t-batch per 16-row
+    tile), q = 8 (two per tile: the block-diagonal G), q = 6 with Matern-5/2,
+    and a rank's b = 256 share of C3."""
+    from botorch_amd import _lib, kernels
+    g = torch.Generator().manual_seed(n + B + q)
+    X = torch.rand(n, 6, generator=g, dtype=torch.float64).to(DEV)
+    y = torch.randn(n, generator=g, dtype=torch.float64).to(DEV)
+    ls = torch.full((6,), 0.35, dtype=torch.float64, device=DEV)
+    cache = kernels.build_gp_cache(X, y, ls, 1e-3, 0.1, kind=kind, outputscale=1.3)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64).to(DEV)
+    pp = kernels.post_partials(cache, Xc, store_R=True)
+    dmean = torch.randn(B, q, generator=g, dtype=torch.float64).to(DEV)
+    dcov = torch.randn(B, q, q, generator=g, dtype=torch.float64).to(DEV)
+    dx_f = kernels.post_w_dx(cache, pp, dmean, dcov, 0.7)
+    assert dx_f is not None, "the fused one-pass grid should apply here"
+    Wg = kernels.gemm(pp.Rt, cache.U, transA=True, transB=True, flags=_lib.GEMM_B_LOWER)
+    dx_r = kernels.post_backward(cache, pp, kernels.WMat(Wg, False), dmean, dcov, 0.7)
+    torch.testing.assert_close(dx_f, dx_r, rtol=1e-9, atol=1e-10)
+    # below the one-pass grid the fused entry declines (the caller falls back)
+    pp_s = kernels.post_partials(cache, Xc[:64], store_R=True)
+    assert kernels.post_w_dx(cache, pp_s, dmean[:64], dcov[:64], 0.7) is None

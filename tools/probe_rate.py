@@ -5,6 +5,8 @@ import os
 import sys
 
 import torch
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _toolslib  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from botorch_amd import _lib  # noqa: E402
@@ -29,7 +31,7 @@ valu = {}
 for waves in (1, 4, 8):
     o = torch.zeros(8, dtype=torch.int64, device=dev)
     for _ in range(2):
-        _lib.check(_lib.lib().bo_probe_valu_f64(waves, ctypes.c_void_p(o.data_ptr()), st))
+        _lib.check(_toolslib.tools().bo_probe_valu_f64(waves, ctypes.c_void_p(o.data_ptr()), st))
     torch.cuda.synchronize()
     t = o.cpu().tolist()
     valu[waves] = {"dep_fma_cyc": t[0] / 256, "indep_fma_cyc": t[1] / 2048,

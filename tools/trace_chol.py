@@ -9,6 +9,8 @@ import os
 import sys
 
 import torch
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _toolslib  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from botorch_amd import kernels  # noqa: E402
@@ -38,7 +40,7 @@ def main():
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        check(lib().bo_probe_chol_dag(kernels._p(A), kernels._p(Linv), np_, kernels._p(info),
+        check(_toolslib.tools().bo_probe_chol_dag(kernels._p(A), kernels._p(Linv), np_, kernels._p(info),
                                       kernels._p(work), kernels._p(trace), ctypes.byref(nt),
                                       kernels._stream(dev)), "probe_chol_dag")
         e1.record()
