@@ -19,7 +19,8 @@ RBF, MATERN52 = 0, 1
 GEMM_LOWER_C, GEMM_A_LOWER, GEMM_B_UPPER, GEMM_A_UPPER, GEMM_B_LOWER = 1, 2, 4, 8, 16
 QMC_POSTERIOR, QMC_QEI, QMC_QNEI, QMC_CHOL, QMC_QLOGEI, QMC_QLOGNEI = 0, 1, 2, 3, 4, 5
 LOG_MODES = (QMC_QLOGEI, QMC_QLOGNEI)
-ABI_VERSION = 9
+ABI_VERSION = 10
+RT_ROWMAJOR, RT_BLOCKED = 0, 1  # BoPostPartialsArgs.rt_layout (include/botorch_amd.h)
 
 _P = c_void_p  # device pointers travel as void*
 
@@ -143,7 +144,8 @@ class PostPartialsArgs(_Args):
                        ("Xq", _D), ("Xt_scaled", _D), ("n", c_int64), ("U", _D), ("ldu", c_int64),
                        ("beta", _D), ("outputscale", c_double), ("Spart", _D), ("mpart", _D),
                        ("Rt", _D), ("kc_len", c_int32), ("rq", c_int32), ("work", _D),
-                       ("Qc", _D), ("ldq", c_int64), ("Cx", _D), ("Kt", _D)]
+                       ("Qc", _D), ("ldq", c_int64), ("Cx", _D), ("Kt", _D),
+                       ("rt_layout", c_int32), ("_pad", c_int32)]
 
 
 class QmcFinalizeArgs(_Args):

@@ -28,11 +28,19 @@ bool header_ok(const T* a, const char* name) {
 
 extern "C" {
 
+// bo_post_partials with the R^T layout of ABI 10 (post.hip)
+int bo_post_partials_layout(int kind, const double* Xq, int B, int q, int d,
+                            const double* Xt_scaled, int64_t n, const double* U, int64_t ldu,
+                            const double* beta, double outputscale, double* Spart, double* mpart,
+                            double* Rt, int kc_len, double* work, const double* Qc, int rq,
+                            int64_t ldq, double* Cx, const double* Kt, int rt_layout, void* stream);
+
 int bo_post_partials_v(const BoPostPartialsArgs* a, void* stream) {
   if (!header_ok(a, "bo_post_partials_v")) return BO_ERR_ARG;
-  return bo_post_partials(a->kind, a->Xq, a->B, a->q, a->d, a->Xt_scaled, a->n, a->U, a->ldu,
-                          a->beta, a->outputscale, a->Spart, a->mpart, a->Rt, a->kc_len, a->work,
-                          a->Qc, a->rq, a->ldq, a->Cx, a->Kt, stream);
+  return bo_post_partials_layout(a->kind, a->Xq, a->B, a->q, a->d, a->Xt_scaled, a->n, a->U,
+                                 a->ldu, a->beta, a->outputscale, a->Spart, a->mpart, a->Rt,
+                                 a->kc_len, a->work, a->Qc, a->rq, a->ldq, a->Cx, a->Kt,
+                                 a->rt_layout, stream);
 }
 
 int bo_qmc_finalize_v(const BoQmcFinalizeArgs* a, void* stream) {

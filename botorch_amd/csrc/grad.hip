@@ -21,7 +21,7 @@ namespace {
 constexpr int QMAX = 16;
 constexpr int DP = 8;
 constexpr int THREADS = 256;
-constexpr int SMAX = 4096;  // samples staged in LDS per pass (winner masks)
+constexpr int SMAX = 256;  // samples staged in LDS per pass (winner masks + base samples)
 
 enum { MODE_QEI = 1, MODE_QNEI = 2, MODE_QLOGEI = 4, MODE_QLOGNEI = 5 };
 
@@ -166,6 +166,7 @@ __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
   __shared__ double mu[QMAX];
   __shared__ unsigned short win[SMAX];
   __shared__ double wgt[SMAX];
+  __shared__ double Zs[SMAX * QMAX];   // the chunk's base samples (shared by every t-batch)
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -186,9 +187,11 @@ __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
   }
   for (int s0 = 0; s0 < S; s0 += SMAX) {
     const int ns = min(SMAX, S - s0);
+    for (int e = tid; e < ns * q; e += THREADS) Zs[(e / q) * QMAX + e % q] = Z[(int64_t)s0 * q + e];
     // Pass 1: the winning (maximal, non-clamped) q-index set per sample.
+    __syncthreads();  // Zs
     for (int s = tid; s < ns; s += THREADS) {
-      const double* z = Z + (int64_t)(s0 + s) * q;
+      const double* z = Zs + s * QMAX;
       const double bf = (MODE == MODE_QNEI) ? best_f_s[s0 + s] : best_f;
       double v[QMAX];
       double m = 0.0;
@@ -222,14 +225,14 @@ __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
       }
     }
     __syncthreads();
-    // Pass 2: deterministic accumulation per (a, j).
+    // Pass 2: deterministic accumulation per (a, j), operands from LDS (a
+    // zero weight where a did not win: the same sums as a branch, in order).
     if (ta >= 0 && tj <= ta) {
+#pragma unroll 8
       for (int s = 0; s < ns; ++s) {
-        if (win[s] & (1u << ta)) {
-          const double w = wgt[s];
-          dl_acc = fma(w, Z[(int64_t)(s0 + s) * q + tj], dl_acc);
-          if (tj == 0) dmu_acc += w;
-        }
+        const double w = (win[s] >> ta & 1u) ? wgt[s] : 0.0;
+        dl_acc = fma(w, Zs[s * QMAX + tj], dl_acc);
+        dmu_acc += w;
       }
     }
     __syncthreads();
@@ -255,7 +258,7 @@ __global__ __launch_bounds__(THREADS) void qmc_log_backward_kernel(
     const double* __restrict__ acq_fwd, LogRedParams lp, const double* __restrict__ dacq,
     double* __restrict__ dmean, double* __restrict__ dcov, const double* __restrict__ F,
     int64_t ldF, int Qp, double* __restrict__ dF) {
-  constexpr int SL = 512;  // samples per LDS chunk
+  constexpr int SL = 256;  // samples per LDS chunk (weights + base samples: two workgroups per CU)
   __shared__ double L[QMAX][QMAX + 1];
   __shared__ double Li[QMAX][QMAX + 1];
   __shared__ double dL[QMAX][QMAX + 1];
@@ -263,6 +266,7 @@ __global__ __launch_bounds__(THREADS) void qmc_log_backward_kernel(
   __shared__ double Tm[QMAX][QMAX + 1];
   __shared__ double mu[QMAX];
   __shared__ double w[SL][QMAX + 1];
+  __shared__ double Zs[SL * QMAX];
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -283,8 +287,10 @@ __global__ __launch_bounds__(THREADS) void qmc_log_backward_kernel(
   }
   for (int s0 = 0; s0 < S; s0 += SL) {
     const int ns = min(SL, S - s0);
+    for (int e = tid; e < ns * q; e += THREADS) Zs[(e / q) * QMAX + e % q] = Z[(int64_t)s0 * q + e];
+    __syncthreads();
     for (int s = tid; s < ns; s += THREADS) {
-      const double* z = Z + (int64_t)(s0 + s) * q;
+      const double* z = Zs + s * QMAX;
       const double bf = PERSAMPLE ? best_f_s[s0 + s] : best_f;
       const double* Fs = PERSAMPLE ? F + (int64_t)(s0 + s) * ldF + (int64_t)b * Qp : nullptr;
       double li[QMAX], dli[QMAX], gq[QMAX];
@@ -312,10 +318,11 @@ __global__ __launch_bounds__(THREADS) void qmc_log_backward_kernel(
     }
     __syncthreads();
     if (ta >= 0 && tj <= ta) {
+#pragma unroll 8
       for (int s = 0; s < ns; ++s) {
         const double v = w[s][ta];
-        dl_acc = fma(v, Z[(int64_t)(s0 + s) * q + tj], dl_acc);
-        if (tj == 0) dmu_acc += v;
+        dl_acc = fma(v, Zs[s * QMAX + tj], dl_acc);
+        dmu_acc += v;
       }
     }
     __syncthreads();

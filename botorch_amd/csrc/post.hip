@@ -158,7 +158,8 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     double outputscale, int nC, int nI, double* __restrict__ Spart, double* __restrict__ mpart,
     double* __restrict__ Rt, const int4* __restrict__ segs, const int* __restrict__ wg_off,
     double* __restrict__ work, const double* __restrict__ Qc, int rq, int64_t ldq,
-    double* __restrict__ Cx, const double* __restrict__ Kt, int grouped, FusedDx fx = FusedDx{}) {
+    double* __restrict__ Cx, const double* __restrict__ Kt, int grouped, FusedDx fx = FusedDx{},
+    int rt_blk = 0) {
   // Two LDS stages: while the MFMAs consume stage t, the U rows of step t+1
   // are in flight to registers and this thread evaluates its 8 kernel values
   // of step t+1 between the MFMAs (VALU work hidden under the matrix pipe);
@@ -341,10 +342,14 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   double bc[2][4], bn[2][4];
   const double* ktw = PRE ? Kt + i0 + wave * 32 + (lane & 15) + (int64_t)(lane >> 4) * (nI * PI)
                           : nullptr;
+  // FUSEDX reads R^T in the blocked layout (BO_RT_BLOCKED): one 512-B
+  // segment per load instruction
+  const double* ktb = FUSEDX ? Kt + (int64_t)((i0 + wave * 32) >> 4) * 256 + lane : nullptr;
 #define BO_LOAD_B(K0, DST)                                                          \
   _Pragma("unroll") for (int it = 0; it < 2; ++it)                                 \
     _Pragma("unroll") for (int ks = 0; ks < 4; ++ks)                              \
-      DST[it][ks] = ktw[(int64_t)((K0) + 4 * ks) * (nI * PI) + it * 16];
+      DST[it][ks] = FUSEDX ? ktb[((int64_t)((K0) >> 4) * (nI * (PI / 16)) + it) * 256 + ks * 64] \
+                           : ktw[(int64_t)((K0) + 4 * ks) * (nI * PI) + it * 16];
   BO_LOAD_U(kbeg);
   if (PRE) {
     BO_LOAD_B(kbeg, bc);
@@ -543,7 +548,19 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     // [ct][it] accumulators (passing sub-arrays costs this kernel spills).
     const int nrows16 = nI * (PI / 16);
     const int nrows_pad = nI * PI;
-    if (Rt != nullptr) {
+    if (Rt != nullptr && rt_blk) {
+      // BO_RT_BLOCKED: each 16 x 16 block as its accumulator registers stand,
+      // register-major, lane-minor -- one 512-B segment per store
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          double* blk = Rt + ((int64_t)((c0 >> 4) + ct) * nrows16 +
+                              ((i0 + wave * 32 + it * 16) >> 4)) * 256 + lane;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) blk[r * 64] = acc[ct][it][r];
+        }
+    } else if (Rt != nullptr) {
 #pragma unroll
       for (int ct = 0; ct < 8; ++ct)
 #pragma unroll
@@ -971,11 +988,30 @@ int bo_post_kxt(int kind, const double* Xq, int B, int q, int d, const double* X
   return BO_OK;
 }
 
+int bo_post_partials_layout(int kind, const double* Xq, int B, int q, int d,
+                            const double* Xt_scaled, int64_t n, const double* U, int64_t ldu,
+                            const double* beta, double outputscale, double* Spart, double* mpart,
+                            double* Rt, int kc_len, double* work, const double* Qc, int rq,
+                            int64_t ldq, double* Cx, const double* Kt, int rt_layout, void* stream);
+
 int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
                      const double* Xt_scaled, int64_t n, const double* U, int64_t ldu, const double* beta,
                      double outputscale, double* Spart, double* mpart, double* Rt,
                      int kc_len, double* work, const double* Qc, int rq, int64_t ldq, double* Cx,
                      const double* Kt, void* stream) {
+  return bo_post_partials_layout(kind, Xq, B, q, d, Xt_scaled, n, U, ldu, beta, outputscale, Spart,
+                                 mpart, Rt, kc_len, work, Qc, rq, ldq, Cx, Kt, BO_RT_ROWMAJOR,
+                                 stream);
+}
+
+int bo_post_partials_layout(int kind, const double* Xq, int B, int q, int d,
+                            const double* Xt_scaled, int64_t n, const double* U, int64_t ldu,
+                            const double* beta, double outputscale, double* Spart, double* mpart,
+                            double* Rt, int kc_len, double* work, const double* Qc, int rq,
+                            int64_t ldq, double* Cx, const double* Kt, int rt_layout, void* stream) {
+  BO_CHECK_ARG(rt_layout == BO_RT_ROWMAJOR || (rt_layout == BO_RT_BLOCKED && kc_len == 0 && !Qc),
+               "rt_layout %d: the blocked R^T is stored by one-pass grids without a cross term",
+               rt_layout);
   BO_CHECK_ARG(Qc == nullptr || (kc_len == 0 && rq >= 1 && rq <= 16 && ldq >= n && Cx != nullptr),
                "cross term: one-pass only, 1 <= rq <= 16 rows (got %d), ldq >= n, Cx given", rq);
   BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
@@ -1017,7 +1053,7 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
 #define BO_POST_GO(KIND, ND, SPL, CRS, PRE_)                                                \
   post_partials_kernel<KIND, ND, SPL, CRS, PRE_><<<(unsigned)blocks, 256, 0, st>>>(          \
       Xq, nrows, Xt_scaled, (int)n, U, ldu, beta, outputscale, nC, nI, Spart, mpart, Rt,    \
-      segs, wg_off, work, Qc, rq, ldq, Cx, Kt, grouped)
+      segs, wg_off, work, Qc, rq, ldq, Cx, Kt, grouped, FusedDx{}, rt_layout == BO_RT_BLOCKED)
 #define BO_POST_LAUNCH(KIND, ND)                                                            \
   if (kc_len != 0) {                                                                        \
     if (pre) BO_POST_GO(KIND, ND, true, false, true);                                       \

@@ -182,6 +182,13 @@ std::vector<at::Tensor> qmc_acq_native(
   pa.kc_len = kc;
   pa.work = mp(work);
   pa.Kt = cp(Kt);
+  if (need_grad) {
+    // the backward reads R^T in the blocked layout where its fused W -> dX
+    // pass applies (bo_post_w_dx), row-major everywhere else
+    int64_t wdx = 0;
+    ck(bo_post_w_dx_work(B, q, n, &wdx), "post_w_dx_work");
+    pa.rt_layout = (wdx > 0 && kc == 0) ? BO_RT_BLOCKED : BO_RT_ROWMAJOR;
+  }
   hipEvent_t t0 = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_time_mu);

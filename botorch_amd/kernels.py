@@ -402,7 +402,7 @@ def split_plan(B: int, q: int, n: int, slots: int = 0):
 
 def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
                   split: Optional[int] = None, cross: Optional[torch.Tensor] = None,
-                  kxt: Optional[bool] = None) -> PostPartials:
+                  kxt: Optional[bool] = None, rt_layout: int = 0) -> PostPartials:
     """Column-tile partials of R R^T and R beta for X (B x q x d).  ``split``:
     None = the library's plan, 0 = one pass, k > 0 = chunks of k rows,
     -1 = stream-K (equal k-step shares over the resident slots).
@@ -410,7 +410,8 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
     (rq x nrows_pad) from the same pass -- on one-pass plans only; under a
     split-k plan pp.Cx is None and R^T is stored instead.  ``kxt``: build
     K*x^T first and read it in the posterior kernel (None: when it fits
-    kxt_cap)."""
+    kxt_cap).  ``rt_layout``: _lib.RT_BLOCKED stores R^T in the blocked
+    layout bo_post_w_dx reads (one-pass plans only)."""
     dev = _dev(X)
     B, q, d = X.shape
     if d != cache.d:
@@ -456,7 +457,8 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
                               outputscale=cache.outputscale, Spart=Spart, mpart=mpart, Rt=Rt,
                               kc_len=kc_len, work=work, Qc=cross if Cx is not None else None,
                               rq=cross.shape[0] if Cx is not None else 0,
-                              ldq=cross.shape[1] if Cx is not None else 0, Cx=Cx, Kt=Kt)
+                              ldq=cross.shape[1] if Cx is not None else 0, Cx=Cx, Kt=Kt,
+                              rt_layout=int(rt_layout))
     check(lib().bo_post_partials_v(ctypes.byref(a), st), "post_partials")
     if TIMING_HOOK is not None:
         TIMING_HOOK("post_partials_end")

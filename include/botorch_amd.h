@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 9
+#define BO_ABI_VERSION 10
 
 /* status codes */
 #define BO_OK 0
@@ -43,6 +43,17 @@ extern "C" {
 #define BO_GEMM_B_UPPER 4 /* op(B)[k][n] == 0 for k > n */
 #define BO_GEMM_A_UPPER 8 /* op(A)[m][k] == 0 for k < m */
 #define BO_GEMM_B_LOWER 16 /* op(B)[k][n] == 0 for k < n */
+
+/* layouts of the stored R^T (BoPostPartialsArgs.rt_layout): row-major
+ * (nC*128) x nrows_pad, or blocked in the posterior kernel's MFMA accumulator
+ * order -- 16 x 16 blocks (training block kb, test block ib) at
+ * (kb * nrows_pad / 16 + ib) * 256, element (k, i) of a block at
+ * ((k % 16) / 4) * 64 + (k % 4) * 16 + i % 16 -- so every store and every
+ * load of it is one 512-B segment per instruction.  bo_post_w_dx reads the
+ * blocked layout; every other consumer (bo_post_w, bo_post_w_split,
+ * bo_gemm_f64) the row-major one. */
+#define BO_RT_ROWMAJOR 0
+#define BO_RT_BLOCKED 1
 
 /* qmc modes */
 #define BO_QMC_POSTERIOR 0
@@ -266,7 +277,8 @@ int bo_post_w_split(const double* Linv, int64_t ldl, const double* Rt, int B, in
  * - G W (G_b = s^2 (dcov_b + dcov_b^T)) -> dX fused into their epilogue, W
  * never written; then the K** term and 1 / lengthscale (generation/gen.py:
  * 194-222 -> autograd through [G] exact prediction).
- * work >= bo_post_w_dx_work doubles (nC x nrows_pad x 8 partials); a zero
+ * Rt in the BO_RT_BLOCKED layout (bo_post_partials_v with rt_layout =
+ * BO_RT_BLOCKED).  work >= bo_post_w_dx_work doubles (nC x nrows_pad x 8 partials); a zero
  * size means the one-pass grid does not apply (stream-K plans: use
  * bo_post_w_split + bo_post_backward) and bo_post_w_dx returns BO_ERR_ARG. */
 int bo_post_w_dx_work(int B, int q, int64_t n, int64_t* work_elems);
@@ -493,7 +505,7 @@ int bo_sobol_box(const int64_t* state, const int64_t* shift, int dim, int64_t n,
                  int first_f32, const double* lower, const double* range, int d, double* out,
                  void* stream);
 
-/* ---- Parameter-struct entry points (ABI 9) ------------------------------------
+/* ---- Parameter-struct entry points (ABI 9; ABI 10 adds rt_layout) -------------
  * The widest calls above also take one struct of named fields, so a binding
  * declares a record instead of a positional list of 20-33 arguments.  Every
  * struct opens with struct_size = sizeof(struct) and abi_version =
@@ -521,6 +533,7 @@ typedef struct BoPostPartialsArgs { /* bo_post_partials */
   int64_t ldq;
   double* Cx;
   const double* Kt;
+  int32_t rt_layout, _pad; /* ABI 10: BO_RT_ROWMAJOR or BO_RT_BLOCKED (the layout of Rt) */
 } BoPostPartialsArgs;
 int bo_post_partials_v(const BoPostPartialsArgs* a, void* stream);
 

@@ -40,7 +40,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(handle, s), s
     assert set(syms) == set(_lib.exported_symbols()), set(syms) ^ set(_lib.exported_symbols())
     lib = _lib.lib()
-    assert lib.bo_version() == _lib.ABI_VERSION == 9
+    assert lib.bo_version() == _lib.ABI_VERSION == 10
     assert lib.bo_padded_order(4096) == 4096 and lib.bo_padded_order(20) == 128
 
 

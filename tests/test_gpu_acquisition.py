@@ -520,10 +520,17 @@ def test_post_w_dx_fused_matches_w_route(n, B, q, kind):
     ls = torch.full((6,), 0.35, dtype=torch.float64, device=DEV)
     cache = kernels.build_gp_cache(X, y, ls, 1e-3, 0.1, kind=kind, outputscale=1.3)
     Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64).to(DEV)
-    pp = kernels.post_partials(cache, Xc, store_R=True)
+    pp = kernels.post_partials(cache, Xc, store_R=True)                    # row-major R^T
+    ppb = kernels.post_partials(cache, Xc, store_R=True, rt_layout=_lib.RT_BLOCKED)
+    assert torch.equal(ppb.Spart, pp.Spart)  # the layout changes nothing else
+    # the blocked layout is a permutation of the row-major R^T
+    nb = pp.nrows_pad // 16
+    blk = ppb.Rt.view(-1, nb, 4, 4, 16)          # [kb][ib][k%16/4][k%4][i%16]
+    rm = blk.permute(0, 2, 3, 1, 4).reshape(-1, pp.nrows_pad)
+    assert torch.equal(rm, pp.Rt)
     dmean = torch.randn(B, q, generator=g, dtype=torch.float64).to(DEV)
     dcov = torch.randn(B, q, q, generator=g, dtype=torch.float64).to(DEV)
-    dx_f = kernels.post_w_dx(cache, pp, dmean, dcov, 0.7)
+    dx_f = kernels.post_w_dx(cache, ppb, dmean, dcov, 0.7)
     assert dx_f is not None, "the fused one-pass grid should apply here"
     Wg = kernels.gemm(pp.Rt, cache.U, transA=True, transB=True, flags=_lib.GEMM_B_LOWER)
     dx_r = kernels.post_backward(cache, pp, kernels.WMat(Wg, False), dmean, dcov, 0.7)

@@ -22,7 +22,7 @@ m.likelihood.noise = torch.tensor([bench.NOISE], dtype=f64)
 m.mean_module.constant = torch.tensor(bench.CONSTANT, dtype=f64)
 m.eval()
 m.prediction_cache()
-acqf = qExpectedImprovement(m, float(Ytr.max()), sampler=SobolQMCNormalSampler(torch.Size([bench.MC]), seed=0))
+acqf = qExpectedImprovement(m, float(Ytr.max()) - 1.5, sampler=SobolQMCNormalSampler(torch.Size([bench.MC]), seed=0))
 Xg = Xc.to(dev).clone().requires_grad_(True)
 for it in range(8):
     v = acqf(Xg)
