@@ -19,7 +19,7 @@ RBF, MATERN52 = 0, 1
 GEMM_LOWER_C, GEMM_A_LOWER, GEMM_B_UPPER, GEMM_A_UPPER, GEMM_B_LOWER = 1, 2, 4, 8, 16
 QMC_POSTERIOR, QMC_QEI, QMC_QNEI, QMC_CHOL, QMC_QLOGEI, QMC_QLOGNEI = 0, 1, 2, 3, 4, 5
 LOG_MODES = (QMC_QLOGEI, QMC_QLOGNEI)
-ABI_VERSION = 10
+ABI_VERSION = 11
 RT_ROWMAJOR, RT_BLOCKED = 0, 1  # BoPostPartialsArgs.rt_layout (include/botorch_amd.h)
 
 _P = c_void_p  # device pointers travel as void*
@@ -76,6 +76,11 @@ _SIGNATURES = {
     "bo_post_w_dx": (c_int, [c_int, _P, c_int64, _P, c_int, c_int, c_int, c_int64, _P, _P, _P, _P,
                              _P, _P, c_double, c_double, _P, _P, _P]),
     "bo_ainv": (c_int, [_P, c_int64, c_int64, _P, _P, _P]),
+    "bo_sym_lower": (c_int, [_P, c_int64, c_int64, _P]),
+    "bo_post_kxt_rows": (c_int, [c_int, _P, c_int, c_int, c_int, _P, _P, c_int64, c_double, _P,
+                                 _P, _P]),
+    "bo_post_quad_plan": (c_int, [c_int64, c_int, c_int64, POINTER(c_int)]),
+    "bo_post_quad": (c_int, [_P, _P, c_int64, _P, c_int64, c_int, c_int64, _P, _P, _P]),
     "bo_post_split_table": (c_int, [c_int64, c_int, c_int64, c_int, _P, c_int, _P, c_int,
                                     POINTER(c_int), POINTER(c_int)]),
     "bo_qmc_finalize": (c_int, [c_int, c_int, c_int, c_int, _P, _P, _P, c_int64, c_double,
@@ -157,7 +162,9 @@ class QmcFinalizeArgs(_Args):
                        ("acq", _D), ("mean_out", _D), ("cov_out", _D), ("L_out", _D),
                        ("info_out", _D), ("jitter_out", _D), ("Tm", _D), ("r", c_int32),
                        ("fat", c_int32), ("ldT", c_int64), ("F", _D), ("ldF", c_int64),
-                       ("tau_relu", c_double), ("tau_max", c_double)]
+                       ("tau_relu", c_double), ("tau_max", c_double),
+                       ("nparts", c_int32), ("sym_parts", c_int32), ("status_out", _D),
+                       ("status_count", _D)]
 
 
 class QmcBackwardArgs(_Args):

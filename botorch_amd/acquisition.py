@@ -156,8 +156,8 @@ class MCAcquisitionFunction(AcquisitionFunction):
 def _fused_mc(X3: torch.Tensor, acqf, mode: int, best_f: float, best_f_s, Z: torch.Tensor):
     """qEI / qLogEI value of B t-batches on the gfx950 fused path through
     bo::qmc_acq (one torch.ops call; its registered backward gives dX).  The
-    jitter-ladder status is checked now when a gradient follows (the root must
-    have factored), else one call later (kernels.raise_not_psd_deferred)."""
+    jitter-ladder status is read at the end of the backward when a gradient
+    follows, else one call later (kernels.raise_not_psd_deferred)."""
     from . import ops  # noqa: F401  (torch.ops.bo registration)
     model = acqf.model
     cache = model.prediction_cache()
@@ -172,23 +172,27 @@ def _fused_mc(X3: torch.Tensor, acqf, mode: int, best_f: float, best_f_s, Z: tor
     if not need_grad and not kernels.SYNC_LADDER and idx not in kernels._CAPTURE:
         # eager forward-only: ONE native call issues the whole chain and defers
         # the ladder status (the previous call's is returned and acted on here)
-        outs = _lib.torch_ops().qmc_acq_native(
-            X3.contiguous(), cache.Xt_scaled, cache.U, cache.Linv, cache.beta, cache.lengthscale,
+        acq, prev = _lib.torch_ops().qmc_acq_eager(
+            X3.contiguous(), cache.Xt_scaled, cache.U, cache.beta, cache.lengthscale,
             Z, best_f_s, int(cache.kind), int(mode), int(cache.n), float(cache.outputscale),
             float(cache.constant), float(ymean), float(ystd), float(best_f), bool(fat),
-            float(tau_relu), float(tau_max), False, kernels.kxt_cap(dev), True)
-        kernels.ladder_prev_outcome(outs[8], idx, type(acqf).__name__)
-        return outs[0]
+            float(tau_relu), float(tau_max), kernels.kxt_cap(dev),
+            kernels.quad_ainv(cache, X3.shape[0], X3.shape[1]), cache.alpha)
+        kernels.ladder_prev_outcome(prev, idx, type(acqf).__name__)
+        return acq
     outs = torch.ops.bo.qmc_acq(
         X3, cache.Xt, cache.Xt_scaled, cache.U, cache.Linv, cache.beta, cache.alpha,
         cache.lengthscale, Z, best_f_s, int(cache.kind), int(mode), float(cache.outputscale),
         float(cache.constant), float(ymean), float(ystd), float(best_f), bool(fat),
-        float(tau_relu), float(tau_max), bool(need_grad))
+        float(tau_relu), float(tau_max), bool(need_grad),
+        None if need_grad else kernels.quad_ainv(cache, X3.shape[0], X3.shape[1]))
     acq, jit, info = outs[0], outs[6], outs[7]
-    if need_grad:
-        kernels._raise_not_psd(info, jit, type(acqf).__name__)
-    else:
-        kernels.raise_not_psd_deferred(info, jit, type(acqf).__name__)
+    # deferred either way: with a gradient the status is read at the end of the
+    # registered backward (ops._acq_bwd), once the backward's launches are
+    # queued behind the forward -- so the evaluation that produced a failed
+    # root raises NotPSDError (as gen.py's closure sees the reference's) but
+    # the device does not drain between the forward and the backward
+    kernels.raise_not_psd_deferred(info, jit, type(acqf).__name__)
     return acq
 
 def _ensemble_mean(model, acq: torch.Tensor) -> torch.Tensor:

@@ -1,4 +1,4 @@
-// Parameter-struct entry points of the C ABI (include/botorch_amd.h, ABI 9):
+// Parameter-struct entry points of the C ABI (include/botorch_amd.h, ABI 9-11):
 // each validates the struct header and forwards to the positional function.
 // Host code only (g++): no device work of its own.
 #include <cstdio>
@@ -35,6 +35,17 @@ int bo_post_partials_layout(int kind, const double* Xq, int B, int q, int d,
                             double* Rt, int kc_len, double* work, const double* Qc, int rq,
                             int64_t ldq, double* Cx, const double* Kt, int rt_layout, void* stream);
 
+// bo_qmc_finalize with the quad-plan partials and the fused ladder status of
+// ABI 11 (qmc.hip)
+int bo_qmc_finalize_ext(int kind, int mode, int B, int q, const double* Xq, const double* Spart,
+                        const double* mpart, int64_t n, double outputscale, double constant,
+                        double ymean, double ystd, const double* Z, int S, double best_f,
+                        const double* best_f_s, int max_tries, double jitter0, double* acq,
+                        double* mean_out, double* cov_out, double* L_out, int* info_out,
+                        double* jitter_out, const double* Tm, int r, int64_t ldT, const double* F,
+                        int64_t ldF, int fat, double tau_relu, double tau_max, int nparts,
+                        int sym_parts, double* status_out, int* status_count, void* stream);
+
 int bo_post_partials_v(const BoPostPartialsArgs* a, void* stream) {
   if (!header_ok(a, "bo_post_partials_v")) return BO_ERR_ARG;
   return bo_post_partials_layout(a->kind, a->Xq, a->B, a->q, a->d, a->Xt_scaled, a->n, a->U,
@@ -45,11 +56,12 @@ int bo_post_partials_v(const BoPostPartialsArgs* a, void* stream) {
 
 int bo_qmc_finalize_v(const BoQmcFinalizeArgs* a, void* stream) {
   if (!header_ok(a, "bo_qmc_finalize_v")) return BO_ERR_ARG;
-  return bo_qmc_finalize(a->kind, a->mode, a->B, a->q, a->Xq, a->Spart, a->mpart, a->n,
-                         a->outputscale, a->constant, a->ymean, a->ystd, a->Z, a->S, a->best_f,
-                         a->best_f_s, a->max_tries, a->jitter0, a->acq, a->mean_out, a->cov_out,
-                         a->L_out, a->info_out, a->jitter_out, a->Tm, a->r, a->ldT, a->F, a->ldF,
-                         a->fat, a->tau_relu, a->tau_max, stream);
+  return bo_qmc_finalize_ext(a->kind, a->mode, a->B, a->q, a->Xq, a->Spart, a->mpart, a->n,
+                             a->outputscale, a->constant, a->ymean, a->ystd, a->Z, a->S,
+                             a->best_f, a->best_f_s, a->max_tries, a->jitter0, a->acq,
+                             a->mean_out, a->cov_out, a->L_out, a->info_out, a->jitter_out, a->Tm,
+                             a->r, a->ldT, a->F, a->ldF, a->fat, a->tau_relu, a->tau_max,
+                             a->nparts, a->sym_parts, a->status_out, a->status_count, stream);
 }
 
 int bo_qmc_backward_v(const BoQmcBackwardArgs* a, void* stream) {

@@ -607,20 +607,46 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
 // average) instead of re-evaluating its exponentials each time: at C3 the
 // posterior kernel runs 3.0 ms from precomputed values against 3.7 ms with
 // the exponentials between its MFMAs, for 0.08 ms of build.
-template <int KIND, int ND>
+// RowsFromX (bo_post_kxt_rows): the thread takes its test row straight from
+// X (B x q x d) divided by the lengthscale, and the blockIdx.y == 0 threads
+// write the padded row layout Xq (prepare_rows_kernel's output) on the way --
+// one launch instead of two.
+struct RowsFromX {
+  const double* X;
+  const double* ls;
+  int B, q, d, Qp;
+  double* Xq_out;
+};
+
+template <int KIND, int ND, int KK = KXT_K, bool FROMX = false>
 __global__ __launch_bounds__(256) void kxt_build_kernel(const double* __restrict__ Xq, int nrows,
                                                         const double* __restrict__ Xt, int n,
                                                         int np, int nrows_pad, double outputscale,
-                                                        double* __restrict__ Kt) {
+                                                        double* __restrict__ Kt,
+                                                        RowsFromX rx = RowsFromX{}) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  const int k0 = blockIdx.y * KXT_K;
+  const int k0 = blockIdx.y * KK;
   const bool iv = i < nrows;
   double xi[ND];
+  if constexpr (FROMX) {
+    const int b = i / rx.Qp, a = i - (i / rx.Qp) * rx.Qp;
+    const bool real = iv && b < rx.B && a < rx.q;
 #pragma unroll
-  for (int t = 0; t < ND; ++t) xi[t] = iv ? Xq[(int64_t)i * DP + t] : 0.0;
+    for (int t = 0; t < ND; ++t)
+      xi[t] = (real && t < rx.d) ? rx.X[((int64_t)b * rx.q + a) * rx.d + t] / rx.ls[t] : 0.0;
+    if (blockIdx.y == 0 && i < nrows_pad) {
+#pragma unroll
+      for (int t = 0; t < DP; ++t)
+        rx.Xq_out[(int64_t)i * DP + t] =
+            (real && t < rx.d) ? rx.X[((int64_t)b * rx.q + a) * rx.d + t] / rx.ls[t] : 0.0;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < ND; ++t) xi[t] = iv ? Xq[(int64_t)i * DP + t] : 0.0;
+  }
   if (i >= nrows_pad) return;
 #pragma unroll 4
-  for (int kk = 0; kk < KXT_K; ++kk) {
+  for (int kk = 0; kk < KK; ++kk) {
     const int k = k0 + kk;
     if (k < np) Kt[(int64_t)k * nrows_pad + i] = eval_kernel_row<KIND, ND>(xi, Xt, n, k, outputscale, iv);
   }
@@ -963,10 +989,17 @@ int bo_post_kxt(int kind, const double* Xq, int B, int q, int d, const double* X
   const int np = nC * PC;
   const int nrows = B * Qp;
   hipStream_t st = as_stream(stream);
-  const dim3 grid((unsigned)ceil_div(nrows_pad, 256), (unsigned)ceil_div(np, KXT_K));
-#define BO_KXT(KIND, ND)                                                                   \
-  kxt_build_kernel<KIND, ND><<<grid, 256, 0, st>>>(Xq, nrows, Xt_scaled, (int)n, np, nrows_pad, \
-                                                   outputscale, Kt)
+  // 16 training points per thread where the grid fills the chip (C3: 4096
+  // workgroups); small grids (C2: 128 workgroups at 16) take 2 per thread
+  const bool small = ceil_div(nrows_pad, 256) * ceil_div(np, KXT_K) < 1024;
+  const dim3 grid((unsigned)ceil_div(nrows_pad, 256), (unsigned)ceil_div(np, small ? 2 : KXT_K));
+#define BO_KXT(KIND, ND)                                                                        \
+  if (small)                                                                                    \
+    kxt_build_kernel<KIND, ND, 2><<<grid, 256, 0, st>>>(Xq, nrows, Xt_scaled, (int)n, np,       \
+                                                        nrows_pad, outputscale, Kt);            \
+  else                                                                                          \
+    kxt_build_kernel<KIND, ND><<<grid, 256, 0, st>>>(Xq, nrows, Xt_scaled, (int)n, np, nrows_pad, \
+                                                     outputscale, Kt)
 #define BO_KXT_D(KIND)                       \
   switch (d) {                               \
     case 1: BO_KXT(KIND, 1); break;          \
@@ -984,6 +1017,51 @@ int bo_post_kxt(int kind, const double* Xq, int B, int q, int d, const double* X
   }
 #undef BO_KXT_D
 #undef BO_KXT
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+// bo_prepare_rows + bo_post_kxt in one launch: Xq and K*x^T from X itself.
+int bo_post_kxt_rows(int kind, const double* X, int B, int q, int d, const double* lengthscale,
+                     const double* Xt_scaled, int64_t n, double outputscale, double* Xq, double* Kt,
+                     void* stream) {
+  BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
+  BO_CHECK_ARG(d >= 1 && d <= DP, "fused posterior kernel supports 1 <= d <= %d", DP);
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  if (nrows_pad == 0) return BO_OK;  // no t-batches (empty outputs may carry null pointers)
+  BO_CHECK_ARG(X && lengthscale && Xt_scaled && Xq && Kt, "bo_post_kxt_rows: null buffer");
+  const int np = nC * PC;
+  const int nrows = B * Qp;
+  hipStream_t st = as_stream(stream);
+  const RowsFromX rx{X, lengthscale, B, q, d, Qp, Xq};
+  const bool small = ceil_div(nrows_pad, 256) * ceil_div(np, KXT_K) < 1024;
+  const dim3 grid((unsigned)ceil_div(nrows_pad, 256), (unsigned)ceil_div(np, small ? 2 : KXT_K));
+#define BO_KXTR(KIND, ND)                                                                      \
+  if (small)                                                                                   \
+    kxt_build_kernel<KIND, ND, 2, true><<<grid, 256, 0, st>>>(nullptr, nrows, Xt_scaled, (int)n, \
+                                                              np, nrows_pad, outputscale, Kt, rx); \
+  else                                                                                         \
+    kxt_build_kernel<KIND, ND, KXT_K, true><<<grid, 256, 0, st>>>(                              \
+        nullptr, nrows, Xt_scaled, (int)n, np, nrows_pad, outputscale, Kt, rx)
+#define BO_KXTR_D(KIND)                      \
+  switch (d) {                               \
+    case 1: BO_KXTR(KIND, 1); break;         \
+    case 2: BO_KXTR(KIND, 2); break;         \
+    case 3: BO_KXTR(KIND, 3); break;         \
+    case 4: BO_KXTR(KIND, 4); break;         \
+    case 5: BO_KXTR(KIND, 5); break;         \
+    case 6: BO_KXTR(KIND, 6); break;         \
+    default: BO_KXTR(KIND, 8); break;        \
+  }
+  if (kind == BO_RBF) {
+    BO_KXTR_D(BO_RBF)
+  } else {
+    BO_KXTR_D(BO_MATERN52)
+  }
+#undef BO_KXTR_D
+#undef BO_KXTR
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

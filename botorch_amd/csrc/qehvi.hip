@@ -15,12 +15,18 @@
 //
 // One workgroup per t-batch: its samples go to LDS, the hypercells are read
 // through L1/L2, threads stride over (sample, cell) pairs, the per-thread sums
-// reduce with wavefront shuffles.
+// reduce with wavefront shuffles.  C4 has only 128 t-batches for 256 CUs and
+// every (sample, cell) step waits on L1 / LDS loads and a data-dependent
+// subset loop, so the workgroups are wide: 16 waves (forward) / 8 waves
+// (backward, 220 VGPRs) per t-batch hide that latency (at 4 waves the forward
+// kernel issued one VALU instruction per ~25 cycles per wave, PMC r03).
 #include "common.h"
 
 namespace {
 
-constexpr int THREADS = 256;
+constexpr int THREADS = 256;   // mc_reduce_kernel
+constexpr int FWD_THREADS = 1024;
+constexpr int BWD_THREADS = 512;
 constexpr int QMAX = 12;
 constexpr int MMAX = 4;
 constexpr int LDS_SAMPLES_DOUBLES = 6144;  // 48 KiB of samples per pass
@@ -50,35 +56,51 @@ __device__ __forceinline__ double sample_value(int B, int b, int q, int p, int t
   return v;
 }
 
-template <int M>
-__global__ __launch_bounds__(THREADS) void qehvi_kernel(
+// CELLS_LDS: the K hypercells (shared by all samples: cell_stride 0) staged in
+// LDS once, so the (sample, cell) loop reads only LDS
+constexpr int LDS_CELL_DOUBLES = 2048;  // K * M <= 1024 (C4: 294 x 3)
+
+template <int M, int NT = FWD_THREADS, bool CELLS_LDS = false>
+__global__ __launch_bounds__(NT) void qehvi_kernel(
     int B, int q, const double* __restrict__ mean, const double* __restrict__ L,
     const double* __restrict__ Z, int S, const double* __restrict__ lo,
     const double* __restrict__ hi, int K, QehviExt ex, double* __restrict__ acq) {
   __shared__ double f[LDS_SAMPLES_DOUBLES];
-  __shared__ double red[THREADS / 64];
+  __shared__ double red[NT / 64];
+  __shared__ double cells[CELLS_LDS ? LDS_CELL_DOUBLES : 1];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int per_sample = q * M;
   const int chunk = LDS_SAMPLES_DOUBLES / per_sample;
+  if constexpr (CELLS_LDS) {
+    for (int e = tid; e < K * M; e += NT) {
+      cells[e] = lo[e];
+      cells[LDS_CELL_DOUBLES / 2 + e] = hi[e];
+    }
+  }
   double sum = 0.0;
   for (int s0 = 0; s0 < S; s0 += chunk) {
     const int ns = min(chunk, S - s0);
     __syncthreads();
-    for (int e = tid; e < ns * per_sample; e += THREADS) {
+    for (int e = tid; e < ns * per_sample; e += NT) {
       const int s = e / per_sample;
       f[e] = sample_value<M>(B, b, q, (e / M) % q, e % M, s0 + s, mean, L, Z, ex);
     }
     __syncthreads();
-    for (int e = tid; e < ns * K; e += THREADS) {
+    for (int e = tid; e < ns * K; e += NT) {
       const int s = e / K;
       const int k = e % K;
       double l[M], u[M];
       const int64_t co = (int64_t)(s0 + s) * ex.cstride + (int64_t)k * M;
 #pragma unroll
       for (int t = 0; t < M; ++t) {
-        l[t] = lo[co + t];
-        u[t] = hi[co + t];
+        if constexpr (CELLS_LDS) {
+          l[t] = cells[k * M + t];
+          u[t] = cells[LDS_CELL_DOUBLES / 2 + k * M + t];
+        } else {
+          l[t] = lo[co + t];
+          u[t] = hi[co + t];
+        }
       }
       const double* fs = f + s * per_sample;
       double a[QMAX][M];
@@ -117,7 +139,7 @@ __global__ __launch_bounds__(THREADS) void qehvi_kernel(
   __syncthreads();
   if (tid == 0) {
     double t = 0.0;
-    for (int w = 0; w < THREADS / 64; ++w) t += red[w];
+    for (int w = 0; w < NT / 64; ++w) t += red[w];
     acq[b] = t / S;
   }
 }
@@ -130,8 +152,8 @@ __global__ __launch_bounds__(THREADS) void qehvi_kernel(
 // clamped-at-lower term is zero with zero gradient).  df[s] is summed by one
 // 16-lane group over the cells in a fixed order (no atomics), then dmean_t[p] = sum_s df[s][p][t] and
 // dL_t[p][j] = sum_s df[s][p][t] Z[s][j m + t] (j <= p), scaled by dacq / S.
-template <int M>
-__global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
+template <int M, int NT = BWD_THREADS>
+__global__ __launch_bounds__(NT) void qehvi_backward_kernel(
     int B, int q, const double* __restrict__ mean, const double* __restrict__ L,
     const double* __restrict__ Z, int S, const double* __restrict__ lo,
     const double* __restrict__ hi, int K, QehviExt ex, const double* __restrict__ dacq,
@@ -150,7 +172,7 @@ __global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
   for (int s0 = 0; s0 < S; s0 += chunk) {
     const int ns = min(chunk, S - s0);
     __syncthreads();
-    for (int e = tid; e < ns * per_sample; e += THREADS) {
+    for (int e = tid; e < ns * per_sample; e += NT) {
       const int s = e / per_sample;
       f[e] = sample_value<M>(B, b, q, (e / M) % q, e % M, s0 + s, mean, L, Z, ex);
     }
@@ -158,7 +180,7 @@ __global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
     // GROUP consecutive lanes share one sample: lane g of the group takes the
     // cells k = g, g + GROUP, ...; the group's partial gradients reduce in a
     // fixed butterfly, so df (and every gradient) is bitwise reproducible
-    for (int s = tid / GROUP; s < ns; s += THREADS / GROUP) {
+    for (int s = tid / GROUP; s < ns; s += NT / GROUP) {
       const double* fs = f + s * per_sample;
       double gacc[QMAX][M];
 #pragma unroll
@@ -231,13 +253,13 @@ __global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
     }
     __syncthreads();
     if (dF) {  // cotangent of the cached-root baseline term (rows b * Qp + p)
-      for (int e = tid; e < ns * per_sample; e += THREADS) {
+      for (int e = tid; e < ns * per_sample; e += NT) {
         const int s = e / per_sample, p = (e / M) % q, t = e % M;
         dF[t * ex.sF + (int64_t)(s0 + s) * ex.ldF + (int64_t)b * ex.Qp + p] = g * df[e];
       }
     }
     for (int w = 0; w < 2; ++w) {
-      const int ent = tid + w * THREADS;
+      const int ent = tid + w * NT;
       if (ent >= nent) continue;
       const int per_t = q * (q + 3) / 2;
       const int t = ent / per_t;
@@ -257,7 +279,7 @@ __global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
     }
   }
   for (int w = 0; w < 2; ++w) {
-    const int ent = tid + w * THREADS;
+    const int ent = tid + w * NT;
     if (ent >= nent) continue;
     const int per_t = q * (q + 3) / 2;
     const int t = ent / per_t;
@@ -277,7 +299,7 @@ __global__ __launch_bounds__(THREADS) void qehvi_backward_kernel(
     }
   }
   // strict upper triangle of dL
-  for (int e = tid; e < M * q * q; e += THREADS) {
+  for (int e = tid; e < M * q * q; e += NT) {
     const int t = e / (q * q), p = (e / q) % q, j = e % q;
     if (j > p) dL[(((int64_t)t * B + b) * q + p) * q + j] = 0.0;
   }
@@ -323,12 +345,21 @@ extern "C" int bo_qehvi(int B, int q, int m, const double* mean, const double* L
   if (B == 0) return BO_OK;
   hipStream_t st = as_stream(stream);
   const QehviExt ex{cell_stride, F, ldF, sF, Qp};
-  if (m == 2)
-    qehvi_kernel<2><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, acq);
-  else if (m == 3)
-    qehvi_kernel<3><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, acq);
-  else
-    qehvi_kernel<4><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, acq);
+  const bool cl = cell_stride == 0 && (int64_t)K * m <= LDS_CELL_DOUBLES / 2;
+#define BO_QF(MM)                                                                              \
+  if (cl)                                                                                      \
+    qehvi_kernel<MM, FWD_THREADS, true><<<B, FWD_THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, \
+                                                                    cell_hi, K, ex, acq);      \
+  else                                                                                         \
+    qehvi_kernel<MM><<<B, FWD_THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, acq)
+  if (m == 2) {
+    BO_QF(2);
+  } else if (m == 3) {
+    BO_QF(3);
+  } else {
+    BO_QF(4);
+  }
+#undef BO_QF
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
@@ -347,10 +378,10 @@ extern "C" int bo_qehvi_backward(int B, int q, int m, const double* mean, const 
   if (B == 0) return BO_OK;
   hipStream_t st = as_stream(stream);
   const QehviExt ex{cell_stride, F, ldF, sF, Qp};
-#define BO_QB(MM) qehvi_backward_kernel<MM><<<B, THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, dacq, dmean, dL, dF)
-  if (m == 2) BO_QB(2);
-  else if (m == 3) BO_QB(3);
-  else BO_QB(4);
+#define BO_QB(MM, NT) qehvi_backward_kernel<MM, NT><<<B, NT, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, dacq, dmean, dL, dF)
+  if (m == 2) BO_QB(2, BWD_THREADS);
+  else if (m == 3) BO_QB(3, BWD_THREADS);
+  else BO_QB(4, 256);  // m = 4 needs 256 VGPRs: 4 waves per workgroup
 #undef BO_QB
   BO_LAUNCH_CHECK();
   return BO_OK;

@@ -42,20 +42,30 @@ __host__ __device__ constexpr bool log_mode(int mode) {
   return mode == QMC_QLOGEI || mode == QMC_QLOGNEI;
 }
 
-// sum_{ct < n} p[ct * stride] with 8 independent partial sums, so the column
-// tiles' loads are in flight together instead of one latency per tile.
+// sum_{ct < n} p[ct * stride] with U independent partial sums, so U of the
+// partials' loads are in flight together instead of one latency per partial
+// (U = 16 for the quad plan's long partial lists: C2 has 136 block pairs).
+template <int U = 8>
 __device__ __forceinline__ double strided_sum(const double* __restrict__ p, int64_t stride, int n) {
-  double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  double s[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) s[u] = 0.0;
   int ct = 0;
-  for (; ct + 8 <= n; ct += 8) {
-    double v[8];
+  for (; ct + U <= n; ct += U) {
+    double v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(ct + u) * stride];
+    for (int u = 0; u < U; ++u) v[u] = p[(int64_t)(ct + u) * stride];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s[u] += v[u];
+    for (int u = 0; u < U; ++u) s[u] += v[u];
   }
-  for (int u = 0; ct < n; ++ct, ++u) s[u] += p[(int64_t)ct * stride];
-  return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (ct + u < n) s[u] += p[(int64_t)(ct + u) * stride];
+#pragma unroll
+  for (int w = U / 2; w > 0; w >>= 1)
+#pragma unroll
+    for (int u = 0; u < w; ++u) s[u] += s[u + w];
+  return s[0];
 }
 
 template <int KIND, int MODE>
@@ -67,7 +77,8 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     double* __restrict__ acq, double* __restrict__ mean_out, double* __restrict__ cov_out,
     double* __restrict__ L_out, int* __restrict__ info_out, double* __restrict__ jitter_out,
     const double* __restrict__ Tm, int r, int64_t ldT, const double* __restrict__ F,
-    int64_t ldF, LogRedParams lp) {
+    int64_t ldF, LogRedParams lp, int sym, double* __restrict__ status_out,
+    int* __restrict__ status_count) {
   // qNEI with the cached baseline root (utils/low_rank.py:85-173): Tm (r x ldT)
   // holds bl_chol^T = L_rr^{-1} Sigma'(X_base, X) per padded test row and F
   // (S x ldF) the samples' baseline term Z_base T; then
@@ -79,6 +90,9 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   __shared__ double red2[THREADS / 64];
   __shared__ int s_info;
   __shared__ double s_jit;
+  __shared__ int s_last;
+  __shared__ double psum[THREADS];
+  __shared__ double msum[THREADS];
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -88,12 +102,40 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   const int nrows16 = nrows_pad >> 4;
   const double s2 = ystd * ystd;
 
-  // 1. finalise the q x q covariance and the mean.
-  if (tid < q * q) {
+  // 1. finalise the q x q covariance and the mean.  The partial sums use all
+  // threads: nsplit threads per entry (q = 8: 4) each take every nsplit-th
+  // partial, combined in a fixed order below -- the quad plan's partial count
+  // (C2: 136 block pairs, summed as P + P^T) would otherwise put ~35 dependent
+  // load rounds on 64 threads.
+  const int E = q * q;
+  const int nsplit = THREADS / E;  // >= 1 (q <= 16)
+  if (tid < E * nsplit) {
+    const int e = tid % E, j = tid / E;
+    const int a = e / q, c = e % q;
+    const int64_t pstride = (int64_t)nrows16 * 256;
+    const int cnt = nC > j ? (nC - 1 - j) / nsplit + 1 : 0;
+    const double* sp = Spart + (int64_t)j * pstride + (int64_t)tile * 256 + (off + a) * 16 + (off + c);
+    double part = strided_sum<16>(sp, pstride * nsplit, cnt);
+    if (sym) {  // quad plan partials (quad.hip): Sigma = sum_p P_p + P_p^T
+      const double* spt =
+          Spart + (int64_t)j * pstride + (int64_t)tile * 256 + (off + c) * 16 + (off + a);
+      part += strided_sum<16>(spt, pstride * nsplit, cnt);
+    }
+    psum[tid] = part;
+  }
+  {  // the mean's partials likewise: THREADS / q threads per test row
+    const int ms = THREADS / q;
+    const int a = tid % q, j = tid / q;
+    if (j < ms) {
+      const int cnt = nC > j ? (nC - 1 - j) / ms + 1 : 0;
+      msum[tid] = strided_sum<16>(mpart + (int64_t)j * nrows_pad + row0 + a, (int64_t)nrows_pad * ms, cnt);
+    }
+  }
+  __syncthreads();
+  if (tid < E) {
     const int a = tid / q, c = tid % q;
     double acc = 0.0;
-    const double* sp = Spart + (int64_t)tile * 256 + (off + a) * 16 + (off + c);
-    acc = strided_sum(sp, (int64_t)nrows16 * 256, nC);
+    for (int j = 0; j < nsplit; ++j) acc += psum[j * E + tid];
     double kxx;
     if (a == c) {
       kxx = outputscale;
@@ -119,8 +161,7 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   }
   if (tid < q) {
     double m = 0.0;
-    const double* mp = mpart + row0 + tid;
-    m = strided_sum(mp, nrows_pad, nC);
+    for (int j = 0; j < THREADS / q; ++j) m += msum[j * q + tid];
     const double v = ymean + ystd * (constant + m);
     mu[tid] = v;
     if (mean_out) mean_out[(int64_t)b * q + tid] = v;
@@ -171,8 +212,48 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   __syncthreads();
   const int info = s_info;
   if (tid == 0) {
-    if (info_out) info_out[b] = info;
-    if (jitter_out) jitter_out[b] = s_jit;
+    // agent-scope (write-through) stores: the fused status below reads them
+    // from other XCDs' workgroups without an L2 write-back fence
+    if (info_out) __hip_atomic_store(info_out + b, info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (jitter_out)
+      __hip_atomic_store(jitter_out + b, s_jit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (status_out != nullptr) {
+    // The batch's ladder status (bo_ladder_status's [max info, max jitter])
+    // folded in: every workgroup publishes its entries and counts itself in;
+    // the last to arrive reduces all B of them and re-arms the counter.  The
+    // hand-off follows MI355X_MICROARCH.md's inter-workgroup recipe (as
+    // chol_dag.hip): write-through stores drained (vmcnt(0)) before the
+    // agent-scope count, agent-scope loads on the reading side -- an
+    // agent-scope release fence would write back the whole L2 per workgroup.
+    if (tid == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      s_last = __hip_atomic_fetch_add(status_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (s_last) {
+      double mi = 0.0, mj = 0.0;
+      for (int bb = tid; bb < (int)gridDim.x; bb += THREADS) {
+        mi = fmax(mi, (double)__hip_atomic_load(info_out + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        mj = fmax(mj, __hip_atomic_load(jitter_out + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        mi = fmax(mi, __shfl_xor(mi, o));
+        mj = fmax(mj, __shfl_xor(mj, o));
+      }
+      if ((tid & 63) == 0) {
+        red[tid >> 6] = mi;
+        red2[tid >> 6] = mj;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        status_out[0] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+        status_out[1] = fmax(fmax(red2[0], red2[1]), fmax(red2[2], red2[3]));
+        __hip_atomic_store(status_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();  // red / red2 are reused by the reduction below
+    }
   }
   if (L_out && tid < q * q) {
     const int a = tid / q, c = tid % q;
@@ -256,6 +337,9 @@ struct QmcArgs {
   const double* F;
   int64_t ldF;
   LogRedParams lp;
+  int sym;
+  double* status_out;
+  int* status_count;
 };
 
 template <int KIND, int MODE>
@@ -263,7 +347,8 @@ void launch_mode(int B, const QmcArgs& a, hipStream_t st) {
   qmc_kernel<KIND, MODE><<<B, THREADS, 0, st>>>(
       a.q, a.Qp, a.Xq, a.Spart, a.mpart, a.nC, a.nrows_pad, a.outputscale, a.constant, a.ymean,
       a.ystd, a.Z, a.S, a.best_f, a.best_f_s, a.max_tries, a.jitter0, a.acq, a.mean_out,
-      a.cov_out, a.L_out, a.info_out, a.jitter_out, a.Tm, a.r, a.ldT, a.F, a.ldF, a.lp);
+      a.cov_out, a.L_out, a.info_out, a.jitter_out, a.Tm, a.r, a.ldT, a.F, a.ldF, a.lp, a.sym,
+      a.status_out, a.status_count);
 }
 
 template <int KIND>
@@ -280,6 +365,17 @@ void launch_qmc(int mode, int B, const QmcArgs& a, hipStream_t st) {
 
 extern "C" int bo_post_geometry(int64_t B, int q, int64_t n, int* Qp, int* nrows_pad, int* nC);
 
+extern "C" int bo_qmc_finalize_ext(int kind, int mode, int B, int q, const double* Xq,
+                                   const double* Spart, const double* mpart, int64_t n,
+                                   double outputscale, double constant, double ymean,
+                                   double ystd, const double* Z, int S, double best_f,
+                                   const double* best_f_s, int max_tries, double jitter0,
+                                   double* acq, double* mean_out, double* cov_out, double* L_out,
+                                   int* info_out, double* jitter_out, const double* Tm, int r,
+                                   int64_t ldT, const double* F, int64_t ldF, int fat,
+                                   double tau_relu, double tau_max, int nparts, int sym_parts,
+                                   double* status_out, int* status_count, void* stream);
+
 extern "C" int bo_qmc_finalize(int kind, int mode, int B, int q, const double* Xq,
                                const double* Spart, const double* mpart, int64_t n,
                                double outputscale, double constant, double ymean, double ystd,
@@ -289,7 +385,28 @@ extern "C" int bo_qmc_finalize(int kind, int mode, int B, int q, const double* X
                                double* jitter_out, const double* Tm, int r, int64_t ldT,
                                const double* F, int64_t ldF, int fat, double tau_relu,
                                double tau_max, void* stream) {
+  return bo_qmc_finalize_ext(kind, mode, B, q, Xq, Spart, mpart, n, outputscale, constant, ymean,
+                             ystd, Z, S, best_f, best_f_s, max_tries, jitter0, acq, mean_out,
+                             cov_out, L_out, info_out, jitter_out, Tm, r, ldT, F, ldF, fat,
+                             tau_relu, tau_max, 0, 0, nullptr, nullptr, stream);
+}
+
+extern "C" int bo_qmc_finalize_ext(int kind, int mode, int B, int q, const double* Xq,
+                               const double* Spart, const double* mpart, int64_t n,
+                               double outputscale, double constant, double ymean, double ystd,
+                               const double* Z, int S, double best_f, const double* best_f_s,
+                               int max_tries, double jitter0, double* acq, double* mean_out,
+                               double* cov_out, double* L_out, int* info_out,
+                               double* jitter_out, const double* Tm, int r, int64_t ldT,
+                               const double* F, int64_t ldF, int fat, double tau_relu,
+                               double tau_max, int nparts, int sym_parts, double* status_out,
+                               int* status_count, void* stream) {
   BO_CHECK_ARG(mode >= 0 && mode <= 5, "bo_qmc_finalize: bad mode %d", mode);
+  BO_CHECK_ARG(nparts >= 0 && (sym_parts == 0 || nparts > 0),
+               "bo_qmc_finalize: nparts %d / sym_parts %d", nparts, sym_parts);
+  BO_CHECK_ARG(status_out == nullptr ||
+                   (status_count && info_out && jitter_out && mode != QMC_POSTERIOR),
+               "bo_qmc_finalize: the fused ladder status needs a counter, info and jitter outputs");
   if (B == 0) return BO_OK;  // no t-batches (empty outputs may carry null pointers)
   BO_CHECK_ARG(!log_mode(mode) || (tau_relu > 0.0 && tau_max > 0.0),
                "bo_qmc_finalize: tau_relu and tau_max must be positive");
@@ -303,10 +420,12 @@ extern "C" int bo_qmc_finalize(int kind, int mode, int B, int q, const double* X
   int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
   if (s) return s;
   if (B == 0) return BO_OK;
+  if (nparts > 0) nC = nparts;
   QmcArgs a{q,      Qp,     Xq,       Spart,     mpart,     nC,      nrows_pad, outputscale,
             constant, ymean, ystd,   Z,        S,         best_f,  best_f_s,  max_tries,
             jitter0, acq,    mean_out, cov_out,  L_out,     info_out, jitter_out, Tm,
-            r,       ldT,    F,        ldF,      LogRedParams{tau_relu, tau_max, fat}};
+            r,       ldT,    F,        ldF,      LogRedParams{tau_relu, tau_max, fat},
+            sym_parts, status_out, status_count};
   hipStream_t st = as_stream(stream);
   if (kind == BO_RBF) launch_qmc<BO_RBF>(mode, B, a, st);
   else launch_qmc<BO_MATERN52>(mode, B, a, st);

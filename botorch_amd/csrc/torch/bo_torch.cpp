@@ -50,7 +50,9 @@ void check_f64(const at::Tensor& t, const char* name) {
 // ---- deferred ladder status ---------------------------------------------------------
 struct Slot {
   double* host = nullptr;   // pinned [info_max, jitter_max]
+  double* host_dev = nullptr;  // the same pinned words as a device pointer (zero-copy)
   double* dev = nullptr;    // device [info_max, jitter_max]
+  int* count = nullptr;     // arrival counter of the fused status (qmc_kernel re-zeroes it)
   hipEvent_t ev = nullptr;
 };
 struct DeviceLadder {
@@ -64,9 +66,13 @@ DeviceLadder& ladder_for(int dev) {
   auto& L = g_ladder[dev];
   if (!L.slot[0].host) {
     for (auto& s : L.slot) {
-      hk(hipHostMalloc(reinterpret_cast<void**>(&s.host), 2 * sizeof(double), hipHostMallocDefault),
-         "hipHostMalloc");
+      hk(hipHostMalloc(reinterpret_cast<void**>(&s.host), 2 * sizeof(double),
+                       hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+      hk(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.host_dev), s.host, 0),
+         "hipHostGetDevicePointer");
       hk(hipMalloc(reinterpret_cast<void**>(&s.dev), 2 * sizeof(double)), "hipMalloc");
+      hk(hipMalloc(reinterpret_cast<void**>(&s.count), sizeof(int)), "hipMalloc");
+      hk(hipMemset(s.count, 0, sizeof(int)), "hipMemset");
       hk(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
     }
   }
@@ -89,22 +95,33 @@ at::Tensor take_pending(DeviceLadder& L) {
   return out;
 }
 
-// Enqueue this call's status into a free slot, then return (and clear) the
-// previous call's.
-at::Tensor defer_status(const at::Tensor& info, const at::Tensor& jitter, void* stream, int dev) {
-  std::lock_guard<std::mutex> lk(g_ladder_mu);
-  auto& L = ladder_for(dev);
-  const int prev = L.pending;
-  const int mine = prev == 0 ? 1 : 0;
+// The slot this call's status goes to: the one not pending.  Caller holds
+// g_ladder_mu until publish_slot.
+int free_slot(DeviceLadder& L) { return L.pending == 0 ? 1 : 0; }
+
+// Copy the slot's device status to its pinned host words (unless the kernel
+// wrote them there itself: zero_copy) behind an event, then return (and
+// clear) the previous call's.  Caller holds g_ladder_mu.
+at::Tensor publish_slot(DeviceLadder& L, int mine, void* stream, bool zero_copy = false) {
   Slot& s = L.slot[mine];
-  ck(bo_ladder_status(info.data_ptr<int>(), jitter.data_ptr<double>(), info.numel(), s.dev, stream),
-     "ladder_status");
-  hk(hipMemcpyAsync(s.host, s.dev, 2 * sizeof(double), hipMemcpyDeviceToHost,
-                    static_cast<hipStream_t>(stream)), "hipMemcpyAsync");
+  if (!zero_copy)
+    hk(hipMemcpyAsync(s.host, s.dev, 2 * sizeof(double), hipMemcpyDeviceToHost,
+                      static_cast<hipStream_t>(stream)), "hipMemcpyAsync");
   hk(hipEventRecord(s.ev, static_cast<hipStream_t>(stream)), "hipEventRecord");
   auto out = take_pending(L);  // the previous forward's (enqueued long before)
   L.pending = mine;
   return out;
+}
+
+// Enqueue this call's status (bo_ladder_status over info / jitter) into a free
+// slot, then return (and clear) the previous call's.
+at::Tensor defer_status(const at::Tensor& info, const at::Tensor& jitter, void* stream, int dev) {
+  std::lock_guard<std::mutex> lk(g_ladder_mu);
+  auto& L = ladder_for(dev);
+  const int mine = free_slot(L);
+  ck(bo_ladder_status(info.data_ptr<int>(), jitter.data_ptr<double>(), info.numel(),
+                      L.slot[mine].dev, stream), "ladder_status");
+  return publish_slot(L, mine, stream);
 }
 
 // ---- post_partials launch timing (bench.py: HIP events around the launch) ------------
@@ -120,12 +137,18 @@ hipEvent_t timing_event(void* stream) {
 }
 
 // ---- the fused forward ------------------------------------------------------------------
-std::vector<at::Tensor> qmc_acq_native(
+// The fused forward.  lean (bo::qmc_acq_eager, forward-only eager calls):
+// every intermediate (rows, K*x^T, partials, split-k workspace, ladder
+// entries) is carved from ONE allocation and only [acq, previous status] is
+// returned -- each at::empty costs host time on the critical path of small
+// calls (C2: ~70 us of host issue per call against ~45 us of kernels).
+std::vector<at::Tensor> qmc_acq_impl(
     const at::Tensor& X, const at::Tensor& Xt_scaled, const at::Tensor& U, const at::Tensor& Linv,
     const at::Tensor& beta, const at::Tensor& lengthscale, const at::Tensor& Z,
     const c10::optional<at::Tensor>& best_f_s, int64_t kind, int64_t mode, int64_t n,
     double outputscale, double constant, double ymean, double ystd, double best_f, bool fat,
-    double tau_relu, double tau_max, bool need_grad, int64_t kxt_cap, bool defer_ladder) {
+    double tau_relu, double tau_max, bool need_grad, int64_t kxt_cap, bool defer_ladder,
+    const c10::optional<at::Tensor>& Ainv, const c10::optional<at::Tensor>& alpha, bool lean) {
   check_f64(X, "X");
   check_f64(Xt_scaled, "Xt_scaled");
   check_f64(U, "U");
@@ -138,6 +161,7 @@ std::vector<at::Tensor> qmc_acq_native(
   TORCH_CHECK(Xt_scaled.size(0) == n && lengthscale.numel() == d,
               "bo::qmc_acq_native: model and X disagree (n, d)");
   TORCH_CHECK(Z.dim() == 2 && Z.size(1) == q, "bo::qmc_acq_native: Z must be S x q");
+  TORCH_CHECK(!(lean && need_grad), "bo::qmc_acq_eager is forward-only");
   if (need_grad) check_f64(Linv, "Linv");
   const int dev = X.device().index();
   void* st = c10::hip::getCurrentHIPStream(dev).stream();
@@ -146,65 +170,103 @@ std::vector<at::Tensor> qmc_acq_native(
 
   int Qp = 0, nrows = 0, nC = 0;
   ck(bo_post_geometry(B, q, n, &Qp, &nrows, &nC), "post_geometry");
-  auto Xq = at::empty({nrows, 8}, f64);
-  auto Spart = at::empty({nC, nrows / 16, 16, 16}, f64);
-  auto mpart = at::empty({nC, nrows}, f64);
-  ck(bo_prepare_rows(X.data_ptr<double>(), B, q, d, lengthscale.data_ptr<double>(),
-                     Xq.data_ptr<double>(), st), "prepare_rows");
-  at::Tensor Rt = need_grad ? at::empty({int64_t(nC) * 128, nrows}, f64) : at::Tensor();
+  const bool kxt = np * int64_t(nrows) * 8 <= kxt_cap;
+  // forward-only small grids: the quad plan over the cached A^{-1} (quad.hip)
+  int npairs = 0;
+  const bool quad_operands = !need_grad && kxt && Ainv.has_value() && Ainv->defined() &&
+                             alpha.has_value() && alpha->defined();
+  if (quad_operands) {
+    check_f64(*Ainv, "Ainv");
+    check_f64(*alpha, "alpha");
+    TORCH_CHECK(Ainv->size(0) == np && Ainv->size(1) == np, "bo::qmc_acq_native: Ainv must be np x np");
+    ck(bo_post_quad_plan(B, q, n, &npairs), "post_quad_plan");
+  }
+  const int nparts = npairs > 0 ? npairs : nC;
   int kc = 0;
   int64_t we = 0;
-  ck(bo_post_split_plan(B, q, n, 0, &kc, &we), "post_split_plan");
-  at::Tensor work = kc ? at::empty({std::max<int64_t>(we, 1)}, f64) : at::Tensor();
-  at::Tensor Kt;
-  if (np * int64_t(nrows) * 8 <= kxt_cap) {
-    Kt = at::empty({np, nrows}, f64);
-    ck(bo_post_kxt(int(kind), Xq.data_ptr<double>(), B, q, d, Xt_scaled.data_ptr<double>(), n,
-                   outputscale, Kt.data_ptr<double>(), st), "post_kxt");
-  }
-  BoPostPartialsArgs pa{};
-  pa.struct_size = sizeof(pa);
-  pa.abi_version = BO_ABI_VERSION;
-  pa.kind = int(kind);
-  pa.B = B;
-  pa.q = q;
-  pa.d = d;
-  pa.Xq = Xq.data_ptr<double>();
-  pa.Xt_scaled = Xt_scaled.data_ptr<double>();
-  pa.n = n;
-  pa.U = U.data_ptr<double>();
-  pa.ldu = np;
-  pa.beta = beta.data_ptr<double>();
-  pa.outputscale = outputscale;
-  pa.Spart = Spart.data_ptr<double>();
-  pa.mpart = mpart.data_ptr<double>();
-  pa.Rt = mp(Rt);
-  pa.kc_len = kc;
-  pa.work = mp(work);
-  pa.Kt = cp(Kt);
-  if (need_grad) {
-    // the backward reads R^T in the blocked layout where its fused W -> dX
-    // pass applies (bo_post_w_dx), row-major everywhere else
-    int64_t wdx = 0;
-    ck(bo_post_w_dx_work(B, q, n, &wdx), "post_w_dx_work");
-    pa.rt_layout = (wdx > 0 && kc == 0) ? BO_RT_BLOCKED : BO_RT_ROWMAJOR;
+  if (npairs == 0) ck(bo_post_split_plan(B, q, n, 0, &kc, &we), "post_split_plan");
+
+  // one workspace for the intermediates (offsets in doubles, 16-B aligned)
+  auto al2 = [](int64_t v) { return (v + 1) & ~int64_t(1); };
+  const bool own_xq = need_grad;  // the backward keeps Xq
+  const int64_t o_spart = 0;
+  const int64_t o_mpart = o_spart + al2(int64_t(nparts) * nrows * 16);
+  const int64_t o_kt = o_mpart + al2(int64_t(nparts) * nrows);
+  const int64_t o_work = o_kt + (kxt ? al2(np * nrows) : 0);
+  const int64_t o_xq = o_work + (kc ? al2(std::max<int64_t>(we, 1)) : 0);
+  const int64_t o_info = o_xq + (own_xq ? 0 : al2(int64_t(nrows) * 8));
+  const int64_t o_jit = o_info + (lean ? al2((B + 1) / 2) : 0);
+  const int64_t total = o_jit + (lean ? al2(B) : 0);
+  auto ws = at::empty({std::max<int64_t>(total, 2)}, f64);
+  double* w = ws.data_ptr<double>();
+  double* Spart = w + o_spart;
+  double* mpart = w + o_mpart;
+  double* Kt = kxt ? w + o_kt : nullptr;
+  double* work = kc ? w + o_work : nullptr;
+  at::Tensor Xq_t = own_xq ? at::empty({nrows, 8}, f64) : at::Tensor();
+  double* Xq = own_xq ? Xq_t.data_ptr<double>() : w + o_xq;
+  at::Tensor Rt = need_grad ? at::empty({int64_t(nC) * 128, nrows}, f64) : at::Tensor();
+
+  if (kxt) {  // rows and K*x^T in one launch
+    ck(bo_post_kxt_rows(int(kind), X.data_ptr<double>(), B, q, d, lengthscale.data_ptr<double>(),
+                        Xt_scaled.data_ptr<double>(), n, outputscale, Xq, Kt, st), "post_kxt_rows");
+  } else {
+    ck(bo_prepare_rows(X.data_ptr<double>(), B, q, d, lengthscale.data_ptr<double>(), Xq, st),
+       "prepare_rows");
   }
   hipEvent_t t0 = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_time_mu);
     if (g_time_on) t0 = timing_event(st);
   }
-  ck(bo_post_partials_v(&pa, st), "post_partials");
+  if (npairs > 0) {
+    ck(bo_post_quad(Kt, Ainv->data_ptr<double>(), np, alpha->data_ptr<double>(), B, q, n, Spart,
+                    mpart, st), "post_quad");
+  } else {
+    BoPostPartialsArgs pa{};
+    pa.struct_size = sizeof(pa);
+    pa.abi_version = BO_ABI_VERSION;
+    pa.kind = int(kind);
+    pa.B = B;
+    pa.q = q;
+    pa.d = d;
+    pa.Xq = Xq;
+    pa.Xt_scaled = Xt_scaled.data_ptr<double>();
+    pa.n = n;
+    pa.U = U.data_ptr<double>();
+    pa.ldu = np;
+    pa.beta = beta.data_ptr<double>();
+    pa.outputscale = outputscale;
+    pa.Spart = Spart;
+    pa.mpart = mpart;
+    pa.Rt = mp(Rt);
+    pa.kc_len = kc;
+    pa.work = work;
+    pa.Kt = Kt;
+    if (need_grad) {
+      // the backward reads R^T in the blocked layout where its fused W -> dX
+      // pass applies (bo_post_w_dx), row-major everywhere else
+      int64_t wdx = 0;
+      ck(bo_post_w_dx_work(B, q, n, &wdx), "post_w_dx_work");
+      pa.rt_layout = (wdx > 0 && kc == 0) ? BO_RT_BLOCKED : BO_RT_ROWMAJOR;
+    }
+    ck(bo_post_partials_v(&pa, st), "post_partials");
+  }
   if (t0) {
     std::lock_guard<std::mutex> lk(g_time_mu);
     g_time_ev.emplace_back(t0, timing_event(st));
   }
 
   auto acq = at::empty({B}, f64);
-  auto info = at::empty({B}, X.options().dtype(at::kInt));
-  auto jit = at::empty({B}, f64);
-  at::Tensor mean = need_grad ? at::empty({B, q}, f64) : at::empty({0}, f64);
-  at::Tensor L = need_grad ? at::empty({B, q, q}, f64) : at::empty({0}, f64);
+  at::Tensor info, jit;
+  if (!lean) {
+    info = at::empty({B}, X.options().dtype(at::kInt));
+    jit = at::empty({B}, f64);
+  }
+  int* info_p = lean ? reinterpret_cast<int*>(w + o_info) : info.data_ptr<int>();
+  double* jit_p = lean ? w + o_jit : jit.data_ptr<double>();
+  at::Tensor mean = need_grad ? at::empty({B, q}, f64) : at::Tensor();
+  at::Tensor L = need_grad ? at::empty({B, q, q}, f64) : at::Tensor();
   const at::Tensor bfs = best_f_s.has_value() ? best_f_s->contiguous() : at::Tensor();
   BoQmcFinalizeArgs fa{};
   fa.struct_size = sizeof(fa);
@@ -213,9 +275,9 @@ std::vector<at::Tensor> qmc_acq_native(
   fa.mode = int(mode);
   fa.B = B;
   fa.q = q;
-  fa.Xq = Xq.data_ptr<double>();
-  fa.Spart = Spart.data_ptr<double>();
-  fa.mpart = mpart.data_ptr<double>();
+  fa.Xq = Xq;
+  fa.Spart = Spart;
+  fa.mpart = mpart;
   fa.n = n;
   fa.outputscale = outputscale;
   fa.constant = constant;
@@ -230,23 +292,70 @@ std::vector<at::Tensor> qmc_acq_native(
   fa.acq = acq.data_ptr<double>();
   fa.mean_out = mp(mean);
   fa.L_out = mp(L);
-  fa.info_out = info.data_ptr<int>();
-  fa.jitter_out = jit.data_ptr<double>();
+  fa.info_out = info_p;
+  fa.jitter_out = jit_p;
   fa.fat = fat ? 1 : 0;
   fa.tau_relu = tau_relu;
   fa.tau_max = tau_max;
-  ck(bo_qmc_finalize_v(&fa, st), "qmc_finalize");
+  fa.nparts = npairs;
+  fa.sym_parts = npairs > 0 ? 1 : 0;
 
   // (the backward's W = R L^-1 is formed by qmc_acq_backward_native, fused
   // into its dX reduction where the grid allows: nothing of it is stored here)
-  at::Tensor Wt = at::empty({0}, f64);
-  at::Tensor prev = at::zeros({3}, at::TensorOptions().dtype(at::kDouble));
-  if (defer_ladder && B > 0) prev = defer_status(info, jit, st, dev);
-  if (!need_grad) {
-    Xq = at::empty({0}, f64);
-    Rt = at::empty({0}, f64);
+  at::Tensor prev;
+  if (defer_ladder && B > 0 && mode != BO_QMC_POSTERIOR) {
+    // the ladder status reduced by the finalisation launch itself (its last
+    // workgroup) straight into this call's pinned slot (zero-copy: no copy
+    // launch), read behind an event one call later
+    std::lock_guard<std::mutex> lk(g_ladder_mu);
+    auto& Ld = ladder_for(dev);
+    const int mine = free_slot(Ld);
+    fa.status_out = Ld.slot[mine].host_dev;
+    fa.status_count = Ld.slot[mine].count;
+    ck(bo_qmc_finalize_v(&fa, st), "qmc_finalize");
+    prev = publish_slot(Ld, mine, st, true);
+  } else {
+    ck(bo_qmc_finalize_v(&fa, st), "qmc_finalize");
+    TORCH_CHECK(!(lean && defer_ladder && B > 0), "bo::qmc_acq_eager: posterior mode has no status");
+    prev = (defer_ladder && B > 0) ? defer_status(info, jit, st, dev)
+                                   : at::zeros({3}, at::TensorOptions().dtype(at::kDouble));
   }
-  return {acq, mean, L, Xq, Rt, Wt, jit, info, prev};
+  if (lean) return {acq, prev};
+  auto empty = [&]() { return at::empty({0}, f64); };
+  return {acq,
+          need_grad ? mean : empty(),
+          need_grad ? L : empty(),
+          need_grad ? Xq_t : empty(),
+          need_grad ? Rt : empty(),
+          empty(),
+          jit,
+          info,
+          prev};
+}
+
+std::vector<at::Tensor> qmc_acq_native(
+    const at::Tensor& X, const at::Tensor& Xt_scaled, const at::Tensor& U, const at::Tensor& Linv,
+    const at::Tensor& beta, const at::Tensor& lengthscale, const at::Tensor& Z,
+    const c10::optional<at::Tensor>& best_f_s, int64_t kind, int64_t mode, int64_t n,
+    double outputscale, double constant, double ymean, double ystd, double best_f, bool fat,
+    double tau_relu, double tau_max, bool need_grad, int64_t kxt_cap, bool defer_ladder,
+    const c10::optional<at::Tensor>& Ainv, const c10::optional<at::Tensor>& alpha) {
+  return qmc_acq_impl(X, Xt_scaled, U, Linv, beta, lengthscale, Z, best_f_s, kind, mode, n,
+                      outputscale, constant, ymean, ystd, best_f, fat, tau_relu, tau_max, need_grad,
+                      kxt_cap, defer_ladder, Ainv, alpha, false);
+}
+
+// Forward-only eager calls: [acq, previous deferred status [has, info_max, jitter_max]].
+std::vector<at::Tensor> qmc_acq_eager(
+    const at::Tensor& X, const at::Tensor& Xt_scaled, const at::Tensor& U,
+    const at::Tensor& beta, const at::Tensor& lengthscale, const at::Tensor& Z,
+    const c10::optional<at::Tensor>& best_f_s, int64_t kind, int64_t mode, int64_t n,
+    double outputscale, double constant, double ymean, double ystd, double best_f, bool fat,
+    double tau_relu, double tau_max, int64_t kxt_cap, const c10::optional<at::Tensor>& Ainv,
+    const c10::optional<at::Tensor>& alpha) {
+  return qmc_acq_impl(X, Xt_scaled, U, U, beta, lengthscale, Z, best_f_s, kind, mode, n,
+                      outputscale, constant, ymean, ystd, best_f, fat, tau_relu, tau_max, false,
+                      kxt_cap, true, Ainv, alpha, true);
 }
 
 // dX of qmc_acq_native (the registered autograd formula of bo::qmc_acq): the
@@ -397,8 +506,12 @@ TORCH_LIBRARY_FRAGMENT(bo, m) {
   m.def("qmc_acq_native(Tensor X, Tensor Xt_scaled, Tensor U, Tensor Linv, Tensor beta, "
         "Tensor lengthscale, Tensor Z, Tensor? best_f_s, int kind, int mode, int n, "
         "float outputscale, float constant, float ymean, float ystd, float best_f, bool fat, "
-        "float tau_relu, float tau_max, bool need_grad, int kxt_cap, bool defer_ladder) "
-        "-> Tensor[]");
+        "float tau_relu, float tau_max, bool need_grad, int kxt_cap, bool defer_ladder, "
+        "Tensor? Ainv=None, Tensor? alpha=None) -> Tensor[]");
+  m.def("qmc_acq_eager(Tensor X, Tensor Xt_scaled, Tensor U, Tensor beta, Tensor lengthscale, "
+        "Tensor Z, Tensor? best_f_s, int kind, int mode, int n, float outputscale, float constant, "
+        "float ymean, float ystd, float best_f, bool fat, float tau_relu, float tau_max, "
+        "int kxt_cap, Tensor? Ainv=None, Tensor? alpha=None) -> Tensor[]");
   m.def("qmc_acq_backward_native(Tensor dacq, Tensor acq, Tensor mean, Tensor L, Tensor Z, "
         "Tensor? best_f_s, Tensor Xq, Tensor Rt, Tensor Linv, Tensor U, Tensor Xt_scaled, "
         "Tensor alpha, Tensor lengthscale, int kind, int mode, int d, int n, float outputscale, "
@@ -411,6 +524,7 @@ TORCH_LIBRARY_FRAGMENT(bo, m) {
 
 TORCH_LIBRARY_IMPL(bo, CUDA, m) {
   m.impl("qmc_acq_native", &qmc_acq_native);
+  m.impl("qmc_acq_eager", &qmc_acq_eager);
   m.impl("qmc_acq_backward_native", &qmc_acq_backward_native);
   m.impl("ladder_defer", &ladder_defer);
 }

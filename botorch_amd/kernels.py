@@ -391,6 +391,29 @@ def ainv(cache: "GPCache") -> torch.Tensor:
 
 
 @functools.lru_cache(maxsize=256)
+def quad_pairs(B: int, q: int, n: int) -> int:
+    """Block pairs of the quad plan (bo_post_quad_plan) at this geometry; 0
+    where the posterior keeps the R route."""
+    npairs = ctypes.c_int()
+    check(lib().bo_post_quad_plan(B, q, n, ctypes.byref(npairs)), "post_quad_plan")
+    return npairs.value
+
+
+def quad_ainv(cache: "GPCache", B: int, q: int) -> Optional[torch.Tensor]:
+    """The full symmetric A^{-1} (np x np) of ``cache`` when the quad plan
+    applies to (B, q, n) -- built once per cache (bo_ainv + bo_sym_lower) --
+    else None."""
+    if B == 0 or quad_pairs(B, q, cache.n) == 0:
+        return None
+    A = getattr(cache, "_ainv_full", None)
+    if A is None:
+        A = ainv(cache)
+        check(lib().bo_sym_lower(_p(A), cache.np, cache.np, _stream(A.device)), "sym_lower")
+        cache._ainv_full = A
+    return A
+
+
+@functools.lru_cache(maxsize=256)
 def split_plan(B: int, q: int, n: int, slots: int = 0):
     """(kc_len, workspace doubles) of the posterior plan; kc_len = 0: one pass,
     -1: stream-K."""

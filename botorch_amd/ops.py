@@ -255,6 +255,10 @@ def _post_setup(ctx, inputs, output):
     X, Xt, Xt_scaled, U, Linv, beta, alpha, lengthscale, kind, outputscale, constant, ymean, ystd, \
         need_grad = inputs
     _, _, Xq, Rt, Wt = output
+    # the saved intermediates carry no gradient: without this autograd would
+    # zero-fill a grad for each of them (R^T and W^T: 268 MB each at C3)
+    ctx.mark_non_differentiable(Xq, Rt, Wt)
+    ctx.set_materialize_grads(False)
     ctx.save_for_backward(Xq, Rt, Wt, Xt, Xt_scaled, alpha, lengthscale)
     ctx.meta = (kind, outputscale, ystd, X.shape[0], X.shape[1])
 
@@ -264,6 +268,8 @@ def _post_bwd(ctx, dmean, dcov, *_):
     kind, outputscale, ystd, B, q = ctx.meta
     if Rt.numel() == 0:
         raise RuntimeError("bo::gp_posterior was called with need_grad=False")
+    if dmean is None and dcov is None:
+        return (None,) * 14
     if dmean is None:
         dmean = Wt.new_zeros(B, q)
     if dcov is None:
@@ -281,27 +287,29 @@ gp_posterior.register_autograd(_post_bwd, setup_context=_post_setup)
 def qmc_acq(X: Tensor, Xt: Tensor, Xt_scaled: Tensor, U: Tensor, Linv: Tensor, beta: Tensor,
             alpha: Tensor, lengthscale: Tensor, Z: Tensor, best_f_s: Optional[Tensor], kind: int,
             mode: int, outputscale: float, constant: float, ymean: float, ystd: float,
-            best_f: float, fat: bool, tau_relu: float, tau_max: float, need_grad: bool
+            best_f: float, fat: bool, tau_relu: float, tau_max: float, need_grad: bool,
+            Ainv: Optional[Tensor] = None
             ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
     """MC acquisition value (B) of B t-batches on the fused path: posterior
     partials, finalisation with the per-member jitter ladder, reparameterised
     Sobol samples and the qEI / qLogEI reduction, one launch each.  With
     need_grad also (mean, L, Xq, R^T) for the registered backward (the W^T slot
     stays empty: the backward forms W itself); the last output is the ladder
-    status tensor (info)."""
+    status tensor (info).  Ainv (forward only): the model's full A^{-1}
+    (kernels.quad_ainv) where the quad plan applies to this geometry."""
     # the whole host sequence is one native call (csrc/torch/bo_torch.cpp)
     n = Xt.shape[0]
     out = _lib.torch_ops().qmc_acq_native(
         X.contiguous(), Xt_scaled, U, Linv, beta, lengthscale, Z.reshape(-1, X.shape[1]).contiguous(),
         best_f_s, kind, mode, n, outputscale, constant, ymean, ystd, best_f, fat, tau_relu, tau_max,
-        need_grad, kernels.kxt_cap(X.device), False)
+        need_grad, kernels.kxt_cap(X.device), False, Ainv, alpha)
     acq, mean, L, Xq, Rt, Wt, jit, info, _ = out
     return acq, mean, L, Xq, Rt, Wt, jit, info
 
 
 @qmc_acq.register_fake
 def _(X, Xt, Xt_scaled, U, Linv, beta, alpha, lengthscale, Z, best_f_s, kind, mode, outputscale,
-      constant, ymean, ystd, best_f, fat, tau_relu, tau_max, need_grad):
+      constant, ymean, ystd, best_f, fat, tau_relu, tau_max, need_grad, Ainv=None):
     B, q, _ = X.shape
     mk = lambda *s: X.new_empty(*s, dtype=F64)  # noqa: E731
     info = X.new_empty(B, dtype=torch.int32)
@@ -336,8 +344,12 @@ def _(dacq, acq, mean, L, Z, best_f_s, Xq, Rt, Linv, U, Xt, Xt_scaled, alpha, le
 
 def _acq_setup(ctx, inputs, output):
     (X, Xt, Xt_scaled, U, Linv, beta, alpha, lengthscale, Z, best_f_s, kind, mode, outputscale,
-     constant, ymean, ystd, best_f, fat, tau_relu, tau_max, need_grad) = inputs
-    acq, mean, L, Xq, Rt, _, _, _ = output
+     constant, ymean, ystd, best_f, fat, tau_relu, tau_max, need_grad, *_) = inputs
+    acq, mean, L, Xq, Rt, Wt, jit, info = output
+    # only acq is differentiable; unmaterialised grads keep autograd from
+    # zero-filling R^T (268 MB at C3) on every backward
+    ctx.mark_non_differentiable(mean, L, Xq, Rt, Wt, jit, info)
+    ctx.set_materialize_grads(False)
     ctx.save_for_backward(acq, mean, L, Z, Xq, Rt, Linv, U, Xt, Xt_scaled, alpha, lengthscale)
     ctx.best_f_s = best_f_s
     ctx.meta = (kind, mode, outputscale, ystd, best_f, fat, tau_relu, tau_max)
@@ -348,10 +360,16 @@ def _acq_bwd(ctx, dacq, *_):
     if Rt.numel() == 0:
         raise RuntimeError("bo::qmc_acq was called with need_grad=False")
     kind, mode, outputscale, ystd, best_f, fat, tau_relu, tau_max = ctx.meta
+    if dacq is None:
+        return (None,) * 22
     dX = torch.ops.bo.qmc_acq_backward(dacq, acq, mean, L, Z, ctx.best_f_s, Xq, Rt, Linv, U, Xt,
                                        Xt_scaled, alpha, lengthscale, kind, mode, outputscale,
                                        ystd, best_f, fat, tau_relu, tau_max)
-    return (dX,) + (None,) * 20
+    # the forward's deferred ladder status, now that the backward is queued
+    # (waits only for the forward's event; raises NotPSDError / warns here)
+    if not torch.cuda.is_current_stream_capturing():
+        kernels.check_ladder_status(dX.device)
+    return (dX,) + (None,) * 21
 
 
 qmc_acq.register_autograd(_acq_bwd, setup_context=_acq_setup)

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 10
+#define BO_ABI_VERSION 11
 
 /* status codes */
 #define BO_OK 0
@@ -254,6 +254,12 @@ int bo_post_partials(int kind, const double* Xq, int B, int q, int d,
 int bo_post_kxt(int kind, const double* Xq, int B, int q, int d, const double* Xt_scaled,
                 int64_t n, double outputscale, double* Kt, void* stream);
 
+/* bo_prepare_rows and bo_post_kxt in one launch (ABI 11): Xq (nrows_pad x 8)
+ * and Kt from X (B x q x d) and the lengthscale directly. */
+int bo_post_kxt_rows(int kind, const double* X, int B, int q, int d, const double* lengthscale,
+                     const double* Xt_scaled, int64_t n, double outputscale, double* Xq, double* Kt,
+                     void* stream);
+
 /* W^T = L^{-T} R^T = (K*x (K + s2 I)^{-1})^T for the posterior backward, np x
  * nrows_pad, from bo_post_partials' stored R^T (np x nrows_pad) and L^{-1}
  * (lower, ld ldl): the posterior kernel's MFMA tiles over the lower k-range
@@ -303,6 +309,25 @@ int bo_post_split_work(int64_t B, int q, int64_t n, int kc_len, int64_t* work_el
  * tile column; diagonal tiles whole).  work >= bo_ainv_work doubles. */
 int bo_ainv_work(int64_t n, int64_t* work_elems);
 int bo_ainv(const double* Linv, int64_t ld, int64_t n, double* Ainv, double* work, void* stream);
+
+/* A[r][c] = A[c][r] for r < c < n: the full symmetric A^{-1} from bo_ainv's
+ * lower tiles (call with n = np so the identity pad is mirrored too). */
+int bo_sym_lower(double* A, int64_t ld, int64_t n, void* stream);
+
+/* Forward-only posterior partials of small grids through A^{-1} (the "quad"
+ * plan, csrc/quad.hip): Sigma_b = K**_b - sum_{kb <= lb} (P + P^T) over 64 x 64
+ * block pairs of the full symmetric A^{-1} = (K + s2 I)^{-1} (bo_ainv +
+ * bo_sym_lower), mu_b = c + K*x alpha -- the same [G] exact_predictive_mean /
+ * covar as bo_post_partials (models/gpytorch.py:405-466), linear in the blocks
+ * of A^{-1}, so the units' partials are 16 x 16 blocks and no split-k
+ * reduction runs.  bo_post_quad_plan: *npairs > 0 when the plan applies to
+ * (B, q, n) (stream-K geometries with n <= 2048 and <= 1024 units; BO_POST_QUAD=0/1 disables /
+ * forces it); the caller then sizes Spart as npairs x nrows_pad/16 x 16 x 16
+ * and mpart as npairs x nrows_pad and finalises with BoQmcFinalizeArgs
+ * nparts = npairs, sym_parts = 1.  Kt: bo_post_kxt's K*x^T (np x nrows_pad). */
+int bo_post_quad_plan(int64_t B, int q, int64_t n, int* npairs);
+int bo_post_quad(const double* Kt, const double* Ainv, int64_t lda, const double* alpha, int64_t B,
+                 int q, int64_t n, double* Spart, double* mpart, void* stream);
 
 /* The segment table of a split plan (host only; tests): up to cap segments as
  * 4 ints (ci | ii << 16, kbeg, kend, chunk or -1 = whole tile in place) and
@@ -505,7 +530,8 @@ int bo_sobol_box(const int64_t* state, const int64_t* shift, int dim, int64_t n,
                  int first_f32, const double* lower, const double* range, int d, double* out,
                  void* stream);
 
-/* ---- Parameter-struct entry points (ABI 9; ABI 10 adds rt_layout) -------------
+/* ---- Parameter-struct entry points (ABI 9; ABI 10 adds rt_layout, ABI 11 the
+ * quad-plan and fused-status fields of BoQmcFinalizeArgs) ------------------------
  * The widest calls above also take one struct of named fields, so a binding
  * declares a record instead of a positional list of 20-33 arguments.  Every
  * struct opens with struct_size = sizeof(struct) and abi_version =
@@ -557,6 +583,15 @@ typedef struct BoQmcFinalizeArgs { /* bo_qmc_finalize */
   const double* F;
   int64_t ldF;
   double tau_relu, tau_max;
+  /* ABI 11.  nparts: the number of partials in Spart / mpart (0: the column
+   * tiles of bo_post_geometry); sym_parts = 1: the quad plan's partials
+   * (bo_post_quad), summed as P + P^T.  status_out (2 doubles) + status_count
+   * (one int, zero before the first call): the batch's [max info, max jitter]
+   * of bo_ladder_status computed by the same launch (the last workgroup to
+   * finish reduces them and re-zeroes the counter); null: not computed. */
+  int32_t nparts, sym_parts;
+  double* status_out;
+  int32_t* status_count;
 } BoQmcFinalizeArgs;
 int bo_qmc_finalize_v(const BoQmcFinalizeArgs* a, void* stream);
 

@@ -40,7 +40,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(handle, s), s
     assert set(syms) == set(_lib.exported_symbols()), set(syms) ^ set(_lib.exported_symbols())
     lib = _lib.lib()
-    assert lib.bo_version() == _lib.ABI_VERSION == 10
+    assert lib.bo_version() == _lib.ABI_VERSION == 11
     assert lib.bo_padded_order(4096) == 4096 and lib.bo_padded_order(20) == 128
 
 
@@ -183,7 +183,7 @@ def test_native_torch_operators_load():
     import torch
     from botorch_amd import _lib
     ops = _lib.torch_ops()
-    for name in ("qmc_acq_native", "ladder_defer", "ladder_poll", "post_timing",
+    for name in ("qmc_acq_native", "qmc_acq_eager", "ladder_defer", "ladder_poll", "post_timing",
                  "post_timing_read"):
         assert hasattr(ops, name), name
     schema = str(torch.ops.bo.qmc_acq_native.default._schema)
@@ -191,3 +191,28 @@ def test_native_torch_operators_load():
     assert torch.ops.bo.ladder_poll(7).tolist() == [0.0, 0.0, 0.0]
     torch.ops.bo.post_timing(False)
     assert torch.ops.bo.post_timing_read().numel() == 0
+
+
+def test_quad_plan_geometries(monkeypatch):
+    """bo_post_quad_plan (host): the quad plan takes the stream-K geometries
+    with n <= 2048 and <= 1024 units (C2), not the C3 one-pass grid, large n
+    or many units; BO_POST_QUAD=0
+    disables and =1 forces it; the pair count is nb (nb + 1) / 2 of 64-blocks."""
+    import ctypes
+    from botorch_amd import _lib
+    lib = _lib.lib()
+
+    def pairs(B, q, n):
+        out = ctypes.c_int()
+        assert lib.bo_post_quad_plan(B, q, n, ctypes.byref(out)) == 0
+        return out.value
+
+    monkeypatch.delenv("BO_POST_QUAD", raising=False)
+    assert pairs(64, 8, 1024) == 16 * 17 // 2       # C2: 544 units
+    assert pairs(50, 3, 1500) == 24 * 25 // 2       # 600 units, ragged n
+    assert pairs(33, 16, 2048) == 0                 # 2640 units: the R route
+    assert pairs(512, 16, 4096) == 0 and pairs(64, 16, 4096) == 0 and pairs(0, 8, 1024) == 0
+    monkeypatch.setenv("BO_POST_QUAD", "0")
+    assert pairs(64, 8, 1024) == 0
+    monkeypatch.setenv("BO_POST_QUAD", "1")
+    assert pairs(512, 16, 4096) == 64 * 65 // 2

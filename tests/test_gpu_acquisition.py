@@ -538,3 +538,42 @@ def test_post_w_dx_fused_matches_w_route(n, B, q, kind):
     # below the one-pass grid the fused entry declines (the caller falls back)
     pp_s = kernels.post_partials(cache, Xc[:64], store_R=True)
     assert kernels.post_w_dx(cache, pp_s, dmean[:64], dcov[:64], 0.7) is None
+
+
+@pytest.mark.parametrize("n,B,q,S", [(1024, 64, 8, 256), (768, 100, 4, 128), (1500, 50, 3, 64)])
+def test_quad_plan_matches_r_route_and_oracle(n, B, q, S, monkeypatch):
+    """Forward-only small grids take the quad plan (64 x 64 block pairs of the
+    cached A^{-1}, csrc/quad.hip) with the ladder status fused into the
+    finalisation; its qEI equals the R route's (the same posterior through
+    L^{-T}) and the oracle's, over repeated calls (the status counter re-arms)."""
+    from botorch_amd import kernels
+    from botorch_amd.acquisition import qExpectedImprovement
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import qei
+    from oracle.sampling import draw_sobol_normal_samples
+    X, Y, m, orc = _setup(n=n, ls=0.3, noise=1e-3)
+    best = float(Y.mean())  # most random t-batches improve on it: non-zero values
+    acqf = qExpectedImprovement(m, best, sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
+    g = torch.Generator().manual_seed(1)
+    Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64)
+    Xd = Xc.to(DEV)
+    kernels.quad_pairs.cache_clear()
+    assert kernels.quad_pairs(B, q, n) > 0
+    kernels.check_ladder_status()
+    with torch.no_grad():
+        vals = [acqf(Xd) for _ in range(3)]
+    kernels.check_ladder_status()
+    assert getattr(m.prediction_cache(), "_ainv_full", None) is not None
+    for v in vals[1:]:
+        torch.testing.assert_close(v, vals[0], rtol=0, atol=0)
+    monkeypatch.setenv("BO_POST_QUAD", "0")
+    kernels.quad_pairs.cache_clear()
+    assert kernels.quad_pairs(B, q, n) == 0
+    with torch.no_grad():
+        v_r = acqf(Xd)
+    monkeypatch.delenv("BO_POST_QUAD")
+    kernels.quad_pairs.cache_clear()
+    torch.testing.assert_close(vals[0], v_r, rtol=1e-9, atol=1e-13)
+    ref = qei(orc, Xc, draw_sobol_normal_samples(q, S, 0), best)
+    torch.testing.assert_close(vals[0].cpu(), ref, rtol=1e-7, atol=1e-12)
+    assert (ref > 0).sum() >= B // 4
