@@ -189,7 +189,8 @@ class QehviArgs(_Args):
                        ("mean", _D), ("L", _D), ("Z", _D), ("cell_lo", _D), ("cell_hi", _D),
                        ("K", c_int32), ("Qp", c_int32), ("cell_stride", c_int64), ("F", _D),
                        ("ldF", c_int64), ("sF", c_int64), ("acq", _D), ("dacq", _D),
-                       ("dmean", _D), ("dL", _D), ("dF", _D)]
+                       ("dmean", _D), ("dL", _D), ("dF", _D), ("work", _D),
+                       ("work_elems", c_int64)]
 
 
 class LbfgsStepArgs(_Args):

@@ -46,6 +46,18 @@ int bo_qmc_finalize_ext(int kind, int mode, int B, int q, const double* Xq, cons
                         int64_t ldF, int fat, double tau_relu, double tau_max, int nparts,
                         int sym_parts, double* status_out, int* status_count, void* stream);
 
+// bo_qehvi with the sample-split workspace of ABI 11 (qehvi.hip)
+int bo_qehvi_ext(int B, int q, int m, const double* mean, const double* L, const double* Z, int S,
+                 const double* cell_lo, const double* cell_hi, int K, int64_t cell_stride,
+                 const double* F, int64_t ldF, int64_t sF, int Qp, double* acq, double* work,
+                 int64_t work_elems, void* stream);
+
+int bo_qehvi_backward_ext(int B, int q, int m, const double* mean, const double* L, const double* Z,
+                          int S, const double* cell_lo, const double* cell_hi, int K,
+                          int64_t cell_stride, const double* F, int64_t ldF, int64_t sF, int Qp,
+                          const double* dacq, double* dmean, double* dL, double* dF, double* work,
+                          int64_t work_elems, void* stream);
+
 int bo_post_partials_v(const BoPostPartialsArgs* a, void* stream) {
   if (!header_ok(a, "bo_post_partials_v")) return BO_ERR_ARG;
   return bo_post_partials_layout(a->kind, a->Xq, a->B, a->q, a->d, a->Xt_scaled, a->n, a->U,
@@ -80,15 +92,16 @@ int bo_post_backward_v(const BoPostBackwardArgs* a, void* stream) {
 
 int bo_qehvi_v(const BoQehviArgs* a, void* stream) {
   if (!header_ok(a, "bo_qehvi_v")) return BO_ERR_ARG;
-  return bo_qehvi(a->B, a->q, a->m, a->mean, a->L, a->Z, a->S, a->cell_lo, a->cell_hi, a->K,
-                  a->cell_stride, a->F, a->ldF, a->sF, a->Qp, a->acq, stream);
+  return bo_qehvi_ext(a->B, a->q, a->m, a->mean, a->L, a->Z, a->S, a->cell_lo, a->cell_hi, a->K,
+                      a->cell_stride, a->F, a->ldF, a->sF, a->Qp, a->acq, a->work, a->work_elems,
+                      stream);
 }
 
 int bo_qehvi_backward_v(const BoQehviArgs* a, void* stream) {
   if (!header_ok(a, "bo_qehvi_backward_v")) return BO_ERR_ARG;
-  return bo_qehvi_backward(a->B, a->q, a->m, a->mean, a->L, a->Z, a->S, a->cell_lo, a->cell_hi,
-                           a->K, a->cell_stride, a->F, a->ldF, a->sF, a->Qp, a->dacq, a->dmean,
-                           a->dL, a->dF, stream);
+  return bo_qehvi_backward_ext(a->B, a->q, a->m, a->mean, a->L, a->Z, a->S, a->cell_lo,
+                               a->cell_hi, a->K, a->cell_stride, a->F, a->ldF, a->sF, a->Qp,
+                               a->dacq, a->dmean, a->dL, a->dF, a->work, a->work_elems, stream);
 }
 
 int bo_lbfgs_step_v(const BoLbfgsStepArgs* a, void* stream) {

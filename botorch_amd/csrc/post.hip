@@ -744,6 +744,18 @@ struct SplitPlan {
   int64_t max_steps = 0;  // k-steps of the busiest workgroup
 };
 
+// Fewest k-steps per stream-K segment (BO_SK_MIN_SHARE, default 4; read once).
+// Every cut segment costs a 128 KB partial R^T tile written and read back by
+// the reduction, so tiny grids trade parallelism against that traffic.
+static int sk_min_share() {
+  static const int v = [] {
+    const char* e = std::getenv("BO_SK_MIN_SHARE");
+    const int x = e ? std::atoi(e) : 4;
+    return x >= 1 ? x : 4;
+  }();
+  return v;
+}
+
 // kc_len > 0: uniform chunks of kc_len; kc_len < 0: stream-K over `slots`.
 // mode PLAN_POST: posterior tiles, k-range [0, min(n, 128 ci + 128));
 // PLAN_AINV: the tiles of A^{-1} = L^{-T} L^{-1} (bo_ainv), column tiles ci >=
@@ -803,8 +815,8 @@ SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, int mod
     // those slices are fetched into its L2 once.
     int64_t lane_total = 0;
     for (int ci = 0; ci < nC; ++ci) lane_total += ceil_div(kend_of(ci) - kbeg_of(ci), PK);
-    const int64_t per_lane =
-        std::max<int64_t>(1, std::min<int64_t>(std::max(1, slots / nI), lane_total / 4));
+    const int64_t per_lane = std::max<int64_t>(
+        1, std::min<int64_t>(std::max(1, slots / nI), lane_total / sk_min_share()));
     const int64_t share = ceil_div(lane_total, per_lane);
     const int64_t jn = ceil_div(lane_total, share);  // workgroups used per lane
     wg.resize((size_t)(ceil_div(jn, 8) * 8 * nI));
@@ -1021,6 +1033,17 @@ int bo_post_kxt(int kind, const double* Xq, int B, int q, int d, const double* X
   return BO_OK;
 }
 
+// Points per thread of the small-grid K*x^T build: BO_KXT_SMALL (1, 2, 4 or
+// 8; default 2), read once -- an A/B knob for tools/time_kxt.py.
+static int kxt_small_k() {
+  static const int k = [] {
+    const char* e = std::getenv("BO_KXT_SMALL");
+    const int v = e ? std::atoi(e) : 2;
+    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 2;
+  }();
+  return k;
+}
+
 // bo_prepare_rows + bo_post_kxt in one launch: Xq and K*x^T from X itself.
 int bo_post_kxt_rows(int kind, const double* X, int B, int q, int d, const double* lengthscale,
                      const double* Xt_scaled, int64_t n, double outputscale, double* Xq, double* Kt,
@@ -1037,14 +1060,19 @@ int bo_post_kxt_rows(int kind, const double* X, int B, int q, int d, const doubl
   hipStream_t st = as_stream(stream);
   const RowsFromX rx{X, lengthscale, B, q, d, Qp, Xq};
   const bool small = ceil_div(nrows_pad, 256) * ceil_div(np, KXT_K) < 1024;
-  const dim3 grid((unsigned)ceil_div(nrows_pad, 256), (unsigned)ceil_div(np, small ? 2 : KXT_K));
-#define BO_KXTR(KIND, ND)                                                                      \
-  if (small)                                                                                   \
-    kxt_build_kernel<KIND, ND, 2, true><<<grid, 256, 0, st>>>(nullptr, nrows, Xt_scaled, (int)n, \
-                                                              np, nrows_pad, outputscale, Kt, rx); \
-  else                                                                                         \
-    kxt_build_kernel<KIND, ND, KXT_K, true><<<grid, 256, 0, st>>>(                              \
-        nullptr, nrows, Xt_scaled, (int)n, np, nrows_pad, outputscale, Kt, rx)
+  const int kk = small ? kxt_small_k() : KXT_K;
+  const dim3 grid((unsigned)ceil_div(nrows_pad, 256), (unsigned)ceil_div(np, kk));
+#define BO_KXTR_K(KIND, ND, K)                                                                 \
+  kxt_build_kernel<KIND, ND, K, true><<<grid, 256, 0, st>>>(nullptr, nrows, Xt_scaled, (int)n,  \
+                                                            np, nrows_pad, outputscale, Kt, rx)
+#define BO_KXTR(KIND, ND)                  \
+  switch (kk) {                            \
+    case 1: BO_KXTR_K(KIND, ND, 1); break; \
+    case 2: BO_KXTR_K(KIND, ND, 2); break; \
+    case 4: BO_KXTR_K(KIND, ND, 4); break; \
+    case 8: BO_KXTR_K(KIND, ND, 8); break; \
+    default: BO_KXTR_K(KIND, ND, KXT_K); break; \
+  }
 #define BO_KXTR_D(KIND)                      \
   switch (d) {                               \
     case 1: BO_KXTR(KIND, 1); break;         \
@@ -1062,6 +1090,7 @@ int bo_post_kxt_rows(int kind, const double* X, int B, int q, int d, const doubl
   }
 #undef BO_KXTR_D
 #undef BO_KXTR
+#undef BO_KXTR_K
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

@@ -22,6 +22,8 @@
 // kernel issued one VALU instruction per ~25 cycles per wave, PMC r03).
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int THREADS = 256;   // mc_reduce_kernel
@@ -64,11 +66,18 @@ template <int M, int NT = FWD_THREADS, bool CELLS_LDS = false>
 __global__ __launch_bounds__(NT) void qehvi_kernel(
     int B, int q, const double* __restrict__ mean, const double* __restrict__ L,
     const double* __restrict__ Z, int S, const double* __restrict__ lo,
-    const double* __restrict__ hi, int K, QehviExt ex, double* __restrict__ acq) {
+    const double* __restrict__ hi, int K, QehviExt ex, double* __restrict__ acq, int H = 1,
+    double* __restrict__ part = nullptr) {
+  // H > 1: the t-batch's samples are split over H workgroups (C4's 128
+  // t-batches would leave half the CUs idle); workgroup h sums the samples
+  // [h S / H, (h + 1) S / H) into part[b H + h], qehvi_part_reduce_kernel
+  // adds the H partials in order
   __shared__ double f[LDS_SAMPLES_DOUBLES];
   __shared__ double red[NT / 64];
   __shared__ double cells[CELLS_LDS ? LDS_CELL_DOUBLES : 1];
-  const int b = blockIdx.x;
+  const int b = blockIdx.x / H;
+  const int h = blockIdx.x - b * H;
+  const int sbeg = (int)((int64_t)S * h / H), send = (int)((int64_t)S * (h + 1) / H);
   const int tid = threadIdx.x;
   const int per_sample = q * M;
   const int chunk = LDS_SAMPLES_DOUBLES / per_sample;
@@ -79,8 +88,8 @@ __global__ __launch_bounds__(NT) void qehvi_kernel(
     }
   }
   double sum = 0.0;
-  for (int s0 = 0; s0 < S; s0 += chunk) {
-    const int ns = min(chunk, S - s0);
+  for (int s0 = sbeg; s0 < send; s0 += chunk) {
+    const int ns = min(chunk, send - s0);
     __syncthreads();
     for (int e = tid; e < ns * per_sample; e += NT) {
       const int s = e / per_sample;
@@ -140,8 +149,18 @@ __global__ __launch_bounds__(NT) void qehvi_kernel(
   if (tid == 0) {
     double t = 0.0;
     for (int w = 0; w < NT / 64; ++w) t += red[w];
-    acq[b] = t / S;
+    if (H == 1) acq[b] = t / S;
+    else part[blockIdx.x] = t;
   }
+}
+
+__global__ __launch_bounds__(64) void qehvi_part_reduce_kernel(const double* __restrict__ part, int B,
+                                                               int H, int S, double* __restrict__ acq) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= B) return;
+  double t = 0.0;
+  for (int h = 0; h < H; ++h) t += part[(int64_t)b * H + h];
+  acq[b] = t / S;
 }
 
 // Backward of qehvi_kernel (gen_candidates_scipy's autograd.grad through
@@ -157,11 +176,17 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
     int B, int q, const double* __restrict__ mean, const double* __restrict__ L,
     const double* __restrict__ Z, int S, const double* __restrict__ lo,
     const double* __restrict__ hi, int K, QehviExt ex, const double* __restrict__ dacq,
-    double* __restrict__ dmean, double* __restrict__ dL, double* __restrict__ dF) {
+    double* __restrict__ dmean, double* __restrict__ dL, double* __restrict__ dF, int H = 1,
+    double* __restrict__ part = nullptr) {
+  // H > 1: samples split over H workgroups as in qehvi_kernel; workgroup h
+  // writes its (dmean, dL) entries to part[(b H + h) nent + .] (dF rows are
+  // per sample: written directly), qehvi_backward_reduce_kernel sums them
   constexpr int CH = LDS_SAMPLES_DOUBLES / 2;
   __shared__ double f[CH];
   __shared__ double df[CH];
-  const int b = blockIdx.x;
+  const int b = blockIdx.x / H;
+  const int h = blockIdx.x - b * H;
+  const int sbeg = (int)((int64_t)S * h / H), send = (int)((int64_t)S * (h + 1) / H);
   const int tid = threadIdx.x;
   const int per_sample = q * M;
   const int chunk = CH / per_sample;
@@ -169,8 +194,8 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
   // entries owned by this thread: (t, p, j) with j <= p (j == p + 1 -> dmean)
   const int nent = M * q * (q + 3) / 2;
   double accv[2] = {0.0, 0.0};
-  for (int s0 = 0; s0 < S; s0 += chunk) {
-    const int ns = min(chunk, S - s0);
+  for (int s0 = sbeg; s0 < send; s0 += chunk) {
+    const int ns = min(chunk, send - s0);
     __syncthreads();
     for (int e = tid; e < ns * per_sample; e += NT) {
       const int s = e / per_sample;
@@ -278,6 +303,13 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
       accv[w] += acc;
     }
   }
+  if (H > 1) {
+    for (int w = 0; w < 2; ++w) {
+      const int ent = tid + w * NT;
+      if (ent < nent) part[(int64_t)blockIdx.x * nent + ent] = g * accv[w];
+    }
+    return;
+  }
   for (int w = 0; w < 2; ++w) {
     const int ent = tid + w * NT;
     if (ent >= nent) continue;
@@ -300,6 +332,34 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
   }
   // strict upper triangle of dL
   for (int e = tid; e < M * q * q; e += NT) {
+    const int t = e / (q * q), p = (e / q) % q, j = e % q;
+    if (j > p) dL[(((int64_t)t * B + b) * q + p) * q + j] = 0.0;
+  }
+}
+
+// Sum of the H sample-split partials of qehvi_backward_kernel (in order), then
+// its output layout: dL lower triangle + dmean, strict upper triangle zero.
+__global__ __launch_bounds__(256) void qehvi_backward_reduce_kernel(const double* __restrict__ part,
+                                                                    int B, int q, int M, int H,
+                                                                    double* __restrict__ dmean,
+                                                                    double* __restrict__ dL) {
+  const int b = blockIdx.x;
+  const int nent = M * q * (q + 3) / 2;
+  const int per_t = q * (q + 3) / 2;
+  for (int ent = threadIdx.x; ent < nent; ent += 256) {
+    double v = 0.0;
+    for (int h = 0; h < H; ++h) v += part[((int64_t)b * H + h) * nent + ent];
+    const int t = ent / per_t;
+    int r = ent % per_t;
+    int p = 0;
+    while (r >= p + 2) {
+      r -= p + 2;
+      ++p;
+    }
+    if (r <= p) dL[(((int64_t)t * B + b) * q + p) * q + r] = v;
+    else dmean[((int64_t)t * B + b) * q + p] = v;
+  }
+  for (int e = threadIdx.x; e < M * q * q; e += 256) {
     const int t = e / (q * q), p = (e / q) % q, j = e % q;
     if (j > p) dL[(((int64_t)t * B + b) * q + p) * q + j] = 0.0;
   }
@@ -334,10 +394,25 @@ __global__ __launch_bounds__(THREADS) void mc_reduce_kernel(
 
 }  // namespace
 
+extern "C" int bo_qehvi_ext(int B, int q, int m, const double* mean, const double* L,
+                            const double* Z, int S, const double* cell_lo, const double* cell_hi,
+                            int K, int64_t cell_stride, const double* F, int64_t ldF, int64_t sF,
+                            int Qp, double* acq, double* work, int64_t work_elems, void* stream);
+
 extern "C" int bo_qehvi(int B, int q, int m, const double* mean, const double* L, const double* Z,
                         int S, const double* cell_lo, const double* cell_hi, int K,
                         int64_t cell_stride, const double* F, int64_t ldF, int64_t sF, int Qp,
                         double* acq, void* stream) {
+  return bo_qehvi_ext(B, q, m, mean, L, Z, S, cell_lo, cell_hi, K, cell_stride, F, ldF, sF, Qp, acq,
+                      nullptr, 0, stream);
+}
+
+// work (>= 2 B doubles, optional): the samples of each t-batch split over H =
+// min(8, 256 / B, work_elems / B) workgroups when B leaves CUs idle.
+extern "C" int bo_qehvi_ext(int B, int q, int m, const double* mean, const double* L,
+                            const double* Z, int S, const double* cell_lo, const double* cell_hi,
+                            int K, int64_t cell_stride, const double* F, int64_t ldF, int64_t sF,
+                            int Qp, double* acq, double* work, int64_t work_elems, void* stream) {
   BO_CHECK_ARG(q >= 1 && q <= QMAX, "bo_qehvi: 1 <= q <= %d (got %d)", QMAX, q);
   BO_CHECK_ARG(m >= 2 && m <= MMAX, "bo_qehvi: 2 <= m <= %d (got %d)", MMAX, m);
   BO_CHECK_ARG(S > 0 && K >= 0 && cell_stride >= 0, "bo_qehvi: bad S/K/cell_stride");
@@ -346,12 +421,19 @@ extern "C" int bo_qehvi(int B, int q, int m, const double* mean, const double* L
   hipStream_t st = as_stream(stream);
   const QehviExt ex{cell_stride, F, ldF, sF, Qp};
   const bool cl = cell_stride == 0 && (int64_t)K * m <= LDS_CELL_DOUBLES / 2;
+  int H = 1;
+  if (work != nullptr && work_elems >= 2 * (int64_t)B) {
+    H = (int)std::min<int64_t>(std::min(8, std::max(1, 256 / B)), work_elems / B);
+    H = std::max(1, std::min(H, S));
+  }
+  const unsigned grid = (unsigned)((int64_t)B * H);
 #define BO_QF(MM)                                                                              \
   if (cl)                                                                                      \
-    qehvi_kernel<MM, FWD_THREADS, true><<<B, FWD_THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, \
-                                                                    cell_hi, K, ex, acq);      \
+    qehvi_kernel<MM, FWD_THREADS, true><<<grid, FWD_THREADS, 0, st>>>(                         \
+        B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, acq, H, work);                           \
   else                                                                                         \
-    qehvi_kernel<MM><<<B, FWD_THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, acq)
+    qehvi_kernel<MM><<<grid, FWD_THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, \
+                                                   acq, H, work)
   if (m == 2) {
     BO_QF(2);
   } else if (m == 3) {
@@ -361,8 +443,19 @@ extern "C" int bo_qehvi(int B, int q, int m, const double* mean, const double* L
   }
 #undef BO_QF
   BO_LAUNCH_CHECK();
+  if (H > 1) {
+    qehvi_part_reduce_kernel<<<(unsigned)ceil_div(B, 64), 64, 0, st>>>(work, B, H, S, acq);
+    BO_LAUNCH_CHECK();
+  }
   return BO_OK;
 }
+
+extern "C" int bo_qehvi_backward_ext(int B, int q, int m, const double* mean, const double* L,
+                                     const double* Z, int S, const double* cell_lo,
+                                     const double* cell_hi, int K, int64_t cell_stride,
+                                     const double* F, int64_t ldF, int64_t sF, int Qp,
+                                     const double* dacq, double* dmean, double* dL, double* dF,
+                                     double* work, int64_t work_elems, void* stream);
 
 extern "C" int bo_qehvi_backward(int B, int q, int m, const double* mean, const double* L,
                                  const double* Z, int S, const double* cell_lo,
@@ -370,6 +463,18 @@ extern "C" int bo_qehvi_backward(int B, int q, int m, const double* mean, const 
                                  const double* F, int64_t ldF, int64_t sF, int Qp,
                                  const double* dacq, double* dmean, double* dL, double* dF,
                                  void* stream) {
+  return bo_qehvi_backward_ext(B, q, m, mean, L, Z, S, cell_lo, cell_hi, K, cell_stride, F, ldF, sF,
+                               Qp, dacq, dmean, dL, dF, nullptr, 0, stream);
+}
+
+// work (>= 2 B nent doubles, nent = m q (q + 3) / 2, optional): the sample
+// split of bo_qehvi_ext for the backward.
+extern "C" int bo_qehvi_backward_ext(int B, int q, int m, const double* mean, const double* L,
+                                 const double* Z, int S, const double* cell_lo,
+                                 const double* cell_hi, int K, int64_t cell_stride,
+                                 const double* F, int64_t ldF, int64_t sF, int Qp,
+                                 const double* dacq, double* dmean, double* dL, double* dF,
+                                 double* work, int64_t work_elems, void* stream) {
   BO_CHECK_ARG(q >= 1 && q <= QMAX, "bo_qehvi_backward: 1 <= q <= %d (got %d)", QMAX, q);
   BO_CHECK_ARG(m >= 2 && m <= MMAX, "bo_qehvi_backward: 2 <= m <= %d (got %d)", MMAX, m);
   BO_CHECK_ARG(S > 0 && K >= 0 && cell_stride >= 0, "bo_qehvi_backward: bad S/K/cell_stride");
@@ -378,12 +483,23 @@ extern "C" int bo_qehvi_backward(int B, int q, int m, const double* mean, const 
   if (B == 0) return BO_OK;
   hipStream_t st = as_stream(stream);
   const QehviExt ex{cell_stride, F, ldF, sF, Qp};
-#define BO_QB(MM, NT) qehvi_backward_kernel<MM, NT><<<B, NT, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, dacq, dmean, dL, dF)
+  const int64_t nent = (int64_t)m * q * (q + 3) / 2;
+  int H = 1;
+  if (work != nullptr && work_elems >= 2 * (int64_t)B * nent) {
+    H = (int)std::min<int64_t>(std::min(8, std::max(1, 256 / B)), work_elems / ((int64_t)B * nent));
+    H = std::max(1, std::min(H, S));
+  }
+  const unsigned grid = (unsigned)((int64_t)B * H);
+#define BO_QB(MM, NT) qehvi_backward_kernel<MM, NT><<<grid, NT, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, dacq, dmean, dL, dF, H, work)
   if (m == 2) BO_QB(2, BWD_THREADS);
   else if (m == 3) BO_QB(3, BWD_THREADS);
   else BO_QB(4, 256);  // m = 4 needs 256 VGPRs: 4 waves per workgroup
 #undef BO_QB
   BO_LAUNCH_CHECK();
+  if (H > 1) {
+    qehvi_backward_reduce_kernel<<<(unsigned)B, 256, 0, st>>>(work, B, q, m, H, dmean, dL);
+    BO_LAUNCH_CHECK();
+  }
   return BO_OK;
 }
 

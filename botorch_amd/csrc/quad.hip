@@ -33,121 +33,171 @@ constexpr int QB = 64;    // A^{-1} block edge (k and l)
 constexpr int QI = 128;   // test rows per unit (4 waves x 32)
 constexpr int QLD = 68;   // LDS pitch of the A^{-1} block (doubles)
 
-// Unit u -> (pair, row tile); pairs (kb, lb), kb <= lb, row-major over the
-// block upper triangle.  Consecutive units share a pair (and its A^{-1}
-// block): the grid deals them XCD by XCD (block b runs on XCD b % 8), so the
-// row tiles of one pair meet in one L2.
+// Unit u -> (chunk, row tile).  The block pairs (kb, lb), kb <= lb, of one
+// block row kb are cut into chunks of G consecutive lb; a chunk's pairs share
+// the k-loop's K*x^T operands (loaded once) and ONE partial (their P's summed
+// in registers), so the finalisation reads sum_kb ceil((nb - kb) / G)
+// partials per row tile instead of nb (nb + 1) / 2.  Inside a chunk the next
+// pair's A^{-1} block is fetched into registers under the current pair's
+// MFMAs and parked in the other LDS buffer.  Consecutive units share a chunk:
+// the grid deals them XCD by XCD (block b runs on XCD b % 8), so the row
+// tiles of one chunk meet in one L2.
 __global__ __launch_bounds__(256, 2) void post_quad_kernel(
     const double* __restrict__ Kt, int nrows_pad, const double* __restrict__ Ainv, int64_t lda,
-    const double* __restrict__ alpha, int n, int nb, int nI, int units,
+    const double* __restrict__ alpha, int n, int nb, int G, int nI, int units,
     double* __restrict__ Spart, double* __restrict__ mpart) {
-  __shared__ __attribute__((aligned(16))) double As[QB][QLD];
+  __shared__ __attribute__((aligned(16))) double As[2][QB][QLD];
   const int bid = blockIdx.x;
   const int per_xcd = gridDim.x >> 3;  // the grid is a multiple of 8
   const int u = (bid & 7) * per_xcd + (bid >> 3);
   if (u >= units) return;  // whole workgroup: no barrier below is skipped by part of it
-  const int pair = u / nI;
-  const int ii = u - pair * nI;
-  int kb = 0, rem = pair;
-  while (rem >= nb - kb) {
-    rem -= nb - kb;
+  const int chunk = u / nI;
+  const int ii = u - chunk * nI;
+  int kb = 0, rem = chunk;
+  for (;;) {
+    const int nc = (nb - kb + G - 1) / G;
+    if (rem < nc) break;
+    rem -= nc;
     ++kb;
   }
-  const int lb = kb + rem;
-  const int k0 = kb * QB, l0 = lb * QB, i0 = ii * QI;
+  const int lb_begin = kb + rem * G;
+  const int lb_end = min(nb, lb_begin + G);
+  const int k0 = kb * QB, i0 = ii * QI;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-  // the A^{-1} block (64 x 64) into LDS, 16-B loads
+  // A^{-1} block (kb, lb): 64 x 64, 8 x 16 B per thread
+  auto load_a = [&](int lb, double2 (&v)[(QB * QB / 2) / 256]) {
 #pragma unroll
-  for (int j = 0; j < (QB * QB / 2) / 256; ++j) {
-    const int e = tid + 256 * j;
-    const int r = e >> 5, c2 = (e & 31) * 2;
-    const double2 v = *reinterpret_cast<const double2*>(Ainv + (int64_t)(k0 + r) * lda + l0 + c2);
-    *reinterpret_cast<double2*>(&As[r][c2]) = v;
-  }
+    for (int j = 0; j < (QB * QB / 2) / 256; ++j) {
+      const int e = tid + 256 * j;
+      v[j] = *reinterpret_cast<const double2*>(Ainv + (int64_t)(k0 + (e >> 5)) * lda + lb * QB +
+                                               (e & 31) * 2);
+    }
+  };
+  auto park_a = [&](int buf, const double2 (&v)[(QB * QB / 2) / 256]) {
+#pragma unroll
+    for (int j = 0; j < (QB * QB / 2) / 256; ++j) {
+      const int e = tid + 256 * j;
+      *reinterpret_cast<double2*>(&As[buf][e >> 5][(e & 31) * 2]) = v[j];
+    }
+  };
+  double2 av[(QB * QB / 2) / 256];
+  load_a(lb_begin, av);
   // MFMA B operands of the k-loop (K*x^T rows k0 + 4 ks + (lane >> 4), 16
-  // consecutive test rows per 16 lanes) and of the epilogue (rows l0 + 16 ct
-  // + 4 r + (lane >> 4)): all issued before the first MFMA, one latency.
+  // consecutive test rows per 16 lanes): loaded once for the chunk
   const double* kt = Kt + i0 + wave * 32 + (lane & 15) + (int64_t)(lane >> 4) * nrows_pad;
   double b[QB / 4][2];
 #pragma unroll
   for (int ks = 0; ks < QB / 4; ++ks)
 #pragma unroll
     for (int it = 0; it < 2; ++it) b[ks][it] = kt[(int64_t)(k0 + 4 * ks) * nrows_pad + 16 * it];
-  double e[QB / 16][4][2];
-#pragma unroll
-  for (int ct = 0; ct < QB / 16; ++ct)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int it = 0; it < 2; ++it)
-        e[ct][r][it] = kt[(int64_t)(l0 + 16 * ct + 4 * r) * nrows_pad + 16 * it];
+  park_a(0, av);
   __syncthreads();
 
-  // T^T[l][i] = sum_{k in kb} A^{-1}[k][l] K*x[i][k]: lane l, register r of
-  // acc[ct][it] holds l = l0 + 16 ct + (lane >> 4) + 4 r, i = row16 + (lane & 15)
-  v4d acc[QB / 16][2];
-#pragma unroll
-  for (int ct = 0; ct < QB / 16; ++ct) {
-    acc[ct][0] = v4d_zero();
-    acc[ct][1] = v4d_zero();
-  }
-#pragma unroll
-  for (int ks = 0; ks < QB / 4; ++ks) {
-    double a[QB / 16];
-#pragma unroll
-    for (int ct = 0; ct < QB / 16; ++ct) a[ct] = As[4 * ks + (lane >> 4)][16 * ct + (lane & 15)];
+  // the chunk's P, one accumulator chain per 16-row tile (the two chains
+  // interleave)
+  v4d Pc[2] = {v4d_zero(), v4d_zero()};
+  double m[2] = {0.0, 0.0};
+  for (int lb = lb_begin; lb < lb_end; ++lb) {
+    const int cur = (lb - lb_begin) & 1;
+    const int l0 = lb * QB;
+    // epilogue operands (K*x^T rows l0 + 16 ct + 4 r + (lane >> 4)) and the
+    // next pair's A^{-1} block: in flight under this pair's k-loop
+    double e[QB / 16][4][2];
 #pragma unroll
     for (int ct = 0; ct < QB / 16; ++ct)
 #pragma unroll
-      for (int it = 0; it < 2; ++it) acc[ct][it] = mfma_f64(a[ct], b[ks][it], acc[ct][it]);
-  }
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+          e[ct][r][it] = kt[(int64_t)(l0 + 16 * ct + 4 * r) * nrows_pad + 16 * it];
+    const bool more = lb + 1 < lb_end;
+    if (more) load_a(lb + 1, av);
 
-  // P[i][j] = sum_{l in lb} T[i][l] K*x[j][l]: the accumulator register is the
-  // A operand as it stands (k index = (lane >> 4) + 4 r), K*x^T the B operand.
-  // Four independent accumulator chains (two per 16-row tile) instead of one
-  // 16-deep dependent chain per tile: the epilogue is a fifth of this short
-  // unit's MFMAs, and back-to-back dependent fp64 MFMAs wait out the full
-  // pass latency.
-  const bool diag = kb == lb;
-  const int nrows16 = nrows_pad >> 4;
-  v4d Pc[2][2];
+    // T^T[l][i] = sum_{k in kb} A^{-1}[k][l] K*x[i][k]: lane l, register r of
+    // acc[ct][it] holds l = l0 + 16 ct + (lane >> 4) + 4 r, i = row16 + (lane & 15)
+    v4d acc[QB / 16][2];
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    Pc[it][0] = v4d_zero();
-    Pc[it][1] = v4d_zero();
-  }
+    for (int ct = 0; ct < QB / 16; ++ct) {
+      acc[ct][0] = v4d_zero();
+      acc[ct][1] = v4d_zero();
+    }
 #pragma unroll
-  for (int ct = 0; ct < QB / 16; ++ct)
+    for (int ks = 0; ks < QB / 4; ++ks) {
+      double a[QB / 16];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int it = 0; it < 2; ++it)
-        Pc[it][ct & 1] = mfma_f64(acc[ct][it][r], e[ct][r][it], Pc[it][ct & 1]);
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const v4d P = Pc[it][0] + Pc[it][1];
-    const int row16 = i0 + wave * 32 + it * 16;
-    double* sp = Spart + ((int64_t)pair * nrows16 + (row16 >> 4)) * 256;
-    const double h = diag ? 0.5 : 1.0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sp[mfma_row(lane, r) * 16 + mfma_col(lane)] = h * P[r];
-    // mean partial K*x[j, lb] alpha[lb] from the same operands (diagonal pairs
-    // own their block's share; the others write zeros)
-    double m = 0.0;
-    if (diag) {
+      for (int ct = 0; ct < QB / 16; ++ct)
+        a[ct] = As[cur][4 * ks + (lane >> 4)][16 * ct + (lane & 15)];
 #pragma unroll
       for (int ct = 0; ct < QB / 16; ++ct)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int l = l0 + 16 * ct + 4 * r + (lane >> 4);
-          m = fma(e[ct][r][it], l < n ? alpha[l] : 0.0, m);
-        }
-      m += __shfl_xor(m, 16);
-      m += __shfl_xor(m, 32);
+        for (int it = 0; it < 2; ++it) acc[ct][it] = mfma_f64(a[ct], b[ks][it], acc[ct][it]);
     }
-    if (lane < 16) mpart[(int64_t)pair * nrows_pad + row16 + lane] = m;
+    // the diagonal pair stands for itself only: P / 2 (summed as P + P^T),
+    // applied to T (exact: a power of two)
+    if (lb == kb) {
+#pragma unroll
+      for (int ct = 0; ct < QB / 16; ++ct) {
+        acc[ct][0] *= 0.5;
+        acc[ct][1] *= 0.5;
+      }
+    }
+    // P[i][j] += sum_{l in lb} T[i][l] K*x[j][l]: the accumulator register is
+    // the A operand as it stands (k index = (lane >> 4) + 4 r), K*x^T the B
+#pragma unroll
+    for (int ct = 0; ct < QB / 16; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+          Pc[it] = mfma_f64(acc[ct][it][r], e[ct][r][it], Pc[it]);
+    // mean K*x[j, kb] alpha[kb] from the diagonal pair's operands
+    if (lb == kb) {
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+#pragma unroll
+        for (int ct = 0; ct < QB / 16; ++ct)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int l = l0 + 16 * ct + 4 * r + (lane >> 4);
+            m[it] = fma(e[ct][r][it], l < n ? alpha[l] : 0.0, m[it]);
+          }
+    }
+    if (more) park_a(cur ^ 1, av);
+    __syncthreads();
   }
+
+  const int nrows16 = nrows_pad >> 4;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const v4d P = Pc[it];
+    const int row16 = i0 + wave * 32 + it * 16;
+    double* sp = Spart + ((int64_t)chunk * nrows16 + (row16 >> 4)) * 256;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sp[mfma_row(lane, r) * 16 + mfma_col(lane)] = P[r];
+    double mm = m[it];
+    mm += __shfl_xor(mm, 16);
+    mm += __shfl_xor(mm, 32);
+    if (lane < 16) mpart[(int64_t)chunk * nrows_pad + row16 + lane] = mm;
+  }
+}
+
+// Partials per row tile of the quad plan: sum_kb ceil((nb - kb) / G).
+int quad_chunks(int nb, int G) {
+  int c = 0;
+  for (int kb = 0; kb < nb; ++kb) c += (nb - kb + G - 1) / G;
+  return c;
+}
+
+// Pairs per chunk: BO_QUAD_G (1..16) or 1 (chunks of 4 measured slower at C2:
+// 35 vs 26-31 us for the posterior, the finalisation 17 vs 21 us).
+int quad_group() {
+  static const int g = [] {
+    const char* e = std::getenv("BO_QUAD_G");
+    const int v = e ? std::atoi(e) : 0;
+    return (v >= 1 && v <= 16) ? v : 1;
+  }();
+  return g;
 }
 
 // A[r][c] = A[c][r] for r < c (the upper triangle from the lower), 32 x 32
@@ -176,18 +226,23 @@ extern "C" {
 int bo_post_geometry(int64_t B, int q, int64_t n, int* Qp, int* nrows_pad, int* nC);
 int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len, int64_t* work_elems);
 
-// The quad plan applies to forward-only calls whose one-pass grid would be
-// split (bo_post_split_plan: stream-K) with n <= 2048 and at most ~1000
-// units.  Environment BO_POST_QUAD=0 disables it, =1 forces it wherever the
-// geometry allows (A/B timing).
+// The quad plan (opt-in, BO_POST_QUAD=auto) applies to forward-only calls
+// whose one-pass grid would be split (bo_post_split_plan: stream-K) with
+// n <= 2048 and at most ~1000 pair units; =1 forces it wherever the geometry
+// allows, =0 / unset keeps the R route.
 int bo_post_quad_plan(int64_t B, int q, int64_t n, int* npairs) {
   int Qp, nrows_pad, nC;
   int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
   if (s) return s;
   *npairs = 0;
   if (nrows_pad == 0 || n <= 0) return BO_OK;
+  // Opt-in (BO_POST_QUAD=1 or =auto): measured at C2 the quad posterior takes
+  // 26-31 us against 25 + 13 us for the R route's stream-K pass and split-k
+  // reduction, but its 136 partials (40 in chunks of 4) cost the
+  // finalisation 10-14 us more than the R route's 8, so the eager call is no
+  // faster (0.064-0.066 ms both, profiles/r03/c2/).  Default: the R route.
   const char* env = std::getenv("BO_POST_QUAD");
-  const int force = env ? (env[0] == '0' ? 0 : (env[0] == '1' ? 1 : -1)) : -1;
+  const int force = env ? (env[0] == '0' ? 0 : (env[0] == '1' ? 1 : -1)) : 0;
   if (force == 0) return BO_OK;
   const int nb = (int)ceil_div(n, QB);
   bool use = force == 1;
@@ -202,9 +257,9 @@ int bo_post_quad_plan(int64_t B, int q, int64_t n, int* npairs) {
     // ~1000 units (C2: 544 units, 30 vs 41 us; n = 1024, b = 256: 2176 units,
     // 74 vs 67 us)
     const int64_t units = (int64_t)nb * (nb + 1) / 2 * (nrows_pad / QI);
-    use = kc != 0 && n <= 2048 && units <= 1024;
+    use = kc != 0 && n <= 2048 && units <= 1024;  // counted in pairs
   }
-  if (use) *npairs = nb * (nb + 1) / 2;
+  if (use) *npairs = quad_chunks(nb, quad_group());
   return BO_OK;
 }
 
@@ -220,12 +275,13 @@ int bo_post_quad(const double* Kt, const double* Ainv, int64_t lda, const double
                nC * 128);
   const int nb = (int)ceil_div(n, QB);
   const int nI = nrows_pad / QI;
-  const int64_t units = (int64_t)nb * (nb + 1) / 2 * nI;
+  const int G = quad_group();
+  const int64_t units = (int64_t)quad_chunks(nb, G) * nI;
   BO_CHECK_ARG(units < (1LL << 30), "bo_post_quad: %lld units", (long long)units);
   const int64_t grid = ceil_div(units, 8) * 8;
   // Kt (np x nrows_pad) has rows up to nC * 128 >= nb * 64: every block row read exists
   post_quad_kernel<<<(unsigned)grid, 256, 0, as_stream(stream)>>>(
-      Kt, nrows_pad, Ainv, lda, alpha, (int)n, nb, nI, (int)units, Spart, mpart);
+      Kt, nrows_pad, Ainv, lda, alpha, (int)n, nb, G, nI, (int)units, Spart, mpart);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

@@ -392,8 +392,8 @@ def ainv(cache: "GPCache") -> torch.Tensor:
 
 @functools.lru_cache(maxsize=256)
 def quad_pairs(B: int, q: int, n: int) -> int:
-    """Block pairs of the quad plan (bo_post_quad_plan) at this geometry; 0
-    where the posterior keeps the R route."""
+    """Partials of the quad plan (bo_post_quad_plan: chunks of A^{-1} block
+    pairs) at this geometry; 0 where the posterior keeps the R route."""
     npairs = ctypes.c_int()
     check(lib().bo_post_quad_plan(B, q, n, ctypes.byref(npairs)), "post_quad_plan")
     return npairs.value
@@ -959,12 +959,14 @@ def qehvi(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor, cell_lo: torch.T
     S = Z.shape[0]
     K, cstride = _cells_layout(cell_lo, S)
     acq = torch.empty(B, dtype=torch.float64, device=dev)
+    work = torch.empty(8 * B, dtype=torch.float64, device=dev)  # sample split (B < 256)
     Fc = F.contiguous() if F is not None else None
     a = _lib.QehviArgs(B=B, q=q, m=m, S=S, mean=mean.contiguous(), L=L.contiguous(),
                        Z=Z.reshape(S, q * m).contiguous(), cell_lo=cell_lo.contiguous(),
                        cell_hi=cell_hi.contiguous(), K=K, Qp=Qp, cell_stride=cstride, F=Fc,
                        ldF=Fc.shape[-1] if Fc is not None else 0,
-                       sF=Fc.shape[-1] * S if Fc is not None else 0, acq=acq)
+                       sF=Fc.shape[-1] * S if Fc is not None else 0, acq=acq, work=work,
+                       work_elems=work.numel())
     check(lib().bo_qehvi_v(ctypes.byref(a), _stream(dev)), "qehvi")
     return acq
 
@@ -981,12 +983,13 @@ def qehvi_backward(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor, cell_lo
     dL = torch.empty(m, B, q, q, dtype=torch.float64, device=dev)
     Fc = F.contiguous() if F is not None else None
     dF = torch.zeros_like(Fc) if Fc is not None else None
+    work = torch.empty(8 * B * m * q * (q + 3) // 2, dtype=torch.float64, device=dev)
     a = _lib.QehviArgs(B=B, q=q, m=m, S=S, mean=mean.contiguous(), L=L.contiguous(),
                        Z=Z.reshape(S, q * m).contiguous(), cell_lo=cell_lo.contiguous(),
                        cell_hi=cell_hi.contiguous(), K=K, Qp=Qp, cell_stride=cstride, F=Fc,
                        ldF=Fc.shape[-1] if Fc is not None else 0,
                        sF=Fc.shape[-1] * S if Fc is not None else 0, dacq=dacq.contiguous(),
-                       dmean=dmean, dL=dL, dF=dF)
+                       dmean=dmean, dL=dL, dF=dF, work=work, work_elems=work.numel())
     check(lib().bo_qehvi_backward_v(ctypes.byref(a), _stream(dev)), "qehvi_backward")
     if F is not None:
         return dmean, dL, dF

@@ -320,11 +320,15 @@ int bo_sym_lower(double* A, int64_t ld, int64_t n, void* stream);
  * bo_sym_lower), mu_b = c + K*x alpha -- the same [G] exact_predictive_mean /
  * covar as bo_post_partials (models/gpytorch.py:405-466), linear in the blocks
  * of A^{-1}, so the units' partials are 16 x 16 blocks and no split-k
- * reduction runs.  bo_post_quad_plan: *npairs > 0 when the plan applies to
- * (B, q, n) (stream-K geometries with n <= 2048 and <= 1024 units; BO_POST_QUAD=0/1 disables /
- * forces it); the caller then sizes Spart as npairs x nrows_pad/16 x 16 x 16
- * and mpart as npairs x nrows_pad and finalises with BoQmcFinalizeArgs
- * nparts = npairs, sym_parts = 1.  Kt: bo_post_kxt's K*x^T (np x nrows_pad). */
+ * reduction runs; the pairs of one block row are taken in chunks of G (one
+ * partial per chunk and row tile).  bo_post_quad_plan: *npairs = the partial
+ * count (> 0) when the plan applies to (B, q, n) (opt-in: BO_POST_QUAD=auto
+ * for stream-K geometries with n <= 2048 and <= 1024 pair units, =1 forces
+ * it; unset / 0: the R route, measured as fast at C2; BO_QUAD_G sets the
+ * chunk, default 1); the caller then sizes Spart as npairs x
+ * nrows_pad/16 x 16 x 16 and mpart as npairs x nrows_pad and finalises with
+ * BoQmcFinalizeArgs nparts = npairs, sym_parts = 1.  Kt: bo_post_kxt's K*x^T
+ * (np x nrows_pad). */
 int bo_post_quad_plan(int64_t B, int q, int64_t n, int* npairs);
 int bo_post_quad(const double* Kt, const double* Ainv, int64_t lda, const double* alpha, int64_t B,
                  int q, int64_t n, double* Spart, double* mpart, void* stream);
@@ -637,6 +641,11 @@ typedef struct BoQehviArgs { /* bo_qehvi and bo_qehvi_backward (d* fields: backw
   double* acq;
   const double* dacq;
   double *dmean, *dL, *dF;
+  /* ABI 11 (optional): a workspace lets the samples of each t-batch split
+   * over several workgroups when B leaves CUs idle -- forward >= 2 B doubles,
+   * backward >= 2 B m q (q + 3) / 2 */
+  double* work;
+  int64_t work_elems;
 } BoQehviArgs;
 int bo_qehvi_v(const BoQehviArgs* a, void* stream);
 int bo_qehvi_backward_v(const BoQehviArgs* a, void* stream);

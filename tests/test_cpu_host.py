@@ -194,10 +194,11 @@ def test_native_torch_operators_load():
 
 
 def test_quad_plan_geometries(monkeypatch):
-    """bo_post_quad_plan (host): the quad plan takes the stream-K geometries
-    with n <= 2048 and <= 1024 units (C2), not the C3 one-pass grid, large n
-    or many units; BO_POST_QUAD=0
-    disables and =1 forces it; the pair count is nb (nb + 1) / 2 of 64-blocks."""
+    """bo_post_quad_plan (host): opt-in (BO_POST_QUAD=auto), the quad plan
+    takes the stream-K geometries with n <= 2048 and <= 1024 units (C2), not
+    the C3 one-pass grid, large n or many units; BO_POST_QUAD=0
+    disables and =1 forces it; the partial count is that of the chunks (of 1
+    by default) of block pairs (64 x 64 blocks of A^{-1}) sharing a block row."""
     import ctypes
     from botorch_amd import _lib
     lib = _lib.lib()
@@ -208,11 +209,16 @@ def test_quad_plan_geometries(monkeypatch):
         return out.value
 
     monkeypatch.delenv("BO_POST_QUAD", raising=False)
-    assert pairs(64, 8, 1024) == 16 * 17 // 2       # C2: 544 units
-    assert pairs(50, 3, 1500) == 24 * 25 // 2       # 600 units, ragged n
-    assert pairs(33, 16, 2048) == 0                 # 2640 units: the R route
+    def chunks(nb, g=1):  # partials per row tile: sum_kb ceil((nb - kb) / g)
+        return sum(-(-(nb - kb) // g) for kb in range(nb))
+
+    assert pairs(64, 8, 1024) == 0                  # opt-in: the R route by default
+    monkeypatch.setenv("BO_POST_QUAD", "auto")
+    assert pairs(64, 8, 1024) == chunks(16) == 136  # C2: 136 pairs, 544 pair units
+    assert pairs(50, 3, 1500) == chunks(24)         # 600 pair units, ragged n
+    assert pairs(33, 16, 2048) == 0                 # 2640 pair units: the R route
     assert pairs(512, 16, 4096) == 0 and pairs(64, 16, 4096) == 0 and pairs(0, 8, 1024) == 0
     monkeypatch.setenv("BO_POST_QUAD", "0")
     assert pairs(64, 8, 1024) == 0
     monkeypatch.setenv("BO_POST_QUAD", "1")
-    assert pairs(512, 16, 4096) == 64 * 65 // 2
+    assert pairs(512, 16, 4096) == chunks(64)

@@ -557,6 +557,7 @@ def test_quad_plan_matches_r_route_and_oracle(n, B, q, S, monkeypatch):
     g = torch.Generator().manual_seed(1)
     Xc = torch.rand(B, q, 6, generator=g, dtype=torch.float64)
     Xd = Xc.to(DEV)
+    monkeypatch.setenv("BO_POST_QUAD", "auto")  # opt-in plan
     kernels.quad_pairs.cache_clear()
     assert kernels.quad_pairs(B, q, n) > 0
     kernels.check_ladder_status()
@@ -573,6 +574,7 @@ def test_quad_plan_matches_r_route_and_oracle(n, B, q, S, monkeypatch):
         v_r = acqf(Xd)
     monkeypatch.delenv("BO_POST_QUAD")
     kernels.quad_pairs.cache_clear()
+    assert kernels.quad_pairs(B, q, n) == 0  # the default
     torch.testing.assert_close(vals[0], v_r, rtol=1e-9, atol=1e-13)
     ref = qei(orc, Xc, draw_sobol_normal_samples(q, S, 0), best)
     torch.testing.assert_close(vals[0].cpu(), ref, rtol=1e-7, atol=1e-12)
