@@ -579,6 +579,166 @@ __device__ void potrf_trtri64(const Ctx& c, double* S, double* D, double* rinv, 
   __syncthreads();
 }
 
+// ---- the diagonal tile, column-owner form (round 3) ---------------------------------
+// Lane r of every wave holds row r of the 64 x 64 block; wave w holds its
+// columns 16 w .. 16 w + 15 (v[m] = A[r][16 w + m]).  Column J is factored by
+// its owner wave J / 16 with no workgroup barrier: the pivot comes by
+// v_readlane, L[J+1][J] too (the chain: pivot -> rsq -> scale -> the next
+// pivot's update), the column goes to the column buffer Lc (column-major,
+// stride 64) and a column counter in LDS; the later waves apply it to their
+// columns as it appears (their row's L[r][J] and the uniform L[16 w + m][J]
+// read back from Lc), so wave w + 1 starts factoring one column behind wave w's
+// last.  Each wave then inverts its own 16 x 16 diagonal block from Lc while
+// the later waves factor, and the inverse is merged by recursive doubling as
+// in potrf_trtri64.  Replaces the four-panel scheme's panel solves and
+// trailing updates, each behind a workgroup barrier, on the Cholesky's chain.
+template <int JL>
+__device__ __forceinline__ void lcol_step(double (&v)[16], int r, int c0, int& fail, double* Lc,
+                                          double* rinv, lds_cnt_t* cnt, bool lane0) {
+  const int J = c0 + JL;
+  const double piv = readlane_d(v[JL], J);
+  if (!(piv > 0.0) && fail == 0) fail = J + 1;
+  const double rr = rsq_nr(piv);
+  const double l = (r >= J) ? v[JL] * rr : 0.0;  // L[r][J] (r == J: sqrt(piv))
+  v[JL] = l;
+  if constexpr (JL + 1 < 16) v[JL + 1] = fma(-l, readlane_d(l, J + 1), v[JL + 1]);
+  // every lane stores the uniform rinv and counter words (no branch: a lane-0
+  // branch per column let the compiler sink each column's updates to the next
+  // pivot, i.e. onto the chain)
+  Lc[J * 64 + r] = l;
+  rinv[J] = rr;
+  asm volatile("" ::: "memory");  // (compiler order only: LDS writes of one wave land in order)
+  *cnt = J + 1;
+#pragma unroll
+  for (int m = JL + 2; m < 16; ++m) v[m] = fma(-l, Lc[J * 64 + c0 + m], v[m]);
+}
+
+template <int... JL>
+__device__ __forceinline__ void lcol_steps(std::integer_sequence<int, JL...>, double (&v)[16], int r,
+                                           int c0, int& fail, double* Lc, double* rinv, lds_cnt_t* cnt,
+                                           bool lane0) {
+  (lcol_step<JL>(v, r, c0, fail, Lc, rinv, cnt, lane0), ...);
+}
+
+// Column JJ of the inverse of the 16 x 16 diagonal block at c0 (its L columns
+// final in Lc): group g of the wave owns inverse columns 4 g .. 4 g + 3.
+template <int JJ>
+__device__ __forceinline__ void lcol_inv_step(double (&x)[4], int r, const double* rinv,
+                                              const double* Lcb) {
+  const double rr = rinv[JJ];
+  const double l = Lcb[JJ * 64 + r];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double xs = (r == JJ) ? x[q] * rr : x[q];
+    const double sv = row_bcast<JJ>(xs);
+    x[q] = (r > JJ) ? fma(-l, sv, xs) : xs;
+  }
+}
+
+template <int... JJ>
+__device__ __forceinline__ void lcol_inv_steps(std::integer_sequence<int, JJ...>, double (&x)[4], int r,
+                                               const double* rinv, const double* Lcb) {
+  (lcol_inv_step<JJ>(x, r, rinv, Lcb), ...);
+}
+
+// S (64 x 64, lower part meaningful) -> L (lower, upper zeroed) in place, and
+// D = L^{-1}; Lc: 64 x 64 doubles of LDS scratch (the column buffer); sfail:
+// 4 ints of LDS.
+__device__ void potrf_trtri64_cols(const Ctx& c, double* S, double* D, double* rinv, int* info, int row0,
+                                   double* Lc, lds_cnt_t* cnt, int* sfail, long long* ct = nullptr) {
+  if (c.tid == 0) *cnt = 0;
+  __syncthreads();
+  const int w = c.wave, r = c.lane, c0 = 16 * w;
+  double v[16];
+#pragma unroll
+  for (int m = 0; m < 16; m += 2) {
+    const double2 a = *reinterpret_cast<const double2*>(S + r * LP + c0 + m);
+    v[m] = a.x;
+    v[m + 1] = a.y;
+  }
+  // the earlier waves' columns, applied as they appear
+  int avail = 0;
+  for (int J = 0; J < c0; ++J) {
+    if (J >= avail) {
+      while ((avail = *cnt) <= J) __builtin_amdgcn_s_sleep(0);
+      asm volatile("" ::: "memory");
+    }
+    const double lr = Lc[J * 64 + r];
+    const double2* col = reinterpret_cast<const double2*>(Lc + J * 64 + c0);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const double2 lm = col[m];
+      v[2 * m] = fma(-lr, lm.x, v[2 * m]);
+      v[2 * m + 1] = fma(-lr, lm.y, v[2 * m + 1]);
+    }
+  }
+  if (ct && r == 0 && (w == 1 || w == 3)) ct[w == 1 ? 6 : 7] = wall_clock64();
+  if (ct && r == 0 && (w == 1 || w == 3)) ct[w == 1 ? 6 : 7] = wall_clock64();
+  int fail = 0;  // first non-positive pivot of the wave's columns (1-based), uniform
+  lcol_steps(std::make_integer_sequence<int, 16>{}, v, r, c0, fail, Lc, rinv, cnt, r == 0);
+  if (r == 0) sfail[w] = fail;
+  if (ct && c.tid == 192) ct[4] = wall_clock64();
+#pragma unroll
+  for (int m = 0; m < 16; m += 2) {
+    double2 a;
+    a.x = c0 + m <= r ? v[m] : 0.0;
+    a.y = c0 + m + 1 <= r ? v[m + 1] : 0.0;
+    *reinterpret_cast<double2*>(S + r * LP + c0 + m) = a;
+  }
+  {  // the wave's 16 x 16 diagonal block inverse, and the zeros of its D band
+    const int rb = r & 15, g = r >> 4;
+    double x[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = (rb == 4 * g + q) ? 1.0 : 0.0;
+    for (int e = r; e < 16 * 64; e += 64) {
+      const int rr = e >> 6, col = e & 63;
+      if (col < c0 || col >= c0 + 16) D[(c0 + rr) * LP + col] = 0.0;
+    }
+    lcol_inv_steps(std::make_integer_sequence<int, 16>{}, x, rb, rinv + c0, Lc + c0 * 64 + c0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) D[(c0 + rb) * LP + c0 + 4 * g + q] = x[q];
+  }
+  __syncthreads();
+  if (c.tid == 0) {
+    for (int q = 0; q < 4; ++q)
+      if (sfail[q]) {
+        atomicCAS(info, 0, row0 + sfail[q]);
+        break;
+      }
+  }
+  if (ct && c.tid == 0) ct[5] = wall_clock64();
+  // 16 -> 32: pairs (0, 1) and (2, 3) (waves 0, 1): X21 = -X22 (L21 X11)
+  if (c.wave < 2) {
+    const int b1 = 32 * c.wave, b2 = b1 + 16;
+    double* Tb = S + b1 * LP + b2;  // strictly-upper scratch
+    v4d a = mma16<false>(S + b2 * LP + b1, D + b1 * LP + b1, 1, c.lane);
+    put16(Tb, a, c.lane, 1.0);
+    a = mma16<false>(D + b2 * LP + b2, Tb, 1, c.lane);
+    put16(D + b2 * LP + b1, a, c.lane, -1.0);
+  }
+  __syncthreads();
+  // 32 -> 64: X21 (rows 32.., cols 0..31) = -X22 (L21 X11); one 16 x 16 tile per wave
+  {
+    const int ti = c.wave >> 1, tj = c.wave & 1;
+    double* Tb = S + 32;  // rows 0..31, cols 32..63: strictly upper
+    const v4d a = mma16<false>(S + (32 + 16 * ti) * LP, D + 16 * tj, 2, c.lane);
+    __syncthreads();
+    put16(Tb + 16 * ti * LP + 16 * tj, a, c.lane, 1.0);
+    __syncthreads();
+    const v4d b = mma16<false>(D + (32 + 16 * ti) * LP + 32, Tb + 16 * tj, 2, c.lane);
+    put16(D + (32 + 16 * ti) * LP + 16 * tj, b, c.lane, -1.0);
+  }
+  __syncthreads();
+  for (int e = c.tid; e < 32 * 32; e += 256) S[(e >> 5) * LP + 32 + (e & 31)] = 0.0;
+  if (c.tid < 64) {  // the two 16 x 16 scratch blocks of the 16 -> 32 merges
+    for (int e = c.tid; e < 256; e += 64) {
+      S[(e >> 4) * LP + 16 + (e & 15)] = 0.0;
+      S[(32 + (e >> 4)) * LP + 48 + (e & 15)] = 0.0;
+    }
+  }
+  __syncthreads();
+}
+
 // ---- the bulk tasks: a chunk of tile rows i in [i0, i1) ----------------------------
 // KIND 0 TRSM    X0 <- A_ik,                   acc  = X0 X1^T  -> A_ik = L_ik, fL[i][k] = 1
 // KIND 1 COLUPD  X0 <- L_ik (X1 if i == j),    acc  = A_ij - X0 X1^T -> A_ij, fA[i][j] = k + 1
@@ -835,7 +995,8 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
                                                        int np, int T, const int4* __restrict__ tasks,
                                                        int ntasks, u32* __restrict__ flags,
                                                        int* __restrict__ info,
-                                                       long long* __restrict__ trace, int nb) {
+                                                       long long* __restrict__ trace, int nb,
+                                                       int prows) {
   __shared__ __attribute__((aligned(16))) double X0[TB * LP];
   __shared__ __attribute__((aligned(16))) double X1[TB * LP];
   __shared__ __attribute__((aligned(16))) double X2[TB * LP];  // batched update operands
@@ -843,6 +1004,7 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
   __shared__ double rinv[TB];
   __shared__ double Lcol[512];  // diagonal-block columns, double-buffered by block parity
   __shared__ int s_cnt;
+  __shared__ int s_fail[4];
   __shared__ int s_ok;
   __shared__ int s_rdy[2];
   __shared__ int s_task;
@@ -930,7 +1092,10 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
         __syncthreads();
         long long* ct = trace ? trace + 4 * ntasks + 8 * k : nullptr;
         if (ct && c.tid == 0) ct[0] = wall_clock64();
-        potrf_trtri64(c, X0, X1, rinv, minfo, k * TB, Lcol, (lds_cnt_t*)&s_cnt, ct);
+        if (prows)
+          potrf_trtri64_cols(c, X0, X1, rinv, minfo, k * TB, X2, (lds_cnt_t*)&s_cnt, s_fail, ct);
+        else
+          potrf_trtri64(c, X0, X1, rinv, minfo, k * TB, Lcol, (lds_cnt_t*)&s_cnt, ct);
         if (ct && c.tid == 0) ct[1] = wall_clock64();
         if (ct && c.tid == 0) ct[2] = wall_clock64();
         lds_to_tile(c, X0, c.rA, k, k);
@@ -1259,8 +1424,13 @@ int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipS
   // one workgroup per CU: two per CU (74 KB of LDS each fits) measured slower,
   // 2.35 -> 2.97 ms at n = 4096 -- the sc1 tile traffic, not latency, is the limit
   const int grid = cus < tb->n ? cus : tb->n;
+  // the diagonal tile's factor: row-per-lane (1, default) or the four-panel form (0)
+  static const int prows = [] {
+    const char* e = getenv("BO_CHOL_POTRF_ROWS");
+    return e ? atoi(e) : 1;
+  }();
   chol_dag_kernel<<<grid, 256, 0, st>>>(A, Linv, (int)np, T, tb->dev, tb->n, (u32*)work, info,
-                                          trace, nb);
+                                          trace, nb, prows);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
@@ -1277,6 +1447,46 @@ extern "C" int bo_probe_chol_dag(double* A, double* Linv, int64_t np, int* info,
   if (s) return s;
   *ntasks = tb->n;
   return bo_chol_dag(A, Linv, np, info, work, as_stream(stream), trace, 1);
+}
+
+// One workgroup factors + inverts the 64 x 64 SPD matrix A (row-major) reps
+// times in LDS with the diagonal-tile routine of the DAG (variant 1: column
+// owners, 0: four panels); out = [L | D] (2 x 4096), ct[8] = the phase stamps
+// of the last rep, ct[8] = total wall-clock ticks of all reps.
+__global__ __launch_bounds__(256) void potrf64_probe_kernel(const double* A, double* out, long long* ct,
+                                                            int* info, int variant, int reps) {
+  __shared__ __attribute__((aligned(16))) double S[TB * LP];
+  __shared__ __attribute__((aligned(16))) double D[TB * LP];
+  __shared__ __attribute__((aligned(16))) double Lc[TB * LP];
+  __shared__ double rinv[TB];
+  __shared__ double Lcol[512];
+  __shared__ int s_cnt;
+  __shared__ int s_fail[4];
+  Ctx c;
+  c.np = 64; c.tid = threadIdx.x; c.lane = c.tid & 63; c.wave = c.tid >> 6;
+  c.wm = (c.wave >> 1) * 32; c.wn = (c.wave & 1) * 32;
+  const long long t0 = wall_clock64();
+  for (int it = 0; it < reps; ++it) {
+    for (int e = c.tid; e < 4096; e += 256) S[(e >> 6) * LP + (e & 63)] = A[e];
+    __syncthreads();
+    if (c.tid == 0) ct[0] = wall_clock64();
+    if (variant) potrf_trtri64_cols(c, S, D, rinv, info, 0, Lc, (lds_cnt_t*)&s_cnt, s_fail, ct);
+    else potrf_trtri64(c, S, D, rinv, info, 0, Lcol, (lds_cnt_t*)&s_cnt, ct);
+    if (c.tid == 0) ct[1] = wall_clock64();
+    __syncthreads();
+  }
+  if (c.tid == 0) ct[8] = wall_clock64() - t0;
+  for (int e = c.tid; e < 4096; e += 256) {
+    out[e] = S[(e >> 6) * LP + (e & 63)];
+    out[4096 + e] = D[(e >> 6) * LP + (e & 63)];
+  }
+}
+
+extern "C" int bo_probe_potrf64(const double* A, double* out, long long* ct, int* info, int variant,
+                                int reps, void* stream) {
+  potrf64_probe_kernel<<<1, 256, 0, as_stream(stream)>>>(A, out, ct, info, variant, reps);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
 }
 
 // Cycles (s_memtime ticks) per 16 x 16 diagonal factor + inverse on one wave:

@@ -8,7 +8,8 @@ PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libbotorch_amd_
 _P, _I, _I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
 _SIG = {"bo_probe_valu_f64": [_I, _P, _P],
         "bo_probe_chol_dag": [_P, _P, _I64, _P, _P, _P, _P, _P],
-        "bo_probe_diag16": [_P, _P, _P]}
+        "bo_probe_diag16": [_P, _P, _P],
+        "bo_probe_potrf64": [_P, _P, _P, _P, _I, _I, _P]}
 _h = None
 
 

@@ -30,6 +30,13 @@ int bo_probe_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work
  * only; sink: one double of scratch. */
 int bo_probe_diag16(long long* out, double* sink, void* stream);
 
+/* One workgroup factors + inverts a 64 x 64 SPD A (row-major) reps times with
+ * the DAG's diagonal-tile routine (variant 1 column owners, 0 four panels):
+ * out = [L | L^{-1}], ct[0..7] the last rep's phase stamps, ct[8] all reps'
+ * wall-clock ticks (tools/probe_potrf64.py). */
+int bo_probe_potrf64(const double* A, double* out, long long* ct, int* info, int variant, int reps,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

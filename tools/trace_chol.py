@@ -79,7 +79,10 @@ def main():
                                  "store_publish": float(ph[:, 2].mean()),
                                  "diag0": float(((ct[:, 4] - ct[:, 0]).double() / 100.0).mean()),
                                  "loop3": float(((ct[:, 5] - ct[:, 4]).double() / 100.0).mean()),
-                                 "merges": float(((ct[:, 1] - ct[:, 5]).double() / 100.0).mean())}
+                                 "merges": float(((ct[:, 1] - ct[:, 5]).double() / 100.0).mean()),
+                                 # column-owner factor: waves 1 and 3 start their own columns
+                                 "w1_start": float(((ct[:, 6] - ct[:, 0]).double() / 100.0).mean()),
+                                 "w3_start": float(((ct[:, 7] - ct[:, 0]).double() / 100.0).mean())}
     pre = [(int(ct[kk, 0]) - int(st[i])) / 100.0 for kk, i in enumerate(crit.tolist())]
     out["crit_pre_us_mean"] = sum(pre) / len(pre)
     ph = trace[4 * ntask + 8 * (np_ // 64): 4 * ntask + 8 * (np_ // 64) + 8 * ntask].view(ntask, 8).cpu()
