@@ -315,6 +315,7 @@ __device__ __forceinline__ double row_bcast(double v) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+#ifdef BO_TOOLS  // the round-2 four-panel diagonal tile: timing reference of tools/probe_potrf64.py
 template <int JJ, int M>
 __device__ __forceinline__ void col_update(double (&v)[16], double l) {
   if constexpr (M > JJ) v[M] = fma(-l, row_bcast<M>(l), v[M]);
@@ -447,6 +448,8 @@ __global__ void diag16_probe_kernel(int iters, long long* out, double* sink) {
   if (chk == 12345.0) sink[0] = chk;
 }
 
+#endif  // BO_TOOLS
+
 // 16 x 16 MFMA tile: acc = sum_k A[k] op(B) over K = 16 * nk columns/rows from LDS.
 // A(m, k) = SA[m * LP + k]; BT: B(k, n) = SB[n * LP + k], else SB[k * LP + n].
 template <bool BT>
@@ -467,6 +470,7 @@ __device__ __forceinline__ void put16(double* D, v4d a, int lane, double scale) 
   for (int q = 0; q < 4; ++q) D[mfma_row(lane, q) * LP + mfma_col(lane)] = scale * a[q];
 }
 
+#ifdef BO_TOOLS
 // S (64 x 64, lower part meaningful) -> L (lower, upper zeroed) in place, and
 // D = L^{-1} (lower, upper zero).  Four 16-column panels: wave 0 factors the
 // 16 x 16 diagonal block AND inverts it (pivots and columns broadcast inside
@@ -579,6 +583,8 @@ __device__ void potrf_trtri64(const Ctx& c, double* S, double* D, double* rinv, 
   __syncthreads();
 }
 
+#endif  // BO_TOOLS
+
 // ---- the diagonal tile, column-owner form (round 3) ---------------------------------
 // Lane r of every wave holds row r of the 64 x 64 block; wave w holds its
 // columns 16 w .. 16 w + 15 (v[m] = A[r][16 w + m]).  Column J is factored by
@@ -592,16 +598,56 @@ __device__ void potrf_trtri64(const Ctx& c, double* S, double* D, double* rinv, 
 // the later waves factor, and the inverse is merged by recursive doubling as
 // in potrf_trtri64.  Replaces the four-panel scheme's panel solves and
 // trailing updates, each behind a workgroup barrier, on the Cholesky's chain.
-template <int JL>
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+
+// Column J = c0 + JL on its owner wave; d enters as the pivot d_J and leaves as
+// d_{J+1}.  The pivots run on a chain of their own: d_{J+1} = a'_{J+1,J+1} -
+// a'_{J+1,J}^2 / d_J (a' = the entries updated through column J - 1, read from
+// lane J + 1 before this column's update), so one reciprocal per column is on
+// it and 1 / sqrt(d_J) (the column's scale) runs beside it; the entries the
+// next two pivots need (columns JL + 1, JL + 2) take L[.][J] by v_readlane,
+// the others from the column buffer.
+// VAR (timing variants, tools/probe_potrf64.py): 0 pivots from the column
+// itself, 1 pivots on their own reciprocal chain, 2 = 0 with one Newton step
+// on 1/sqrt, 3 = 0 without the LDS-fed updates (wrong results: the chain alone)
+template <int VAR>
+__device__ __forceinline__ double rsq_var(double v) {
+  double r = __builtin_amdgcn_rsq(v);
+  r = r * fma(-0.5 * v * r, r, 1.5);
+  if (VAR != 2) r = r * fma(-0.5 * v * r, r, 1.5);
+  return r;
+}
+
+// Column J = c0 + JL on its owner wave (VAR 1: d enters as the pivot d_J and
+// leaves as d_{J+1}, computed as d_{J+1} = a'_{J+1,J+1} - a'_{J+1,J}^2 / d_J
+// from lane J + 1's entries before this column's update).  The entries the
+// next two pivots need (columns JL + 1, JL + 2) take L[.][J] by v_readlane,
+// the others from the column buffer.
+template <int JL, int VAR>
 __device__ __forceinline__ void lcol_step(double (&v)[16], int r, int c0, int& fail, double* Lc,
-                                          double* rinv, lds_cnt_t* cnt, bool lane0) {
+                                          double* rinv, lds_cnt_t* cnt, double& d) {
   const int J = c0 + JL;
-  const double piv = readlane_d(v[JL], J);
-  if (!(piv > 0.0) && fail == 0) fail = J + 1;
-  const double rr = rsq_nr(piv);
-  const double l = (r >= J) ? v[JL] * rr : 0.0;  // L[r][J] (r == J: sqrt(piv))
+  if (VAR != 1) d = readlane_d(v[JL], J);
+  if (!(d > 0.0) && fail == 0) fail = J + 1;
+  const double rr = rsq_var<VAR>(d);
+  double dn = 0.0;
+  if constexpr (VAR == 1 && JL + 1 < 16) {
+    const double inv = rcp_nr(d);
+    const double x = readlane_d(v[JL], J + 1), y = readlane_d(v[JL + 1], J + 1);
+    dn = fma(-(x * x), inv, y);
+  }
+  double l;
+  if (VAR == 1) l = r > J ? v[JL] * rr : (r == J ? d * rr : 0.0);  // L[r][J] (r == J: sqrt(d_J))
+  else l = r >= J ? v[JL] * rr : 0.0;
   v[JL] = l;
   if constexpr (JL + 1 < 16) v[JL + 1] = fma(-l, readlane_d(l, J + 1), v[JL + 1]);
+  if constexpr (JL + 2 < 16) v[JL + 2] = fma(-l, readlane_d(l, J + 2), v[JL + 2]);
   // every lane stores the uniform rinv and counter words (no branch: a lane-0
   // branch per column let the compiler sink each column's updates to the next
   // pivot, i.e. onto the chain)
@@ -609,22 +655,30 @@ __device__ __forceinline__ void lcol_step(double (&v)[16], int r, int c0, int& f
   rinv[J] = rr;
   asm volatile("" ::: "memory");  // (compiler order only: LDS writes of one wave land in order)
   *cnt = J + 1;
+  if (VAR != 3) {
 #pragma unroll
-  for (int m = JL + 2; m < 16; ++m) v[m] = fma(-l, Lc[J * 64 + c0 + m], v[m]);
+    for (int m = JL + 3; m < 16; ++m) v[m] = fma(-l, Lc[J * 64 + c0 + m], v[m]);
+  }
+  if (VAR == 1) d = dn;
 }
 
-template <int... JL>
+template <int VAR, int... JL>
 __device__ __forceinline__ void lcol_steps(std::integer_sequence<int, JL...>, double (&v)[16], int r,
                                            int c0, int& fail, double* Lc, double* rinv, lds_cnt_t* cnt,
-                                           bool lane0) {
-  (lcol_step<JL>(v, r, c0, fail, Lc, rinv, cnt, lane0), ...);
+                                           double& d) {
+  (lcol_step<JL, VAR>(v, r, c0, fail, Lc, rinv, cnt, d), ...);
 }
 
-// Column JJ of the inverse of the 16 x 16 diagonal block at c0 (its L columns
-// final in Lc): group g of the wave owns inverse columns 4 g .. 4 g + 3.
-template <int JJ>
+// Column JJ of the inverse of the 16 x 16 diagonal block at c0 (POLL: wait for
+// its L column on the counter): group g of the wave owns inverse columns
+// 4 g .. 4 g + 3.
+template <int JJ, bool POLL>
 __device__ __forceinline__ void lcol_inv_step(double (&x)[4], int r, const double* rinv,
-                                              const double* Lcb) {
+                                              const double* Lcb, lds_cnt_t* cnt, int c0) {
+  if (POLL) {
+    while (*cnt < c0 + JJ + 1) __builtin_amdgcn_s_sleep(0);
+    asm volatile("" ::: "memory");
+  }
   const double rr = rinv[JJ];
   const double l = Lcb[JJ * 64 + r];
 #pragma unroll
@@ -635,17 +689,55 @@ __device__ __forceinline__ void lcol_inv_step(double (&x)[4], int r, const doubl
   }
 }
 
-template <int... JJ>
+template <bool POLL, int... JJ>
 __device__ __forceinline__ void lcol_inv_steps(std::integer_sequence<int, JJ...>, double (&x)[4], int r,
-                                               const double* rinv, const double* Lcb) {
-  (lcol_inv_step<JJ>(x, r, rinv, Lcb), ...);
+                                               const double* rinv, const double* Lcb, lds_cnt_t* cnt,
+                                               int c0) {
+  (lcol_inv_step<JJ, POLL>(x, r, rinv, Lcb, cnt, c0), ...);
+}
+
+// The 16 x 16 diagonal block inverse at c0 into D, and the zeros of its D band.
+template <bool POLL>
+__device__ __forceinline__ void lcol_block_inverse(int lane, int c0, double* D, const double* rinv,
+                                                   const double* Lc, lds_cnt_t* cnt) {
+  const int rb = lane & 15, g = lane >> 4;
+  double x[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) x[q] = (rb == 4 * g + q) ? 1.0 : 0.0;
+  for (int e = lane; e < 16 * 64; e += 64) {
+    const int rr = e >> 6, col = e & 63;
+    if (col < c0 || col >= c0 + 16) D[(c0 + rr) * LP + col] = 0.0;
+  }
+  lcol_inv_steps<POLL>(std::make_integer_sequence<int, 16>{}, x, rb, rinv + c0, Lc + c0 * 64 + c0, cnt,
+                       c0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) D[(c0 + rb) * LP + c0 + 4 * g + q] = x[q];
+}
+
+// LDS flag handshake between waves of one workgroup (no barrier): the setter's
+// LDS writes land in order before the flag; the waiter polls.
+__device__ __forceinline__ void lds_flag_set(lds_cnt_t* f) {
+  asm volatile("" ::: "memory");
+  *f = 1;
+}
+__device__ __forceinline__ void lds_flag_wait(lds_cnt_t* f) {
+  while (*f == 0) __builtin_amdgcn_s_sleep(0);
+  asm volatile("" ::: "memory");
 }
 
 // S (64 x 64, lower part meaningful) -> L (lower, upper zeroed) in place, and
-// D = L^{-1}; Lc: 64 x 64 doubles of LDS scratch (the column buffer); sfail:
-// 4 ints of LDS.
+// D = L^{-1}; Lc, Tsc: 64 x 64 (pitch LP) doubles of LDS scratch (the column
+// buffer, the merges' products); sfail, fl: 4 ints of LDS each.  The inverse
+// is merged from the four block inverses while the later waves still factor:
+//   wave 1:  X10 = -D11 (L10 D00), then T2 = L21 X11 (32 x 32)
+//   wave 2:  T' = L32 D22
+//   wave 3:  X32 = -D33 T' (D33: wave 0, one column behind wave 3's factor)
+// and, after the one barrier, X21 = -X22 T2 (one 16 x 16 tile per wave).
+template <int VAR>
 __device__ void potrf_trtri64_cols(const Ctx& c, double* S, double* D, double* rinv, int* info, int row0,
-                                   double* Lc, lds_cnt_t* cnt, int* sfail, long long* ct = nullptr) {
+                                   double* Lc, double* Tsc, lds_cnt_t* cnt, int* sfail, lds_cnt_t* fl,
+                                   long long* ct = nullptr) {
+  if (c.tid < 4) fl[c.tid] = 0;
   if (c.tid == 0) *cnt = 0;
   __syncthreads();
   const int w = c.wave, r = c.lane, c0 = 16 * w;
@@ -673,9 +765,9 @@ __device__ void potrf_trtri64_cols(const Ctx& c, double* S, double* D, double* r
     }
   }
   if (ct && r == 0 && (w == 1 || w == 3)) ct[w == 1 ? 6 : 7] = wall_clock64();
-  if (ct && r == 0 && (w == 1 || w == 3)) ct[w == 1 ? 6 : 7] = wall_clock64();
   int fail = 0;  // first non-positive pivot of the wave's columns (1-based), uniform
-  lcol_steps(std::make_integer_sequence<int, 16>{}, v, r, c0, fail, Lc, rinv, cnt, r == 0);
+  double d = readlane_d(v[0], c0);
+  lcol_steps<VAR>(std::make_integer_sequence<int, 16>{}, v, r, c0, fail, Lc, rinv, cnt, d);
   if (r == 0) sfail[w] = fail;
   if (ct && c.tid == 192) ct[4] = wall_clock64();
 #pragma unroll
@@ -685,18 +777,28 @@ __device__ void potrf_trtri64_cols(const Ctx& c, double* S, double* D, double* r
     a.y = c0 + m + 1 <= r ? v[m + 1] : 0.0;
     *reinterpret_cast<double2*>(S + r * LP + c0 + m) = a;
   }
-  {  // the wave's 16 x 16 diagonal block inverse, and the zeros of its D band
-    const int rb = r & 15, g = r >> 4;
-    double x[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) x[q] = (rb == 4 * g + q) ? 1.0 : 0.0;
-    for (int e = r; e < 16 * 64; e += 64) {
-      const int rr = e >> 6, col = e & 63;
-      if (col < c0 || col >= c0 + 16) D[(c0 + rr) * LP + col] = 0.0;
+  if (w < 3) lcol_block_inverse<false>(r, c0, D, rinv, Lc, cnt);
+  if (w == 0) {
+    lds_flag_set(fl + 0);                             // D00
+    lcol_block_inverse<true>(r, 48, D, rinv, Lc, cnt);  // D33, one column behind wave 3
+    lds_flag_set(fl + 1);
+  } else if (w == 1) {
+    lds_flag_wait(fl + 0);
+    put16(Tsc, mma16<false>(S + 16 * LP, D, 1, r), r, 1.0);                         // L10 D00
+    put16(D + 16 * LP, mma16<false>(D + 16 * LP + 16, Tsc, 1, r), r, -1.0);          // X10
+#pragma unroll 1
+    for (int t = 0; t < 4; ++t) {  // T2 = L21 X11
+      const int ti = t >> 1, tj = t & 1;
+      put16(Tsc + (32 + 16 * ti) * LP + 16 * tj, mma16<false>(S + (32 + 16 * ti) * LP, D + 16 * tj, 2, r),
+            r, 1.0);
     }
-    lcol_inv_steps(std::make_integer_sequence<int, 16>{}, x, rb, rinv + c0, Lc + c0 * 64 + c0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) D[(c0 + rb) * LP + c0 + 4 * g + q] = x[q];
+  } else if (w == 2) {
+    put16(Tsc + 16, mma16<false>(S + 48 * LP + 32, D + 32 * LP + 32, 1, r), r, 1.0);  // L32 D22
+    lds_flag_set(fl + 2);
+  } else {
+    lds_flag_wait(fl + 1);
+    lds_flag_wait(fl + 2);
+    put16(D + 48 * LP + 32, mma16<false>(D + 48 * LP + 48, Tsc + 16, 1, r), r, -1.0);  // X32
   }
   __syncthreads();
   if (c.tid == 0) {
@@ -707,34 +809,10 @@ __device__ void potrf_trtri64_cols(const Ctx& c, double* S, double* D, double* r
       }
   }
   if (ct && c.tid == 0) ct[5] = wall_clock64();
-  // 16 -> 32: pairs (0, 1) and (2, 3) (waves 0, 1): X21 = -X22 (L21 X11)
-  if (c.wave < 2) {
-    const int b1 = 32 * c.wave, b2 = b1 + 16;
-    double* Tb = S + b1 * LP + b2;  // strictly-upper scratch
-    v4d a = mma16<false>(S + b2 * LP + b1, D + b1 * LP + b1, 1, c.lane);
-    put16(Tb, a, c.lane, 1.0);
-    a = mma16<false>(D + b2 * LP + b2, Tb, 1, c.lane);
-    put16(D + b2 * LP + b1, a, c.lane, -1.0);
-  }
-  __syncthreads();
-  // 32 -> 64: X21 (rows 32.., cols 0..31) = -X22 (L21 X11); one 16 x 16 tile per wave
-  {
-    const int ti = c.wave >> 1, tj = c.wave & 1;
-    double* Tb = S + 32;  // rows 0..31, cols 32..63: strictly upper
-    const v4d a = mma16<false>(S + (32 + 16 * ti) * LP, D + 16 * tj, 2, c.lane);
-    __syncthreads();
-    put16(Tb + 16 * ti * LP + 16 * tj, a, c.lane, 1.0);
-    __syncthreads();
-    const v4d b = mma16<false>(D + (32 + 16 * ti) * LP + 32, Tb + 16 * tj, 2, c.lane);
-    put16(D + (32 + 16 * ti) * LP + 16 * tj, b, c.lane, -1.0);
-  }
-  __syncthreads();
-  for (int e = c.tid; e < 32 * 32; e += 256) S[(e >> 5) * LP + 32 + (e & 31)] = 0.0;
-  if (c.tid < 64) {  // the two 16 x 16 scratch blocks of the 16 -> 32 merges
-    for (int e = c.tid; e < 256; e += 64) {
-      S[(e >> 4) * LP + 16 + (e & 15)] = 0.0;
-      S[(32 + (e >> 4)) * LP + 48 + (e & 15)] = 0.0;
-    }
+  {  // X21 = -X22 T2, one 16 x 16 tile per wave
+    const int ti = w >> 1, tj = w & 1;
+    put16(D + (32 + 16 * ti) * LP + 16 * tj,
+          mma16<false>(D + (32 + 16 * ti) * LP + 32, Tsc + 32 * LP + 16 * tj, 2, r), r, -1.0);
   }
   __syncthreads();
 }
@@ -995,16 +1073,15 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
                                                        int np, int T, const int4* __restrict__ tasks,
                                                        int ntasks, u32* __restrict__ flags,
                                                        int* __restrict__ info,
-                                                       long long* __restrict__ trace, int nb,
-                                                       int prows) {
+                                                       long long* __restrict__ trace, int nb) {
   __shared__ __attribute__((aligned(16))) double X0[TB * LP];
   __shared__ __attribute__((aligned(16))) double X1[TB * LP];
   __shared__ __attribute__((aligned(16))) double X2[TB * LP];  // batched update operands
   __shared__ __attribute__((aligned(16))) double X3[TB * LP];
   __shared__ double rinv[TB];
-  __shared__ double Lcol[512];  // diagonal-block columns, double-buffered by block parity
   __shared__ int s_cnt;
   __shared__ int s_fail[4];
+  __shared__ int s_fl[4];
   __shared__ int s_ok;
   __shared__ int s_rdy[2];
   __shared__ int s_task;
@@ -1092,10 +1169,8 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
         __syncthreads();
         long long* ct = trace ? trace + 4 * ntasks + 8 * k : nullptr;
         if (ct && c.tid == 0) ct[0] = wall_clock64();
-        if (prows)
-          potrf_trtri64_cols(c, X0, X1, rinv, minfo, k * TB, X2, (lds_cnt_t*)&s_cnt, s_fail, ct);
-        else
-          potrf_trtri64(c, X0, X1, rinv, minfo, k * TB, Lcol, (lds_cnt_t*)&s_cnt, ct);
+        potrf_trtri64_cols<0>(c, X0, X1, rinv, minfo, k * TB, X2, X3, (lds_cnt_t*)&s_cnt, s_fail,
+                              (lds_cnt_t*)s_fl, ct);
         if (ct && c.tid == 0) ct[1] = wall_clock64();
         if (ct && c.tid == 0) ct[2] = wall_clock64();
         lds_to_tile(c, X0, c.rA, k, k);
@@ -1238,6 +1313,12 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
   };
   std::vector<std::vector<int>> deps(n);
   std::vector<double> dur(n);
+  // CRIT's weight in the bottom levels: above 1 it lifts the factorisation's
+  // tasks (every path to a diagonal step) over the inverse's XSTEP chains, which
+  // feed no diagonal step (BO_CHOL_CRIT_W; dependants still sort after their
+  // inputs, so the queue stays a topological order)
+  double crit_w = 1.0;
+  if (const char* e = getenv("BO_CHOL_CRIT_W")) crit_w = atof(e);
   for (int t = 0; t < n; ++t) {
     const int type = v[t].x & 0xff, fin = (v[t].x >> 8) & 0xff, k = v[t].y, j = v[t].z;
     const int nk = std::max(1, v[t].x >> 16);
@@ -1250,7 +1331,7 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
         d.push_back(prodL[tix(k - 1, k - 1)]);
         d.push_back(verA(k, k, k - 1));
       }
-      dur[t] = 28.0;
+      dur[t] = 28.0 * crit_w;
     } else if (type == T_TRSM) {
       d.push_back(prodL[tix(k, k)]);
       for (int i = i0; i < i1; ++i) d.push_back(verA(i, k, k));
@@ -1424,13 +1505,8 @@ int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipS
   // one workgroup per CU: two per CU (74 KB of LDS each fits) measured slower,
   // 2.35 -> 2.97 ms at n = 4096 -- the sc1 tile traffic, not latency, is the limit
   const int grid = cus < tb->n ? cus : tb->n;
-  // the diagonal tile's factor: row-per-lane (1, default) or the four-panel form (0)
-  static const int prows = [] {
-    const char* e = getenv("BO_CHOL_POTRF_ROWS");
-    return e ? atoi(e) : 1;
-  }();
   chol_dag_kernel<<<grid, 256, 0, st>>>(A, Linv, (int)np, T, tb->dev, tb->n, (u32*)work, info,
-                                          trace, nb, prows);
+                                          trace, nb);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
@@ -1458,10 +1534,12 @@ __global__ __launch_bounds__(256) void potrf64_probe_kernel(const double* A, dou
   __shared__ __attribute__((aligned(16))) double S[TB * LP];
   __shared__ __attribute__((aligned(16))) double D[TB * LP];
   __shared__ __attribute__((aligned(16))) double Lc[TB * LP];
+  __shared__ __attribute__((aligned(16))) double Tsc[TB * LP];
   __shared__ double rinv[TB];
   __shared__ double Lcol[512];
   __shared__ int s_cnt;
   __shared__ int s_fail[4];
+  __shared__ int s_fl[4];
   Ctx c;
   c.np = 64; c.tid = threadIdx.x; c.lane = c.tid & 63; c.wave = c.tid >> 6;
   c.wm = (c.wave >> 1) * 32; c.wn = (c.wave & 1) * 32;
@@ -1470,8 +1548,13 @@ __global__ __launch_bounds__(256) void potrf64_probe_kernel(const double* A, dou
     for (int e = c.tid; e < 4096; e += 256) S[(e >> 6) * LP + (e & 63)] = A[e];
     __syncthreads();
     if (c.tid == 0) ct[0] = wall_clock64();
-    if (variant) potrf_trtri64_cols(c, S, D, rinv, info, 0, Lc, (lds_cnt_t*)&s_cnt, s_fail, ct);
-    else potrf_trtri64(c, S, D, rinv, info, 0, Lcol, (lds_cnt_t*)&s_cnt, ct);
+    lds_cnt_t* cn = (lds_cnt_t*)&s_cnt;
+    lds_cnt_t* fl = (lds_cnt_t*)s_fl;
+    if (variant == 1) potrf_trtri64_cols<0>(c, S, D, rinv, info, 0, Lc, Tsc, cn, s_fail, fl, ct);
+    else if (variant == 2) potrf_trtri64_cols<1>(c, S, D, rinv, info, 0, Lc, Tsc, cn, s_fail, fl, ct);
+    else if (variant == 3) potrf_trtri64_cols<2>(c, S, D, rinv, info, 0, Lc, Tsc, cn, s_fail, fl, ct);
+    else if (variant == 4) potrf_trtri64_cols<3>(c, S, D, rinv, info, 0, Lc, Tsc, cn, s_fail, fl, ct);
+    else potrf_trtri64(c, S, D, rinv, info, 0, Lcol, cn, ct);
     if (c.tid == 0) ct[1] = wall_clock64();
     __syncthreads();
   }

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """The DAG Cholesky's 64 x 64 diagonal-tile factor + inverse alone on one
 workgroup (bo_probe_potrf64): microseconds per call and per phase for the
-column-owner form (variant 1) and the four-panel form (0), and the result
+column-owner form (variants 1-4: pivots from the column, on a reciprocal
+chain, one Newton step on 1/sqrt, the chain without the LDS-fed updates) and
+the four-panel form (0), and the result
 against torch."""
 import json
 import os
@@ -24,7 +26,7 @@ def main():
     L = torch.linalg.cholesky(A)
     D = torch.linalg.inv(L)
     res = {}
-    for var in (1, 0):
+    for var in (1, 2, 3, 4, 0):
         out = torch.zeros(2 * 4096, dtype=torch.float64, device=dev)
         ct = torch.zeros(9, dtype=torch.int64, device=dev)
         info = torch.zeros(1, dtype=torch.int32, device=dev)
