@@ -508,12 +508,12 @@ def other_configs(dev, cpu=True):
     return out
 
 
-def time_cholesky(Xtr, dev, reps=10):
+def time_cholesky(Xtr, dev, reps=10, shapes=((3, 2048), (4, 4096), (8, 4096))):
     """Standalone n x n Cholesky + triangular inverse (bo_cholesky_inverse, the
     persistent task DAG) on the C3 kernel matrix ("standalone
     n x n Cholesky ms and MFMA %"): HIP events on the launch stream around the
     launch alone (the input copy excluded), median of ``reps``; flops n^3/3
-    (factor) + n^3/3 (inverse)."""
+    (factor) + n^3/3 (inverse); then the batched ``shapes`` (nb, n)."""
     import ctypes
     from botorch_amd import kernels
     from botorch_amd._lib import check, lib
@@ -552,7 +552,7 @@ def time_cholesky(Xtr, dev, reps=10):
     # (bo_cholesky_inverse_batched), the shapes of the path's multi-model fits
     # and caches: C4's ModelListGP(3) at n = 2048, multi-output models at C3's n
     batched = []
-    for nb, nn in ((3, 2048), (4, 4096), (8, 4096)):
+    for nb, nn in shapes:
         npb = kernels.padded_order(nn)
         Bb = torch.eye(npb, dtype=torch.float64, device=dev).repeat(nb, 1, 1)
         for m in range(nb):  # the C3 kernel matrix scaled per member (distinct SPD inputs)

@@ -6,7 +6,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r03z
+O=gpurun_out/r03final
 mkdir -p $O
 bash tools/gpu_run.sh test smoke || exit $?
 timeout -k 10 700 python3 bench.py > $O/bench_default.log 2>&1 || exit $?
@@ -18,6 +18,12 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $B --no-fit > $O/write.log 2>&1 || exit $?
 timeout -s KILL 500 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --output-format csv -d $O/mfma -o run -- $B > $O/mfma.log 2>&1 || exit $?
 python3 tools/pmc_summary.py $O/pmc_summary.json $O/fetch $O/write $O/mfma || exit $?
+# the n = 4096 Cholesky alone: kernel trace and its PMC passes (single problems)
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/chol -o run -- python3 tools/chol_only.py > $O/chol.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/chol_fetch -o run -- python3 tools/chol_only.py > $O/chol_fetch.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/chol_write -o run -- python3 tools/chol_only.py > $O/chol_write.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES --output-format csv -d $O/chol_mfma -o run -- python3 tools/chol_only.py > $O/chol_mfma.log 2>&1 || exit $?
+python3 tools/pmc_summary.py $O/pmc_chol.json $O/chol_fetch $O/chol_write $O/chol_mfma || exit $?
 # C2 eager forward and the C4 qEHVI forward + backward, kernel traces
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c2 -o run -- python3 tools/prof_small.py c2 > $O/c2.log 2>&1 || exit $?
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4 -o run -- python3 tools/c4_qehvi.py 5 > $O/c4.log 2>&1 || exit $?
