@@ -439,7 +439,7 @@ def other_configs(dev, cpu=True):
     Xc = draw_sobol_samples(unit(6), b, q, seed=1)
     Xd = Xc.to(dev)
     with torch.no_grad():
-        t = _gpu_time(lambda: acqf(Xd), steps=5, warmup=1)
+        t = _gpu_time(lambda: acqf(Xd), steps=20, warmup=3)
     lo, hi = part.get_hypercell_bounds()
     e = {"config": "C4 qEHVI ModelListGP(3) DTLZ2 n=2048 d=6 q=8 S=128 b=128",
          "cells": int(lo.shape[0]), "gpu_evals_per_s": q * S * b / t, "gpu_ms": 1e3 * t}
@@ -464,14 +464,14 @@ def other_configs(dev, cpu=True):
     torch.cuda.synchronize()
     init_ms = 1e3 * (time.perf_counter() - t0)
     with torch.no_grad():
-        t = _gpu_time(lambda: acqf(Xd), steps=5, warmup=1)
+        t = _gpu_time(lambda: acqf(Xd), steps=20, warmup=3)
     Xg = Xd.clone().requires_grad_(True)
 
     def fb_nehvi():
         (gx,) = torch.autograd.grad(acqf(Xg).sum(), Xg)
         return gx
 
-    tfb = _gpu_time(fb_nehvi, steps=3, warmup=1)
+    tfb = _gpu_time(fb_nehvi, steps=10, warmup=2)
     out["C4_qNEHVI"] = {"config": "C4 qNEHVI ModelListGP(3) DTLZ2 n=2048 d=6 q=8 S=128 b=128, pruned baseline",
                         "r": int(acqf.X_baseline.shape[0]),
                         "cells_per_sample_max": int(acqf.cell_lower_bounds.shape[1]),
