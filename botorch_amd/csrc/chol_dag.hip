@@ -1313,11 +1313,15 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
   };
   std::vector<std::vector<int>> deps(n);
   std::vector<double> dur(n);
-  // CRIT's weight in the bottom levels: above 1 it lifts the factorisation's
-  // tasks (every path to a diagonal step) over the inverse's XSTEP chains, which
-  // feed no diagonal step (BO_CHOL_CRIT_W; dependants still sort after their
-  // inputs, so the queue stays a topological order)
-  double crit_w = 1.0;
+  // CRIT's weight in the bottom levels (BO_CHOL_CRIT_W): above 1 it lifts the
+  // factorisation's tasks (every path to a diagonal step) over the inverse's
+  // XSTEP chains, which feed no diagonal step -- measured slower (the inverse's
+  // work piles up into the tail: 1.76 -> 1.85-2.35 ms at 2-16); below 1 the
+  // 28 us estimate matches round 3's shorter diagonal step: 0.25 measured
+  // n = 4096 1.769-1.779 -> 1.760-1.762 ms, 3 x 2048 0.866-0.883 -> 0.855-0.859
+  // ms (profiles/r03/cholesky/critw*.log).  Dependants still sort after their
+  // inputs (ties keep the generation order), so the queue stays topological.
+  double crit_w = 0.25;
   if (const char* e = getenv("BO_CHOL_CRIT_W")) crit_w = atof(e);
   for (int t = 0; t < n; ++t) {
     const int type = v[t].x & 0xff, fin = (v[t].x >> 8) & 0xff, k = v[t].y, j = v[t].z;
