@@ -666,7 +666,30 @@ __global__ __launch_bounds__(64) void post_splitk_reduce_kernel(
   v4d acc[8];
 #pragma unroll
   for (int ct = 0; ct < 8; ++ct) acc[ct] = v4d_zero();
-  for (int c = r4.z; c < r4.z + r4.w; ++c) {
+  // two chunks' loads in flight per round, added in k order (the same
+  // additions in the same order as one chunk at a time: C2's longest tiles
+  // have 16 chunks, and each round's loads cost one memory latency)
+  const int cend = r4.z + r4.w;
+  int c = r4.z;
+  for (; c + 1 < cend; c += 2) {
+    const double* w0 = work + ((int64_t)c * (PI / 16) + sub) * kTileDoubles + lane;
+    const double* w1 = w0 + (PI / 16) * kTileDoubles;
+    double v0[32], v1[32];
+#pragma unroll
+    for (int e = 0; e < 32; ++e) {
+      v0[e] = w0[e * 64];
+      v1[e] = w1[e * 64];
+    }
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[ct][r] += v0[ct * 4 + r];
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[ct][r] += v1[ct * 4 + r];
+  }
+  if (c < cend) {
     const double* w = work + ((int64_t)c * (PI / 16) + sub) * kTileDoubles + lane;
 #pragma unroll
     for (int ct = 0; ct < 8; ++ct)
