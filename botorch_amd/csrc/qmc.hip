@@ -23,6 +23,13 @@
 namespace {
 
 constexpr int QMAX = 16;
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), l);
+  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 constexpr int DP = 8;
 constexpr int THREADS = 256;
 
@@ -84,6 +91,7 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   // (S x ldF) the samples' baseline term Z_base T; then
   //   br = Sigma'_qq - T^T T,  f = mu' + F + chol(br) Z_q.
   __shared__ double Sig[QMAX][QMAX + 1];
+  __shared__ double colb[QMAX];  // the Cholesky's current column (wave 0)
   __shared__ double Lq[QMAX][QMAX + 1];
   __shared__ double mu[QMAX];
   __shared__ double red[THREADS / 64];
@@ -184,16 +192,19 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
 #pragma unroll
       for (int j = 0; j < QMAX; ++j) {
         if (j < q) {
-          const double ajj = __shfl(r[j], j);
+          const double ajj = readlane_d(r[j], j);
           if (!(ajj > 0.0) && info == 0) info = j + 1;
           const double djj = sqrt(ajj);
           double lij = (a == j) ? djj : r[j] / djj;
           if (a < j) lij = 0.0;
           r[j] = lij;
+          // column j of L to every lane through LDS (one write, uniform
+          // reads) instead of a ds_bpermute pair per entry: the same values,
+          // the same FMAs (round 3: 300 bpermutes per t-batch at q = 16)
+          if (a < QMAX) colb[a] = lij;
 #pragma unroll
           for (int l = j + 1; l < QMAX; ++l) {
-            const double llj = __shfl(lij, l);
-            r[l] = fma(-lij, llj, r[l]);
+            if (l < q) r[l] = fma(-lij, colb[l], r[l]);
           }
         }
       }
