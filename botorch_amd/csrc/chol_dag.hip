@@ -1381,15 +1381,19 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
   return out;
 }
 
-std::vector<int4> build_tasks(int T) {
+// ch: tile rows per single-step task -- 4 for one matrix, CH (8) for batches:
+// at n = 4096 one matrix ran 1.727-1.733 ms with 4 against 1.753-1.771 with 8
+// and 1.91-1.92 with 16, while 4 x 4096 ran 5.42-5.45 against 5.38 ms
+// (profiles/r03/cholesky/ab_ch.log)
+std::vector<int4> build_tasks(int T, int ch = 4) {
   std::vector<int4> v;
   auto crit = [&](int k) { v.push_back(make_int4(T_CRIT, k, k, 0)); };
   crit(0);
   if (T > 1) crit(1);
   for (int k = 0; k + 1 < T; ++k) {
-    push_rows(v, T_TRSM, k, k, k + 2, T, false);
+    push_rows(v, T_TRSM, k, k, k + 2, T, false, ch);
     // the two chunks CRIT(k + 2) waits on: tiles (k+2, k+1) and (k+2, k+2) at step k
-    const int c1 = (k + 2 + CH < T) ? k + 2 + CH : T;
+    const int c1 = (k + 2 + ch < T) ? k + 2 + ch : T;
     if (k + 2 < T) {
       v.push_back(make_int4(T_COLUPD, k, k + 1, (k + 2) | (c1 << 16)));
       v.push_back(make_int4(T_COLUPD, k, k + 2, (k + 2) | (c1 << 16)));
@@ -1401,7 +1405,7 @@ std::vector<int4> build_tasks(int T) {
     // update of the far rows [ke, T) over all its steps
     for (int j = 0; j <= k; ++j) {
       const int kb = j + ((k - j) / GB) * GB, ke = std::min(kb + GB, T);
-      if (k + 1 < ke) push_rows(v, T_XSTEP, k, j, k + 1, ke, true);
+      if (k + 1 < ke) push_rows(v, T_XSTEP, k, j, k + 1, ke, true, ch);
       else if (k > j) v.push_back(make_int4(T_XSTEP | 256, k, j, 0));
       if (k == ke - 1 && ke < T) {
         const size_t first = v.size();
@@ -1410,8 +1414,8 @@ std::vector<int4> build_tasks(int T) {
       }
     }
     if (k + 2 < T) {
-      push_rows(v, T_COLUPD, k, k + 1, c1, T, false);
-      push_rows(v, T_COLUPD, k, k + 2, c1, T, false);
+      push_rows(v, T_COLUPD, k, k + 1, c1, T, false, ch);
+      push_rows(v, T_COLUPD, k, k + 2, c1, T, false, ch);
     }
     // columns j >= k + 3 at step k: the steps of an aligned batch [kb, kb + GB)
     // that lies wholly at or below j - 3 go in one batched task at the batch's
@@ -1425,7 +1429,7 @@ std::vector<int4> build_tasks(int T) {
           for (size_t t = first; t < v.size(); ++t) v[t].x |= GB << 16;
         }
       } else {
-        push_rows(v, T_COLUPD, k, j, j, T, false);
+        push_rows(v, T_COLUPD, k, j, j, T, false, ch);
       }
     }
   }
@@ -1442,7 +1446,7 @@ std::vector<int4> build_tasks(int T) {
 // matrix's chain-bound tail overlaps the next one's update-heavy opening
 // instead of all matrices opening together.
 std::vector<int4> build_tasks_batched(int T, int nb) {
-  const std::vector<int4> one = build_tasks(T);
+  const std::vector<int4> one = build_tasks(T, nb == 1 ? 4 : CH);
   if (nb == 1) return one;
   double stagger = 0.0;
   if (const char* e = getenv("BO_CHOL_BATCH_STAGGER")) stagger = atof(e);
