@@ -48,10 +48,10 @@ namespace {
 
 constexpr int TB = 64;  // tile
 constexpr int LP = 68;  // LDS pitch in doubles (rows 16-B aligned)
-constexpr int CH = 8;   // tile rows per chunked task
+constexpr int CH = 8;   // tile rows per chunked task of a multi-matrix launch (one matrix: 4)
 constexpr int NFLAG0 = 16;  // head counter, abort word, padding
 constexpr int GB = 3;       // steps per batched column update (LDS: X0 + GB operand tiles)
-constexpr int CHB = 8;      // tile rows per batched task (4 measured slower: 2.11 vs 2.00 ms)
+constexpr int CHB = 8;      // tile rows per batched task of a multi-matrix launch (one matrix: 4, build_tasks)
 constexpr long long SPIN_TIMEOUT = 200000000;  // wall-clock ticks (100 MHz): 2 s
 
 enum : int { T_CRIT = 0, T_TRSM = 1, T_COLUPD = 2, T_XSTEP = 3 };
@@ -1381,11 +1381,13 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
   return out;
 }
 
-// ch: tile rows per single-step task -- 4 for one matrix, CH (8) for batches:
-// at n = 4096 one matrix ran 1.727-1.733 ms with 4 against 1.753-1.771 with 8
-// and 1.91-1.92 with 16, while 4 x 4096 ran 5.42-5.45 against 5.38 ms
-// (profiles/r03/cholesky/ab_ch.log)
-std::vector<int4> build_tasks(int T, int ch = 4) {
+// ch / chb: tile rows per single-step / batched task -- 4 / 4 for one matrix,
+// CH / CHB (8 / 8) for batches: at n = 4096 one matrix ran 1.727-1.733 ms with
+// ch 4 against 1.753-1.771 with 8 and 1.91-1.92 with 16, while 4 x 4096 ran
+// 5.42-5.45 against 5.38 ms (profiles/r03/cholesky/ab_ch.log); chb 4 then
+// 1.709-1.718 against 1.721-1.744 ms for one matrix, but 3 x 2048 0.90 against
+// 0.85 ms (ab_chb.log)
+std::vector<int4> build_tasks(int T, int ch = 4, int chb = 4) {
   std::vector<int4> v;
   auto crit = [&](int k) { v.push_back(make_int4(T_CRIT, k, k, 0)); };
   crit(0);
@@ -1409,7 +1411,7 @@ std::vector<int4> build_tasks(int T, int ch = 4) {
       else if (k > j) v.push_back(make_int4(T_XSTEP | 256, k, j, 0));
       if (k == ke - 1 && ke < T) {
         const size_t first = v.size();
-        push_rows(v, T_XSTEP, kb, j, ke, T, false, CHB);
+        push_rows(v, T_XSTEP, kb, j, ke, T, false, chb);
         for (size_t t = first; t < v.size(); ++t) v[t].x |= (ke - kb) << 16;
       }
     }
@@ -1425,7 +1427,7 @@ std::vector<int4> build_tasks(int T, int ch = 4) {
       if (GB > 1 && kb + GB - 1 <= j - 3) {
         if (k == kb + GB - 1) {
           const size_t first = v.size();
-          push_rows(v, T_COLUPD, kb, j, j, T, false, CHB);
+          push_rows(v, T_COLUPD, kb, j, j, T, false, chb);
           for (size_t t = first; t < v.size(); ++t) v[t].x |= GB << 16;
         }
       } else {
@@ -1446,7 +1448,7 @@ std::vector<int4> build_tasks(int T, int ch = 4) {
 // matrix's chain-bound tail overlaps the next one's update-heavy opening
 // instead of all matrices opening together.
 std::vector<int4> build_tasks_batched(int T, int nb) {
-  const std::vector<int4> one = build_tasks(T, nb == 1 ? 4 : CH);
+  const std::vector<int4> one = nb == 1 ? build_tasks(T, 4, 4) : build_tasks(T, CH, CHB);
   if (nb == 1) return one;
   double stagger = 0.0;
   if (const char* e = getenv("BO_CHOL_BATCH_STAGGER")) stagger = atof(e);
