@@ -48,7 +48,7 @@ namespace {
 
 constexpr int TB = 64;  // tile
 constexpr int LP = 68;  // LDS pitch in doubles (rows 16-B aligned)
-constexpr int CH = 8;   // tile rows per chunked task of a multi-matrix launch (one matrix: 4)
+constexpr int CH = 8;   // tile rows per chunked task of a multi-matrix launch (one matrix: 2)
 constexpr int NFLAG0 = 16;  // head counter, abort word, padding
 constexpr int GB = 3;       // steps per batched column update (LDS: X0 + GB operand tiles)
 constexpr int CHB = 8;      // tile rows per batched task of a multi-matrix launch (one matrix: 4, build_tasks)
@@ -1381,13 +1381,14 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
   return out;
 }
 
-// ch / chb: tile rows per single-step / batched task -- 4 / 4 for one matrix,
+// ch / chb: tile rows per single-step / batched task -- 2 / 4 for one matrix,
 // CH / CHB (8 / 8) for batches: at n = 4096 one matrix ran 1.727-1.733 ms with
 // ch 4 against 1.753-1.771 with 8 and 1.91-1.92 with 16, while 4 x 4096 ran
 // 5.42-5.45 against 5.38 ms (profiles/r03/cholesky/ab_ch.log); chb 4 then
 // 1.709-1.718 against 1.721-1.744 ms for one matrix, but 3 x 2048 0.90 against
-// 0.85 ms (ab_chb.log)
-std::vector<int4> build_tasks(int T, int ch = 4, int chb = 4) {
+// 0.85 ms (ab_chb.log); ch 2 then 1.650-1.684 against 1.684-1.733 ms with 4
+// (1: 1.70-1.72, 3: 1.70-1.72; ab_ch23.log, ab_ch21.log): one matrix takes 2 / 4
+std::vector<int4> build_tasks(int T, int ch = 2, int chb = 4) {
   std::vector<int4> v;
   auto crit = [&](int k) { v.push_back(make_int4(T_CRIT, k, k, 0)); };
   crit(0);
@@ -1448,7 +1449,7 @@ std::vector<int4> build_tasks(int T, int ch = 4, int chb = 4) {
 // matrix's chain-bound tail overlaps the next one's update-heavy opening
 // instead of all matrices opening together.
 std::vector<int4> build_tasks_batched(int T, int nb) {
-  const std::vector<int4> one = nb == 1 ? build_tasks(T, 4, 4) : build_tasks(T, CH, CHB);
+  const std::vector<int4> one = nb == 1 ? build_tasks(T, 2, 4) : build_tasks(T, CH, CHB);
   if (nb == 1) return one;
   double stagger = 0.0;
   if (const char* e = getenv("BO_CHOL_BATCH_STAGGER")) stagger = atof(e);
