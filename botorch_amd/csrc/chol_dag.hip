@@ -1449,7 +1449,10 @@ std::vector<int4> build_tasks(int T, int ch = 2, int chb = 4) {
 // matrix's chain-bound tail overlaps the next one's update-heavy opening
 // instead of all matrices opening together.
 std::vector<int4> build_tasks_batched(int T, int nb) {
-  const std::vector<int4> one = nb == 1 ? build_tasks(T, 2, 4) : build_tasks(T, CH, CHB);
+  // one matrix, or batches of small ones (n <= 2048: C4's 3 x 2048 0.855-0.867
+  // -> 0.797-0.805 ms), take 2 / 4 rows; batches of n = 4096 keep 8 / 8 (with
+  // 2 / 4: 4 x 4096 5.38 -> 5.69 ms; profiles/r03/cholesky/ab_ch_batched_small.log)
+  const std::vector<int4> one = (nb == 1 || T <= 32) ? build_tasks(T, 2, 4) : build_tasks(T, CH, CHB);
   if (nb == 1) return one;
   double stagger = 0.0;
   if (const char* e = getenv("BO_CHOL_BATCH_STAGGER")) stagger = atof(e);
