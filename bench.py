@@ -11,17 +11,18 @@ jittered q x q Cholesky, reparameterised sampling and the MC reduction
 (Cholesky, L^{-T}) are built once before timing, as the reference builds them
 on the first eval-mode call.
 
-Multi-GPU: one process per GPU (torchrun).  Default (weak scaling): each rank
-evaluates its own 512 restarts, no data-path collective, and the step ends
-with one all-reduce(MAX) of the best acquisition value (the argmax/gather of
-optimize_acqf, botorch/optim/optimize.py:384-387).  ``--strong``: the 512
+Multi-GPU: one process per GPU (torchrun; ``--gpus N`` without torchrun's
+environment starts the ranks itself).  N > 1 default (strong scaling): the 512
 restarts of ONE global candidate draw are sharded over the ranks
 (distributed.shard_range, north_star's "512 restarts sharded over 8 GPUs"),
 and the step ends with the values gathered by one all-reduce of a zeroed
-512-entry buffer (distributed.allgather_rows) and the global argmax.  On one
-GPU the line also carries the projected strong-scaling curve: the same step at
-b = 512/W restarts for W = 2, 4, 8 (a projection from single-GPU timings,
-collectives excluded).
+512-entry buffer (distributed.allgather_rows) and the global argmax (the
+argmax/gather of optimize_acqf, botorch/optim/optimize.py:384-387).
+``--weak``: each rank evaluates its own 512 restarts, no data-path
+collective, one all-reduce(MAX) of the best value per step.  N = 1 is labelled
+"single".  On one GPU the line also carries the projected strong-scaling
+curve: the same step at b = 512/W restarts for W = 2, 4, 8 (a projection from
+single-GPU timings, collectives excluded).
 
 Prints ONE JSON line (rank 0).
 """
@@ -69,20 +70,46 @@ def post_partials_bytes(B, q, n):
     return 8 * (B * q * n + n * n // 2 + (n // 128) * (B * 256 + B * q))
 
 
-def pmc_traffic(kernel="post_partials_kernel<0, 6, false, false, true, false>"):
-    """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 PMC
-    summary (profiles/rNN/pmc_summary.json, written by tools/pmc_summary.py from
-    separate --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command,
-    FETCH_SIZE doubled per the gfx950 correction).  None if absent."""
+def _pmc_rank(path):
+    """Sort key of a PMC summary: its round (profiles/rNN/...), then its own
+    creation stamp (tools/pmc_summary.py writes ``_meta.created``), then the
+    path -- so the newest round's newest summary wins at any depth."""
+    import re
+    rel = os.path.relpath(path, os.path.join(ROOT, "profiles"))
+    m = re.match(r"r(\d+)", rel)
+    try:
+        created = float(json.load(open(path)).get("_meta", {}).get("created", 0.0))
+    except Exception:
+        created = 0.0
+    return (int(m.group(1)) if m else -1, created, rel)
+
+
+def pmc_traffic(restarts, kernel="post_partials_kernel<0, 6, false, false, true, false>"):
+    """HBM bytes per launch of ``kernel`` at ``restarts`` t-batches, from the
+    newest committed rocprofv3 PMC summary under profiles/ at any depth
+    (``BO_PMC_SUMMARY`` names one explicitly), written by tools/pmc_summary.py
+    from separate --pmc FETCH_SIZE / WRITE_SIZE passes of the bench command,
+    FETCH_SIZE doubled per the gfx950 correction.  A summary collected at a
+    different restart count (``_meta.restarts``; 512 when absent) is scaled by
+    restarts / its count and says so.  (None, None, None) if absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")))
+    env = os.environ.get("BO_PMC_SUMMARY")
+    files = ([env] if env else
+             glob.glob(os.path.join(ROOT, "profiles", "r*", "**", "pmc_summary.json"), recursive=True))
     if not files:
-        return None, None
-    summ = json.load(open(files[-1]))
+        return None, None, None
+    path = max(files, key=_pmc_rank)
+    summ = json.load(open(path))
     # the template argument list grows between rounds: match the named prefix
     keys = [k for k in summ if k == kernel or k.startswith(kernel.rstrip(">") + ",")]
     e = summ[keys[0]] if keys else {}
-    return e.get("hbm_bytes"), os.path.relpath(files[-1], ROOT)
+    hbm = e.get("hbm_bytes")
+    at = int(summ.get("_meta", {}).get("restarts", RESTARTS))
+    note = None
+    if hbm is not None and at != restarts:
+        hbm = hbm * restarts / at
+        note = f"scaled from the PMC pass at {at} restarts to {restarts}"
+    return hbm, os.path.relpath(path, ROOT), note
 
 
 def mfma_f64_ceiling(dev):
@@ -700,7 +727,7 @@ def rehearse_cpu(args, ws, rank):
                           "value": None, "unit": "acq-evals/s", "n_gpus": ws,
                           "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": 1e3 * elapsed / args.steps,
-                          "scaling": "strong" if strong else "weak",
+                          "scaling": "single" if ws == 1 else ("strong" if strong else "weak"),
                           "rehearsal": "cpu stub: launch, split and collectives only",
                           "config": {"restarts_per_gpu": r1 - r0,
                                      "parallelism": f"restart-sharded x{ws}"}}), flush=True)
@@ -730,6 +757,36 @@ def verify_step(acqf, Xd, r0, Xtr, Ytr, Xc_local, best_f, k=8):
                          f"{got} vs {ref}")
     return {"t_batches": [int(r0 + i) for i in idx], "nonzero": int(pos.sum()),
             "max_rel_err_nonzero": err, "rtol": 1e-7, "atol": 1e-12}
+
+
+def verify_grad(acqf, Xd, r0, Xtr, Ytr, Xc_local, best_f, k=8):
+    """Outside the timed region, on rank 0: dX of the timed forward + backward
+    (the fused W = R L^-1 -> dX pass at this size, asserted) at k t-batches
+    spread over those with a non-zero value, against torch.autograd through the
+    CPU restatement (oracle/, the checker) on those t-batches, rtol 1e-5."""
+    from oracle.acquisition import qei
+    from oracle.gp import ExactGPOracle, GPHyper
+    from oracle.sampling import draw_sobol_normal_samples
+    Xg = Xd.detach().clone().requires_grad_(True)
+    v = acqf(Xg)
+    (g,) = torch.autograd.grad(v.sum(), Xg)
+    route = int(torch.ops.bo.last_backward_route())
+    v, g = v.detach().cpu(), g.cpu()
+    nz = (v > 0).nonzero().flatten()
+    if nz.numel() < k:
+        raise SystemExit(f"bench: only {nz.numel()} non-zero values to check gradients on")
+    idx = nz[torch.linspace(0, nz.numel() - 1, k).round().long()]
+    h = GPHyper(torch.full((D,), LENGTHSCALE, dtype=torch.float64), NOISE, CONSTANT)
+    Xo = Xc_local[idx].clone().requires_grad_(True)
+    ref = qei(ExactGPOracle(Xtr, Ytr, h), Xo, draw_sobol_normal_samples(Q, MC, 0), best_f)
+    (go,) = torch.autograd.grad(ref.sum(), Xo)
+    err = ((g[idx] - go).abs() / go.abs().clamp_min(1e-8)).max().item()
+    ok = bool(torch.allclose(g[idx], go, rtol=1e-5, atol=1e-8))
+    if not ok or route != 1:
+        raise SystemExit(f"bench: the timed gradient disagrees with the oracle (route {route}): "
+                         f"max rel err {err}")
+    return {"t_batches": [int(r0 + i) for i in idx], "route": "fused W -> dX (bo_post_w_dx)",
+            "max_rel_err": err, "rtol": 1e-5, "atol": 1e-8}
 
 
 def main():
@@ -841,7 +898,7 @@ def main():
     achieved = fl / (kern_avg_ms * 1e-3) / 1e12
     peak = 78.6  # MI355X dense FP64 matrix TFLOP/s (MI355X_MICROARCH.md / SURVEY.md 8(d))
     peak_box = mfma_f64_ceiling(dev)
-    traffic, traffic_src = pmc_traffic()
+    traffic, traffic_src, traffic_note = pmc_traffic(r1 - r0)
     alg_bytes = post_partials_bytes(r1 - r0, Q, N_TRAIN)
 
     weak = None
@@ -903,6 +960,8 @@ def main():
         if not args.no_cpu_baseline:
             # the CPU leg: the oracle checks the timed forward, then (N = 1) is timed
             check = verify_step(acqf, Xd, r0, Xtr, Ytr, Xc, best_f)
+            if fwd_bwd is not None:
+                fwd_bwd["check"] = verify_grad(acqf, Xd, r0, Xtr, Ytr, Xc, best_f)
             if ws == 1:
                 cpu = cpu_baseline(Xtr, Ytr, Xc, best_f)
         line = {
@@ -914,7 +973,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "strong" if strong else "weak",
+            "scaling": "single" if ws == 1 else ("strong" if strong else "weak"),
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: Hartmann6 on Sobol(seed 0) training inputs, "
@@ -934,6 +993,7 @@ def main():
                          "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "algorithmic_bytes": alg_bytes,
                          "traffic_ratio": traffic / alg_bytes if traffic else None,
+                         "traffic_note": traffic_note,
                          "kernel_ms": kern_avg_ms, "flops_per_launch": fl},
             "cpu_baseline": cpu,
             "check": check,

@@ -1217,18 +1217,32 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
         return acq.reshape(batch) + self._prev_nehvi.to(acq)
 
 
+def _acq_device(acqf) -> Optional[torch.device]:
+    """The device an acquisition's model lives on (its training inputs, or a
+    ModelListGP member's), None when it has none."""
+    model = getattr(acqf, "model", None)
+    for m in [model] + list(getattr(model, "models", None) or []):
+        ti = getattr(m, "train_inputs", None) if m is not None else None
+        if ti:
+            return ti[0].device
+    return None
+
+
 class FixedFeatureAcquisitionFunction(AcquisitionFunction):
     """acquisition/fixed_feature.py:54-200: the base acquisition over the full
     d-dim input, evaluated on X of dim d' = d - d_f with the ``columns`` filled
     from ``values``.  The optimisers use it to drop fixed features from the
-    search space (generation/utils.py:102-196).  Filling the columns is one
-    concatenation and one column gather on the device, so the fused forward of
-    the base acquisition (and its HIP-graph capture) is unchanged."""
+    search space (generation/utils.py:102-196).  The fixed values live on the
+    base acquisition's device from construction, and filling the columns is one
+    concatenation and one index_select with a device index, so no host data
+    moves per call and the fused forward of the base acquisition (and its
+    HIP-graph capture) is unchanged."""
 
     def __init__(self, acq_function: AcquisitionFunction, d: int, columns: List[int], values):
         nn.Module.__init__(self)
         self.acq_func = acq_function
         self.d = d
+        home = _acq_device(acq_function)
         if torch.is_tensor(values):
             vals = values.detach().clone()
         else:
@@ -1236,13 +1250,15 @@ class FixedFeatureAcquisitionFunction(AcquisitionFunction):
             single = all(torch.is_tensor(v) and v.dtype == torch.float32 for v in values)
             dtype = torch.float32 if single else torch.float64
             dev = next((v.device for v in values if torch.is_tensor(v) and v.is_cuda),
-                       torch.device("cpu"))
+                       home or torch.device("cpu"))
             parts = []
             for v in values:
                 t = torch.tensor([float(v)], dtype=dtype) if not torch.is_tensor(v) else (
                     v.detach().clone().reshape(1) if v.ndim == 0 else v.detach().clone())
                 parts.append(t.to(dtype=dtype, device=dev))
             vals = torch.cat(torch.broadcast_tensors(*parts), dim=-1)
+        if home is not None:
+            vals = vals.to(home)
         self.register_buffer("values", vals)
         # column i of X_full: from X (free) or from the appended values (fixed)
         d_f = vals.shape[-1]
@@ -1250,6 +1266,7 @@ class FixedFeatureAcquisitionFunction(AcquisitionFunction):
         free = iter(range(d - d_f))
         fixed = iter(range(d - d_f, d))
         self._selector = [next(fixed) if i in cols else next(free) for i in range(d)]
+        self._placed = {}  # (device, dtype) -> (values, device index of the selector)
 
     @property
     def model(self):
@@ -1274,13 +1291,26 @@ class FixedFeatureAcquisitionFunction(AcquisitionFunction):
         self.acq_func.set_X_pending(self._construct_X_full(X_pending) if X_pending is not None
                                     else None)
 
+    def _on(self, X: torch.Tensor):
+        """The values and the column selector on X's device and dtype (placed
+        once per device / dtype: a call under stream capture copies nothing)."""
+        key = (X.device, X.dtype)
+        hit = self._placed.get(key)
+        if hit is None or hit[2] is not self.values:  # rebuilt if values was replaced
+            vals = self.values.to(device=X.device, dtype=X.dtype)
+            sel = torch.tensor(self._selector, dtype=torch.long, device=X.device)
+            hit = (vals, sel, self.values)
+            self._placed[key] = hit
+        return hit[0], hit[1]
+
     def _construct_X_full(self, X: torch.Tensor) -> torch.Tensor:
         d_prime, d_f = X.shape[-1], self.values.shape[-1]
         if d_prime + d_f != self.d:
             raise ValueError(f"Feature dimension d' ({d_prime}) of input must be "
                              f"d - d_f ({self.d - d_f}).")
-        vals = self.values.to(X).expand(*X.shape[:-1], d_f)
-        return torch.cat([X, vals], dim=-1)[..., self._selector]
+        vals, sel = self._on(X)
+        vals = vals.expand(*X.shape[:-1], d_f)
+        return torch.cat([X, vals], dim=-1).index_select(-1, sel)
 
     def forward(self, X: torch.Tensor) -> torch.Tensor:
         return self.acq_func(self._construct_X_full(X))

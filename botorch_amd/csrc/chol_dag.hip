@@ -35,6 +35,7 @@
 // agent-scope (sc1) load and read the tiles with sc1 loads only (L1 bypassed),
 // one workgroup per CU.
 #include <algorithm>
+#include <cmath>
 #include <map>
 #include <utility>
 #include <mutex>
@@ -1321,8 +1322,15 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
   // n = 4096 1.769-1.779 -> 1.760-1.762 ms, 3 x 2048 0.866-0.883 -> 0.855-0.859
   // ms (profiles/r03/cholesky/critw*.log).  Dependants still sort after their
   // inputs (ties keep the generation order), so the queue stays topological.
+  // Only finite weights >= 0 are taken: a negative one would give CRIT a
+  // negative duration, sort dependants ahead of their inputs and leave the
+  // persistent launch spinning until its timeout.
   double crit_w = 0.25;
-  if (const char* e = getenv("BO_CHOL_CRIT_W")) crit_w = atof(e);
+  if (const char* e = getenv("BO_CHOL_CRIT_W")) {
+    char* end = nullptr;
+    const double w = strtod(e, &end);
+    if (end != e && std::isfinite(w) && w >= 0.0) crit_w = w;
+  }
   for (int t = 0; t < n; ++t) {
     const int type = v[t].x & 0xff, fin = (v[t].x >> 8) & 0xff, k = v[t].y, j = v[t].z;
     const int nk = std::max(1, v[t].x >> 16);
@@ -1376,6 +1384,13 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
   std::vector<int> idx(n);
   for (int t = 0; t < n; ++t) idx[t] = t;
   std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return bl[a] > bl[b]; });
+  // the queue must stay topological (a task waits only on tasks claimed
+  // before it): check it, and keep the generation order if it is not
+  std::vector<int> pos(n);
+  for (int t = 0; t < n; ++t) pos[idx[t]] = t;
+  for (int t = 0; t < n; ++t)
+    for (int dd : deps[t])
+      if (dd >= 0 && pos[dd] > pos[t]) return v;
   std::vector<int4> out(n);
   for (int t = 0; t < n; ++t) out[t] = v[idx[t]];
   return out;

@@ -23,6 +23,7 @@
 #include <torch/library.h>
 
 #include <array>
+#include <atomic>
 #include <mutex>
 #include <unordered_map>
 #include <utility>
@@ -206,6 +207,7 @@ std::vector<at::Tensor> qmc_acq_impl(
   at::Tensor Xq_t = own_xq ? at::empty({nrows, 8}, f64) : at::Tensor();
   double* Xq = own_xq ? Xq_t.data_ptr<double>() : w + o_xq;
   at::Tensor Rt = need_grad ? at::empty({int64_t(nC) * 128, nrows}, f64) : at::Tensor();
+  int rt_layout = BO_RT_ROWMAJOR;
 
   if (kxt) {  // rows and K*x^T in one launch
     ck(bo_post_kxt_rows(int(kind), X.data_ptr<double>(), B, q, d, lengthscale.data_ptr<double>(),
@@ -248,7 +250,8 @@ std::vector<at::Tensor> qmc_acq_impl(
       // pass applies (bo_post_w_dx), row-major everywhere else
       int64_t wdx = 0;
       ck(bo_post_w_dx_work(B, q, n, &wdx), "post_w_dx_work");
-      pa.rt_layout = (wdx > 0 && kc == 0) ? BO_RT_BLOCKED : BO_RT_ROWMAJOR;
+      rt_layout = (wdx > 0 && kc == 0) ? BO_RT_BLOCKED : BO_RT_ROWMAJOR;
+      pa.rt_layout = rt_layout;
     }
     ck(bo_post_partials_v(&pa, st), "post_partials");
   }
@@ -326,7 +329,10 @@ std::vector<at::Tensor> qmc_acq_impl(
           need_grad ? mean : empty(),
           need_grad ? L : empty(),
           need_grad ? Xq_t : empty(),
-          need_grad ? Rt : empty(),
+          // the layout travels with the tensor: a blocked R^T is returned as
+          // [column blocks][row blocks][256], a row-major one as [columns][rows]
+          need_grad ? (rt_layout == BO_RT_BLOCKED ? Rt.view({int64_t(nC) * 8, nrows / 16, 256}) : Rt)
+                    : empty(),
           empty(),
           jit,
           info,
@@ -357,6 +363,14 @@ std::vector<at::Tensor> qmc_acq_eager(
                       outputscale, constant, ymean, ystd, best_f, fat, tau_relu, tau_max, false,
                       kxt_cap, true, Ainv, alpha, true);
 }
+
+// The posterior-backward route the last qmc_acq_backward_native call took
+// (bo::last_backward_route; tests assert the config-size gradient goes
+// through the fused pass).
+enum { BO_ROUTE_NONE = 0, BO_ROUTE_W_DX = 1, BO_ROUTE_W_SPLIT = 2, BO_ROUTE_W_GEMM = 3 };
+std::atomic<int> g_last_route{BO_ROUTE_NONE};
+
+int64_t last_backward_route() { return g_last_route.load(); }
 
 // dX of qmc_acq_native (the registered autograd formula of bo::qmc_acq): the
 // reduction + sampling + q x q Cholesky backward (bo_qmc_backward), then the
@@ -405,9 +419,18 @@ at::Tensor qmc_acq_backward_native(
   qa.tau_max = tau_max;
   ck(bo_qmc_backward_v(&qa, st), "qmc_backward");
 
+  // R^T's layout is the forward's decision, carried by its shape: blocked
+  // (3-d) R^T is read only by the fused W -> dX pass, row-major (2-d) R^T
+  // only by the W^T routes below
+  const bool rt_blocked = Rt.dim() == 3;
+  TORCH_CHECK(Rt.dim() == 2 || rt_blocked, "bo::qmc_acq_backward_native: R^T must be 2-d or blocked 3-d");
   int64_t wdx = 0;
   ck(bo_post_w_dx_work(B, q, n, &wdx), "post_w_dx_work");
-  if (wdx > 0) {
+  TORCH_CHECK(!rt_blocked || wdx > 0,
+              "bo::qmc_acq_backward_native: blocked R^T but the fused W -> dX grid does not apply "
+              "to (B, q, n) = (", B, ", ", q, ", ", n, ")");
+  if (rt_blocked) {
+    g_last_route.store(BO_ROUTE_W_DX);
     auto work = at::empty({wdx}, f64);
     ck(bo_post_w_dx(int(kind), Linv.data_ptr<double>(), np, Rt.data_ptr<double>(), B, q, int(d), n,
                     Xq.data_ptr<double>(), Xt_scaled.data_ptr<double>(), alpha.data_ptr<double>(),
@@ -423,6 +446,7 @@ at::Tensor qmc_acq_backward_native(
   ck(bo_post_w_work(B, q, n, &wkc, &wwe), "post_w_work");
   at::Tensor W;
   bool kmajor = true;
+  g_last_route.store(wkc == -1 ? BO_ROUTE_W_SPLIT : BO_ROUTE_W_GEMM);
   if (wkc == -1) {
     W = at::empty({np, nrows}, f64);
     auto ww = at::empty({std::max<int64_t>(wwe, 1)}, f64);
@@ -520,6 +544,7 @@ TORCH_LIBRARY_FRAGMENT(bo, m) {
   m.def("ladder_poll(int device) -> Tensor", &ladder_poll);
   m.def("post_timing(bool on) -> ()", &post_timing);
   m.def("post_timing_read() -> Tensor", &post_timing_read);
+  m.def("last_backward_route() -> int", &last_backward_route);
 }
 
 TORCH_LIBRARY_IMPL(bo, CUDA, m) {

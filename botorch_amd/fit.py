@@ -374,6 +374,9 @@ def fit_gpytorch_mll_scipy(mll: ExactMarginalLogLikelihood, parameters=None, bou
 
         def wrapped(x):
             step[0] += 1
+            # the iterate goes into the model first (the reference's closure
+            # writes its state into the parameters before the callback runs)
+            layout.set(x)
             res = OptimizationResult(step=step[0], fval=float(layout.value_and_grad(x)[0]),
                                      status=OptimizationStatus.RUNNING,
                                      runtime=time.monotonic() - t0)

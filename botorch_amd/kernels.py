@@ -366,7 +366,9 @@ class PostPartials:
     Xq: torch.Tensor
     Spart: torch.Tensor
     mpart: torch.Tensor
-    Rt: Optional[torch.Tensor] = None  # R^T (nC*128 x nrows_pad) on the gradient path
+    # R^T on the gradient path: nC*128 x nrows_pad row-major, or blocked
+    # (nC*8 x nrows_pad/16 x 256, rt_layout=RT_BLOCKED) for the fused W -> dX pass
+    Rt: Optional[torch.Tensor] = None
     Cx: Optional[torch.Tensor] = None  # cross K*x^T (rq x nrows_pad), fused cross term
 
 
@@ -421,6 +423,16 @@ def split_plan(B: int, q: int, n: int, slots: int = 0):
     check(lib().bo_post_split_plan(B, q, n, slots, ctypes.byref(kc), ctypes.byref(we)),
           "post_split_plan")
     return kc.value, we.value
+
+
+@functools.lru_cache(maxsize=256)
+def rt_blocked_plan(B: int, q: int, n: int) -> bool:
+    """Whether the fused forward (bo::qmc_acq_native) stores R^T blocked for
+    (B, q, n): the one-pass grid of the fused W -> dX backward.  Shape metadata
+    only (the op's fake): the real layout travels with the tensor's shape."""
+    we = ctypes.c_int64()
+    check(lib().bo_post_w_dx_work(B, q, n, ctypes.byref(we)), "post_w_dx_work")
+    return we.value > 0 and split_plan(B, q, n)[0] == 0
 
 
 def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
@@ -485,6 +497,8 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
     check(lib().bo_post_partials_v(ctypes.byref(a), st), "post_partials")
     if TIMING_HOOK is not None:
         TIMING_HOOK("post_partials_end")
+    if Rt is not None and rt_layout == _lib.RT_BLOCKED:
+        Rt = Rt.view(nC * 8, nrows_pad // 16, 256)  # the layout travels with the shape
     return PostPartials(B, q, Qp, nrows_pad, nC, Xq, Spart, mpart, Rt,
                         Cx.sum(dim=0) if Cx is not None else None)
 
@@ -578,6 +592,8 @@ def w_matrix(cache: GPCache, pp: PostPartials, post_w: Optional[bool] = None) ->
     above, True = bo_post_w whenever the grid allows it, False = the GEMM."""
     if pp.Rt is None:
         raise RuntimeError("post_partials(store_R=True) is required for gradients")
+    if pp.Rt.dim() != 2:
+        raise ValueError("w_matrix reads the row-major R^T; this one is blocked (use post_w_dx)")
     dev = pp.Rt.device
     nI = pp.nrows_pad // 128
     kc, we = ctypes.c_int(), ctypes.c_int64()
@@ -608,13 +624,15 @@ def post_w_dx(cache: GPCache, pp: PostPartials, dmean: torch.Tensor, dcov: torch
               ystd: float) -> Optional[torch.Tensor]:
     """dX of the posterior moments' cotangents with W = R L^{-1} reduced into
     dX tile by tile (bo_post_w_dx; W never stored); None where the one-pass
-    grid does not apply (then w_matrix + post_backward)."""
+    grid does not apply or R^T was stored row-major (then w_matrix +
+    post_backward): the fused pass reads only the blocked R^T
+    (post_partials(rt_layout=RT_BLOCKED), 3-d)."""
     if pp.Rt is None:
         raise RuntimeError("post_partials(store_R=True) is required for gradients")
     dev = pp.Rt.device
     we = ctypes.c_int64()
     check(lib().bo_post_w_dx_work(pp.B, pp.q, cache.n, ctypes.byref(we)), "post_w_dx_work")
-    if we.value == 0:
+    if we.value == 0 or pp.Rt.dim() != 3:
         return None
     work = torch.empty(we.value, dtype=torch.float64, device=dev)
     dX = torch.empty(pp.B, pp.q, cache.d, dtype=torch.float64, device=dev)

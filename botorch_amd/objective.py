@@ -128,59 +128,86 @@ def repeat_to_match_aug_dim(target_tensor: torch.Tensor, reference_tensor: torch
 
 
 # -- outcome constraints --------------------------------------------------------------
+# The reference's helpers (utils/objective.py:101-180, acquisition/utils.py:
+# 90-242) are restated here around one primitive: every constraint evaluated
+# once on the samples and stacked on a leading constraint axis.  Hard
+# feasibility, the smoothed (log-)indicator and the best feasible objective
+# are reductions over that axis.  Pinned by tests/test_objective_cpu.py
+# against the reference's own outputs (golden.npz ``feas_*``).
+def _constraint_stack(constraints: List[Callable], samples: torch.Tensor) -> torch.Tensor:
+    """c x samples.shape[:-1]: constraint i's values in row i (<= 0 feasible)."""
+    shape = samples.shape[:-1]
+    return torch.stack([torch.as_tensor(c(samples)).to(samples.device).expand(shape)
+                        for c in constraints])
+
+
+def _majority(ind: torch.Tensor, dim: int) -> torch.Tensor:
+    """Feasible in at least half of the entries along ``dim`` (rounded mean).
+    A negative ``dim`` counts from the first batch dimension, as the
+    reference's ``1 + (dim % ndim)`` does."""
+    if dim < 0:
+        dim = dim % ind.ndim + 1
+    return ind.to(torch.float32).mean(dim=dim).round().to(torch.bool)
+
+
 def compute_feasibility_indicator(constraints: Optional[List[Callable]], samples: torch.Tensor,
                                   marginalize_dim: Optional[int] = None) -> torch.Tensor:
-    """utils/objective.py:101-131: Boolean feasibility (all constraints <= 0)."""
-    ind = torch.ones(samples.shape[:-1], dtype=torch.bool, device=samples.device)
-    if constraints is not None:
-        for constraint in constraints:
-            ind = ind.logical_and(constraint(samples) <= 0)
-    if ind.ndim >= 3 and marginalize_dim is not None:
-        if marginalize_dim < 0:
-            marginalize_dim = 1 + (marginalize_dim % ind.ndim)
-        ind = ind.float().mean(dim=marginalize_dim).round().bool()
+    """utils/objective.py:101-131: True where every constraint is <= 0 (all
+    True without constraints); with ``marginalize_dim`` (3+-dim indicators)
+    the majority vote along it."""
+    if constraints:
+        ind = (_constraint_stack(constraints, samples) <= 0).all(dim=0)
+    else:
+        ind = torch.ones(samples.shape[:-1], dtype=torch.bool, device=samples.device)
+    if marginalize_dim is not None and ind.ndim >= 3:
+        ind = _majority(ind, marginalize_dim)
     return ind
+
+
+def _as_etas(eta: Union[torch.Tensor, float], count: int) -> torch.Tensor:
+    etas = eta if torch.is_tensor(eta) else torch.full((count,), float(eta))
+    if len(etas) != count:
+        raise ValueError("Number of provided constraints and number of provided etas do not match.")
+    if not bool((etas > 0).all()):
+        raise ValueError("eta must be positive.")
+    return etas
 
 
 def compute_smoothed_feasibility_indicator(constraints: List[Callable], samples: torch.Tensor,
                                            eta: Union[torch.Tensor, float], log: bool = False,
                                            fat: bool = False) -> torch.Tensor:
-    """utils/objective.py:134-180: prod_i sigmoid(-c_i(samples) / eta_i) (or its
-    log, or the fat-tailed fatmoid form)."""
-    if type(eta) is not torch.Tensor:
-        eta = torch.full((len(constraints),), eta)
-    if len(eta) != len(constraints):
-        raise ValueError("Number of provided constraints and number of provided etas do not match.")
-    if not (eta > 0).all():
-        raise ValueError("eta must be positive.")
-    is_feasible = torch.zeros_like(samples[..., 0])
-    log_sigmoid = log_fatmoid if fat else logexpit
-    for constraint, e in zip(constraints, eta):
-        is_feasible = is_feasible + log_sigmoid(-constraint(samples) / e.to(samples))
-    return is_feasible if log else is_feasible.exp()
+    """utils/objective.py:134-180: the product over constraints of
+    sigmoid(-c_i / eta_i) (fatmoid with ``fat``), summed in log space in the
+    constraints' order; its log with ``log``."""
+    etas = _as_etas(eta, len(constraints))
+    log_sig = log_fatmoid if fat else logexpit
+    vals = _constraint_stack(constraints, samples)
+    total = torch.zeros_like(samples[..., 0])
+    for i in range(vals.shape[0]):  # in order: the same rounding as a running sum
+        total = total + log_sig(-vals[i] / etas[i].to(samples))
+    return total if log else total.exp()
 
 
 def get_infeasible_cost(X: torch.Tensor, model, objective=None, posterior_transform=None):
-    """acquisition/utils.py:203-242: M with -M < min_x f(x) (6-sigma lower bound)."""
-    if objective is None:
-        def objective(Y, X=None):
-            return Y.squeeze(-1)
+    """acquisition/utils.py:203-242: M >= 0 with -M below the objective's
+    6-sigma lower bound over X (one entry per output of the objective)."""
     with torch.no_grad():
-        posterior = model.posterior(X, posterior_transform=posterior_transform)
-        lb = objective(posterior.mean - 6 * posterior.variance.clamp_min(0).sqrt(), X=X)
-    if lb.ndim < posterior.mean.ndim:
+        post = model.posterior(X, posterior_transform=posterior_transform)
+        lower = post.mean - 6.0 * post.variance.clamp_min(0).sqrt()
+        lb = lower.squeeze(-1) if objective is None else objective(lower, X=X)
+    if lb.ndim < post.mean.ndim:
         lb = lb.unsqueeze(-1)
-    while lb.dim() > 1:
-        lb = lb.min(dim=-2).values
-    return -(lb.clamp_max(0.0))
+    lb = lb.reshape(-1, lb.shape[-1]).amin(dim=0) if lb.ndim > 1 else lb
+    return lb.clamp_max(0.0).neg()
 
 
 def _estimate_objective_lower_bound(model, objective, posterior_transform, X: torch.Tensor):
-    """acquisition/utils.py:166-200: -M over 32 random convex combinations of X."""
-    w = torch.rand(32, X.shape[-2], dtype=X.dtype, device=X.device)
-    w = w / w.sum(dim=0, keepdim=True)
-    return -get_infeasible_cost(X=w @ X, model=model, objective=objective,
-                                posterior_transform=posterior_transform)
+    """acquisition/utils.py:166-200: the lower bound over 32 random convex
+    combinations of the rows of X."""
+    mix = torch.rand(32, X.shape[-2], dtype=X.dtype, device=X.device)
+    mix = mix / mix.sum(dim=0, keepdim=True)
+    return get_infeasible_cost(X=mix @ X, model=model, objective=objective,
+                               posterior_transform=posterior_transform).neg()
 
 
 def compute_best_feasible_objective(samples: torch.Tensor, obj: torch.Tensor,
@@ -188,26 +215,25 @@ def compute_best_feasible_objective(samples: torch.Tensor, obj: torch.Tensor,
                                     objective=None, posterior_transform=None,
                                     X_baseline: Optional[torch.Tensor] = None,
                                     infeasible_obj: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """acquisition/utils.py:90-163: max over q of the feasible objective values
-    (infeasible entries replaced by -inf, or by a model-based lower bound when a
-    sample has no feasible point at all)."""
-    if constraints is None:
-        with torch.no_grad():
-            return obj.amax(dim=-1, keepdim=False)
-    is_feasible = compute_feasibility_indicator(constraints=constraints, samples=samples)
-    if is_feasible.any(dim=-1).all():
-        infeasible_value = -torch.inf
-    elif infeasible_obj is not None:
-        infeasible_value = infeasible_obj.item()
-    else:
-        if model is None:
+    """acquisition/utils.py:90-163: the best objective value over the q points
+    counting only feasible ones.  An infeasible entry counts as -inf when every
+    sample has a feasible point, else as ``infeasible_obj`` or the model's
+    lower bound over ``X_baseline``."""
+    if constraints is not None:
+        feas = compute_feasibility_indicator(constraints=constraints, samples=samples)
+        if bool(feas.any(dim=-1).all()):
+            fill = -torch.inf
+        elif infeasible_obj is not None:
+            fill = infeasible_obj.item()
+        elif model is None:
             raise ValueError("Must specify `model` when no feasible observation exists.")
-        if X_baseline is None:
+        elif X_baseline is None:
             raise ValueError("Must specify `X_baseline` when no feasible observation exists.")
-        infeasible_value = _estimate_objective_lower_bound(model=model, objective=objective,
-                                                           posterior_transform=posterior_transform,
-                                                           X=X_baseline).item()
-    is_feasible = repeat_to_match_aug_dim(is_feasible, obj)
-    obj = torch.where(is_feasible, obj, infeasible_value)
+        else:
+            fill = _estimate_objective_lower_bound(model=model, objective=objective,
+                                                   posterior_transform=posterior_transform,
+                                                   X=X_baseline).item()
+        obj = obj.where(repeat_to_match_aug_dim(feas, obj), torch.as_tensor(fill, dtype=obj.dtype,
+                                                                            device=obj.device))
     with torch.no_grad():
-        return obj.amax(dim=-1, keepdim=False)
+        return obj.amax(dim=-1)

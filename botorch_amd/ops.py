@@ -316,8 +316,11 @@ def _(X, Xt, Xt_scaled, U, Linv, beta, alpha, lengthscale, Z, best_f_s, kind, mo
     if not need_grad:
         return mk(B), mk(0), mk(0), mk(0), mk(0), mk(0), mk(B), info
     Qp, nrows_pad, nC = _geometry(B, q, Xt.shape[0])
-    return (mk(B), mk(B, q), mk(B, q, q), mk(nrows_pad, kernels.DP), mk(nC * 128, nrows_pad),
-            mk(0), mk(B), info)
+    # R^T's layout is carried by its shape (csrc/torch/bo_torch.cpp): blocked
+    # where the backward's fused W -> dX pass applies
+    Rt = (mk(nC * 8, nrows_pad // 16, 256) if kernels.rt_blocked_plan(B, q, Xt.shape[0])
+          else mk(nC * 128, nrows_pad))
+    return (mk(B), mk(B, q), mk(B, q, q), mk(nrows_pad, kernels.DP), Rt, mk(0), mk(B), info)
 
 
 @torch.library.custom_op("bo::qmc_acq_backward", mutates_args=(), device_types="cuda")

@@ -766,6 +766,8 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     timed = compact == "auto" and est is None  # no estimate: time two evaluations
     eval_ms = []
 
+    graph_errors = []  # why capture was refused, recorded (not swallowed)
+
     def _graph(state, shape):
         if not use_graph:
             return None
@@ -773,8 +775,11 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
         try:
             return GraphedAcquisition(acquisition_function, state.xt.view(shape), with_grad=True,
                                       warmup=1, check_each_call=False)
-        except RuntimeError:  # capture refused (e.g. a generic route with host reads)
+        except RuntimeError as e:  # capture refused (e.g. a generic route with host reads)
             torch.cuda.synchronize(X0.device)
+            graph_errors.append(f"{type(e).__name__}: {e}")
+            logger.info("gen_candidates_device: evaluation graph not captured, eager "
+                        "evaluations instead (%s)", graph_errors[-1])
             return None
 
     # expensive evaluations (the auto-compaction regime): the first capture
@@ -784,10 +789,12 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     ga = None if defer else _graph(st, shapeX)
     full, active = st, None   # the whole batch; rows of `full` that `st` holds
     shrinks = []
+    graphed_evals = 0
     t0 = time.monotonic()
     it = 0
     for it in range(max_evals):
         if ga is not None:
+            graphed_evals += 1
             v, g = ga(st.xt.view(shapeX))
             ft = (-v).reshape(-1).to(torch.float64).contiguous()
             gt = (-g).reshape(st.B, st.n).to(torch.float64).contiguous()
@@ -863,6 +870,9 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     gen_candidates_device.last_state = st
     gen_candidates_device.last_evals = it + 1
     gen_candidates_device.last_shrinks = shrinks  # (evaluation, restarts kept)
+    # evaluations replayed from a captured graph, and why a capture was refused
+    gen_candidates_device.last_graphed_evals = graphed_evals
+    gen_candidates_device.last_graph_error = graph_errors[-1] if graph_errors else None
     return cands, acq
 
 

@@ -162,10 +162,25 @@ def test_fixed_features_on_device(gen):
     bounds = torch.stack([torch.zeros(6), torch.ones(6)]).to(DEV, torch.float64)
     g = gen_candidates_scipy if gen == "scipy" else gen_candidates_device
     torch.manual_seed(0)
-    c, v = optimize_acqf(acqf, bounds, q=2, num_restarts=6, raw_samples=64,
-                         fixed_features={1: 0.25, 4: 0.5}, gen_candidates=g)
+    with warnings.catch_warnings(record=True) as ws:
+        warnings.simplefilter("always")
+        c, v = optimize_acqf(acqf, bounds, q=2, num_restarts=6, raw_samples=64,
+                             fixed_features={1: 0.25, 4: 0.5}, gen_candidates=g)
+    assert not any("Graph is empty" in str(w.message) for w in ws)
     assert torch.all(c[:, 1] == 0.25) and torch.all(c[:, 4] == 0.5)
     torch.testing.assert_close(v.reshape(1), acqf(c.unsqueeze(0)).reshape(1))
+    if gen == "device":
+        # the fixed-feature wrapper copies nothing from the host, so the
+        # evaluation graph is captured and replayed (not a silent eager run),
+        # and its candidates are the eager evaluations' bit for bit
+        assert gen_candidates_device.last_graph_error is None, gen_candidates_device.last_graph_error
+        assert gen_candidates_device.last_graphed_evals > 0
+        torch.manual_seed(0)
+        c_e, v_e = optimize_acqf(acqf, bounds, q=2, num_restarts=6, raw_samples=64,
+                                 options={"use_graph": False},
+                                 fixed_features={1: 0.25, 4: 0.5}, gen_candidates=g)
+        assert gen_candidates_device.last_graphed_evals == 0
+        assert torch.equal(c, c_e) and torch.equal(v, v_e)
     torch.manual_seed(0)
     _, v_free = optimize_acqf(acqf, bounds, q=2, num_restarts=6, raw_samples=64, gen_candidates=g)
     assert float(v) <= float(v_free) + 1e-9

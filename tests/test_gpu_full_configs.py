@@ -235,3 +235,45 @@ def test_fit_matches_oracle_scipy_fit():
     np.testing.assert_allclose(x_gpu, res.x, rtol=1e-3, atol=1e-5)
     lg, _ = _oracle_loss_grad(X, Y, x_gpu)
     assert abs(lg - res.fun) <= 1e-7 * max(1.0, abs(res.fun))
+
+
+def _spread_nonzero(v, k):
+    """k t-batch indices spread over the batch among those with a non-zero
+    value (so their gradients are not trivially zero)."""
+    nz = (v != 0).nonzero().flatten()
+    assert nz.numel() >= k, f"only {nz.numel()} non-zero values"
+    return nz[torch.linspace(0, nz.numel() - 1, k).round().long()]
+
+
+@pytest.mark.parametrize("b,acq", [(512, "qei"), (256, "qei"), (512, "qlogei")])
+def test_c3_gradient_fused_route_matches_oracle(c3, b, acq):
+    """The gradient every C3 optimiser evaluation takes (generation/gen.py:
+    194-222): forward + backward at the config size (n = 4096, q = 16, S = 512;
+    b = 512 restarts, and a 2-rank shard's 256) goes through the fused
+    W = R L^-1 -> dX pass (bo_post_w_dx, asserted), and dX at 16 spread t-batches
+    equals torch.autograd through the oracle's qEI / qLogEI on those t-batches
+    (rtol 1e-5).  best_f = max Y - 1.5 so the improvements are non-zero."""
+    from botorch_amd.acquisition import qExpectedImprovement, qLogExpectedImprovement
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import qei, qlogei
+    from oracle.sampling import draw_sobol_normal_samples
+    Xtr, Ytr, Xc, m, orc = c3
+    best_f = Ytr.max().item() - 1.5
+    cls, ref_fn = ((qExpectedImprovement, qei) if acq == "qei"
+                   else (qLogExpectedImprovement, qlogei))
+    acqf = cls(m, best_f, sampler=SobolQMCNormalSampler(torch.Size([S3]), seed=0))
+    Xd = Xc[:b].to(DEV).requires_grad_(True)
+    torch.ops.bo.last_backward_route()  # registers the op library
+    v = acqf(Xd)
+    (gd,) = torch.autograd.grad(v.sum(), Xd)
+    assert torch.ops.bo.last_backward_route() == 1, "config-size gradient left the fused W -> dX pass"
+    v, gd = v.detach().cpu(), gd.cpu()
+    assert torch.isfinite(gd).all()
+    idx = _spread_nonzero(v if acq == "qei" else v.exp(), 16)
+    Z = draw_sobol_normal_samples(Q3, S3, 0)
+    Xo = Xc[idx].clone().requires_grad_(True)
+    ref = ref_fn(orc, Xo, Z, best_f)
+    (go,) = torch.autograd.grad(ref.sum(), Xo)
+    torch.testing.assert_close(v[idx], ref.detach(), rtol=1e-6, atol=1e-10)
+    assert go.abs().amax(dim=(1, 2)).min() > 0
+    torch.testing.assert_close(gd[idx], go, rtol=1e-5, atol=1e-8)

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc counter CSVs per kernel into one JSON file.
 
-usage: python tools/pmc_summary.py OUT.json DIR [DIR ...]
-Each DIR holds a run_counter_collection.csv from one `rocprofv3 --pmc ...`
+usage: python tools/pmc_summary.py [--meta key=value ...] OUT.json DIR [DIR ...]
+``_meta`` records the creation time and the --meta pairs (bench.py reads
+``restarts``: the launch size the passes ran at).  Each DIR holds a run_counter_collection.csv from one `rocprofv3 --pmc ...`
 pass (FETCH_SIZE and WRITE_SIZE need separate passes on gfx950).
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are in KiB;
@@ -17,6 +18,7 @@ import json
 import os
 import re
 import sys
+import time
 
 SIMDS, XCDS = 1024, 8
 
@@ -27,7 +29,13 @@ def short(name: str) -> str:
 
 
 def main():
-    out, dirs = sys.argv[1], sys.argv[2:]
+    argv = sys.argv[1:]
+    meta = {"created": time.time()}
+    while argv and argv[0] == "--meta":
+        k, v = argv[1].split("=", 1)
+        meta[k] = int(v) if v.isdigit() else v
+        argv = argv[2:]
+    out, dirs = argv[0], argv[1:]
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for d in dirs:
         path = os.path.join(d, "run_counter_collection.csv")
@@ -46,8 +54,10 @@ def main():
         if "SQ_VALU_MFMA_BUSY_CYCLES" in e and e.get("GRBM_GUI_ACTIVE"):
             e["mfma_util"] = e["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * e["GRBM_GUI_ACTIVE"] / XCDS)
         summary[k] = e
+    summary["_meta"] = meta
     json.dump(summary, open(out, "w"), indent=1, sort_keys=True)
-    for k, e in sorted(summary.items(), key=lambda kv: -kv[1].get("GRBM_GUI_ACTIVE", 0)):
+    for k, e in sorted(((k, e) for k, e in summary.items() if k != "_meta"),
+                       key=lambda kv: -kv[1].get("GRBM_GUI_ACTIVE", 0)):
         print(f"{k:50s} n={e['dispatches']:4d} hbm={e.get('hbm_bytes', 0) / 1e6:10.2f} MB "
               f"mfma={e.get('mfma_util', float('nan')):.3f}")
 
