@@ -60,28 +60,85 @@ struct WaveCtx {
   }
 };
 
+// NW waves as one lane context (NL = 64 NW lanes): the joint problem of
+// gen.py:252-267 -- ONE L-BFGS-B over all restarts' b q d variables -- is a
+// single restart with n in the thousands, so its dot products, breakpoint scans
+// and formk products are spread over a whole workgroup.  Reductions: the wave
+// butterfly, then the NW wave results through LDS in wave order (the same
+// result on every lane, as WaveCtx's).
+template <int NW>
+struct BlockCtx {
+  static constexpr int NL = 64 * NW;
+  int lane;
+  double* red;  // LDS, NW doubles
+  int* redi;    // LDS, NW ints
+  __device__ void sync() { __syncthreads(); }
+  __device__ unsigned long long clock() { return wall_clock64(); }
+  template <class F>
+  __device__ double all(double v, F op) {
+    for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o));
+    __syncthreads();  // the previous reduction's reads are done
+    if ((lane & 63) == 0) red[lane >> 6] = v;
+    __syncthreads();
+    double r = red[0];
+    for (int w = 1; w < NW; ++w) r = op(r, red[w]);
+    return r;
+  }
+  __device__ double sum(double v) { return all(v, [](double a, double b) { return a + b; }); }
+  __device__ double max(double v) { return all(v, [](double a, double b) { return fmax(a, b); }); }
+  __device__ double min(double v) { return all(v, [](double a, double b) { return fmin(a, b); }); }
+  __device__ void argmin(double& v, int& i) {  // ties to the smallest index
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(v, o);
+      const int oi = __shfl_xor(i, o);
+      if (ov < v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
+      }
+    }
+    __syncthreads();
+    if ((lane & 63) == 0) {
+      red[lane >> 6] = v;
+      redi[lane >> 6] = i;
+    }
+    __syncthreads();
+    v = red[0];
+    i = redi[0];
+    for (int w = 1; w < NW; ++w)
+      if (red[w] < v || (red[w] == v && redi[w] < i)) {
+        v = red[w];
+        i = redi[w];
+      }
+  }
+};
+
 // Bytes of LDS a restart's working set takes (vectors, int vectors, S / Y ring).
 inline size_t staged_bytes(int n, int m) {
   return sizeof(double) * ((size_t)bolb::V_COUNT * n + 2 * (size_t)m * n) +
          sizeof(int) * (size_t)bolb::IV_COUNT * n;
 }
 constexpr size_t STAGE_LIMIT = 64 * 1024 - sizeof(bolb::Shared);  // dynamic LDS budget
+constexpr int JOINT_N = 1024;  // wider restarts run on a 4-wave workgroup
 
 // One wave per restart.  With `staged`, the restart's vectors and ring are
 // copied into LDS for the launch (coalesced, once) and back at the end: every
 // dot product, breakpoint scan and formk product then reads LDS instead of
 // chaining dependent HBM / L2 loads, which set the duration of the slowest
 // restart (the launch's duration).
-__global__ __launch_bounds__(64) void lbfgsb_kernel(bolb::Problem P, double* __restrict__ xt,
-                                                    const double* __restrict__ ft,
-                                                    const double* __restrict__ gt,
-                                                    double* __restrict__ v, int* __restrict__ iv,
-                                                    double* __restrict__ ws,
-                                                    double* __restrict__ wy,
-                                                    double* __restrict__ mat,
-                                                    double* __restrict__ ds, int* __restrict__ is,
-                                                    int staged) {
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void lbfgsb_kernel(bolb::Problem P, double* __restrict__ xt,
+                                                         const double* __restrict__ ft,
+                                                         const double* __restrict__ gt,
+                                                         double* __restrict__ v, int* __restrict__ iv,
+                                                         double* __restrict__ ws,
+                                                         double* __restrict__ wy,
+                                                         double* __restrict__ mat,
+                                                         double* __restrict__ ds, int* __restrict__ is,
+                                                         int staged) {
+  constexpr int NL = 64 * NW;
   __shared__ bolb::Shared S;
+  __shared__ double red[NW];
+  __shared__ int redi[NW];
   extern __shared__ double lds_dyn[];
   const long b = blockIdx.x;
   const long n = P.n, m = P.m;
@@ -106,29 +163,35 @@ __global__ __launch_bounds__(64) void lbfgsb_kernel(bolb::Problem P, double* __r
     double* lws = lv + nv;
     double* lwy = lws + nr;
     int* liv = reinterpret_cast<int*>(lwy + nr);
-    for (long k = lane; k < nv; k += 64) lv[k] = gv[k];
-    for (long k = lane; k < nr; k += 64) {
+    for (long k = lane; k < nv; k += NL) lv[k] = gv[k];
+    for (long k = lane; k < nr; k += NL) {
       lws[k] = gws[k];
       lwy[k] = gwy[k];
     }
-    for (long k = lane; k < ni; k += 64) liv[k] = giv[k];
+    for (long k = lane; k < ni; k += NL) liv[k] = giv[k];
     __syncthreads();
     R.v = lv;
     R.ws = lws;
     R.wy = lwy;
     R.iv = liv;
   }
-  WaveCtx c{lane};
-  bolb::Step<WaveCtx> st(c, P, R, S);
-  st.run(P.prof ? P.prof + b * bolb::PROF_SLOTS : nullptr);
+  if constexpr (NW == 1) {
+    WaveCtx c{lane};
+    bolb::Step<WaveCtx> st(c, P, R, S);
+    st.run(P.prof ? P.prof + b * bolb::PROF_SLOTS : nullptr);
+  } else {
+    BlockCtx<NW> c{lane, red, redi};
+    bolb::Step<BlockCtx<NW>> st(c, P, R, S);
+    st.run(P.prof ? P.prof + b * bolb::PROF_SLOTS : nullptr);
+  }
   if (staged) {
     __syncthreads();
-    for (long k = lane; k < nv; k += 64) gv[k] = R.v[k];
-    for (long k = lane; k < nr; k += 64) {
+    for (long k = lane; k < nv; k += NL) gv[k] = R.v[k];
+    for (long k = lane; k < nr; k += NL) {
       gws[k] = R.ws[k];
       gwy[k] = R.wy[k];
     }
-    for (long k = lane; k < ni; k += 64) giv[k] = R.iv[k];
+    for (long k = lane; k < ni; k += NL) giv[k] = R.iv[k];
   }
 }
 
@@ -182,8 +245,14 @@ extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int m
   bolb::Problem P{n, m, maxls, maxiter, maxfun, ftol, pgtol, lower, upper, prof};
   const size_t bytes = staged_bytes(n, m);
   const int staged = bytes <= STAGE_LIMIT && !g_lbfgsb_unstaged.load();
-  lbfgsb_kernel<<<B, 64, staged ? bytes : 0, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws, wy,
-                                                                  mat, ds, is, staged);
+  // one wave per restart; a restart wider than the wave's working set (the
+  // joint problem over all restarts, n = b q d) takes a 4-wave workgroup
+  if (n <= JOINT_N)
+    lbfgsb_kernel<1><<<B, 64, staged ? bytes : 0, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws, wy,
+                                                                       mat, ds, is, staged);
+  else
+    lbfgsb_kernel<4><<<B, 256, staged ? bytes : 0, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws,
+                                                                        wy, mat, ds, is, staged);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

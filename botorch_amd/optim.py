@@ -681,6 +681,10 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     restart's trial points are scipy's on the same objective; the reference
     runs ONE L-BFGS-B over the sum of the restarts' objectives, so its
     iterates equal these at b = 1 and differ (same stationary points) at b > 1.
+    ``joint=True``: the reference's problem itself -- one L-BFGS-B over all
+    b q d variables of the batch and the summed objective (one line search,
+    one memory; a single device "restart" on a 4-wave workgroup), whose
+    iterates are scipy's on gen_candidates_scipy's objective.
     ``algorithm="projected"``: the round-1 projected L-BFGS with Armijo
     backtracking (``maxiter`` bounds its evaluations).
 
@@ -732,20 +736,27 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
         raise RuntimeError("gen_candidates_device runs on ROCm device tensors")
     shapeX = X0.shape
     lbfgsb = algorithm == "lbfgsb"
+    # joint: the reference's own problem (gen.py:252-267) -- ONE L-BFGS-B over
+    # all b q d variables with f = -sum_b acq(X_b), one line search and one
+    # memory for the whole batch (a single device "restart" of n = b q d)
+    joint = bool(options.get("joint", False))
+    if joint and not lbfgsb:
+        raise ValueError("joint=True runs scipy's L-BFGS-B (algorithm='lbfgsb')")
     if lbfgsb:
         maxiter = int(options.get("maxiter", 2000))  # gen_candidates_scipy's default
         maxfun = int(options.get("maxfun", 15000))
         maxls = int(options.get("maxls", 20))
         max_evals = maxfun + maxls + 1
-        st = _LBFGSBState(X0, m)
+        st = _LBFGSBState(X0.reshape(1, -1) if joint else X0, m)
     else:
         maxiter = int(options.get("maxiter", 200))
         max_evals = maxiter + 1
         st = _LBFGSState(X0, m)
-    lo = (torch.as_tensor(lower_bounds, dtype=torch.float64, device=X0.device).expand(shapeX[-2:])
+    bshape = shapeX if joint else shapeX[-2:]  # the bounds of one device restart
+    lo = (torch.as_tensor(lower_bounds, dtype=torch.float64, device=X0.device).expand(bshape)
           .reshape(-1).contiguous() if lower_bounds is not None
           else torch.full((st.n,), -math.inf, dtype=torch.float64, device=X0.device))
-    hi = (torch.as_tensor(upper_bounds, dtype=torch.float64, device=X0.device).expand(shapeX[-2:])
+    hi = (torch.as_tensor(upper_bounds, dtype=torch.float64, device=X0.device).expand(bshape)
           .reshape(-1).contiguous() if upper_bounds is not None
           else torch.full((st.n,), math.inf, dtype=torch.float64, device=X0.device))
     stream = kernels._stream(X0.device)
@@ -753,7 +764,7 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     # replay where the acquisition allows capture (the fused qEI / qLogEI
     # paths); the eager autograd evaluation otherwise
     use_graph = bool(options.get("use_graph", True))
-    compact = options.get("compact", "auto") if lbfgsb else False
+    compact = options.get("compact", "auto") if lbfgsb and not joint else False
     compact_min = int(options.get("compact_min", 8))
     # "auto": shrink only expensive evaluations (the re-capture of the graph
     # costs a few evaluations' worth: measured C3 55 -> 35 ms, C2 9.1 -> 14.5 ms
@@ -796,14 +807,16 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
         if ga is not None:
             graphed_evals += 1
             v, g = ga(st.xt.view(shapeX))
-            ft = (-v).reshape(-1).to(torch.float64).contiguous()
-            gt = (-g).reshape(st.B, st.n).to(torch.float64).contiguous()
+            ft, gt = -v, -g
         else:
             Xt = st.xt.view(shapeX).detach().requires_grad_(True)
             ft = -acquisition_function(Xt)
             (gt,) = torch.autograd.grad(ft.sum(), Xt)
-            ft = ft.detach().reshape(-1).to(torch.float64).contiguous()
-            gt = gt.reshape(st.B, st.n).to(torch.float64).contiguous()
+            ft = ft.detach()
+        if joint:  # gen.py's loss: -acq(X).sum() over the whole batch
+            ft = ft.sum()
+        ft = ft.reshape(-1).to(torch.float64).contiguous()
+        gt = gt.reshape(st.B, st.n).to(torch.float64).contiguous()
         if lbfgsb:
             a = _lib.LbfgsbArgs(B=st.B, n=st.n, m=m, maxls=maxls, maxiter=maxiter, maxfun=maxfun,
                                 ftol=ftol, pgtol=pgtol, lower=lo, upper=hi, xt=st.xt, ft=ft, gt=gt,

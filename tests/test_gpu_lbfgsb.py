@@ -223,3 +223,59 @@ def test_kernel_unconstrained_and_fixed_variables():
     assert len(trials[0]) == len(sp) and nit[0] == res.nit
     np.testing.assert_allclose(x[0], res.x, atol=1e-10, rtol=0)
     assert x[0][0] == 0.3 and x[0][1] == 0.3 and x[0][9] == 0.5
+
+
+@pytest.mark.parametrize("q", [200, 300])
+def test_kernel_joint_width_trial_points_equal_scipy(q):
+    """A restart wider than one wave's working set (n = 6 q = 1200 / 1800 > 1024:
+    the 4-wave workgroup the joint problem runs on, block-wide reductions) on
+    one Hartmann q-batch: scipy's trial points in scipy's order (the opening 25),
+    its final value."""
+    n = 6 * q
+    x0 = np.random.default_rng(q).uniform(0, 1, n)
+    lo, hi = np.zeros(n), np.ones(n)
+    fg = _hartmann_batch(q)
+    trials, x, f, status, nit = _drive([fg], x0[None], lo, hi, maxiter=60)
+    sp, res = scipy_trials(fg, x0, list(zip(lo, hi)), maxiter=60)
+    k = min(25, len(sp))
+    assert len(trials[0]) >= k
+    for i in range(k):
+        np.testing.assert_allclose(trials[0][i], sp[i], atol=1e-9, rtol=0, err_msg=f"trial {i}")
+    np.testing.assert_allclose(f[0], res.fun, rtol=1e-7, atol=1e-9)
+
+
+@pytest.mark.parametrize("b", [8, 32])
+def test_gen_candidates_device_joint_equals_scipy(b):
+    """joint=True is the reference's problem (generation/gen.py:252-267: one
+    L-BFGS-B over the b q d stacked variables and -sum_b acq): at C2 size
+    (n = 1024, q = 8, S = 256) its candidates and values equal
+    gen_candidates_scipy's on the same initial conditions -- b = 8 (384
+    variables, one wave) and b = 32 (1536, the 4-wave workgroup)."""
+    from botorch_amd.acquisition import qExpectedImprovement
+    from botorch_amd.models import SingleTaskGP
+    from botorch_amd.optim import (gen_batch_initial_conditions, gen_candidates_device,
+                                   gen_candidates_scipy)
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from botorch_amd.test_functions import Hartmann
+    from botorch_amd.utils_sampling import draw_sobol_samples
+    box = torch.stack([torch.zeros(6), torch.ones(6)]).to(torch.float64)
+    X = draw_sobol_samples(box, 1024, 1, seed=0).squeeze(1)
+    Y = Hartmann(negate=True)(X).unsqueeze(-1)
+    m = SingleTaskGP(X.to(DEV), Y.to(DEV))
+    m.covar_module.lengthscale = torch.full((1, 6), 0.5016, dtype=torch.float64)
+    m.likelihood.noise = torch.tensor([6.737947e-3], dtype=torch.float64)
+    m.eval()
+    acqf = qExpectedImprovement(m, float(Y.max()) - 0.3,
+                                sampler=SobolQMCNormalSampler(torch.Size([256]), seed=0))
+    bounds = box.to(DEV)
+    ics = gen_batch_initial_conditions(acqf, bounds, q=8, num_restarts=b, raw_samples=4 * b,
+                                       options={"seed": 3})
+    opts = {"maxiter": 100}
+    cs, vs = gen_candidates_scipy(ics, acqf, bounds[0], bounds[1], options=opts)
+    cd, vd = gen_candidates_device(ics, acqf, bounds[0], bounds[1], options={**opts, "joint": True})
+    st = gen_candidates_device.last_state
+    assert st.B == 1 and st.n == b * 8 * 6
+    assert gen_candidates_device.last_graph_error is None
+    torch.testing.assert_close(cd, cs, atol=1e-6, rtol=0)
+    torch.testing.assert_close(vd, vs, atol=1e-10, rtol=1e-7)
+    assert float(vs.max()) > 0
