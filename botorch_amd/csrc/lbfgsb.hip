@@ -58,6 +58,15 @@ struct WaveCtx {
       }
     }
   }
+  __device__ int exscan(int v, int& total) {  // exclusive prefix sum in lane order
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    total = __shfl(x, 63);
+    return x - v;
+  }
 };
 
 // NW waves as one lane context (NL = 64 NW lanes): the joint problem of
@@ -66,13 +75,56 @@ struct WaveCtx {
 // and formk products are spread over a whole workgroup.  Reductions: the wave
 // butterfly, then the NW wave results through LDS in wave order (the same
 // result on every lane, as WaveCtx's).
-template <int NW>
+template <int NW_>
 struct BlockCtx {
+  static constexpr int NW = NW_;
   static constexpr int NL = 64 * NW;
   int lane;
-  double* red;  // LDS, NW doubles
-  int* redi;    // LDS, NW ints
+  double* red;   // LDS, NW doubles
+  int* redi;     // LDS, NW ints
+  double* reds;  // LDS, NW x M2 doubles (sums)
+  __device__ int wave() const { return lane >> 6; }
+  __device__ int wlane() const { return lane & 63; }
   __device__ void sync() { __syncthreads(); }
+  __device__ double wave_sum(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+  }
+  // every entry of v summed over all NL lanes (waves in order), on every lane
+  template <int K>
+  __device__ void sums(double (&v)[K]) {
+    static_assert(K <= bolb::M2, "sums: scratch holds M2 values per wave");
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = wave_sum(v[k]);
+    __syncthreads();
+    if (wlane() == 0)
+#pragma unroll
+      for (int k = 0; k < K; ++k) reds[wave() * bolb::M2 + k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      double r = reds[k];
+      for (int w = 1; w < NW; ++w) r += reds[w * bolb::M2 + k];
+      v[k] = r;
+    }
+  }
+  __device__ int exscan(int v, int& total) {  // exclusive prefix sum in lane order
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (wlane() >= o) x += y;
+    }
+    __syncthreads();
+    if (wlane() == 63) redi[wave()] = x;
+    __syncthreads();
+    int before = 0;
+    total = 0;
+    for (int w = 0; w < NW; ++w) {
+      if (w < wave()) before += redi[w];
+      total += redi[w];
+    }
+    return before + x - v;
+  }
   __device__ unsigned long long clock() { return wall_clock64(); }
   template <class F>
   __device__ double all(double v, F op) {
@@ -118,7 +170,8 @@ inline size_t staged_bytes(int n, int m) {
          sizeof(int) * (size_t)bolb::IV_COUNT * n;
 }
 constexpr size_t STAGE_LIMIT = 64 * 1024 - sizeof(bolb::Shared);  // dynamic LDS budget
-constexpr int JOINT_N = 1024;  // wider restarts run on a 4-wave workgroup
+constexpr int JOINT_N = 1024;  // wider restarts run on a JOINT_W-wave workgroup
+constexpr int JOINT_W = 8;
 
 // One wave per restart.  With `staged`, the restart's vectors and ring are
 // copied into LDS for the launch (coalesced, once) and back at the end: every
@@ -139,6 +192,7 @@ __global__ __launch_bounds__(64 * NW) void lbfgsb_kernel(bolb::Problem P, double
   __shared__ bolb::Shared S;
   __shared__ double red[NW];
   __shared__ int redi[NW];
+  __shared__ double reds[NW > 1 ? NW * bolb::M2 : 1];
   extern __shared__ double lds_dyn[];
   const long b = blockIdx.x;
   const long n = P.n, m = P.m;
@@ -180,7 +234,7 @@ __global__ __launch_bounds__(64 * NW) void lbfgsb_kernel(bolb::Problem P, double
     bolb::Step<WaveCtx> st(c, P, R, S);
     st.run(P.prof ? P.prof + b * bolb::PROF_SLOTS : nullptr);
   } else {
-    BlockCtx<NW> c{lane, red, redi};
+    BlockCtx<NW> c{lane, red, redi, reds};
     bolb::Step<BlockCtx<NW>> st(c, P, R, S);
     st.run(P.prof ? P.prof + b * bolb::PROF_SLOTS : nullptr);
   }
@@ -246,13 +300,13 @@ extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int m
   const size_t bytes = staged_bytes(n, m);
   const int staged = bytes <= STAGE_LIMIT && !g_lbfgsb_unstaged.load();
   // one wave per restart; a restart wider than the wave's working set (the
-  // joint problem over all restarts, n = b q d) takes a 4-wave workgroup
+  // joint problem over all restarts, n = b q d) takes an 8-wave workgroup
   if (n <= JOINT_N)
     lbfgsb_kernel<1><<<B, 64, staged ? bytes : 0, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws, wy,
                                                                        mat, ds, is, staged);
   else
-    lbfgsb_kernel<4><<<B, 256, staged ? bytes : 0, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws,
-                                                                        wy, mat, ds, is, staged);
+    lbfgsb_kernel<JOINT_W><<<B, 64 * JOINT_W, staged ? bytes : 0, as_stream(stream)>>>(
+        P, xt, ft, gt, v, iv, ws, wy, mat, ds, is, staged);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

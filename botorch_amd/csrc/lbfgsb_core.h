@@ -21,12 +21,23 @@
 // The code is written once against a lane context C:
 //   C::NL lanes; c.lane; c.sync(); c.sum / c.max / c.min (all-lane reduction,
 //   identical result on every lane); c.argmin(v, i) (smallest v, ties to the
-//   smallest i).  Vector work is strided over lanes; the small dense algebra
-//   (2m x 2m) runs on lane 0 in the block-shared record and is published by
-//   c.sync().  The including file defines BO_HD (device or host qualifiers).
+//   smallest i); c.exscan(v, total) (exclusive prefix sum in lane order).
+//   Vector work is strided over lanes; the small dense algebra (2m x 2m) runs
+//   on lane 0 in the block-shared record and is published by c.sync().  A
+//   context wider than one wave (C::NL > 64: the joint problem over all
+//   restarts, n = b q d in the thousands) also provides waves: c.wave(),
+//   c.wlane(), c.wave_sum(v) (within the wave) and c.sums(v) (NL-wide sums of
+//   a register array); its Step batches the 2m dot products of a pass over
+//   the vectors into one pass (wdots) and splits formk's products over the
+//   waves (formk_wide).  The including file defines BO_HD.
 #pragma once
 
 namespace bolb {
+
+// Strided vector loops: four iterations' loads in flight instead of one memory
+// latency per iteration (a joint problem's n = b q d runs ~24 iterations per
+// lane); sums keep their per-lane order.
+#define BO_UNROLL4 _Pragma("unroll 4")
 
 constexpr int MMAX = 20;  // history limit (scipy default maxcor = 10)
 constexpr int M2 = 2 * MMAX;
@@ -375,6 +386,9 @@ struct Step {
     cnstnd = boxed = false;
   }
 
+  // a workgroup-wide restart: batched dot products, formk split over waves
+  static constexpr bool WIDE = C::NL > 64;
+
   unsigned long long tprev = 0;
   unsigned long long* prof = nullptr;  // this restart's PROF_SLOTS clocks
   BO_HD void tick(int phase) {  // attribute the time since the last tick to `phase`
@@ -393,12 +407,47 @@ struct Step {
 
   BO_HD double dot(const double* a, const double* b) {
     double s = 0.0;
+#pragma unroll 4  // loads issue ahead; the sum keeps its order
     for (int i = c.lane; i < n; i += C::NL) s += a[i] * b[i];
     return c.sum(s);
   }
 
+  // WIDE: out[j] = WY(j) . b, out[col + j] = WS(j) . b (j < col) over the
+  // first cnt entries of b, WY / WS read at index[i] with GATHER -- every
+  // product of one pass over the vectors, 2 MMAX partial sums per lane, one
+  // NL-wide reduction (lane 0 writes out; the caller syncs).
+  template <bool GATHER>
+  BO_HD void wdots(const double* b, int cnt, double* out) {
+    if constexpr (WIDE) {
+      const int col = S.i[I_COL];
+      int sl[MMAX];  // ring offsets of the ordered columns
+#pragma unroll
+      for (int j = 0; j < MMAX; ++j) sl[j] = slot(j < col ? j : 0) * n;
+      // the WY products, then the WS ones (MMAX partial sums per lane each)
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const double* W = half ? R.ws : R.wy;
+        double acc[MMAX];
+#pragma unroll
+        for (int j = 0; j < MMAX; ++j) acc[j] = 0.0;
+        BO_UNROLL4
+        for (int i = c.lane; i < cnt; i += C::NL) {
+          const int k = GATHER ? index[i] : i;
+          const double bi = b[i];
+#pragma unroll
+          for (int j = 0; j < MMAX; ++j)
+            if (j < col) acc[j] += W[sl[j] + k] * bi;
+        }
+        c.sums(acc);
+        if (c.lane == 0)
+          for (int j = 0; j < col; ++j) out[half * col + j] = acc[j];
+      }
+    }
+  }
+
   BO_HD double projgr() {  // sup-norm of the projected gradient
     double nrm = 0.0;
+    BO_UNROLL4
     for (int i = c.lane; i < n; i += C::NL) {
       double gi = g[i];
       const int nb = nbd(i);
@@ -441,11 +490,13 @@ struct Step {
     const double theta = S.d[D_THETA];
     const double inf = __builtin_inf();
     if (S.d[D_SBGNRM] <= 0.0) {
+      BO_UNROLL4
       for (int i = c.lane; i < n; i += C::NL) z[i] = x[i];
       c.sync();
       return 0;
     }
     double f1 = 0.0, nbreak = 0.0, nunb = 0.0, moving = 0.0;
+    BO_UNROLL4
     for (int i = c.lane; i < n; i += C::NL) {
       const double neggi = -g[i];
       const int nb = nbd(i);
@@ -491,12 +542,16 @@ struct Step {
     const int nfr = (int)c.sum(nunb);
     const bool bnded = c.max(moving) == 0.0;
     c.sync();
-    for (int j = 0; j < col; ++j) {  // p = W^T dc
-      const double py = dot(WY(j), dc);
-      const double ps = dot(WS(j), dc);
-      if (c.lane == 0) {
-        S.p[j] = py;
-        S.p[col + j] = ps;
+    if constexpr (WIDE) {  // p = W^T dc
+      wdots<false>(dc, n, S.p);
+    } else {
+      for (int j = 0; j < col; ++j) {
+        const double py = dot(WY(j), dc);
+        const double ps = dot(WS(j), dc);
+        if (c.lane == 0) {
+          S.p[j] = py;
+          S.p[col + j] = ps;
+        }
       }
     }
     if (c.lane == 0 && theta != 1.0)
@@ -532,6 +587,7 @@ struct Step {
       while (true) {
         double tmin = inf;
         int ibp = n;
+#pragma unroll 4
         for (int i = c.lane; i < n; i += C::NL)
           if (tb[i] < tmin) {
             tmin = tb[i];
@@ -608,6 +664,7 @@ struct Step {
     }
     if (dtm <= 0.0) dtm = 0.0;
     tsum += dtm;
+    BO_UNROLL4
     for (int i = c.lane; i < n; i += C::NL) z[i] += tsum * dc[i];
     if (c.lane == 0 && col > 0)
       for (int j = 0; j < 2 * col; ++j) S.c[j] += dtm * S.p[j];
@@ -616,28 +673,122 @@ struct Step {
   }
 
   // ---- freev: free (iwhere <= 0, ascending) then active (descending from n-1) ----
+  // A stream compaction: each lane takes a contiguous chunk, counts its free
+  // variables, and the exclusive prefix sums over the lanes place them (the
+  // same index array as the serial loop).
   BO_HD void freev() {
     c.sync();
-    if (c.lane == 0) {
-      int nfree = 0, iact = n;
-      for (int i = 0; i < n; ++i) {
-        if (iwhere[i] <= 0)
-          index[nfree++] = i;
-        else
-          index[--iact] = i;
-      }
-      S.i[I_NFREE] = nfree;
+    const int ch = (n + C::NL - 1) / C::NL;
+    const int i0 = c.lane * ch < n ? c.lane * ch : n;
+    const int i1 = i0 + ch < n ? i0 + ch : n;
+    int nf = 0;
+    for (int i = i0; i < i1; ++i) nf += iwhere[i] <= 0 ? 1 : 0;
+    int tot_f = 0, tot_a = 0;
+    int of = c.exscan(nf, tot_f);
+    int oa = c.exscan(i1 - i0 - nf, tot_a);
+    for (int i = i0; i < i1; ++i) {
+      if (iwhere[i] <= 0)
+        index[of++] = i;
+      else
+        index[n - 1 - (oa++)] = i;
     }
+    if (c.lane == 0) S.i[I_NFREE] = tot_f;
     c.sync();
   }
 
   // ---- formk: the LEL^T factorisation of the 2col x 2col K in S.wn ----
+  // WIDE: the products of formk are the lower triangle of the Gram matrix of
+  // the 2col vectors u < col: WY(u), u >= col: WS(u - col), each over the
+  // free set (Y.Y, and S_i.Y_j with i <= j) or the active set (S.S, and
+  // S_i.Y_j with i > j).  4 x 4 blocks of it go round-robin to the waves; a
+  // wave's lanes stride over the variables in natural order (free: iwhere <=
+  // 0, as freev decides), 16 partial sums each, then a wave reduction.
+  BO_HD void formk_wide() {
+    if constexpr (WIDE) {
+      const int col = S.i[I_COL];
+      const double theta = S.d[D_THETA];
+      const int nv = 2 * col, nb = (nv + 3) / 4;
+      const int nblk = nb * (nb + 1) / 2;
+      for (int blk = c.wave(); blk < nblk; blk += C::NW) {
+        int bu = 0, rem = blk;
+        while (rem > bu) {
+          rem -= bu + 1;
+          ++bu;
+        }
+        const int bv = rem;  // block (bu, bv), bv <= bu
+        const double* pu[4];
+        const double* pv[4];
+        bool free_e[4][4], ok[4][4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const int u = 4 * bu + a, v = 4 * bv + a;
+          const int uu = u < nv ? u : 0, vv = v < nv ? v : 0;
+          pu[a] = uu < col ? WY(uu) : WS(uu - col);
+          pv[a] = vv < col ? WY(vv) : WS(vv - col);
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int u = 4 * bu + a, v = 4 * bv + b;
+            ok[a][b] = u < nv && v < nv && v <= u;
+            // Y.Y free; S.S active; S_i.Y_j (u = col + i, v = j) free iff i <= j
+            free_e[a][b] = v < col && (u < col || u - col <= v);
+          }
+        double acc[4][4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+#pragma unroll 2
+        for (int k = c.wlane(); k < n; k += 64) {
+          const bool fr = iwhere[k] <= 0;
+          double xu[4], xv[4];
+#pragma unroll
+          for (int a = 0; a < 4; ++a) {
+            xu[a] = pu[a][k];
+            xv[a] = pv[a][k];
+          }
+#pragma unroll
+          for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+              if (ok[a][b] && free_e[a][b] == fr) acc[a][b] += xu[a] * xv[b];
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) acc[a][b] = c.wave_sum(acc[a][b]);
+        if (c.wlane() == 0) {
+#pragma unroll
+          for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              if (!ok[a][b]) continue;
+              const int u = 4 * bu + a, v = 4 * bv + b;
+              const double sm = acc[a][b];
+              if (u < col) {  // Y_u . Y_v over the free set
+                double val = sm / theta;
+                if (u == v) val += S.sy[u + u * MMAX];
+                S.wn[v + u * M2] = val;
+              } else if (v >= col) {  // S_i . S_j over the active set
+                S.wn[(v) + (u) * M2] = sm * theta;
+              } else {  // S_i . Y_j: -L_a (i > j, active) / R_z (i <= j, free)
+                S.wn[v + u * M2] = (u - col > v) ? -sm : sm;
+              }
+            }
+        }
+      }
+    }
+  }
+
   BO_HD int formk() {
     const int col = S.i[I_COL];
     const int nfree = S.i[I_NFREE];
     const double theta = S.d[D_THETA];
     const int ntri = col * (col + 1) / 2;
-    const int npairs = 2 * ntri + col * col;
+    const int npairs = WIDE ? 0 : 2 * ntri + col * col;
+    if constexpr (WIDE) formk_wide();
     for (int p = c.lane; p < npairs; p += C::NL) {
       int kind, i, j;
       if (p < 2 * ntri) {
@@ -681,20 +832,30 @@ struct Step {
       }
     }
     c.sync();
-    if (c.lane == 0) {
-      int info = dpofa(S.wn, M2, col) ? -1 : 0;
-      if (!info) {
-        for (int js = col; js < 2 * col; ++js) dtrsl_t(S.wn, M2, col, S.wn + js * M2);
-        for (int is = col; is < 2 * col; ++is)
-          for (int js = is; js < 2 * col; ++js) {
-            double s = 0.0;
-            #pragma unroll 4
-            for (int k = 0; k < col; ++k) s += S.wn[k + is * M2] * S.wn[k + js * M2];
-            S.wn[is + js * M2] += s;
-          }
-        if (dpofa(S.wn + col + col * M2, M2, col)) info = -2;
+    // LEL^T: the upper-left Cholesky, then the col right-hand columns' solves
+    // and the lower-right block's col(col+1)/2 products spread over the lanes
+    // (each column / entry computed by one lane exactly as the serial loops
+    // do: the same values), then the lower-right Cholesky
+    if (c.lane == 0) S.k0 = dpofa(S.wn, M2, col) ? -1 : 0;
+    c.sync();
+    if (S.k0 == 0) {
+      for (int js = col + c.lane; js < 2 * col; js += C::NL) dtrsl_t(S.wn, M2, col, S.wn + js * M2);
+      c.sync();
+      for (int e = c.lane; e < ntri; e += C::NL) {
+        int is = 0, q = e;  // e -> (is, js), col <= is <= js < 2 col, row-major over is
+        while (q >= col - is) {
+          q -= col - is;
+          ++is;
+        }
+        const int js = col + is + q;
+        is += col;
+        double s = 0.0;
+        #pragma unroll 4
+        for (int k = 0; k < col; ++k) s += S.wn[k + is * M2] * S.wn[k + js * M2];
+        S.wn[is + js * M2] += s;
       }
-      S.k0 = info;
+      c.sync();
+      if (c.lane == 0 && dpofa(S.wn + col + col * M2, M2, col)) S.k0 = -2;
     }
     c.sync();
     return S.k0;
@@ -706,6 +867,7 @@ struct Step {
     const int nfree = S.i[I_NFREE];
     const double theta = S.d[D_THETA];
     if (unconstrained) {
+      BO_UNROLL4
       for (int i = c.lane; i < n; i += C::NL) rs[i] = -g[i];
       c.sync();
       return 0;
@@ -713,6 +875,7 @@ struct Step {
     if (c.lane == 0) S.k0 = bmv(S.sy, S.wt, col, S.c, S.v) ? -8 : 0;
     c.sync();
     if (S.k0) return S.k0;
+    BO_UNROLL4
     for (int i = c.lane; i < nfree; i += C::NL) {
       const int k = index[i];
       double acc = -theta * (z[k] - x[k]) - g[k];
@@ -729,18 +892,25 @@ struct Step {
     const int nsub = S.i[I_NFREE];
     const double theta = S.d[D_THETA];
     if (nsub <= 0) return 0;
-    for (int j = 0; j < col; ++j) {
-      const double *wy = WY(j), *ws = WS(j);
-      double a = 0.0, b = 0.0;
-      for (int i = c.lane; i < nsub; i += C::NL) {
-        a += wy[index[i]] * rs[i];
-        b += ws[index[i]] * rs[i];
-      }
-      a = c.sum(a);
-      b = c.sum(b);
-      if (c.lane == 0) {
-        S.wv[j] = a;
-        S.wv[col + j] = theta * b;
+    if constexpr (WIDE) {
+      wdots<true>(rs, nsub, S.wv);
+      if (c.lane == 0)
+        for (int j = 0; j < col; ++j) S.wv[col + j] *= theta;
+    } else {
+      for (int j = 0; j < col; ++j) {
+        const double *wy = WY(j), *ws = WS(j);
+        double a = 0.0, b = 0.0;
+        BO_UNROLL4
+        for (int i = c.lane; i < nsub; i += C::NL) {
+          a += wy[index[i]] * rs[i];
+          b += ws[index[i]] * rs[i];
+        }
+        a = c.sum(a);
+        b = c.sum(b);
+        if (c.lane == 0) {
+          S.wv[j] = a;
+          S.wv[col + j] = theta * b;
+        }
       }
     }
     c.sync();
@@ -756,14 +926,17 @@ struct Step {
     if (S.k0) return S.k0;
     const double rtheta = 1.0 / theta;
     double iword = 0.0;
+    BO_UNROLL4
     for (int i = c.lane; i < nsub; i += C::NL) {
       const int k = index[i];
       double acc = rs[i];
       for (int jy = 0; jy < col; ++jy) acc = acc + WY(jy)[k] * S.wv[jy] / theta + WS(jy)[k] * S.wv[col + jy];
       rs[i] = acc * rtheta;
     }
+    BO_UNROLL4
     for (int i = c.lane; i < n; i += C::NL) xp[i] = z[i];
     c.sync();
+    BO_UNROLL4
     for (int i = c.lane; i < nsub; i += C::NL) {  // projected Newton point
       const int k = index[i];
       const double dk = rs[i];
@@ -788,14 +961,17 @@ struct Step {
     c.sync();
     if (iword == 0.0) return 0;
     double ddp = 0.0;
+    BO_UNROLL4
     for (int i = c.lane; i < n; i += C::NL) ddp += (z[i] - x[i]) * g[i];
     ddp = c.sum(ddp);
     if (!(ddp > 0.0)) return 0;
     // positive directional derivative of the projection: the backtracking step
+    BO_UNROLL4
     for (int i = c.lane; i < n; i += C::NL) z[i] = xp[i];
     c.sync();
     double cand = __builtin_inf();
     int ibd = nsub;
+    BO_UNROLL4
     for (int i = c.lane; i < nsub; i += C::NL) {
       const int k = index[i];
       const double dk = rs[i];
@@ -830,6 +1006,7 @@ struct Step {
       }
     }
     c.sync();
+    BO_UNROLL4
     for (int i = c.lane; i < nsub; i += C::NL) z[index[i]] += alpha * rs[i];
     c.sync();
     return 0;
@@ -838,12 +1015,14 @@ struct Step {
   // trial point of the line search: z at stp = 1, t + stp d otherwise
   BO_HD void write_trial() {
     const double stp = S.d[D_STP];
+    BO_UNROLL4
     for (int i = c.lane; i < n; i += C::NL) R.xt[i] = (stp == 1.0) ? z[i] : stp * dd[i] + t[i];
   }
 
   // line-search failure or ascent direction: restore the iterate; stop
   // without memory, else refresh it and recompute the direction
   BO_HD bool restore_or_refresh() {
+    BO_UNROLL4
     for (int i = c.lane; i < n; i += C::NL) {
       x[i] = t[i];
       g[i] = r[i];
@@ -864,6 +1043,7 @@ struct Step {
       const int col = S.i[I_COL];
       const bool unconstrained = !cnstnd && col > 0;
       if (unconstrained) {
+        BO_UNROLL4
         for (int i = c.lane; i < n; i += C::NL) {
           z[i] = x[i];
           index[i] = i;
@@ -894,6 +1074,7 @@ struct Step {
         }
       }
       // lnsrlb (first entry)
+      BO_UNROLL4
       for (int i = c.lane; i < n; i += C::NL) dd[i] = z[i] - x[i];
       c.sync();
       const double dtd = dot(dd, dd);
@@ -904,6 +1085,7 @@ struct Step {
           stpmx = 1.0;
         } else {
           double sm = BIG;
+          BO_UNROLL4
           for (int i = c.lane; i < n; i += C::NL) {
             const double a1 = dd[i];
             const int nb = nbd(i);
@@ -920,6 +1102,7 @@ struct Step {
         }
       }
       const double stp = (S.i[I_ITER] == 0 && !boxed) ? fmin(1.0 / dnorm, stpmx) : 1.0;
+      BO_UNROLL4
       for (int i = c.lane; i < n; i += C::NL) {
         t[i] = x[i];
         r[i] = g[i];
@@ -961,6 +1144,7 @@ struct Step {
 
   // ---- matupd + formt after an accepted step ----
   BO_HD void update() {
+    BO_UNROLL4
     for (int i = c.lane; i < n; i += C::NL) r[i] = g[i] - r[i];
     c.sync();
     const double rr = dot(r, r);
@@ -972,6 +1156,7 @@ struct Step {
       ddum = -gdold;
     } else {
       dr = (gd - gdold) * stp;
+      BO_UNROLL4
       for (int i = c.lane; i < n; i += C::NL) dd[i] *= stp;
       ddum = -gdold * stp;
     }
@@ -990,6 +1175,7 @@ struct Step {
     c.sync();
     const int col = S.i[I_COL];
     const int itail = S.i[I_ITAIL];
+    BO_UNROLL4
     for (int i = c.lane; i < n; i += C::NL) {
       R.ws[(long)itail * n + i] = dd[i];
       R.wy[(long)itail * n + i] = r[i];
@@ -1004,12 +1190,21 @@ struct Step {
       }
     }
     c.sync();
-    for (int j = 0; j < col - 1; ++j) {  // new row of SY, new column of SS
-      const double a = dot(dd, WY(j));
-      const double b = dot(WS(j), dd);
-      if (c.lane == 0) {
-        S.sy[(col - 1) + j * MMAX] = a;
-        S.ss[j + (col - 1) * MMAX] = b;
+    if constexpr (WIDE) {  // new row of SY, new column of SS
+      wdots<false>(dd, n, S.wbp);  // (the Cauchy search's scratch, free here)
+      if (c.lane == 0)
+        for (int j = 0; j < col - 1; ++j) {
+          S.sy[(col - 1) + j * MMAX] = S.wbp[j];
+          S.ss[j + (col - 1) * MMAX] = S.wbp[col + j];
+        }
+    } else {
+      for (int j = 0; j < col - 1; ++j) {
+        const double a = dot(dd, WY(j));
+        const double b = dot(WS(j), dd);
+        if (c.lane == 0) {
+          S.sy[(col - 1) + j * MMAX] = a;
+          S.ss[j + (col - 1) * MMAX] = b;
+        }
       }
     }
     if (c.lane == 0) {
@@ -1035,6 +1230,7 @@ struct Step {
       S.wt[k] = R.mat[2 * MMAX * MMAX + k];
     }
     double anyb = 0.0, allbox = 1.0;
+    BO_UNROLL4
     for (int i = c.lane; i < n; i += C::NL) {
       const int nb = nbd(i);
       if (nb != 0) anyb = 1.0;
@@ -1045,11 +1241,13 @@ struct Step {
     c.sync();
     const int phase = S.i[I_PHASE];
     if (phase == PH_STOP) {
+      BO_UNROLL4
       for (int i = c.lane; i < n; i += C::NL) R.xt[i] = x[i];
       return;
     }
     const double fnew = R.f_new;
     double finite = (fnew - fnew == 0.0) ? 1.0 : 0.0;
+    BO_UNROLL4
     for (int i = c.lane; i < n; i += C::NL) {
       const double gi = R.g_new[i];
       if (!(gi - gi == 0.0)) finite = 0.0;
@@ -1057,6 +1255,7 @@ struct Step {
     finite = c.min(finite);
     tick(0);
     if (phase == PH_START) {
+      BO_UNROLL4
       for (int i = c.lane; i < n; i += C::NL) {
         x[i] = R.xt[i];
         g[i] = R.g_new[i];
@@ -1083,6 +1282,7 @@ struct Step {
           direction();
       }
     } else {  // PH_LNSRCH: x <- the trial point
+      BO_UNROLL4
       for (int i = c.lane; i < n; i += C::NL) {
         x[i] = R.xt[i];
         g[i] = R.g_new[i];
@@ -1093,6 +1293,7 @@ struct Step {
       }
       c.sync();
       if (finite == 0.0) {  // a non-finite trial value: keep the last iterate
+        BO_UNROLL4
         for (int i = c.lane; i < n; i += C::NL) {
           x[i] = t[i];
           g[i] = r[i];
@@ -1145,6 +1346,7 @@ struct Step {
     c.sync();
     tick(6);
     if (S.i[I_PHASE] == PH_STOP)
+      BO_UNROLL4
       for (int i = c.lane; i < n; i += C::NL) R.xt[i] = x[i];
     for (int k = c.lane; k < DSLOTS; k += C::NL) R.ds[k] = S.d[k];
     for (int k = c.lane; k < ISLOTS; k += C::NL) R.is[k] = S.i[k];

@@ -33,7 +33,7 @@ def build_host():
                         _SRC[0]], check=True)
     lib = ctypes.CDLL(HOST_SO)
     P = ctypes.c_void_p
-    for fn in (lib.bo_lbfgsb_host_step, lib.bo_lbfgsb_host_step_lanes):
+    for fn in (lib.bo_lbfgsb_host_step, lib.bo_lbfgsb_host_step_lanes, lib.bo_lbfgsb_host_step_wide):
         fn.restype = ctypes.c_int
         fn.argtypes = ([ctypes.c_int] * 5 + [ctypes.c_double] * 2 + [P, P, P, ctypes.c_double]
                        + [P] * 8)
@@ -62,12 +62,14 @@ def scipy_trials(fun_and_grad, x0, bounds, maxiter=15000, maxcor=10, ftol=2.2204
 
 class HostLbfgsb:
     """One restart of the host build; ``run`` returns (trial points, x, f, status, nit).
-    ``lanes=True``: the 64-thread emulation of the kernel's wave."""
+    ``lanes=True``: the 64-thread emulation of the kernel's wave; ``lanes="wide"``:
+    128 threads as two waves, the kernel's workgroup-wide (joint-problem) paths."""
 
     def __init__(self, n, m=10, maxls=20, maxiter=15000, maxfun=15000,
                  ftol=2.2204460492503131e-09, gtol=1e-05, lower=None, upper=None, lanes=False):
         self.lib = build_host()
-        self._step = self.lib.bo_lbfgsb_host_step_lanes if lanes else self.lib.bo_lbfgsb_host_step
+        self._step = (self.lib.bo_lbfgsb_host_step_wide if lanes == "wide" else
+                      self.lib.bo_lbfgsb_host_step_lanes if lanes else self.lib.bo_lbfgsb_host_step)
         lay = (ctypes.c_int * 6)()
         self.lib.bo_lbfgsb_host_layout(lay)
         nv, niv, nmat, nd, ni, _ = list(lay)
