@@ -172,6 +172,7 @@ inline size_t staged_bytes(int n, int m) {
 constexpr size_t STAGE_LIMIT = 64 * 1024 - sizeof(bolb::Shared);  // dynamic LDS budget
 constexpr int JOINT_N = 1024;  // wider restarts run on a JOINT_W-wave workgroup
 constexpr int JOINT_W = 8;
+constexpr int JOINT_TB_LDS = 16384;  // breakpoints of a wide restart up to 128 KB of LDS
 
 // One wave per restart.  With `staged`, the restart's vectors and ring are
 // copied into LDS for the launch (coalesced, once) and back at the end: every
@@ -212,7 +213,7 @@ __global__ __launch_bounds__(64 * NW) void lbfgsb_kernel(bolb::Problem P, double
                   ds + b * bolb::DSLOTS,
                   is + b * bolb::ISLOTS};
   const long nv = bolb::V_COUNT * n, nr = m * n, ni = bolb::IV_COUNT * n;
-  if (staged) {
+  if (staged == 1) {
     double* lv = lds_dyn;
     double* lws = lv + nv;
     double* lwy = lws + nr;
@@ -229,6 +230,7 @@ __global__ __launch_bounds__(64 * NW) void lbfgsb_kernel(bolb::Problem P, double
     R.wy = lwy;
     R.iv = liv;
   }
+  if (staged == 2) R.tb_scratch = lds_dyn;  // the breakpoints in LDS (wide, unstaged)
   if constexpr (NW == 1) {
     WaveCtx c{lane};
     bolb::Step<WaveCtx> st(c, P, R, S);
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(64 * NW) void lbfgsb_kernel(bolb::Problem P, double
     bolb::Step<BlockCtx<NW>> st(c, P, R, S);
     st.run(P.prof ? P.prof + b * bolb::PROF_SLOTS : nullptr);
   }
-  if (staged) {
+  if (staged == 1) {
     __syncthreads();
     for (long k = lane; k < nv; k += NL) gv[k] = R.v[k];
     for (long k = lane; k < nr; k += NL) {
@@ -304,9 +306,19 @@ extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int m
   if (n <= JOINT_N)
     lbfgsb_kernel<1><<<B, 64, staged ? bytes : 0, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws, wy,
                                                                        mat, ds, is, staged);
-  else
-    lbfgsb_kernel<JOINT_W><<<B, 64 * JOINT_W, staged ? bytes : 0, as_stream(stream)>>>(
-        P, xt, ft, gt, v, iv, ws, wy, mat, ds, is, staged);
+  else {
+    // an unstaged wide restart keeps the Cauchy breakpoints in LDS (staged = 2)
+    const int mode = staged ? 1 : (n <= JOINT_TB_LDS ? 2 : 0);
+    const size_t dyn = mode == 1 ? bytes : (mode == 2 ? sizeof(double) * (size_t)n : 0);
+    static std::once_flag once;
+    std::call_once(once, [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lbfgsb_kernel<JOINT_W>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(sizeof(double) * JOINT_TB_LDS));
+    });
+    lbfgsb_kernel<JOINT_W><<<B, 64 * JOINT_W, dyn, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws,
+                                                                         wy, mat, ds, is, mode);
+  }
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

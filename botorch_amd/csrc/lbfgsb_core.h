@@ -96,6 +96,9 @@ struct Restart {   // global buffers of one restart
   double* mat;     // NMAT x MMAX*MMAX
   double* ds;      // DSLOTS
   int* is;         // ISLOTS
+  // the Cauchy search's breakpoints (n doubles, scratch of one call): the
+  // V_TB vector unless the caller gives faster memory (the wide kernel: LDS)
+  double* tb_scratch = nullptr;
 };
 
 struct Shared {    // block-shared record (LDS on the device)
@@ -379,7 +382,8 @@ struct Step {
       : c(c_), P(P_), R(R_), S(S_), n(P_.n), m(P_.m) {
     x = R.v + (long)V_X * n;   g = R.v + (long)V_G * n;   t = R.v + (long)V_T * n;
     r = R.v + (long)V_R * n;   z = R.v + (long)V_Z * n;   dd = R.v + (long)V_D * n;
-    dc = R.v + (long)V_DC * n; tb = R.v + (long)V_TB * n; rs = R.v + (long)V_RS * n;
+    dc = R.v + (long)V_DC * n;
+    tb = R.tb_scratch ? R.tb_scratch : R.v + (long)V_TB * n; rs = R.v + (long)V_RS * n;
     xp = R.v + (long)V_XP * n;
     iwhere = R.iv + (long)IV_WHERE * n;
     index = R.iv + (long)IV_INDEX * n;
