@@ -1470,7 +1470,11 @@ std::vector<int4> build_tasks_batched(int T, int nb) {
   const std::vector<int4> one = (nb == 1 || T <= 32) ? build_tasks(T, 2, 4) : build_tasks(T, CH, CHB);
   if (nb == 1) return one;
   double stagger = 0.0;
-  if (const char* e = getenv("BO_CHOL_BATCH_STAGGER")) stagger = atof(e);
+  if (const char* e = getenv("BO_CHOL_BATCH_STAGGER")) {  // finite values only (sort keys)
+    char* end = nullptr;
+    const double v = strtod(e, &end);
+    if (end != e && std::isfinite(v)) stagger = v;
+  }
   const double shift = stagger * (double)one.size() / nb;
   std::vector<std::pair<double, int4>> keyed;
   keyed.reserve(one.size() * nb);

@@ -117,6 +117,25 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   // load rounds on 64 threads.
   const int E = q * q;
   const int nsplit = THREADS / E;  // >= 1 (q <= 16)
+  // K** of this thread's entry first: its row loads are in flight with the
+  // partials' below instead of after them
+  double kxx = 0.0;
+  if (tid < E) {
+    const int a = tid / q, c = tid % q;
+    if (a == c) {
+      kxx = outputscale;
+    } else {
+      const double* xa = Xq + (int64_t)(row0 + a) * DP;
+      const double* xc = Xq + (int64_t)(row0 + c) * DP;
+      double d2 = 0.0;
+#pragma unroll
+      for (int t = 0; t < DP; ++t) {
+        const double df = xa[t] - xc[t];
+        d2 = fma(df, df, d2);
+      }
+      kxx = outputscale * kernel_from_d2<KIND>(d2);
+    }
+  }
   if (tid < E * nsplit) {
     const int e = tid % E, j = tid / E;
     const int a = e / q, c = e % q;
@@ -144,20 +163,6 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     const int a = tid / q, c = tid % q;
     double acc = 0.0;
     for (int j = 0; j < nsplit; ++j) acc += psum[j * E + tid];
-    double kxx;
-    if (a == c) {
-      kxx = outputscale;
-    } else {
-      const double* xa = Xq + (int64_t)(row0 + a) * DP;
-      const double* xc = Xq + (int64_t)(row0 + c) * DP;
-      double d2 = 0.0;
-#pragma unroll
-      for (int t = 0; t < DP; ++t) {
-        const double df = xa[t] - xc[t];
-        d2 = fma(df, df, d2);
-      }
-      kxx = outputscale * kernel_from_d2<KIND>(d2);
-    }
     double v = s2 * (kxx - acc);
     if (Tm != nullptr) {
       double tt = 0.0;
@@ -223,56 +228,62 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   __syncthreads();
   const int info = s_info;
   if (tid == 0) {
-    // agent-scope (write-through) stores: the fused status below reads them
-    // from other XCDs' workgroups without an L2 write-back fence
+    // agent-scope (write-through) stores: the fused status reads them from
+    // other XCDs' workgroups without an L2 write-back fence
     if (info_out) __hip_atomic_store(info_out + b, info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (jitter_out)
       __hip_atomic_store(jitter_out + b, s_jit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (status_out != nullptr) {
-    // The batch's ladder status (bo_ladder_status's [max info, max jitter])
-    // folded in: every workgroup publishes its entries and counts itself in;
-    // the last to arrive reduces all B of them and re-arms the counter.  The
-    // hand-off follows MI355X_MICROARCH.md's inter-workgroup recipe (as
-    // chol_dag.hip): write-through stores drained (vmcnt(0)) before the
-    // agent-scope count, agent-scope loads on the reading side -- an
-    // agent-scope release fence would write back the whole L2 per workgroup.
+  // The batch's ladder status (bo_ladder_status's [max info, max jitter])
+  // folded in at the workgroup's exit: every workgroup counts itself in once
+  // its entries are drained, the last to arrive reduces all B of them and
+  // re-arms the counter.  Counting at the exit keeps the counter's round trip
+  // (one address for the whole grid) off the sampling.  The hand-off follows
+  // MI355X_MICROARCH.md's inter-workgroup recipe (as chol_dag.hip):
+  // write-through stores drained (vmcnt(0)) before the agent-scope count,
+  // agent-scope loads on the reading side -- an agent-scope release fence
+  // would write back the whole L2 per workgroup.  Called by every thread.
+  auto status_arrive = [&]() {
+    if (status_out == nullptr) return;
+    __syncthreads();  // red / red2 free (the reduction below is done with them)
     if (tid == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       s_last = __hip_atomic_fetch_add(status_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                (int)gridDim.x - 1;
     }
     __syncthreads();
-    if (s_last) {
-      double mi = 0.0, mj = 0.0;
-      for (int bb = tid; bb < (int)gridDim.x; bb += THREADS) {
-        mi = fmax(mi, (double)__hip_atomic_load(info_out + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        mj = fmax(mj, __hip_atomic_load(jitter_out + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      }
-      for (int o = 32; o > 0; o >>= 1) {
-        mi = fmax(mi, __shfl_xor(mi, o));
-        mj = fmax(mj, __shfl_xor(mj, o));
-      }
-      if ((tid & 63) == 0) {
-        red[tid >> 6] = mi;
-        red2[tid >> 6] = mj;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        status_out[0] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
-        status_out[1] = fmax(fmax(red2[0], red2[1]), fmax(red2[2], red2[3]));
-        __hip_atomic_store(status_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();  // red / red2 are reused by the reduction below
+    if (!s_last) return;
+    double mi = 0.0, mj = 0.0;
+    for (int bb = tid; bb < (int)gridDim.x; bb += THREADS) {
+      mi = fmax(mi, (double)__hip_atomic_load(info_out + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      mj = fmax(mj, __hip_atomic_load(jitter_out + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     }
-  }
+    for (int o = 32; o > 0; o >>= 1) {
+      mi = fmax(mi, __shfl_xor(mi, o));
+      mj = fmax(mj, __shfl_xor(mj, o));
+    }
+    if ((tid & 63) == 0) {
+      red[tid >> 6] = mi;
+      red2[tid >> 6] = mj;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      status_out[0] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+      status_out[1] = fmax(fmax(red2[0], red2[1]), fmax(red2[2], red2[3]));
+      __hip_atomic_store(status_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
   if (L_out && tid < q * q) {
     const int a = tid / q, c = tid % q;
     L_out[((int64_t)b * q + a) * q + c] = info ? NAN : Lq[a][c];
   }
-  if (MODE == QMC_CHOL) return;
+  if (MODE == QMC_CHOL) {
+    status_arrive();
+    return;
+  }
   if (info) {
     if (tid == 0) acq[b] = NAN;
+    status_arrive();
     return;
   }
 
@@ -316,6 +327,7 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
       for (int w = 0; w < THREADS / 64; ++w) t = lse_merge(t, LseAcc{red[w], red2[w]});
       acq[b] = t.m + log(t.s) - log((double)S);
     }
+    status_arrive();
     return;
   }
   for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
@@ -326,6 +338,7 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     for (int w = 0; w < THREADS / 64; ++w) t += red[w];
     acq[b] = t / S;
   }
+  status_arrive();
 }
 
 struct QmcArgs {

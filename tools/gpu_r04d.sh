@@ -1,0 +1,10 @@
+#!/bin/bash
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/r04d
+mkdir -p $O
+timeout -k 10 200 python3 tools/time_qmc_phases.py > $O/qmc_phases.log 2>&1 || exit $?
+cat $O/qmc_phases.log
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_acquisition.py tests/test_gpu_graphs.py tests/test_gpu_logei.py tests/test_gpu_full_configs.py -m gpu -q -x --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+tail -3 $O/pytest.log
