@@ -12,10 +12,14 @@ buffer, replays the graph and returns the captured outputs.
 
 The reference has no counterpart (it evaluates eagerly through gpytorch); the
 values are the eager path's, bit for bit (tests/test_gpu_graphs.py).  The
-jitter-ladder status of a replay is kept on the device and checked at the next
-call (``check_each_call``) or by ``check_status()`` (the same deferral as the
-eager forward-only path, kernels.raise_not_psd_deferred; the device optimiser
-checks it at its own status reads only).
+jitter-ladder status never stalls a replay: the graph folds every replay's
+[max info, max jitter] into a sticky device maximum and copies it to pinned
+host memory as its last node; an event follows each replay.  With
+``check_each_call`` a call acts on the status as soon as a finished replay has
+published it (an event query, no wait: the host keeps issuing while the GPU
+runs); ``check_status()`` waits for the last replay and acts (the device
+optimiser's status reads).  NotPSDError / the jitter warning are raised as
+[G] psd_safe_cholesky's are, a call or two late instead of one.
 
 Constraints of capture: the model's caches, the Sobol base samples and the
 split plans must exist before capture (two eager warm-up calls build them),
@@ -53,10 +57,19 @@ class GraphedAcquisition:
         torch.cuda.current_stream(self.dev).wait_stream(side)
         kernels.check_ladder_status(self.dev)
         self.graph = torch.cuda.CUDAGraph()
-        with kernels.capturing(self.dev):
+        self._sticky = torch.zeros(2, dtype=torch.float64, device=self.dev)
+        self._host = torch.zeros(2, dtype=torch.float64).pin_memory()
+        self._what = None
+        with kernels.capturing(self.dev) as cap:
             with torch.cuda.graph(self.graph):
                 self.out = self._body()
-        self._status = kernels.take_captured_status(self.dev)
+                st = kernels._CAPTURE.get(cap.idx)
+                if st is not None:  # the replay's status: sticky max, then to the host
+                    torch.maximum(self._sticky, st[0], out=self._sticky)
+                    self._host.copy_(self._sticky, non_blocking=True)
+        taken = kernels.take_captured_status(self.dev)
+        self._what = taken[1] if taken is not None else None
+        self._event = torch.cuda.Event()
         self._pending = False
 
     def _key(self):
@@ -73,13 +86,29 @@ class GraphedAcquisition:
         with torch.no_grad():
             return self.acqf(self.X)
 
+    def _act(self) -> None:
+        """The replays' status published to the host so far (sticky max):
+        raise / warn, and re-arm the device maximum after a warning."""
+        info_max, jitter_max = float(self._host[0]), float(self._host[1])
+        if info_max > 0 or jitter_max > 0:
+            if info_max <= 0:  # a warning is given once per jittered stretch
+                self._sticky.zero_()
+                self._host.zero_()
+            kernels._ladder_outcome(info_max, jitter_max, self._what)
+
     def check_status(self) -> None:
-        """Raise NotPSDError / warn for the last replay's jitter ladder."""
-        if self._pending and self._status is not None:
+        """Wait for the last replay, then raise NotPSDError / warn for the
+        jitter ladders of the replays so far."""
+        if self._pending and self._what is not None:
+            self._event.synchronize()
             self._pending = False
-            packed, what = self._status
-            vals = packed.cpu()
-            kernels._ladder_outcome(float(vals[0]), float(vals[1]), what)
+            self._act()
+
+    def _poll(self) -> None:
+        """The same without waiting: acts only once the last replay finished."""
+        if self._pending and self._what is not None and self._event.query():
+            self._pending = False
+            self._act()
 
     def __call__(self, X: torch.Tensor):
         if X.shape != self.X.shape:
@@ -87,9 +116,10 @@ class GraphedAcquisition:
         if self._key() != self._model_key:
             raise RuntimeError("the model changed since capture; build a new GraphedAcquisition")
         if self.check_each_call:
-            self.check_status()  # the previous replay's ladder (one call behind)
+            self._poll()  # a finished replay's ladder status, without stalling this call
         self.X.copy_(X.detach())
         self.graph.replay()
+        self._event.record(torch.cuda.current_stream(self.dev))
         self._pending = True
         return self.out
 

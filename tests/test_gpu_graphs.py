@@ -74,3 +74,42 @@ def test_graphed_rejects_changed_model_and_shape():
     m.likelihood.noise = torch.tensor([2e-3], dtype=torch.float64)
     with pytest.raises(RuntimeError):
         ga(X)
+
+
+def test_graphed_forward_status_without_stalls():
+    """A replay never waits on the previous one's ladder status: a call acts
+    on it once a finished replay has published it to pinned memory (event
+    query), check_status() waits.  A jittered q x q root (duplicated rows at
+    training points of a noiseless model) still reaches the caller as the
+    NumericalWarning [G] psd_safe_cholesky gives, and a clean batch after the
+    warning re-arms silently."""
+    import warnings
+    from botorch_amd import kernels
+    from botorch_amd.acquisition import qExpectedImprovement
+    from botorch_amd.exceptions import NumericalWarning
+    from botorch_amd.graphs import GraphedAcquisition
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from tests.test_gpu_acquisition import _setup
+    X, Y, m, orc = _setup(n=64, noise=1e-4)
+    m.likelihood.noise = torch.tensor([1e-12], dtype=torch.float64)
+    m.eval()
+    acqf = qExpectedImprovement(m, Y.max().item(), sampler=SobolQMCNormalSampler(torch.Size([32]), seed=0))
+    bad = X[:3].unsqueeze(1).repeat(1, 2, 1).to(DEV)   # singular 2 x 2 covariances
+    good = torch.rand(3, 2, 6, dtype=torch.float64).to(DEV)
+    kernels.check_ladder_status()
+    ga = GraphedAcquisition(acqf, good)
+    with warnings.catch_warnings(record=True) as ws:
+        warnings.simplefilter("always")
+        ga(good)
+        ga.check_status()
+        assert not any(issubclass(w.category, NumericalWarning) for w in ws)
+        ga(bad)
+        torch.cuda.synchronize()
+        ga(good)  # the finished bad replay is seen here, without a wait
+        assert any(issubclass(w.category, NumericalWarning) for w in ws)
+        n_warn = sum(issubclass(w.category, NumericalWarning) for w in ws)
+        ga.check_status()  # the good replay after the re-arm: nothing new
+        for _ in range(3):
+            ga(good)
+        ga.check_status()
+        assert sum(issubclass(w.category, NumericalWarning) for w in ws) == n_warn
