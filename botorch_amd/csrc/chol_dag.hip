@@ -1066,6 +1066,127 @@ __device__ bool batched_update(const Ctx& c, const Flags& f, int kb, int nk, int
   return true;
 }
 
+// The same batched update with the operand tiles prefetched two steps ahead
+// (round 4): the chunk's (row, step) pairs form one stream e = (i - i0) nk + g;
+// while step e's MFMAs run, the operand of e + 2 is in flight into the
+// register slot step e just committed to LDS (two slots, e & 1; the slot is a
+// compile-time index: the stream is walked two elements per iteration).  A
+// sc1 operand load takes longer than one 64 x 64 x 64 step of MFMAs (round 3
+// trace: ~0.9 us of every step waited on it); two steps cover it.  The next
+// row's C tile goes with its first operand; rows are only prefetched when
+// the poll at the last waited row start found them ready (as batched_update).
+template <int KIND>
+__device__ bool batched_update2(const Ctx& c, const Flags& f, int kb, int nk, int j, int i0, int i1,
+                                double* X0, double* XB0, double* XB1, double* XB2, int* s_ok,
+                                int* s_rdy, long long* wsum) {
+  auto XB = [&](int g) { return g == 0 ? XB0 : (g == 1 ? XB1 : XB2); };
+  const rsrc_t rc = KIND == 1 ? c.rA : c.rI;
+  u32* const fC = KIND == 1 ? f.fA : f.fX;
+  const u32 v0 = KIND == 1 ? (u32)kb : (u32)(kb - j);
+  const u32 v1 = v0 + (u32)nk;
+  const double sgn = KIND == 1 ? -1.0 : 1.0;
+  const int ke = kb + nk;
+  const int E = (i1 - i0) * nk;
+  double2 pv0[8], pv1[8];
+  double pa[16];
+  Acc acc;
+  int issued = 0;  // stream elements whose loads are issued (a prefix)
+  int mask = 0;    // bit r: row i + r found ready by the last poll
+  auto own = [&](int i) { return KIND == 2 || i != j; };
+  auto issue_a = [&](double2 (&pv)[8], int i, int k) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int e = c.tid + 256 * p;
+      pv[p] = ld16(c.rA, toff(c, i, k, e >> 5, (e & 31) * 2));
+    }
+  };
+  auto issue_c = [&](int i) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          pa[8 * a + 4 * b + q] = ld8(rc, toff(c, i, j, c.wm + 16 * a + mfma_row(c.lane, q),
+                                               c.wn + 16 * b + mfma_col(c.lane)));
+  };
+  bool ok = true;
+  // one stream element in register slot S (the other slot: O)
+  auto step = [&](int e, double2 (&pvS)[8], double2 (&pvO)[8]) {
+    const int r = e / nk, g = e - r * nk, i = i0 + r;
+    if (g == 0) {
+      if (issued <= e) {  // not prefetched: wait for the row, then its C and two operands
+        if (!wait2(c, f.at(f.fL, i, ke - 1), 1u, f.at(fC, i, j), v0, f.abortw, s_ok, wsum)) {
+          ok = false;
+          return;
+        }
+        issue_c(i);
+        if (own(i)) issue_a(pvS, i, kb);
+        issued = e + 1;
+        if (nk > 1) {
+          if (own(i)) issue_a(pvO, i, kb + 1);
+          issued = e + 2;
+        }
+        if (c.tid == 0) {
+          int m = 0;
+          for (int ii = i + 1; ii < i1 && ii < i + 31; ++ii) {
+            if (flag_load(f.at(f.fL, ii, ke - 1)) >= 1u && flag_load(f.at(fC, ii, j)) >= v0)
+              m |= 1 << (ii - i);
+            else
+              break;
+          }
+          s_rdy[i & 1] = m;
+        }
+        __syncthreads();
+        mask = s_rdy[i & 1];
+      } else {
+        mask >>= 1;  // this row was prefetched: the last poll's word, one row on
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc.t[a][b][q] = pa[8 * a + 4 * b + q];
+    }
+    if (own(i)) {
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        const int x = c.tid + 256 * p;
+        *reinterpret_cast<double2*>(X0 + (x >> 5) * LP + (x & 31) * 2) = pvS[p];
+      }
+      __syncthreads();
+    }
+    // element e + 2 into the slot just committed: this row, or the next one
+    // when the poll found it ready (its C tile with its first operand; this
+    // row's C was taken at its start)
+    const int e2 = e + 2;
+    if (e2 < E && issued == e2) {
+      const int r2 = e2 / nk, g2 = e2 - r2 * nk, i2 = i0 + r2;
+      if (r2 == r || (r2 == r + 1 && (mask & 2))) {
+        if (g2 == 0) issue_c(i2);
+        if (own(i2)) issue_a(pvS, i2, kb + g2);
+        issued = e2 + 1;
+      }
+    }
+    acc_mma_nt(c, acc, own(i) ? X0 : XB(g), XB(g), sgn);
+    __syncthreads();  // X0 free for the next element's operand
+    if (g == nk - 1) {
+      acc_store(c, acc, rc, i, j);
+      publish(c, f.at(fC, i, j), v1);
+    }
+  };
+  for (int e = 0; e < E; e += 2) {
+    step(e, pv0, pv1);
+    if (!ok) return false;
+    if (e + 1 < E) {
+      step(e + 1, pv1, pv0);
+      if (!ok) return false;
+    }
+  }
+  return true;
+}
+
 // nb > 1: nb independent matrices (A + m * np^2, Linv + m * np^2, info[m], flag
 // block m) share the launch; each task names its matrix in bits 9-15 of x, and
 // the queue interleaves the matrices' own queues, so one matrix's diagonal
@@ -1074,7 +1195,8 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
                                                        int np, int T, const int4* __restrict__ tasks,
                                                        int ntasks, u32* __restrict__ flags,
                                                        int* __restrict__ info,
-                                                       long long* __restrict__ trace, int nb) {
+                                                       long long* __restrict__ trace, int nb,
+                                                       int pf2) {
   __shared__ __attribute__((aligned(16))) double X0[TB * LP];
   __shared__ __attribute__((aligned(16))) double X1[TB * LP];
   __shared__ __attribute__((aligned(16))) double X2[TB * LP];  // batched update operands
@@ -1189,7 +1311,8 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
         for (int g = 0; g < nk; ++g)  // L_jk of the batch
           tile_to_lds(c, c.rA, j, k + g, g == 0 ? X1 : (g == 1 ? X2 : X3));
         __syncthreads();
-        ok = batched_update<1>(c, fl, k, nk, j, i0, i1, X0, X1, X2, X3, &s_ok, s_rdy, &wsum, ph);
+        ok = (pf2 && !ph) ? batched_update2<1>(c, fl, k, nk, j, i0, i1, X0, X1, X2, X3, &s_ok, s_rdy, &wsum)
+                          : batched_update<1>(c, fl, k, nk, j, i0, i1, X0, X1, X2, X3, &s_ok, s_rdy, &wsum, ph);
       }
     } else if (type == T_COLUPD) {
       ok = wait2(c, F(fL, j, k), 1u, F(fL, j, k), 1u, abortw, &s_ok, &wsum);
@@ -1203,7 +1326,8 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
         for (int g = 0; g < nk; ++g)  // X_kj transposed (X_jj = D_j)
           tile_to_lds_t(c, c.rI, k + g, j, g == 0 ? X1 : (g == 1 ? X2 : X3));
         __syncthreads();
-        ok = batched_update<2>(c, fl, k, nk, j, i0, i1, X0, X1, X2, X3, &s_ok, s_rdy, &wsum, ph);
+        ok = (pf2 && !ph) ? batched_update2<2>(c, fl, k, nk, j, i0, i1, X0, X1, X2, X3, &s_ok, s_rdy, &wsum)
+                          : batched_update<2>(c, fl, k, nk, j, i0, i1, X0, X1, X2, X3, &s_ok, s_rdy, &wsum, ph);
       }
     } else {  // T_XSTEP: column j of X at step k
       if (k == j) {
@@ -1538,8 +1662,13 @@ int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipS
   // one workgroup per CU: two per CU (74 KB of LDS each fits) measured slower,
   // 2.35 -> 2.97 ms at n = 4096 -- the sc1 tile traffic, not latency, is the limit
   const int grid = cus < tb->n ? cus : tb->n;
+  // BO_CHOL_PREFETCH2 (default 1): batched updates prefetch two steps ahead
+  static const int pf2 = [] {
+    const char* e = getenv("BO_CHOL_PREFETCH2");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
   chol_dag_kernel<<<grid, 256, 0, st>>>(A, Linv, (int)np, T, tb->dev, tb->n, (u32*)work, info,
-                                          trace, nb);
+                                          trace, nb, pf2);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
