@@ -307,14 +307,7 @@ __device__ __forceinline__ bool wait2(const Ctx& c, const u32* f1, u32 t1, const
 }
 
 // ---- the diagonal tile ------------------------------------------------------------
-// v broadcast from lane K of each 16-lane row (DPP row_newbcast on gfx950).
-template <int K>
-__device__ __forceinline__ double row_bcast(double v) {
-  const long long x = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_mov_dpp((int)(x & 0xffffffffll), 0x150 + K, 0xf, 0xf, true);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(x >> 32), 0x150 + K, 0xf, 0xf, true);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
+// (row_bcast<K>: lane K of each 16-lane row to the whole row, common.h)
 
 #ifdef BO_TOOLS  // the round-2 four-panel diagonal tile: timing reference of tools/probe_potrf64.py
 template <int JJ, int M>

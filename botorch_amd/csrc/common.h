@@ -37,6 +37,15 @@ __device__ __forceinline__ v4d mfma_f64(double a, double b, v4d c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// v broadcast from lane K of each 16-lane row (DPP row_newbcast on gfx950).
+template <int K>
+__device__ __forceinline__ double row_bcast(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(x & 0xffffffffll), 0x150 + K, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(x >> 32), 0x150 + K, 0xf, 0xf, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 __device__ __forceinline__ v4d v4d_zero() {
   v4d z = {0.0, 0.0, 0.0, 0.0};
   return z;

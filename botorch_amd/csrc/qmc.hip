@@ -33,6 +33,41 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 constexpr int DP = 8;
 constexpr int THREADS = 256;
 
+// f + sum_{j >= J} Lr[j] z_j with z_j = lane j's z of this 16-lane row (DPP)
+template <int J>
+__device__ __forceinline__ double lq_chain(const double (&Lr)[QMAX], double z, double f) {
+  f = fma(Lr[J], row_bcast<J>(z), f);
+  if constexpr (J + 1 < QMAX) return lq_chain<J + 1>(Lr, z, f);
+  return f;
+}
+
+// max / sum over the 16 lanes of a row (xor shuffles inside the row)
+__device__ __forceinline__ double row_max16(double v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ double row_sum16(double v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// log_q_reduce (logred.h) across a 16-lane row: li of the active lanes
+__device__ __forceinline__ double row_log_q_reduce(double li, bool act, const LogRedParams& p) {
+  const double tau = p.tau_max;
+  const double M = row_max16(act ? li : -INFINITY);
+  if (p.fat) {
+    const double x = (M - li) / tau;
+    const double den = 2.0 + 2.0 * x + x * x;
+    const double P = row_sum16(act ? 2.0 / den : 0.0);
+    return M + tau * log(P);
+  }
+  const double Ms = M / tau;
+  const double ssum = row_sum16(act ? exp(li / tau - Ms) : 0.0);
+  return tau * (Ms + log(ssum));
+}
+
 enum QmcMode : int {
   QMC_POSTERIOR = 0,
   QMC_QEI = 1,
@@ -287,30 +322,38 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     return;
   }
 
-  // 3. samples and the reduction.
+  // 3. samples and the reduction.  Lane (grp = lane >> 4, a = lane & 15) of
+  // wave w holds row a of L_q in registers and takes test point a of sample
+  // s = s0 + 4 w + grp: z[s][a] is one coalesced load, z[s][j] reaches the
+  // row's lanes by DPP broadcast, f_a is the same FMA chain (j ascending) as
+  // the serial form, and the q-reductions are shuffles inside the 16-lane row.
+  // (The serial per-sample loop read L_q from LDS once per FMA: 22 us of C3's
+  // 38 us finalisation, profiles/r04/qmc.)
+  const int lane = tid & 63, a_ = lane & 15, grp = lane >> 4, wv = tid >> 6;
+  const bool arow = a_ < q;
+  double Lr[QMAX];
+#pragma unroll
+  for (int j = 0; j < QMAX; ++j) Lr[j] = (arow && j <= a_) ? Lq[a_][j] : 0.0;
+  const double mu_a = arow ? mu[a_] : 0.0;
   double sum = 0.0;
   LseAcc lse{-INFINITY, 0.0};
-  for (int s = tid; s < S; s += THREADS) {
-    const double* z = Z + (int64_t)s * q;
-    double zs[QMAX];
-#pragma unroll
-    for (int j = 0; j < QMAX; ++j) zs[j] = (j < q) ? z[j] : 0.0;
-    const double bf = per_sample_best(MODE) ? best_f_s[s] : best_f;
-    double vmax = 0.0;
-    double li[QMAX];
-#pragma unroll
-    for (int a = 0; a < QMAX; ++a) {
-      li[a] = 0.0;
-      if (a < q) {
-        double f = mu[a] + ((F != nullptr) ? F[(int64_t)s * ldF + row0 + a] : 0.0);
-#pragma unroll
-        for (int j = 0; j <= a; ++j) f = fma(Lq[a][j], zs[j], f);
-        if (log_mode(MODE)) li[a] = log_soft_relu(f - bf, lp, nullptr);
-        else vmax = fmax(vmax, f - bf);
-      }
+  for (int s0 = 0; s0 < S; s0 += THREADS / 16) {
+    const int s = s0 + 4 * wv + grp;
+    const bool sv = s < S;
+    const bool act = sv && arow;
+    const double z = act ? Z[(int64_t)s * q + a_] : 0.0;
+    double f = mu_a + ((F != nullptr && act) ? F[(int64_t)s * ldF + row0 + a_] : 0.0);
+    f = lq_chain<0>(Lr, z, f);
+    const double bf = per_sample_best(MODE) ? (sv ? best_f_s[s] : 0.0) : best_f;
+    if (log_mode(MODE)) {
+      const double li = act ? log_soft_relu(f - bf, lp, nullptr) : -INFINITY;
+      const double u = row_log_q_reduce(li, act, lp);
+      if (a_ == 0 && sv) lse = lse_push(lse, u);
+    } else {
+      // max_a relu(f_a - best_f) = relu(max_a (f_a - best_f)): fmax is exact
+      const double v = row_max16(act ? f - bf : -INFINITY);
+      if (a_ == 0 && sv) sum += fmax(v, 0.0);
     }
-    if (log_mode(MODE)) lse = lse_push(lse, log_q_reduce<QMAX>(li, q, lp, nullptr));
-    else sum += vmax;
   }
   if (log_mode(MODE)) {
     for (int o = 32; o > 0; o >>= 1) {
