@@ -337,22 +337,35 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   const double mu_a = arow ? mu[a_] : 0.0;
   double sum = 0.0;
   LseAcc lse{-INFINITY, 0.0};
-  for (int s0 = 0; s0 < S; s0 += THREADS / 16) {
-    const int s = s0 + 4 * wv + grp;
-    const bool sv = s < S;
-    const bool act = sv && arow;
-    const double z = act ? Z[(int64_t)s * q + a_] : 0.0;
-    double f = mu_a + ((F != nullptr && act) ? F[(int64_t)s * ldF + row0 + a_] : 0.0);
-    f = lq_chain<0>(Lr, z, f);
-    const double bf = per_sample_best(MODE) ? (sv ? best_f_s[s] : 0.0) : best_f;
-    if (log_mode(MODE)) {
-      const double li = act ? log_soft_relu(f - bf, lp, nullptr) : -INFINITY;
-      const double u = row_log_q_reduce(li, act, lp);
-      if (a_ == 0 && sv) lse = lse_push(lse, u);
-    } else {
-      // max_a relu(f_a - best_f) = relu(max_a (f_a - best_f)): fmax is exact
-      const double v = row_max16(act ? f - bf : -INFINITY);
-      if (a_ == 0 && sv) sum += fmax(v, 0.0);
+  // SB samples' loads per lane in flight at once (one L2 latency per SB
+  // samples instead of one per sample)
+  constexpr int SB = 8;
+  for (int s0 = 0; s0 < S; s0 += SB * (THREADS / 16)) {
+    double zb[SB], fb[SB], bb[SB];
+#pragma unroll
+    for (int u = 0; u < SB; ++u) {
+      const int s = s0 + u * (THREADS / 16) + 4 * wv + grp;
+      const bool act = s < S && arow;
+      zb[u] = act ? Z[(int64_t)s * q + a_] : 0.0;
+      fb[u] = (F != nullptr && act) ? F[(int64_t)s * ldF + row0 + a_] : 0.0;
+      bb[u] = per_sample_best(MODE) ? (s < S ? best_f_s[s] : 0.0) : best_f;
+    }
+#pragma unroll
+    for (int u = 0; u < SB; ++u) {
+      const int s = s0 + u * (THREADS / 16) + 4 * wv + grp;
+      const bool sv = s < S;
+      const bool act = sv && arow;
+      const double f = lq_chain<0>(Lr, zb[u], mu_a + fb[u]);
+      const double bf = bb[u];
+      if (log_mode(MODE)) {
+        const double li = act ? log_soft_relu(f - bf, lp, nullptr) : -INFINITY;
+        const double uu = row_log_q_reduce(li, act, lp);
+        if (a_ == 0 && sv) lse = lse_push(lse, uu);
+      } else {
+        // max_a relu(f_a - best_f) = relu(max_a (f_a - best_f)): fmax is exact
+        const double v = row_max16(act ? f - bf : -INFINITY);
+        if (a_ == 0 && sv) sum += fmax(v, 0.0);
+      }
     }
   }
   if (log_mode(MODE)) {

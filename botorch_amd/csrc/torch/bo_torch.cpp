@@ -14,15 +14,18 @@
 //
 // The jitter-ladder status of a forward-only call is deferred, as [G]
 // psd_safe_cholesky's host check would otherwise synchronise every call: the
-// status is reduced on the device and copied to pinned host memory behind an
-// event, and read one call later (or at the driver's own sync, bo::ladder_poll)
-// -- two slots per device, so reading call t-1's status never waits on call t.
+// status is reduced on the device into pinned host memory behind an event, and
+// read once that event has passed (a later call's query, or the driver's own
+// sync, bo::ladder_poll) -- a ring of slots per device, so a call waits on an
+// older one only when the whole ring is in flight.
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <array>
+#include <deque>
 #include <atomic>
 #include <mutex>
 #include <unordered_map>
@@ -49,16 +52,23 @@ void check_f64(const at::Tensor& t, const char* name) {
 }
 
 // ---- deferred ladder status ---------------------------------------------------------
+// A ring of NSLOT status slots per device.  A call enqueues its status into a
+// free slot behind an event and returns what the FINISHED calls reported
+// (event queries, no wait); it waits only when every slot is in flight, so the
+// host keeps issuing while the GPU runs (a failed root is reported within
+// NSLOT calls, or at bo::ladder_poll, which waits for all of them).
+constexpr int NSLOT = 4;
 struct Slot {
   double* host = nullptr;   // pinned [info_max, jitter_max]
   double* host_dev = nullptr;  // the same pinned words as a device pointer (zero-copy)
   double* dev = nullptr;    // device [info_max, jitter_max]
   int* count = nullptr;     // arrival counter of the fused status (qmc_kernel re-zeroes it)
   hipEvent_t ev = nullptr;
+  bool busy = false;
 };
 struct DeviceLadder {
-  std::array<Slot, 2> slot;
-  int pending = -1;  // slot of the forward whose status is still unread
+  std::array<Slot, NSLOT> slot;
+  std::deque<int> pending;  // slots in flight, oldest first
 };
 std::mutex g_ladder_mu;
 std::unordered_map<int, DeviceLadder> g_ladder;
@@ -80,49 +90,73 @@ DeviceLadder& ladder_for(int dev) {
   return L;
 }
 
-// [has_status, info_max, jitter_max] of the pending slot (waits for it), and
-// clears it.  Caller holds g_ladder_mu.
-at::Tensor take_pending(DeviceLadder& L) {
+// Fold the oldest pending slot into out = [has, info_max, jitter_max] and free it.
+void fold_front(DeviceLadder& L, double* o) {
+  Slot& s = L.slot[L.pending.front()];
+  o[0] = 1.0;
+  o[1] = std::max(o[1], s.host[0]);
+  o[2] = std::max(o[2], s.host[1]);
+  s.busy = false;
+  L.pending.pop_front();
+}
+
+// [has_status, info_max, jitter_max] over the finished calls (all pending ones
+// with wait_all), freeing their slots.  Caller holds g_ladder_mu.
+at::Tensor take_pending(DeviceLadder& L, bool wait_all) {
   auto out = at::zeros({3}, at::TensorOptions().dtype(at::kDouble));
-  if (L.pending >= 0) {
-    Slot& s = L.slot[L.pending];
-    hk(hipEventSynchronize(s.ev), "hipEventSynchronize");
-    auto* o = out.data_ptr<double>();
-    o[0] = 1.0;
-    o[1] = s.host[0];
-    o[2] = s.host[1];
-    L.pending = -1;
+  auto* o = out.data_ptr<double>();
+  while (!L.pending.empty()) {
+    Slot& s = L.slot[L.pending.front()];
+    if (wait_all) {
+      hk(hipEventSynchronize(s.ev), "hipEventSynchronize");
+    } else {
+      const hipError_t q = hipEventQuery(s.ev);
+      if (q == hipErrorNotReady) break;
+      hk(q, "hipEventQuery");
+    }
+    fold_front(L, o);
   }
   return out;
 }
 
-// The slot this call's status goes to: the one not pending.  Caller holds
+// The slot this call's status goes to: a free one, after waiting for the
+// oldest call when all are in flight (folded into *prev).  Caller holds
 // g_ladder_mu until publish_slot.
-int free_slot(DeviceLadder& L) { return L.pending == 0 ? 1 : 0; }
+int free_slot(DeviceLadder& L, at::Tensor& prev) {
+  prev = take_pending(L, false);
+  if ((int)L.pending.size() == NSLOT) {
+    hk(hipEventSynchronize(L.slot[L.pending.front()].ev), "hipEventSynchronize");
+    fold_front(L, prev.data_ptr<double>());
+  }
+  for (int i = 0; i < NSLOT; ++i)
+    if (!L.slot[i].busy) return i;
+  TORCH_CHECK(false, "botorch_amd: no free ladder-status slot");
+}
 
 // Copy the slot's device status to its pinned host words (unless the kernel
-// wrote them there itself: zero_copy) behind an event, then return (and
-// clear) the previous call's.  Caller holds g_ladder_mu.
-at::Tensor publish_slot(DeviceLadder& L, int mine, void* stream, bool zero_copy = false) {
+// wrote them there itself: zero_copy) behind an event; it joins the pending
+// ring.  Caller holds g_ladder_mu.
+void publish_slot(DeviceLadder& L, int mine, void* stream, bool zero_copy = false) {
   Slot& s = L.slot[mine];
   if (!zero_copy)
     hk(hipMemcpyAsync(s.host, s.dev, 2 * sizeof(double), hipMemcpyDeviceToHost,
                       static_cast<hipStream_t>(stream)), "hipMemcpyAsync");
   hk(hipEventRecord(s.ev, static_cast<hipStream_t>(stream)), "hipEventRecord");
-  auto out = take_pending(L);  // the previous forward's (enqueued long before)
-  L.pending = mine;
-  return out;
+  s.busy = true;
+  L.pending.push_back(mine);
 }
 
 // Enqueue this call's status (bo_ladder_status over info / jitter) into a free
-// slot, then return (and clear) the previous call's.
+// slot; return the finished calls' statuses.
 at::Tensor defer_status(const at::Tensor& info, const at::Tensor& jitter, void* stream, int dev) {
   std::lock_guard<std::mutex> lk(g_ladder_mu);
   auto& L = ladder_for(dev);
-  const int mine = free_slot(L);
+  at::Tensor prev;
+  const int mine = free_slot(L, prev);
   ck(bo_ladder_status(info.data_ptr<int>(), jitter.data_ptr<double>(), info.numel(),
                       L.slot[mine].dev, stream), "ladder_status");
-  return publish_slot(L, mine, stream);
+  publish_slot(L, mine, stream);
+  return prev;
 }
 
 // ---- post_partials launch timing (bench.py: HIP events around the launch) ------------
@@ -312,11 +346,11 @@ std::vector<at::Tensor> qmc_acq_impl(
     // launch), read behind an event one call later
     std::lock_guard<std::mutex> lk(g_ladder_mu);
     auto& Ld = ladder_for(dev);
-    const int mine = free_slot(Ld);
+    const int mine = free_slot(Ld, prev);
     fa.status_out = Ld.slot[mine].host_dev;
     fa.status_count = Ld.slot[mine].count;
     ck(bo_qmc_finalize_v(&fa, st), "qmc_finalize");
-    prev = publish_slot(Ld, mine, st, true);
+    publish_slot(Ld, mine, st, true);
   } else {
     ck(bo_qmc_finalize_v(&fa, st), "qmc_finalize");
     TORCH_CHECK(!(lean && defer_ladder && B > 0), "bo::qmc_acq_eager: posterior mode has no status");
@@ -498,7 +532,7 @@ at::Tensor ladder_poll(int64_t device) {
   std::lock_guard<std::mutex> lk(g_ladder_mu);
   auto it = g_ladder.find(static_cast<int>(device));
   if (it == g_ladder.end()) return at::zeros({3}, at::TensorOptions().dtype(at::kDouble));
-  return take_pending(it->second);
+  return take_pending(it->second, true);
 }
 
 void post_timing(bool on) {
