@@ -33,41 +33,6 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 constexpr int DP = 8;
 constexpr int THREADS = 256;
 
-// f + sum_{j >= J} Lr[j] z_j with z_j = lane j's z of this 16-lane row (DPP)
-template <int J>
-__device__ __forceinline__ double lq_chain(const double (&Lr)[QMAX], double z, double f) {
-  f = fma(Lr[J], row_bcast<J>(z), f);
-  if constexpr (J + 1 < QMAX) return lq_chain<J + 1>(Lr, z, f);
-  return f;
-}
-
-// max / sum over the 16 lanes of a row (xor shuffles inside the row)
-__device__ __forceinline__ double row_max16(double v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-  return v;
-}
-__device__ __forceinline__ double row_sum16(double v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-
-// log_q_reduce (logred.h) across a 16-lane row: li of the active lanes
-__device__ __forceinline__ double row_log_q_reduce(double li, bool act, const LogRedParams& p) {
-  const double tau = p.tau_max;
-  const double M = row_max16(act ? li : -INFINITY);
-  if (p.fat) {
-    const double x = (M - li) / tau;
-    const double den = 2.0 + 2.0 * x + x * x;
-    const double P = row_sum16(act ? 2.0 / den : 0.0);
-    return M + tau * log(P);
-  }
-  const double Ms = M / tau;
-  const double ssum = row_sum16(act ? exp(li / tau - Ms) : 0.0);
-  return tau * (Ms + log(ssum));
-}
-
 enum QmcMode : int {
   QMC_POSTERIOR = 0,
   QMC_QEI = 1,
@@ -108,6 +73,112 @@ __device__ __forceinline__ double strided_sum(const double* __restrict__ p, int6
 #pragma unroll
     for (int u = 0; u < w; ++u) s[u] += s[u + w];
   return s[0];
+}
+
+// z_J of this lane's group of G lanes: lane J of the group (DPP row
+// broadcast; G = 8: the row's two groups take lanes J and 8 + J)
+template <int G, int J>
+__device__ __forceinline__ double group_bcast(double z, bool upper) {
+  if constexpr (G == 16) {
+    return row_bcast<J>(z);
+  } else {
+    const double lo = row_bcast<J>(z), hi = row_bcast<8 + J>(z);
+    return upper ? hi : lo;
+  }
+}
+
+// f + sum_{j >= J} Lr[j] z_j (j ascending: the serial form's FMA chain)
+template <int G, int J>
+__device__ __forceinline__ double lq_chain(const double (&Lr)[QMAX], double z, bool upper, double f) {
+  f = fma(Lr[J], group_bcast<G, J>(z, upper), f);
+  if constexpr (J + 1 < G) return lq_chain<G, J + 1>(Lr, z, upper, f);
+  return f;
+}
+
+// max / sum over the G lanes of a group (xor shuffles inside the group)
+template <int G>
+__device__ __forceinline__ double group_max(double v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// log_q_reduce (logred.h) across a group: li of the active lanes
+template <int G>
+__device__ __forceinline__ double group_log_q_reduce(double li, bool act, const LogRedParams& p) {
+  const double tau = p.tau_max;
+  const double M = group_max<G>(act ? li : -INFINITY);
+  if (p.fat) {
+    const double x = (M - li) / tau;
+    const double den = 2.0 + 2.0 * x + x * x;
+    const double P = group_sum<G>(act ? 2.0 / den : 0.0);
+    return M + tau * log(P);
+  }
+  const double Ms = M / tau;
+  const double ssum = group_sum<G>(act ? exp(li / tau - Ms) : 0.0);
+  return tau * (Ms + log(ssum));
+}
+
+// Samples and the MC reduction of one t-batch.  Lane (slot = lane / G,
+// a = lane % G) of wave w holds row a of L_q in registers and takes test
+// point a of sample s = s0 + (64 / G) w + slot: z[s][a] is one coalesced load,
+// z[s][j] reaches the group by DPP broadcast, f_a is the same FMA chain (j
+// ascending) as the serial form, and the q-reductions are shuffles inside the
+// group.  SB samples' loads per lane are in flight at once.  (The serial
+// per-sample loop read L_q from LDS once per FMA and paid one L2 latency per
+// sample: 22 us of C3's 38 us finalisation, profiles/r04/qmc.)  Accumulates
+// the qEI sum / the log modes' (max, sum-exp) pair in the group's lane 0.
+template <int G, int MODE>
+__device__ __forceinline__ void sample_phase(int tid, int q, int S, int row0,
+                                             const double (&Lq)[QMAX][QMAX + 1],
+                                             const double (&mu)[QMAX], const double* __restrict__ Z,
+                                             const double* __restrict__ F, int64_t ldF, double best_f,
+                                             const double* __restrict__ best_f_s,
+                                             const LogRedParams& lp, double& sum, LseAcc& lse) {
+  constexpr int SLOTS = 64 / G;             // samples per wave per pass
+  constexpr int PER = SLOTS * (THREADS / 64);  // samples per workgroup per pass
+  constexpr int SB = 8;
+  const int lane = tid & 63, a_ = lane % G, slot = lane / G, wv = tid >> 6;
+  const bool upper = (lane & 8) != 0;  // G = 8: the row's second group
+  const bool arow = a_ < q;
+  double Lr[QMAX];
+#pragma unroll
+  for (int j = 0; j < QMAX; ++j) Lr[j] = (arow && j <= a_) ? Lq[a_][j] : 0.0;
+  const double mu_a = arow ? mu[a_] : 0.0;
+  for (int s0 = 0; s0 < S; s0 += SB * PER) {
+    double zb[SB], fb[SB], bb[SB];
+#pragma unroll
+    for (int u = 0; u < SB; ++u) {
+      const int s = s0 + u * PER + SLOTS * wv + slot;
+      const bool act = s < S && arow;
+      zb[u] = act ? Z[(int64_t)s * q + a_] : 0.0;
+      fb[u] = (F != nullptr && act) ? F[(int64_t)s * ldF + row0 + a_] : 0.0;
+      bb[u] = per_sample_best(MODE) ? (s < S ? best_f_s[s] : 0.0) : best_f;
+    }
+#pragma unroll
+    for (int u = 0; u < SB; ++u) {
+      const int s = s0 + u * PER + SLOTS * wv + slot;
+      const bool sv = s < S;
+      const bool act = sv && arow;
+      const double f = lq_chain<G, 0>(Lr, zb[u], upper, mu_a + fb[u]);
+      const double bf = bb[u];
+      if (log_mode(MODE)) {
+        const double li = act ? log_soft_relu(f - bf, lp, nullptr) : -INFINITY;
+        const double uu = group_log_q_reduce<G>(li, act, lp);
+        if (a_ == 0 && sv) lse = lse_push(lse, uu);
+      } else {
+        // max_a relu(f_a - best_f) = relu(max_a (f_a - best_f)): fmax is exact
+        const double v = group_max<G>(act ? f - bf : -INFINITY);
+        if (a_ == 0 && sv) sum += fmax(v, 0.0);
+      }
+    }
+  }
 }
 
 template <int KIND, int MODE>
@@ -322,52 +393,14 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     return;
   }
 
-  // 3. samples and the reduction.  Lane (grp = lane >> 4, a = lane & 15) of
-  // wave w holds row a of L_q in registers and takes test point a of sample
-  // s = s0 + 4 w + grp: z[s][a] is one coalesced load, z[s][j] reaches the
-  // row's lanes by DPP broadcast, f_a is the same FMA chain (j ascending) as
-  // the serial form, and the q-reductions are shuffles inside the 16-lane row.
-  // (The serial per-sample loop read L_q from LDS once per FMA: 22 us of C3's
-  // 38 us finalisation, profiles/r04/qmc.)
-  const int lane = tid & 63, a_ = lane & 15, grp = lane >> 4, wv = tid >> 6;
-  const bool arow = a_ < q;
-  double Lr[QMAX];
-#pragma unroll
-  for (int j = 0; j < QMAX; ++j) Lr[j] = (arow && j <= a_) ? Lq[a_][j] : 0.0;
-  const double mu_a = arow ? mu[a_] : 0.0;
+  // 3. samples and the reduction (sample_phase): groups of G = 16 lanes for
+  // q > 8, G = 8 for q <= 8 (twice the samples per pass).
   double sum = 0.0;
   LseAcc lse{-INFINITY, 0.0};
-  // SB samples' loads per lane in flight at once (one L2 latency per SB
-  // samples instead of one per sample)
-  constexpr int SB = 8;
-  for (int s0 = 0; s0 < S; s0 += SB * (THREADS / 16)) {
-    double zb[SB], fb[SB], bb[SB];
-#pragma unroll
-    for (int u = 0; u < SB; ++u) {
-      const int s = s0 + u * (THREADS / 16) + 4 * wv + grp;
-      const bool act = s < S && arow;
-      zb[u] = act ? Z[(int64_t)s * q + a_] : 0.0;
-      fb[u] = (F != nullptr && act) ? F[(int64_t)s * ldF + row0 + a_] : 0.0;
-      bb[u] = per_sample_best(MODE) ? (s < S ? best_f_s[s] : 0.0) : best_f;
-    }
-#pragma unroll
-    for (int u = 0; u < SB; ++u) {
-      const int s = s0 + u * (THREADS / 16) + 4 * wv + grp;
-      const bool sv = s < S;
-      const bool act = sv && arow;
-      const double f = lq_chain<0>(Lr, zb[u], mu_a + fb[u]);
-      const double bf = bb[u];
-      if (log_mode(MODE)) {
-        const double li = act ? log_soft_relu(f - bf, lp, nullptr) : -INFINITY;
-        const double uu = row_log_q_reduce(li, act, lp);
-        if (a_ == 0 && sv) lse = lse_push(lse, uu);
-      } else {
-        // max_a relu(f_a - best_f) = relu(max_a (f_a - best_f)): fmax is exact
-        const double v = row_max16(act ? f - bf : -INFINITY);
-        if (a_ == 0 && sv) sum += fmax(v, 0.0);
-      }
-    }
-  }
+  if (q > 8)
+    sample_phase<16, MODE>(tid, q, S, row0, Lq, mu, Z, F, ldF, best_f, best_f_s, lp, sum, lse);
+  else
+    sample_phase<8, MODE>(tid, q, S, row0, Lq, mu, Z, F, ldF, best_f, best_f_s, lp, sum, lse);
   if (log_mode(MODE)) {
     for (int o = 32; o > 0; o >>= 1) {
       LseAcc other{__shfl_xor(lse.m, o), __shfl_xor(lse.s, o)};
