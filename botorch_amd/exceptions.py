@@ -59,3 +59,13 @@ class OptimizationTimeoutError(BotorchError):
 
 class BadInitialCandidatesWarning(RuntimeWarning):
     """botorch/exceptions/warnings.py BadInitialCandidatesWarning."""
+
+
+class CandidateGenerationError(BotorchError):
+    """botorch/exceptions/errors.py CandidateGenerationError: e.g. a linear
+    constraint left without free variables by fixed features is violated
+    (optim/parameter_constraints.py:448-454)."""
+
+
+class UserInputWarning(BotorchWarning):
+    """botorch/exceptions/warnings.py UserInputWarning."""

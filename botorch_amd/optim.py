@@ -358,15 +358,19 @@ def gen_batch_initial_conditions(acq_function, bounds, q, num_restarts, raw_samp
     device (bo_sobol_box, bit-identical to draw_sobol_samples) and evaluated
     there chunk by chunk; only the values cross to the host, once, for the
     selection, which draws from the global CPU generator as the reference does
-    (so the picks are the reference's).  Linear constraints need the
-    reference's polytope sampler (utils/sampling.py HitAndRun), which is not on
-    this path: they raise UnsupportedError."""
+    (so the picks are the reference's).  Under linear constraints the raw
+    designs are q-batches of the hit-and-run chain over the feasible polytope
+    (constraints.sample_q_batches_from_polytope, initializers.py:365-375; the
+    chain's steps in native host code), evaluated on the device the same way."""
     from .exceptions import UnsupportedError
-    if inequality_constraints or equality_constraints:
-        raise UnsupportedError("linear parameter constraints are not supported by this "
-                               "initialiser (the reference's polytope sampler is out of scope)")
+    if bounds.isinf().any():
+        raise NotImplementedError("Currently only finite values in `bounds` are supported for "
+                                  "generating initial conditions for optimization.")
     options = options or {}
     sample_around_best = options.get("sample_around_best", False)
+    if sample_around_best and equality_constraints:
+        raise UnsupportedError("Option 'sample_around_best' is not supported when equality"
+                               "constraints are present.")
     if sample_around_best and generator:
         raise UnsupportedError("Option 'sample_around_best' is not supported when custom "
                                "generator is be used.")
@@ -378,6 +382,13 @@ def gen_batch_initial_conditions(acq_function, bounds, q, num_restarts, raw_samp
         n = raw_samples * factor
         if generator is not None:
             X_rnd = generator(n, q, seed)
+        elif inequality_constraints or equality_constraints:
+            from .constraints import sample_q_batches_from_polytope
+            X_rnd = sample_q_batches_from_polytope(
+                n=n, q=q, bounds=bounds, n_burnin=options.get("n_burnin", 10000),
+                n_thinning=options.get("n_thinning", 32), seed=seed,
+                equality_constraints=equality_constraints,
+                inequality_constraints=inequality_constraints)
         elif d * q <= SOBOL_MAXDIM:
             X_rnd = draw_raw_samples(bounds, n, q, seed)
         else:
@@ -488,46 +499,70 @@ def _without_fixed_features(fixed_features, acquisition_function, initial_condit
 
 
 def _reject_constraints(inequality_constraints, equality_constraints,
-                        nonlinear_inequality_constraints) -> None:
-    if inequality_constraints or equality_constraints or nonlinear_inequality_constraints:
-        from .exceptions import UnsupportedError
-        raise UnsupportedError("parameter constraints (SLSQP / trust-constr candidate "
-                               "generation) are not supported on this path")
+                        nonlinear_inequality_constraints, where: str = "this path") -> None:
+    """Nonlinear constraints are out of scope; linear
+    ones are refused only by the device-resident L-BFGS-B."""
+    from .exceptions import UnsupportedError
+    if nonlinear_inequality_constraints:
+        raise UnsupportedError("nonlinear inequality constraints are not supported on "
+                               f"{where}")
+    if inequality_constraints or equality_constraints:
+        raise UnsupportedError(f"linear parameter constraints are not supported by {where}: "
+                               "use gen_candidates_scipy (SLSQP, generation/gen.py:256)")
 
 
 def gen_candidates_scipy(initial_conditions, acquisition_function, lower_bounds=None,
                          upper_bounds=None, inequality_constraints=None, equality_constraints=None,
                          nonlinear_inequality_constraints=None, options=None, fixed_features=None,
                          timeout_sec=None):
-    """generation/gen.py:46-298 (box constraints, L-BFGS-B): fixed features
-    are removed from the search space (gen.py:124-175), the run is bounded by
-    ``timeout_sec`` (minimize_with_timeout, gen.py:252-267) and its exit is
-    resolved by _process_scipy_result (gen.py:268).  Linear and nonlinear
-    constraints raise UnsupportedError."""
-    _reject_constraints(inequality_constraints, equality_constraints,
-                        nonlinear_inequality_constraints)
+    """generation/gen.py:46-298: scipy.optimize.minimize over the flattened
+    t-batch -- L-BFGS-B on the box, SLSQP (the reference's default there)
+    when linear constraints are given (make_scipy_linear_constraints records,
+    gen.py:182-189, 256).  Fixed features are removed from the search space
+    (gen.py:124-175; the constraints rewritten on the free features) unless a
+    constraint is present and some fixed value is None, in which case the
+    full space is searched with the features pinned inside the objective
+    (gen.py:208).  The run is bounded by ``timeout_sec`` (minimize_with_timeout,
+    gen.py:252-267), its exit resolved by _process_scipy_result (gen.py:268),
+    the result clamped with raise_on_violation.  Nonlinear constraints raise
+    UnsupportedError."""
+    from .constraints import (_generate_unfixed_lin_constraints, make_scipy_bounds,
+                              make_scipy_linear_constraints)
+    _reject_constraints(None, None, nonlinear_inequality_constraints, "gen_candidates_scipy")
     options = dict(options or {})
     options = {**options, "maxiter": options.get("maxiter", 2000)}
-    if fixed_features:
+    linear = bool(inequality_constraints or equality_constraints)
+    if fixed_features and (not linear or None not in fixed_features.values()):
+        d = initial_conditions.shape[-1]
         ff, ics, lo, hi = _without_fixed_features(fixed_features, acquisition_function,
                                                   initial_conditions, lower_bounds, upper_bounds)
-        c, acq = gen_candidates_scipy(ics, ff, lo, hi, options=options, timeout_sec=timeout_sec)
+        ineq = _generate_unfixed_lin_constraints(inequality_constraints, fixed_features, d, False)
+        eq = _generate_unfixed_lin_constraints(equality_constraints, fixed_features, d, True)
+        c, acq = gen_candidates_scipy(ics, ff, lo, hi, inequality_constraints=ineq,
+                                      equality_constraints=eq, options=options,
+                                      timeout_sec=timeout_sec)
         return ff._construct_X_full(c), acq
+    pinned = fixed_features or None  # only reached with constraints and a None value
     clamped = columnwise_clamp(initial_conditions, lower_bounds, upper_bounds)
     shapeX = clamped.shape
     x0 = clamped.detach().reshape(-1).cpu().numpy()
-    lb = (torch.as_tensor(lower_bounds).expand(shapeX).reshape(-1).cpu().numpy()
-          if lower_bounds is not None else np.full(x0.shape, -np.inf))
-    ub = (torch.as_tensor(upper_bounds).expand(shapeX).reshape(-1).cpu().numpy()
-          if upper_bounds is not None else np.full(x0.shape, np.inf))
-    scipy_bounds = list(zip(lb, ub))
+    if linear:
+        scipy_bounds = make_scipy_bounds(initial_conditions, lower_bounds, upper_bounds)
+        cons = make_scipy_linear_constraints(shapeX, inequality_constraints, equality_constraints)
+    else:
+        lb = (torch.as_tensor(lower_bounds).expand(shapeX).reshape(-1).cpu().numpy()
+              if lower_bounds is not None else np.full(x0.shape, -np.inf))
+        ub = (torch.as_tensor(upper_bounds).expand(shapeX).reshape(-1).cpu().numpy()
+              if upper_bounds is not None else np.full(x0.shape, np.inf))
+        scipy_bounds = list(zip(lb, ub))
+        cons = []
     with_grad = options.get("with_grad", True)
 
     def f_np_wrapper(x: np.ndarray):
         if np.isnan(x).any():
             raise RuntimeError(f"{np.isnan(x).sum()} elements of the {x.size} element array `x` are NaN.")
         X = torch.from_numpy(x).to(initial_conditions).view(shapeX).contiguous().requires_grad_(True)
-        loss = -acquisition_function(X).sum()
+        loss = -acquisition_function(fix_features(X, pinned)).sum()
         grad = torch.autograd.grad(loss, X)[0].contiguous().view(-1).cpu().numpy()
         _check_deferred(X)
         if np.isnan(grad).any():
@@ -538,18 +573,20 @@ def gen_candidates_scipy(initial_conditions, acquisition_function, lower_bounds=
     def f_only(x):
         X = torch.from_numpy(x).to(initial_conditions).view(shapeX).contiguous()
         with torch.no_grad():
-            val = -acquisition_function(X).sum().item()
+            val = -acquisition_function(fix_features(X, pinned)).sum().item()
         _check_deferred(X)
         return val
 
     res = minimize_with_timeout(f_np_wrapper if with_grad else f_only, x0,
-                                method=options.get("method", "L-BFGS-B"), jac=with_grad,
-                                bounds=scipy_bounds, callback=options.get("callback", None),
+                                method=options.get("method", "SLSQP" if cons else "L-BFGS-B"),
+                                jac=with_grad, bounds=scipy_bounds, constraints=cons,
+                                callback=options.get("callback", None),
                                 options={k: v for k, v in options.items()
                                          if k not in ("method", "callback", "with_grad")},
                                 timeout_sec=timeout_sec)
     _process_scipy_result(res, options)
-    candidates = torch.from_numpy(res.x).to(initial_conditions).reshape(shapeX)
+    candidates = fix_features(torch.from_numpy(res.x).to(initial_conditions).reshape(shapeX),
+                              pinned)
     clamped = columnwise_clamp(candidates, lower_bounds, upper_bounds, raise_on_violation=True)
     with torch.no_grad():
         acq = acquisition_function(clamped)
@@ -715,7 +752,7 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     from . import _lib, kernels
     from ._lib import check, lib
     _reject_constraints(inequality_constraints, equality_constraints,
-                        nonlinear_inequality_constraints)
+                        nonlinear_inequality_constraints, "gen_candidates_device")
     if fixed_features:  # the search space without them (generation/utils.py:102-196)
         ff, ics, lo_b, hi_b = _without_fixed_features(fixed_features, acquisition_function,
                                                       initial_conditions, lower_bounds,
@@ -890,7 +927,7 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
 
 
 def generate_in_chunks(acq_function, ics, bounds, batch_limit, options, gen_candidates,
-                       fixed_features=None, timeout_sec=None):
+                       fixed_features=None, timeout_sec=None, **constraints):
     """_optimize_acqf_batch's loop over batch_limit chunks of the initial
     conditions (optimize.py:277-326): ``timeout_sec`` is shared evenly by the
     chunks, an all-infinite bound is passed as None.  Returns (candidates,
@@ -906,7 +943,7 @@ def generate_in_chunks(acq_function, ics, bounds, batch_limit, options, gen_cand
             warnings.simplefilter("always", category=OptimizationWarning)
             c, v = gen_candidates(chunk, acq_function, lower_bounds=lo, upper_bounds=hi,
                                   options=gen_options, fixed_features=fixed_features,
-                                  timeout_sec=t_chunk)
+                                  timeout_sec=t_chunk, **constraints)
         opt_ws += [x for x in w if issubclass(x.category, OptimizationWarning)]
         for x in w:  # everything else is passed on, as the reference's recorder does not
             if not issubclass(x.category, OptimizationWarning):
@@ -940,8 +977,10 @@ def _validate_optimize_inputs(bounds, raw_samples, batch_initial_conditions, ic_
 def _optimize_acqf_batch(acq_function, bounds, q, num_restarts, raw_samples, options,
                          fixed_features, post_processing_func, batch_initial_conditions,
                          return_best_only, gen_candidates, ic_generator, timeout_sec,
-                         retry_on_optimization_warning, ic_gen_kwargs):
-    """optimize.py:246-394."""
+                         retry_on_optimization_warning, ic_gen_kwargs,
+                         inequality_constraints=None, equality_constraints=None):
+    """optimize.py:246-394 (the linear constraints go to the initial-condition
+    generator always and to ``gen_candidates`` when given, :255-303)."""
     options = options or {}
     provided = batch_initial_conditions is not None
     ic_gen = ic_generator or gen_batch_initial_conditions
@@ -949,14 +988,18 @@ def _optimize_acqf_batch(acq_function, bounds, q, num_restarts, raw_samples, opt
     def _ics():
         return ic_gen(acq_function=acq_function, bounds=bounds, q=q, num_restarts=num_restarts,
                       raw_samples=raw_samples, fixed_features=fixed_features, options=options,
-                      **ic_gen_kwargs)
+                      inequality_constraints=inequality_constraints,
+                      equality_constraints=equality_constraints, **ic_gen_kwargs)
 
     ics = batch_initial_conditions if provided else _ics()
     batch_limit = options.get("batch_limit", num_restarts)
+    linear = {k: v for k, v in (("inequality_constraints", inequality_constraints),
+                                ("equality_constraints", equality_constraints)) if v is not None}
 
     def _run(x0):
         return generate_in_chunks(acq_function, x0, bounds, batch_limit, options, gen_candidates,
-                                  fixed_features=fixed_features, timeout_sec=timeout_sec)
+                                  fixed_features=fixed_features, timeout_sec=timeout_sec,
+                                  **linear)
 
     cands, vals, ws = _run(ics)
     if ws and retry_on_optimization_warning:
@@ -1001,13 +1044,14 @@ def optimize_acqf(acq_function, bounds, q, num_restarts, raw_samples=None, optio
     with fixed features and the timeout split over the chunks, one retry on
     OptimizationWarning, post-processing, argmax over restarts.
 
-    Linear / nonlinear parameter constraints raise UnsupportedError (they need
-    SLSQP and the reference's polytope sampler, not on this path); every other
-    argument has the reference's meaning.  ``return_full_tree`` only matters
-    for one-shot acquisitions, which are not on this path."""
+    Linear (in)equality constraints take the reference's route: polytope raw
+    samples (hit-and-run) for the initial conditions and SLSQP in
+    gen_candidates_scipy (the device L-BFGS-B refuses them).  Nonlinear
+    constraints raise UnsupportedError (out of scope); every other argument has
+    the reference's meaning.  ``return_full_tree`` only matters for one-shot
+    acquisitions, which are not on this path."""
     from .exceptions import UnsupportedError
-    _reject_constraints(inequality_constraints, equality_constraints,
-                        nonlinear_inequality_constraints)
+    _reject_constraints(None, None, nonlinear_inequality_constraints, "optimize_acqf")
     gen_candidates = gen_candidates or gen_candidates_scipy
     _validate_optimize_inputs(bounds, raw_samples, batch_initial_conditions, ic_generator,
                               inequality_constraints)
@@ -1024,10 +1068,15 @@ def optimize_acqf(acq_function, bounds, q, num_restarts, raw_samples=None, optio
                 return_best_only=return_best_only, gen_candidates=gen_candidates,
                 ic_generator=ic_generator, timeout_sec=timeout_sec,
                 retry_on_optimization_warning=retry_on_optimization_warning,
-                ic_gen_kwargs=ic_gen_kwargs)
+                ic_gen_kwargs=ic_gen_kwargs, inequality_constraints=inequality_constraints,
+                equality_constraints=equality_constraints)
     if not (sequential and q > 1):
         return _optimize_acqf_batch(**args)
     # _validate_sequential_inputs (optimize.py:162-199), then q greedy picks
+    for group, kind in ((inequality_constraints, "inequality"), (equality_constraints, "equality")):
+        if any(len(c[0].shape) > 1 for c in group or []):
+            raise UnsupportedError(f"Linear {kind} constraints across the q-dimension are not "
+                                   "supported for sequential optimization.")
     if batch_initial_conditions is not None:
         raise UnsupportedError("`batch_initial_conditions` is not supported for sequential "
                                "optimization. Either avoid specifying `batch_initial_conditions` "

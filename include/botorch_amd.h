@@ -525,6 +525,19 @@ int bo_nd_partition_host(const double* Y, int64_t S, int64_t n, int m, const dou
                          int64_t K_cap, int64_t* K_out, double* cell_lo, double* cell_hi,
                          int nthreads);
 
+/* HOST function (plain host pointers; no GPU involved): the hit-and-run chain
+ * of sample_polytope (botorch/utils/sampling.py:219-309) over {y : A y <= b}
+ * (A m x k row-major, b m), from y0 (k).  Step t moves along the unit direction
+ * R[t] (n_tot x k) by lo + u[t] (hi - lo), [lo, hi] the feasible segment from
+ * the slacks max(b - A y, 0) / AR[t] (AR = R A^T, n_tot x m, made by the caller
+ * with torch as the reference makes it); after n0 burn-in steps every n_thin-th
+ * point goes to out (n x k); n_tot must equal n0 + n * n_thin.  Replaces the
+ * Python loop at sampling.py:278-308 that gen_batch_initial_conditions runs
+ * under linear constraints (optim/initializers.py:365-375). */
+int bo_hit_and_run_host(const double* A, const double* b, int64_t m, int64_t k, const double* y0,
+                        const double* R, const double* AR, const double* u, int64_t n_tot,
+                        int64_t n0, int64_t n_thin, double* out, int64_t n);
+
 /* Scrambled Sobol raw designs in a box, points skip..skip+n-1: out (n x dim),
  * dim = q * d, out[i][j] = lower[j % d] + range[j % d] * u_i[j] (device
  * lower/range of length d).  Same engine state as bo_sobol_normal.

@@ -21,6 +21,7 @@ _STUB_PACKAGES = [
     "botorch.utils.multi_objective.box_decompositions",
     "botorch.sampling",
     "botorch.test_functions",
+    "botorch.optim",
 ]
 
 

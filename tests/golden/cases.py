@@ -29,3 +29,13 @@ LOGEI_CASES = {
 
 # Dominated-hypervolume fixtures: (m objectives, n points).
 HV_CASES = [(2, 30), (3, 25), (3, 8)]
+
+# Linear-constraint / polytope fixtures (make_golden_polytope.py).
+POLYTOPE_CASES = {
+    # (n, n0 burn-in, n_thinning, seed)
+    "sample_polytope": [(40, 50, 3, 7), (25, 0, 1, 123)],
+    # (n_burnin, n_thinning, seed, first draw, second draw)
+    "hit_and_run": [(30, 5, 11, 12, 7), (200, 20, 0, 16, 16)],
+    # (n, n_burnin, n_thinning, seed)
+    "get_polytope_samples": [(20, 100, 4, 3), (64, 1000, 32, 0)],
+}

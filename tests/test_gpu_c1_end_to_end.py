@@ -108,6 +108,43 @@ def test_c1_qei_optimize_acqf(gen):
         assert float(val) > 0
 
 
+def test_c1_qei_optimize_acqf_linear_constraints():
+    """optimize_acqf under linear constraints with the HIP qEI: polytope raw
+    samples (native hit-and-run, initializers.py:365-375) evaluated on the
+    device, SLSQP candidates (gen.py:256) through the HIP forward + backward;
+    the candidates are feasible and their values are the oracle's qEI."""
+    from botorch_amd.acquisition import qExpectedImprovement
+    from botorch_amd.optim import optimize_acqf
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import qei
+    from oracle.sampling import draw_sobol_normal_samples
+    m, X, Y, *_ = _fitted_c1()
+    orc = _oracle_of(m, X, Y)
+    best_f = float(Y.max()) - 0.5
+    acqf = qExpectedImprovement(m, best_f=best_f,
+                                sampler=SobolQMCNormalSampler(torch.Size([512]), seed=0))
+    bounds = torch.stack([torch.zeros(6), torch.ones(6)]).to(DEV, torch.float64)
+    f64 = dict(dtype=torch.float64, device=DEV)
+    ineq = [(torch.tensor([0, 1], device=DEV), torch.tensor([-1.0, -1.0], **f64), -0.8),
+            (torch.tensor([[0, 2], [1, 2]], device=DEV), torch.tensor([1.0, 1.0], **f64), 0.6)]
+    eq = [(torch.tensor([3, 4], device=DEV), torch.tensor([1.0, 1.0], **f64), 1.0)]
+    torch.manual_seed(0)
+    cand, val = optimize_acqf(acqf, bounds, q=2, num_restarts=6, raw_samples=32,
+                              options={"maxiter": 50, "seed": 0, "n_burnin": 500},
+                              inequality_constraints=ineq, equality_constraints=eq)
+    assert cand.shape == (2, 6)
+    c = cand.cpu()
+    assert torch.all(c >= -EPS) and torch.all(c <= 1 + EPS)
+    assert torch.all(c[:, 0] + c[:, 1] <= 0.8 + 1e-6)
+    assert float(c[0, 2] + c[1, 2]) >= 0.6 - 1e-6
+    torch.testing.assert_close(c[:, 3] + c[:, 4], torch.ones(2, dtype=torch.float64), atol=1e-6,
+                               rtol=0)
+    Z = draw_sobol_normal_samples(2, 512, 0)
+    ref = qei(orc, c.unsqueeze(0), Z, best_f)
+    torch.testing.assert_close(val.cpu().reshape(1), ref, rtol=1e-6, atol=1e-12)
+    assert float(val) > 0
+
+
 def _sin_setup(dtype):
     """test/test_end_to_end.py:37-72: 10 noisy sin points in [0, 1]."""
     from botorch_amd.exceptions import OptimizationWarning

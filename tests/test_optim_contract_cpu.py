@@ -1,6 +1,6 @@
 """The caller contract of optimize_acqf / gen_candidates_scipy / fit_gpytorch_mll
 on the host (no GPU): fixed features, timeouts, the scipy exit handling, the
-rejected constraint kwargs, sequential greedy q, post-processing, and the
+rejected nonlinear constraints, sequential greedy q, post-processing, and the
 failure / retry / pick-best policy of _fit_fallback with scripted optimisers.
 
 Reference: optim/optimize.py:140-564, generation/gen.py:46-298, 458-493,
@@ -141,18 +141,27 @@ def test_process_scipy_result_policy():
     assert not ws
 
 
-@pytest.mark.parametrize("kw", [
-    {"inequality_constraints": [(torch.tensor([0, 1]), torch.tensor([1.0, 1.0]), 0.5)]},
-    {"equality_constraints": [(torch.tensor([0]), torch.tensor([1.0]), 0.5)]},
-    {"nonlinear_inequality_constraints": [(lambda x: x.sum() - 1, True)]},
-])
-def test_constraints_are_rejected_not_dropped(kw):
+def test_nonlinear_constraints_are_rejected_not_dropped():
     acq = _Quad()
+    kw = {"nonlinear_inequality_constraints": [(lambda x: x.sum() - 1, True)]}
     with pytest.raises(UnsupportedError):
         optimize_acqf(acq, BOUNDS, q=1, num_restarts=2, raw_samples=8, **kw)
     with pytest.raises(UnsupportedError):
         gen_candidates_scipy(torch.full((1, 1, 3), 0.5, dtype=torch.float64), acq,
                              BOUNDS[0], BOUNDS[1], **kw)
+
+
+@pytest.mark.parametrize("kw", [
+    {"inequality_constraints": [(torch.tensor([0, 1]), torch.tensor([1.0, 1.0]), 0.5)]},
+    {"equality_constraints": [(torch.tensor([0]), torch.tensor([1.0]), 0.5)]},
+])
+def test_device_optimizer_rejects_linear_constraints(kw):
+    """The device L-BFGS-B handles boxes only: it refuses linear constraints
+    (before touching the GPU) instead of dropping them."""
+    from botorch_amd.optim import gen_candidates_device
+    with pytest.raises(UnsupportedError, match="gen_candidates_scipy"):
+        gen_candidates_device(torch.full((1, 1, 3), 0.5, dtype=torch.float64), _Quad(),
+                              BOUNDS[0], BOUNDS[1], **kw)
 
 
 def test_optimize_acqf_input_validation():
