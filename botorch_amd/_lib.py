@@ -106,6 +106,8 @@ _SIGNATURES = {
     "bo_lbfgsb_set_staging": (c_int, [c_int]),
     "bo_nd_partition_host": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, POINTER(c_int64), _P,
                                      _P, c_int]),
+    "bo_nd_partition_alpha_host": (c_int, [_P, c_int64, c_int64, c_int, _P, c_double, c_int64,
+                                           POINTER(c_int64), _P, _P, c_int]),
     "bo_hit_and_run_host": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P, _P, c_int64, c_int64,
                                     c_int64, _P, c_int64]),
     "bo_sobol_box": (c_int, [_P, _P, c_int, c_int64, c_int64, c_int, _P, _P, c_int, _P, _P]),

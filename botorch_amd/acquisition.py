@@ -1098,18 +1098,26 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
     """MC q-noisy expected hypervolume improvement (acquisition/multi_objective/
     monte_carlo.py:325-468; NoisyExpectedHypervolumeMixin,
     utils/multi_objective/hypervolume.py:507-835) for a ModelListGP of
-    SingleTaskGPs with the cached baseline root (cache_root=True) and the
-    incremental formulation (incremental_nehvi=True):
+    SingleTaskGPs with the cached baseline root (cache_root=True):
 
-      qNEHVI(X) = mean_s HVI(f_s(X) | Pareto front of f_s(X_baseline)).
+      qNEHVI(X) = mean_s HVI(f_s(X, X_pending) | Pareto front of f_s(X_baseline))
+                  + prev_nehvi.
 
-    Construction: the joint baseline samples (Sobol dimension r m), one exact
-    box decomposition of the non-dominated region per sample
-    (FastNondominatedPartitioning on the host, as the reference does for m > 2),
-    padded with empty cells to a common count (BoxDecompositionList), resident on
-    the device as S x K x m.  Forward / backward: _FusedQNEHVI.  Pending points
-    join the baseline (cache_pending=True, max_iep=0) and the decompositions are
-    rebuilt."""
+    Construction: the joint baseline samples (Sobol dimension r m), one box
+    decomposition of the non-dominated region per sample (exact:
+    FastNondominatedPartitioning; alpha > 0: the approximate binary
+    partitioning of NondominatedPartitioning, m > 2; both in native host code,
+    as the reference runs them on the CPU for m > 2), padded with empty cells to
+    a common count (BoxDecompositionList), resident on the device as S x K x m.
+    Forward / backward: _FusedQNEHVI over the q new points and the pending
+    points not yet in the baseline.
+
+    Pending points (hypervolume.py:778-822): with cache_pending, more than
+    max_iep new ones join the baseline and the decompositions are rebuilt
+    (without incremental_nehvi, the hypervolume they add to every sample's
+    front, mean_s (HV_s - HV0_s)+, is carried in prev_nehvi); up to max_iep, or
+    all of them without cache_pending, are appended to every forward's q-batch
+    (concatenate_pending_points)."""
 
     _default_sample_shape = torch.Size([128])
 
@@ -1125,11 +1133,9 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
                                    f"X_baseline. Expected 2 dims, got {X_baseline.ndim}.")
         if constraints is not None:
             raise UnsupportedError("outcome constraints are not on the accelerated path")
-        if not (cache_root and incremental_nehvi and cache_pending and max_iep == 0):
-            raise UnsupportedError("qNEHVI here runs with cache_root, incremental_nehvi, "
-                                   "cache_pending and max_iep=0 (the reference defaults)")
-        if alpha > 0:
-            raise UnsupportedError("approximate partitioning (alpha > 0) is out of scope")
+        if not cache_root:
+            raise UnsupportedError("qNEHVI here runs with the cached baseline root "
+                                   "(cache_root=True, the reference default)")
         models = getattr(model, "models", None)
         if models is None or not all(hasattr(mm, "prediction_cache") for mm in models):
             raise UnsupportedError("qNEHVI here runs on a ModelListGP of SingleTaskGPs")
@@ -1144,23 +1150,29 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
         self.ref_point = torch.as_tensor(ref_point, dtype=torch.float64, device=X_baseline.device)
         self.fat = fat
         self.alpha = alpha
+        self.cache_pending = bool(cache_pending)
+        self._max_iep = int(max_iep)
+        self.incremental_nehvi = bool(incremental_nehvi)
         self.X_pending = None
         if prune_baseline:
             X_baseline = prune_inferior_points_multi_objective(model, X_baseline, self.ref_point)
         self._X_baseline = X_baseline
         self._X_baseline_and_pending = X_baseline
+        self._partitioned = False
         self.register_buffer("_prev_nehvi", torch.tensor(0.0, dtype=torch.float64))
-        self._set_cell_bounds()
         if X_pending is not None:
             self.set_X_pending(X_pending)
+        # hypervolume.py:643-644: the first decomposition, unless set_X_pending
+        # already made it (more than max_iep pending points)
+        if X_pending is None or X_pending.shape[-2] <= self._max_iep:
+            self._set_cell_bounds()
 
     @property
     def X_baseline(self) -> torch.Tensor:
         return self._X_baseline_and_pending
 
     def set_X_pending(self, X_pending=None) -> None:
-        """hypervolume.py:766-800 with cache_pending=True, max_iep=0 and the
-        incremental formulation: pending points join the baseline."""
+        """hypervolume.py:778-822."""
         if X_pending is None:
             self.X_pending = None
             return
@@ -1168,14 +1180,28 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
             warnings.warn("Pending points require a gradient but the acquisition function"
                           " will not provide a gradient to these points.", BotorchWarning)
         X_pending = X_pending.detach().clone()
-        self._X_baseline_and_pending = torch.cat([self._X_baseline, X_pending], dim=-2)
-        self._set_cell_bounds()
-        self.X_pending = None
+        if not self.cache_pending:
+            self.X_pending = X_pending
+            return
+        joined = torch.cat([self._X_baseline, X_pending], dim=-2)
+        num_new = joined.shape[0] - self.X_baseline.shape[0]
+        if num_new <= 0:
+            return
+        if num_new > self._max_iep:
+            self._X_baseline_and_pending = joined
+            self._set_cell_bounds()
+            if not self.incremental_nehvi:
+                self._prev_nehvi = (self._hypervolumes - self._initial_hvs).clamp_min(0.0).mean()
+            self.X_pending = None
+        else:
+            self.X_pending = X_pending[-num_new:]
 
     def _set_cell_bounds(self) -> None:
-        """hypervolume.py:627-700: baseline samples and one box decomposition per
+        """hypervolume.py:680-776: baseline samples and one box decomposition per
         MC sample (native host threads), padded to a common cell count
-        (box_decomposition_list.py:62-94), then resident on the device."""
+        (box_decomposition_list.py:62-94), then resident on the device.  The
+        first decomposition of a non-incremental qNEHVI records every sample's
+        baseline hypervolume (_compute_initial_hvs, :654-678)."""
         Xb = self.X_baseline
         models = self.model.models
         r, m = Xb.shape[-2], len(models)
@@ -1189,12 +1215,26 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
         if not all(rt.fused_ready for rt in self._roots):
             raise UnsupportedError(f"qNEHVI here needs d <= {kernels.DP}")
         Y = torch.stack([rt.samples for rt in self._roots], dim=-1).cpu()  # S x r x m
-        lo, hi = kernels.nd_partition_host(Y, self.ref_point.cpu())  # native, threaded
+        if self.alpha > 0 and m > 2:  # NondominatedPartitioning(alpha); m = 2 is exact there
+            lo, hi = kernels.nd_partition_host(Y, self.ref_point.cpu(), alpha=self.alpha)
+        else:
+            lo, hi = kernels.nd_partition_host(Y, self.ref_point.cpu())  # native, threaded
         self.cell_lower_bounds = lo.to(Xb.device)
         self.cell_upper_bounds = hi.to(Xb.device)
         self._cells = (self.cell_lower_bounds, self.cell_upper_bounds)
         self.baseline_samples = Y
         self._zq = {}
+        if not self._partitioned and not self.incremental_nehvi:
+            self._initial_hvs = dominated_hypervolume(Y, self.ref_point.cpu()).to(self.ref_point)
+        self._partitioned = True
+
+    @property
+    def _hypervolumes(self) -> torch.Tensor:
+        """hypervolume.py:824-835: every sample's hypervolume over the current
+        baseline, from its cells (non_dominated.py:445-457)."""
+        return cells_hypervolume(self.baseline_samples, self.ref_point.cpu(),
+                                 self.cell_lower_bounds.cpu(),
+                                 self.cell_upper_bounds.cpu()).to(self.ref_point)
 
     def _base_samples_q(self, q: int, device) -> torch.Tensor:
         """The q m new columns of the (r+q) m-dim Sobol draw (sampling/normal.py:
@@ -1207,14 +1247,40 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
         return self._zq[q]
 
     def forward(self, X: torch.Tensor) -> torch.Tensor:
-        X = t_batch_mode(X)
+        X = self._concat_pending(t_batch_mode(X))
         batch = X.shape[:-2]
         q, d = X.shape[-2], X.shape[-1]
         if q > 12 or d > kernels.DP or not X.is_cuda:
-            raise UnsupportedError(f"fused qNEHVI supports q <= 12 and d <= {kernels.DP} on the device")
+            raise UnsupportedError(f"fused qNEHVI supports q <= 12 (pending points included) "
+                                   f"and d <= {kernels.DP} on the device")
         X3 = X.reshape(-1, q, d)
         acq = _FusedQNEHVI.apply(X3, self)
         return acq.reshape(batch) + self._prev_nehvi.to(acq)
+
+
+def cells_hypervolume(Y: torch.Tensor, ref: torch.Tensor, lo: torch.Tensor,
+                      hi: torch.Tensor) -> torch.Tensor:
+    """FastNondominatedPartitioning.compute_hypervolume (box_decompositions/
+    non_dominated.py:445-457) per sample: the box [ref, ideal] less the
+    non-dominated cells clipped to it; ideal = the best value of every outcome
+    over the points above ref (those of the Pareto front); 0 without one.
+    Y: S x n x m, lo / hi: S x K x m (padded cells are empty)."""
+    above = (Y > ref).all(dim=-1, keepdim=True)
+    ideal = torch.where(above, Y, torch.full_like(Y, float("-inf"))).max(dim=-2, keepdim=True).values
+    has = above.any(dim=-2).squeeze(-1)
+    total = (ideal.squeeze(-2) - ref).clamp_min(0.0).prod(dim=-1)
+    clip_lo, clip_hi = torch.minimum(lo, ideal), torch.minimum(hi, ideal)
+    non_dom = (clip_hi - clip_lo).clamp_min(0.0).prod(dim=-1).sum(dim=-1)
+    return torch.where(has, total - non_dom, torch.zeros_like(total))
+
+
+def dominated_hypervolume(Y: torch.Tensor, ref: torch.Tensor) -> torch.Tensor:
+    """Every sample's dominated hypervolume (DominatedPartitioning.
+    compute_hypervolume, box_decompositions/dominated.py:51-62, as
+    _compute_initial_hvs uses it): through the exact non-dominated cells of the
+    same points, whose complement in [ref, ideal] it is."""
+    lo, hi = kernels.nd_partition_host(Y, ref)
+    return cells_hypervolume(Y, ref, lo, hi)
 
 
 def _acq_device(acqf) -> Optional[torch.device]:

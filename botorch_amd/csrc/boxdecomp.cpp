@@ -177,20 +177,127 @@ Cells partition(const double* Y, int64_t n, int m, const double* ref) {
   return c;
 }
 
-}  // namespace
-
-extern "C" int bo_nd_partition_host(const double* Y, int64_t S, int64_t n, int m,
-                                    const double* ref, int64_t K_cap, int64_t* K_out,
-                                    double* cell_lo, double* cell_hi, int nthreads) {
-  if (S < 0 || n < 0 || m < 2 || (!Y && S * n > 0) || !ref || !K_out) {
-    bo_set_error("bo_nd_partition_host: bad arguments (S %lld, n %lld, m %d)", (long long)S,
-                 (long long)n, m);
-    return BO_ERR_ARG;
+// NondominatedPartitioning's binary partitioning (box_decompositions/
+// non_dominated.py:81-192, Couckuyt et al. 2012), the decomposition qNEHVI uses
+// with alpha > 0 for m > 2 (utils/multi_objective/hypervolume.py:606-612).
+// Under minimisation of -Y: cells are pairs of index vectors into the Pareto
+// points sorted per outcome, augmented with an ideal row 0 and an anti-ideal
+// row np + 1.  A cell popped from the stack whose upper corner no Pareto point
+// dominates is kept; one whose lower corner no point dominates straddles the
+// front and is halved along its longest index range -- unless every range is
+// down to adjacent indices or its volume is at most alpha of the whole box,
+// in which case it is dropped (the approximation); any other cell is dominated.
+Cells binary_partition(const double* Y, int64_t n, int m, const double* ref, double alpha) {
+  Cells c;
+  std::vector<double> P = pareto_above_ref(Y, n, m, ref);
+  const int64_t np = (int64_t)P.size() / m;
+  if (np == 0) {
+    c.k = 1;
+    c.lo.assign(ref, ref + m);
+    c.hi.assign(m, INF);
+    return c;
   }
+  // the minimisation front -P, ordered by its first outcome (sort=True)
+  std::vector<int64_t> ord(np);
+  for (int64_t i = 0; i < np; ++i) ord[i] = i;
+  std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return -P[a * m] < -P[b * m]; });
+  std::vector<double> N((size_t)np * m);
+  for (int64_t i = 0; i < np; ++i)
+    for (int t = 0; t < m; ++t) N[i * m + t] = -P[ord[i] * m + t];
+  // aug_idx[r][t]: row r of the per-outcome order (0: ideal, 1..np: points, np+1: anti-ideal)
+  std::vector<int64_t> aug_idx((size_t)(np + 2) * m);
+  for (int t = 0; t < m; ++t) {
+    std::vector<int64_t> o(np);
+    for (int64_t i = 0; i < np; ++i) o[i] = i;
+    std::stable_sort(o.begin(), o.end(), [&](int64_t a, int64_t b) { return N[a * m + t] < N[b * m + t]; });
+    aug_idx[t] = 0;
+    for (int64_t i = 0; i < np; ++i) aug_idx[(i + 1) * m + t] = o[i] + 1;
+    aug_idx[(np + 1) * m + t] = np + 1;
+  }
+  // aug values for the tests: ideal - 1, the points, anti-ideal + 1
+  std::vector<double> aug((size_t)(np + 2) * m);
+  for (int t = 0; t < m; ++t) {
+    double lo = INF, hi = -INF;
+    for (int64_t i = 0; i < np; ++i) {
+      lo = std::min(lo, N[i * m + t]);
+      hi = std::max(hi, N[i * m + t]);
+    }
+    aug[t] = lo - 1.0;
+    for (int64_t i = 0; i < np; ++i) aug[(i + 1) * m + t] = N[i * m + t];
+    aug[(np + 1) * m + t] = hi + 1.0;
+  }
+  double total = 1.0;
+  for (int t = 0; t < m; ++t) total *= aug[(np + 1) * m + t] - aug[t];
+  // final bounds (maximisation): lower from the cell's upper index, upper from
+  // its lower index; row 0 -> +inf, row np + 1 -> ref, point rows -> P
+  auto bound = [&](int64_t row, int t, bool upper) {
+    if (row == 0) return INF;
+    if (row == np + 1) return ref[t];
+    (void)upper;
+    return -N[(row - 1) * m + t];
+  };
+  std::vector<int64_t> stack;  // cells: 2 m index entries each (lower row, upper row per outcome)
+  stack.reserve(64 * m);
+  for (int t = 0; t < m; ++t) stack.push_back(0);
+  for (int t = 0; t < m; ++t) stack.push_back(np + 1);
+  std::vector<int64_t> cell(2 * m), bidx(2 * m);
+  std::vector<double> bval(2 * m);
+  while (!stack.empty()) {
+    std::copy(stack.end() - 2 * m, stack.end(), cell.begin());
+    stack.resize(stack.size() - 2 * m);
+    for (int b = 0; b < 2; ++b)
+      for (int t = 0; t < m; ++t) {
+        bidx[b * m + t] = aug_idx[cell[b * m + t] * m + t];
+        bval[b * m + t] = aug[bidx[b * m + t] * m + t];
+      }
+    // for every point some outcome where the corner is no worse
+    auto corner_free = [&](int b) {
+      for (int64_t i = 0; i < np; ++i) {
+        bool any = false;
+        for (int t = 0; t < m && !any; ++t) any = bval[b * m + t] <= N[i * m + t];
+        if (!any) return false;
+      }
+      return true;
+    };
+    if (corner_free(1)) {
+      for (int t = 0; t < m; ++t) c.lo.push_back(bound(bidx[m + t], t, false));
+      for (int t = 0; t < m; ++t) c.hi.push_back(bound(bidx[t], t, true));
+      ++c.k;
+    } else if (corner_free(0)) {
+      bool not_adjacent = false;
+      int64_t length = -1;
+      int longest = 0;
+      double vol = 1.0;
+      for (int t = 0; t < m; ++t) {
+        const int64_t dist = cell[m + t] - cell[t];
+        not_adjacent = not_adjacent || dist > 1;
+        if (dist > length) {  // first maximum, as torch.max
+          length = dist;
+          longest = t;
+        }
+        vol *= bval[m + t] - bval[t];
+      }
+      if (not_adjacent && vol / total > alpha) {
+        const int64_t h1 = (int64_t)std::nearbyint((double)length / 2.0);  // round half to even
+        const int64_t h2 = length - h1;
+        std::vector<int64_t> a(cell), b(cell);
+        a[m + longest] -= h1;  // the upper half's bound
+        b[longest] += h2;      // the lower half's bound
+        stack.insert(stack.end(), a.begin(), a.end());
+        stack.insert(stack.end(), b.begin(), b.end());
+      }
+    }
+  }
+  return c;
+}
+
+template <class F>
+int partition_all(const double* Y, int64_t S, int64_t n, int m, int64_t K_cap, int64_t* K_out,
+                  double* cell_lo, double* cell_hi, int nthreads, F&& one) {
   std::vector<Cells> cells((size_t)S);
   std::atomic<int64_t> next(0);
   auto work = [&]() {
-    for (int64_t s = next++; s < S; s = next++) cells[s] = partition(Y + s * n * m, n, m, ref);
+    for (int64_t s = next++; s < S; s = next++) cells[s] = one(Y + s * n * m);
   };
   const int nt = std::max(1, std::min<int>(nthreads, (int)std::max<int64_t>(S, 1)));
   std::vector<std::thread> pool;
@@ -202,7 +309,7 @@ extern "C" int bo_nd_partition_host(const double* Y, int64_t S, int64_t n, int m
   *K_out = K;
   if (!cell_lo || !cell_hi) return BO_OK;  // size query
   if (K > K_cap) {
-    bo_set_error("bo_nd_partition_host: %lld cells needed, capacity %lld", (long long)K,
+    bo_set_error("box decomposition: %lld cells needed, capacity %lld", (long long)K,
                  (long long)K_cap);
     return BO_ERR_ARG;
   }
@@ -215,4 +322,31 @@ extern "C" int bo_nd_partition_host(const double* Y, int64_t S, int64_t n, int m
     std::copy(cells[s].hi.begin(), cells[s].hi.end(), hi);
   }
   return BO_OK;
+}
+
+}  // namespace
+
+extern "C" int bo_nd_partition_alpha_host(const double* Y, int64_t S, int64_t n, int m,
+                                          const double* ref, double alpha, int64_t K_cap,
+                                          int64_t* K_out, double* cell_lo, double* cell_hi,
+                                          int nthreads) {
+  if (S < 0 || n < 0 || m < 2 || (!Y && S * n > 0) || !ref || !K_out || !(alpha >= 0.0)) {
+    bo_set_error("bo_nd_partition_alpha_host: bad arguments (S %lld, n %lld, m %d, alpha %g)",
+                 (long long)S, (long long)n, m, alpha);
+    return BO_ERR_ARG;
+  }
+  return partition_all(Y, S, n, m, K_cap, K_out, cell_lo, cell_hi, nthreads,
+                       [&](const double* Ys) { return binary_partition(Ys, n, m, ref, alpha); });
+}
+
+extern "C" int bo_nd_partition_host(const double* Y, int64_t S, int64_t n, int m,
+                                    const double* ref, int64_t K_cap, int64_t* K_out,
+                                    double* cell_lo, double* cell_hi, int nthreads) {
+  if (S < 0 || n < 0 || m < 2 || (!Y && S * n > 0) || !ref || !K_out) {
+    bo_set_error("bo_nd_partition_host: bad arguments (S %lld, n %lld, m %d)", (long long)S,
+                 (long long)n, m);
+    return BO_ERR_ARG;
+  }
+  return partition_all(Y, S, n, m, K_cap, K_out, cell_lo, cell_hi, nthreads,
+                       [&](const double* Ys) { return partition(Ys, n, m, ref); });
 }

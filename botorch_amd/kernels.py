@@ -930,10 +930,14 @@ def sample_mvn(mean: torch.Tensor, L: torch.Tensor, Z: torch.Tensor) -> torch.Te
     return out.permute(1, 0, 2) + mean.unsqueeze(0)
 
 
-def nd_partition_host(Y: torch.Tensor, ref_point: torch.Tensor, nthreads: int = 0):
-    """Exact non-dominated box decompositions of S point sets (host, native
-    threads): Y (S x n x m, or n x m) -> (lo, hi) each S x K x m (K x m for a
-    single set), padded with empty cells as BoxDecompositionList does."""
+def nd_partition_host(Y: torch.Tensor, ref_point: torch.Tensor, nthreads: int = 0,
+                      alpha=None):
+    """Non-dominated box decompositions of S point sets (host, native threads):
+    Y (S x n x m, or n x m) -> (lo, hi) each S x K x m (K x m for a single
+    set), padded with empty cells as BoxDecompositionList does.  alpha None:
+    the exact FastNondominatedPartitioning cells (bo_nd_partition_host); a
+    number: NondominatedPartitioning's binary partitioning with that
+    approximation threshold (bo_nd_partition_alpha_host)."""
     single = Y.dim() == 2
     Yc = Y.detach().to("cpu", torch.float64).contiguous()
     if single:
@@ -946,8 +950,12 @@ def nd_partition_host(Y: torch.Tensor, ref_point: torch.Tensor, nthreads: int = 
     while True:
         lo = torch.empty(S, cap, m, dtype=torch.float64)
         hi = torch.empty(S, cap, m, dtype=torch.float64)
-        st = lib().bo_nd_partition_host(_p(Yc), S, n, m, _p(ref), cap, ctypes.byref(K), _p(lo),
-                                        _p(hi), nthreads)
+        if alpha is None:
+            st = lib().bo_nd_partition_host(_p(Yc), S, n, m, _p(ref), cap, ctypes.byref(K),
+                                            _p(lo), _p(hi), nthreads)
+        else:
+            st = lib().bo_nd_partition_alpha_host(_p(Yc), S, n, m, _p(ref), float(alpha), cap,
+                                                  ctypes.byref(K), _p(lo), _p(hi), nthreads)
         if st == _lib.BO_ERR_ARG and K.value > cap:
             cap = int(K.value)  # one retry with the exact size
             continue

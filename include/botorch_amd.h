@@ -525,6 +525,17 @@ int bo_nd_partition_host(const double* Y, int64_t S, int64_t n, int m, const dou
                          int64_t K_cap, int64_t* K_out, double* cell_lo, double* cell_hi,
                          int nthreads);
 
+/* HOST function: bo_nd_partition_host's contract with NondominatedPartitioning's
+ * binary partitioning instead (botorch/utils/multi_objective/box_decompositions/
+ * non_dominated.py:81-192 + get_hypercell_bounds :248-335): cells that straddle
+ * the front are halved until adjacent, and with alpha > 0 dropped once their
+ * volume is at most alpha of the box around the front (the approximate
+ * decomposition qNEHVI uses for alpha > 0, m > 2:
+ * utils/multi_objective/hypervolume.py:606-612, 744-758). */
+int bo_nd_partition_alpha_host(const double* Y, int64_t S, int64_t n, int m, const double* ref,
+                               double alpha, int64_t K_cap, int64_t* K_out, double* cell_lo,
+                               double* cell_hi, int nthreads);
+
 /* HOST function (plain host pointers; no GPU involved): the hit-and-run chain
  * of sample_polytope (botorch/utils/sampling.py:219-309) over {y : A y <= b}
  * (A m x k row-major, b m), from y0 (k).  Step t moves along the unit direction

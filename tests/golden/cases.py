@@ -39,3 +39,11 @@ POLYTOPE_CASES = {
     # (n, n_burnin, n_thinning, seed)
     "get_polytope_samples": [(20, 100, 4, 3), (64, 1000, 32, 0)],
 }
+
+# Approximate box decompositions (make_golden_mo.py): (m, n, seed, alphas).
+MO_ALPHA_CASES = [
+    (2, 20, 0, (0.0, 0.1)),
+    (3, 25, 1, (0.0, 0.001, 0.05)),
+    (3, 40, 2, (0.0, 0.01)),
+    (4, 12, 3, (0.0, 0.01)),
+]

@@ -107,3 +107,117 @@ def test_prune_inferior_points_multi_objective():
     kept_c = kept.cpu()
     for x in X[pm]:
         assert (kept_c == x).all(-1).any()
+
+
+def _qnehvi(model, Xb, S, seed, m, **kw):
+    from botorch_amd.acquisition import qNoisyExpectedHypervolumeImprovement
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    return qNoisyExpectedHypervolumeImprovement(model, [0.0] * m, Xb.to(DEV),
+                                                sampler=SobolQMCNormalSampler(torch.Size([S]),
+                                                                              seed=seed), **kw)
+
+
+def _value_and_grad(acqf, Xc):
+    Xd = Xc.to(DEV).requires_grad_(True)
+    v = acqf(Xd)
+    (g,) = torch.autograd.grad(v.sum(), Xd)
+    return v.detach().cpu(), g.cpu()
+
+
+def test_qnehvi_pending_appended_without_cache():
+    """cache_pending=False (hypervolume.py:821-822): the pending points are
+    appended to every q-batch (concatenate_pending_points) -- the same value
+    as the pending-free acquisition on [X, X_pending], gradient on X only."""
+    from oracle.acquisition import QNEHVIOracle
+    m, S, seed = 2, 16, 5
+    X, Y, model, oracles, Xb = _setup(m, seed=2)
+    Xp = X[40:42]
+    acq_p = _qnehvi(model, Xb, S, seed, m, cache_pending=False, X_pending=Xp.to(DEV))
+    acq_0 = _qnehvi(model, Xb, S, seed, m)
+    assert acq_p.X_baseline.shape[0] == Xb.shape[0] and acq_p.X_pending.shape[0] == 2
+    g = torch.Generator().manual_seed(11)
+    Xc = torch.rand(4, 2, 6, generator=g, dtype=torch.float64)
+    Xcat = torch.cat([Xc, Xp.expand(4, 2, 6)], dim=-2)
+    v, gx = _value_and_grad(acq_p, Xc)
+    v0, g0 = _value_and_grad(acq_0, Xcat)
+    torch.testing.assert_close(v, v0, rtol=0, atol=0)
+    torch.testing.assert_close(gx, g0[:, :2], rtol=0, atol=0)
+    orc = QNEHVIOracle(oracles, Xb, [0.0] * m, S, seed=seed)
+    torch.testing.assert_close(v, orc.value_exact(Xcat), rtol=1e-7, atol=1e-10)
+
+
+def test_qnehvi_max_iep():
+    """max_iep (hypervolume.py:795-820): up to max_iep new pending points ride
+    along with the q-batch; more join the baseline (decompositions rebuilt)."""
+    m, S, seed = 2, 16, 3
+    X, Y, model, oracles, Xb = _setup(m, seed=4)
+    acqf = _qnehvi(model, Xb, S, seed, m, max_iep=2)
+    g = torch.Generator().manual_seed(7)
+    Xc = torch.rand(3, 1, 6, generator=g, dtype=torch.float64)
+    acqf.set_X_pending(X[50:52].to(DEV))  # 2 <= max_iep: appended
+    assert acqf.X_baseline.shape[0] == Xb.shape[0] and acqf.X_pending.shape[0] == 2
+    ref = _qnehvi(model, Xb, S, seed, m, cache_pending=False, X_pending=X[50:52].to(DEV))
+    with torch.no_grad():
+        torch.testing.assert_close(acqf(Xc.to(DEV)), ref(Xc.to(DEV)), rtol=0, atol=0)
+    acqf.set_X_pending(X[50:53].to(DEV))  # 3 new > max_iep: joins the baseline
+    assert acqf.X_baseline.shape[0] == Xb.shape[0] + 3 and acqf.X_pending is None
+    fresh = _qnehvi(model, torch.cat([Xb, X[50:53]]), S, seed, m)
+    with torch.no_grad():
+        torch.testing.assert_close(acqf(Xc.to(DEV)), fresh(Xc.to(DEV)), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("m", [2, 3])
+def test_qnehvi_not_incremental(m):
+    """incremental_nehvi=False (hypervolume.py:741-742, 807-812): absorbing
+    pending points carries mean_s (HV_s(baseline + pending) - HV_s(baseline))+
+    in prev_nehvi; checked against exact hypervolumes of the oracle's samples."""
+    from oracle.acquisition import QNEHVIOracle
+    S, seed = 16, 9
+    X, Y, model, oracles, Xb = _setup(m, seed=6)
+    Xp = X[45:48]
+    acqf = _qnehvi(model, Xb, S, seed, m, incremental_nehvi=False)
+    init = QNEHVIOracle(oracles, Xb, [0.0] * m, S, seed=seed).initial_hv
+    torch.testing.assert_close(acqf._initial_hvs.cpu(), init, rtol=1e-9, atol=1e-12)
+    acqf.set_X_pending(Xp.to(DEV))
+    after = QNEHVIOracle(oracles, torch.cat([Xb, Xp]), [0.0] * m, S, seed=seed).initial_hv
+    prev = (after - init).clamp_min(0.0).mean()
+    assert prev > 0
+    torch.testing.assert_close(acqf._prev_nehvi.cpu(), prev, rtol=1e-9, atol=1e-12)
+    fresh = _qnehvi(model, torch.cat([Xb, Xp]), S, seed, m)
+    g = torch.Generator().manual_seed(3)
+    Xc = torch.rand(3, 2, 6, generator=g, dtype=torch.float64)
+    with torch.no_grad():
+        torch.testing.assert_close(acqf(Xc.to(DEV)), fresh(Xc.to(DEV)) + acqf._prev_nehvi,
+                                   rtol=0, atol=0)
+
+
+def test_qnehvi_approximate_partitioning():
+    """alpha > 0, m = 3: the per-sample cells are NondominatedPartitioning's
+    approximate binary partitioning (bo_nd_partition_alpha_host); the value is
+    the inclusion-exclusion over those cells (oracle restatement), and can only
+    fall below the exact one (dropped cells are non-dominated space)."""
+    from botorch_amd import kernels
+    from oracle.acquisition import QNEHVIOracle
+    m, S, seed = 3, 8, 2
+    X, Y, model, oracles, Xb = _setup(m, seed=8)
+    acqf = _qnehvi(model, Xb, S, seed, m, alpha=0.01)
+    lo, hi = kernels.nd_partition_host(acqf.baseline_samples, torch.zeros(m, dtype=torch.float64),
+                                       alpha=0.01)
+    assert torch.equal(acqf.cell_lower_bounds.cpu(), lo) and torch.equal(acqf.cell_upper_bounds.cpu(), hi)
+    g = torch.Generator().manual_seed(1)
+    Xc = torch.rand(4, 2, 6, generator=g, dtype=torch.float64)
+    orc = QNEHVIOracle(oracles, Xb, [0.0] * m, S, seed=seed)
+    v, gx = _value_and_grad(acqf, Xc)
+    Xo = Xc.clone().requires_grad_(True)
+    rv = orc.value_cells(Xo, lo, hi)
+    (go,) = torch.autograd.grad(rv.sum(), Xo)
+    torch.testing.assert_close(v, rv.detach(), rtol=1e-7, atol=1e-10)
+    torch.testing.assert_close(gx, go, rtol=1e-5, atol=1e-8)
+    assert (v <= orc.value_exact(Xc) + 1e-10).all()
+
+
+def test_qnehvi_without_cached_root_is_refused():
+    from botorch_amd.exceptions import UnsupportedError
+    X, Y, model, oracles, Xb = _setup(2)
+    with pytest.raises(UnsupportedError, match="cache_root"):
+        _qnehvi(model, Xb, 8, 0, 2, cache_root=False)
