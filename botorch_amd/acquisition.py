@@ -1163,8 +1163,11 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
         if X_pending is not None:
             self.set_X_pending(X_pending)
         # hypervolume.py:643-644: the first decomposition, unless set_X_pending
-        # already made it (more than max_iep pending points)
-        if X_pending is None or X_pending.shape[-2] <= self._max_iep:
+        # already made it (more than max_iep pending points joined the
+        # baseline).  Without cache_pending nothing joins, and the reference's
+        # condition would skip the decomposition altogether (its first forward
+        # then fails on the missing cell bounds): it is made here.
+        if not self._partitioned:
             self._set_cell_bounds()
 
     @property
