@@ -1094,11 +1094,31 @@ class _FusedQNEHVI(torch.autograd.Function):
         return dX, None
 
 
+class _QEHVIFromRoots(torch.autograd.Function):
+    """The fused hypervolume-improvement kernel (bo_qehvi) on caller-made
+    sample roots, f_s = mean + F_s + L z_s (mean m x B x q, L m x B x q x q,
+    F m x S x B q), as a differentiable function of (mean, L, F)."""
+
+    @staticmethod
+    def forward(ctx, mean, L, F, Zq, lo, hi, q):
+        acq = kernels.qehvi(mean, L, Zq, lo, hi, F=F, Qp=q)
+        ctx.save_for_backward(mean, L, F, Zq, lo, hi)
+        ctx.q = q
+        return acq
+
+    @staticmethod
+    def backward(ctx, dacq):
+        mean, L, F, Zq, lo, hi = ctx.saved_tensors
+        dmean, dL, dF = kernels.qehvi_backward(mean, L, Zq, lo, hi, dacq.contiguous(), F=F,
+                                               Qp=ctx.q)
+        return dmean, dL, dF, None, None, None, None
+
+
 class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
     """MC q-noisy expected hypervolume improvement (acquisition/multi_objective/
     monte_carlo.py:325-468; NoisyExpectedHypervolumeMixin,
     utils/multi_objective/hypervolume.py:507-835) for a ModelListGP of
-    SingleTaskGPs with the cached baseline root (cache_root=True):
+    SingleTaskGPs:
 
       qNEHVI(X) = mean_s HVI(f_s(X, X_pending) | Pareto front of f_s(X_baseline))
                   + prev_nehvi.
@@ -1111,6 +1131,11 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
     a common count (BoxDecompositionList), resident on the device as S x K x m.
     Forward / backward: _FusedQNEHVI over the q new points and the pending
     points not yet in the baseline.
+
+    cache_root=False: every forward samples the joint posterior of each
+    t-batch with its own root (_joint_forward) instead of the cached baseline
+    root and its low-rank update; the same quantity up to the jitter of the
+    (r + q) root.
 
     Pending points (hypervolume.py:778-822): with cache_pending, more than
     max_iep new ones join the baseline and the decompositions are rebuilt
@@ -1133,9 +1158,6 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
                                    f"X_baseline. Expected 2 dims, got {X_baseline.ndim}.")
         if constraints is not None:
             raise UnsupportedError("outcome constraints are not on the accelerated path")
-        if not cache_root:
-            raise UnsupportedError("qNEHVI here runs with the cached baseline root "
-                                   "(cache_root=True, the reference default)")
         models = getattr(model, "models", None)
         if models is None or not all(hasattr(mm, "prediction_cache") for mm in models):
             raise UnsupportedError("qNEHVI here runs on a ModelListGP of SingleTaskGPs")
@@ -1153,6 +1175,7 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
         self.cache_pending = bool(cache_pending)
         self._max_iep = int(max_iep)
         self.incremental_nehvi = bool(incremental_nehvi)
+        self._cache_root = bool(cache_root)
         self.X_pending = None
         if prune_baseline:
             X_baseline = prune_inferior_points_multi_objective(model, X_baseline, self.ref_point)
@@ -1257,8 +1280,39 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
             raise UnsupportedError(f"fused qNEHVI supports q <= 12 (pending points included) "
                                    f"and d <= {kernels.DP} on the device")
         X3 = X.reshape(-1, q, d)
-        acq = _FusedQNEHVI.apply(X3, self)
+        if self._cache_root:
+            acq = _FusedQNEHVI.apply(X3, self)
+        else:
+            acq = self._joint_forward(X3)
         return acq.reshape(batch) + self._prev_nehvi.to(acq)
+
+    def _joint_forward(self, X3: torch.Tensor) -> torch.Tensor:
+        """cache_root=False (monte_carlo.py:444-468, cached_cholesky.py:161-165):
+        every forward samples the joint posterior over [X_baseline; X] of each
+        t-batch -- its own jittered (r + q) Cholesky -- with the cached
+        baseline base samples in the leading r columns (the base sampler's)
+        and the new point's columns after them, and keeps the new rows:
+        f = mean_X + Z_b L[X, b]^T + L[X, X] z.  The hypervolume improvement
+        over the per-sample cells is the fused kernel's; moments, the joint
+        root and its gradient are the general differentiable kernels'."""
+        B, q, d = X3.shape
+        Xb = self.X_baseline.to(X3)
+        r = Xb.shape[-2]
+        Xf = torch.cat([Xb.expand(B, r, d), X3], dim=-2)
+        means, Ls, Fs = [], [], []
+        for t, mm in enumerate(self.model.models):
+            post = mm.posterior(Xf)
+            mean = post.distribution.mean.reshape(B, r + q)
+            Lj = post.distribution.scale_tril.reshape(B, r + q, r + q)
+            Zb = self._roots[t].Z_base.to(Lj)                              # S x r
+            F = torch.matmul(Zb, Lj[:, r:, :r].mT).permute(1, 0, 2)       # S x B x q
+            means.append(mean[:, r:])
+            Ls.append(Lj[:, r:, r:])
+            Fs.append(F.reshape(Zb.shape[0], B * q))
+        Zq = self._base_samples_q(q, X3.device)
+        lo, hi = self._cells
+        return _QEHVIFromRoots.apply(torch.stack(means), torch.stack(Ls), torch.stack(Fs), Zq,
+                                     lo, hi, q)
 
 
 def cells_hypervolume(Y: torch.Tensor, ref: torch.Tensor, lo: torch.Tensor,

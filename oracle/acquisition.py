@@ -312,6 +312,29 @@ class QNEHVIOracle:
             out.append(f)
         return torch.stack(out, dim=-1)
 
+    def samples_joint(self, X):
+        """cache_root=False (monte_carlo.py:444-468, cached_cholesky.py:161-165):
+        the joint posterior over [X_baseline; X] of each t-batch, its own
+        psd_safe_cholesky, base samples with the baseline draw in the leading
+        r columns; the new rows.  S x b x q x m."""
+        b, q, d = X.shape
+        r, m = self.Xb.shape[0], len(self.models)
+        Zq = draw_sobol_normal_samples((r + q) * m, self.S, self.seed).view(self.S, r + q, m)[:, r:, :]
+        Xf = torch.cat([self.Xb.expand(b, r, d), X], dim=-2)
+        out = []
+        for t, mdl in enumerate(self.models):
+            mean, cov = mdl.posterior(Xf)
+            L, _ = psd_safe_cholesky(cov)
+            z = torch.cat([self.Zb[:, :, t], Zq[:, :, t]], dim=-1)   # S x (r + q)
+            f = mean.unsqueeze(0) + torch.einsum("bij,sj->sbi", L, z)
+            out.append(f[..., r:])
+        return torch.stack(out, dim=-1)
+
+    def value_cells_joint(self, X, cell_lo, cell_hi):
+        f = self.samples_joint(X)
+        vals = [qehvi_from_samples(f[s:s + 1], cell_lo[s], cell_hi[s]) for s in range(f.shape[0])]
+        return torch.stack(vals, dim=0).mean(dim=0)
+
     def value_exact(self, X):
         """mean_s [HV(front_s + new points) - HV(front_s)] by exact hypervolumes."""
         f = self.samples(X).detach()

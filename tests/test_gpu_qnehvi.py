@@ -216,8 +216,28 @@ def test_qnehvi_approximate_partitioning():
     assert (v <= orc.value_exact(Xc) + 1e-10).all()
 
 
-def test_qnehvi_without_cached_root_is_refused():
-    from botorch_amd.exceptions import UnsupportedError
-    X, Y, model, oracles, Xb = _setup(2)
-    with pytest.raises(UnsupportedError, match="cache_root"):
-        _qnehvi(model, Xb, 8, 0, 2, cache_root=False)
+@pytest.mark.parametrize("m,q", [(2, 2), (3, 1)])
+def test_qnehvi_without_cached_root(m, q):
+    """cache_root=False: the joint (r + q) root of every t-batch per forward;
+    value and gradient against the oracle's joint sampling over the same cells,
+    and the cached-root value (the same quantity without jitter)."""
+    from oracle.acquisition import QNEHVIOracle
+    S, seed = 16, 4
+    X, Y, model, oracles, Xb = _setup(m, seed=3)
+    acq_j = _qnehvi(model, Xb, S, seed, m, cache_root=False)
+    acq_c = _qnehvi(model, Xb, S, seed, m)
+    assert torch.equal(acq_j.cell_lower_bounds, acq_c.cell_lower_bounds)
+    g = torch.Generator().manual_seed(2 + m)
+    Xc = torch.rand(4, q, 6, generator=g, dtype=torch.float64)
+    v, gx = _value_and_grad(acq_j, Xc)
+    vc, gc = _value_and_grad(acq_c, Xc)
+    orc = QNEHVIOracle(oracles, Xb, [0.0] * m, S, seed=seed)
+    Xo = Xc.clone().requires_grad_(True)
+    lo, hi = acq_j.cell_lower_bounds.cpu(), acq_j.cell_upper_bounds.cpu()
+    rv = orc.value_cells_joint(Xo, lo, hi)
+    (go,) = torch.autograd.grad(rv.sum(), Xo)
+    assert (rv > 0).any()
+    torch.testing.assert_close(v, rv.detach(), rtol=1e-7, atol=1e-10)
+    torch.testing.assert_close(gx, go, rtol=1e-5, atol=1e-8)
+    torch.testing.assert_close(v, vc, rtol=1e-6, atol=1e-9)
+    torch.testing.assert_close(gx, gc, rtol=1e-4, atol=1e-7)
