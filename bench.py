@@ -265,15 +265,17 @@ def other_configs(dev, cpu=True):
     m_c2, bf_c2 = m, float(Y.max()) - 0.3
     acqf = qExpectedImprovement(m, float(Y.max()), sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
     Xd = Xc.to(dev)
+    # a call is ~0.07 ms: 200 back-to-back calls give the steady per-call rate
+    # (20 of them were dominated by the first call's latency)
     with torch.no_grad():
-        t = _gpu_time(lambda: acqf(Xd), steps=20, warmup=3)
+        t = _gpu_time(lambda: acqf(Xd), steps=200, warmup=20)
     e = {"config": "C2 qEI n=1024 d=6 q=8 S=256 b=64", "gpu_evals_per_s": q * S * b / t,
-         "gpu_ms": 1e3 * t}
+         "gpu_ms": 1e3 * t, "calls_timed": 200}
     # the same forward (and forward + backward) captured once as a HIP graph and
     # replayed (botorch_amd.graphs; values bit-equal to the eager call)
     from botorch_amd.graphs import GraphedAcquisition
     ga = GraphedAcquisition(acqf, Xd)
-    tg = _gpu_time(lambda: ga(Xd), steps=50, warmup=5)
+    tg = _gpu_time(lambda: ga(Xd), steps=200, warmup=20)
     Xg = Xd.clone().requires_grad_(True)
 
     def c2_fb():
