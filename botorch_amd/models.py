@@ -30,6 +30,35 @@ LENGTHSCALE_LOWER = 2.5e-2       # gpytorch_modules.py:123
 SQRT2, SQRT3 = math.sqrt(2), math.sqrt(3)
 
 
+# Generation of the model trees' structure: bumped whenever a parameter or a
+# submodule is (re)assigned inside one (an in-place change of a parameter's
+# values bumps its tensor _version instead).  SingleTaskGP._key() reuses its
+# list of parameters until this changes -- walking the module tree on every
+# acquisition call was its largest host cost.
+_STRUCTURE = [0]
+
+
+class _TrackedModule(nn.Module):
+    """nn.Module whose parameter / submodule (re)assignments bump _STRUCTURE."""
+
+    def __setattr__(self, name, value):
+        super().__setattr__(name, value)
+        if isinstance(value, (nn.Parameter, nn.Module)):
+            _STRUCTURE[0] += 1
+
+    def __delattr__(self, name):
+        super().__delattr__(name)
+        _STRUCTURE[0] += 1
+
+    def register_parameter(self, name, param):
+        super().register_parameter(name, param)
+        _STRUCTURE[0] += 1
+
+    def add_module(self, name, module):
+        super().add_module(name, module)
+        _STRUCTURE[0] += 1
+
+
 class LogNormalPrior:
     """[G] LogNormalPrior(loc, scale) (torch LogNormal)."""
 
@@ -46,7 +75,7 @@ class LogNormalPrior:
                 - 0.5 * math.log(2 * math.pi) - lx)
 
 
-class _Kernel(nn.Module):
+class _Kernel(_TrackedModule):
     kind = _lib.RBF
 
     def __init__(self, ard_num_dims: int, lengthscale_prior: Optional[LogNormalPrior] = None,
@@ -86,7 +115,7 @@ class MaternKernel(_Kernel):
         super().__init__(**kw)
 
 
-class ScaleKernel(nn.Module):
+class ScaleKernel(_TrackedModule):
     """outputscale * base_kernel ([G] ScaleKernel)."""
 
     def __init__(self, base_kernel: _Kernel, outputscale: float = 1.0, outputscale_prior=None):
@@ -112,7 +141,7 @@ class ScaleKernel(nn.Module):
             self.raw_outputscale.fill_(float(v))
 
 
-class GaussianLikelihood(nn.Module):
+class GaussianLikelihood(_TrackedModule):
     """Homoskedastic Gaussian noise ([G] GaussianLikelihood) with BoTorch's
     LogNormal(-4, 1) prior and noise >= 1e-4 (gpytorch_modules.py:74-97)."""
 
@@ -134,7 +163,7 @@ class GaussianLikelihood(nn.Module):
             self.raw_noise.copy_(torch.as_tensor(v, dtype=torch.float64).reshape(1))
 
 
-class FixedNoiseGaussianLikelihood(nn.Module):
+class FixedNoiseGaussianLikelihood(_TrackedModule):
     """Observed per-point noise variances ([G] FixedNoiseGaussianLikelihood with
     learn_additional_noise=False), the likelihood SingleTaskGP builds from
     train_Yvar (botorch/models/gp_regression.py:187-194).  Nothing is learned:
@@ -149,7 +178,7 @@ class FixedNoiseGaussianLikelihood(nn.Module):
         self.register_buffer("noise", torch.as_tensor(noise, dtype=torch.float64).reshape(-1).clone())
 
 
-class ConstantMean(nn.Module):
+class ConstantMean(_TrackedModule):
     def __init__(self):
         super().__init__()
         self.raw_constant = nn.Parameter(torch.tensor(0.0, dtype=torch.float64))
@@ -177,7 +206,7 @@ def get_gaussian_likelihood_with_lognormal_prior():
     return GaussianLikelihood(noise_prior=LogNormalPrior(-4.0, 1.0))
 
 
-class Standardize(nn.Module):
+class Standardize(_TrackedModule):
     """Outcome standardisation (botorch/models/transforms/outcome.py:217-447)."""
 
     def __init__(self, m: int, min_stdv: float = 1e-8):
@@ -231,7 +260,7 @@ class _StackedView:
                              "model.models[t]")
 
 
-class Model(nn.Module):
+class Model(_TrackedModule):
     """Abstract model with BoTorch's ``posterior`` contract (models/model.py:82-117)."""
 
     _num_outputs = 1
@@ -402,7 +431,11 @@ class SingleTaskGP(Model):
     def _key(self):
         if self._is_multi_output:
             return tuple(mm._key() for mm in self.models)
-        ps = [self.train_inputs[0], self.train_targets] + list(self.parameters())
+        d = self.__dict__
+        if d.get("_plist_gen") != _STRUCTURE[0]:
+            d["_plist"] = list(self.parameters())
+            d["_plist_gen"] = _STRUCTURE[0]
+        ps = [self.train_inputs[0], self.train_targets] + d["_plist"]
         return tuple((p.data_ptr(), p._version) for p in ps)
 
     def prediction_cache(self, key=None):
