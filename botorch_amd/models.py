@@ -276,11 +276,13 @@ class Model(_TrackedModule):
         """(mean, std) of the Standardize transform as host floats, read back once
         per change of the buffers (not per acquisition call: each read is a
         device-to-host sync)."""
-        if not hasattr(self, "outcome_transform"):
+        ot = self._modules.get("outcome_transform")
+        if ot is None:
             return 0.0, 1.0
-        ot = self.outcome_transform
-        m, s = ot.means, ot.stdvs
-        key = (getattr(ot, "_generation", 0), m.data_ptr(), m._version, s.data_ptr(), s._version)
+        bufs = ot._buffers  # (direct: nn.Module attribute lookups cost per call)
+        m, s = bufs["means"], bufs["stdvs"]
+        key = (ot.__dict__.get("_generation", 0), m.data_ptr(), m._version, s.data_ptr(),
+               s._version)
         if getattr(self, "_ostats_key", None) != key:
             self._ostats = (float(m.reshape(-1)[0]), float(s.reshape(-1)[0]))
             self._ostats_key = key
