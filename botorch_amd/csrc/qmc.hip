@@ -24,6 +24,13 @@ namespace {
 
 constexpr int QMAX = 16;
 
+__device__ __forceinline__ double rsq_nr(double v) {
+  double r = __builtin_amdgcn_rsq(v);
+  r = r * fma(-0.5 * v * r, r, 1.5);
+  r = r * fma(-0.5 * v * r, r, 1.5);
+  return r;
+}
+
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const long long x = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), l);
@@ -229,7 +236,6 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   // (S x ldF) the samples' baseline term Z_base T; then
   //   br = Sigma'_qq - T^T T,  f = mu' + F + chol(br) Z_q.
   __shared__ double Sig[QMAX][QMAX + 1];
-  __shared__ double colb[QMAX];  // the Cholesky's current column (wave 0)
   __shared__ double Lq[QMAX][QMAX + 1];
   __shared__ double mu[QMAX];
   __shared__ double red[THREADS / 64];
@@ -337,17 +343,19 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
         if (j < q) {
           const double ajj = readlane_d(r[j], j);
           if (!(ajj > 0.0) && info == 0) info = j + 1;
-          const double djj = sqrt(ajj);
-          double lij = (a == j) ? djj : r[j] / djj;
+          // one reciprocal square root (two Newton steps) instead of sqrt and
+          // a division on the column's dependent chain: l_jj = a_jj / sqrt(a_jj)
+          // rounds like sqrt to within an ulp
+          const double rinv = rsq_nr(ajj);
+          double lij = (a == j) ? ajj * rinv : r[j] * rinv;
           if (a < j) lij = 0.0;
           r[j] = lij;
-          // column j of L to every lane through LDS (one write, uniform
-          // reads) instead of a ds_bpermute pair per entry: the same values,
-          // the same FMAs (round 3: 300 bpermutes per t-batch at q = 16)
-          if (a < QMAX) colb[a] = lij;
+          // column j to every lane by v_readlane (uniform, into SGPRs): no LDS
+          // round trip on the chain (round 3: the LDS broadcast replaced 300
+          // ds_bpermute per t-batch at q = 16)
 #pragma unroll
           for (int l = j + 1; l < QMAX; ++l) {
-            if (l < q) r[l] = fma(-lij, colb[l], r[l]);
+            if (l < q) r[l] = fma(-lij, readlane_d(lij, l), r[l]);
           }
         }
       }
