@@ -891,6 +891,26 @@ SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, int mod
   return p;
 }
 
+// The chunk count of a plan (its workspace size), memoised: building a plan
+// walks every segment of the grid (C2's stream-K plan: ~56 us of host time,
+// b = 128 at n = 4096: ~255 us), and the eager operator asks for the
+// workspace on every call.
+std::mutex g_chunks_mu;
+std::map<std::tuple<int, int, int, int, int, int>, int> g_chunks;  // (nC, nI, n, kc, slots, mode)
+
+int plan_chunks(int nC, int nI, int n, int kc_len, int slots, int mode) {
+  const auto key = std::make_tuple(nC, nI, n, kc_len, slots, mode);
+  {
+    std::lock_guard<std::mutex> lk(g_chunks_mu);
+    auto it = g_chunks.find(key);
+    if (it != g_chunks.end()) return it->second;
+  }
+  const int c = build_split_plan(nC, nI, n, kc_len, slots, mode).nchunks;
+  std::lock_guard<std::mutex> lk(g_chunks_mu);
+  g_chunks[key] = c;
+  return c;
+}
+
 struct DevPlan {
   int4 *segs = nullptr, *red = nullptr;
   int* wg_off = nullptr;
@@ -959,9 +979,8 @@ int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len,
   const bool paired = nC % 16 == 0 && nI % 8 == 0 && paired_enabled();
   if (paired && tiles >= 2 * (int64_t)slots) return BO_OK;
   if (tiles < 4 * (int64_t)slots && steps >= slots) {
-    const SplitPlan p = build_split_plan(nC, (int)nI, (int)n, -1, slots);
     *kc_len = -1;
-    *work_elems = (int64_t)p.nchunks * PI * PC;
+    *work_elems = (int64_t)plan_chunks(nC, (int)nI, (int)n, -1, slots, PLAN_POST) * PI * PC;
   }
   return BO_OK;
 }
@@ -972,8 +991,7 @@ int bo_post_split_work(int64_t B, int q, int64_t n, int kc_len, int64_t* work_el
   if (s) return s;
   *work_elems = 0;
   if (kc_len == 0 || nrows_pad == 0) return BO_OK;
-  const SplitPlan p = build_split_plan(nC, nrows_pad / PI, (int)n, kc_len, kSlots);
-  *work_elems = (int64_t)p.nchunks * PI * PC;
+  *work_elems = (int64_t)plan_chunks(nC, nrows_pad / PI, (int)n, kc_len, kSlots, PLAN_POST) * PI * PC;
   return BO_OK;
 }
 
@@ -1326,9 +1344,8 @@ int bo_post_w_work(int B, int q, int64_t n, int* kc_len, int64_t* work_elems) {
   const bool paired = nC % 16 == 0 && nI % 8 == 0 && paired_enabled();  // as bo_post_split_plan
   if (paired && (int64_t)nC * nI >= 2 * (int64_t)kSlots) return BO_OK;
   if (nI > 0 && (int64_t)nC * nI < 4 * (int64_t)kSlots && steps >= kSlots) {
-    const SplitPlan p = build_split_plan(nC, nI, (int)n, -1, kSlots, PLAN_LOWER);
     *kc_len = -1;
-    *work_elems = (int64_t)p.nchunks * PI * PC;
+    *work_elems = (int64_t)plan_chunks(nC, nI, (int)n, -1, kSlots, PLAN_LOWER) * PI * PC;
   }
   return BO_OK;
 }
@@ -1367,8 +1384,7 @@ int bo_post_w_split(const double* Linv, int64_t ldl, const double* Rt, int B, in
 // k-ranges [128 ci, n) are very unequal), partial tiles reduced in k order.
 int bo_ainv_work(int64_t n, int64_t* work_elems) {
   const int nC = (int)ceil_div(n, PC);
-  const SplitPlan p = build_split_plan(nC, nC, (int)n, -1, kSlots, PLAN_AINV);
-  *work_elems = (int64_t)p.nchunks * PI * PC;
+  *work_elems = (int64_t)plan_chunks(nC, nC, (int)n, -1, kSlots, PLAN_AINV) * PI * PC;
   return BO_OK;
 }
 
