@@ -23,6 +23,8 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/chol_fe
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/chol_write -o run -- python3 tools/chol_only.py > $O/chol_write.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $O/chol_mfma -o run -- python3 tools/chol_only.py > $O/chol_mfma.log 2>&1 || exit $?
 python3 tools/pmc_summary.py --meta command=chol_only $O/pmc_chol.json $O/chol_fetch $O/chol_write $O/chol_mfma || exit $?
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c2 -o run -- python3 tools/prof_small.py c2 > $O/c2.log 2>&1 || exit $?
+timeout -k 10 300 python3 tools/host_c2_breakdown.py > $O/host_c2.log 2>&1 || exit $?
 timeout -k 10 700 python3 bench.py > $O/bench_default.log 2>&1 || exit $?
 echo "bench: $(grep -c '^{' $O/bench_default.log) line(s)"
 find $O -name '*_trace.csv' -size +2M -delete
