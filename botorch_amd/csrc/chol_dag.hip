@@ -1584,7 +1584,20 @@ std::vector<int4> build_tasks_batched(int T, int nb) {
   // one matrix, or batches of small ones (n <= 2048: C4's 3 x 2048 0.855-0.867
   // -> 0.797-0.805 ms), take 2 / 4 rows; batches of n = 4096 keep 8 / 8 (with
   // 2 / 4: 4 x 4096 5.38 -> 5.69 ms; profiles/r03/cholesky/ab_ch_batched_small.log)
-  const std::vector<int4> one = (nb == 1 || T <= 32) ? build_tasks(T, 2, 4) : build_tasks(T, CH, CHB);
+  // (BO_CHOL_CH / BO_CHOL_CHB override the one-matrix chunk rows: an A/B knob,
+  // read once, 1..16)
+  static const int ch1 = [] {
+    const char* e = getenv("BO_CHOL_CH");
+    const int v = e ? atoi(e) : 2;
+    return v >= 1 && v <= 16 ? v : 2;
+  }();
+  static const int chb1 = [] {
+    const char* e = getenv("BO_CHOL_CHB");
+    const int v = e ? atoi(e) : 4;
+    return v >= 1 && v <= 16 ? v : 4;
+  }();
+  const std::vector<int4> one =
+      (nb == 1 || T <= 32) ? build_tasks(T, ch1, chb1) : build_tasks(T, CH, CHB);
   if (nb == 1) return one;
   double stagger = 0.0;
   if (const char* e = getenv("BO_CHOL_BATCH_STAGGER")) {  // finite values only (sort keys)
