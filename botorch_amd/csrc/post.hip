@@ -652,28 +652,31 @@ __global__ __launch_bounds__(256) void kxt_build_kernel(const double* __restrict
   }
 }
 
-// Split reduction: one wave per 16-row tile of every tile split over several
-// chunks (red: column tile, row tile, first chunk, chunk count) sums the
-// chunk partials in k order and runs the epilogue.
-__global__ __launch_bounds__(64) void post_splitk_reduce_kernel(
+// Split reduction: one workgroup of four waves per 16-row tile of every tile
+// split over several chunks (red: column tile, row tile, first chunk, chunk
+// count).  Wave w sums the chunks first + w, first + w + 4, ... in k order
+// (two chunks' loads in flight per round), waves 1-3 hand their sums to wave 0
+// through LDS, which adds them in wave order and runs the epilogue: four
+// times the loads in flight per tile of the one-wave form (C2's longest tiles
+// have 16 chunks, each round one memory latency), a fixed summation order.
+__global__ __launch_bounds__(256) void post_splitk_reduce_kernel(
     const double* __restrict__ work, const int4* __restrict__ red, int n, int nI,
     const double* __restrict__ beta, double* __restrict__ Spart, double* __restrict__ mpart,
     double* __restrict__ Rt) {
+  __shared__ double part[3][32][64];
   const int4 r4 = red[blockIdx.x / (PI / 16)];
   const int sub = blockIdx.x % (PI / 16);
   const int ci = r4.x, rt = r4.y * (PI / 16) + sub;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
   v4d acc[8];
 #pragma unroll
   for (int ct = 0; ct < 8; ++ct) acc[ct] = v4d_zero();
-  // two chunks' loads in flight per round, added in k order (the same
-  // additions in the same order as one chunk at a time: C2's longest tiles
-  // have 16 chunks, and each round's loads cost one memory latency)
   const int cend = r4.z + r4.w;
-  int c = r4.z;
-  for (; c + 1 < cend; c += 2) {
+  int c = r4.z + wave;
+  for (; c + 4 < cend; c += 8) {
     const double* w0 = work + ((int64_t)c * (PI / 16) + sub) * kTileDoubles + lane;
-    const double* w1 = w0 + (PI / 16) * kTileDoubles;
+    const double* w1 = w0 + 4 * (PI / 16) * kTileDoubles;
     double v0[32], v1[32];
 #pragma unroll
     for (int e = 0; e < 32; ++e) {
@@ -696,6 +699,20 @@ __global__ __launch_bounds__(64) void post_splitk_reduce_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[ct][r] += w[(ct * 4 + r) * 64];
   }
+  if (wave > 0) {
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[wave - 1][ct * 4 + r][lane] = acc[ct][r];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[ct][r] += part[w][ct * 4 + r][lane];
   if (Rt != nullptr) post_store_rt(acc, ci, rt * 16, lane, nI, Rt);
   if (Spart != nullptr) post_epilogue(acc, ci, rt * 16, lane, n, beta, nI, Spart, mpart);
 }
@@ -1233,7 +1250,7 @@ int bo_post_partials_layout(int kind, const double* Xq, int B, int q, int d,
 #undef BO_POST_GO
   BO_LAUNCH_CHECK();
   if (plan && plan->nred > 0) {
-    post_splitk_reduce_kernel<<<(unsigned)(plan->nred * (PI / 16)), 64, 0, st>>>(
+    post_splitk_reduce_kernel<<<(unsigned)(plan->nred * (PI / 16)), 256, 0, st>>>(
         work, plan->red, (int)n, nI, beta, Spart, mpart, Rt);
     BO_LAUNCH_CHECK();
   }
@@ -1371,7 +1388,7 @@ int bo_post_w_split(const double* Linv, int64_t ldl, const double* Rt, int B, in
       plan->wg_off, work, nullptr, 0, 0, nullptr, Rt, 0);
   BO_LAUNCH_CHECK();
   if (plan->nred > 0) {
-    post_splitk_reduce_kernel<<<(unsigned)(plan->nred * (PI / 16)), 64, 0, st>>>(
+    post_splitk_reduce_kernel<<<(unsigned)(plan->nred * (PI / 16)), 256, 0, st>>>(
         work, plan->red, (int)n, nI, nullptr, nullptr, nullptr, Wt);
     BO_LAUNCH_CHECK();
   }
@@ -1403,7 +1420,7 @@ int bo_ainv(const double* Linv, int64_t ld, int64_t n, double* Ainv, double* wor
       plan->wg_off, work, nullptr, 0, 0, nullptr, Linv, 0);
   BO_LAUNCH_CHECK();
   if (plan->nred > 0) {
-    post_splitk_reduce_kernel<<<(unsigned)(plan->nred * (PI / 16)), 64, 0, st>>>(
+    post_splitk_reduce_kernel<<<(unsigned)(plan->nred * (PI / 16)), 256, 0, st>>>(
         work, plan->red, (int)n, nC, nullptr, nullptr, nullptr, Ainv);
     BO_LAUNCH_CHECK();
   }
