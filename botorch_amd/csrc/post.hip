@@ -995,7 +995,12 @@ int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len,
   // (paired one pass) vs 1266 us (stream-K) (profiles/r03/time_posterior_paired.json).
   const bool paired = nC % 16 == 0 && nI % 8 == 0 && paired_enabled();
   if (paired && tiles >= 2 * (int64_t)slots) return BO_OK;
-  if (tiles < 4 * (int64_t)slots && steps >= slots) {
+  // ... or wherever one tile's k-range alone is long: a one-pass grid of a few
+  // row tiles runs its longest column tile as one workgroup's chain of k-steps
+  // (b = 1, q = 8, n = 1024: 8 workgroups, 64 steps in a row, ~165 us per
+  // call against ~60 us cut into shares)
+  const int64_t longest = ceil_div(std::min<int64_t>(n, (int64_t)nC * PC), PK);
+  if (tiles < 4 * (int64_t)slots && (steps >= slots || longest > 4 * sk_min_share())) {
     *kc_len = -1;
     *work_elems = (int64_t)plan_chunks(nC, (int)nI, (int)n, -1, slots, PLAN_POST) * PI * PC;
   }
@@ -1360,7 +1365,9 @@ int bo_post_w_work(int B, int q, int64_t n, int* kc_len, int64_t* work_elems) {
   for (int ci = 0; ci < nC; ++ci) steps += (int64_t)nI * ceil_div(n - ci * PC, PK);
   const bool paired = nC % 16 == 0 && nI % 8 == 0 && paired_enabled();  // as bo_post_split_plan
   if (paired && (int64_t)nC * nI >= 2 * (int64_t)kSlots) return BO_OK;
-  if (nI > 0 && (int64_t)nC * nI < 4 * (int64_t)kSlots && steps >= kSlots) {
+  const int64_t longest = ceil_div(n, PK);  // tile 0's k-range [0, n)
+  if (nI > 0 && (int64_t)nC * nI < 4 * (int64_t)kSlots &&
+      (steps >= kSlots || longest > 4 * sk_min_share())) {
     *kc_len = -1;
     *work_elems = (int64_t)plan_chunks(nC, nI, (int)n, -1, kSlots, PLAN_LOWER) * PI * PC;
   }
