@@ -623,7 +623,7 @@ __global__ __launch_bounds__(256) void kxt_build_kernel(const double* __restrict
                                                         const double* __restrict__ Xt, int n,
                                                         int np, int nrows_pad, double outputscale,
                                                         double* __restrict__ Kt,
-                                                        RowsFromX rx = RowsFromX{}, int nt = 0) {
+                                                        RowsFromX rx = RowsFromX{}) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int k0 = blockIdx.y * KK;
   const bool iv = i < nrows;
@@ -648,12 +648,7 @@ __global__ __launch_bounds__(256) void kxt_build_kernel(const double* __restrict
 #pragma unroll 4
   for (int kk = 0; kk < KK; ++kk) {
     const int k = k0 + kk;
-    if (k < np) {
-      const double v = eval_kernel_row<KIND, ND>(xi, Xt, n, k, outputscale, iv);
-      double* dst = Kt + (int64_t)k * nrows_pad + i;
-      if (nt) __builtin_nontemporal_store(v, dst);  // (uniform) streaming store: an A/B knob
-      else *dst = v;
-    }
+    if (k < np) Kt[(int64_t)k * nrows_pad + i] = eval_kernel_row<KIND, ND>(xi, Xt, n, k, outputscale, iv);
   }
 }
 
@@ -1113,16 +1108,6 @@ static int kxt_small_k() {
 }
 
 // bo_prepare_rows + bo_post_kxt in one launch: Xq and K*x^T from X itself.
-// BO_KXT_NT=1: the K*x^T build writes with nontemporal (streaming) stores -- an
-// A/B knob, read once (default 0: plain stores).
-static int kxt_nt() {
-  static const int v = [] {
-    const char* e = std::getenv("BO_KXT_NT");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  return v;
-}
-
 int bo_post_kxt_rows(int kind, const double* X, int B, int q, int d, const double* lengthscale,
                      const double* Xt_scaled, int64_t n, double outputscale, double* Xq, double* Kt,
                      void* stream) {
@@ -1142,8 +1127,7 @@ int bo_post_kxt_rows(int kind, const double* X, int B, int q, int d, const doubl
   const dim3 grid((unsigned)ceil_div(nrows_pad, 256), (unsigned)ceil_div(np, kk));
 #define BO_KXTR_K(KIND, ND, K)                                                                 \
   kxt_build_kernel<KIND, ND, K, true><<<grid, 256, 0, st>>>(nullptr, nrows, Xt_scaled, (int)n,  \
-                                                            np, nrows_pad, outputscale, Kt, rx, \
-                                                            kxt_nt())
+                                                            np, nrows_pad, outputscale, Kt, rx)
 #define BO_KXTR(KIND, ND)                  \
   switch (kk) {                            \
     case 1: BO_KXTR_K(KIND, ND, 1); break; \
