@@ -40,6 +40,23 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 constexpr int DP = 8;
 constexpr int THREADS = 256;
 
+// Phase clocks of the tools-only build (-DBO_QMC_PHASES, tools/qmc_phases.sh):
+// workgroup b's 100 MHz wall clock at entry (0), the finalised covariance (1),
+// the factor (2), the reduced value (3) and its exit (4); never in the product.
+#ifdef BO_QMC_PHASES
+constexpr int PH_N = 5, PH_WG = 1024;
+__device__ unsigned long long g_qmc_phase[PH_WG * PH_N];
+#define QMC_PHASE(k)                                                     \
+  do {                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < PH_WG)                          \
+      g_qmc_phase[blockIdx.x * PH_N + (k)] = wall_clock64();             \
+  } while (0)
+#else
+#define QMC_PHASE(k) \
+  do {               \
+  } while (0)
+#endif
+
 enum QmcMode : int {
   QMC_POSTERIOR = 0,
   QMC_QEI = 1,
@@ -188,21 +205,16 @@ __device__ __forceinline__ void sample_phase(int tid, int q, int S, int row0,
   }
 }
 
-// One sample per thread (S <= THREADS): z row in registers, L_q from LDS.
+// One sample per thread (S <= THREADS): the z row (zs) and the sample's best
+// (bf) were loaded at the kernel's entry, L_q from LDS.
 template <int MODE>
 __device__ __forceinline__ void sample_serial(int tid, int q, int S, int row0,
                                               const double (&Lq)[QMAX][QMAX + 1],
-                                              const double (&mu)[QMAX], const double* __restrict__ Z,
-                                              const double* __restrict__ F, int64_t ldF,
-                                              double best_f, const double* __restrict__ best_f_s,
+                                              const double (&mu)[QMAX], const double (&zs)[QMAX],
+                                              double bf, const double* __restrict__ F, int64_t ldF,
                                               const LogRedParams& lp, double& sum, LseAcc& lse) {
   const int s = tid;
   if (s >= S) return;
-  const double* z = Z + (int64_t)s * q;
-  double zs[QMAX];
-#pragma unroll
-  for (int j = 0; j < QMAX; ++j) zs[j] = (j < q) ? z[j] : 0.0;
-  const double bf = per_sample_best(MODE) ? best_f_s[s] : best_f;
   double vmax = 0.0;
   double li[QMAX];
 #pragma unroll
@@ -218,6 +230,75 @@ __device__ __forceinline__ void sample_serial(int tid, int q, int S, int row0,
   }
   if (log_mode(MODE)) lse = lse_push(lse, log_q_reduce<QMAX>(li, q, lp, nullptr));
   else sum += vmax;
+}
+
+// psd_safe_cholesky's ladder on the q x q covariance, one wave.  Lane l owns
+// the entries (a0 + RS k, c) of a W-wide layout (c = l % W, a0 = l / W, RS =
+// 64 / W rows apart; W = 8: one entry, W = 16: four).  Column j: the pivot by
+// v_readlane, l_aj = a_aj / sqrt(a_jj) written to colb by the column's lanes,
+// then every trailing entry a_ac -= l_aj l_cj with both factors from colb (in
+// order within the wave: no barrier).  Per entry the FMA sequence (j
+// ascending, fma(-l_aj, l_cj, .)) is the row-per-lane form's: the same bits.
+// (The row-per-lane form broadcast each column entry by a v_readlane pair per
+// row: ~2700 instructions on one wave, 3.8 us of C2's 11.5 us kernel span.)
+template <int W>
+__device__ __forceinline__ void ladder_factor(int lane, int q, const double (&Sig)[QMAX][QMAX + 1],
+                                              double (&Lq)[QMAX][QMAX + 1], double* colb,
+                                              int max_tries, double jitter0, int& s_info,
+                                              double& s_jit) {
+  constexpr int RS = 64 / W, R = W / RS;  // rows apart, entries per lane
+  const int c = lane % W, a0 = lane / W;
+  double jit = 0.0;
+  int info = 0;
+  for (int attempt = 0; attempt <= max_tries; ++attempt) {
+    if (attempt > 0) jit = jitter0 * pow(10.0, (double)(attempt - 1));
+    double v[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int a = a0 + RS * k;
+      v[k] = (a < q && c <= a) ? Sig[a][c] + ((a == c) ? jit : 0.0) : 0.0;
+    }
+    info = 0;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      if (j < q) {
+        const double ajj = readlane_d(v[j / RS], (j % RS) * W + j);
+        if (!(ajj > 0.0) && info == 0) info = j + 1;
+        const double rinv = rsq_nr(ajj);
+        if (c == j) {
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            const int a = a0 + RS * k;
+            if (a >= j && a < q) {
+              const double l = (a == j) ? ajj * rinv : v[k] * rinv;
+              v[k] = l;
+              colb[a] = l;
+            }
+          }
+        }
+        if (c > j && c < q) {
+          const double lc = colb[c];
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            const int a = a0 + RS * k;
+            if (a >= c && a < q) v[k] = fma(-colb[a], lc, v[k]);
+          }
+        }
+      }
+    }
+    if (info == 0) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int a = a0 + RS * k;
+        Lq[a][c] = (c <= a && a < q) ? v[k] : 0.0;
+      }
+      break;
+    }
+  }
+  if (lane == 0) {
+    s_info = info;
+    s_jit = jit;
+  }
 }
 
 template <int KIND, int MODE>
@@ -243,9 +324,11 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   __shared__ int s_info;
   __shared__ double s_jit;
   __shared__ int s_last;
+  __shared__ double colb[QMAX];
   __shared__ double psum[THREADS];
   __shared__ double msum[THREADS];
 
+  QMC_PHASE(0);
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int row0 = b * Qp;               // first padded test row of this t-batch
@@ -253,6 +336,22 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   const int off = row0 & 15;             // offset inside the tile
   const int nrows16 = nrows_pad >> 4;
   const double s2 = ystd * ystd;
+
+  // The one-sample-per-thread form's z row and best first (S <= THREADS, C2):
+  // their loads are in flight with the partials' instead of after the q x q
+  // Cholesky
+  const bool serial = S <= THREADS && MODE != QMC_POSTERIOR && MODE != QMC_CHOL;
+  double zs[QMAX];
+  double bf_s = best_f;
+#pragma unroll
+  for (int j = 0; j < QMAX; ++j) zs[j] = 0.0;
+  if (serial && tid < S) {
+    const double* z = Z + (int64_t)tid * q;
+#pragma unroll
+    for (int j = 0; j < QMAX; ++j)
+      if (j < q) zs[j] = z[j];
+    if (per_sample_best(MODE)) bf_s = best_f_s[tid];
+  }
 
   // 1. finalise the q x q covariance and the mean.  The partial sums use all
   // threads: nsplit threads per entry (q = 8: 4) each take every nsplit-th
@@ -324,54 +423,18 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     if (mean_out) mean_out[(int64_t)b * q + tid] = v;
   }
   __syncthreads();
+  QMC_PHASE(1);
   if (MODE == QMC_POSTERIOR) return;
 
-  // 2. Cholesky with the jitter ladder (wave 0; lane a owns row a).
+  // 2. Cholesky with the jitter ladder (wave 0, one lane per entry: ladder_factor)
   if (tid < 64) {
-    const int a = tid;
-    double jit = 0.0;
-    int info = 0;
-    for (int attempt = 0; attempt <= max_tries; ++attempt) {
-      if (attempt > 0) jit = jitter0 * pow(10.0, (double)(attempt - 1));
-      double r[QMAX];
-#pragma unroll
-      for (int j = 0; j < QMAX; ++j)
-        r[j] = (a < q && j < q && j <= a) ? Sig[a][j] + ((j == a) ? jit : 0.0) : 0.0;
-      info = 0;
-#pragma unroll
-      for (int j = 0; j < QMAX; ++j) {
-        if (j < q) {
-          const double ajj = readlane_d(r[j], j);
-          if (!(ajj > 0.0) && info == 0) info = j + 1;
-          // one reciprocal square root (two Newton steps) instead of sqrt and
-          // a division on the column's dependent chain: l_jj = a_jj / sqrt(a_jj)
-          // rounds like sqrt to within an ulp
-          const double rinv = rsq_nr(ajj);
-          double lij = (a == j) ? ajj * rinv : r[j] * rinv;
-          if (a < j) lij = 0.0;
-          r[j] = lij;
-          // column j to every lane by v_readlane (uniform, into SGPRs): no LDS
-          // round trip on the chain (round 3: the LDS broadcast replaced 300
-          // ds_bpermute per t-batch at q = 16)
-#pragma unroll
-          for (int l = j + 1; l < QMAX; ++l) {
-            if (l < q) r[l] = fma(-lij, readlane_d(lij, l), r[l]);
-          }
-        }
-      }
-      if (info == 0) {
-        if (a < q)
-#pragma unroll
-          for (int j = 0; j < QMAX; ++j) Lq[a][j] = (j <= a && j < q) ? r[j] : 0.0;
-        break;
-      }
-    }
-    if (a == 0) {
-      s_info = info;
-      s_jit = jit;
-    }
+    if (q <= 8)
+      ladder_factor<8>(tid, q, Sig, Lq, colb, max_tries, jitter0, s_info, s_jit);
+    else
+      ladder_factor<16>(tid, q, Sig, Lq, colb, max_tries, jitter0, s_info, s_jit);
   }
   __syncthreads();
+  QMC_PHASE(2);
   const int info = s_info;
   if (tid == 0) {
     // agent-scope (write-through) stores: the fused status reads them from
@@ -390,6 +453,7 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   // agent-scope loads on the reading side -- an agent-scope release fence
   // would write back the whole L2 per workgroup.  Called by every thread.
   auto status_arrive = [&]() {
+    QMC_PHASE(3);
     if (status_out == nullptr) return;
     __syncthreads();  // red / red2 free (the reduction below is done with them)
     if (tid == 0) {
@@ -398,7 +462,10 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
                (int)gridDim.x - 1;
     }
     __syncthreads();
-    if (!s_last) return;
+    if (!s_last) {
+      QMC_PHASE(4);
+      return;
+    }
     double mi = 0.0, mj = 0.0;
     for (int bb = tid; bb < (int)gridDim.x; bb += THREADS) {
       mi = fmax(mi, (double)__hip_atomic_load(info_out + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -418,6 +485,7 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
       status_out[1] = fmax(fmax(red2[0], red2[1]), fmax(red2[2], red2[3]));
       __hip_atomic_store(status_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    QMC_PHASE(4);
   };
   if (L_out && tid < q * q) {
     const int a = tid / q, c = tid % q;
@@ -440,8 +508,8 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
   // serial against 14.0 grouped).
   double sum = 0.0;
   LseAcc lse{-INFINITY, 0.0};
-  if (S <= THREADS)
-    sample_serial<MODE>(tid, q, S, row0, Lq, mu, Z, F, ldF, best_f, best_f_s, lp, sum, lse);
+  if (serial)
+    sample_serial<MODE>(tid, q, S, row0, Lq, mu, zs, bf_s, F, ldF, lp, sum, lse);
   else if (q > 8)
     sample_phase<16, MODE>(tid, q, S, row0, Lq, mu, Z, F, ldF, best_f, best_f_s, lp, sum, lse);
   else
@@ -631,3 +699,11 @@ extern "C" int bo_ladder_status(const int* info, const double* jitter, int64_t B
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
+
+#ifdef BO_QMC_PHASES
+extern "C" int bo_qmc_phase_dump(unsigned long long* out, int n) {
+  if (n > PH_WG * PH_N) n = PH_WG * PH_N;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qmc_phase), sizeof(unsigned long long) * n, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
