@@ -99,6 +99,19 @@ __device__ __forceinline__ double strided_sum(const double* __restrict__ p, int6
   return s[0];
 }
 
+// strided_sum<U> at the narrowest width that holds n partials in one pass:
+// the same bits (with n <= U' every partial sits alone in its slot and the
+// wider tree only adds exact zeros in the same pairing order), without the
+// wide form's predicated tail -- a compare, a 64-bit address and a branch per
+// slot for 16 slots when C2's threads hold one or two partials.
+template <int U>
+__device__ __forceinline__ double strided_sum_fit(const double* __restrict__ p, int64_t stride, int n) {
+  if (n <= 2) return strided_sum<2>(p, stride, n);
+  if (n <= 4) return strided_sum<4>(p, stride, n);
+  if (U > 8 && n <= 8) return strided_sum<8>(p, stride, n);
+  return strided_sum<U>(p, stride, n);
+}
+
 // z_J of this lane's group of G lanes: lane J of the group (DPP row
 // broadcast; G = 8: the row's two groups take lanes J and 8 + J)
 template <int G, int J>
@@ -385,11 +398,11 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     const int64_t pstride = (int64_t)nrows16 * 256;
     const int cnt = nC > j ? (nC - 1 - j) / nsplit + 1 : 0;
     const double* sp = Spart + (int64_t)j * pstride + (int64_t)tile * 256 + (off + a) * 16 + (off + c);
-    double part = strided_sum<16>(sp, pstride * nsplit, cnt);
+    double part = strided_sum_fit<16>(sp, pstride * nsplit, cnt);
     if (sym) {  // quad plan partials (quad.hip): Sigma = sum_p P_p + P_p^T
       const double* spt =
           Spart + (int64_t)j * pstride + (int64_t)tile * 256 + (off + c) * 16 + (off + a);
-      part += strided_sum<16>(spt, pstride * nsplit, cnt);
+      part += strided_sum_fit<16>(spt, pstride * nsplit, cnt);
     }
     psum[tid] = part;
   }
@@ -398,7 +411,7 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     const int a = tid % q, j = tid / q;
     if (j < ms) {
       const int cnt = nC > j ? (nC - 1 - j) / ms + 1 : 0;
-      msum[tid] = strided_sum<16>(mpart + (int64_t)j * nrows_pad + row0 + a, (int64_t)nrows_pad * ms, cnt);
+      msum[tid] = strided_sum_fit<16>(mpart + (int64_t)j * nrows_pad + row0 + a, (int64_t)nrows_pad * ms, cnt);
     }
   }
   __syncthreads();
