@@ -67,7 +67,10 @@ def test_posterior_general_path_q_gt_16():
     torch.testing.assert_close(post.covariance_matrix.cpu(), cr, rtol=1e-4, atol=1e-9)
 
 
-@pytest.mark.parametrize("B,q,S", [(16, 4, 128), (40, 8, 256), (9, 16, 64), (5, 1, 32), (3, 3, 16)])
+# q = 7 / 9-15: the q x q ladder's 8- and 16-wide entry layouts with rows
+# past q masked (qmc.hip ladder_factor); S = 300 / 512 the grouped sampling
+@pytest.mark.parametrize("B,q,S", [(16, 4, 128), (40, 8, 256), (9, 16, 64), (5, 1, 32), (3, 3, 16),
+                                   (7, 7, 64), (6, 9, 128), (4, 12, 512), (3, 13, 300), (5, 15, 64)])
 def test_qei_api_value(B, q, S):
     from botorch_amd.acquisition import qExpectedImprovement
     from botorch_amd.sampling import SobolQMCNormalSampler
@@ -83,7 +86,7 @@ def test_qei_api_value(B, q, S):
     torch.testing.assert_close(v, ref, rtol=1e-6, atol=1e-10)
 
 
-@pytest.mark.parametrize("B,q", [(8, 4), (3, 16), (4, 1), (2, 5)])
+@pytest.mark.parametrize("B,q", [(8, 4), (3, 16), (4, 1), (2, 5), (3, 11)])
 def test_qei_gradient_matches_oracle(B, q):
     from botorch_amd.acquisition import qExpectedImprovement
     from botorch_amd.sampling import SobolQMCNormalSampler

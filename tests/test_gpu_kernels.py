@@ -184,6 +184,37 @@ def test_posterior_matches_oracle(n, B, q):
     torch.testing.assert_close(out["cov"].cpu(), cov_r, rtol=1e-4, atol=1e-9)
 
 
+@pytest.mark.parametrize("q", list(range(1, 17)))
+def test_qmc_root_every_q_and_ladder(q):
+    """The q x q root of qmc_kernel (QMC_CHOL) at every q: the 8- and 16-wide
+    entry layouts of ladder_factor, rows past q masked.  The root of the
+    finalised covariance against torch's Cholesky of the same matrix.  A
+    t-batch whose points repeat has a rank-1 covariance: whether its first
+    zero pivot rounds to + or - is arithmetic-dependent, so it is held to the
+    ladder's contract (psd_safe_cholesky, [G]): the jitter is 0 or one of
+    jitter0 * 10^i, and L L^T reproduces cov + jitter I."""
+    from botorch_amd import kernels, _lib
+    X, Y, orc, h = _oracle_model(256, noise=1e-4)
+    c = _device_cache(X, Y, h, orc)
+    g = torch.Generator().manual_seed(100 + q)
+    Xc = torch.rand(6, q, 6, generator=g, dtype=torch.float64)
+    if q > 1:
+        Xc[5, 1:] = Xc[5, 0]  # t-batch 5: one point repeated -> rank-1 covariance
+    pp = kernels.post_partials(c, Xc.to(DEV))
+    out = kernels.qmc_finalize(c, pp, _lib.QMC_CHOL, orc.ymean.item(), orc.ystd.item(), want_L=True)
+    cov, L = out["cov"].cpu(), out["L"].cpu()
+    info, jit = out["info"].cpu(), out["jitter"].cpu()
+    assert (info == 0).all()
+    torch.testing.assert_close(L[:5], torch.linalg.cholesky(cov[:5]), rtol=1e-9, atol=1e-12)
+    assert (jit[:5] == 0).all()
+    j5 = jit[5].item()
+    assert j5 == 0.0 or any(j5 == pytest.approx(kernels.CHOLESKY_JITTER_F64 * 10.0 ** i, rel=1e-12)
+                            for i in range(kernels.CHOLESKY_MAX_TRIES))
+    A5 = cov[5] + j5 * torch.eye(q, dtype=torch.float64)
+    torch.testing.assert_close(L[5] @ L[5].T, A5, rtol=1e-9, atol=1e-12)
+    assert torch.equal(L[5], L[5].tril())
+
+
 @pytest.mark.parametrize("n,B,q,split", [(1024, 64, 8, None), (1024, 64, 8, 64), (1000, 20, 3, 128),
                                          (513, 9, 5, 256), (300, 33, 16, 64), (4096, 64, 16, None),
                                          (1000, 20, 3, -1), (300, 33, 16, -1), (2048, 40, 16, -1)])
