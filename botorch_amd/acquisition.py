@@ -158,7 +158,7 @@ def _fused_mc(X3: torch.Tensor, acqf, mode: int, best_f: float, best_f_s, Z: tor
     bo::qmc_acq (one torch.ops call; its registered backward gives dX).  The
     jitter-ladder status is read at the end of the backward when a gradient
     follows, else one call later (kernels.raise_not_psd_deferred)."""
-    from . import ops  # noqa: F401  (torch.ops.bo registration)
+    from . import ops  # torch.ops.bo registration, QmcAcqGrad
     model = acqf.model
     cache = model.prediction_cache()
     ymean, ystd = model.outcome_stats()
@@ -180,13 +180,20 @@ def _fused_mc(X3: torch.Tensor, acqf, mode: int, best_f: float, best_f_s, Z: tor
             kernels.quad_ainv(cache, X3.shape[0], X3.shape[1]), cache.alpha)
         kernels.ladder_prev_outcome(prev, idx, type(acqf).__name__)
         return acq
-    outs = torch.ops.bo.qmc_acq(
-        X3, cache.Xt, cache.Xt_scaled, cache.U, cache.Linv, cache.beta, cache.alpha,
-        cache.lengthscale, Z, best_f_s, int(cache.kind), int(mode), float(cache.outputscale),
-        float(cache.constant), float(ymean), float(ystd), float(best_f), bool(fat),
-        float(tau_relu), float(tau_max), bool(need_grad),
-        None if need_grad else kernels.quad_ainv(cache, X3.shape[0], X3.shape[1]))
-    acq, jit, info = outs[0], outs[6], outs[7]
+    if need_grad:  # the registered op's semantics without its autograd wrapper
+        acq, jit, info = ops.QmcAcqGrad.apply(
+            X3, cache.Xt, cache.Xt_scaled, cache.U, cache.Linv, cache.beta, cache.alpha,
+            cache.lengthscale, Z, best_f_s, int(cache.kind), int(mode), float(cache.outputscale),
+            float(cache.constant), float(ymean), float(ystd), float(best_f), bool(fat),
+            float(tau_relu), float(tau_max))
+    else:
+        outs = torch.ops.bo.qmc_acq(
+            X3, cache.Xt, cache.Xt_scaled, cache.U, cache.Linv, cache.beta, cache.alpha,
+            cache.lengthscale, Z, best_f_s, int(cache.kind), int(mode), float(cache.outputscale),
+            float(cache.constant), float(ymean), float(ystd), float(best_f), bool(fat),
+            float(tau_relu), float(tau_max), False,
+            kernels.quad_ainv(cache, X3.shape[0], X3.shape[1]))
+        acq, jit, info = outs[0], outs[6], outs[7]
     # deferred either way: with a gradient the status is read at the end of the
     # registered backward (ops._acq_bwd), once the backward's launches are
     # queued behind the forward -- so the evaluation that produced a failed

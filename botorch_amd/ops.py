@@ -378,6 +378,49 @@ def _acq_bwd(ctx, dacq, *_):
 qmc_acq.register_autograd(_acq_bwd, setup_context=_acq_setup)
 
 
+class QmcAcqGrad(torch.autograd.Function):
+    """bo::qmc_acq with need_grad, as a plain autograd Function: the same two
+    native calls (qmc_acq_native, qmc_acq_backward_native) and the semantics
+    of _acq_setup / _acq_bwd (only acq differentiable, no materialised zero
+    grads, the ladder status read once the backward is queued), without the
+    torch.library autograd wrapper around the registered op -- its per-call
+    schema handling (fill_defaults over 22 arguments) and redispatch cost ~90
+    us of host time per C2 forward + backward (tools/host_c2_fwd_bwd.py), the
+    per-iteration path of gen_candidates_scipy.  The registered op stays the
+    interface for opcheck / fake tensors and the forward-only calls."""
+
+    @staticmethod
+    def forward(ctx, X, Xt, Xt_scaled, U, Linv, beta, alpha, lengthscale, Z, best_f_s, kind, mode,
+                outputscale, constant, ymean, ystd, best_f, fat, tau_relu, tau_max):
+        out = _lib.torch_ops().qmc_acq_native(
+            X.contiguous(), Xt_scaled, U, Linv, beta, lengthscale,
+            Z.reshape(-1, X.shape[1]).contiguous(), best_f_s, kind, mode, Xt.shape[0], outputscale,
+            constant, ymean, ystd, best_f, fat, tau_relu, tau_max, True, kernels.kxt_cap(X.device),
+            False, None, alpha)
+        acq, mean, L, Xq, Rt, _, jit, info, _ = out
+        ctx.mark_non_differentiable(jit, info)
+        ctx.set_materialize_grads(False)
+        # intermediates held on ctx (released with the graph)
+        ctx.st = (acq, mean, L, Z, Xq, Rt, Linv, U, Xt_scaled, alpha, lengthscale, best_f_s)
+        ctx.meta = (kind, mode, outputscale, ystd, best_f, fat, tau_relu, tau_max, Xt.shape[1],
+                    Xt.shape[0])
+        return acq, jit, info
+
+    @staticmethod
+    def backward(ctx, dacq, *_):
+        if dacq is None:
+            return (None,) * 20
+        acq, mean, L, Z, Xq, Rt, Linv, U, Xt_scaled, alpha, lengthscale, best_f_s = ctx.st
+        kind, mode, outputscale, ystd, best_f, fat, tau_relu, tau_max, d, n = ctx.meta
+        dX = _lib.torch_ops().qmc_acq_backward_native(
+            dacq.contiguous(), acq, mean, L, Z.reshape(-1, mean.shape[1]).contiguous(), best_f_s,
+            Xq, Rt, Linv, U, Xt_scaled, alpha, lengthscale, kind, mode, d, n, outputscale, ystd,
+            best_f, fat, tau_relu, tau_max)
+        if not torch.cuda.is_current_stream_capturing():
+            kernels.check_ladder_status(dX.device)
+        return (dX,) + (None,) * 19
+
+
 # ---- bo::qehvi ---------------------------------------------------------------------------
 @torch.library.custom_op("bo::qehvi", mutates_args=(), device_types="cuda")
 def qehvi(mean: Tensor, L: Tensor, Z: Tensor, cell_lo: Tensor, cell_hi: Tensor) -> Tensor:
