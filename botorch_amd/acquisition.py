@@ -915,8 +915,9 @@ class _FusedQEHVI(torch.autograd.Function):
         Z = sampler.base_samples_2d(q * len(models), X3.device)
         lo, hi = acqf._cells(X3.device)
         mean, L = torch.stack(means), torch.stack(Ls)
-        from . import ops  # noqa: F401  (torch.ops.bo registration)
-        acq = torch.ops.bo.qehvi(mean, L, Z, lo, hi)
+        # the kernel itself (as the backward below): this Function already is
+        # the autograd node, the registered op's wrapper would only add host time
+        acq = kernels.qehvi(mean, L, Z, lo, hi)
         if need_grad:
             ctx.saved, ctx.mean, ctx.L, ctx.Z, ctx.cells = saved, mean, L, Z, (lo, hi)
         return acq
