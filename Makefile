@@ -58,7 +58,18 @@ tools: $(TOOLS_LIB)
 $(TOOLS_LIB): $(TOOLS_OBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(TOOLS_OBJ) -pthread -o $@
 
-clean:
-	rm -rf build $(LIB) $(TORCH_LIB) $(TOOLS_LIB)
+# qmc_kernel phase clocks (tools/qmc_phases.sh swaps it in for one run): the
+# product objects with qmc.hip built -DBO_QMC_PHASES; never the product
+PH_LIB := ab_libs/libP.so
 
-.PHONY: all clean tools
+$(PH_LIB): $(OBJ) botorch_amd/csrc/qmc.hip $(HDR)
+	@mkdir -p build/ph ab_libs
+	$(HIPCC) $(HIPFLAGS) -DBO_QMC_PHASES -c botorch_amd/csrc/qmc.hip -o build/ph/qmc.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(filter-out build/qmc.o,$(OBJ)) build/ph/qmc.o -pthread -o $@
+
+qmc-phases: $(PH_LIB)
+
+clean:
+	rm -rf build $(LIB) $(TORCH_LIB) $(TOOLS_LIB) $(PH_LIB)
+
+.PHONY: all clean tools qmc-phases

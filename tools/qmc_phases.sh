@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU-box: qmc_kernel phase clocks with the -DBO_QMC_PHASES build (ab_libs/libP.so)
+# GPU-box: qmc_kernel phase clocks with the -DBO_QMC_PHASES build (`make qmc-phases` -> ab_libs/libP.so)
 # swapped in for the product library, which is restored afterwards.
 set -u
 cd "$GRAFT_REPO_ROOT"
