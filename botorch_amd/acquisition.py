@@ -1427,10 +1427,14 @@ class FixedFeatureAcquisitionFunction(AcquisitionFunction):
         once per device / dtype: a call under stream capture copies nothing)."""
         key = (X.device, X.dtype)
         hit = self._placed.get(key)
-        if hit is None or hit[2] is not self.values:  # rebuilt if values was replaced
-            vals = self.values.to(device=X.device, dtype=X.dtype)
+        v = self.values
+        # rebuilt if values was replaced or updated in place (version counter,
+        # storage): .to() may have made a copy that an in-place update misses
+        src = (v, v._version, v.data_ptr())
+        if hit is None or hit[2][0] is not v or hit[2][1:] != src[1:]:
+            vals = v.to(device=X.device, dtype=X.dtype)
             sel = torch.tensor(self._selector, dtype=torch.long, device=X.device)
-            hit = (vals, sel, self.values)
+            hit = (vals, sel, src)
             self._placed[key] = hit
         return hit[0], hit[1]
 

@@ -299,67 +299,76 @@ def sample_polytope(A: torch.Tensor, b: torch.Tensor, x0: torch.Tensor, n: int =
     return out.to(dtype=A.dtype, device=A.device)
 
 
+def _stack_rows(parts, d, like):
+    """Concatenate (rows, rhs) blocks of A x <= b; an empty polytope of
+    dimension d when there are none."""
+    parts = [p for p in parts if p is not None]
+    if not parts:
+        return like.new_zeros(0, d), like.new_zeros(0, 1)
+    return torch.cat([p[0] for p in parts], 0), torch.cat([p[1] for p in parts], 0)
+
+
+def _equality_chart(C: Optional[torch.Tensor], d: int, like: torch.Tensor) -> torch.Tensor:
+    """Orthonormal columns spanning {x : C x = 0}: the right singular vectors
+    past C's numerical rank (no equality: the identity).  Moves of the chain
+    are taken in these coordinates, so every sample keeps C x = rhs."""
+    if C is None:
+        return torch.eye(d, dtype=like.dtype, device=like.device)
+    _, sv, Vh = torch.linalg.svd(C)
+    return Vh[int((sv != 0).sum()):].mT
+
+
 class PolytopeSampler:
-    """sampling.py:457-578: the polytope {x : A x <= b, C x = d} (bounds added
-    as inequalities), the null space of C from its SVD, and an interior point
-    (given, or the LP's)."""
+    """sampling.py:457-578.  The region {x : A x <= b, C x = rhs} with the box
+    appended as inequalities, the chart of C's null space in which the chain
+    moves, and a starting point inside (the one given, if feasible, else the
+    Chebyshev-like LP point of ``find_interior_point``)."""
 
     def __init__(self, inequality_constraints=None, equality_constraints=None, bounds=None,
                  interior_point=None):
-        if inequality_constraints is None:
-            if bounds is None:
-                raise BotorchError("PolytopeSampler requires either inequality constraints or "
-                                   "bounds.")
-            A = torch.empty(0, bounds.shape[-1], dtype=bounds.dtype, device=bounds.device)
-            b = torch.empty(0, 1, dtype=bounds.dtype, device=bounds.device)
-        else:
-            A, b = inequality_constraints
-        if bounds is not None:
-            Ab, bb = _box_as_inequalities(bounds)
-            A, b = torch.cat([A, Ab], dim=0), torch.cat([b, bb], dim=0)
-        self.A, self.b = A, b
+        if inequality_constraints is None and bounds is None:
+            raise BotorchError("PolytopeSampler requires either inequality constraints or "
+                               "bounds.")
+        like = bounds if bounds is not None else inequality_constraints[0]
+        d = like.shape[-1]
+        self.A, self.b = _stack_rows(
+            [inequality_constraints, _box_as_inequalities(bounds) if bounds is not None else None],
+            d, like)
         self.equality_constraints = equality_constraints
-        if equality_constraints is not None:
-            self.C, self.d = equality_constraints
-            _, sv, Vh = torch.linalg.svd(self.C)
-            rank = torch.nonzero(sv).size(0)
-            self.nullC = Vh[rank:, :].transpose(-1, -2)
-        else:
-            self.C = self.d = None
-            self.nullC = torch.eye(A.size(-1), dtype=A.dtype, device=A.device)
-        self.new_A = self.A @ self.nullC
+        self.C, self.d = equality_constraints if equality_constraints is not None else (None, None)
+        self.nullC = _equality_chart(self.C, d, self.A)
+        self.new_A = self.A @ self.nullC  # the inequalities in chart coordinates
         if interior_point is None:
             self.x0 = self.find_interior_point()
-        elif self.feasible(interior_point):
-            self.x0 = interior_point
-        else:
+        elif not self.feasible(interior_point):
             raise ValueError("The given input point is not feasible.")
+        else:
+            self.x0 = interior_point
 
     def feasible(self, x: torch.Tensor) -> bool:
-        inside = (self.A @ x - self.b <= 0).all()
-        if self.equality_constraints is None:
-            return inside
-        return inside & (self.C @ x - self.d == 0).all()
+        ok = bool((self.A @ x <= self.b).all())
+        if self.C is not None:
+            ok = ok and bool((self.C @ x == self.d).all())
+        return ok
 
     def find_interior_point(self) -> torch.Tensor:
-        A_eq = b_eq = None
-        if self.equality_constraints:
-            A_eq = np.zeros((self.C.size(0), self.C.size(-1) + 1))
-            A_eq[:, :-1] = self.C.cpu().numpy()
-            b_eq = self.d.cpu().numpy()
-        x0 = find_interior_point(A=self.A.cpu().numpy(), b=self.b.cpu().numpy(), A_eq=A_eq,
-                                 b_eq=b_eq)
-        return torch.from_numpy(x0).to(self.A).unsqueeze(-1)
+        eq = None
+        if self.C is not None:  # the LP's slack column is not in the equalities
+            eq = (np.pad(self.C.cpu().numpy(), ((0, 0), (0, 1))), self.d.cpu().numpy())
+        x = find_interior_point(self.A.cpu().numpy(), self.b.cpu().numpy(),
+                                *(eq if eq is not None else (None, None)))
+        return torch.from_numpy(x).to(self.A).reshape(-1, 1)
 
     def draw(self, n: int = 1) -> torch.Tensor:  # pragma: no cover - abstract
         raise NotImplementedError
 
 
 class HitAndRunPolytopeSampler(PolytopeSampler):
-    """sampling.py:581-704.  With bounds, the constraints are first mapped to
-    the unit cube (sampling.py:624-652); samples come back in the original
-    coordinates.  Each draw continues the chain from the last sample; only the
-    first draw burns in; a seeded sampler advances its seed by n per draw."""
+    """sampling.py:581-704.  Given bounds, the problem is posed on the unit
+    cube (x = lower + width * z, sampling.py:624-652) and samples are mapped
+    back.  Draws continue one chain: the burn-in runs before the first draw
+    only, the chain restarts each draw from the previous draw's last sample,
+    and a seeded sampler's seed moves on by n per draw."""
 
     def __init__(self, inequality_constraints=None, equality_constraints=None, bounds=None,
                  interior_point=None, n_burnin: int = 200, n_thinning: int = 20,
@@ -367,48 +376,42 @@ class HitAndRunPolytopeSampler(PolytopeSampler):
         if inequality_constraints is None and bounds is None:
             raise BotorchError("HitAndRunPolytopeSampler requires either inequality constraints "
                                "or bounds.")
-        offset = scale = None
-        if inequality_constraints or equality_constraints:
-            if bounds is None:
-                warnings.warn("HitAndRunPolytopeSampler did not receive `bounds`, which can lead "
-                              "to non-uniform sampling if the parameter ranges are very different "
-                              "(see https://github.com/pytorch/botorch/issues/1225).",
-                              UserInputWarning, stacklevel=3)
-            else:
-                if inequality_constraints:
-                    inequality_constraints = normalize_dense_linear_constraints(
-                        bounds, inequality_constraints)
-                if equality_constraints:
-                    equality_constraints = normalize_dense_linear_constraints(
-                        bounds, equality_constraints)
-                offset, scale = bounds[0], bounds[1] - bounds[0]
-                if interior_point is not None:
-                    interior_point = (interior_point - offset[:, None]) / scale[:, None]
-                bounds = torch.zeros_like(bounds)
-                bounds[1, :] = 1.0
-        super().__init__(inequality_constraints=inequality_constraints,
-                         equality_constraints=equality_constraints, bounds=bounds,
-                         interior_point=interior_point)
-        self.n_burnin = n_burnin
-        self.n_thinning = n_thinning
+        self._to_box = None  # (lower, width) when the chain runs on the unit cube
+        if (inequality_constraints or equality_constraints) and bounds is None:
+            warnings.warn("HitAndRunPolytopeSampler did not receive `bounds`, which can lead "
+                          "to non-uniform sampling if the parameter ranges are very different "
+                          "(see https://github.com/pytorch/botorch/issues/1225).",
+                          UserInputWarning, stacklevel=3)
+        elif inequality_constraints or equality_constraints:
+            lower, width = bounds[0], bounds[1] - bounds[0]
+            unit = lambda c: normalize_dense_linear_constraints(bounds, c) if c else c  # noqa: E731
+            inequality_constraints, equality_constraints = (unit(inequality_constraints),
+                                                            unit(equality_constraints))
+            if interior_point is not None:
+                interior_point = (interior_point - lower.unsqueeze(-1)) / width.unsqueeze(-1)
+            bounds = torch.stack([torch.zeros_like(lower), torch.ones_like(lower)])
+            self._to_box = (lower, width)
+        super().__init__(inequality_constraints, equality_constraints, bounds, interior_point)
+        self.n_burnin, self.n_thinning = n_burnin, n_thinning
         self.num_samples_generated = 0
         self._seed = seed
-        self._offset, self._scale = offset, scale
 
     def draw(self, n: int = 1) -> torch.Tensor:
-        # the chain runs in the null-space coordinates of C, centred on x0
-        z = sample_polytope(A=self.new_A.cpu(), b=(self.b - self.A @ self.x0).cpu(),
-                            x0=torch.zeros((self.nullC.size(1), 1), dtype=self.A.dtype), n=n,
-                            n0=self.n_burnin if self.num_samples_generated == 0 else 0,
-                            n_thinning=self.n_thinning, seed=self._seed).to(self.b)
+        # chart coordinates y (x = x0 + nullC y), the chain starting at y = 0
+        first = self.num_samples_generated == 0
+        y = sample_polytope(A=self.new_A.cpu(), b=(self.b - self.A @ self.x0).cpu(),
+                            x0=self.new_A.new_zeros(self.nullC.shape[1], 1).cpu(), n=n,
+                            n0=self.n_burnin if first else 0, n_thinning=self.n_thinning,
+                            seed=self._seed).to(self.b)
         if self._seed is not None:
             self._seed += n
-        samples = self.x0.transpose(-1, -2) + z @ self.nullC.transpose(-1, -2)
-        self.x0 = samples[-1].reshape(-1, 1)
-        if self._scale is not None:
-            samples = self._offset + self._scale * samples
+        pts = self.x0.mT + y @ self.nullC.mT
+        self.x0 = pts[-1:].mT.clone()  # the next draw continues from here
         self.num_samples_generated += n
-        return samples
+        if self._to_box is None:
+            return pts
+        lower, width = self._to_box
+        return lower + width * pts
 
 
 def get_polytope_samples(n: int, bounds: torch.Tensor, inequality_constraints=None,

@@ -310,12 +310,23 @@ extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int m
     // an unstaged wide restart keeps the Cauchy breakpoints in LDS (staged = 2)
     const int mode = staged ? 1 : (n <= JOINT_TB_LDS ? 2 : 0);
     const size_t dyn = mode == 1 ? bytes : (mode == 2 ? sizeof(double) * (size_t)n : 0);
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&lbfgsb_kernel<JOINT_W>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(sizeof(double) * JOINT_TB_LDS));
-    });
+    // the attribute is per device: set it once for each device this process
+    // launches the joint kernel on, and report a refusal here, not as a
+    // launch failure later
+    if (dyn > 64 * 1024) {
+      int dev = 0;
+      BO_HIP(hipGetDevice(&dev));
+      static std::mutex mu;
+      static uint64_t set_mask = 0;
+      std::lock_guard<std::mutex> lock(mu);
+      const uint64_t bit = dev < 64 ? (uint64_t(1) << dev) : 0;
+      if (!bit || !(set_mask & bit)) {
+        BO_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&lbfgsb_kernel<JOINT_W>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(sizeof(double) * JOINT_TB_LDS)));
+        set_mask |= bit;
+      }
+    }
     lbfgsb_kernel<JOINT_W><<<B, 64 * JOINT_W, dyn, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws,
                                                                          wy, mat, ds, is, mode);
   }

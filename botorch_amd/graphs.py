@@ -69,6 +69,7 @@ class GraphedAcquisition:
                     self._host.copy_(self._sticky, non_blocking=True)
         taken = kernels.take_captured_status(self.dev)
         self._what = taken[1] if taken is not None else None
+        kernels.drop_keepalive()  # captured: no launch still needs the argument refs
         self._event = torch.cuda.Event()
         self._pending = False
 
@@ -78,10 +79,12 @@ class GraphedAcquisition:
 
     def _body(self):
         if self.with_grad:
-            Xg = self.X.requires_grad_(True)
+            # a fresh leaf per call over the captured buffer's storage: a leaf
+            # reused across the side-stream warm-up and the capture would keep
+            # its first AccumulateGrad node (bound to the warm-up stream)
+            Xg = self.X.detach().requires_grad_(True)
             v = self.acqf(Xg)
             (g,) = torch.autograd.grad(v.sum(), Xg)
-            self.X.requires_grad_(False)
             return v.detach(), g
         with torch.no_grad():
             return self.acqf(self.X)
@@ -91,9 +94,12 @@ class GraphedAcquisition:
         raise / warn, and re-arm the device maximum after a warning."""
         info_max, jitter_max = float(self._host[0]), float(self._host[1])
         if info_max > 0 or jitter_max > 0:
-            if info_max <= 0:  # a warning is given once per jittered stretch
-                self._sticky.zero_()
-                self._host.zero_()
+            # re-armed before acting: a warning is given once per jittered
+            # stretch, and a NotPSDError reports only the replays up to now
+            # (psd_safe_cholesky raises for the failing evaluation alone; a
+            # later replay that factors cleanly must not raise again)
+            self._sticky.zero_()
+            self._host.zero_()
             kernels._ladder_outcome(info_max, jitter_max, self._what)
 
     def check_status(self) -> None:

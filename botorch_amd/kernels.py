@@ -51,6 +51,15 @@ TIMING_HOOK = None
 _KEEPALIVE = collections.deque(maxlen=64)
 
 
+def drop_keepalive() -> None:
+    """Release the held references once every launch that used them is
+    enqueued (or captured): the caching allocator is stream-ordered, so a
+    block freed after its launch is queued is reused only behind it.  Called
+    where a caller is done issuing (the end of a graph capture, of the device
+    optimiser), so the deque does not pin graph-pool or large blocks."""
+    _KEEPALIVE.clear()
+
+
 def _p(t: Optional[torch.Tensor]):
     if t is None:
         return ctypes.c_void_p(0)

@@ -400,8 +400,13 @@ class QmcAcqGrad(torch.autograd.Function):
         acq, mean, L, Xq, Rt, _, jit, info, _ = out
         ctx.mark_non_differentiable(jit, info)
         ctx.set_materialize_grads(False)
-        # intermediates held on ctx (released with the graph)
-        ctx.st = (acq, mean, L, Z, Xq, Rt, Linv, U, Xt_scaled, alpha, lengthscale, best_f_s)
+        # every tensor through save_for_backward (the output acq included): a
+        # tensor held as a plain ctx attribute, above all an output, forms an
+        # output -> grad_fn -> ctx -> output cycle that keeps R^T (268 MB at C3)
+        # and the whole graph alive until the cyclic GC runs, and skips the
+        # saved-tensor version check on the cached U / L^-1 / alpha
+        ctx.save_for_backward(acq, mean, L, Z, Xq, Rt, Linv, U, Xt_scaled, alpha, lengthscale,
+                              best_f_s)
         ctx.meta = (kind, mode, outputscale, ystd, best_f, fat, tau_relu, tau_max, Xt.shape[1],
                     Xt.shape[0])
         return acq, jit, info
@@ -410,7 +415,8 @@ class QmcAcqGrad(torch.autograd.Function):
     def backward(ctx, dacq, *_):
         if dacq is None:
             return (None,) * 20
-        acq, mean, L, Z, Xq, Rt, Linv, U, Xt_scaled, alpha, lengthscale, best_f_s = ctx.st
+        acq, mean, L, Z, Xq, Rt, Linv, U, Xt_scaled, alpha, lengthscale, best_f_s = \
+            ctx.saved_tensors
         kind, mode, outputscale, ystd, best_f, fat, tau_relu, tau_max, d, n = ctx.meta
         dX = _lib.torch_ops().qmc_acq_backward_native(
             dacq.contiguous(), acq, mean, L, Z.reshape(-1, mean.shape[1]).contiguous(), best_f_s,

@@ -923,6 +923,7 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     # evaluations replayed from a captured graph, and why a capture was refused
     gen_candidates_device.last_graphed_evals = graphed_evals
     gen_candidates_device.last_graph_error = graph_errors[-1] if graph_errors else None
+    kernels.drop_keepalive()
     return cands, acq
 
 

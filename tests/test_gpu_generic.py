@@ -289,6 +289,6 @@ def test_saas_observation_noise_scaled_by_outcome_transform():
     p0 = m.posterior(Xc)
     p1 = m.posterior(Xc, observation_noise=True)
     s2 = float(Y.std()) ** 2
-    noise = torch.tensor([float(mm.likelihood.noise) for mm in m._members], dtype=torch.float64)
+    noise = torch.tensor([float(mm.likelihood.noise.detach()) for mm in m._members], dtype=torch.float64)
     diff = (p1.variance - p0.variance).squeeze(-1).cpu()                 # 3 x M x 2
     torch.testing.assert_close(diff, (noise * s2).view(1, M, 1).expand_as(diff), rtol=1e-9, atol=1e-12)
