@@ -24,6 +24,12 @@ collective, one all-reduce(MAX) of the best value per step.  N = 1 is labelled
 curve: the same step at b = 512/W restarts for W = 2, 4, 8 (a projection from
 single-GPU timings, collectives excluded).
 
+``--acq qnei`` times C3's qNEI instead (X_baseline = X_tr, pruned on every
+rank from the same seed: replicated, not sharded) and ``--acq qehvi`` C4's
+qEHVI (ModelListGP(3) on DTLZ2, n = 2048, q = 8, S = 128, 128 restarts; the
+box decomposition replicated); both shard their restarts exactly as qEI does.
+At N > 1 the default qEI line also carries both as ``sharded_other_acqs``.
+
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
@@ -805,6 +811,208 @@ def verify_grad(acqf, Xd, r0, Xtr, Ytr, Xc_local, best_f, k=8):
             "max_rel_err": err, "rtol": 1e-5, "atol": 1e-8}
 
 
+
+class HookTimer:
+    """HIP events around every post_partials launch issued through
+    kernels.post_partials (the qNEI / qEHVI routes), recorded on the stream
+    the launch is enqueued on (kernels.TIMING_HOOK)."""
+
+    def __init__(self, dev):
+        self.dev, self.pairs, self.on = dev, [], False
+
+    def __call__(self, tag):
+        if not self.on:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(self.dev))
+        if tag.endswith("_begin"):
+            self.pairs.append([ev, None])
+        else:
+            self.pairs[-1][1] = ev
+
+    def read(self):
+        torch.cuda.synchronize(self.dev)
+        out = [a.elapsed_time(b) for a, b in self.pairs]
+        self.pairs = []
+        return out
+
+
+def c4_problem():
+    """C4: DTLZ2(d=6, m=3) on torch.rand(2048, 6, seed 0),
+    ref point -1.1, lengthscale 0.6, noise 1e-3 per member."""
+    from botorch_amd.test_functions import DTLZ2
+    g = torch.Generator().manual_seed(0)
+    X = torch.rand(2048, D, generator=g, dtype=torch.float64)
+    Y = -DTLZ2(dim=D, num_objectives=3, negate=True).evaluate_true(X)
+    return X, Y, torch.full((3,), -1.1, dtype=torch.float64), 0.6, 1e-3
+
+
+def make_workload(acq, dev):
+    """The bench workload for ``--acq``: the acquisition on one GPU's
+    replicated model, the GLOBAL candidate draw (sliced by the caller), and
+    the algorithmic work of its dominant kernel.  qei / qnei: C3 (n = 4096,
+    q = 16, S = 512, 512 restarts; qNEI prunes X_baseline = X_tr on every rank
+    from the same seed, replicated); qehvi: C4 (ModelListGP(3) on DTLZ2,
+    n = 2048, q = 8, S = 128, 128 restarts; the box decomposition built on
+    every rank)."""
+    from types import SimpleNamespace
+    from botorch_amd.acquisition import (qExpectedHypervolumeImprovement, qExpectedImprovement,
+                                         qNoisyExpectedImprovement)
+    from botorch_amd.models import ModelListGP, SingleTaskGP
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from botorch_amd.utils_sampling import draw_sobol_samples
+    unit = torch.stack([torch.zeros(D, dtype=torch.float64), torch.ones(D, dtype=torch.float64)])
+
+    def stgp(X, Y, ls, noise):
+        m = SingleTaskGP(X.to(dev), Y.to(dev))
+        m.covar_module.lengthscale = torch.full((1, D), ls, dtype=torch.float64)
+        m.likelihood.noise = torch.tensor([noise], dtype=torch.float64)
+        m.mean_module.constant = torch.tensor(CONSTANT, dtype=torch.float64)
+        return m.eval()
+
+    if acq in ("qei", "qnei"):
+        Xtr, Ytr, Xc = build_problem(dev, RESTARTS)
+        model = stgp(Xtr, Ytr, LENGTHSCALE, NOISE)
+        model.prediction_cache()  # the reference builds its caches on the first eval call
+        sampler = SobolQMCNormalSampler(torch.Size([MC]), seed=0)
+        w = SimpleNamespace(acq=acq, q=Q, S=MC, restarts=RESTARTS, n=N_TRAIN, Xtr=Xtr, Ytr=Ytr,
+                            Xc=Xc, launches=1)
+        if acq == "qei":
+            # best_f 1.5 below the data maximum (DESIGN.md section 5): with best_f =
+            # max Y no Sobol candidate improves on 4096 observations and every value
+            # would be exactly 0; the work per step does not depend on it
+            w.best_f = Ytr.max().item() - 1.5
+            w.acqf = qExpectedImprovement(model, w.best_f, sampler=sampler)
+            w.name = "qEI"
+            w.extra_flops = 0
+            w.workload = "C3 qEI forward: SingleTaskGP n=4096 d=6, q=16"
+            w.tail = "512 Sobol MC samples, best_f = max(Y) - 1.5"
+        else:
+            torch.manual_seed(0)  # the pruning's sampler seed: identical on every rank
+            t0 = time.perf_counter()
+            w.acqf = qNoisyExpectedImprovement(model, Xtr.to(dev), sampler=sampler,
+                                               prune_baseline=True)
+            torch.cuda.synchronize(dev)
+            w.init_ms = 1e3 * (time.perf_counter() - t0)
+            w.r = int(w.acqf.X_baseline.shape[0])
+            w.name = "qNEI"
+            # the cached-root cross term rides the posterior pass: + 2 B q r n
+            w.extra_flops = 2 * Q * w.r * N_TRAIN
+            w.workload = (f"C3 qNEI forward: SingleTaskGP n=4096 d=6, q=16, X_baseline = X_tr "
+                          f"pruned on every rank (r = {w.r}, cache_root)")
+            w.tail = "512 Sobol MC samples"
+        w.flops_launch = lambda b: flops_post_partials(b, Q, N_TRAIN) + b * w.extra_flops
+        w.bytes_launch = lambda b: post_partials_bytes(b, Q, N_TRAIN)
+        w.kernel_prefix = "post_partials_kernel<0, 6, false, false, true, false>"
+        return w
+    X, Y, ref, ls, noise = c4_problem()
+    from botorch_amd.multi_objective import FastNondominatedPartitioning
+    models = [stgp(X, Y[:, t:t + 1], ls, noise) for t in range(3)]
+    part = FastNondominatedPartitioning(ref, Y)
+    q, S, b, n = 8, 128, 128, 2048
+    w = SimpleNamespace(acq=acq, q=q, S=S, restarts=b, n=n, Xtr=X, Ytr=Y, ref=ref, ls=ls,
+                        noise=noise, launches=3, name="qEHVI", extra_flops=0)
+    w.acqf = qExpectedHypervolumeImprovement(ModelListGP(*models), ref.tolist(), part,
+                                             sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
+    w.cells = part.get_hypercell_bounds()
+    w.Xc = draw_sobol_samples(unit, b, q, seed=1)
+    w.flops_launch = lambda bb: flops_post_partials(bb, q, n)
+    w.bytes_launch = lambda bb: post_partials_bytes(bb, q, n)
+    w.kernel_prefix = "post_partials_kernel<0, 6, false, false, true, false>"
+    w.workload = (f"C4 qEHVI forward: ModelListGP(3) on DTLZ2 n=2048 d=6, q=8, "
+                  f"{int(w.cells[0].shape[0])} hypercells")
+    w.tail = "128 Sobol MC samples, ref point -1.1"
+    return w
+
+
+def verify_other(w, acqf, Xd, r0, Xc_local, k=4):
+    """verify_step for qNEI / qEHVI: the timed forward's values at k spread
+    t-batches against the CPU restatement (oracle/, the checker) at 1e-7."""
+    from oracle import acquisition as oacq
+    from oracle.gp import ExactGPOracle, GPHyper
+    from oracle.sampling import base_samples_multi_output
+    b = Xd.shape[0]
+    idx = torch.linspace(0, b - 1, k).round().long()
+    with torch.no_grad():
+        got = acqf(Xd).cpu()[idx]
+    if w.acq == "qnei":
+        orc = ExactGPOracle(w.Xtr, w.Ytr, GPHyper(torch.full((D,), LENGTHSCALE, dtype=torch.float64),
+                                                  NOISE, CONSTANT))
+        ref = oacq.QNEIOracle(orc, acqf.X_baseline.cpu(), w.S, seed=0)(Xc_local[idx])
+    else:
+        orcs = [ExactGPOracle(w.Xtr, w.Ytr[:, t:t + 1],
+                              GPHyper(torch.full((D,), w.ls, dtype=torch.float64), w.noise, 0.0))
+                for t in range(3)]
+        lo, hi = w.cells
+        ref = oacq.qehvi(orcs, Xc_local[idx], base_samples_multi_output(w.S, w.q, 3, 0), lo, hi)
+    ok = bool(torch.allclose(got, ref, rtol=1e-7, atol=1e-12))
+    if not ok or not bool((ref > 0).any()):
+        raise SystemExit(f"bench: the timed {w.name} forward disagrees with the oracle (or is "
+                         f"degenerate): {got} vs {ref}")
+    pos = ref > 0
+    return {"t_batches": [int(r0 + i) for i in idx], "nonzero": int(pos.sum()),
+            "max_rel_err_nonzero": ((got - ref).abs()[pos] / ref[pos]).max().item(),
+            "rtol": 1e-7, "atol": 1e-12}
+
+
+def cpu_baseline_other(w, acqf, budget_s=20.0):
+    """cpu_baseline for qNEI / qEHVI: the oracle's forward on a bounded slice
+    of the same workload (8 / 2 restarts), median per call."""
+    from oracle import acquisition as oacq
+    from oracle.gp import ExactGPOracle, GPHyper
+    from oracle.sampling import base_samples_multi_output
+    torch.set_num_threads(cpu_cores())
+    if w.acq == "qnei":
+        orc = ExactGPOracle(w.Xtr, w.Ytr, GPHyper(torch.full((D,), LENGTHSCALE, dtype=torch.float64),
+                                                  NOISE, CONSTANT))
+        ref = oacq.QNEIOracle(orc, acqf.X_baseline.cpu(), w.S, seed=0)
+        bs = 8
+        fn = lambda: ref(w.Xc[:bs])  # noqa: E731
+        what = "full (r+q) posterior per t-batch, as the reference"
+    else:
+        orcs = [ExactGPOracle(w.Xtr, w.Ytr[:, t:t + 1],
+                              GPHyper(torch.full((D,), w.ls, dtype=torch.float64), w.noise, 0.0))
+                for t in range(3)]
+        Zm = base_samples_multi_output(w.S, w.q, 3, 0)
+        lo, hi = w.cells
+        bs = 2
+        fn = lambda: oacq.qehvi(orcs, w.Xc[:bs], Zm, lo, hi)  # noqa: E731
+        what = "dense inclusion-exclusion over all 255 q-subsets x cells, as the reference"
+    med, runs = _cpu_time(fn, budget_s=budget_s, max_runs=7)
+    return {"value": bs * w.q * w.S / med, "unit": "acq-evals/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{w.name} forward, {bs} of the {w.restarts} restarts ({what}), median of "
+                      f"{runs} runs; torch fp64 CPU restatement (oracle/), {cpu_model()}"}
+
+
+def sharded_other_acqs(dev, dist, ws, rank, steps, warmup):
+    """N > 1: C3 qNEI (pruning replicated) and C4 qEHVI (partitioning
+    replicated) with their restarts sharded over the ranks and the values
+    gathered by one all-reduce, timed like the headline (barriers, max over
+    ranks); SURVEY.md 8(e) for the configs BASELINE.json names on 8 / 4 GPUs."""
+    from botorch_amd.distributed import allgather_rows, shard_range
+    out = {}
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+    for acq in ("qnei", "qehvi"):
+        w = make_workload(acq, dev)
+        r0, r1 = shard_range(w.restarts, ws, rank)
+        Xd = w.Xc[r0:r1].to(dev)
+        best = torch.empty(1, dtype=torch.float64, device=dev)
+
+        def step():
+            with torch.no_grad():
+                acq_v = w.acqf(Xd)
+            torch.amax(allgather_rows(acq_v, w.restarts), dim=0, keepdim=True, out=best)
+
+        el = timed_steps(step, steps, warmup, dist, sync, dev)
+        out[w.name] = {"workload": w.workload, "value": w.q * w.restarts * w.S * steps / el,
+                       "unit": "acq-evals/s", "ms_per_step": 1e3 * el / steps,
+                       "restarts_per_gpu": r1 - r0, "scaling": "strong",
+                       **({"r": w.r} if acq == "qnei" else {})}
+        del w
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -817,6 +1025,9 @@ def main():
     ap.add_argument("--weak", action="store_true",
                     help="N > 1: each rank its own 512 restarts (weak scaling) as the headline")
     ap.add_argument("--strong", action="store_true", help=argparse.SUPPRESS)  # the N > 1 default
+    ap.add_argument("--acq", choices=("qei", "qnei", "qehvi"), default="qei",
+                    help="the timed acquisition: C3 qEI (default, the BASELINE metric), C3 qNEI "
+                         "(pruning replicated per rank) or C4 qEHVI (partitioning replicated)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the other section-8 configurations (C2, C3 qNEI, C4, C5)")
     args = ap.parse_args()
@@ -849,43 +1060,33 @@ def main():
     # restarts sharded over the ranks (strong scaling); --weak: 512 per rank
     strong = ws > 1 and not args.weak
 
-    from botorch_amd.acquisition import qExpectedImprovement
-    from botorch_amd.models import SingleTaskGP
-    from botorch_amd.sampling import SobolQMCNormalSampler
-
+    from botorch_amd import _lib, kernels
     from botorch_amd.distributed import allgather_rows, shard_range
-    r0, r1 = 0, RESTARTS
-    Xtr, Ytr, Xc_all = build_problem(dev, RESTARTS, seed_offset=0)
-    Xc = Xc_all
+    w = make_workload(args.acq, dev)
+    acqf, R = w.acqf, w.restarts
+    r0, r1 = 0, R
+    Xc = w.Xc
     if strong:  # one global draw, each rank its contiguous slice
-        r0, r1 = shard_range(RESTARTS, ws, rank)
-        Xc = Xc_all[r0:r1]
-    elif ws > 1:
+        r0, r1 = shard_range(R, ws, rank)
+        Xc = w.Xc[r0:r1]
+    elif ws > 1 and w.acq == "qei":
         Xc = build_problem(dev, RESTARTS, seed_offset=rank)[2]
-    # best_f 1.5 below the data maximum: with best_f =
-    # max Y no Sobol candidate improves on 4096 observations and every value
-    # would be exactly 0; the work per step does not depend on it
-    best_f = Ytr.max().item() - 1.5
-    model = SingleTaskGP(Xtr.to(dev), Ytr.to(dev))
-    model.covar_module.lengthscale = torch.full((1, D), LENGTHSCALE, dtype=torch.float64)
-    model.likelihood.noise = torch.tensor([NOISE], dtype=torch.float64)
-    model.mean_module.constant = torch.tensor(CONSTANT, dtype=torch.float64)
-    model.eval()
-    model.prediction_cache()  # the reference builds its caches on the first eval call
-    acqf = qExpectedImprovement(model, best_f, sampler=SobolQMCNormalSampler(torch.Size([MC]), seed=0))
     Xd = Xc.to(dev)
+    Xtr, Ytr = w.Xtr, w.Ytr
 
-    # HIP events around every post_partials launch of the timed steps, recorded
-    # by the native operator on the stream it launches on (bo::post_timing)
-    from botorch_amd import _lib
+    # HIP events around every post_partials launch of the timed steps, on the
+    # stream it is launched on: recorded by the native operator (qEI,
+    # bo::post_timing) or by kernels.post_partials's hook (qNEI / qEHVI)
     native = _lib.torch_ops()
+    hook = HookTimer(dev)
+    kernels.TIMING_HOOK = hook
     best = torch.empty(1, dtype=torch.float64, device=dev)
 
     def step():
         with torch.no_grad():
             acq = acqf(Xd)
         if strong:
-            allv = allgather_rows(acq, RESTARTS)   # every rank: all 512 values
+            allv = allgather_rows(acq, R)   # every rank: all the step's values
             torch.amax(allv, dim=0, keepdim=True, out=best)
             return allv
         torch.amax(acq, dim=0, keepdim=True, out=best)
@@ -899,26 +1100,31 @@ def main():
         step()
     sync()
     native.post_timing_read()  # drop anything recorded before
+    hook.read()
     native.post_timing(True)
+    hook.on = True
     elapsed = timed_steps(step, args.steps, 0, dist, sync, dev)
     native.post_timing(False)
-    kern_ms = native.post_timing_read().tolist()
-    if len(kern_ms) != args.steps:
-        raise SystemExit(f"bench: {len(kern_ms)} timed post_partials launches for {args.steps} steps")
+    hook.on = False
+    kern_ms = native.post_timing_read().tolist() + hook.read()
+    if len(kern_ms) != args.steps * w.launches:
+        raise SystemExit(f"bench: {len(kern_ms)} timed post_partials launches for {args.steps} "
+                         f"steps of {w.launches}")
     ms_step = 1e3 * elapsed / args.steps
-    evals_per_step = Q * RESTARTS * MC * (1 if strong else ws)
+    evals_per_step = w.q * R * w.S * (1 if strong else ws)
     value = evals_per_step * args.steps / elapsed
 
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
-    fl = flops_post_partials(r1 - r0, Q, N_TRAIN)
+    fl = w.flops_launch(r1 - r0)
     achieved = fl / (kern_avg_ms * 1e-3) / 1e12
     peak = 78.6  # MI355X dense FP64 matrix TFLOP/s (MI355X_MICROARCH.md / SURVEY.md 8(d))
     peak_box = mfma_f64_ceiling(dev)
-    traffic, traffic_src, traffic_note = pmc_traffic(r1 - r0)
-    alg_bytes = post_partials_bytes(r1 - r0, Q, N_TRAIN)
+    # the committed PMC passes are of the qEI bench command
+    traffic, traffic_src, traffic_note = pmc_traffic(r1 - r0) if w.acq == "qei" else (None,) * 3
+    alg_bytes = w.bytes_launch(r1 - r0)
 
     weak = None
-    if strong:
+    if strong and w.acq == "qei":
         # the weak line beside it: each rank its own 512 restarts (seed 1 + rank)
         Xw = build_problem(dev, RESTARTS, seed_offset=rank)[2].to(dev)
 
@@ -932,6 +1138,9 @@ def main():
         weak = {"value": Q * RESTARTS * MC * ws * args.steps / ew,
                 "ms_per_step": 1e3 * ew / args.steps, "restarts_per_gpu": RESTARTS,
                 "note": "each rank its own 512 restarts, one all-reduce(MAX) per step"}
+    sharded_other = None
+    if ws > 1 and w.acq == "qei" and not args.no_extra:
+        sharded_other = sharded_other_acqs(dev, dist, ws, rank, args.steps, args.warmup)
 
     # forward + backward (the optimize_acqf call pattern, gen.py:194-222)
     Xg = Xd.clone().requires_grad_(True)
@@ -944,10 +1153,10 @@ def main():
         fwd_bwd = None
     else:
         fb_s = _gpu_time(fwd_bwd, steps=5, warmup=2)
-        fwd_bwd = {"evals_per_s": Q * (r1 - r0) * MC / fb_s, "ms": 1e3 * fb_s}
+        fwd_bwd = {"evals_per_s": w.q * (r1 - r0) * w.S / fb_s, "ms": 1e3 * fb_s}
 
     strong_proj = None
-    if ws == 1 and not args.no_extra:
+    if ws == 1 and not args.no_extra and w.acq == "qei":
         # the per-rank shard of the strong split, timed on this GPU (projection)
         strong_proj = {"note": "projection: the C3 qEI step at b = 512/W restarts on one GPU, "
                                "collectives excluded; value = 512*q*S / step time"}
@@ -966,22 +1175,28 @@ def main():
     gp_fit = None
     extra = None
     check = None
-    chol = time_cholesky(Xtr, dev) if rank == 0 else None
-    if rank == 0 and ws == 1 and not args.no_extra:
+    chol = time_cholesky(build_problem(dev, 1)[0], dev) if rank == 0 else None
+    if rank == 0 and ws == 1 and not args.no_extra and w.acq == "qei":
         extra = other_configs(dev, cpu=not args.no_cpu_baseline)
     if rank == 0 and not args.no_fit:
-        gp_fit = time_gp_fit(Xtr, Ytr, dev, cpu=(not args.no_cpu_baseline and ws == 1))
+        Xf, Yf, _ = build_problem(dev, 1)
+        gp_fit = time_gp_fit(Xf, Yf, dev, cpu=(not args.no_cpu_baseline and ws == 1))
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline:
             # the CPU leg: the oracle checks the timed forward, then (N = 1) is timed
-            check = verify_step(acqf, Xd, r0, Xtr, Ytr, Xc, best_f)
-            if fwd_bwd is not None:
-                fwd_bwd["check"] = verify_grad(acqf, Xd, r0, Xtr, Ytr, Xc, best_f)
-            if ws == 1:
-                cpu = cpu_baseline(Xtr, Ytr, Xc, best_f)
+            if w.acq == "qei":
+                check = verify_step(acqf, Xd, r0, Xtr, Ytr, Xc, w.best_f)
+                if fwd_bwd is not None:
+                    fwd_bwd["check"] = verify_grad(acqf, Xd, r0, Xtr, Ytr, Xc, w.best_f)
+                if ws == 1:
+                    cpu = cpu_baseline(Xtr, Ytr, Xc, w.best_f)
+            else:
+                check = verify_other(w, acqf, Xd, r0, Xc)
+                if ws == 1:
+                    cpu = cpu_baseline_other(w, acqf)
         line = {
-            "metric": "acq-evals/sec (q x restarts x MC), qEI forward",
+            "metric": f"acq-evals/sec (q x restarts x MC), {w.name} forward",
             "value": value,
             "unit": "acq-evals/s",
             "n_gpus": ws,
@@ -992,14 +1207,15 @@ def main():
             "scaling": "single" if ws == 1 else ("strong" if strong else "weak"),
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: Hartmann6 on Sobol(seed 0) training inputs, "
+            "data": ("synthetic: Hartmann6 on Sobol(seed 0) training inputs, " if w.acq != "qehvi"
+                     else "synthetic: DTLZ2 on torch.rand(seed 0) training inputs, ")
                     + ("Sobol(seed 1) candidates, rank slice" if strong
-                       else "Sobol(seed 1+rank) candidates"),
-            "config": {"workload": ("C3 qEI forward: SingleTaskGP n=4096 d=6, q=16, "
-                                    + ("512 restarts sharded over the GPUs" if strong
-                                       else "512 restarts/GPU") + ", 512 Sobol MC samples, "
-                                    "best_f = max(Y) - 1.5"),
-                       "n": N_TRAIN, "d": D, "q": Q, "restarts_per_gpu": r1 - r0, "mc": MC,
+                       else ("Sobol(seed 1+rank) candidates" if w.acq == "qei"
+                             else "Sobol(seed 1) candidates")),
+            "config": {"workload": w.workload + ", "
+                                   + (f"{R} restarts sharded over the GPUs" if strong
+                                      else f"{R} restarts/GPU") + ", " + w.tail,
+                       "n": w.n, "d": D, "q": w.q, "restarts_per_gpu": r1 - r0, "mc": w.S,
                        "parallelism": f"restart-sharded x{ws}"},
             "roofline": {"bound": "mfma", "kernel": "post_partials_kernel",
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
@@ -1010,23 +1226,26 @@ def main():
                          "algorithmic_bytes": alg_bytes,
                          "traffic_ratio": traffic / alg_bytes if traffic else None,
                          "traffic_note": traffic_note,
-                         "kernel_ms": kern_avg_ms, "flops_per_launch": fl},
+                         "kernel_ms": kern_avg_ms, "flops_per_launch": fl,
+                         "launches_per_step": w.launches},
             "cpu_baseline": cpu,
             "check": check,
             "weak": weak,
+            "sharded_other_acqs": sharded_other,
             "fwd_bwd": fwd_bwd,
             "strong_scaling_projection": strong_proj,
             "cholesky": chol,
             "gp_fit": gp_fit,
             "other_configs": extra,
         }
+        if w.acq == "qnei":
+            line["config"].update(r=w.r, init_ms=w.init_ms)
         if cpu:
             line["speedup_vs_cpu"] = value / cpu["value"]
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()  # rank 0's CPU baseline / report must finish before teardown
         dist.destroy_process_group()
-
 
 if __name__ == "__main__":
     main()

@@ -80,6 +80,8 @@ _SIGNATURES = {
     "bo_post_kxt_rows": (c_int, [c_int, _P, c_int, c_int, c_int, _P, _P, c_int64, c_double, _P,
                                  _P, _P]),
     "bo_post_quad_plan": (c_int, [c_int64, c_int, c_int64, POINTER(c_int)]),
+    "bo_post_small_plan": (c_int, [c_int64, c_int, c_int64, POINTER(c_int)]),
+    "bo_post_small": (c_int, [_P, c_int64, c_int, c_int64, _P, c_int64, _P, _P, _P, _P]),
     "bo_post_quad": (c_int, [_P, _P, c_int64, _P, c_int64, c_int, c_int64, _P, _P, _P]),
     "bo_post_split_table": (c_int, [c_int64, c_int, c_int64, c_int, _P, c_int, _P, c_int,
                                     POINTER(c_int), POINTER(c_int)]),

@@ -765,6 +765,165 @@ __global__ void prepare_rows_kernel(const double* __restrict__ X, int B, int q, 
   Xq[idx] = v;
 }
 
+// ---- small grids: 32 x 32 units over column-tile pairs (round 5) -------------------
+// Forward-only posteriors too small for the 128 x 128 tiles (C2: 32 tiles for
+// 256 CUs) ran stream-K: k-ranges cut into shares, each cut share writing a
+// 128 KB partial R^T tile that post_splitk_reduce_kernel read back (37 MB per
+// C2 call, 21% of its kernel time).  Here the unit is 32 test rows x a PAIR of
+// 32-column tiles (ct, nct - 1 - ct): the pair's triangular k-ranges add up to
+// the same 32 (nct + 1) for every pair, so the units are equal and each covers
+// whole k-ranges -- R R^T and R beta are complete per unit and the partials
+// are 16 x 16 blocks per pair (nct / 2 of them per 16-row tile), summed by
+// qmc_kernel as it sums the column-tile partials.  No split-k workspace and no
+// reduction launch.  The 4 waves of a unit take the pair's 16-deep k-steps in
+// turn (wave w: steps w, w + 4, ...), each wave its own 32 x 32 accumulators
+// fed straight from L2 (U rows and K*x^T rows: 16 lanes = one 128-B segment per
+// load), two k-steps of operands in flight; the four partial accumulators are
+// summed in LDS in wave order (deterministic), then wave (t, h) runs the
+// epilogue of tile t, row half h.
+constexpr int SMU = 32;  // test rows and training columns per unit tile
+
+__device__ __forceinline__ void small_load(const double* __restrict__ U, int64_t ldu,
+                                           const double* __restrict__ Kt, int64_t ldk, int kb,
+                                           int c0, int r0, int lane, double (&a)[4][2],
+                                           double (&b)[4][2]) {
+  const int kr = lane >> 4, cl = lane & 15;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int64_t k = kb + 4 * ks + kr;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      a[ks][h] = U[k * ldu + c0 + 16 * h + cl];
+      b[ks][h] = Kt[k * ldk + r0 + 16 * h + cl];
+    }
+  }
+}
+
+// Steps s = first, first + 4, ... < nsteps of one 32-column tile at c0 into acc.
+__device__ __forceinline__ void small_tile(const double* __restrict__ U, int64_t ldu,
+                                           const double* __restrict__ Kt, int64_t ldk, int c0,
+                                           int r0, int nsteps, int first, int lane,
+                                           v4d (&acc)[2][2]) {
+  double a0[4][2], b0[4][2], a1[4][2], b1[4][2];
+  int s = first;
+  if (s < nsteps) small_load(U, ldu, Kt, ldk, PK * s, c0, r0, lane, a0, b0);
+  if (s + 4 < nsteps) small_load(U, ldu, Kt, ldk, PK * (s + 4), c0, r0, lane, a1, b1);
+  for (; s < nsteps; s += 4) {
+    double a2[4][2], b2[4][2];
+    const bool more = s + 8 < nsteps;
+    if (more) small_load(U, ldu, Kt, ldk, PK * (s + 8), c0, r0, lane, a2, b2);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int hc = 0; hc < 2; ++hc)
+#pragma unroll
+        for (int hr = 0; hr < 2; ++hr) acc[hc][hr] = mfma_f64(a0[ks][hc], b0[ks][hr], acc[hc][hr]);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        a0[ks][h] = a1[ks][h];
+        b0[ks][h] = b1[ks][h];
+        if (more) {
+          a1[ks][h] = a2[ks][h];
+          b1[ks][h] = b2[ks][h];
+        }
+      }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void post_small_kernel(
+    const double* __restrict__ Kt, int64_t ldk, const double* __restrict__ U, int64_t ldu,
+    const double* __restrict__ beta, int n, int nct, double* __restrict__ Spart,
+    double* __restrict__ mpart) {
+  // [source wave][tile][hc][hr][register][lane]: 64 KB
+  __shared__ __attribute__((aligned(16))) double red[4][2][2][2][4][64];
+  const int npair = nct >> 1;
+  const int unit = blockIdx.x;
+  // consecutive blocks go to different XCDs: the 8 units of one row tile that
+  // an XCD holds at once share its K*x^T rows, the pairs spread U over the L2s
+  const int p = unit % npair, ru = unit / npair;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r0 = ru * SMU;
+  const int ctA = p, ctB = nct - 1 - p;
+  v4d acc[2][2][2];  // [tile][hc][hr]
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int hc = 0; hc < 2; ++hc)
+#pragma unroll
+      for (int hr = 0; hr < 2; ++hr) acc[t][hc][hr] = v4d_zero();
+  // tile t: k in [0, 32 (ct + 1)), 2 (ct + 1) steps of 16; the second tile's
+  // steps are dealt from the wave after the one that took the first's last step
+  const int sA = 2 * (ctA + 1), sB = 2 * (ctB + 1);
+  small_tile(U, ldu, Kt, ldk, SMU * ctA, r0, sA, wave, lane, acc[0]);
+  small_tile(U, ldu, Kt, ldk, SMU * ctB, r0, sB, (wave - sA % 4 + 4) % 4, lane, acc[1]);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int hc = 0; hc < 2; ++hc)
+#pragma unroll
+      for (int hr = 0; hr < 2; ++hr)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wave][t][hc][hr][r][lane] = acc[t][hc][hr][r];
+  __syncthreads();
+  // wave (t, hr): the unit's R^T block of tile t, row half hr, summed in wave order
+  const int t = wave >> 1, hr = wave & 1;
+  double v[2][4];
+#pragma unroll
+  for (int hc = 0; hc < 2; ++hc)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double x = red[0][t][hc][hr][r][lane];
+      x += red[1][t][hc][hr][r][lane];
+      x += red[2][t][hc][hr][r][lane];
+      x += red[3][t][hc][hr][r][lane];
+      v[hc][r] = x;
+    }
+  v4d P = v4d_zero();
+  double m = 0.0;
+  const int c0 = SMU * (t ? ctB : ctA);
+#pragma unroll
+  for (int hc = 0; hc < 2; ++hc)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      P = mfma_f64(v[hc][r], v[hc][r], P);
+      const int c = c0 + 16 * hc + mfma_row(lane, r);
+      m = fma(v[hc][r], c < n ? beta[c] : 0.0, m);
+    }
+  m += __shfl_xor(m, 16);
+  m += __shfl_xor(m, 32);
+  __syncthreads();  // every wave's reads of red done
+  double* xP = &red[0][0][0][0][0][0];  // tile 1's blocks handed to tile 0's waves
+  double* xm = xP + 2 * 4 * 64;
+  if (t == 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) xP[(hr * 4 + r) * 64 + lane] = P[r];
+    xm[hr * 64 + lane] = m;
+  }
+  __syncthreads();
+  if (t == 0) {
+    const int nrows16 = (int)(ldk >> 4);
+    const int row16 = (r0 >> 4) + hr;
+    double* sp = Spart + ((int64_t)p * nrows16 + row16) * 256;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      sp[mfma_row(lane, r) * 16 + mfma_col(lane)] = P[r] + xP[(hr * 4 + r) * 64 + lane];
+    if (lane < 16) mpart[(int64_t)p * ldk + row16 * 16 + lane] = m + xm[hr * 64 + lane];
+  }
+}
+
+// Small-grid plan switch: BO_POST_SMALL=0 off, 1 whenever it applies, unset /
+// auto: where the 128-tile plan would be stream-K (read once).
+static int small_mode() {
+  static const int v = [] {
+    const char* e = std::getenv("BO_POST_SMALL");
+    if (!e) return 2;
+    return e[0] == '0' ? 0 : (e[0] == '1' ? 1 : 2);
+  }();
+  return v;
+}
+
 // Paired super-tile schedule switch (default on; BO_POST_PAIRED=0: off), read once.
 static bool paired_enabled() {
   static const bool on = [] {
@@ -1004,6 +1163,49 @@ int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len,
     *kc_len = -1;
     *work_elems = (int64_t)plan_chunks(nC, (int)nI, (int)n, -1, slots, PLAN_POST) * PI * PC;
   }
+  return BO_OK;
+}
+
+// Small-grid posterior plan (post_small_kernel): *nparts = the number of
+// pair partials per 16-row tile (np / 64), 0 when the 128-tile plan is kept.
+int bo_post_small_plan(int64_t B, int q, int64_t n, int* nparts) {
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  *nparts = 0;
+  const int mode = small_mode();
+  if (mode == 0 || B <= 0) return BO_OK;
+  if (mode == 2) {
+    int kc = 0;
+    int64_t we = 0;
+    s = bo_post_split_plan(B, q, n, 0, &kc, &we);
+    if (s) return s;
+    if (kc == 0) return BO_OK;
+  }
+  *nparts = (int)(ceil_div(n, PC) * PC / (2 * SMU));
+  return BO_OK;
+}
+
+// R R^T and R beta partials of the forward posterior from K*x^T (Kt, np x
+// nrows_pad, bo_post_kxt), U = L^{-T} (np x np, ld ldu): Spart nparts x
+// nrows_pad/16 x 16 x 16, mpart nparts x nrows_pad, nparts from
+// bo_post_small_plan.
+int bo_post_small(const double* Kt, int64_t B, int q, int64_t n, const double* U, int64_t ldu,
+                  const double* beta, double* Spart, double* mpart, void* stream) {
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  BO_CHECK_ARG(Kt && U && beta && Spart && mpart, "bo_post_small: null buffer");
+  const int64_t np = (int64_t)nC * PC;
+  BO_CHECK_ARG(ldu >= np, "bo_post_small: ldu %lld < padded order %lld", (long long)ldu,
+               (long long)np);
+  if (B == 0) return BO_OK;
+  const int nct = (int)(np / SMU);
+  const int64_t nru = ceil_div(B * Qp, SMU);
+  const int64_t grid = nru * (nct / 2);
+  post_small_kernel<<<(unsigned)grid, 256, 0, as_stream(stream)>>>(Kt, nrows_pad, U, ldu, beta,
+                                                                    (int)n, nct, Spart, mpart);
+  BO_LAUNCH_CHECK();
   return BO_OK;
 }
 

@@ -216,10 +216,14 @@ std::vector<at::Tensor> qmc_acq_impl(
     TORCH_CHECK(Ainv->size(0) == np && Ainv->size(1) == np, "bo::qmc_acq_native: Ainv must be np x np");
     ck(bo_post_quad_plan(B, q, n, &npairs), "post_quad_plan");
   }
-  const int nparts = npairs > 0 ? npairs : nC;
+  // forward-only small grids: equal 32-row units over column-tile pairs
+  // (post_small_kernel), no split-k workspace or reduction launch
+  int nsmall = 0;
+  if (!need_grad && kxt && npairs == 0) ck(bo_post_small_plan(B, q, n, &nsmall), "post_small_plan");
+  const int nparts = npairs > 0 ? npairs : (nsmall > 0 ? nsmall : nC);
   int kc = 0;
   int64_t we = 0;
-  if (npairs == 0) ck(bo_post_split_plan(B, q, n, 0, &kc, &we), "post_split_plan");
+  if (npairs == 0 && nsmall == 0) ck(bo_post_split_plan(B, q, n, 0, &kc, &we), "post_split_plan");
 
   // one workspace for the intermediates (offsets in doubles, 16-B aligned)
   auto al2 = [](int64_t v) { return (v + 1) & ~int64_t(1); };
@@ -258,6 +262,9 @@ std::vector<at::Tensor> qmc_acq_impl(
   if (npairs > 0) {
     ck(bo_post_quad(Kt, Ainv->data_ptr<double>(), np, alpha->data_ptr<double>(), B, q, n, Spart,
                     mpart, st), "post_quad");
+  } else if (nsmall > 0) {
+    ck(bo_post_small(Kt, B, q, n, U.data_ptr<double>(), np, beta.data_ptr<double>(), Spart, mpart,
+                     st), "post_small");
   } else {
     BoPostPartialsArgs pa{};
     pa.struct_size = sizeof(pa);
@@ -334,7 +341,7 @@ std::vector<at::Tensor> qmc_acq_impl(
   fa.fat = fat ? 1 : 0;
   fa.tau_relu = tau_relu;
   fa.tau_max = tau_max;
-  fa.nparts = npairs;
+  fa.nparts = npairs > 0 ? npairs : nsmall;
   fa.sym_parts = npairs > 0 ? 1 : 0;
 
   // (the backward's W = R L^-1 is formed by qmc_acq_backward_native, fused

@@ -33,6 +33,7 @@ from __future__ import annotations
 import warnings
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -179,3 +180,59 @@ def optimize_acqf_sharded(acq_function, bounds, q: int, num_restarts: int,
         best = torch.argmax(all_vals, dim=0)
         return all_cands[best], all_vals[best]
     return all_cands, all_vals
+
+
+def _fit_layouts(mll):
+    """The flat hyperparameter layouts a fit writes: one per exact GP (a
+    ModelListGP's SumMarginalLogLikelihood fits its members one by one,
+    fit.py:262-283)."""
+    from .fit import SumMarginalLogLikelihood, _layout
+    if isinstance(mll, SumMarginalLogLikelihood):
+        return [_layout(sub.model) for sub in mll.mlls]
+    return [_layout(mll.model)]
+
+
+def fit_gpytorch_mll_replicated(mll, group=None, fit=None, **kwargs):
+    """``fit_gpytorch_mll`` (fit.py:75-113) for replicated models (SURVEY.md
+    8(e): the GP fit is one O(n^3) problem, so it is not sharded).  Rank 0
+    runs the fit -- retries, prior resampling and rollback included -- and
+    broadcasts ``[ok, x]``, x the fitted hyperparameter vector in the layout
+    order of get_parameters_and_bounds (8 numbers at d = 6); every other rank
+    writes x into its own model.  Every rank then holds bit-identical
+    hyperparameters and ends in eval mode, and builds its prediction caches
+    locally on first use (cheaper than moving L, L^-1: 2 x 134 MB at C3).  A
+    ModelFittingError on rank 0 is raised on every rank, with every model left
+    at its starting state in train mode (the reference's failure contract).
+    ``fit`` replaces the fit routine (default fit.fit_gpytorch_mll)."""
+    from .exceptions import ModelFittingError
+    from .fit import fit_gpytorch_mll
+    fit = fit or fit_gpytorch_mll
+    ws, rank = world(group)
+    if ws == 1:
+        return fit(mll, **kwargs)
+    layouts = _fit_layouts(mll)
+    sizes = [lay.size for lay in layouts]
+    dev = mll.model.train_inputs[0].device if hasattr(mll.model, "train_inputs") else \
+        mll.mlls[0].model.train_inputs[0].device
+    msg = torch.zeros(1 + sum(sizes), dtype=torch.float64)
+    err = None
+    if rank == 0:
+        try:
+            fit(mll, **kwargs)
+            msg[0] = 1.0
+            msg[1:] = torch.from_numpy(np.concatenate([lay.get() for lay in layouts]))
+        except ModelFittingError as e:
+            err = e
+    msg = _broadcast_from_rank0(msg.to(dev), group).cpu()
+    if not bool(msg[0]):
+        if err is not None:
+            raise err
+        mll.train()
+        raise ModelFittingError("All attempts to fit the model have failed (rank 0 of the "
+                                "replicated fit).")
+    if rank != 0:
+        off = 1
+        for lay, k in zip(layouts, sizes):
+            lay.set(msg[off:off + k].numpy().astype(np.float64))
+            off += k
+    return mll.eval()

@@ -302,6 +302,22 @@ int bo_post_split_plan(int64_t B, int q, int64_t n, int slots, int* kc_len,
 /* Workspace doubles of bo_post_partials under a given kc_len (0, -1 or a
  * chunk length). */
 int bo_post_split_work(int64_t B, int q, int64_t n, int kc_len, int64_t* work_elems);
+
+/* Small-grid forward posterior (round 5; replaces the stream-K split + split-k
+ * reduction of small forward-only grids such as C2, the R R^T / R beta
+ * contraction of [G] exact prediction, botorch/models/gpytorch.py:446 under
+ * acquisition/monte_carlo.py:405-414): units of 32 test rows x a pair of
+ * 32-column tiles of U = L^{-T} whose triangular k-ranges sum to a constant,
+ * so every unit covers whole k-ranges and emits finished 16 x 16 partials.
+ * bo_post_small_plan: *nparts = np / 64 partials per 16-row tile where the
+ * library takes this route (BO_POST_SMALL: 0 never, 1 always, default where
+ * the 128-tile plan would be stream-K), else 0.  bo_post_small: Kt = K*x^T
+ * (np x nrows_pad, bo_post_kxt), U (ld ldu >= np), beta (n); writes Spart
+ * (nparts x nrows_pad/16 x 16 x 16) and mpart (nparts x nrows_pad), the
+ * bo_qmc_finalize inputs with nparts = *nparts, sym_parts = 0. */
+int bo_post_small_plan(int64_t B, int q, int64_t n, int* nparts);
+int bo_post_small(const double* Kt, int64_t B, int q, int64_t n, const double* U, int64_t ldu,
+                  const double* beta, double* Spart, double* mpart, void* stream);
 /* A^{-1} = L^{-T} L^{-1} for the MLL gradient (replaces the U U^T GEMM of
  * fit.py's closure, optim/closures/model_closures.py:171-184 -> [G]
  * ExactMarginalLogLikelihood backward): Linv np x np (ld = np = n rounded up

@@ -123,3 +123,76 @@ def test_sharded_optimize_acqf_equals_single_process(tmp_path, ws):
         assert torch.equal(o["ics"], ics)
         assert torch.equal(o["cands"], cands) and torch.equal(o["vals"], vals)
         assert torch.equal(o["cand"], cand) and torch.equal(o["val"].reshape(()), val.reshape(()))
+
+
+def _fit_worker(rank, ws, port, outdir, mode):
+    """fit_gpytorch_mll_replicated over gloo with a stand-in fit routine (the
+    device MLL needs a GPU; tests/test_gpu_distributed.py runs the real one):
+    rank 0's fitted hyperparameters reach every rank bit for bit, a failure on
+    rank 0 raises on every rank, and a ModelListGP's members all travel."""
+    import torch.distributed as dist
+    from botorch_amd.distributed import fit_gpytorch_mll_replicated
+    from botorch_amd.exceptions import ModelFittingError
+    from botorch_amd.fit import ExactMarginalLogLikelihood, SumMarginalLogLikelihood
+    from botorch_amd.models import ModelListGP, SingleTaskGP
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        g = torch.Generator().manual_seed(0)
+        X = torch.rand(32, 6, generator=g, dtype=torch.float64)
+        Y = torch.rand(32, 2, generator=g, dtype=torch.float64)
+        calls = []
+
+        def fake_fit(mll, **kw):  # "fits" to rank-specific values: only rank 0's may survive
+            calls.append(rank)
+            mods = [s.model for s in mll.mlls] if isinstance(mll, SumMarginalLogLikelihood) \
+                else [mll.model]
+            if mode == "fail":
+                raise ModelFittingError("All attempts to fit the model have failed.")
+            for t, mm in enumerate(mods):
+                mm.covar_module.lengthscale = torch.linspace(0.1, 0.7, 6, dtype=torch.float64
+                                                             ).reshape(1, 6) * (1 + t) / 3 + rank
+                mm.likelihood.noise = torch.tensor([1e-3 * (t + 1) / 7 + rank], dtype=torch.float64)
+                mm.mean_module.constant = 0.1 / 3 * (t + 1) + rank
+            return mll.eval()
+
+        if mode == "list":
+            model = ModelListGP(SingleTaskGP(X, Y[:, :1]), SingleTaskGP(X, Y[:, 1:]))
+            mll = SumMarginalLogLikelihood(None, model)
+            mods = list(model.models)
+        else:
+            model = SingleTaskGP(X, Y[:, :1])
+            mll = ExactMarginalLogLikelihood(model.likelihood, model)
+            mods = [model]
+        out = {"calls": calls}
+        try:
+            fit_gpytorch_mll_replicated(mll, fit=fake_fit)
+            out["state"] = [torch.cat([mm.covar_module.lengthscale.detach().reshape(-1),
+                                       mm.likelihood.noise.detach().reshape(-1),
+                                       mm.mean_module.constant.detach().reshape(-1)])
+                            for mm in mods]
+            out["training"] = any(mm.training for mm in mods)
+        except ModelFittingError as e:
+            out["error"] = str(e)
+        torch.save(out, os.path.join(outdir, f"r{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,ws", [("single", 2), ("single", 3), ("list", 2), ("fail", 2)])
+def test_replicated_fit_broadcasts_rank0(tmp_path, mode, ws):
+    port = _free_port()
+    mp.spawn(_fit_worker, args=(ws, port, str(tmp_path), mode), nprocs=ws, join=True)
+    outs = [torch.load(os.path.join(tmp_path, f"r{r}.pt"), weights_only=True) for r in range(ws)]
+    assert outs[0]["calls"] == [0] and all(o["calls"] == [] for o in outs[1:])
+    if mode == "fail":
+        assert all("failed" in o["error"] for o in outs)
+        return
+    for o in outs:
+        assert not o["training"]
+        for a, b in zip(o["state"], outs[0]["state"]):
+            assert torch.equal(a, b)
+    # rank 0's values, not any other rank's
+    assert float(outs[0]["state"][0][0]) < 1.0
