@@ -1107,15 +1107,15 @@ def main():
     native.post_timing(False)
     hook.on = False
     kern_ms = native.post_timing_read().tolist() + hook.read()
-    if len(kern_ms) != args.steps * w.launches:
-        raise SystemExit(f"bench: {len(kern_ms)} timed post_partials launches for {args.steps} "
-                         f"steps of {w.launches}")
+    if not kern_ms or len(kern_ms) % args.steps:
+        raise SystemExit(f"bench: {len(kern_ms)} timed posterior launches for {args.steps} steps")
+    launches = len(kern_ms) // args.steps  # qEHVI: one batched launch for its three members
     ms_step = 1e3 * elapsed / args.steps
     evals_per_step = w.q * R * w.S * (1 if strong else ws)
     value = evals_per_step * args.steps / elapsed
 
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
-    fl = w.flops_launch(r1 - r0)
+    fl = w.flops_launch(r1 - r0) * w.launches / launches  # the step's posterior flops per launch
     achieved = fl / (kern_avg_ms * 1e-3) / 1e12
     peak = 78.6  # MI355X dense FP64 matrix TFLOP/s (MI355X_MICROARCH.md / SURVEY.md 8(d))
     peak_box = mfma_f64_ceiling(dev)
@@ -1227,7 +1227,7 @@ def main():
                          "traffic_ratio": traffic / alg_bytes if traffic else None,
                          "traffic_note": traffic_note,
                          "kernel_ms": kern_avg_ms, "flops_per_launch": fl,
-                         "launches_per_step": w.launches},
+                         "launches_per_step": launches},
             "cpu_baseline": cpu,
             "check": check,
             "weak": weak,

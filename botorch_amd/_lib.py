@@ -51,6 +51,8 @@ _SIGNATURES = {
                                 _P]),
     "bo_gemv": (c_int, [_P, c_int64, c_int64, _P, c_double, _P, _P]),
     "bo_gemv_tri": (c_int, [_P, c_int64, c_int64, _P, c_double, _P, c_int, _P]),
+    "bo_gemv_lt_work": (c_int, [c_int64, POINTER(c_int64)]),
+    "bo_gemv_lt": (c_int, [_P, c_int64, c_int64, _P, c_double, _P, _P, _P]),
     "bo_scale_inputs": (c_int, [_P, c_int64, c_int, _P, _P, c_int, _P, _P]),
     "bo_gp_cache_build": (c_int, [c_int, _P, c_int64, c_int, _P, c_double, c_double, c_double,
                                   _P, _P, _P, _P, _P, _P, c_int, c_double, POINTER(c_double),
@@ -81,7 +83,9 @@ _SIGNATURES = {
                                  _P, _P]),
     "bo_post_quad_plan": (c_int, [c_int64, c_int, c_int64, POINTER(c_int)]),
     "bo_post_small_plan": (c_int, [c_int64, c_int, c_int64, POINTER(c_int)]),
-    "bo_post_small": (c_int, [_P, c_int64, c_int, c_int64, _P, c_int64, _P, _P, _P, _P]),
+    "bo_post_small": (c_int, [_P, c_int64, c_int, c_int64, _P, c_int64, _P, _P, _P, _P, _P]),
+    "bo_post_small_batched": (c_int, [c_int, _P, _P, _P, _P, _P, _P, c_int64, c_int, c_int64,
+                                      c_int64, _P]),
     "bo_post_quad": (c_int, [_P, _P, c_int64, _P, c_int64, c_int, c_int64, _P, _P, _P]),
     "bo_post_split_table": (c_int, [c_int64, c_int, c_int64, c_int, _P, c_int, _P, c_int,
                                     POINTER(c_int), POINTER(c_int)]),

@@ -900,10 +900,12 @@ class _FusedQEHVI(torch.autograd.Function):
         q = X3.shape[-2]
         means, Ls, saved = [], [], []
         keys = prime_prediction_caches(models)
-        for mm, key in zip(models, keys):
-            cache = mm.prediction_cache(key=key)
+        caches = [mm.prediction_cache(key=key) for mm, key in zip(models, keys)]
+        # every member's posterior partials in one launch where the small-grid
+        # plan applies (C4: the three outputs of the ModelListGP)
+        pps = kernels.post_partials_members(caches, X3.detach(), store_R=need_grad)
+        for mm, cache, pp in zip(models, caches, pps):
             ymean, ystd = mm.outcome_stats()
-            pp = kernels.post_partials(cache, X3.detach(), store_R=need_grad)
             out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
                                        want_cov=False, want_L=True)
             kernels._raise_not_psd(out["info"], out["jitter"], "qEHVI posterior root")

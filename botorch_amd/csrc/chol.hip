@@ -198,6 +198,49 @@ __global__ __launch_bounds__(256) void gemv_tri_kernel(const double* __restrict_
   if (lane == 0) y[row] = s;
 }
 
+// y = M^T (x - xshift) for a lower-triangular M (y[c] = sum_{k >= c} M[k][c]
+// (x[k] - xshift)) without forming M^T: block (column block of 64, row chunk of
+// 256) -- lane = column, so every row is one coalesced 512-B read -- writes
+// its partial sums part[chunk][c] (the 4 waves' row subsets summed in wave
+// order through LDS); gemv_lt_sum_kernel adds the chunks in order.
+constexpr int GLT_ROWS = 256;
+__global__ __launch_bounds__(256) void gemv_lt_kernel(const double* __restrict__ M, int64_t ld,
+                                                      int64_t n, const double* __restrict__ x,
+                                                      double xshift, double* __restrict__ part,
+                                                      int64_t ldp) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t k0 = (int64_t)blockIdx.y * GLT_ROWS;
+  const int64_t k1 = k0 + GLT_ROWS < n ? k0 + GLT_ROWS : n;
+  double s = 0.0;
+  if (c < n) {
+    const int64_t kb = k0 > c ? k0 : c;  // rows k >= c only
+#pragma unroll 4
+    for (int64_t k = kb + ((wave - kb) % 4 + 4) % 4; k < k1; k += 4)
+      s = fma(M[k * ld + c], x[k] - xshift, s);
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0) {
+    s = red[0][lane];
+    s += red[1][lane];
+    s += red[2][lane];
+    s += red[3][lane];
+    if (c < n) part[(int64_t)blockIdx.y * ldp + c] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void gemv_lt_sum_kernel(const double* __restrict__ part,
+                                                          int64_t ldp, int nchunk, int64_t n,
+                                                          double* __restrict__ y) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  double s = 0.0;
+  for (int j = 0; j < nchunk; ++j) s += part[(int64_t)j * ldp + c];
+  y[c] = s;
+}
+
 __global__ void scale_inputs_kernel(const double* __restrict__ X, int64_t n, int d,
                                     const double* __restrict__ ls, const double* __restrict__ center,
                                     int dp, double* __restrict__ Xs) {
@@ -332,6 +375,25 @@ int bo_gemv_tri(const double* M, int64_t ld, int64_t n, const double* x, double 
   return BO_OK;
 }
 
+int bo_gemv_lt_work(int64_t n, int64_t* work_elems) {
+  *work_elems = ceil_div(n, GLT_ROWS) * n;
+  return BO_OK;
+}
+
+int bo_gemv_lt(const double* M, int64_t ld, int64_t n, const double* x, double xshift, double* y,
+               double* work, void* stream) {
+  BO_CHECK_ARG(M && x && y && work && ld >= n, "bo_gemv_lt: bad arguments");
+  if (n <= 0) return BO_OK;
+  const int nchunk = (int)ceil_div(n, GLT_ROWS);
+  hipStream_t st = as_stream(stream);
+  gemv_lt_kernel<<<dim3((unsigned)ceil_div(n, 64), (unsigned)nchunk), 256, 0, st>>>(M, ld, n, x,
+                                                                                  xshift, work, n);
+  BO_LAUNCH_CHECK();
+  gemv_lt_sum_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(work, n, nchunk, n, y);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
 int bo_scale_inputs(const double* X, int64_t n, int d, const double* lengthscale,
                     const double* center, int dp, double* Xs, void* stream) {
   BO_CHECK_ARG(dp >= d, "bo_scale_inputs: dp < d");
@@ -387,7 +449,16 @@ static int gp_cache_build_impl(int kind, const double* Xt, int64_t n, int d,
   if (s) return s;
   s = bo_gemv_tri(Linv, np, n, y, constant, beta, 1, stream);  // beta = L^{-1} (y - c)
   if (s) return s;
-  return bo_gemv_tri(U, np, n, beta, 0.0, alpha, 2, stream);   // alpha = L^{-T} beta
+  // alpha = L^{-T} beta from L^{-1}'s columns (the MLL closure's path, which
+  // forms no U, takes the same kernel: the two agree bit for bit); the chunk
+  // partials in stream-ordered scratch
+  int64_t we = 0;
+  bo_gemv_lt_work(n, &we);
+  double* work = nullptr;
+  BO_HIP(hipMallocAsync(reinterpret_cast<void**>(&work), sizeof(double) * we, st));
+  s = bo_gemv_lt(Linv, np, n, beta, 0.0, alpha, work, stream);
+  BO_HIP(hipFreeAsync(work, st));
+  return s;
 }
 
 extern "C" {

@@ -832,16 +832,37 @@ __device__ __forceinline__ void small_tile(const double* __restrict__ U, int64_t
   }
 }
 
-__global__ __launch_bounds__(256, 2) void post_small_kernel(
-    const double* __restrict__ Kt, int64_t ldk, const double* __restrict__ U, int64_t ldu,
-    const double* __restrict__ beta, int n, int nct, double* __restrict__ Spart,
-    double* __restrict__ mpart) {
+// One launch serves up to 8 models of one shape (the members of a
+// ModelListGP: C4's three outputs): block b -> member b / units, unit b % units.
+constexpr int SMALL_MAXM = 8;
+struct SmallMember {
+  const double* Kt;    // np x ldk
+  const double* U;     // np x ldu
+  const double* beta;  // n
+  double* Spart;       // nparts x ldk/16 x 16 x 16
+  double* mpart;       // nparts x ldk
+  double* Rt;          // np x ldk, row-major R^T (the gradient path), or null
+};
+struct SmallArgs {
+  SmallMember m[SMALL_MAXM];
+  int64_t ldk, ldu;
+  int n, nct, units;
+};
+
+__global__ __launch_bounds__(256, 2) void post_small_kernel(const SmallArgs a) {
   // [source wave][tile][hc][hr][register][lane]: 64 KB
   __shared__ __attribute__((aligned(16))) double red[4][2][2][2][4][64];
-  const int npair = nct >> 1;
-  const int unit = blockIdx.x;
-  // consecutive blocks go to different XCDs: the 8 units of one row tile that
-  // an XCD holds at once share its K*x^T rows, the pairs spread U over the L2s
+  const int npair = a.nct >> 1;
+  const int mem = blockIdx.x / a.units;
+  const int unit = blockIdx.x - mem * a.units;
+  const SmallMember& M = a.m[mem];
+  const double* __restrict__ Kt = M.Kt;
+  const double* __restrict__ U = M.U;
+  const int64_t ldk = a.ldk, ldu = a.ldu;
+  const int n = a.n, nct = a.nct;
+  // consecutive blocks go to different XCDs: the units of one row tile spread
+  // over the XCDs and share K*x^T rows through the MALL, each XCD's L2 holds
+  // the U columns of its pairs
   const int p = unit % npair, ru = unit / npair;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r0 = ru * SMU;
@@ -880,16 +901,24 @@ __global__ __launch_bounds__(256, 2) void post_small_kernel(
       x += red[3][t][hc][hr][r][lane];
       v[hc][r] = x;
     }
+  const int c0 = SMU * (t ? ctB : ctA);
+  if (M.Rt != nullptr) {  // row-major R^T: 16 lanes = one 128-B row segment
+#pragma unroll
+    for (int hc = 0; hc < 2; ++hc)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        M.Rt[(int64_t)(c0 + 16 * hc + mfma_row(lane, r)) * ldk + r0 + 16 * hr + mfma_col(lane)] =
+            v[hc][r];
+  }
   v4d P = v4d_zero();
   double m = 0.0;
-  const int c0 = SMU * (t ? ctB : ctA);
 #pragma unroll
   for (int hc = 0; hc < 2; ++hc)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       P = mfma_f64(v[hc][r], v[hc][r], P);
       const int c = c0 + 16 * hc + mfma_row(lane, r);
-      m = fma(v[hc][r], c < n ? beta[c] : 0.0, m);
+      m = fma(v[hc][r], c < n ? M.beta[c] : 0.0, m);
     }
   m += __shfl_xor(m, 16);
   m += __shfl_xor(m, 32);
@@ -905,11 +934,11 @@ __global__ __launch_bounds__(256, 2) void post_small_kernel(
   if (t == 0) {
     const int nrows16 = (int)(ldk >> 4);
     const int row16 = (r0 >> 4) + hr;
-    double* sp = Spart + ((int64_t)p * nrows16 + row16) * 256;
+    double* sp = M.Spart + ((int64_t)p * nrows16 + row16) * 256;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       sp[mfma_row(lane, r) * 16 + mfma_col(lane)] = P[r] + xP[(hr * 4 + r) * 64 + lane];
-    if (lane < 16) mpart[(int64_t)p * ldk + row16 * 16 + lane] = m + xm[hr * 64 + lane];
+    if (lane < 16) M.mpart[(int64_t)p * ldk + row16 * 16 + lane] = m + xm[hr * 64 + lane];
   }
 }
 
@@ -1186,27 +1215,43 @@ int bo_post_small_plan(int64_t B, int q, int64_t n, int* nparts) {
   return BO_OK;
 }
 
-// R R^T and R beta partials of the forward posterior from K*x^T (Kt, np x
-// nrows_pad, bo_post_kxt), U = L^{-T} (np x np, ld ldu): Spart nparts x
-// nrows_pad/16 x 16 x 16, mpart nparts x nrows_pad, nparts from
-// bo_post_small_plan.
-int bo_post_small(const double* Kt, int64_t B, int q, int64_t n, const double* U, int64_t ldu,
-                  const double* beta, double* Spart, double* mpart, void* stream) {
+// R R^T and R beta partials of the posterior from K*x^T (Kt, np x nrows_pad,
+// bo_post_kxt) and U = L^{-T} (np x np, ld ldu) for nm <= 8 models of one
+// shape in one launch: Spart[m] nparts x nrows_pad/16 x 16 x 16, mpart[m]
+// nparts x nrows_pad (nparts from bo_post_small_plan); Rt[m] (optional, null
+// array or entries): R^T row-major, np x nrows_pad.
+int bo_post_small_batched(int nm, const double* const* Kt, const double* const* U,
+                          const double* const* beta, double* const* Spart, double* const* mpart,
+                          double* const* Rt, int64_t B, int q, int64_t n, int64_t ldu,
+                          void* stream) {
   int Qp, nrows_pad, nC;
   int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
   if (s) return s;
-  BO_CHECK_ARG(Kt && U && beta && Spart && mpart, "bo_post_small: null buffer");
+  BO_CHECK_ARG(nm >= 1 && nm <= SMALL_MAXM, "bo_post_small_batched: %d models (1..%d)", nm,
+               SMALL_MAXM);
+  BO_CHECK_ARG(Kt && U && beta && Spart && mpart, "bo_post_small_batched: null pointer array");
   const int64_t np = (int64_t)nC * PC;
   BO_CHECK_ARG(ldu >= np, "bo_post_small: ldu %lld < padded order %lld", (long long)ldu,
                (long long)np);
+  SmallArgs a{};
+  for (int m = 0; m < nm; ++m) {
+    BO_CHECK_ARG(Kt[m] && U[m] && beta[m] && Spart[m] && mpart[m], "bo_post_small: null buffer");
+    a.m[m] = SmallMember{Kt[m], U[m], beta[m], Spart[m], mpart[m], Rt ? Rt[m] : nullptr};
+  }
   if (B == 0) return BO_OK;
-  const int nct = (int)(np / SMU);
-  const int64_t nru = ceil_div(B * Qp, SMU);
-  const int64_t grid = nru * (nct / 2);
-  post_small_kernel<<<(unsigned)grid, 256, 0, as_stream(stream)>>>(Kt, nrows_pad, U, ldu, beta,
-                                                                    (int)n, nct, Spart, mpart);
+  a.ldk = nrows_pad;
+  a.ldu = ldu;
+  a.n = (int)n;
+  a.nct = (int)(np / SMU);
+  a.units = (int)(ceil_div(B * Qp, SMU) * (a.nct / 2));
+  post_small_kernel<<<(unsigned)(a.units * nm), 256, 0, as_stream(stream)>>>(a);
   BO_LAUNCH_CHECK();
   return BO_OK;
+}
+
+int bo_post_small(const double* Kt, int64_t B, int q, int64_t n, const double* U, int64_t ldu,
+                  const double* beta, double* Spart, double* mpart, double* Rt, void* stream) {
+  return bo_post_small_batched(1, &Kt, &U, &beta, &Spart, &mpart, &Rt, B, q, n, ldu, stream);
 }
 
 int bo_post_split_work(int64_t B, int q, int64_t n, int kc_len, int64_t* work_elems) {

@@ -216,10 +216,11 @@ std::vector<at::Tensor> qmc_acq_impl(
     TORCH_CHECK(Ainv->size(0) == np && Ainv->size(1) == np, "bo::qmc_acq_native: Ainv must be np x np");
     ck(bo_post_quad_plan(B, q, n, &npairs), "post_quad_plan");
   }
-  // forward-only small grids: equal 32-row units over column-tile pairs
-  // (post_small_kernel), no split-k workspace or reduction launch
+  // small grids: equal 32-row units over column-tile pairs (post_small_kernel),
+  // no split-k workspace or reduction launch; with need_grad it also stores
+  // R^T row-major for the backward's W^T routes
   int nsmall = 0;
-  if (!need_grad && kxt && npairs == 0) ck(bo_post_small_plan(B, q, n, &nsmall), "post_small_plan");
+  if (kxt && npairs == 0) ck(bo_post_small_plan(B, q, n, &nsmall), "post_small_plan");
   const int nparts = npairs > 0 ? npairs : (nsmall > 0 ? nsmall : nC);
   int kc = 0;
   int64_t we = 0;
@@ -264,7 +265,7 @@ std::vector<at::Tensor> qmc_acq_impl(
                     mpart, st), "post_quad");
   } else if (nsmall > 0) {
     ck(bo_post_small(Kt, B, q, n, U.data_ptr<double>(), np, beta.data_ptr<double>(), Spart, mpart,
-                     st), "post_small");
+                     mp(Rt), st), "post_small");
   } else {
     BoPostPartialsArgs pa{};
     pa.struct_size = sizeof(pa);

@@ -273,7 +273,12 @@ def build_gp_cache_optimistic(Xt, y, lengthscale, noise: float, constant: float,
     f64 = dict(dtype=torch.float64, device=dev)
     L = torch.empty(np_, np_, **f64)
     Linv = torch.empty(np_, np_, **f64)
-    U = torch.empty(np_, np_, **f64)  # the DAG's counters, then L^{-T}
+    # the DAG's tile counters (4 (np/64)^2 + 16 ints) and alpha's chunk partials;
+    # the MLL closure forms no U = L^{-T} (alpha from L^{-1}'s columns)
+    T = np_ // 64
+    we = ctypes.c_int64()
+    check(lib().bo_gemv_lt_work(n, ctypes.byref(we)), "gemv_lt_work")
+    work = torch.empty(max((16 + 4 * T * T + 1) // 2, we.value), **f64)
     beta = torch.empty(n, **f64)
     alpha = torch.empty(n, **f64)
     info = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -281,11 +286,12 @@ def build_gp_cache_optimistic(Xt, y, lengthscale, noise: float, constant: float,
     st = _stream(dev)
     check(lib().bo_covar_matrix(kind, _p(Xt), n, _p(Xt), n, d, _p(ls), float(outputscale),
                                 float(noise), 1, _p(L), np_, np_, np_, st), "covar_matrix")
-    check(lib().bo_cholesky_inverse(_p(L), _p(Linv), _p(U), np_, _p(info), st), "cholesky_inverse")
-    check(lib().bo_transpose(_p(Linv), _p(U), np_, np_, st), "transpose")
+    check(lib().bo_cholesky_inverse(_p(L), _p(Linv), _p(work), np_, _p(info), st),
+          "cholesky_inverse")
     check(lib().bo_gemv_tri(_p(Linv), np_, n, _p(y), float(constant), _p(beta), 1, st),
           "gemv_tri")
-    check(lib().bo_gemv_tri(_p(U), np_, n, _p(beta), 0.0, _p(alpha), 2, st), "gemv_tri")
+    check(lib().bo_gemv_lt(_p(Linv), np_, n, _p(beta), 0.0, _p(alpha), _p(work), st), "gemv_lt")
+    U = Linv.new_empty(0)  # not formed (no posterior is taken from this cache)
     Xs = torch.empty(n, DP, **f64)
     if d <= DP:
         check(lib().bo_scale_inputs(_p(Xt), n, d, _p(ls), ctypes.c_void_p(0), DP, _p(Xs), st),
@@ -355,7 +361,11 @@ def build_gp_caches(specs, check_nan: bool = True):
         c = float(sp["constant"])
         check(lib().bo_transpose(_p(Linv), _p(U), np_, np_, st), "transpose")
         check(lib().bo_gemv_tri(_p(Linv), np_, n, _p(y), c, _p(beta), 1, st), "gemv_tri")
-        check(lib().bo_gemv_tri(_p(U), np_, n, _p(beta), 0.0, _p(alpha), 2, st), "gemv_tri")
+        we = ctypes.c_int64()
+        check(lib().bo_gemv_lt_work(n, ctypes.byref(we)), "gemv_lt_work")
+        wlt = torch.empty(max(1, we.value), **f64)
+        check(lib().bo_gemv_lt(_p(Linv), np_, n, _p(beta), 0.0, _p(alpha), _p(wlt), st),
+              "gemv_lt")  # alpha = L^{-T} beta, as bo_gp_cache_build
         Xs = torch.empty(n, DP, **f64)
         if d <= DP:
             check(lib().bo_scale_inputs(_p(Xt), n, d, _p(ls), ctypes.c_void_p(0), DP, _p(Xs), st),
@@ -444,9 +454,83 @@ def rt_blocked_plan(B: int, q: int, n: int) -> bool:
     return we.value > 0 and split_plan(B, q, n)[0] == 0
 
 
+def small_plan(B: int, q: int, n: int) -> int:
+    """Pair partials per 16-row tile of the small-grid posterior
+    (bo_post_small_plan), 0 where the 128-tile plan is kept."""
+    v = ctypes.c_int()
+    check(lib().bo_post_small_plan(B, q, n, ctypes.byref(v)), "post_small_plan")
+    return v.value
+
+
+def post_partials_members(caches, X: torch.Tensor, store_R: bool = False) -> list:
+    """post_partials of one X under several models of one shape (a
+    ModelListGP's members, models/gpytorch.py:629-726): where the small-grid
+    plan applies, every member's K*x^T is built and ONE bo_post_small_batched
+    launch forms all members' partials (C4: three outputs, one launch);
+    elsewhere one post_partials per member."""
+    c0 = caches[0]
+    B, q, d = X.shape
+    same = all(c.n == c0.n and c.np == c0.np and c.d == c0.d for c in caches)
+    nparts = small_plan(B, q, c0.n) if same and 1 < len(caches) <= 8 else 0
+    if nparts == 0 or c0.np * geometry(B, q, c0.n)[1] * 8 > kxt_cap(_dev(X)):
+        return [post_partials(c, X, store_R=store_R) for c in caches]
+    dev = _dev(X)
+    Qp, nrows_pad, nC = geometry(B, q, c0.n)
+    f64 = dict(dtype=torch.float64, device=dev)
+    st = _stream(dev)
+    Xc = X.contiguous()
+    pps, ptrs = [], {k: [] for k in ("Kt", "U", "beta", "S", "m", "Rt")}
+    for c in caches:
+        Xq = torch.empty(nrows_pad, DP, **f64)
+        Kt = torch.empty(c.np, nrows_pad, **f64)
+        check(lib().bo_post_kxt_rows(c.kind, _p(Xc), B, q, d, _p(c.lengthscale), _p(c.Xt_scaled),
+                                     c.n, c.outputscale, _p(Xq), _p(Kt), st), "post_kxt_rows")
+        Sp = torch.empty(nparts, nrows_pad // 16, 16, 16, **f64)
+        mp = torch.empty(nparts, nrows_pad, **f64)
+        Rt = torch.empty(nC * 128, nrows_pad, **f64) if store_R else None
+        pps.append(PostPartials(B, q, Qp, nrows_pad, nC, Xq, Sp, mp, Rt))
+        for k, t in (("Kt", Kt), ("U", c.U), ("beta", c.beta), ("S", Sp), ("m", mp), ("Rt", Rt)):
+            ptrs[k].append(_p(t).value if t is not None else None)
+    nm = len(caches)
+    arr = {k: (ctypes.c_void_p * nm)(*v) for k, v in ptrs.items()}
+    if TIMING_HOOK is not None:
+        TIMING_HOOK("post_partials_begin")
+    check(lib().bo_post_small_batched(nm, arr["Kt"], arr["U"], arr["beta"], arr["S"], arr["m"],
+                                      arr["Rt"], B, q, c0.n, c0.np, st), "post_small_batched")
+    if TIMING_HOOK is not None:
+        TIMING_HOOK("post_partials_end")
+    return pps
+
+
+def _post_small_one(cache: GPCache, X: torch.Tensor, store_R: bool) -> PostPartials:
+    """post_partials on the small-grid kernel, one model."""
+    dev = _dev(X)
+    B, q, d = X.shape
+    Qp, nrows_pad, nC = geometry(B, q, cache.n)
+    nparts = small_plan(B, q, cache.n)
+    f64 = dict(dtype=torch.float64, device=dev)
+    st = _stream(dev)
+    Xq = torch.empty(nrows_pad, DP, **f64)
+    Kt = torch.empty(cache.np, nrows_pad, **f64)
+    check(lib().bo_post_kxt_rows(cache.kind, _p(X.contiguous()), B, q, d, _p(cache.lengthscale),
+                                 _p(cache.Xt_scaled), cache.n, cache.outputscale, _p(Xq), _p(Kt),
+                                 st), "post_kxt_rows")
+    Sp = torch.empty(nparts, nrows_pad // 16, 16, 16, **f64)
+    mp = torch.empty(nparts, nrows_pad, **f64)
+    Rt = torch.empty(nC * 128, nrows_pad, **f64) if store_R else None
+    if TIMING_HOOK is not None:
+        TIMING_HOOK("post_partials_begin")
+    check(lib().bo_post_small(_p(Kt), B, q, cache.n, _p(cache.U), cache.np, _p(cache.beta), _p(Sp),
+                              _p(mp), _p(Rt), st), "post_small")
+    if TIMING_HOOK is not None:
+        TIMING_HOOK("post_partials_end")
+    return PostPartials(B, q, Qp, nrows_pad, nC, Xq, Sp, mp, Rt)
+
+
 def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
                   split: Optional[int] = None, cross: Optional[torch.Tensor] = None,
-                  kxt: Optional[bool] = None, rt_layout: int = 0) -> PostPartials:
+                  kxt: Optional[bool] = None, rt_layout: int = 0,
+                  small: Optional[bool] = None) -> PostPartials:
     """Column-tile partials of R R^T and R beta for X (B x q x d).  ``split``:
     None = the library's plan, 0 = one pass, k > 0 = chunks of k rows,
     -1 = stream-K (equal k-step shares over the resident slots).
@@ -455,13 +539,21 @@ def post_partials(cache: GPCache, X: torch.Tensor, store_R: bool = False,
     split-k plan pp.Cx is None and R^T is stored instead.  ``kxt``: build
     K*x^T first and read it in the posterior kernel (None: when it fits
     kxt_cap).  ``rt_layout``: _lib.RT_BLOCKED stores R^T in the blocked
-    layout bo_post_w_dx reads (one-pass plans only)."""
+    layout bo_post_w_dx reads (one-pass plans only).  ``small``: None = the
+    small-grid plan (bo_post_small) where the library takes it and nothing
+    above asks for the 128-tile kernel (no cross term, library split plan,
+    row-major R^T, K*x^T within the cap); False = never (the bo::post_partials
+    op, whose schema has nC partials)."""
     dev = _dev(X)
     B, q, d = X.shape
     if d != cache.d:
         raise ValueError(f"X has d={d}, model has d={cache.d}")
     Qp, nrows_pad, nC = geometry(B, q, cache.n)
     f64 = dict(dtype=torch.float64, device=dev)
+    if (small is not False and cross is None and split is None and rt_layout == 0
+            and kxt is not False and cache.np * nrows_pad * 8 <= kxt_cap(dev)
+            and small_plan(B, q, cache.n) > 0):
+        return _post_small_one(cache, X, store_R)
     Xq = torch.empty(nrows_pad, DP, **f64)
     Spart = torch.empty(nC, nrows_pad // 16, 16, 16, **f64)
     mpart = torch.empty(nC, nrows_pad, **f64)
@@ -542,7 +634,7 @@ def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd
                              r=T.shape[0] if T is not None else 0, fat=int(bool(fat)),
                              ldT=T.shape[1] if T is not None else 0, F=F,
                              ldF=F.shape[1] if F is not None else 0, tau_relu=float(tau_relu),
-                             tau_max=float(tau_max))
+                             tau_max=float(tau_max), nparts=int(pp.Spart.shape[0]))
     check(lib().bo_qmc_finalize_v(ctypes.byref(a), _stream(dev)), "qmc_finalize")
     return dict(acq=acq, mean=mean, cov=cov, L=L, info=info, jitter=jit)
 

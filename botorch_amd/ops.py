@@ -156,7 +156,7 @@ def post_partials(X: Tensor, Xt: Tensor, Xt_scaled: Tensor, U: Tensor, beta: Ten
     """Column-tile partials of R R^T and R beta for X (B x q x d), R = K*x L^{-T}:
     (Spart nC x B Qp/16 x 16 x 16, mpart nC x B Qp, Xq B Qp x 8, R^T or empty)."""
     c = _cache_from(Xt, Xt_scaled, lengthscale, U, beta, beta, kind, outputscale, 0.0)
-    pp = kernels.post_partials(c, X, store_R=store_R)
+    pp = kernels.post_partials(c, X, store_R=store_R, small=False)  # the schema's nC partials
     Rt = pp.Rt if pp.Rt is not None else X.new_empty(0, dtype=F64)
     return pp.Spart, pp.mpart, pp.Xq, Rt
 

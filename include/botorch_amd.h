@@ -178,9 +178,17 @@ int bo_gemv(const double* M, int64_t ld, int64_t n, const double* x, double xshi
             void* stream);
 /* bo_gemv for a triangular M (uplo 1: lower, 2: upper), reading only the
  * triangle; bit-identical to bo_gemv on the same (zero-filled) matrix.  The
- * cache builds' beta = L^{-1}(y - c) and alpha = L^{-T} beta. */
+ * cache builds' beta = L^{-1}(y - c). */
 int bo_gemv_tri(const double* M, int64_t ld, int64_t n, const double* x, double xshift, double* y,
                 int uplo, void* stream);
+/* y = M^T (x - xshift) for a lower-triangular M (y[c] = sum_{k >= c} M[k][c]
+ * (x[k] - xshift)) read column-wise, without forming M^T: the caches' alpha =
+ * L^{-T} beta = (K + s2 I)^{-1}(y - c), [G] mean_cache (botorch/models/
+ * gpytorch.py:446; the MLL closure, optim/closures/model_closures.py:171-184,
+ * forms no L^{-T}).  work >= bo_gemv_lt_work(n) doubles. */
+int bo_gemv_lt_work(int64_t n, int64_t* work_elems);
+int bo_gemv_lt(const double* M, int64_t ld, int64_t n, const double* x, double xshift, double* y,
+               double* work, void* stream);
 
 /* Xs[i][t] = (X[i][t] - center[t]) / lengthscale[t] for t < d, 0 for d <= t < dp
  * (center may be NULL). */
@@ -314,10 +322,20 @@ int bo_post_split_work(int64_t B, int q, int64_t n, int kc_len, int64_t* work_el
  * the 128-tile plan would be stream-K), else 0.  bo_post_small: Kt = K*x^T
  * (np x nrows_pad, bo_post_kxt), U (ld ldu >= np), beta (n); writes Spart
  * (nparts x nrows_pad/16 x 16 x 16) and mpart (nparts x nrows_pad), the
- * bo_qmc_finalize inputs with nparts = *nparts, sym_parts = 0. */
+ * bo_qmc_finalize inputs with nparts = *nparts, sym_parts = 0, and with Rt
+ * non-null R^T row-major (np x nrows_pad) for the gradient's W^T routes. */
 int bo_post_small_plan(int64_t B, int q, int64_t n, int* nparts);
 int bo_post_small(const double* Kt, int64_t B, int q, int64_t n, const double* U, int64_t ldu,
-                  const double* beta, double* Spart, double* mpart, void* stream);
+                  const double* beta, double* Spart, double* mpart, double* Rt, void* stream);
+/* nm <= 8 models of one shape (B, q, n, ldu) in ONE launch -- the members of
+ * a ModelListGP (botorch/models/gpytorch.py:629-726: C4's three outputs), each
+ * with its own K*x^T, U, beta and outputs (host arrays of device pointers; Rt
+ * may be null, or hold nulls).  Rt[m]: R^T row-major (np x nrows_pad), the
+ * gradient path's input to the W^T routes. */
+int bo_post_small_batched(int nm, const double* const* Kt, const double* const* U,
+                          const double* const* beta, double* const* Spart, double* const* mpart,
+                          double* const* Rt, int64_t B, int q, int64_t n, int64_t ldu,
+                          void* stream);
 /* A^{-1} = L^{-T} L^{-1} for the MLL gradient (replaces the U U^T GEMM of
  * fit.py's closure, optim/closures/model_closures.py:171-184 -> [G]
  * ExactMarginalLogLikelihood backward): Linv np x np (ld = np = n rounded up

@@ -166,3 +166,27 @@ def test_covar_matrix_against_torch():
     torch.testing.assert_close(Kc[:n, :n], torch.tril(ref), rtol=1e-12, atol=1e-13)
     torch.testing.assert_close(Kc[n:, n:], torch.eye(np_ - n, dtype=torch.float64))
     assert float(Kc[:n, n:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("n,ld", [(1000, 1024), (4096, 4096), (37, 128)])
+def test_gemv_lt_matches_transposed_product(n, ld):
+    """bo_gemv_lt: y = M^T (x - s) for a lower-triangular M read column-wise
+    (alpha = L^{-T} beta without forming L^{-T}), against torch in fp64; entries
+    above the diagonal are never read (filled with NaN here)."""
+    import ctypes
+    from botorch_amd import kernels
+    from botorch_amd._lib import check, lib
+    g = torch.Generator().manual_seed(n)
+    M = torch.tril(torch.randn(ld, ld, generator=g, dtype=torch.float64))
+    x = torch.randn(ld, generator=g, dtype=torch.float64)
+    Mn = M.clone()
+    Mn[torch.triu(torch.ones(ld, ld, dtype=torch.bool), 1)] = float("nan")
+    we = ctypes.c_int64()
+    check(lib().bo_gemv_lt_work(n, ctypes.byref(we)), "gemv_lt_work")
+    work = torch.empty(we.value, dtype=torch.float64, device=DEV)
+    y = torch.empty(n, dtype=torch.float64, device=DEV)
+    Md, xd = Mn.to(DEV), x.to(DEV)
+    check(lib().bo_gemv_lt(kernels._p(Md), ld, n, kernels._p(xd), 0.25, kernels._p(y),
+                           kernels._p(work), kernels._stream(y.device)), "gemv_lt")
+    ref = M[:n, :n].T @ (x[:n] - 0.25)
+    torch.testing.assert_close(y.cpu(), ref, rtol=1e-12, atol=1e-12)

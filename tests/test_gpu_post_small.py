@@ -74,7 +74,7 @@ def test_small_kernel_partials_match_dense_algebra():
     P = ctypes.c_void_p
     st = torch.cuda.current_stream().cuda_stream
     check(lib().bo_post_small(P(Kd.data_ptr()), B, q, n, P(Ud.data_ptr()), np_, P(bd.data_ptr()),
-                              P(Sp.data_ptr()), P(mp.data_ptr()), P(st)), "post_small")
+                              P(Sp.data_ptr()), P(mp.data_ptr()), None, P(st)), "post_small")
     torch.cuda.synchronize()
     R = K[:, :rows].T @ U            # rows x np
     S = Sp.sum(0).cpu()[: rows // 16]
