@@ -597,6 +597,44 @@ def time_cholesky(Xtr, dev, reps=10, shapes=((3, 2048), (4, 4096), (8, 4096))):
     out = {"n": n, "ms": ms, "flops": fl, "tflops": fl / (ms * 1e-3) / 1e12,
            "frac_of_spec": fl / (ms * 1e-3) / 1e12 / 78.6,
            "note": "factor + inverse, one persistent task-DAG launch, input in HBM"}
+    # the MLL closure's launch: factor + inverse + A^{-1} = L^{-T} L^{-1} (n^3/3
+    # more) in one DAG (bo_cholesky_inverse_ainv), against the two launches
+    # (DAG, then bo_ainv) it replaces
+    T = np_ // 64
+    work5 = torch.empty((16 + 5 * T * T + 1) // 2, dtype=torch.float64, device=dev)
+    Ai = torch.empty_like(base)
+    wk = ctypes.c_int64()
+    check(lib().bo_ainv_work(n, ctypes.byref(wk)), "ainv_work")
+    wa = torch.empty(max(1, wk.value), dtype=torch.float64, device=dev)
+    t_fold, t_two = [], []
+    for r in range(reps + 2):
+        for fold, acc in ((True, t_fold), (False, t_two)):
+            W.copy_(base)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            if fold:
+                check(lib().bo_cholesky_inverse_ainv(kernels._p(W), kernels._p(Linv), kernels._p(Ai),
+                                                     kernels._p(work5), np_, kernels._p(info),
+                                                     ctypes.c_void_p(st.cuda_stream)), "chol_ainv")
+            else:
+                check(lib().bo_cholesky_inverse(kernels._p(W), kernels._p(Linv), kernels._p(work),
+                                                np_, kernels._p(info), ctypes.c_void_p(st.cuda_stream)),
+                      "chol")
+                check(lib().bo_ainv(kernels._p(Linv), np_, n, kernels._p(Ai), kernels._p(wa),
+                                    ctypes.c_void_p(st.cuda_stream)), "ainv")
+            e1.record(st)
+            torch.cuda.synchronize(dev)
+            if r >= 2:
+                acc.append(e0.elapsed_time(e1))
+    t_fold.sort()
+    t_two.sort()
+    fl3 = fl + n ** 3 / 3.0
+    out["with_ainv"] = {"ms_one_launch": t_fold[len(t_fold) // 2],
+                        "ms_two_launches": t_two[len(t_two) // 2],
+                        "flops": fl3,
+                        "frac_of_spec_one_launch": fl3 / (t_fold[len(t_fold) // 2] * 1e-3) / 1e12 / 78.6,
+                        "note": "factor + inverse + A^-1 (the MLL closure's), one DAG launch vs "
+                                "the DAG then bo_ainv"}
     # batched: nb independent factor + inverse problems in one launch
     # (bo_cholesky_inverse_batched), the shapes of the path's multi-model fits
     # and caches: C4's ModelListGP(3) at n = 2048, multi-output models at C3's n

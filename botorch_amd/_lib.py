@@ -40,6 +40,8 @@ _SIGNATURES = {
                                  c_int, _P, c_int64, c_int64, _P, c_int64, c_int64, _P, c_int64,
                                  c_int64, c_int64, c_int, c_int, _P]),
     "bo_cholesky_inverse": (c_int, [_P, _P, _P, c_int64, _P, _P]),
+    "bo_cholesky_inverse_ainv": (c_int, [_P, _P, _P, _P, c_int64, _P, _P]),
+    "bo_chol_dag_tasks_ainv": (c_int, [c_int, _P, c_int]),
     "bo_cholesky_inverse_batched": (c_int, [_P, _P, _P, c_int, c_int64, _P, _P]),
     "bo_transpose": (c_int, [_P, _P, c_int64, c_int64, _P]),
     "bo_cholesky_jitter": (c_int, [_P, c_int64, _P, _P, _P, c_int, c_double, POINTER(c_double),

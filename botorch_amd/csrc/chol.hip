@@ -25,7 +25,7 @@
 #include "gemm.h"
 
 int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipStream_t st,
-                long long* trace = nullptr, int nb = 1);
+                long long* trace = nullptr, int nb = 1, double* Ainv = nullptr);
 
 namespace {
 
@@ -348,6 +348,16 @@ int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* 
   BO_CHECK_ARG(((uintptr_t)A & 15) == 0 && ((uintptr_t)Linv & 15) == 0,
                "bo_cholesky_inverse: buffers must be 16-B aligned");
   return bo_chol_dag(A, Linv, np, info, work, as_stream(stream));
+}
+
+int bo_cholesky_inverse_ainv(double* A, double* Linv, double* Ainv, double* work, int64_t np,
+                             int* info, void* stream) {
+  BO_CHECK_ARG(np > 0 && np % NBO == 0, "bo_cholesky_inverse_ainv: order %lld not a multiple of %d",
+               (long long)np, NBO);
+  BO_CHECK_ARG(Ainv && ((uintptr_t)A & 15) == 0 && ((uintptr_t)Linv & 15) == 0 &&
+                   ((uintptr_t)Ainv & 15) == 0,
+               "bo_cholesky_inverse_ainv: buffers must be 16-B aligned (and Ainv given)");
+  return bo_chol_dag(A, Linv, np, info, work, as_stream(stream), nullptr, 1, Ainv);
 }
 
 int bo_transpose(const double* A, double* B, int64_t n, int64_t ld, void* stream) {

@@ -23,6 +23,10 @@
 //   COLUPD(j, k, rows) A_ij -= L_ik L_jk^T               (step k update of column j)
 //   XSTEP(j, k, rows)  X_kj = -D_k acc_kj (k > j; X_jj = D_j), then
 //                      acc_ij += L_ik X_kj for the rows i > k  (right-looking trtri)
+//   AINV(kb, j, rows)  (optional, round 5: A^{-1} = X^T X for the MLL gradient)
+//                      Ainv_ij += sum_{K in [kb, kb + 3), K >= i} X_Ki^T X_Kj, i >= j,
+//                      in increasing K per tile (version flags), as soon as the
+//                      X rows K are final -- in the idle CUs of the chain-bound tail
 // Task order (host-built table): CRIT(0), CRIT(1), then per step k: TRSM(k,.),
 // the two COLUPD chunks CRIT(k+2) needs, CRIT(k+2), XSTEP(., k), the other
 // COLUPD chunks; finally the X_{T-1,j} finalisations.
@@ -55,7 +59,8 @@ constexpr int GB = 3;       // steps per batched column update (LDS: X0 + GB ope
 constexpr int CHB = 8;      // tile rows per batched task of a multi-matrix launch (one matrix: 4, build_tasks)
 constexpr long long SPIN_TIMEOUT = 200000000;  // wall-clock ticks (100 MHz): 2 s
 
-enum : int { T_CRIT = 0, T_TRSM = 1, T_COLUPD = 2, T_XSTEP = 3 };
+enum : int { T_CRIT = 0, T_TRSM = 1, T_COLUPD = 2, T_XSTEP = 3, T_AINV = 4 };
+constexpr int GA = 3;  // steps K per A^{-1} task (LDS: X0 + GA operand tiles)
 
 typedef unsigned int u32;
 typedef u32 v2u __attribute__((ext_vector_type(2)));
@@ -811,6 +816,61 @@ __device__ void potrf_trtri64_cols(const Ctx& c, double* S, double* D, double* r
   __syncthreads();
 }
 
+// ---- the diagonal step's two tile products, triangle-aware (round 5) -----------
+// CRIT(k)'s L_{k,k-1} = A_{k,k-1} D_{k-1}^T and A_kk -= L L^T sit on the
+// factorisation's chain.  As 32 x 32 quadrants per wave both ran the full
+// 64-deep product on every quadrant (64 MFMAs per wave each).  D_{k-1} is lower
+// triangular, so column block C of L needs only k < 16 (C + 1): wave w takes
+// the 16 rows 16 w .. 16 w + 15 of L, 4 + 8 + 12 + 16 = 40 MFMAs, the same for
+// every wave.  Only the 10 lower 16 x 16 blocks of A_kk are updated (the
+// column-owner factor never reads above the diagonal), at most 3 per wave:
+// 48 MFMAs.  Operands are read 16 B at a time as in acc_mma_nt (lane group kq
+// takes k = 8 s + 2 kq and 8 s + 2 kq + 1 on both operands).
+__device__ __forceinline__ void crit_trsm(const Ctx& c, v4d (&t)[4], const double* SA,
+                                          const double* SD) {
+  const int r16 = c.lane & 15, kq = c.lane >> 4;
+  const double* pa = SA + (16 * c.wave + r16) * LP + 2 * kq;
+#pragma unroll
+  for (int C = 0; C < 4; ++C) t[C] = v4d_zero();
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const double2 a = *reinterpret_cast<const double2*>(pa + 8 * s);
+#pragma unroll
+    for (int C = 0; C < 4; ++C) {
+      if (s < 2 * (C + 1)) {
+        const double2 b = *reinterpret_cast<const double2*>(SD + (16 * C + r16) * LP + 8 * s + 2 * kq);
+        t[C] = mfma_f64(a.x, b.x, t[C]);
+        t[C] = mfma_f64(a.y, b.y, t[C]);
+      }
+    }
+  }
+}
+
+// The lower blocks (I, J) of A_kk per wave: {(0,0), (3,0), (3,3)}, {(1,0),
+// (1,1), (3,1)}, {(2,0), (2,1), (2,2)}, {(3,2)}.
+__device__ __forceinline__ int syrk_blocks(int wave, int (&I)[3], int (&J)[3]) {
+  if (wave == 0) { I[0] = 0; J[0] = 0; I[1] = 3; J[1] = 0; I[2] = 3; J[2] = 3; return 3; }
+  if (wave == 1) { I[0] = 1; J[0] = 0; I[1] = 1; J[1] = 1; I[2] = 3; J[2] = 1; return 3; }
+  if (wave == 2) { I[0] = 2; J[0] = 0; I[1] = 2; J[1] = 1; I[2] = 2; J[2] = 2; return 3; }
+  I[0] = 3; J[0] = 2; I[1] = 3; J[1] = 2; I[2] = 3; J[2] = 2;
+  return 1;
+}
+
+// blk -= L_I L_J^T (16 x 16, 64-deep) from the L tile in LDS.
+__device__ __forceinline__ v4d syrk_block(const Ctx& c, v4d blk, const double* SL, int I, int J) {
+  const int r16 = c.lane & 15, kq = c.lane >> 4;
+  const double* pa = SL + (16 * I + r16) * LP + 2 * kq;
+  const double* pb = SL + (16 * J + r16) * LP + 2 * kq;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const double2 a = *reinterpret_cast<const double2*>(pa + 8 * s);
+    const double2 b = *reinterpret_cast<const double2*>(pb + 8 * s);
+    blk = mfma_f64(-a.x, b.x, blk);
+    blk = mfma_f64(-a.y, b.y, blk);
+  }
+  return blk;
+}
+
 // ---- the bulk tasks: a chunk of tile rows i in [i0, i1) ----------------------------
 // KIND 0 TRSM    X0 <- A_ik,                   acc  = X0 X1^T  -> A_ik = L_ik, fL[i][k] = 1
 // KIND 1 COLUPD  X0 <- L_ik (X1 if i == j),    acc  = A_ij - X0 X1^T -> A_ij, fA[i][j] = k + 1
@@ -818,7 +878,7 @@ __device__ void potrf_trtri64_cols(const Ctx& c, double* S, double* D, double* r
 // The next tile's operands are loaded into registers while this tile's MFMAs
 // run (when its inputs are already published; one poll by thread 0 decides).
 struct Flags {
-  u32 *fA, *fL, *fX, *fXd, *abortw;
+  u32 *fA, *fL, *fX, *fXd, *fAi, *abortw;
   int T;
   __device__ __forceinline__ u32* at(u32* a, int i, int j) const { return a + i * T + j; }
 };
@@ -1180,6 +1240,42 @@ __device__ bool batched_update2(const Ctx& c, const Flags& f, int kb, int nk, in
   return true;
 }
 
+// A^{-1} tiles (KIND 3 of the batched updates): Ainv_ij += sum_{K in [kb, ke),
+// K >= i} X_Ki^T X_Kj for the rows i of the chunk (i >= j), the X_Kj^T of the
+// batch resident in LDS (XB[g]).  acc_mma_nt forms SA SB^T, so both operands
+// sit transposed in LDS (tile_to_lds_t).  Row i's first contribution (K = i)
+// starts from zero, so A^{-1} needs no clearing; fAi[i][j] counts the
+// contributions applied (ke - i after this task).  X_Ki is final once X_{ke-1,
+// i} is (each X_Ki is formed from the X_mi, m < K), so one flag per operand
+// column: fXd[ke-1][i], or fL[i][i] when ke - 1 == i (X_ii = D_i).
+__device__ bool ainv_update(const Ctx& c, const Flags& f, int kb, int nk, int j, int i0, int i1,
+                            double* X0, double* XB0, double* XB1, double* XB2, rsrc_t rAi,
+                            int* s_ok, long long* wsum) {
+  auto XB = [&](int g) { return g == 0 ? XB0 : (g == 1 ? XB1 : XB2); };
+  const int ke = kb + nk;
+  Acc acc;
+  for (int i = i0; i < i1; ++i) {
+    const int g0 = i > kb ? i - kb : 0;  // K = kb + g >= i
+    const u32 v0 = (u32)(kb + g0 - i);
+    const u32* xd = (ke - 1 == i) ? f.at(f.fL, i, i) : f.at(f.fXd, ke - 1, i);
+    if (!wait2(c, xd, 1u, f.at(f.fAi, i, j), v0, f.abortw, s_ok, wsum)) return false;
+    if (v0 == 0) acc_zero(acc);
+    else acc_load(c, acc, rAi, i, j);
+    for (int g = g0; g < nk; ++g) {
+      const bool own = i != j;
+      if (own) {
+        tile_to_lds_t(c, c.rI, kb + g, i, X0);  // X_Ki^T
+        __syncthreads();
+      }
+      acc_mma_nt(c, acc, own ? X0 : XB(g), XB(g), 1.0);
+      __syncthreads();  // X0 free for the next operand
+    }
+    acc_store(c, acc, rAi, i, j);
+    publish(c, f.at(f.fAi, i, j), (u32)(ke - i));
+  }
+  return true;
+}
+
 // nb > 1: nb independent matrices (A + m * np^2, Linv + m * np^2, info[m], flag
 // block m) share the launch; each task names its matrix in bits 9-15 of x, and
 // the queue interleaves the matrices' own queues, so one matrix's diagonal
@@ -1189,7 +1285,7 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
                                                        int ntasks, u32* __restrict__ flags,
                                                        int* __restrict__ info,
                                                        long long* __restrict__ trace, int nb,
-                                                       int pf2) {
+                                                       int pf2, double* __restrict__ Ainv) {
   __shared__ __attribute__((aligned(16))) double X0[TB * LP];
   __shared__ __attribute__((aligned(16))) double X1[TB * LP];
   __shared__ __attribute__((aligned(16))) double X2[TB * LP];  // batched update operands
@@ -1214,14 +1310,16 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
   c.rI = make_rsrc(Linv, bytes);
   u32* head = flags;
   u32* abortw = flags + 1;
-  const int fstride = 4 * T * T;  // flag words per matrix
+  const int fstride = (Ainv ? 5 : 4) * T * T;  // flag words per matrix
   u32* fA = flags + NFLAG0;
   u32* fL = fA + T * T;
   u32* fX = fL + T * T;
   u32* fXd = fX + T * T;
+  const rsrc_t rAi = make_rsrc(Ainv ? Ainv : A, bytes);
 #define F(arr, i, j) (arr + (i) * T + (j))
   Flags fl;
-  fl.fA = fA; fl.fL = fL; fl.fX = fX; fl.fXd = fXd; fl.abortw = abortw; fl.T = T;
+  fl.fA = fA; fl.fL = fL; fl.fX = fX; fl.fXd = fXd; fl.fAi = fXd + T * T;
+  fl.abortw = abortw; fl.T = T;
   int cur = 0;          // matrix of the buffer resources / flags above
   int* minfo = info;
 
@@ -1243,7 +1341,7 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
       fL = fA + T * T;
       fX = fL + T * T;
       fXd = fX + T * T;
-      fl.fA = fA; fl.fL = fL; fl.fX = fX; fl.fXd = fXd;
+      fl.fA = fA; fl.fL = fL; fl.fX = fX; fl.fXd = fXd; fl.fAi = fXd + T * T;
       minfo = info + mid;
     }
     long long wsum = 0;
@@ -1253,44 +1351,67 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
     const int k = tk.y, j = tk.z, i0 = tk.w & 0xffff, i1 = tk.w >> 16;
     bool ok = true;
     if (type == T_CRIT) {
+      // roles: the factor's input S = X1 (free once the TRSM has read D_{k-1}),
+      // its inverse D = X0 (free once the A_kk update has read L_{k,k-1})
       if (k > 0) {
         // the bulk's inputs (A_{k,k-1}, A_kk at version k-1) are usually ready
         // before D_{k-1}: load them while the previous diagonal step runs, so
         // only D_{k-1}'s load, two tile products and the L_{k,k-1} hand-off
         // stay on the chain
-        Acc akk;
+        int bI[3], bJ[3];
+        const int nbk = syrk_blocks(c.wave, bI, bJ);
+        v4d akk[3];
         ok = wait2(c, F(fA, k, k - 1), (u32)(k - 1), F(fA, k, k), (u32)(k - 1), abortw, &s_ok, &wsum);
         if (ok) {
           tile_to_lds(c, c.rA, k, k - 1, X0);
-          acc_load(c, akk, c.rA, k, k);
+#pragma unroll
+          for (int b = 0; b < 3; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              akk[b][r] = b < nbk ? ld8(c.rA, toff(c, k, k, 16 * bI[b] + mfma_row(c.lane, r),
+                                                 16 * bJ[b] + mfma_col(c.lane)))
+                                  : 0.0;
           ok = wait2(c, F(fL, k - 1, k - 1), 1u, F(fL, k - 1, k - 1), 1u, abortw, &s_ok, &wsum);
         }
         if (ok) {
           tile_to_lds(c, c.rI, k - 1, k - 1, X1);
           __syncthreads();
-          acc_zero(acc);
-          acc_mma_nt(c, acc, X0, X1, 1.0);  // L_{k,k-1} = A_{k,k-1} D_{k-1}^T
-          __syncthreads();                  // every wave's reads of X0 done
-          acc_to_lds(c, acc, X0);
-          acc_store(c, acc, c.rA, k, k - 1);  // in flight under the update below
-          __syncthreads();                    // X0 = L_{k,k-1} complete
-          acc_mma_nt(c, akk, X0, X0, -1.0);   // A_kk -= L L^T (step k - 1)
-          publish(c, F(fL, k, k - 1), 1u);    // (its barrier also frees X0)
-          acc_to_lds(c, akk, X0);
+          v4d tl[4];
+          crit_trsm(c, tl, X0, X1);  // rows 16 w.. of L_{k,k-1} = A_{k,k-1} D_{k-1}^T
+          // the wave's own rows: X0 <- L (only this wave read them), and to A
+#pragma unroll
+          for (int C = 0; C < 4; ++C)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * c.wave + mfma_row(c.lane, r), col = 16 * C + mfma_col(c.lane);
+              X0[row * LP + col] = tl[C][r];
+              st8(c.rA, toff(c, k, k - 1, row, col), tl[C][r]);  // in flight under the update
+            }
+          __syncthreads();  // X0 = L_{k,k-1} complete; every wave's reads of X1 done
+#pragma unroll
+          for (int b = 0; b < 3; ++b)
+            if (b < nbk) akk[b] = syrk_block(c, akk[b], X0, bI[b], bJ[b]);  // A_kk -= L L^T
+#pragma unroll
+          for (int b = 0; b < 3; ++b)
+            if (b < nbk)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                X1[(16 * bI[b] + mfma_row(c.lane, r)) * LP + 16 * bJ[b] + mfma_col(c.lane)] = akk[b][r];
+          publish(c, F(fL, k, k - 1), 1u);  // (its barrier also orders the X1 writes)
         }
       } else {
-        tile_to_lds(c, c.rA, 0, 0, X0);
+        tile_to_lds(c, c.rA, 0, 0, X1);
       }
       if (ok) {
         __syncthreads();
         long long* ct = trace ? trace + 4 * ntasks + 8 * k : nullptr;
         if (ct && c.tid == 0) ct[0] = wall_clock64();
-        potrf_trtri64_cols<0>(c, X0, X1, rinv, minfo, k * TB, X2, X3, (lds_cnt_t*)&s_cnt, s_fail,
+        potrf_trtri64_cols<0>(c, X1, X0, rinv, minfo, k * TB, X2, X3, (lds_cnt_t*)&s_cnt, s_fail,
                               (lds_cnt_t*)s_fl, ct);
         if (ct && c.tid == 0) ct[1] = wall_clock64();
         if (ct && c.tid == 0) ct[2] = wall_clock64();
-        lds_to_tile(c, X0, c.rA, k, k);
-        lds_to_tile(c, X1, c.rI, k, k);
+        lds_to_tile(c, X1, c.rA, k, k);
+        lds_to_tile(c, X0, c.rI, k, k);
         publish(c, F(fL, k, k), 1u);
         if (ct && c.tid == 0) ct[3] = wall_clock64();
       }
@@ -1311,6 +1432,16 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
       ok = wait2(c, F(fL, j, k), 1u, F(fL, j, k), 1u, abortw, &s_ok, &wsum);
       if (ok) tile_to_lds(c, c.rA, j, k, X1);  // L_jk
       if (ok) ok = row_loop<1>(c, fl, k, j, i0, i1, X0, X1, &s_ok, s_rdy, &wsum, ph);
+    } else if (type == T_AINV) {
+      const int kl = k + nk - 1;  // X_{k..kl, j} final once X_{kl, j} is
+      if (kl == j) ok = wait2(c, F(fL, j, j), 1u, F(fL, j, j), 1u, abortw, &s_ok, &wsum);
+      else ok = wait2(c, F(fXd, kl, j), 1u, F(fXd, kl, j), 1u, abortw, &s_ok, &wsum);
+      if (ok) {
+        for (int g = j > k ? j - k : 0; g < nk; ++g)  // X_Kj transposed (K >= j: the rest is 0)
+          tile_to_lds_t(c, c.rI, k + g, j, g == 0 ? X1 : (g == 1 ? X2 : X3));
+        __syncthreads();
+        ok = ainv_update(c, fl, k, nk, j, i0, i1, X0, X1, X2, X3, rAi, &s_ok, &wsum);
+      }
     } else if (nk > 1) {  // T_XSTEP, batched: the far rows of steps k .. k + nk - 1
       const int kl = k + nk - 1;  // X_{k..kl, j} final once X_{kl, j} is
       if (kl == j) ok = wait2(c, F(fL, j, j), 1u, F(fL, j, j), 1u, abortw, &s_ok, &wsum);
@@ -1396,7 +1527,7 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
   auto tix = [T](int i, int j) { return (size_t)i * T + j; };
   std::vector<int> prodL((size_t)T * T, -1), prodXd((size_t)T * T, -1);
   // version-indexed producers: A(i,j) after v updates (v = 1..j), X(i,j) after v
-  std::vector<std::vector<int>> prodA((size_t)T * T), prodX((size_t)T * T);
+  std::vector<std::vector<int>> prodA((size_t)T * T), prodX((size_t)T * T), prodAi((size_t)T * T);
   for (int t = 0; t < n; ++t) {
     const int type = v[t].x & 0xff, fin = (v[t].x >> 8) & 0xff, k = v[t].y, j = v[t].z;
     const int nk = std::max(1, v[t].x >> 16);
@@ -1411,6 +1542,12 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
         auto& pa = prodA[tix(i, j)];
         if ((int)pa.size() < k + nk + 1) pa.resize(k + nk + 1, -1);
         pa[k + nk] = t;
+      }
+    } else if (type == T_AINV) {
+      for (int i = i0; i < i1; ++i) {  // version = contributions applied = ke - i
+        auto& pv = prodAi[tix(i, j)];
+        if ((int)pv.size() < k + nk - i + 1) pv.resize(k + nk - i + 1, -1);
+        pv[k + nk - i] = t;
       }
     } else {
       if (fin && k > j) prodXd[tix(k, j)] = t;
@@ -1472,6 +1609,18 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
         d.push_back(verA(i, j, k));
       }
       dur[t] = 2.0 + (nk > 1 ? 2.6 * nk + 1.0 : 3.6) * rows;
+    } else if (type == T_AINV) {
+      const int kl = k + nk - 1;
+      d.push_back(kl == j ? prodL[tix(j, j)] : prodXd[tix(kl, j)]);
+      double steps = 0.0;
+      for (int i = i0; i < i1; ++i) {
+        d.push_back(kl == i ? prodL[tix(i, i)] : prodXd[tix(kl, i)]);
+        const int v0 = std::max(k, i) - i;
+        const auto& pv = prodAi[tix(i, j)];
+        if (v0 > 0) d.push_back(v0 < (int)pv.size() ? pv[v0] : -1);
+        steps += k + nk - std::max(k, i);
+      }
+      dur[t] = 2.0 + 2.6 * steps + 1.0 * rows;
     } else if (nk > 1) {
       const int kl = k + nk - 1;
       d.push_back(kl == j ? prodL[tix(j, j)] : prodXd[tix(kl, j)]);
@@ -1520,7 +1669,7 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
 // 1.709-1.718 against 1.721-1.744 ms for one matrix, but 3 x 2048 0.90 against
 // 0.85 ms (ab_chb.log); ch 2 then 1.650-1.684 against 1.684-1.733 ms with 4
 // (1: 1.70-1.72, 3: 1.70-1.72; ab_ch23.log, ab_ch21.log): one matrix takes 2 / 4
-std::vector<int4> build_tasks(int T, int ch = 2, int chb = 4) {
+std::vector<int4> build_tasks(int T, int ch = 2, int chb = 4, bool ainv = false) {
   std::vector<int4> v;
   auto crit = [&](int k) { v.push_back(make_int4(T_CRIT, k, k, 0)); };
   crit(0);
@@ -1569,6 +1718,20 @@ std::vector<int4> build_tasks(int T, int ch = 2, int chb = 4) {
     }
   }
   for (int j = 0; j + 1 < T; ++j) v.push_back(make_int4(T_XSTEP | 256, T - 1, j, 0));
+  if (ainv) {
+    // A^{-1} = X^T X: per aligned batch [kb, ke) of GA rows K of X (final in
+    // K order), the tiles (i, j), j <= i <= ke - 1, take their contributions
+    // K >= i of the batch; batches in K order, so every tile's contributions
+    // arrive in increasing K (a fixed summation order)
+    for (int kb = 0; kb < T; kb += GA) {
+      const int ke = std::min(kb + GA, T);
+      for (int j = 0; j < ke; ++j) {
+        const size_t first = v.size();
+        push_rows(v, T_AINV, kb, j, j, ke, false, chb);
+        for (size_t t = first; t < v.size(); ++t) v[t].x |= (ke - kb) << 16;
+      }
+    }
+  }
   return priority_order(v, T);
 }
 
@@ -1580,7 +1743,7 @@ std::vector<int4> build_tasks(int T, int ch = 2, int chb = 4) {
 // (merge key: own position + offset, ties to the lower matrix), so one
 // matrix's chain-bound tail overlaps the next one's update-heavy opening
 // instead of all matrices opening together.
-std::vector<int4> build_tasks_batched(int T, int nb) {
+std::vector<int4> build_tasks_batched(int T, int nb, bool ainv = false) {
   // one matrix, or batches of small ones (n <= 2048: C4's 3 x 2048 0.855-0.867
   // -> 0.797-0.805 ms), take 2 / 4 rows; batches of n = 4096 keep 8 / 8 (with
   // 2 / 4: 4 x 4096 5.38 -> 5.69 ms; profiles/r03/cholesky/ab_ch_batched_small.log)
@@ -1597,7 +1760,7 @@ std::vector<int4> build_tasks_batched(int T, int nb) {
     return v >= 1 && v <= 16 ? v : 4;
   }();
   const std::vector<int4> one =
-      (nb == 1 || T <= 32) ? build_tasks(T, ch1, chb1) : build_tasks(T, CH, CHB);
+      (nb == 1 || T <= 32) ? build_tasks(T, ch1, chb1, ainv) : build_tasks(T, CH, CHB, ainv);
   if (nb == 1) return one;
   double stagger = 0.0;
   if (const char* e = getenv("BO_CHOL_BATCH_STAGGER")) {  // finite values only (sort keys)
@@ -1624,15 +1787,15 @@ std::vector<int4> build_tasks_batched(int T, int nb) {
 }
 
 std::mutex g_tab_mu;
-std::map<std::tuple<int, int, int>, DagTable> g_tabs;  // (device, T, nb) -> table
+std::map<std::tuple<int, int, int, int>, DagTable> g_tabs;  // (device, T, nb, ainv) -> table
 
-int dag_table(int T, DagTable** out, int nb = 1) {
+int dag_table(int T, DagTable** out, int nb = 1, bool ainv = false) {
   int dev = 0;
   BO_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_tab_mu);
-  DagTable& tb = g_tabs[std::make_tuple(dev, T, nb)];
+  DagTable& tb = g_tabs[std::make_tuple(dev, T, nb, ainv ? 1 : 0)];
   if (!tb.dev) {
-    const std::vector<int4> v = build_tasks_batched(T, nb);
+    const std::vector<int4> v = build_tasks_batched(T, nb, ainv);
     int4* d = nullptr;
     BO_HIP(hipMalloc(&d, sizeof(int4) * v.size()));
     BO_HIP(hipMemcpy(d, v.data(), sizeof(int4) * v.size(), hipMemcpyHostToDevice));
@@ -1650,18 +1813,20 @@ int dag_table(int T, DagTable** out, int nb = 1) {
 // (16 + 4 nb (np/64)^2) * 4 bytes of scratch for the counters; info[m] as in
 // bo_cholesky_inverse (-1: the task DAG timed out).
 int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipStream_t st,
-                long long* trace, int nb) {
+                long long* trace, int nb, double* Ainv) {
   BO_CHECK_ARG(np > 0 && np % TB == 0 && np <= 16384, "bo_chol_dag: order %lld", (long long)np);
   BO_CHECK_ARG(nb >= 1 && nb <= 128 && (trace == nullptr || nb == 1),
                "bo_chol_dag: batch %d (1..128; traced launches single)", nb);
+  BO_CHECK_ARG(Ainv == nullptr || nb == 1, "bo_chol_dag: A^{-1} tasks take one matrix");
   const int T = (int)(np / TB);
   DagTable* tb = nullptr;
-  int s = dag_table(T, &tb, nb);
+  int s = dag_table(T, &tb, nb, Ainv != nullptr);
   if (s) return s;
   int dev = 0, cus = 0;
   BO_HIP(hipGetDevice(&dev));
   BO_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const size_t fbytes = ((size_t)(NFLAG0 + (size_t)nb * 4 * T * T) * 4 + 15) / 16 * 16;
+  const size_t fbytes =
+      ((size_t)(NFLAG0 + (size_t)nb * (Ainv ? 5 : 4) * T * T) * 4 + 15) / 16 * 16;
   BO_HIP(hipMemsetAsync(work, 0, fbytes, st));
   BO_HIP(hipMemsetAsync(info, 0, sizeof(int) * nb, st));
   BO_HIP(hipMemsetAsync(Linv, 0, sizeof(double) * np * np * nb, st));
@@ -1674,7 +1839,7 @@ int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipS
     return (e && e[0] == '0') ? 0 : 1;
   }();
   chol_dag_kernel<<<grid, 256, 0, st>>>(A, Linv, (int)np, T, tb->dev, tb->n, (u32*)work, info,
-                                          trace, nb, pf2);
+                                          trace, nb, pf2, Ainv);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
@@ -1756,6 +1921,22 @@ extern "C" int bo_probe_diag16(long long* out, double* sink, void* stream) {
 // receives 4 ints per task (type | fin << 8 | nk << 16, k, j, i0 | i1 << 16) in queue
 // order, up to cap tasks; returns the task count (tests/test_chol_dag_cpu.py
 // checks that every dependency precedes its task).
+static int dag_tasks_out(const std::vector<int4>& v, int* out, int cap) {
+  const int n = (int)v.size();
+  for (int t = 0; t < n && t < cap; ++t) {
+    out[4 * t] = v[t].x;
+    out[4 * t + 1] = v[t].y;
+    out[4 * t + 2] = v[t].z;
+    out[4 * t + 3] = v[t].w;
+  }
+  return n;
+}
+
+extern "C" int bo_chol_dag_tasks_ainv(int T, int* out, int cap) {
+  if (T < 1) return 0;
+  return dag_tasks_out(build_tasks(T, 2, 4, true), out, cap);
+}
+
 extern "C" int bo_chol_dag_tasks(int T, int* out, int cap) {
   if (T < 1) return 0;
   const std::vector<int4> v = build_tasks(T);

@@ -200,7 +200,7 @@ def mll_terms(Xt: torch.Tensor, y: torch.Tensor, ls_t: torch.Tensor, noise, cons
     def _sums(cache, info):
         # A^{-1} = L^{-T} L^{-1}, lower tiles (n^3/3 flops on the posterior
         # kernel's MFMA tiles, stream-K over the unequal k-ranges)
-        Ainv = kernels.ainv(cache)
+        Ainv = cache.Ainv if cache.Ainv is not None else kernels.ainv(cache)
         st = kernels._stream(dev)
         part = torch.empty(n, d + 5, dtype=torch.float64, device=dev)
         check(lib().bo_mll_terms(kind, kernels._p(Xt.contiguous()), n, d, kernels._p(ls_t), os_,

@@ -41,6 +41,9 @@ CHOLESKY_JITTER_F64 = 1e-8  # [G] linear_operator.settings.cholesky_jitter (doub
 # Optional callable(tag) invoked around the bo_post_partials launch (bench.py
 # records HIP events on the current stream through it).
 TIMING_HOOK = None
+# the MLL closure's A^{-1} inside the factorisation's launch (round 5); "0": the
+# separate bo_ainv pass
+AINV_IN_DAG = os.environ.get("BO_MLL_AINV_DAG", "1") != "0"
 
 
 # Tensors whose pointers were handed to the C ABI most recently.  A call such as
@@ -181,6 +184,9 @@ class GPCache:
     beta: torch.Tensor         # n  = L^{-1} (y - c)
     alpha: torch.Tensor        # n  = (K + s2 I)^{-1} (y - c)  (mean_cache)
     jitter: float
+    # A^{-1} lower 64 x 64 tiles when the factorisation's launch formed it (the
+    # MLL closure, bo_cholesky_inverse_ainv), else None (kernels.ainv forms it)
+    Ainv: Optional[torch.Tensor] = None
 
 
 def build_gp_cache(Xt, y, lengthscale, noise, constant, kind=_lib.RBF, outputscale=1.0,
@@ -273,12 +279,15 @@ def build_gp_cache_optimistic(Xt, y, lengthscale, noise: float, constant: float,
     f64 = dict(dtype=torch.float64, device=dev)
     L = torch.empty(np_, np_, **f64)
     Linv = torch.empty(np_, np_, **f64)
-    # the DAG's tile counters (4 (np/64)^2 + 16 ints) and alpha's chunk partials;
+    # A^{-1} in the factorisation's own launch (its tile products fill the
+    # chain-bound tail; BO_MLL_AINV_DAG=0: the separate bo_ainv pass instead)
+    Ainv = torch.empty(np_, np_, **f64) if AINV_IN_DAG else None
+    # the DAG's tile counters (5 (np/64)^2 + 16 ints) and alpha's chunk partials;
     # the MLL closure forms no U = L^{-T} (alpha from L^{-1}'s columns)
     T = np_ // 64
     we = ctypes.c_int64()
     check(lib().bo_gemv_lt_work(n, ctypes.byref(we)), "gemv_lt_work")
-    work = torch.empty(max((16 + 4 * T * T + 1) // 2, we.value), **f64)
+    work = torch.empty(max((16 + 5 * T * T + 1) // 2, we.value), **f64)
     beta = torch.empty(n, **f64)
     alpha = torch.empty(n, **f64)
     info = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -286,8 +295,12 @@ def build_gp_cache_optimistic(Xt, y, lengthscale, noise: float, constant: float,
     st = _stream(dev)
     check(lib().bo_covar_matrix(kind, _p(Xt), n, _p(Xt), n, d, _p(ls), float(outputscale),
                                 float(noise), 1, _p(L), np_, np_, np_, st), "covar_matrix")
-    check(lib().bo_cholesky_inverse(_p(L), _p(Linv), _p(work), np_, _p(info), st),
-          "cholesky_inverse")
+    if Ainv is not None:
+        check(lib().bo_cholesky_inverse_ainv(_p(L), _p(Linv), _p(Ainv), _p(work), np_, _p(info),
+                                             st), "cholesky_inverse_ainv")
+    else:
+        check(lib().bo_cholesky_inverse(_p(L), _p(Linv), _p(work), np_, _p(info), st),
+              "cholesky_inverse")
     check(lib().bo_gemv_tri(_p(Linv), np_, n, _p(y), float(constant), _p(beta), 1, st),
           "gemv_tri")
     check(lib().bo_gemv_lt(_p(Linv), np_, n, _p(beta), 0.0, _p(alpha), _p(work), st), "gemv_lt")
@@ -297,7 +310,7 @@ def build_gp_cache_optimistic(Xt, y, lengthscale, noise: float, constant: float,
         check(lib().bo_scale_inputs(_p(Xt), n, d, _p(ls), ctypes.c_void_p(0), DP, _p(Xs), st),
               "scale_inputs")
     cache = GPCache(kind, n, d, np_, Xt, Xs, ls, float(outputscale), float(noise),
-                    float(constant), L, Linv, U, beta, alpha, 0.0)
+                    float(constant), L, Linv, U, beta, alpha, 0.0, Ainv)
     return cache, info
 
 

@@ -82,6 +82,8 @@ int bo_probe_mfma_f64_rate(int blocks, int iters, double* out, void* stream);
  * device work): 4 ints per task (type | fin << 8, k, j, i0 | i1 << 16) into
  * out (capacity cap tasks); returns the task count. */
 int bo_chol_dag_tasks(int T, int* out, int cap);
+/* The same queue with the A^{-1} tasks (bo_cholesky_inverse_ainv). */
+int bo_chol_dag_tasks_ainv(int T, int* out, int cap);
 
 /* Batched C = alpha op(A) op(B) + beta C on the fp64 matrix cores (strides sA,
  * sB, sC between batch members).  Building block of the Cholesky/inverse and
@@ -124,6 +126,15 @@ int bo_covar_batched(int kind, const double* X1, int64_t s1o, int64_t s1i, int n
  * leading minor (torch.linalg.cholesky_ex convention). */
 int bo_cholesky_inverse(double* A, double* Linv, double* work, int64_t np, int* info,
                         void* stream);
+/* bo_cholesky_inverse plus A^{-1} = L^{-T} L^{-1} (the lower 64 x 64 tiles,
+ * diagonal tiles whole) in the SAME persistent launch (round 5): the MLL
+ * gradient's tr(A^{-1} dK/dtheta) (botorch/optim/closures/model_closures.py:
+ * 171-184 -> [G] ExactMarginalLogLikelihood's backward).  Its tile products run
+ * as soon as the rows of L^{-1} they read are final, in the CUs the
+ * factorisation's chain-bound tail leaves idle.  work >= (16 + 5 (np/64)^2)
+ * 4-byte counters. */
+int bo_cholesky_inverse_ainv(double* A, double* Linv, double* Ainv, double* work, int64_t np,
+                             int* info, void* stream);
 
 /* nb independent bo_cholesky_inverse problems in ONE persistent launch: A and
  * Linv hold nb np x np matrices back to back, info nb device ints, work >=

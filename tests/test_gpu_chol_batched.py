@@ -117,8 +117,16 @@ def test_optimistic_mll_closure_matches_the_ladder_path(singular):
         ref_cache = kernels.build_gp_cache(Xd, yd, ls, noise, 0.1, outputscale=1.3)
     assert (ref_cache.jitter > 0) == singular
     ll2, grad2 = mll_terms(Xd, yd, ls, noise, 0.1, 1.3, 0, cache=ref_cache)
-    assert ll == ll2
-    np.testing.assert_array_equal(grad, grad2)
+    if singular or not kernels.AINV_IN_DAG:
+        # both from the ladder's caches: the same bits
+        assert ll == ll2
+        np.testing.assert_array_equal(grad, grad2)
+    else:
+        # the optimistic closure's A^{-1} comes from the factorisation's launch
+        # (64-tile sums in K order), the ladder path's from bo_ainv (128-tile
+        # stream-K): the same sums in another order
+        assert abs(ll - ll2) <= 1e-10 * abs(ll2)
+        np.testing.assert_allclose(grad, grad2, rtol=1e-9, atol=1e-9)
 
 
 class _nullcontext:
