@@ -984,13 +984,29 @@ def verify_other(w, acqf, Xd, r0, Xc_local, k=4):
         lo, hi = w.cells
         ref = oacq.qehvi(orcs, Xc_local[idx], base_samples_multi_output(w.S, w.q, 3, 0), lo, hi)
     ok = bool(torch.allclose(got, ref, rtol=1e-7, atol=1e-12))
+    extra = None
+    if ok and not bool((ref > 0).any()) and w.acq == "qnei":
+        # the Sobol candidates of the timed batch improve on no baseline sample
+        # at C3's hyperparameters (every value exactly 0 on both sides): check
+        # the same acquisition also at 4 t-batches around the kept baseline
+        # point, where it is positive
+        g = torch.Generator().manual_seed(7)
+        Xb = acqf.X_baseline.cpu()[:1]
+        Xn = (Xb.unsqueeze(0) + 0.05 * torch.randn(4, w.q, D, generator=g, dtype=torch.float64)
+              ).clamp(0, 1)
+        with torch.no_grad():
+            gn = acqf(Xn.to(Xd.device)).cpu()
+        rn = oacq.QNEIOracle(orc, acqf.X_baseline.cpu(), w.S, seed=0)(Xn)
+        ok = bool(torch.allclose(gn, rn, rtol=1e-7, atol=1e-12))
+        got, ref = torch.cat([got, gn]), torch.cat([ref, rn])
+        extra = "4 t-batches around the baseline point (the timed ones are all exactly 0)"
     if not ok or not bool((ref > 0).any()):
         raise SystemExit(f"bench: the timed {w.name} forward disagrees with the oracle (or is "
                          f"degenerate): {got} vs {ref}")
     pos = ref > 0
     return {"t_batches": [int(r0 + i) for i in idx], "nonzero": int(pos.sum()),
             "max_rel_err_nonzero": ((got - ref).abs()[pos] / ref[pos]).max().item(),
-            "rtol": 1e-7, "atol": 1e-12}
+            "rtol": 1e-7, "atol": 1e-12, "extra_points": extra}
 
 
 def cpu_baseline_other(w, acqf, budget_s=20.0):

@@ -1210,6 +1210,14 @@ int bo_post_small_plan(int64_t B, int q, int64_t n, int* nparts) {
     s = bo_post_split_plan(B, q, n, 0, &kc, &we);
     if (s) return s;
     if (kc == 0) return BO_OK;
+    // ... and only small: the 32-row units stream both operands from L2 / the
+    // MALL with no reuse across waves, so past ~5e8 MACs the stream-K 128-tile
+    // plan wins (forward ms per call, tools/time_small.py, small vs stream-K:
+    // n = 1024 q = 8 b = 64 0.041 vs 0.052; n = 2048 q = 8 b = 32 0.055 vs
+    // 0.063; n = 4096 q = 16 b = 1 0.095 vs 0.097; but n = 2048 q = 8 b = 128
+    // 0.135 vs 0.124, n = 4096 q = 16 b = 64 0.44 vs 0.35)
+    const double np_ = (double)nC * PC;
+    if ((double)B * Qp * np_ * np_ > 1.2e9) return BO_OK;
   }
   *nparts = (int)(ceil_div(n, PC) * PC / (2 * SMU));
   return BO_OK;

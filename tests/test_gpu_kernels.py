@@ -231,7 +231,7 @@ def test_post_partials_split_k(n, B, q, split):
     if split is None:
         assert kc == -1  # C2 geometry (32 tiles) and a rank's b = 64 share of C3: stream-K
     one = kernels.post_partials(c, Xc, store_R=True, split=0)
-    spl = kernels.post_partials(c, Xc, store_R=True, split=split)
+    spl = kernels.post_partials(c, Xc, store_R=True, split=split, small=False)
     # the split-k plan without the K*x^T buffer (kernel rows
     # evaluated between the MFMAs) -- the path taken above the KXT cap
     nok = kernels.post_partials(c, Xc, store_R=True, split=split, kxt=False)
@@ -241,6 +241,14 @@ def test_post_partials_split_k(n, B, q, split):
     for a, b in ((one.Spart, spl.Spart), (one.mpart, spl.mpart), (one.Rt, spl.Rt),
                  (one.Spart, nok.Spart), (one.mpart, nok.mpart), (one.Rt, nok.Rt)):
         torch.testing.assert_close(b, a, rtol=1e-11, atol=atol)
+    if split is None and kernels.small_plan(B, q, n) > 0:
+        # the library's choice here: the small-grid kernel (pair partials, R^T
+        # row-major) -- the same R^T, and the same sums over its partials
+        sml = kernels.post_partials(c, Xc, store_R=True)
+        assert sml.Spart.shape[0] == kernels.padded_order(n) // 64
+        torch.testing.assert_close(sml.Rt, one.Rt, rtol=1e-11, atol=atol)
+        torch.testing.assert_close(sml.Spart.sum(0), one.Spart.sum(0), rtol=1e-11, atol=atol)
+        torch.testing.assert_close(sml.mpart.sum(0), one.mpart.sum(0), rtol=1e-11, atol=atol)
     out = kernels.qmc_finalize(c, spl, _lib.QMC_POSTERIOR, orc.ymean.item(), orc.ystd.item())
     mean_r, cov_r = orc.posterior(Xc.cpu())
     torch.testing.assert_close(out["mean"].cpu(), mean_r, rtol=1e-4, atol=1e-8)

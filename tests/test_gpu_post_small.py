@@ -22,30 +22,57 @@ def _plan(B, q, n):
     return v.value
 
 
+def _route_128(acqf, m, X):
+    """The same qEI on the 128-tile route: the bo::post_partials op (its schema
+    keeps the 128-tile partials) + bo::qmc_finalize."""
+    from botorch_amd import _lib
+    c = m.prediction_cache()
+    ymean, ystd = m.outcome_stats()
+    q = X.shape[1]
+    Z = acqf._ensure_sampler().base_samples_2d(q, X.device)
+    Sp, mp, Xq, _ = torch.ops.bo.post_partials(X, c.Xt, c.Xt_scaled, c.U, c.beta, c.lengthscale,
+                                               int(c.kind), float(c.outputscale), False)
+    out = torch.ops.bo.qmc_finalize(Sp, mp, Xq, Z, None, X.shape[0], q, int(c.n), int(c.kind),
+                                    _lib.QMC_QEI, float(c.outputscale), float(c.constant),
+                                    float(ymean), float(ystd), float(acqf.best_f), True, 1.0, 1.0)
+    return out[0]
+
+
 @pytest.mark.parametrize("n,B,q,S", [(1024, 64, 8, 256),    # C2
                                      (1024, 1, 8, 256),     # one t-batch
                                      (300, 33, 5, 128),     # ragged n, odd q and b
-                                     (4096, 64, 16, 512)])  # a rank's C3 shard at W = 8
-def test_small_route_matches_gradient_route_and_oracle(n, B, q, S):
+                                     (4096, 1, 16, 512)])   # one C3-sized t-batch
+def test_small_route_matches_128_route_and_oracle(n, B, q, S):
     from botorch_amd.acquisition import qExpectedImprovement
     from botorch_amd.sampling import SobolQMCNormalSampler
     from oracle.acquisition import qei
     from oracle.sampling import draw_sobol_normal_samples
     from tests.test_gpu_acquisition import _setup
     X, Y, m, orc = _setup(n=n, ls=0.4, noise=1e-3)
-    if n == 1024 and B == 64:
-        assert _plan(B, q, n) == 1024 // 64  # C2 takes the small route
-    bf = float(Y.max()) - 0.3
+    assert _plan(B, q, n) == kernels_np(n) // 64  # these grids take the small route
+    bf = float(Y.mean())  # most t-batches improve on it: values and gradients are non-zero
     acqf = qExpectedImprovement(m, bf, sampler=SobolQMCNormalSampler(torch.Size([S]), seed=3))
     Xc = torch.rand(B, q, 6, dtype=torch.float64, generator=torch.Generator().manual_seed(B + q))
     with torch.no_grad():
-        v_fwd = acqf(Xc.to(DEV)).cpu()
+        v_small = acqf(Xc.to(DEV)).cpu()
+        v_128 = _route_128(acqf, m, Xc.to(DEV)).cpu()
+    torch.testing.assert_close(v_small, v_128, rtol=1e-12, atol=1e-15)
+    # the gradient path (R^T stored row-major by the small kernel)
     Xg = Xc.to(DEV).requires_grad_(True)
-    v_grad = acqf(Xg).detach().cpu()
-    torch.testing.assert_close(v_fwd, v_grad, rtol=1e-12, atol=1e-15)
+    v_grad = acqf(Xg)
+    (dx,) = torch.autograd.grad(v_grad.sum(), Xg)
+    assert torch.equal(v_grad.detach().cpu(), v_small)
     ref = qei(orc, Xc, draw_sobol_normal_samples(q, S, 3), bf)
     assert int((ref > 0).sum()) > 0
-    torch.testing.assert_close(v_fwd, ref, rtol=1e-7, atol=1e-12)
+    torch.testing.assert_close(v_small, ref, rtol=1e-7, atol=1e-12)
+    Xo = Xc.clone().requires_grad_(True)
+    (dref,) = torch.autograd.grad(qei(orc, Xo, draw_sobol_normal_samples(q, S, 3), bf).sum(), Xo)
+    torch.testing.assert_close(dx.cpu(), dref, rtol=1e-5, atol=1e-8)
+
+
+def kernels_np(n):
+    from botorch_amd import kernels
+    return kernels.padded_order(n)
 
 
 def test_small_kernel_partials_match_dense_algebra():

@@ -19,7 +19,8 @@ def main():
     dev = torch.device("cuda", 0)
     out = {"BO_POST_SMALL": os.environ.get("BO_POST_SMALL", "auto")}
     unit = torch.stack([torch.zeros(6), torch.ones(6)]).to(torch.float64)
-    for n, q, S, bs in ((1024, 8, 256, (1, 16, 64)), (4096, 16, 512, (1, 64, 128, 256))):
+    for n, q, S, bs in ((1024, 8, 256, (1, 16, 64)), (2048, 8, 128, (32, 128)),
+                       (2048, 16, 512, (64,)), (4096, 16, 512, (1, 64, 128, 256))):
         X = draw_sobol_samples(unit, n, 1, seed=0).squeeze(1)
         Y = Hartmann(negate=True)(X).unsqueeze(-1)
         m = SingleTaskGP(X.to(dev), Y.to(dev))
