@@ -280,7 +280,7 @@ def other_configs(dev, cpu=True):
     # the same forward (and forward + backward) captured once as a HIP graph and
     # replayed (botorch_amd.graphs; values bit-equal to the eager call)
     from botorch_amd.graphs import GraphedAcquisition
-    ga = GraphedAcquisition(acqf, Xd)
+    ga = GraphedAcquisition(acqf, Xd, share_input=True)
     tg = _gpu_time(lambda: ga(Xd), steps=200, warmup=20)
     Xg = Xd.clone().requires_grad_(True)
 
@@ -289,7 +289,7 @@ def other_configs(dev, cpu=True):
         torch.autograd.grad(v.sum(), Xg)
 
     tfb = _gpu_time(c2_fb, steps=20, warmup=3)
-    gab = GraphedAcquisition(acqf, Xd, with_grad=True)
+    gab = GraphedAcquisition(acqf, Xd, with_grad=True, share_input=True)
     tgb = _gpu_time(lambda: gab(Xd), steps=50, warmup=5)
     e.update(graphed_ms=1e3 * tg, graphed_evals_per_s=q * S * b / tg, fwd_bwd_ms=1e3 * tfb,
              graphed_fwd_bwd_ms=1e3 * tgb)
@@ -1219,7 +1219,7 @@ def main():
             Xs = Xd[: RESTARTS // W]
             with torch.no_grad():
                 tW = _gpu_time(lambda: acqf(Xs), steps=10, warmup=2)
-            gW = GraphedAcquisition(acqf, Xs)  # the same forward replayed as a HIP graph
+            gW = GraphedAcquisition(acqf, Xs, share_input=True)  # the same forward as a HIP graph
             tG = _gpu_time(lambda: gW(Xs), steps=10, warmup=2)
             strong_proj[f"W{W}"] = {"restarts_per_gpu": RESTARTS // W, "ms": 1e3 * tW,
                                     "projected_value": Q * RESTARTS * MC / tW,

@@ -169,16 +169,23 @@ def _fused_mc(X3: torch.Tensor, acqf, mode: int, best_f: float, best_f_s, Z: tor
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     if X3.dtype != torch.float64:  # the model computes in fp64; the value returns in X's dtype
         return _fused_mc(X3.to(torch.float64), acqf, mode, best_f, best_f_s, Z).to(X3.dtype)
-    if not need_grad and not kernels.SYNC_LADDER and idx not in kernels._CAPTURE:
+    cap = kernels._CAPTURE_STATUS.get(idx) if idx in kernels._CAPTURE else None
+    if not need_grad and not kernels.SYNC_LADDER and (idx not in kernels._CAPTURE or cap):
         # eager forward-only: ONE native call issues the whole chain and defers
-        # the ladder status (the previous call's is returned and acted on here)
+        # the ladder status (the previous call's is returned and acted on here);
+        # under a graph capture the same call, its status folded into the
+        # graph's pinned words by the finalisation kernel itself
         acq, prev = _lib.torch_ops().qmc_acq_eager(
             X3.contiguous(), cache.Xt_scaled, cache.U, cache.beta, cache.lengthscale,
             Z, best_f_s, int(cache.kind), int(mode), int(cache.n), float(cache.outputscale),
             float(cache.constant), float(ymean), float(ystd), float(best_f), bool(fat),
             float(tau_relu), float(tau_max), kernels.kxt_cap(dev),
-            kernels.quad_ainv(cache, X3.shape[0], X3.shape[1]), cache.alpha)
-        kernels.ladder_prev_outcome(prev, idx, type(acqf).__name__)
+            kernels.quad_ainv(cache, X3.shape[0], X3.shape[1]), cache.alpha,
+            cap[0] if cap else None, cap[1] if cap else None)
+        if cap:
+            kernels._CAPTURE[idx] = ("native", type(acqf).__name__)
+        else:
+            kernels.ladder_prev_outcome(prev, idx, type(acqf).__name__)
         return acq
     if need_grad:  # the registered op's semantics without its autograd wrapper
         acq, jit, info = ops.QmcAcqGrad.apply(

@@ -1240,36 +1240,106 @@ __device__ bool batched_update2(const Ctx& c, const Flags& f, int kb, int nk, in
   return true;
 }
 
-// A^{-1} tiles (KIND 3 of the batched updates): Ainv_ij += sum_{K in [kb, ke),
-// K >= i} X_Ki^T X_Kj for the rows i of the chunk (i >= j), the X_Kj^T of the
-// batch resident in LDS (XB[g]).  acc_mma_nt forms SA SB^T, so both operands
-// sit transposed in LDS (tile_to_lds_t).  Row i's first contribution (K = i)
-// starts from zero, so A^{-1} needs no clearing; fAi[i][j] counts the
-// contributions applied (ke - i after this task).  X_Ki is final once X_{ke-1,
-// i} is (each X_Ki is formed from the X_mi, m < K), so one flag per operand
-// column: fXd[ke-1][i], or fL[i][i] when ke - 1 == i (X_ii = D_i).
+// acc += SA^T SB, 64-deep, both operands as stored (row-major [k][col]): lane
+// (r16, kq) reads SA[k][wm + r16] and SB[k][wn + r16] -- 16 consecutive
+// doubles per k row, no transposed staging (A^{-1}'s X_Ki^T X_Kj).
+__device__ __forceinline__ void acc_mma_tn(const Ctx& c, Acc& a, const double* SA, const double* SB) {
+  const int r16 = c.lane & 15, kq = c.lane >> 4;
+#pragma unroll 4
+  for (int ks = 0; ks < 16; ++ks) {
+    const int k = 4 * ks + kq;
+    const double a0 = SA[k * LP + c.wm + r16], a1 = SA[k * LP + c.wm + 16 + r16];
+    const double b0 = SB[k * LP + c.wn + r16], b1 = SB[k * LP + c.wn + 16 + r16];
+    a.t[0][0] = mfma_f64(a0, b0, a.t[0][0]);
+    a.t[0][1] = mfma_f64(a0, b1, a.t[0][1]);
+    a.t[1][0] = mfma_f64(a1, b0, a.t[1][0]);
+    a.t[1][1] = mfma_f64(a1, b1, a.t[1][1]);
+  }
+}
+
+// A^{-1} tiles: Ainv_ij += sum_{K in [kb, ke), K >= i} X_Ki^T X_Kj for the
+// rows i of the chunk (i >= j), the X_Kj of the batch resident in LDS (XB[g],
+// as stored).  Row i's first contribution (K = i) starts from zero, so A^{-1}
+// needs no clearing; fAi[i][j] counts the contributions applied (ke - i after
+// this task).  X_Ki is final once X_{ke-1, i} is (each X_Ki is formed from the
+// X_mi, m < K), so one flag per operand column: fXd[ke-1][i], or fL[i][i] when
+// ke - 1 == i (X_ii = D_i).  The (row, step) pairs form one stream; the
+// operand of the next pair is in flight in registers under this pair's MFMAs
+// (the next row's only when one poll found its inputs published).
 __device__ bool ainv_update(const Ctx& c, const Flags& f, int kb, int nk, int j, int i0, int i1,
                             double* X0, double* XB0, double* XB1, double* XB2, rsrc_t rAi,
-                            int* s_ok, long long* wsum) {
+                            int* s_ok, int* s_rdy, long long* wsum) {
   auto XB = [&](int g) { return g == 0 ? XB0 : (g == 1 ? XB1 : XB2); };
   const int ke = kb + nk;
   Acc acc;
+  double2 pv[8];
+  double pa[16];
+  auto xd_flag = [&](int i) { return (ke - 1 == i) ? f.at(f.fL, i, i) : f.at(f.fXd, ke - 1, i); };
+  auto g_first = [&](int i) { return i > kb ? i - kb : 0; };  // K = kb + g >= i
+  auto issue_a = [&](int i, int K) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int e = c.tid + 256 * p;
+      pv[p] = ld16(c.rI, toff(c, K, i, e >> 5, (e & 31) * 2));
+    }
+  };
+  auto issue_c = [&](int i) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          pa[8 * a + 4 * b + q] = ld8(rAi, toff(c, i, j, c.wm + 16 * a + mfma_row(c.lane, q),
+                                               c.wn + 16 * b + mfma_col(c.lane)));
+  };
+  bool pre = false;  // this row's C and first operand already in flight
   for (int i = i0; i < i1; ++i) {
-    const int g0 = i > kb ? i - kb : 0;  // K = kb + g >= i
+    const int g0 = g_first(i);
     const u32 v0 = (u32)(kb + g0 - i);
-    const u32* xd = (ke - 1 == i) ? f.at(f.fL, i, i) : f.at(f.fXd, ke - 1, i);
-    if (!wait2(c, xd, 1u, f.at(f.fAi, i, j), v0, f.abortw, s_ok, wsum)) return false;
-    if (v0 == 0) acc_zero(acc);
-    else acc_load(c, acc, rAi, i, j);
+    if (!pre) {
+      if (!wait2(c, xd_flag(i), 1u, f.at(f.fAi, i, j), v0, f.abortw, s_ok, wsum)) return false;
+      if (v0 > 0) issue_c(i);
+      if (i != j) issue_a(i, kb + g0);
+    }
+    // the next row's readiness, polled once
+    if (c.tid == 0) {
+      int r = 0;
+      if (i + 1 < i1) {
+        const u32 v1 = (u32)(kb + g_first(i + 1) - (i + 1));
+        r = flag_load(xd_flag(i + 1)) >= 1u && flag_load(f.at(f.fAi, i + 1, j)) >= v1;
+      }
+      s_rdy[i & 1] = r;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc.t[a][b][q] = v0 > 0 ? pa[8 * a + 4 * b + q] : 0.0;
+    __syncthreads();
+    const bool next = s_rdy[i & 1] != 0;
     for (int g = g0; g < nk; ++g) {
       const bool own = i != j;
       if (own) {
-        tile_to_lds_t(c, c.rI, kb + g, i, X0);  // X_Ki^T
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+          const int e = c.tid + 256 * p;
+          *reinterpret_cast<double2*>(X0 + (e >> 5) * LP + (e & 31) * 2) = pv[p];
+        }
         __syncthreads();
       }
-      acc_mma_nt(c, acc, own ? X0 : XB(g), XB(g), 1.0);
+      if (g + 1 < nk) {
+        if (own) issue_a(i, kb + g + 1);
+      } else if (next) {
+        const int gn = g_first(i + 1);
+        if (kb + gn - (i + 1) > 0) issue_c(i + 1);
+        if (i + 1 != j) issue_a(i + 1, kb + gn);
+      }
+      acc_mma_tn(c, acc, own ? X0 : XB(g), XB(g));
       __syncthreads();  // X0 free for the next operand
     }
+    pre = next;
     acc_store(c, acc, rAi, i, j);
     publish(c, f.at(f.fAi, i, j), (u32)(ke - i));
   }
@@ -1437,10 +1507,10 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
       if (kl == j) ok = wait2(c, F(fL, j, j), 1u, F(fL, j, j), 1u, abortw, &s_ok, &wsum);
       else ok = wait2(c, F(fXd, kl, j), 1u, F(fXd, kl, j), 1u, abortw, &s_ok, &wsum);
       if (ok) {
-        for (int g = j > k ? j - k : 0; g < nk; ++g)  // X_Kj transposed (K >= j: the rest is 0)
-          tile_to_lds_t(c, c.rI, k + g, j, g == 0 ? X1 : (g == 1 ? X2 : X3));
+        for (int g = j > k ? j - k : 0; g < nk; ++g)  // X_Kj as stored (K >= j: the rest is 0)
+          tile_to_lds(c, c.rI, k + g, j, g == 0 ? X1 : (g == 1 ? X2 : X3));
         __syncthreads();
-        ok = ainv_update(c, fl, k, nk, j, i0, i1, X0, X1, X2, X3, rAi, &s_ok, &wsum);
+        ok = ainv_update(c, fl, k, nk, j, i0, i1, X0, X1, X2, X3, rAi, &s_ok, s_rdy, &wsum);
       }
     } else if (nk > 1) {  // T_XSTEP, batched: the far rows of steps k .. k + nk - 1
       const int kl = k + nk - 1;  // X_{k..kl, j} final once X_{kl, j} is
@@ -1647,6 +1717,27 @@ std::vector<int4> priority_order(const std::vector<int4>& v, int T) {
     for (int dd : deps[t])
       if (dd >= 0 && bl[t] > succ[dd]) succ[dd] = bl[t];
   }
+  // A^{-1} tasks (no factorisation task waits on them): by bottom level they
+  // would sort behind nearly every factorisation task, i.e. run after the
+  // factorisation, serially (measured 2.27 ms for n = 4096 against 2.09 ms as
+  // two launches).  ASAP instead: each goes right behind the last of its
+  // inputs in the queue (its key just under the smallest input key), so the
+  // idle workgroups of the chain-bound stretches pick them up as the X rows
+  // become final.  Keys of inputs are final first (generation order is
+  // topological).  Opt-in (BO_CHOL_AINV_ASAP=1): measured 2.28 against 2.25 ms
+  // with the bottom levels (profiles/r05/ainv_fold/).
+  static const bool asap = [] {
+    const char* e = getenv("BO_CHOL_AINV_ASAP");
+    return e && e[0] == '1';
+  }();
+  if (asap)
+    for (int t = 0; t < n; ++t) {
+      if ((v[t].x & 0xff) != T_AINV) continue;
+      double key = 1e300;
+      for (int dd : deps[t])
+        if (dd >= 0) key = std::min(key, bl[dd]);
+      if (key < 1e300) bl[t] = key - 1e-6 * (1 + (t % 1000));
+    }
   std::vector<int> idx(n);
   for (int t = 0; t < n; ++t) idx[t] = t;
   std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return bl[a] > bl[b]; });

@@ -494,8 +494,12 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     }
     __syncthreads();
     if (tid == 0) {
-      status_out[0] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
-      status_out[1] = fmax(fmax(red2[0], red2[1]), fmax(red2[2], red2[3]));
+      // folded into what the words hold (sticky): the eager calls' ring slots
+      // are zeroed by the host before each use, a captured graph's buffer is
+      // zeroed only when its status has been acted on, so it collects the max
+      // over every replay since (graphs.GraphedAcquisition)
+      status_out[0] = fmax(status_out[0], fmax(fmax(red[0], red[1]), fmax(red[2], red[3])));
+      status_out[1] = fmax(status_out[1], fmax(fmax(red2[0], red2[1]), fmax(red2[2], red2[3])));
       __hip_atomic_store(status_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     QMC_PHASE(4);

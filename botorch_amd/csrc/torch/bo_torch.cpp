@@ -129,7 +129,12 @@ int free_slot(DeviceLadder& L, at::Tensor& prev) {
     fold_front(L, prev.data_ptr<double>());
   }
   for (int i = 0; i < NSLOT; ++i)
-    if (!L.slot[i].busy) return i;
+    if (!L.slot[i].busy) {
+      // qmc_kernel folds its status into the words it finds (sticky max)
+      L.slot[i].host[0] = 0.0;
+      L.slot[i].host[1] = 0.0;
+      return i;
+    }
   TORCH_CHECK(false, "botorch_amd: no free ladder-status slot");
 }
 
@@ -183,7 +188,9 @@ std::vector<at::Tensor> qmc_acq_impl(
     const c10::optional<at::Tensor>& best_f_s, int64_t kind, int64_t mode, int64_t n,
     double outputscale, double constant, double ymean, double ystd, double best_f, bool fat,
     double tau_relu, double tau_max, bool need_grad, int64_t kxt_cap, bool defer_ladder,
-    const c10::optional<at::Tensor>& Ainv, const c10::optional<at::Tensor>& alpha, bool lean) {
+    const c10::optional<at::Tensor>& Ainv, const c10::optional<at::Tensor>& alpha, bool lean,
+    const c10::optional<at::Tensor>& cap_status = c10::nullopt,
+    const c10::optional<at::Tensor>& cap_count = c10::nullopt) {
   check_f64(X, "X");
   check_f64(Xt_scaled, "Xt_scaled");
   check_f64(U, "U");
@@ -348,7 +355,24 @@ std::vector<at::Tensor> qmc_acq_impl(
   // (the backward's W = R L^-1 is formed by qmc_acq_backward_native, fused
   // into its dX reduction where the grid allows: nothing of it is stored here)
   at::Tensor prev;
-  if (defer_ladder && B > 0 && mode != BO_QMC_POSTERIOR) {
+  const bool cap = cap_status.has_value() && cap_status->defined();
+  if (cap && B > 0 && mode != BO_QMC_POSTERIOR) {
+    // a forward under HIP-graph capture (graphs.GraphedAcquisition): the
+    // finalisation folds its ladder status straight into the graph's own
+    // pinned words (sticky max over the replays) -- no status kernel, copy
+    // or host bookkeeping among the captured nodes
+    TORCH_CHECK(cap_count.has_value() && cap_count->defined() && cap_count->is_cuda() &&
+                    cap_count->scalar_type() == at::kInt && cap_status->numel() == 2 &&
+                    cap_status->scalar_type() == at::kDouble,
+                "bo::qmc_acq_eager: cap_status (2 pinned doubles) needs cap_count (1 device int)");
+    double* hd = nullptr;
+    hk(hipHostGetDevicePointer(reinterpret_cast<void**>(&hd), cap_status->data_ptr<double>(), 0),
+       "hipHostGetDevicePointer");
+    fa.status_out = hd;
+    fa.status_count = cap_count->data_ptr<int>();
+    ck(bo_qmc_finalize_v(&fa, st), "qmc_finalize");
+    prev = at::zeros({3}, at::TensorOptions().dtype(at::kDouble));
+  } else if (defer_ladder && B > 0 && mode != BO_QMC_POSTERIOR) {
     // the ladder status reduced by the finalisation launch itself (its last
     // workgroup) straight into this call's pinned slot (zero-copy: no copy
     // launch), read behind an event one call later
@@ -400,10 +424,23 @@ std::vector<at::Tensor> qmc_acq_eager(
     const c10::optional<at::Tensor>& best_f_s, int64_t kind, int64_t mode, int64_t n,
     double outputscale, double constant, double ymean, double ystd, double best_f, bool fat,
     double tau_relu, double tau_max, int64_t kxt_cap, const c10::optional<at::Tensor>& Ainv,
-    const c10::optional<at::Tensor>& alpha) {
+    const c10::optional<at::Tensor>& alpha, const c10::optional<at::Tensor>& cap_status,
+    const c10::optional<at::Tensor>& cap_count) {
   return qmc_acq_impl(X, Xt_scaled, U, U, beta, lengthscale, Z, best_f_s, kind, mode, n,
                       outputscale, constant, ymean, ystd, best_f, fat, tau_relu, tau_max, false,
-                      kxt_cap, true, Ainv, alpha, true);
+                      kxt_cap, true, Ainv, alpha, true, cap_status, cap_count);
+}
+
+// Two coherent, device-mapped pinned doubles, zeroed: a captured graph's
+// ladder-status words (bo::qmc_acq_eager's cap_status).
+at::Tensor pinned_status() {
+  double* h = nullptr;
+  hk(hipHostMalloc(reinterpret_cast<void**>(&h), 2 * sizeof(double),
+                   hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+  h[0] = 0.0;
+  h[1] = 0.0;
+  return at::from_blob(h, {2}, [](void* p) { (void)hipHostFree(p); },
+                       at::TensorOptions().dtype(at::kDouble));
 }
 
 // The posterior-backward route the last qmc_acq_backward_native call took
@@ -577,7 +614,8 @@ TORCH_LIBRARY_FRAGMENT(bo, m) {
   m.def("qmc_acq_eager(Tensor X, Tensor Xt_scaled, Tensor U, Tensor beta, Tensor lengthscale, "
         "Tensor Z, Tensor? best_f_s, int kind, int mode, int n, float outputscale, float constant, "
         "float ymean, float ystd, float best_f, bool fat, float tau_relu, float tau_max, "
-        "int kxt_cap, Tensor? Ainv=None, Tensor? alpha=None) -> Tensor[]");
+        "int kxt_cap, Tensor? Ainv=None, Tensor? alpha=None, Tensor? cap_status=None, "
+        "Tensor? cap_count=None) -> Tensor[]");
   m.def("qmc_acq_backward_native(Tensor dacq, Tensor acq, Tensor mean, Tensor L, Tensor Z, "
         "Tensor? best_f_s, Tensor Xq, Tensor Rt, Tensor Linv, Tensor U, Tensor Xt_scaled, "
         "Tensor alpha, Tensor lengthscale, int kind, int mode, int d, int n, float outputscale, "
@@ -587,6 +625,7 @@ TORCH_LIBRARY_FRAGMENT(bo, m) {
   m.def("post_timing(bool on) -> ()", &post_timing);
   m.def("post_timing_read() -> Tensor", &post_timing_read);
   m.def("last_backward_route() -> int", &last_backward_route);
+  m.def("pinned_status() -> Tensor", &pinned_status);
 }
 
 TORCH_LIBRARY_IMPL(bo, CUDA, m) {

@@ -40,14 +40,17 @@ class GraphedAcquisition:
     ``(acq, dacq_sum/dX)`` (the gradient ``gen_candidates_*`` needs)."""
 
     def __init__(self, acqf, X_example: torch.Tensor, with_grad: bool = False, warmup: int = 2,
-                 check_each_call: bool = True):
+                 check_each_call: bool = True, share_input: bool = False):
+        """``share_input``: capture reading X_example's own storage (no copy);
+        a call with that same tensor then replays without copying X in (the
+        device optimiser's trial points; the caller owns the buffer)."""
         if not X_example.is_cuda:
             raise RuntimeError("GraphedAcquisition captures ROCm device work")
         self.acqf = acqf
         self.with_grad = with_grad
         self.check_each_call = check_each_call
         self.dev = X_example.device
-        self.X = X_example.detach().clone()
+        self.X = X_example.detach() if share_input else X_example.detach().clone()
         self._model_key = self._key()
         side = torch.cuda.Stream(self.dev)
         side.wait_stream(torch.cuda.current_stream(self.dev))
@@ -58,15 +61,29 @@ class GraphedAcquisition:
         kernels.check_ladder_status(self.dev)
         self.graph = torch.cuda.CUDAGraph()
         self._sticky = torch.zeros(2, dtype=torch.float64, device=self.dev)
-        self._host = torch.zeros(2, dtype=torch.float64).pin_memory()
         self._what = None
+        from . import _lib
+        # forward-only: the fused forward's finalisation folds the status into
+        # these coherent pinned words itself (sticky max), so the graph holds
+        # just the forward's own kernels; otherwise (gradients, generic routes)
+        # a status reduction, a device max and a pinned copy are captured too
+        self._host = _lib.torch_ops().pinned_status() if not with_grad else \
+            torch.zeros(2, dtype=torch.float64).pin_memory()
+        counter = torch.zeros(1, dtype=torch.int32, device=self.dev)
         with kernels.capturing(self.dev) as cap:
-            with torch.cuda.graph(self.graph):
-                self.out = self._body()
-                st = kernels._CAPTURE.get(cap.idx)
-                if st is not None:  # the replay's status: sticky max, then to the host
-                    torch.maximum(self._sticky, st[0], out=self._sticky)
-                    self._host.copy_(self._sticky, non_blocking=True)
+            if not with_grad:
+                kernels._CAPTURE_STATUS[cap.idx] = (self._host, counter)
+            try:
+                with torch.cuda.graph(self.graph):
+                    self.out = self._body()
+                    st = kernels._CAPTURE.get(cap.idx)
+                    if st is not None and st[0] != "native":
+                        # the replay's status: sticky max, then to the host
+                        torch.maximum(self._sticky, st[0], out=self._sticky)
+                        self._host.copy_(self._sticky, non_blocking=True)
+            finally:
+                kernels._CAPTURE_STATUS.pop(cap.idx, None)
+        self._counter = counter
         taken = kernels.take_captured_status(self.dev)
         self._what = taken[1] if taken is not None else None
         kernels.drop_keepalive()  # captured: no launch still needs the argument refs
@@ -123,7 +140,8 @@ class GraphedAcquisition:
             raise RuntimeError("the model changed since capture; build a new GraphedAcquisition")
         if self.check_each_call:
             self._poll()  # a finished replay's ladder status, without stalling this call
-        self.X.copy_(X.detach())
+        if X.data_ptr() != self.X.data_ptr():  # (a caller that writes the captured buffer itself)
+            self.X.copy_(X.detach())
         self.graph.replay()
         self._event.record(torch.cuda.current_stream(self.dev))
         self._pending = True

@@ -41,9 +41,11 @@ CHOLESKY_JITTER_F64 = 1e-8  # [G] linear_operator.settings.cholesky_jitter (doub
 # Optional callable(tag) invoked around the bo_post_partials launch (bench.py
 # records HIP events on the current stream through it).
 TIMING_HOOK = None
-# the MLL closure's A^{-1} inside the factorisation's launch (round 5); "0": the
-# separate bo_ainv pass
-AINV_IN_DAG = os.environ.get("BO_MLL_AINV_DAG", "1") != "0"
+# the MLL closure's A^{-1} inside the factorisation's launch (round 5, opt-in:
+# BO_MLL_AINV_DAG=1).  Measured slower than the separate bo_ainv pass: n = 4096
+# factor + inverse + A^{-1} 2.25-2.28 ms in one launch against 2.11 ms as two
+# (profiles/r05/ainv_fold/), so the closure keeps the two launches
+AINV_IN_DAG = os.environ.get("BO_MLL_AINV_DAG", "0") == "1"
 
 
 # Tensors whose pointers were handed to the C ABI most recently.  A call such as
@@ -279,8 +281,8 @@ def build_gp_cache_optimistic(Xt, y, lengthscale, noise: float, constant: float,
     f64 = dict(dtype=torch.float64, device=dev)
     L = torch.empty(np_, np_, **f64)
     Linv = torch.empty(np_, np_, **f64)
-    # A^{-1} in the factorisation's own launch (its tile products fill the
-    # chain-bound tail; BO_MLL_AINV_DAG=0: the separate bo_ainv pass instead)
+    # A^{-1} in the factorisation's own launch with BO_MLL_AINV_DAG=1 (opt-in,
+    # see AINV_IN_DAG); by default the separate bo_ainv pass in mll_terms
     Ainv = torch.empty(np_, np_, **f64) if AINV_IN_DAG else None
     # the DAG's tile counters (5 (np/64)^2 + 16 ints) and alpha's chunk partials;
     # the MLL closure forms no U = L^{-T} (alpha from L^{-1}'s columns)
@@ -873,7 +875,11 @@ def _ladder_outcome(info_max: float, jitter_max: float, what: str) -> None:
 # Graph capture (graphs.GraphedAcquisition): inside capturing(dev) the ladder
 # status is reduced into a device buffer that the graph owns and is read by
 # the wrapper after a replay -- no host read, pinned copy or event in the graph.
+# A forward-only capture registers (pinned status words, device counter) in
+# _CAPTURE_STATUS: the fused forward's finalisation kernel then folds the
+# status into those words itself and the capture records ("native", what).
 _CAPTURE = {}
+_CAPTURE_STATUS = {}
 
 
 class capturing:

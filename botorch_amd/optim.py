@@ -822,7 +822,7 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
         from .graphs import GraphedAcquisition
         try:
             return GraphedAcquisition(acquisition_function, state.xt.view(shape), with_grad=True,
-                                      warmup=1, check_each_call=False)
+                                      warmup=1, check_each_call=False, share_input=True)
         except RuntimeError as e:  # capture refused (e.g. a generic route with host reads)
             torch.cuda.synchronize(X0.device)
             graph_errors.append(f"{type(e).__name__}: {e}")

@@ -118,8 +118,8 @@ def test_graph_status_rearms_after_not_psd():
     """A replay whose ladder failed raises NotPSDError once; a later replay
     that factors cleanly does not raise again (psd_safe_cholesky raises only
     for the failing evaluation).  The failing replay is simulated by seeding
-    the graph's sticky device maximum with info = 1, which the next replay
-    folds into the status it publishes."""
+    the graph's pinned status words with info = 1, which the next replay's
+    finalisation kernel folds its own status into (sticky max)."""
     from botorch_amd.exceptions import NotPSDError
     from botorch_amd.graphs import GraphedAcquisition
     acqf = _acqf(256, 64, seed=4)
@@ -127,7 +127,8 @@ def test_graph_status_rearms_after_not_psd():
     ga = GraphedAcquisition(acqf, X)
     ga(X)
     ga.check_status()
-    ga._sticky[0] = 1.0
+    # forward-only graphs: the finalisation kernel folds into the pinned words
+    ga._host[0] = 1.0
     ga(X)
     with pytest.raises(NotPSDError):
         ga.check_status()
