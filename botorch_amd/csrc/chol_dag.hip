@@ -1578,13 +1578,32 @@ struct DagTable {
 };
 
 void push_rows(std::vector<int4>& v, int type, int k, int j, int lo, int hi, bool first_fin,
-               int ch = CH) {
+               int ch = CH, int first_ch = 0) {
   bool first = true;
-  for (int i0 = lo; i0 < hi; i0 += ch) {
-    const int i1 = i0 + ch < hi ? i0 + ch : hi;
+  for (int i0 = lo; i0 < hi;) {
+    const int c = (first && first_ch > 0) ? first_ch : ch;
+    const int i1 = i0 + c < hi ? i0 + c : hi;
     v.push_back(make_int4(type | ((first && first_fin) ? 256 : 0), k, j, i0 | (i1 << 16)));
     first = false;
+    i0 = i1;
   }
+}
+
+// Rows in the first chunk of a batched column update (the chunk holding the
+// diagonal tile A(j, j)): the batched updates of one column are serialised on
+// that tile's versions; with a whole chb-row chunk each link took ~45 us for 3
+// steps at n = 4096, as slow as the diagonal chain it feeds (round-5 trace:
+// every third diagonal step waited 25-35 us on it).  BO_CHOL_DIAG_CH overrides
+// the default at the call (0: chb).  A dedicated workgroup per diagonal chain
+// (CRIT(k) run in order, never claimed late) was measured too: no gain once
+// CRIT waits on its inputs instead, and the restructured loop cost 12% in
+// register allocation (1.65 -> 1.84 ms).
+static int diag_chunk_rows() {
+  static const int r = [] {
+    const char* e = getenv("BO_CHOL_DIAG_CH");
+    return e ? atoi(e) : -1;
+  }();
+  return r;
 }
 
 // Queue order: the generation order above is a topological order of the task
@@ -1800,7 +1819,11 @@ std::vector<int4> build_tasks(int T, int ch = 2, int chb = 4, bool ainv = false)
       if (GB > 1 && kb + GB - 1 <= j - 3) {
         if (k == kb + GB - 1) {
           const size_t first = v.size();
-          push_rows(v, T_COLUPD, kb, j, j, T, false, chb);
+          // 2 rows where chunks are 4 (one matrix, small batches): n = 4096
+          // 1.659-1.661 -> 1.621-1.638 ms, 3 x 2048 0.786-0.791 -> 0.766-0.769;
+          // not with the 8-row chunks of 4096 batches (4 x 4096 5.33 -> 5.38)
+          const int dch = diag_chunk_rows() >= 0 ? diag_chunk_rows() : (chb <= 4 ? 2 : 0);
+          push_rows(v, T_COLUPD, kb, j, j, T, false, chb, dch);
           for (size_t t = first; t < v.size(); ++t) v[t].x |= GB << 16;
         }
       } else {
@@ -1946,7 +1969,7 @@ extern "C" int bo_probe_chol_dag(double* A, double* Linv, int64_t np, int* info,
   int s = dag_table((int)(np / TB), &tb);
   if (s) return s;
   *ntasks = tb->n;
-  return bo_chol_dag(A, Linv, np, info, work, as_stream(stream), trace, 1);
+  return bo_chol_dag(A, Linv, np, info, work, as_stream(stream), trace, 1, nullptr);
 }
 
 // One workgroup factors + inverts the 64 x 64 SPD matrix A (row-major) reps

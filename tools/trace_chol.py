@@ -116,6 +116,49 @@ def main():
     tail.sort(key=lambda r: r[7])
     out["tail_tasks_type_k_j_i0_i1_nk_fin_start_end_block"] = [r for r in tail if r[0] != "XSTEP"] + \
         [r for r in tail if r[0] == "XSTEP"][-8:]
+    # per diagonal step: when its inputs were published (relative to the
+    # CRIT task's start): D_{k-1} (CRIT(k-1) end), the last updates of
+    # A(k, k-1) and A(k, k) (the COLUPD tasks ending at step k - 2)
+    ends = {}
+    for t in range(ntask):
+        x, kk, jj, w = (int(v) for v in qb[t])
+        if (x & 0xFF) != 2:
+            continue
+        nk_ = max(1, x >> 16)
+        i0, i1 = w & 0xFFFF, w >> 16
+        for i in range(i0, i1):
+            if jj in (i, i - 1):  # tiles (i, i) and (i, i - 1)
+                ends.setdefault((i, jj), []).append((kk + nk_ - 1, int(en[t]), int(st[t]), nk_, kk))
+    crit_in = []
+    for idx in crit.tolist():
+        kk = int(k[idx])
+        if kk < 2:
+            continue
+        s0 = int(st[idx])
+        row = [kk, round((crit_end.get(kk - 1, s0) - s0) / 100.0, 1)]
+        for jj in (kk - 1, kk):
+            c = [e for e in ends.get((kk, jj), []) if e[0] == kk - 2]
+            row.append(round((c[0][1] - s0) / 100.0, 1) if c else None)
+            row.append(c[0][3] if c else None)
+        crit_in.append(row)
+    out["crit_inputs_k_Dprev_Akk1_nk_Akk_nk_us_after_start"] = crit_in
+    # the history of tile (k, k) and of tile row k of L for a few steps: every
+    # task writing them (type, k, j, i0, i1, nk, queue slot, start, end, block)
+    hist = {}
+    for kk in [int(s) for s in os.environ.get("BO_TRACE_K", "26,27,28,29,30").split(",")]:
+        rows_ = []
+        for t in range(ntask):
+            x, k2, jj, w = (int(v) for v in qb[t])
+            i0, i1 = w & 0xFFFF, w >> 16
+            ty = x & 0xFF
+            if (ty == 2 and jj == kk and i0 <= kk < i1) or (ty == 1 and i0 <= kk < i1 and k2 >= kk - 5) or \
+               (ty == 0 and kk - 5 <= k2 <= kk):
+                rows_.append([TYPES[ty], k2, jj, i0, i1, max(1, x >> 16), t,
+                              round((int(st[t]) - t0) / 100.0, 1), round((int(en[t]) - t0) / 100.0, 1),
+                              int(blk[t])])
+        rows_.sort(key=lambda r: r[7])
+        hist[kk] = [r for r in rows_ if r[8] > (crit_end.get(kk - 5, t0) - t0) / 100.0]
+    out["diag_history_type_k_j_i0_i1_nk_slot_start_end_block"] = hist
     # the last finishing tasks
     last = torch.argsort(en, descending=True)[:8]
     out["last_tasks"] = [[TYPES[int(typ[i])], int(k[i]), int(j[i]), round((int(st[i]) - t0) / 100.0, 1),
