@@ -687,6 +687,15 @@ def time_gp_fit(Xtr, Ytr, dev, cpu=True):
         calls[0] += 1
         return orig(*a, **k)
 
+    # warm-up: one MLL closure on a throw-away copy of the model, untimed.  The
+    # first closure in a process pays one-time costs (lazy code-object loads of
+    # the closure's kernels, the n = 4096 task table): measured 507-517 ms for
+    # the first fit of a process against 390-394 ms for every later one, or for
+    # the first after one closure (tools/fit_breakdown.py)
+    warm = SingleTaskGP(Xtr.to(dev), Ytr.to(dev))
+    lay = fitmod._layout(warm)
+    fitmod.mll_value_and_grad(warm, lay.get(), lay, sync_model=False)
+    del warm, lay
     fitmod.mll_value_and_grad = counted
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
