@@ -88,6 +88,9 @@ _SIGNATURES = {
     "bo_post_small": (c_int, [_P, c_int64, c_int, c_int64, _P, c_int64, _P, _P, _P, _P, _P]),
     "bo_post_small_batched": (c_int, [c_int, _P, _P, _P, _P, _P, _P, c_int64, c_int, c_int64,
                                       c_int64, _P]),
+    "bo_post_members_work": (c_int, [c_int, c_int64, c_int, c_int64, POINTER(c_int64)]),
+    "bo_post_partials_members": (c_int, [c_int, _P, _P, _P, _P, _P, _P, _P, c_int64, c_int,
+                                         c_int64, c_int64, _P, _P]),
     "bo_post_quad": (c_int, [_P, _P, c_int64, _P, c_int64, c_int, c_int64, _P, _P, _P]),
     "bo_post_split_table": (c_int, [c_int64, c_int, c_int64, c_int, _P, c_int, _P, c_int,
                                     POINTER(c_int), POINTER(c_int)]),

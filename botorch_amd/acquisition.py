@@ -911,11 +911,12 @@ class _FusedQEHVI(torch.autograd.Function):
         # every member's posterior partials in one launch where the small-grid
         # plan applies (C4: the three outputs of the ModelListGP)
         pps = kernels.post_partials_members(caches, X3.detach(), store_R=need_grad)
+        status = []
         for mm, cache, pp in zip(models, caches, pps):
             ymean, ystd = mm.outcome_stats()
             out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
                                        want_cov=False, want_L=True)
-            kernels._raise_not_psd(out["info"], out["jitter"], "qEHVI posterior root")
+            status.append((out["info"], out["jitter"]))
             means.append(out["mean"])
             Ls.append(out["L"])
             if need_grad:
@@ -927,6 +928,10 @@ class _FusedQEHVI(torch.autograd.Function):
         # the kernel itself (as the backward below): this Function already is
         # the autograd node, the registered op's wrapper would only add host time
         acq = kernels.qehvi(mean, L, Z, lo, hi)
+        # the members' ladders checked once, behind the qEHVI launch (one host
+        # read per forward instead of one per member, each of which drained
+        # the queue: ~40 us of idle device between members at C4)
+        kernels.raise_not_psd_many(status, "qEHVI posterior root")
         if need_grad:
             ctx.saved, ctx.mean, ctx.L, ctx.Z, ctx.cells = saved, mean, L, Z, (lo, hi)
         return acq
@@ -1072,7 +1077,7 @@ class _FusedQNEHVI(torch.autograd.Function):
         models = acqf.model.models
         need_grad = ctx.needs_input_grad[0]
         q = X3.shape[-2]
-        means, Ls, Fs, saved = [], [], [], []
+        means, Ls, Fs, saved, status = [], [], [], [], []
         pp = None
         keys = prime_prediction_caches(models)
         for t, mm in enumerate(models):
@@ -1083,7 +1088,7 @@ class _FusedQNEHVI(torch.autograd.Function):
             T, F = acqf._roots[t].forward(cache, pp, ystd)
             out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
                                        want_cov=False, want_L=True, T=T, F=F)
-            kernels._raise_not_psd(out["info"], out["jitter"], "qNEHVI posterior root")
+            status.append((out["info"], out["jitter"]))
             means.append(out["mean"])
             Ls.append(out["L"])
             Fs.append(F)
@@ -1093,6 +1098,7 @@ class _FusedQNEHVI(torch.autograd.Function):
         lo, hi = acqf._cells
         mean, L, F = torch.stack(means), torch.stack(Ls), torch.stack(Fs)
         acq = kernels.qehvi(mean, L, Zq, lo, hi, F=F, Qp=pp.Qp)
+        kernels.raise_not_psd_many(status, "qNEHVI posterior root")  # one read (as qEHVI)
         if need_grad:
             ctx.acqf, ctx.saved, ctx.mean, ctx.L, ctx.F, ctx.Zq, ctx.Qp = (
                 acqf, saved, mean, L, F, Zq, pp.Qp)

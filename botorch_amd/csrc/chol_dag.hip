@@ -1042,14 +1042,18 @@ __device__ bool batched_update(const Ctx& c, const Flags& f, int kb, int nk, int
     }
   };
   auto issue_c = [&](int i) {
+    // X_ij's first contributions (v0 = 0) start from zero: Linv is not
+    // cleared ahead of the launch
+    const bool zero = KIND == 2 && v0 == 0u;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          pa[8 * a + 4 * b + q] = ld8(rc, toff(c, i, j, c.wm + 16 * a + mfma_row(c.lane, q),
-                                               c.wn + 16 * b + mfma_col(c.lane)));
+          pa[8 * a + 4 * b + q] = zero ? 0.0
+                                       : ld8(rc, toff(c, i, j, c.wm + 16 * a + mfma_row(c.lane, q),
+                                                      c.wn + 16 * b + mfma_col(c.lane)));
   };
   for (int i = i0; i < i1; ++i) {
     long long tA = 0;
@@ -1154,14 +1158,18 @@ __device__ bool batched_update2(const Ctx& c, const Flags& f, int kb, int nk, in
     }
   };
   auto issue_c = [&](int i) {
+    // X_ij's first contributions (v0 = 0) start from zero: Linv is not
+    // cleared ahead of the launch
+    const bool zero = KIND == 2 && v0 == 0u;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          pa[8 * a + 4 * b + q] = ld8(rc, toff(c, i, j, c.wm + 16 * a + mfma_row(c.lane, q),
-                                               c.wn + 16 * b + mfma_col(c.lane)));
+          pa[8 * a + 4 * b + q] = zero ? 0.0
+                                       : ld8(rc, toff(c, i, j, c.wm + 16 * a + mfma_row(c.lane, q),
+                                                      c.wn + 16 * b + mfma_col(c.lane)));
   };
   bool ok = true;
   // one stream element in register slot S (the other slot: O)
@@ -1355,7 +1363,8 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
                                                        int ntasks, u32* __restrict__ flags,
                                                        int* __restrict__ info,
                                                        long long* __restrict__ trace, int nb,
-                                                       int pf2, double* __restrict__ Ainv) {
+                                                       int pf2, double* __restrict__ Ainv,
+                                                       int zero_upper) {
   __shared__ __attribute__((aligned(16))) double X0[TB * LP];
   __shared__ __attribute__((aligned(16))) double X1[TB * LP];
   __shared__ __attribute__((aligned(16))) double X2[TB * LP];  // batched update operands
@@ -1393,6 +1402,23 @@ __global__ __launch_bounds__(256) void chol_dag_kernel(double* __restrict__ A, d
   int cur = 0;          // matrix of the buffer resources / flags above
   int* minfo = info;
 
+  // The strictly upper tiles of every Linv (zero in the result): stored here
+  // by the workgroups past the first 8 before their first claim -- the stores
+  // drain while those workgroups wait for the first diagonal steps, where a
+  // memset of the whole np x np ahead of the launch cost 17.9 us of the
+  // closure at n = 4096.  No task reads an upper tile.
+  if (zero_upper && (int)blockIdx.x >= 8) {
+    const int nz = (int)gridDim.x - 8, zb = (int)blockIdx.x - 8;
+    const int row = c.tid >> 2, col = (c.tid & 3) * 16;
+    for (int u = zb; u < nb * T * T; u += nz) {
+      const int m = u / (T * T), r = u - m * (T * T), ti = r / T, tj = r - ti * T;
+      if (ti >= tj) continue;
+      double2* p = reinterpret_cast<double2*>(Linv + (size_t)m * np * np +
+                                              (size_t)(ti * TB + row) * np + tj * TB + col);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) p[e] = make_double2(0.0, 0.0);
+    }
+  }
   if (c.tid == 0) s_task = (int)__hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   int t = s_task;
@@ -1943,17 +1969,23 @@ int bo_chol_dag(double* A, double* Linv, int64_t np, int* info, void* work, hipS
       ((size_t)(NFLAG0 + (size_t)nb * (Ainv ? 5 : 4) * T * T) * 4 + 15) / 16 * 16;
   BO_HIP(hipMemsetAsync(work, 0, fbytes, st));
   BO_HIP(hipMemsetAsync(info, 0, sizeof(int) * nb, st));
-  BO_HIP(hipMemsetAsync(Linv, 0, sizeof(double) * np * np * nb, st));
+  // BO_CHOL_ZERO_IN_DAG=0: memset Linv ahead of the launch instead (A/B knob)
+  static const int zero_in = [] {
+    const char* e = getenv("BO_CHOL_ZERO_IN_DAG");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  if (!zero_in) BO_HIP(hipMemsetAsync(Linv, 0, sizeof(double) * np * np * nb, st));
   // one workgroup per CU: two per CU (74 KB of LDS each fits) measured slower,
   // 2.35 -> 2.97 ms at n = 4096 -- the sc1 tile traffic, not latency, is the limit
   const int grid = cus < tb->n ? cus : tb->n;
+  if (zero_in && grid <= 8) BO_HIP(hipMemsetAsync(Linv, 0, sizeof(double) * np * np * nb, st));
   // BO_CHOL_PREFETCH2 (default 1): batched updates prefetch two steps ahead
   static const int pf2 = [] {
     const char* e = getenv("BO_CHOL_PREFETCH2");
     return (e && e[0] == '0') ? 0 : 1;
   }();
   chol_dag_kernel<<<grid, 256, 0, st>>>(A, Linv, (int)np, T, tb->dev, tb->n, (u32*)work, info,
-                                          trace, nb, pf2, Ainv);
+                                          trace, nb, pf2, Ainv, zero_in && grid > 8 ? 1 : 0);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

@@ -150,6 +150,20 @@ struct FusedDx {
   double* part;         // nC x nrows_pad x 8 partial dX (scaled coordinates)
 };
 
+// Member-batched stream-K plans (bo_post_partials_members): the buffers of up
+// to 8 models of one shape (a ModelListGP's members); a segment's member is
+// bits 24.. of its kbeg word (of the column-tile word in the reduction list).
+constexpr int POST_MAXM = 8;
+struct PostMembers {
+  const double* U[POST_MAXM];
+  const double* beta[POST_MAXM];
+  const double* Kt[POST_MAXM];
+  double* Spart[POST_MAXM];
+  double* mpart[POST_MAXM];
+  double* Rt[POST_MAXM];
+  int nm;  // 0: the kernel's own pointer arguments
+};
+
 template <int KIND, int ND, bool SPLIT, bool CROSS, bool PRE = false, bool LOWERK = false,
           bool FUSEDX = false>
 __global__ __launch_bounds__(256, 2) void post_partials_kernel(
@@ -159,7 +173,7 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     double* __restrict__ Rt, const int4* __restrict__ segs, const int* __restrict__ wg_off,
     double* __restrict__ work, const double* __restrict__ Qc, int rq, int64_t ldq,
     double* __restrict__ Cx, const double* __restrict__ Kt, int grouped, FusedDx fx = FusedDx{},
-    int rt_blk = 0) {
+    int rt_blk = 0, PostMembers pm = PostMembers{}) {
   // Two LDS stages: while the MFMAs consume stage t, the U rows of step t+1
   // are in flight to registers and this thread evaluates its 8 kernel values
   // of step t+1 between the MFMAs (VALU work hidden under the matrix pipe);
@@ -236,6 +250,12 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   // Split plans: this workgroup's segments (uniform control flow: every
   // thread walks the same list; the last k-step's barrier frees the LDS
   // stages before the next segment's prologue writes them).
+  const double* const U_all = U;
+  const double* const beta_all = beta;
+  const double* const Kt_all = Kt;
+  double* const Spart_all = Spart;
+  double* const mpart_all = mpart;
+  double* const Rt_all = Rt;
   int sbeg = 0, send = 1;
   if constexpr (SPLIT) {
     sbeg = wg_off[bid];
@@ -255,14 +275,24 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
       kend = n;
     }
   }
+  int mem = 0;
   if constexpr (SPLIT) {
     const int4 sg = segs[sidx];
     ci = sg.x & 0xffff;
     ii = sg.x >> 16;
-    kbeg = sg.y;
+    kbeg = sg.y & 0xffffff;
+    mem = sg.y >> 24;
     kend = sg.z;
     chunk = sg.w;  // -1: the segment covers its whole tile
   }
+  // this segment's model (member-batched plans), else the arguments
+  const bool memb = SPLIT && pm.nm > 0;
+  const double* U = memb ? pm.U[mem] : U_all;
+  const double* beta = memb ? pm.beta[mem] : beta_all;
+  const double* Kt = memb ? pm.Kt[mem] : Kt_all;
+  double* Spart = memb ? pm.Spart[mem] : Spart_all;
+  double* mpart = memb ? pm.mpart[mem] : mpart_all;
+  double* Rt = memb ? pm.Rt[mem] : Rt_all;
   const int c0 = ci * PC;
   const int i0 = ii * PI;
   const int nsteps = (kend - kbeg + PK - 1) / PK;
@@ -661,12 +691,18 @@ __global__ __launch_bounds__(256) void kxt_build_kernel(const double* __restrict
 // have 16 chunks, each round one memory latency), a fixed summation order.
 __global__ __launch_bounds__(256) void post_splitk_reduce_kernel(
     const double* __restrict__ work, const int4* __restrict__ red, int n, int nI,
-    const double* __restrict__ beta, double* __restrict__ Spart, double* __restrict__ mpart,
-    double* __restrict__ Rt) {
+    const double* __restrict__ beta_all, double* __restrict__ Spart_all,
+    double* __restrict__ mpart_all, double* __restrict__ Rt_all, PostMembers pm = PostMembers{}) {
   __shared__ double part[3][32][64];
   const int4 r4 = red[blockIdx.x / (PI / 16)];
   const int sub = blockIdx.x % (PI / 16);
-  const int ci = r4.x, rt = r4.y * (PI / 16) + sub;
+  const int ci = r4.x & 0xffffff, rt = r4.y * (PI / 16) + sub;
+  const int mem = r4.x >> 24;
+  const bool memb = pm.nm > 0;
+  const double* beta = memb ? pm.beta[mem] : beta_all;
+  double* Spart = memb ? pm.Spart[mem] : Spart_all;
+  double* mpart = memb ? pm.mpart[mem] : mpart_all;
+  double* Rt = memb ? pm.Rt[mem] : Rt_all;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   v4d acc[8];
@@ -990,8 +1026,9 @@ static int sk_min_share() {
 // row tiles ii, k-range [128 ci, n); PLAN_LOWER: every tile, k-range
 // [128 ci, n) (W^T = L^{-T} R^T, bo_post_w).
 enum { PLAN_POST = 0, PLAN_AINV = 1, PLAN_LOWER = 2 };
-SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, int mode = PLAN_POST) {
-  struct Seg { int ci, ii, kb, ke; };
+SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, int mode = PLAN_POST,
+                           int nm = 1) {
+  struct Seg { int ci, ii, kb, ke, m = 0; };
   std::vector<std::vector<Seg>> wg;
   auto kfull = [n](int ci) { return std::min(n, ci * PC + PC); };
   const bool ainv = mode == PLAN_AINV;
@@ -1041,34 +1078,62 @@ SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, int mod
     // tiles, so the nI workgroups of one j read the same U slices at the same
     // time; they are placed on one XCD (block b: XCD b % 8, slot b / 8) so
     // those slices are fetched into its L2 once.
+    // (member-batched plans: nm x nI lanes, member-major; the lanes of one
+    // member's j sit on one XCD as before -- they share that member's U)
+    const int lanes = nI * nm;
     int64_t lane_total = 0;
     for (int ci = 0; ci < nC; ++ci) lane_total += ceil_div(kend_of(ci) - kbeg_of(ci), PK);
     const int64_t per_lane = std::max<int64_t>(
-        1, std::min<int64_t>(std::max(1, slots / nI), lane_total / sk_min_share()));
+        1, std::min<int64_t>(std::max(1, slots / lanes), lane_total / sk_min_share()));
     const int64_t share = ceil_div(lane_total, per_lane);
     const int64_t jn = ceil_div(lane_total, share);  // workgroups used per lane
-    wg.resize((size_t)(ceil_div(jn, 8) * 8 * nI));
-    for (int ii = 0; ii < nI; ++ii) {
-      int64_t pos = 0;
-      for (int t = 0; t < nC; ++t) {
-        const int ci = ci_at(t), kb0 = kbeg_of(ci), ke0 = kend_of(ci);
-        const int L = (int)ceil_div(ke0 - kb0, PK);
-        int s0 = 0;
-        while (s0 < L) {
-          const int64_t j = pos / share;
-          const int take = (int)std::min<int64_t>(L - s0, (j + 1) * share - pos);
-          const int64_t b = ((j / 8) * nI + ii) * 8 + (j % 8);
-          wg[(size_t)b].push_back(Seg{ci, ii, kb0 + s0 * PK, std::min(ke0, kb0 + (s0 + take) * PK)});
-          s0 += take;
-          pos += take;
+    // Workgroup of (member m, lane ii, share j).  One model: ((j / 8) nI + ii)
+    // 8 + j % 8 -- the nI workgroups of one j on one XCD (block b runs on XCD
+    // b % 8), jn padded to a multiple of 8.  Several: that padding would push
+    // the grid past the resident slots (C4: 21 shares x 24 lanes -> 576 > 512,
+    // a second round for the last workgroups), so the (m, j) groups of nI
+    // workgroups are dealt round-robin over the XCDs, each XCD's slots filled
+    // in turn.
+    std::vector<int64_t> xcd_next(8, 0);
+    std::vector<int64_t> group_base((size_t)(nm * jn), 0);
+    if (nm > 1)
+      for (int64_t g = 0; g < nm * jn; ++g) {
+        const int x = (int)(g % 8);
+        group_base[(size_t)g] = xcd_next[x];
+        xcd_next[x] += nI;
+      }
+    auto wg_of = [&](int m, int ii, int64_t j) -> int64_t {
+      if (nm == 1) return ((j / 8) * lanes + ii) * 8 + (j % 8);
+      const int64_t g = m * jn + j;
+      return (group_base[(size_t)g] + ii) * 8 + (g % 8);
+    };
+    int64_t wmax = 0;
+    for (int x = 0; x < 8; ++x) wmax = std::max(wmax, xcd_next[x]);
+    wg.resize(nm == 1 ? (size_t)(ceil_div(jn, 8) * 8 * lanes) : (size_t)(wmax * 8));
+    for (int m = 0; m < nm; ++m)
+      for (int ii = 0; ii < nI; ++ii) {
+        int64_t pos = 0;
+        for (int t = 0; t < nC; ++t) {
+          const int ci = ci_at(t), kb0 = kbeg_of(ci), ke0 = kend_of(ci);
+          const int L = (int)ceil_div(ke0 - kb0, PK);
+          int s0 = 0;
+          while (s0 < L) {
+            const int64_t j = pos / share;
+            const int take = (int)std::min<int64_t>(L - s0, (j + 1) * share - pos);
+            const int64_t b = wg_of(m, ii, j);
+            wg[(size_t)b].push_back(
+                Seg{ci, ii, kb0 + s0 * PK, std::min(ke0, kb0 + (s0 + take) * PK), m});
+            s0 += take;
+            pos += take;
+          }
         }
       }
-    }
   }
   // chunk numbers: the segments of every split tile, in k order
-  std::map<std::pair<int, int>, std::vector<std::pair<int, int>>> tiles;  // -> (wg, idx) in k order
+  std::map<std::tuple<int, int, int>, std::vector<std::pair<int, int>>> tiles;  // -> (wg, idx), k order
   for (int w = 0; w < (int)wg.size(); ++w)
-    for (int j = 0; j < (int)wg[w].size(); ++j) tiles[{wg[w][j].ci, wg[w][j].ii}].push_back({w, j});
+    for (int j = 0; j < (int)wg[w].size(); ++j)
+      tiles[std::make_tuple(wg[w][j].m, wg[w][j].ci, wg[w][j].ii)].push_back({w, j});
   std::vector<std::vector<int>> chunk_of(wg.size());
   for (size_t w = 0; w < wg.size(); ++w) chunk_of[w].assign(wg[w].size(), -1);
   SplitPlan p;
@@ -1078,7 +1143,8 @@ SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, int mod
       return wg[a.first][a.second].kb < wg[b.first][b.second].kb;
     });
     if (lst.size() == 1) continue;  // whole tile in one segment: epilogue in place
-    p.red.push_back(make_int4(kv.first.first, kv.first.second, p.nchunks, (int)lst.size()));
+    p.red.push_back(make_int4(std::get<1>(kv.first) | (std::get<0>(kv.first) << 24),
+                              std::get<2>(kv.first), p.nchunks, (int)lst.size()));
     for (auto& e : lst) chunk_of[e.first][e.second] = p.nchunks++;
   }
   p.wg_off.push_back(0);
@@ -1086,7 +1152,7 @@ SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, int mod
     int64_t steps = 0;
     for (size_t j = 0; j < wg[w].size(); ++j) {
       const Seg& g = wg[w][j];
-      p.segs.push_back(make_int4(g.ci | (g.ii << 16), g.kb, g.ke, chunk_of[w][j]));
+      p.segs.push_back(make_int4(g.ci | (g.ii << 16), g.kb | (g.m << 24), g.ke, chunk_of[w][j]));
       steps += ceil_div(g.ke - g.kb, PK);
     }
     p.wg_off.push_back((int)p.segs.size());
@@ -1101,16 +1167,16 @@ SplitPlan build_split_plan(int nC, int nI, int n, int kc_len, int slots, int mod
 // b = 128 at n = 4096: ~255 us), and the eager operator asks for the
 // workspace on every call.
 std::mutex g_chunks_mu;
-std::map<std::tuple<int, int, int, int, int, int>, int> g_chunks;  // (nC, nI, n, kc, slots, mode)
+std::map<std::tuple<int, int, int, int, int, int>, int> g_chunks;  // (nC, nI, n, kc, slots, mode|nm)
 
-int plan_chunks(int nC, int nI, int n, int kc_len, int slots, int mode) {
-  const auto key = std::make_tuple(nC, nI, n, kc_len, slots, mode);
+int plan_chunks(int nC, int nI, int n, int kc_len, int slots, int mode, int nm = 1) {
+  const auto key = std::make_tuple(nC, nI, n, kc_len, slots, mode | (nm << 8));
   {
     std::lock_guard<std::mutex> lk(g_chunks_mu);
     auto it = g_chunks.find(key);
     if (it != g_chunks.end()) return it->second;
   }
-  const int c = build_split_plan(nC, nI, n, kc_len, slots, mode).nchunks;
+  const int c = build_split_plan(nC, nI, n, kc_len, slots, mode, nm).nchunks;
   std::lock_guard<std::mutex> lk(g_chunks_mu);
   g_chunks[key] = c;
   return c;
@@ -1124,13 +1190,13 @@ struct DevPlan {
 std::mutex g_plan_mu;
 std::map<std::tuple<int, int, int, int, int, int>, DevPlan> g_plans;  // (dev, nC, nI, n, kc, mode)
 
-int device_plan(int nC, int nI, int n, int kc_len, DevPlan** out, int mode = PLAN_POST) {
+int device_plan(int nC, int nI, int n, int kc_len, DevPlan** out, int mode = PLAN_POST, int nm = 1) {
   int dev = 0;
   BO_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_plan_mu);
-  DevPlan& dp = g_plans[std::make_tuple(dev, nC, nI, n, kc_len, mode)];
+  DevPlan& dp = g_plans[std::make_tuple(dev, nC, nI, n, kc_len, mode | (nm << 8))];
   if (!dp.wg_off) {
-    const SplitPlan p = build_split_plan(nC, nI, n, kc_len, kSlots, mode);
+    const SplitPlan p = build_split_plan(nC, nI, n, kc_len, kSlots, mode, nm);
     BO_HIP(hipMalloc(&dp.segs, sizeof(int4) * std::max<size_t>(1, p.segs.size())));
     BO_HIP(hipMalloc(&dp.red, sizeof(int4) * std::max<size_t>(1, p.red.size())));
     BO_HIP(hipMalloc(&dp.wg_off, sizeof(int) * p.wg_off.size()));
@@ -1260,6 +1326,78 @@ int bo_post_small_batched(int nm, const double* const* Kt, const double* const* 
 int bo_post_small(const double* Kt, int64_t B, int q, int64_t n, const double* U, int64_t ldu,
                   const double* beta, double* Spart, double* mpart, double* Rt, void* stream) {
   return bo_post_small_batched(1, &Kt, &U, &beta, &Spart, &mpart, &Rt, B, q, n, ldu, stream);
+}
+
+// Member-batched stream-K posterior (nm models of one shape, K*x^T given):
+// *work_elems = the shared split-k workspace in doubles, or -1 where the
+// one-model plan is not stream-K (the caller then runs one launch per model).
+int bo_post_members_work(int nm, int64_t B, int q, int64_t n, int64_t* work_elems) {
+  BO_CHECK_ARG(nm >= 1 && nm <= POST_MAXM, "bo_post_members_work: %d models (1..%d)", nm, POST_MAXM);
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  int kc = 0;
+  int64_t we = 0;
+  s = bo_post_split_plan(B, q, n, 0, &kc, &we);
+  if (s) return s;
+  *work_elems = -1;
+  if (kc != -1 || nrows_pad == 0) return BO_OK;
+  *work_elems = (int64_t)plan_chunks(nC, nrows_pad / PI, (int)n, -1, kSlots, PLAN_POST, nm) * PI * PC;
+  return BO_OK;
+}
+
+// R R^T / R beta column-tile partials (and R^T, row-major, where Rt[m] is
+// given) of nm models of one shape in ONE stream-K launch over all their
+// tiles (+ one reduction launch): Kt[m] np x nrows_pad (bo_post_kxt_rows),
+// U[m] np x np (ld ldu), Spart[m] nC x nrows_pad/16 x 16 x 16, mpart[m] nC x
+// nrows_pad.  The one-model plan cut C4's 8 x 16 tiles into ~4 shares each
+// (a 128 KB partial R^T per share, written and read back); over the three
+// members' 24 row lanes the shares are three times as long.
+int bo_post_partials_members(int nm, const double* const* Kt, const double* const* U,
+                             const double* const* beta, double* const* Spart, double* const* mpart,
+                             double* const* Rt, const double* Xq0, int64_t B, int q, int64_t n,
+                             int64_t ldu, double* work, void* stream) {
+  BO_CHECK_ARG(nm >= 1 && nm <= POST_MAXM, "bo_post_partials_members: %d models (1..%d)", nm,
+               POST_MAXM);
+  BO_CHECK_ARG(Kt && U && beta && Spart && mpart && Xq0, "bo_post_partials_members: null pointer");
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  if (nrows_pad == 0) return BO_OK;
+  BO_CHECK_ARG(ldu % 2 == 0 && ldu >= (int64_t)nC * PC, "U leading dim %lld too small", (long long)ldu);
+  int64_t we = 0;
+  s = bo_post_members_work(nm, B, q, n, &we);
+  if (s) return s;
+  BO_CHECK_ARG(we >= 0, "bo_post_partials_members: the one-model plan is not stream-K here");
+  BO_CHECK_ARG(we == 0 || work != nullptr, "bo_post_partials_members: workspace of %lld doubles needed",
+               (long long)we);
+  PostMembers pm{};
+  pm.nm = nm;
+  for (int m = 0; m < nm; ++m) {
+    BO_CHECK_ARG(Kt[m] && U[m] && beta[m] && Spart[m] && mpart[m], "bo_post_partials_members: null buffer");
+    pm.U[m] = U[m];
+    pm.beta[m] = beta[m];
+    pm.Kt[m] = Kt[m];
+    pm.Spart[m] = Spart[m];
+    pm.mpart[m] = mpart[m];
+    pm.Rt[m] = Rt ? Rt[m] : nullptr;
+  }
+  const int nI = nrows_pad / PI;
+  DevPlan* plan = nullptr;
+  s = device_plan(nC, nI, (int)n, -1, &plan, PLAN_POST, nm);
+  if (s) return s;
+  hipStream_t st = as_stream(stream);
+  // K*x^T given: the kernel kind and input dimension do not enter (PRE)
+  post_partials_kernel<BO_RBF, 1, true, false, true><<<(unsigned)plan->W, 256, 0, st>>>(
+      Xq0, B * Qp, nullptr, (int)n, U[0], ldu, beta[0], 1.0, nC, nI, Spart[0], mpart[0], nullptr,
+      plan->segs, plan->wg_off, work, nullptr, 0, 0, nullptr, Kt[0], 0, FusedDx{}, 0, pm);
+  BO_LAUNCH_CHECK();
+  if (plan->nred > 0) {
+    post_splitk_reduce_kernel<<<(unsigned)(plan->nred * (PI / 16)), 256, 0, st>>>(
+        work, plan->red, (int)n, nI, beta[0], Spart[0], mpart[0], nullptr, pm);
+    BO_LAUNCH_CHECK();
+  }
+  return BO_OK;
 }
 
 int bo_post_split_work(int64_t B, int q, int64_t n, int kc_len, int64_t* work_elems) {

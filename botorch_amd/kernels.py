@@ -487,7 +487,14 @@ def post_partials_members(caches, X: torch.Tensor, store_R: bool = False) -> lis
     B, q, d = X.shape
     same = all(c.n == c0.n and c.np == c0.np and c.d == c0.d for c in caches)
     nparts = small_plan(B, q, c0.n) if same and 1 < len(caches) <= 8 else 0
-    if nparts == 0 or c0.np * geometry(B, q, c0.n)[1] * 8 > kxt_cap(_dev(X)):
+    fits = c0.np * geometry(B, q, c0.n)[1] * 8 <= kxt_cap(_dev(X))
+    if nparts == 0 and same and 1 < len(caches) <= 8 and fits and MEMBERS_STREAMK:
+        we = ctypes.c_int64()
+        check(lib().bo_post_members_work(len(caches), B, q, c0.n, ctypes.byref(we)),
+              "post_members_work")
+        if we.value >= 0:
+            return _post_members_streamk(caches, X, store_R, we.value)
+    if nparts == 0 or not fits:
         return [post_partials(c, X, store_R=store_R) for c in caches]
     dev = _dev(X)
     Qp, nrows_pad, nC = geometry(B, q, c0.n)
@@ -512,6 +519,46 @@ def post_partials_members(caches, X: torch.Tensor, store_R: bool = False) -> lis
         TIMING_HOOK("post_partials_begin")
     check(lib().bo_post_small_batched(nm, arr["Kt"], arr["U"], arr["beta"], arr["S"], arr["m"],
                                       arr["Rt"], B, q, c0.n, c0.np, st), "post_small_batched")
+    if TIMING_HOOK is not None:
+        TIMING_HOOK("post_partials_end")
+    return pps
+
+
+# BO_POST_MEMBERS=0: one stream-K launch per member instead (A/B knob)
+MEMBERS_STREAMK = os.environ.get("BO_POST_MEMBERS", "1") != "0"
+
+
+def _post_members_streamk(caches, X: torch.Tensor, store_R: bool, work_elems: int) -> list:
+    """post_partials_members on the 128-tile kernel: every member's K*x^T,
+    then ONE member-batched stream-K launch + one reduction
+    (bo_post_partials_members); nC column-tile partials per member."""
+    c0 = caches[0]
+    dev = _dev(X)
+    B, q, d = X.shape
+    Qp, nrows_pad, nC = geometry(B, q, c0.n)
+    f64 = dict(dtype=torch.float64, device=dev)
+    st = _stream(dev)
+    Xc = X.contiguous()
+    pps, ptrs = [], {k: [] for k in ("Kt", "U", "beta", "S", "m", "Rt")}
+    for c in caches:
+        Xq = torch.empty(nrows_pad, DP, **f64)
+        Kt = torch.empty(c.np, nrows_pad, **f64)
+        check(lib().bo_post_kxt_rows(c.kind, _p(Xc), B, q, d, _p(c.lengthscale), _p(c.Xt_scaled),
+                                     c.n, c.outputscale, _p(Xq), _p(Kt), st), "post_kxt_rows")
+        Sp = torch.empty(nC, nrows_pad // 16, 16, 16, **f64)
+        mp = torch.empty(nC, nrows_pad, **f64)
+        Rt = torch.empty(nC * 128, nrows_pad, **f64) if store_R else None
+        pps.append(PostPartials(B, q, Qp, nrows_pad, nC, Xq, Sp, mp, Rt))
+        for k, t in (("Kt", Kt), ("U", c.U), ("beta", c.beta), ("S", Sp), ("m", mp), ("Rt", Rt)):
+            ptrs[k].append(_p(t).value if t is not None else None)
+    nm = len(caches)
+    arr = {k: (ctypes.c_void_p * nm)(*v) for k, v in ptrs.items()}
+    work = torch.empty(max(1, work_elems), **f64)
+    if TIMING_HOOK is not None:
+        TIMING_HOOK("post_partials_begin")
+    check(lib().bo_post_partials_members(nm, arr["Kt"], arr["U"], arr["beta"], arr["S"], arr["m"],
+                                         arr["Rt"] if store_R else None, _p(pps[0].Xq), B, q, c0.n,
+                                         c0.np, _p(work), st), "post_partials_members")
     if TIMING_HOOK is not None:
         TIMING_HOOK("post_partials_end")
     return pps
@@ -926,6 +973,38 @@ def raise_not_psd_deferred(info: torch.Tensor, jitter: torch.Tensor, what: str) 
     # this call's status is enqueued, the previous call's read (one forward behind)
     prev = _lib.torch_ops().ladder_defer(info.contiguous(), jitter.contiguous())
     ladder_prev_outcome(prev, _dev_index(info.device), what)
+
+
+def raise_not_psd_many(pairs, what: str) -> None:
+    """_raise_not_psd over several ladders (a ModelListGP's members) with ONE
+    device-to-host read, issued after the caller has enqueued its remaining
+    work: the members' statuses are packed side by side, then raised / warned
+    in member order, as the per-member checks would.  Under graph capture,
+    the per-member path (its capture slot)."""
+    pairs = [(i, j) for i, j in pairs if i.numel()]
+    if not pairs:
+        return
+    dev = pairs[0][0].device
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx in _CAPTURE or len(pairs) == 1:
+        for info, jitter in pairs:
+            _raise_not_psd(info, jitter, what)
+        return
+    packed = torch.empty(len(pairs), 2, dtype=torch.float64, device=dev)
+    for m, (info, jitter) in enumerate(pairs):
+        check(lib().bo_ladder_status(_p(info.contiguous()), _p(jitter.contiguous()), info.numel(),
+                                     _p(packed[m]), _stream(dev)), "ladder_status")
+    packed = packed.cpu()
+    for m in range(len(pairs)):
+        if packed[m, 0] > 0:
+            from .exceptions import NotPSDError
+            raise NotPSDError(f"{what}: matrix not positive definite after repeatedly adding "
+                              f"jitter up to {CHOLESKY_JITTER_F64 * 10 ** (CHOLESKY_MAX_TRIES - 1):.1e}")
+        if packed[m, 1] > 0:
+            import warnings
+            from .exceptions import NumericalWarning
+            warnings.warn(f"A not p.d., added jitter of {float(packed[m, 1]):.1e} to the diagonal",
+                          NumericalWarning)
 
 
 def _raise_not_psd(info: torch.Tensor, jitter: torch.Tensor, what: str):

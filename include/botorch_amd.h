@@ -347,6 +347,20 @@ int bo_post_small_batched(int nm, const double* const* Kt, const double* const* 
                           const double* const* beta, double* const* Spart, double* const* mpart,
                           double* const* Rt, int64_t B, int q, int64_t n, int64_t ldu,
                           void* stream);
+/* The same nm <= 8 models' partials where the one-model plan is stream-K
+ * (C4: ModelListGP(3), n = 2048, q = 8, b = 128): ONE stream-K launch over
+ * every member's 128 x 128 tiles plus one split-k reduction, replacing one
+ * bo_post_partials per member (models/model_list_gp.py -> [G]
+ * ModelListGP.posterior's per-model loop).  Spart[m] / mpart[m] hold nC
+ * column-tile partials (bo_post_partials' layout); Rt[m] (optional) R^T
+ * row-major; Xq0 any member's padded rows (bo_post_kxt_rows).
+ * bo_post_members_work: the shared workspace in doubles, -1 where the
+ * one-model plan is not stream-K (one launch per model then). */
+int bo_post_members_work(int nm, int64_t B, int q, int64_t n, int64_t* work_elems);
+int bo_post_partials_members(int nm, const double* const* Kt, const double* const* U,
+                             const double* const* beta, double* const* Spart, double* const* mpart,
+                             double* const* Rt, const double* Xq0, int64_t B, int q, int64_t n,
+                             int64_t ldu, double* work, void* stream);
 /* A^{-1} = L^{-T} L^{-1} for the MLL gradient (replaces the U U^T GEMM of
  * fit.py's closure, optim/closures/model_closures.py:171-184 -> [G]
  * ExactMarginalLogLikelihood backward): Linv np x np (ld = np = n rounded up

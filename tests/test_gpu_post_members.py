@@ -1,0 +1,90 @@
+"""Member-batched stream-K posterior (bo_post_partials_members, round 5): the
+posterior partials of a ModelListGP's members (models/model_list_gp.py ->
+[G] ModelListGP.posterior, one posterior per member) in ONE stream-K launch
+over all members' 128 x 128 tiles and one split-k reduction, where the
+one-model plan is stream-K.  Compared member by member with the one-model
+128-tile route (the same sums cut at other k positions: 1e-12 relative, 1e-11 absolute), R^T
+included, and end to end through qEHVI values and gradients (C4's shape)."""
+import ctypes
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _models(n, m=3, seed=0):
+    from botorch_amd.models import SingleTaskGP
+    from botorch_amd.test_functions import DTLZ2
+    g = torch.Generator().manual_seed(seed)
+    X = torch.rand(n, 6, generator=g, dtype=torch.float64)
+    Y = -DTLZ2(dim=6, num_objectives=m, negate=True).evaluate_true(X)
+    out = []
+    for t in range(m):
+        mm = SingleTaskGP(X.to(DEV), Y[:, t:t + 1].to(DEV))
+        mm.covar_module.lengthscale = torch.full((1, 6), 0.5 + 0.1 * t, dtype=torch.float64)
+        mm.likelihood.noise = torch.tensor([1e-3], dtype=torch.float64)
+        out.append(mm.eval())
+    return X, Y, out
+
+
+def _members_work(nm, B, q, n):
+    from botorch_amd._lib import check, lib
+    we = ctypes.c_int64()
+    check(lib().bo_post_members_work(nm, B, q, n, ctypes.byref(we)), "post_members_work")
+    return we.value
+
+
+@pytest.mark.parametrize("n,B,q,store_R", [(2048, 128, 8, False),   # C4
+                                           (2048, 128, 8, True),
+                                           (1500, 40, 5, True)])    # ragged n, odd q
+def test_members_route_matches_one_model_route(n, B, q, store_R):
+    from botorch_amd import kernels
+    _, _, models = _models(n)
+    if _members_work(len(models), B, q, n) < 0:
+        pytest.skip("one-model plan not stream-K at this shape")
+    caches = [mm.prediction_cache() for mm in models]
+    X = torch.rand(B, q, 6, dtype=torch.float64, generator=torch.Generator().manual_seed(7)).to(DEV)
+    pps = kernels._post_members_streamk(caches, X, store_R,
+                                        _members_work(len(models), B, q, n))
+    for c, pp in zip(caches, pps):
+        ref = kernels.post_partials(c, X, store_R=store_R, small=False)
+        assert pp.Spart.shape == ref.Spart.shape
+        # per-tile partials summed: the same R R^T / R beta as the one-model route
+        # (k-sums cut at other positions: rounding of O(1e-16) x the terms'
+        # magnitude, so an absolute floor for the entries that cancel)
+        torch.testing.assert_close(pp.Spart.sum(0), ref.Spart.sum(0), rtol=1e-12, atol=1e-11)
+        torch.testing.assert_close(pp.mpart.sum(0), ref.mpart.sum(0), rtol=1e-12, atol=1e-11)
+        if store_R:
+            torch.testing.assert_close(pp.Rt, ref.Rt, rtol=1e-12, atol=1e-11)
+
+
+def test_qehvi_members_route_values_and_gradients(monkeypatch):
+    """C4-shaped qEHVI through the members route and through one launch per
+    member (BO_POST_MEMBERS off): values 1e-12, gradients 1e-10."""
+    from botorch_amd import kernels
+    from botorch_amd.acquisition import qExpectedHypervolumeImprovement
+    from botorch_amd.models import ModelListGP
+    from botorch_amd.multi_objective import FastNondominatedPartitioning
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    _, Y, models = _models(2048)
+    ref = torch.full((3,), -1.1, dtype=torch.float64)
+    part = FastNondominatedPartitioning(ref, Y)
+    acqf = qExpectedHypervolumeImprovement(ModelListGP(*models), ref.tolist(), part,
+                                           sampler=SobolQMCNormalSampler(torch.Size([128]), seed=0))
+    X = torch.rand(128, 8, 6, dtype=torch.float64, generator=torch.Generator().manual_seed(3)).to(DEV)
+    assert _members_work(3, 128, 8, 2048) >= 0  # C4 takes the members route
+
+    def run():
+        Xg = X.clone().requires_grad_(True)
+        v = acqf(Xg)
+        (g,) = torch.autograd.grad(v.sum(), Xg)
+        return v.detach().cpu(), g.cpu()
+
+    v1, g1 = run()
+    monkeypatch.setattr(kernels, "MEMBERS_STREAMK", False)
+    v0, g0 = run()
+    assert (v0 > 0).sum() > 10
+    torch.testing.assert_close(v1, v0, rtol=1e-12, atol=1e-14)
+    torch.testing.assert_close(g1, g0, rtol=1e-10, atol=1e-12)
