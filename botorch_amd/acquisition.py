@@ -905,33 +905,45 @@ class _FusedQEHVI(torch.autograd.Function):
         models = acqf.model.models
         need_grad = ctx.needs_input_grad[0]
         q = X3.shape[-2]
-        means, Ls, saved = [], [], []
+        saved = []
         keys = prime_prediction_caches(models)
         caches = [mm.prediction_cache(key=key) for mm, key in zip(models, keys)]
         # every member's posterior partials in one launch where the small-grid
         # plan applies (C4: the three outputs of the ModelListGP)
         pps = kernels.post_partials_members(caches, X3.detach(), store_R=need_grad)
         status = []
-        for mm, cache, pp in zip(models, caches, pps):
+        # every member's mean and q x q root written straight into its slice of
+        # the stacked m x B x q (x q) inputs of the qEHVI launch (no stack copies)
+        f64 = dict(dtype=torch.float64, device=X3.device)
+        mean = torch.empty(len(models), X3.shape[0], q, **f64)
+        L = torch.empty(len(models), X3.shape[0], q, q, **f64)
+        # outside graph capture the finalisation launches fold their ladder
+        # outcomes straight into pinned words (no status launches or copy)
+        idx = kernels._dev_index(X3.device)
+        ps = kernels.pinned_status(X3.device) if (idx not in kernels._CAPTURE and
+                                                  len(models) <= 8) else None
+        words = ps.arm(len(models)) if ps is not None else [None] * len(models)
+        for t, (mm, cache, pp) in enumerate(zip(models, caches, pps)):
             ymean, ystd = mm.outcome_stats()
             out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
-                                       want_cov=False, want_L=True)
+                                       want_cov=False, want_L=True, mean_out=mean[t], L_out=L[t],
+                                       status=words[t])
             status.append((out["info"], out["jitter"]))
-            means.append(out["mean"])
-            Ls.append(out["L"])
             if need_grad:
                 saved.append((cache, pp, ystd, kernels.w_matrix(cache, pp)))
         sampler = acqf._ensure_sampler()
         Z = sampler.base_samples_2d(q * len(models), X3.device)
         lo, hi = acqf._cells(X3.device)
-        mean, L = torch.stack(means), torch.stack(Ls)
         # the kernel itself (as the backward below): this Function already is
         # the autograd node, the registered op's wrapper would only add host time
         acq = kernels.qehvi(mean, L, Z, lo, hi)
         # the members' ladders checked once, behind the qEHVI launch (one host
         # read per forward instead of one per member, each of which drained
         # the queue: ~40 us of idle device between members at C4)
-        kernels.raise_not_psd_many(status, "qEHVI posterior root")
+        if ps is not None:
+            kernels.raise_not_psd_members(ps, len(models), X3.device, "qEHVI posterior root")
+        else:
+            kernels.raise_not_psd_many(status, "qEHVI posterior root")
         if need_grad:
             ctx.saved, ctx.mean, ctx.L, ctx.Z, ctx.cells = saved, mean, L, Z, (lo, hi)
         return acq

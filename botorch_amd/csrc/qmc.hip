@@ -18,6 +18,8 @@
 //      q-max and the sample sum are wavefront shuffle reductions (an online
 //      (max, sum-exp) pair for logmeanexp).
 #include "common.h"
+
+#include <cstring>
 #include "logred.h"
 
 namespace {
@@ -714,6 +716,19 @@ extern "C" int bo_ladder_status(const int* info, const double* jitter, int64_t B
   BO_CHECK_ARG(B >= 0 && info && jitter && out, "bo_ladder_status: bad arguments");
   ladder_status_kernel<<<1, 256, 0, as_stream(stream)>>>(info, jitter, B, out);
   BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+extern "C" int bo_pinned_alloc(int64_t bytes, void** host, void** dev) {
+  BO_CHECK_ARG(bytes > 0 && host && dev, "bo_pinned_alloc: bad arguments");
+  BO_HIP(hipHostMalloc(host, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(*host, 0, (size_t)bytes);
+  BO_HIP(hipHostGetDevicePointer(dev, *host, 0));
+  return BO_OK;
+}
+
+extern "C" int bo_pinned_free(void* host) {
+  if (host) BO_HIP(hipHostFree(host));
   return BO_OK;
 }
 

@@ -671,14 +671,22 @@ def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd
                  best_f_s: Optional[torch.Tensor] = None, want_mean=True, want_cov=True,
                  want_L=False, max_tries=CHOLESKY_MAX_TRIES, jitter0=CHOLESKY_JITTER_F64,
                  T: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,
-                 log_params: Optional[tuple] = None):
-    """log_params = (fat, tau_relu, tau_max) for the qLogEI / qLogNEI modes."""
+                 log_params: Optional[tuple] = None, mean_out: Optional[torch.Tensor] = None,
+                 L_out: Optional[torch.Tensor] = None, status=None):
+    """log_params = (fat, tau_relu, tau_max) for the qLogEI / qLogNEI modes.
+    mean_out / L_out: contiguous B x q / B x q x q buffers to write instead of
+    fresh ones (a ModelListGP's members straight into their stacked slices).
+    status: (status_out, status_count) device pointers the launch folds the
+    ladder's [max info, max jitter] into (pinned_status().arm)."""
     dev = pp.Xq.device
     B, q = pp.B, pp.q
     f64 = dict(dtype=torch.float64, device=dev)
-    mean = torch.empty(B, q, **f64) if want_mean else None
+    for t, shp in ((mean_out, (B, q)), (L_out, (B, q, q))):
+        if t is not None and (tuple(t.shape) != shp or not t.is_contiguous() or t.dtype != torch.float64):
+            raise ValueError(f"qmc_finalize: output buffer must be contiguous fp64 {shp}")
+    mean = (mean_out if mean_out is not None else torch.empty(B, q, **f64)) if want_mean else None
     cov = torch.empty(B, q, q, **f64) if want_cov else None
-    L = torch.empty(B, q, q, **f64) if want_L else None
+    L = (L_out if L_out is not None else torch.empty(B, q, q, **f64)) if want_L else None
     need_mc = mode in (_lib.QMC_QEI, _lib.QMC_QNEI) + _lib.LOG_MODES
     fat, tau_relu, tau_max = log_params if log_params is not None else (1, 1.0, 1.0)
     acq = torch.empty(B, **f64) if need_mc else None
@@ -696,7 +704,9 @@ def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd
                              r=T.shape[0] if T is not None else 0, fat=int(bool(fat)),
                              ldT=T.shape[1] if T is not None else 0, F=F,
                              ldF=F.shape[1] if F is not None else 0, tau_relu=float(tau_relu),
-                             tau_max=float(tau_max), nparts=int(pp.Spart.shape[0]))
+                             tau_max=float(tau_max), nparts=int(pp.Spart.shape[0]),
+                             status_out=status[0] if status else None,
+                             status_count=status[1] if status else None)
     check(lib().bo_qmc_finalize_v(ctypes.byref(a), _stream(dev)), "qmc_finalize")
     return dict(acq=acq, mean=mean, cov=cov, L=L, info=info, jitter=jit)
 
@@ -973,6 +983,63 @@ def raise_not_psd_deferred(info: torch.Tensor, jitter: torch.Tensor, what: str) 
     # this call's status is enqueued, the previous call's read (one forward behind)
     prev = _lib.torch_ops().ladder_defer(info.contiguous(), jitter.contiguous())
     ladder_prev_outcome(prev, _dev_index(info.device), what)
+
+
+class _PinnedStatus:
+    """Per device: 8 pairs of pinned, device-mapped status words and 8 device
+    arrival counters -- where bo_qmc_finalize folds each member's ladder
+    outcome (status_out / status_count) for raise_not_psd_members."""
+
+    def __init__(self, dev):
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().bo_pinned_alloc(16 * 8, ctypes.byref(h), ctypes.byref(d)), "pinned_alloc")
+        self.host_ptr, self.dev_ptr = h.value, d.value
+        self.words = (ctypes.c_double * 16).from_address(self.host_ptr)
+        self.count = torch.zeros(8, dtype=torch.int32, device=dev)  # kernels re-zero them
+
+    def arm(self, m: int):
+        """Zero the first m pairs; (status_out, status_count) pointers of each."""
+        ctypes.memset(self.host_ptr, 0, 16 * m)
+        base = self.count.data_ptr()
+        return [(self.dev_ptr + 16 * t, base + 4 * t) for t in range(m)]
+
+    def __del__(self):
+        try:
+            lib().bo_pinned_free(ctypes.c_void_p(self.host_ptr))
+        except Exception:  # interpreter shutdown
+            pass
+
+
+_PINNED = {}
+
+
+def pinned_status(dev) -> "_PinnedStatus":
+    idx = _dev_index(dev)
+    if idx not in _PINNED:
+        _PINNED[idx] = _PinnedStatus(torch.device("cuda", idx))
+    return _PINNED[idx]
+
+
+def raise_not_psd_members(ps: "_PinnedStatus", m: int, dev, what: str) -> None:
+    """The members' ladder outcomes folded into ps's pinned words by their
+    finalisation launches: one stream sync, then raised / warned in member
+    order as per-member checks would (no status launch, no copy)."""
+    _stream_sync(dev)
+    w = ps.words
+    for t in range(m):
+        if w[2 * t] > 0:
+            from .exceptions import NotPSDError
+            raise NotPSDError(f"{what}: matrix not positive definite after repeatedly adding "
+                              f"jitter up to {CHOLESKY_JITTER_F64 * 10 ** (CHOLESKY_MAX_TRIES - 1):.1e}")
+        if w[2 * t + 1] > 0:
+            import warnings
+            from .exceptions import NumericalWarning
+            warnings.warn(f"A not p.d., added jitter of {float(w[2 * t + 1]):.1e} to the diagonal",
+                          NumericalWarning)
+
+
+def _stream_sync(dev):
+    torch.cuda.current_stream(torch.device("cuda", _dev_index(dev))).synchronize()
 
 
 def raise_not_psd_many(pairs, what: str) -> None:

@@ -162,6 +162,14 @@ int bo_cholesky_jitter(const double* A, int64_t n, double* L, double* Linv, doub
  * [G] psd_safe_cholesky's torch.any(info) check does. */
 int bo_ladder_status(const int* info, const double* jitter, int64_t B, double* out, void* stream);
 
+/* Pinned, device-mapped, coherent host memory (zeroed): *host for the CPU,
+ * *dev for kernels -- the status words bo_qmc_finalize folds a ladder's
+ * outcome into (BoQmcFinalizeArgs.status_out), read by the host after a
+ * stream sync without a status launch or copy (a ModelListGP's members in
+ * the qEHVI forward).  bo_pinned_free releases it. */
+int bo_pinned_alloc(int64_t bytes, void** host, void** dev);
+int bo_pinned_free(void* host);
+
 /* Pareto masks of S point sets (Y: S x n x m, m <= 8; out: S x n bytes, 1 =
  * non-dominated): no other point is >= in every objective and > in one
  * (maximize; <= / < otherwise); dedup also drops later copies of equal points.

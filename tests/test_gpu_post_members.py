@@ -88,3 +88,45 @@ def test_qehvi_members_route_values_and_gradients(monkeypatch):
     assert (v0 > 0).sum() > 10
     torch.testing.assert_close(v1, v0, rtol=1e-12, atol=1e-14)
     torch.testing.assert_close(g1, g0, rtol=1e-10, atol=1e-12)
+
+
+def test_qehvi_member_status_words(monkeypatch):
+    """The members' ladder outcomes reach the host through the pinned words
+    their finalisation launches fold into (sticky max): a word seeded with a
+    jitter warns, one seeded with a failure raises NotPSDError, clean calls
+    neither (the reference's per-member psd_safe_cholesky outcomes)."""
+    import warnings
+    from botorch_amd import kernels
+    from botorch_amd.acquisition import qExpectedHypervolumeImprovement
+    from botorch_amd.exceptions import NotPSDError, NumericalWarning
+    from botorch_amd.models import ModelListGP
+    from botorch_amd.multi_objective import FastNondominatedPartitioning
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    _, Y, models = _models(512)
+    ref = torch.full((3,), -1.1, dtype=torch.float64)
+    acqf = qExpectedHypervolumeImprovement(ModelListGP(*models), ref.tolist(),
+                                           FastNondominatedPartitioning(ref, Y),
+                                           sampler=SobolQMCNormalSampler(torch.Size([64]), seed=0))
+    X = torch.rand(16, 4, 6, dtype=torch.float64, generator=torch.Generator().manual_seed(2)).to(DEV)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", NumericalWarning)
+        acqf(X)  # clean: no warning, no error
+    orig = kernels._PinnedStatus.arm
+    seed = {}
+
+    def arm(self, m):
+        out = orig(self, m)
+        for i, v in seed.items():
+            self.words[i] = v
+        return out
+
+    monkeypatch.setattr(kernels._PinnedStatus, "arm", arm)
+    seed.update({3: 1e-6})  # member 1 added jitter
+    with pytest.warns(NumericalWarning, match="1.0e-06"):
+        acqf(X)
+    seed.clear()
+    seed.update({4: 1.0})  # member 2 failed
+    with pytest.raises(NotPSDError):
+        acqf(X)
+    seed.clear()
+    acqf(X)
