@@ -892,6 +892,46 @@ class qLogNoisyExpectedImprovement(qNoisyExpectedImprovement):
 
 
 # -- qEHVI ---------------------------------------------------------------------------
+def _qehvi_members_eager(acqf, X3: torch.Tensor):
+    """Forward-only qEHVI through ONE native call (bo::qehvi_members_eager:
+    every member's rows, K*x^T, posterior partials, finalisation and the
+    qEHVI launch, issued from C++), then one stream sync and the members'
+    ladder outcomes from pinned words, raised / warned in member order.
+    None where it does not apply (graph capture; members of unequal shape or
+    kernel; more than 8 members): the caller takes _FusedQEHVI."""
+    dev = X3.device
+    idx = kernels._dev_index(dev)
+    if idx in kernels._CAPTURE:
+        return None
+    models = acqf.model.models
+    if len(models) > 8:
+        return None
+    keys = prime_prediction_caches(models)
+    key = (tuple(keys), idx)
+    args = acqf.__dict__.get("_native_args")
+    if args is None or args[0] != key:
+        caches = [mm.prediction_cache(key=k) for mm, k in zip(models, keys)]
+        c0 = caches[0]
+        if not all(c.n == c0.n and c.np == c0.np and c.d == c0.d and c.kind == c0.kind
+                   and c.U.numel() for c in caches):
+            return None
+        stats = [mm.outcome_stats() for mm in models]
+        args = (key, [c.Xt_scaled for c in caches], [c.U for c in caches],
+                [c.beta for c in caches], [c.lengthscale for c in caches],
+                [float(c.outputscale) for c in caches], [float(c.constant) for c in caches],
+                [float(m_) for m_, _ in stats], [float(s_) for _, s_ in stats], int(c0.kind),
+                int(c0.n))
+        acqf.__dict__["_native_args"] = args
+    q = X3.shape[-2]
+    Z = acqf._ensure_sampler().base_samples_2d(q * len(models), dev)
+    lo, hi = acqf._cells(dev)
+    acq, status = _lib.torch_ops().qehvi_members_eager(
+        X3.contiguous(), *args[1:], Z, lo, hi, kernels.kxt_cap(dev))
+    kernels._stream_sync(dev)
+    kernels.raise_status_words(status.tolist(), "qEHVI posterior root")
+    return acq
+
+
 class _FusedQEHVI(torch.autograd.Function):
     """qEHVI of B t-batches over a ModelListGP, with its gradient.
 
@@ -1017,7 +1057,11 @@ class qExpectedHypervolumeImprovement(MCAcquisitionFunction):
             raise UnsupportedError("only the identity multi-output objective is accelerated")
         if q > 12 or d > kernels.DP:
             raise UnsupportedError("fused qEHVI supports q <= 12 and d <= 8")
-        acq = _FusedQEHVI.apply(X3, self)
+        acq = None
+        if not (torch.is_grad_enabled() and X3.requires_grad) and X3.dtype == torch.float64:
+            acq = _qehvi_members_eager(self, X3)
+        if acq is None:
+            acq = _FusedQEHVI.apply(X3, self)
         return acq.reshape(batch)
 
 

@@ -603,9 +603,224 @@ at::Tensor post_timing_read() {
   return out;
 }
 
+// ---- qEHVI over a ModelListGP's members, forward only --------------------------------
+// Per device: 8 pairs of pinned, device-mapped status words (one per member)
+// and their arrival counters; the finalisation launches fold each member's
+// ladder outcome into its pair, the caller reads them after a stream sync.
+struct MemberStatus {
+  double* host = nullptr;
+  double* dev = nullptr;
+  int* count = nullptr;
+};
+std::mutex g_member_mu;
+std::unordered_map<int, MemberStatus> g_member;
+
+MemberStatus& member_status(int dev) {
+  auto& M = g_member[dev];
+  if (!M.host) {
+    hk(hipHostMalloc(reinterpret_cast<void**>(&M.host), 16 * sizeof(double),
+                     hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+    hk(hipHostGetDevicePointer(reinterpret_cast<void**>(&M.dev), M.host, 0), "hipHostGetDevicePointer");
+    hk(hipMalloc(reinterpret_cast<void**>(&M.count), 8 * sizeof(int)), "hipMalloc");
+    hk(hipMemset(M.count, 0, 8 * sizeof(int)), "hipMemset");
+  }
+  return M;
+}
+
+// The qEHVI forward of acquisition/multi_objective/monte_carlo.py:146-322 over
+// a ModelListGP of m <= 8 exact GPs of one shape (models/model_list_gp.py ->
+// one posterior per member), in one host call: every member's rows and K*x^T,
+// the members' R R^T / R beta partials (one small-grid or member-batched
+// stream-K launch where those plans apply, else one launch per member), each
+// member's finalisation (mean + jittered q x q root, written into the stacked
+// m x B x q (x q) inputs, ladder outcome folded into pinned words), then the
+// qEHVI launch.  Returns [acq, status]: status is an m x 2 host view of the
+// pinned words ([max info, max jitter] per member), valid once the caller has
+// synchronised the stream (the caller raises / warns in member order).
+std::vector<at::Tensor> qehvi_members_eager(
+    const at::Tensor& X, at::TensorList Xt_scaled, at::TensorList U, at::TensorList beta,
+    at::TensorList lengthscale, at::ArrayRef<double> outputscale, at::ArrayRef<double> constant,
+    at::ArrayRef<double> ymean, at::ArrayRef<double> ystd, int64_t kind, int64_t n,
+    const at::Tensor& Z, const at::Tensor& cell_lo, const at::Tensor& cell_hi, int64_t kxt_cap) {
+  check_f64(X, "X");
+  check_f64(Z, "Z");
+  check_f64(cell_lo, "cell_lo");
+  check_f64(cell_hi, "cell_hi");
+  const int M = static_cast<int>(U.size());
+  TORCH_CHECK(M >= 1 && M <= 8 && Xt_scaled.size() == size_t(M) && beta.size() == size_t(M) &&
+                  lengthscale.size() == size_t(M) && outputscale.size() == size_t(M) &&
+                  constant.size() == size_t(M) && ymean.size() == size_t(M) && ystd.size() == size_t(M),
+              "bo::qehvi_members_eager: 1..8 members, one entry per member in every list");
+  TORCH_CHECK(X.dim() == 3, "bo::qehvi_members_eager: X must be B x q x d");
+  const int B = static_cast<int>(X.size(0)), q = static_cast<int>(X.size(1)),
+            d = static_cast<int>(X.size(2));
+  TORCH_CHECK(cell_lo.dim() == 2 && cell_lo.size(1) == M && cell_hi.sizes() == cell_lo.sizes(),
+              "bo::qehvi_members_eager: shared K x m cells");
+  TORCH_CHECK(Z.dim() == 2 && Z.size(1) == int64_t(q) * M, "bo::qehvi_members_eager: Z must be S x (q m)");
+  const int64_t np = U[0].size(0);
+  for (int m = 0; m < M; ++m) {
+    check_f64(Xt_scaled[m], "Xt_scaled");
+    check_f64(U[m], "U");
+    check_f64(beta[m], "beta");
+    check_f64(lengthscale[m], "lengthscale");
+    TORCH_CHECK(U[m].size(0) == np && Xt_scaled[m].size(0) == n && lengthscale[m].numel() == d,
+                "bo::qehvi_members_eager: members of one shape (n, d) only");
+  }
+  const int dev = X.device().index();
+  void* st = c10::hip::getCurrentHIPStream(dev).stream();
+  auto f64 = X.options().dtype(at::kDouble);
+  auto acq = at::empty({B}, f64);
+  std::lock_guard<std::mutex> lk(g_member_mu);
+  MemberStatus& ms = member_status(dev);
+  for (int e = 0; e < 2 * M; ++e) ms.host[e] = 0.0;
+  auto status = at::from_blob(ms.host, {M, 2}, at::TensorOptions().dtype(at::kDouble));
+  if (B == 0) return {acq, status};
+
+  int Qp = 0, nrows = 0, nC = 0;
+  ck(bo_post_geometry(B, q, n, &Qp, &nrows, &nC), "post_geometry");
+  const bool kxt = np * int64_t(nrows) * 8 <= kxt_cap;
+  int nsmall = 0;
+  int64_t wmem = -1;
+  if (kxt) {
+    ck(bo_post_small_plan(B, q, n, &nsmall), "post_small_plan");
+    if (nsmall == 0 && M > 1) ck(bo_post_members_work(M, B, q, n, &wmem), "post_members_work");
+  }
+  int kc = 0;
+  int64_t we = 0;
+  if (nsmall == 0 && wmem < 0) ck(bo_post_split_plan(B, q, n, 0, &kc, &we), "post_split_plan");
+  const int nparts = nsmall > 0 ? nsmall : nC;
+  const int64_t wsz = wmem >= 0 ? wmem : (kc ? we : 0);
+
+  // one workspace (offsets in doubles, 16-B aligned)
+  auto al2 = [](int64_t v) { return (v + 1) & ~int64_t(1); };
+  const int64_t s_xq = al2(int64_t(nrows) * 8), s_kt = kxt ? al2(np * nrows) : 0,
+                s_sp = al2(int64_t(nparts) * nrows * 16), s_mp = al2(int64_t(nparts) * nrows);
+  const int64_t per = s_xq + s_kt + s_sp + s_mp;
+  const int64_t o_work = per * M;
+  const int64_t o_mean = o_work + al2(std::max<int64_t>(wsz, 0));
+  const int64_t o_L = o_mean + al2(int64_t(M) * B * q);
+  const int64_t o_jit = o_L + al2(int64_t(M) * B * q * q);
+  const int64_t o_info = o_jit + al2(int64_t(M) * B);
+  const int64_t o_qw = o_info + al2((int64_t(M) * B + 1) / 2);
+  const int64_t total = o_qw + al2(8 * int64_t(B));
+  auto ws = at::empty({total}, f64);
+  double* w = ws.data_ptr<double>();
+  const double* Kt_p[8];
+  const double* U_p[8];
+  const double* b_p[8];
+  double* S_p[8];
+  double* m_p[8];
+  double* Xq_p[8];
+  for (int m = 0; m < M; ++m) {
+    double* base = w + per * m;
+    Xq_p[m] = base;
+    Kt_p[m] = kxt ? base + s_xq : nullptr;
+    S_p[m] = base + s_xq + s_kt;
+    m_p[m] = base + s_xq + s_kt + s_sp;
+    U_p[m] = U[m].data_ptr<double>();
+    b_p[m] = beta[m].data_ptr<double>();
+    if (kxt)
+      ck(bo_post_kxt_rows(int(kind), X.data_ptr<double>(), B, q, d, lengthscale[m].data_ptr<double>(),
+                          Xt_scaled[m].data_ptr<double>(), n, outputscale[m], Xq_p[m],
+                          const_cast<double*>(Kt_p[m]), st), "post_kxt_rows");
+    else
+      ck(bo_prepare_rows(X.data_ptr<double>(), B, q, d, lengthscale[m].data_ptr<double>(), Xq_p[m], st),
+         "prepare_rows");
+  }
+  hipEvent_t t0 = nullptr;
+  {
+    std::lock_guard<std::mutex> tl(g_time_mu);
+    if (g_time_on) t0 = timing_event(st);
+  }
+  if (nsmall > 0) {
+    double* const* no_rt = nullptr;
+    ck(bo_post_small_batched(M, Kt_p, U_p, b_p, S_p, m_p, no_rt, B, q, n, np, st), "post_small_batched");
+  } else if (wmem >= 0) {
+    ck(bo_post_partials_members(M, Kt_p, U_p, b_p, S_p, m_p, nullptr, Xq_p[0], B, q, n, np,
+                                w + o_work, st), "post_partials_members");
+  } else {
+    for (int m = 0; m < M; ++m) {
+      BoPostPartialsArgs pa{};
+      pa.struct_size = sizeof(pa);
+      pa.abi_version = BO_ABI_VERSION;
+      pa.kind = int(kind);
+      pa.B = B;
+      pa.q = q;
+      pa.d = d;
+      pa.Xq = Xq_p[m];
+      pa.Xt_scaled = Xt_scaled[m].data_ptr<double>();
+      pa.n = n;
+      pa.U = U_p[m];
+      pa.ldu = np;
+      pa.beta = b_p[m];
+      pa.outputscale = outputscale[m];
+      pa.Spart = S_p[m];
+      pa.mpart = m_p[m];
+      pa.kc_len = kc;
+      pa.work = kc ? w + o_work : nullptr;
+      pa.Kt = Kt_p[m];
+      ck(bo_post_partials_v(&pa, st), "post_partials");
+    }
+  }
+  if (t0) {
+    std::lock_guard<std::mutex> tl(g_time_mu);
+    g_time_ev.emplace_back(t0, timing_event(st));
+  }
+  double* mean = w + o_mean;
+  double* Lq = w + o_L;
+  for (int m = 0; m < M; ++m) {
+    BoQmcFinalizeArgs fa{};
+    fa.struct_size = sizeof(fa);
+    fa.abi_version = BO_ABI_VERSION;
+    fa.kind = int(kind);
+    fa.mode = BO_QMC_CHOL;
+    fa.B = B;
+    fa.q = q;
+    fa.Xq = Xq_p[m];
+    fa.Spart = S_p[m];
+    fa.mpart = m_p[m];
+    fa.n = n;
+    fa.outputscale = outputscale[m];
+    fa.constant = constant[m];
+    fa.ymean = ymean[m];
+    fa.ystd = ystd[m];
+    fa.max_tries = 6;   // botorch/__init__.py:47 (cholesky_max_tries)
+    fa.jitter0 = 1e-8;  // [G] cholesky_jitter, double
+    fa.mean_out = mean + int64_t(m) * B * q;
+    fa.L_out = Lq + int64_t(m) * B * q * q;
+    fa.info_out = reinterpret_cast<int*>(w + o_info) + int64_t(m) * B;
+    fa.jitter_out = w + o_jit + int64_t(m) * B;
+    fa.nparts = nsmall;
+    fa.status_out = ms.dev + 2 * m;
+    fa.status_count = ms.count + m;
+    ck(bo_qmc_finalize_v(&fa, st), "qmc_finalize");
+  }
+  BoQehviArgs qa{};
+  qa.struct_size = sizeof(qa);
+  qa.abi_version = BO_ABI_VERSION;
+  qa.B = B;
+  qa.q = q;
+  qa.m = M;
+  qa.S = static_cast<int32_t>(Z.size(0));
+  qa.mean = mean;
+  qa.L = Lq;
+  qa.Z = Z.data_ptr<double>();
+  qa.cell_lo = cell_lo.data_ptr<double>();
+  qa.cell_hi = cell_hi.data_ptr<double>();
+  qa.K = static_cast<int32_t>(cell_lo.size(0));
+  qa.acq = acq.data_ptr<double>();
+  qa.work = w + o_qw;
+  qa.work_elems = 8 * int64_t(B);
+  ck(bo_qehvi_v(&qa, st), "qehvi");
+  return {acq, status};
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(bo, m) {
+  m.def("qehvi_members_eager(Tensor X, Tensor[] Xt_scaled, Tensor[] U, Tensor[] beta, "
+        "Tensor[] lengthscale, float[] outputscale, float[] constant, float[] ymean, float[] ystd, "
+        "int kind, int n, Tensor Z, Tensor cell_lo, Tensor cell_hi, int kxt_cap) -> Tensor[]");
   m.def("qmc_acq_native(Tensor X, Tensor Xt_scaled, Tensor U, Tensor Linv, Tensor beta, "
         "Tensor lengthscale, Tensor Z, Tensor? best_f_s, int kind, int mode, int n, "
         "float outputscale, float constant, float ymean, float ystd, float best_f, bool fat, "
@@ -633,4 +848,5 @@ TORCH_LIBRARY_IMPL(bo, CUDA, m) {
   m.impl("qmc_acq_eager", &qmc_acq_eager);
   m.impl("qmc_acq_backward_native", &qmc_acq_backward_native);
   m.impl("ladder_defer", &ladder_defer);
+  m.impl("qehvi_members_eager", &qehvi_members_eager);
 }

@@ -1026,15 +1026,21 @@ def raise_not_psd_members(ps: "_PinnedStatus", m: int, dev, what: str) -> None:
     order as per-member checks would (no status launch, no copy)."""
     _stream_sync(dev)
     w = ps.words
-    for t in range(m):
-        if w[2 * t] > 0:
+    raise_status_words([(w[2 * t], w[2 * t + 1]) for t in range(m)], what)
+
+
+def raise_status_words(pairs, what: str) -> None:
+    """[max info, max jitter] per member, in member order: NotPSDError for a
+    failed ladder, the reference's NumericalWarning for added jitter."""
+    for info_max, jit_max in pairs:
+        if info_max > 0:
             from .exceptions import NotPSDError
             raise NotPSDError(f"{what}: matrix not positive definite after repeatedly adding "
                               f"jitter up to {CHOLESKY_JITTER_F64 * 10 ** (CHOLESKY_MAX_TRIES - 1):.1e}")
-        if w[2 * t + 1] > 0:
+        if jit_max > 0:
             import warnings
             from .exceptions import NumericalWarning
-            warnings.warn(f"A not p.d., added jitter of {float(w[2 * t + 1]):.1e} to the diagonal",
+            warnings.warn(f"A not p.d., added jitter of {float(jit_max):.1e} to the diagonal",
                           NumericalWarning)
 
 

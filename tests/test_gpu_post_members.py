@@ -110,7 +110,19 @@ def test_qehvi_member_status_words(monkeypatch):
     X = torch.rand(16, 4, 6, dtype=torch.float64, generator=torch.Generator().manual_seed(2)).to(DEV)
     with warnings.catch_warnings():
         warnings.simplefilter("error", NumericalWarning)
-        acqf(X)  # clean: no warning, no error
+        acqf(X)  # clean: no warning, no error (the native forward-only call)
+        acqf(X.clone().requires_grad_(True))  # the autograd path
+    # a t-batch with a repeated point: its q x q posterior covariance is
+    # singular, the ladder adds the first jitter (psd_safe_cholesky's warning)
+    Xd = X.clone()
+    Xd[3, 1] = Xd[3, 0]
+    with pytest.warns(NumericalWarning, match="1.0e-08"):
+        v_native = acqf(Xd)
+    with pytest.warns(NumericalWarning, match="1.0e-08"):
+        v_grad = acqf(Xd.clone().requires_grad_(True)).detach()
+    torch.testing.assert_close(v_native, v_grad, rtol=1e-12, atol=1e-14)
+    # seeded words (the autograd path's pinned status pairs)
+    X = X.clone().requires_grad_(True)
     orig = kernels._PinnedStatus.arm
     seed = {}
 
