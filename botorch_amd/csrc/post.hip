@@ -648,12 +648,32 @@ struct RowsFromX {
   double* Xq_out;
 };
 
+// Several models' K*x^T from one X in one launch (bo_post_kxt_rows_members):
+// model blockIdx.z's lengthscale, training rows, outputscale and outputs.
+struct KxtMembers {
+  const double* ls[8];
+  const double* Xt[8];
+  double os[8];
+  double* Xq[8];
+  double* Kt[8];
+  int nm;  // 0: the kernel's own arguments
+};
+
 template <int KIND, int ND, int KK = KXT_K, bool FROMX = false>
 __global__ __launch_bounds__(256) void kxt_build_kernel(const double* __restrict__ Xq, int nrows,
                                                         const double* __restrict__ Xt, int n,
                                                         int np, int nrows_pad, double outputscale,
                                                         double* __restrict__ Kt,
-                                                        RowsFromX rx = RowsFromX{}) {
+                                                        RowsFromX rx = RowsFromX{},
+                                                        KxtMembers km = KxtMembers{}) {
+  if (km.nm > 0) {
+    const int m = blockIdx.z;
+    rx.ls = km.ls[m];
+    rx.Xq_out = km.Xq[m];
+    Xt = km.Xt[m];
+    outputscale = km.os[m];
+    Kt = km.Kt[m];
+  }
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int k0 = blockIdx.y * KK;
   const bool iv = i < nrows;
@@ -1498,6 +1518,72 @@ static int kxt_small_k() {
     return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 2;
   }();
   return k;
+}
+
+// bo_post_kxt_rows for nm <= 8 models of one shape and kernel kind (a
+// ModelListGP's members) in ONE launch (grid z = model).
+int bo_post_kxt_rows_members(int nm, int kind, const double* X, int B, int q, int d,
+                             const double* const* lengthscale, const double* const* Xt_scaled,
+                             const double* outputscale, int64_t n, double* const* Xq,
+                             double* const* Kt, void* stream) {
+  BO_CHECK_ARG(nm >= 1 && nm <= 8, "bo_post_kxt_rows_members: %d models (1..8)", nm);
+  BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
+  BO_CHECK_ARG(d >= 1 && d <= DP, "fused posterior kernel supports 1 <= d <= %d", DP);
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  if (nrows_pad == 0) return BO_OK;
+  BO_CHECK_ARG(X && lengthscale && Xt_scaled && outputscale && Xq && Kt,
+               "bo_post_kxt_rows_members: null pointer");
+  KxtMembers km{};
+  km.nm = nm;
+  for (int m = 0; m < nm; ++m) {
+    BO_CHECK_ARG(lengthscale[m] && Xt_scaled[m] && Xq[m] && Kt[m], "bo_post_kxt_rows_members: null buffer");
+    km.ls[m] = lengthscale[m];
+    km.Xt[m] = Xt_scaled[m];
+    km.os[m] = outputscale[m];
+    km.Xq[m] = Xq[m];
+    km.Kt[m] = Kt[m];
+  }
+  const int np = nC * PC;
+  const int nrows = B * Qp;
+  hipStream_t st = as_stream(stream);
+  const RowsFromX rx{X, lengthscale[0], B, q, d, Qp, Xq[0]};
+  // points per thread: the one-model rule over the whole (z-stacked) grid
+  const bool small = ceil_div(nrows_pad, 256) * ceil_div(np, KXT_K) * nm < 1024;
+  const int kk = small ? kxt_small_k() : KXT_K;
+  const dim3 grid((unsigned)ceil_div(nrows_pad, 256), (unsigned)ceil_div(np, kk), (unsigned)nm);
+#define BO_KXTM_K(KIND, ND, K)                                                                 \
+  kxt_build_kernel<KIND, ND, K, true><<<grid, 256, 0, st>>>(nullptr, nrows, Xt_scaled[0], (int)n, \
+                                                            np, nrows_pad, outputscale[0], Kt[0], rx, km)
+#define BO_KXTM(KIND, ND)                  \
+  switch (kk) {                            \
+    case 1: BO_KXTM_K(KIND, ND, 1); break; \
+    case 2: BO_KXTM_K(KIND, ND, 2); break; \
+    case 4: BO_KXTM_K(KIND, ND, 4); break; \
+    case 8: BO_KXTM_K(KIND, ND, 8); break; \
+    default: BO_KXTM_K(KIND, ND, KXT_K); break; \
+  }
+#define BO_KXTM_D(KIND)                      \
+  switch (d) {                               \
+    case 1: BO_KXTM(KIND, 1); break;         \
+    case 2: BO_KXTM(KIND, 2); break;         \
+    case 3: BO_KXTM(KIND, 3); break;         \
+    case 4: BO_KXTM(KIND, 4); break;         \
+    case 5: BO_KXTM(KIND, 5); break;         \
+    case 6: BO_KXTM(KIND, 6); break;         \
+    default: BO_KXTM(KIND, 8); break;        \
+  }
+  if (kind == BO_RBF) {
+    BO_KXTM_D(BO_RBF)
+  } else {
+    BO_KXTM_D(BO_MATERN52)
+  }
+#undef BO_KXTM_D
+#undef BO_KXTM
+#undef BO_KXTM_K
+  BO_LAUNCH_CHECK();
+  return BO_OK;
 }
 
 // bo_prepare_rows + bo_post_kxt in one launch: Xq and K*x^T from X itself.

@@ -711,22 +711,26 @@ std::vector<at::Tensor> qehvi_members_eager(
   double* S_p[8];
   double* m_p[8];
   double* Xq_p[8];
+  const double* ls_p[8];
+  const double* xt_p[8];
+  double* Ktw_p[8];
   for (int m = 0; m < M; ++m) {
     double* base = w + per * m;
     Xq_p[m] = base;
-    Kt_p[m] = kxt ? base + s_xq : nullptr;
+    Ktw_p[m] = kxt ? base + s_xq : nullptr;
+    Kt_p[m] = Ktw_p[m];
     S_p[m] = base + s_xq + s_kt;
     m_p[m] = base + s_xq + s_kt + s_sp;
     U_p[m] = U[m].data_ptr<double>();
     b_p[m] = beta[m].data_ptr<double>();
-    if (kxt)
-      ck(bo_post_kxt_rows(int(kind), X.data_ptr<double>(), B, q, d, lengthscale[m].data_ptr<double>(),
-                          Xt_scaled[m].data_ptr<double>(), n, outputscale[m], Xq_p[m],
-                          const_cast<double*>(Kt_p[m]), st), "post_kxt_rows");
-    else
-      ck(bo_prepare_rows(X.data_ptr<double>(), B, q, d, lengthscale[m].data_ptr<double>(), Xq_p[m], st),
-         "prepare_rows");
+    ls_p[m] = lengthscale[m].data_ptr<double>();
+    xt_p[m] = Xt_scaled[m].data_ptr<double>();
+    if (!kxt)
+      ck(bo_prepare_rows(X.data_ptr<double>(), B, q, d, ls_p[m], Xq_p[m], st), "prepare_rows");
   }
+  if (kxt)  // every member's rows and K*x^T in one launch
+    ck(bo_post_kxt_rows_members(M, int(kind), X.data_ptr<double>(), B, q, d, ls_p, xt_p,
+                                outputscale.data(), n, Xq_p, Ktw_p, st), "post_kxt_rows_members");
   hipEvent_t t0 = nullptr;
   {
     std::lock_guard<std::mutex> tl(g_time_mu);

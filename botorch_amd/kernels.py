@@ -479,9 +479,10 @@ def small_plan(B: int, q: int, n: int) -> int:
 
 def post_partials_members(caches, X: torch.Tensor, store_R: bool = False) -> list:
     """post_partials of one X under several models of one shape (a
-    ModelListGP's members, models/gpytorch.py:629-726): where the small-grid
-    plan applies, every member's K*x^T is built and ONE bo_post_small_batched
-    launch forms all members' partials (C4: three outputs, one launch);
+    ModelListGP's members, models/gpytorch.py:629-726): every member's K*x^T
+    in one launch, then ONE launch for all members' partials -- the
+    small-grid kernel where its plan applies, the member-batched stream-K
+    128-tile kernel where the one-model plan is stream-K (C4: three outputs);
     elsewhere one post_partials per member."""
     c0 = caches[0]
     B, q, d = X.shape
@@ -502,11 +503,8 @@ def post_partials_members(caches, X: torch.Tensor, store_R: bool = False) -> lis
     st = _stream(dev)
     Xc = X.contiguous()
     pps, ptrs = [], {k: [] for k in ("Kt", "U", "beta", "S", "m", "Rt")}
-    for c in caches:
-        Xq = torch.empty(nrows_pad, DP, **f64)
-        Kt = torch.empty(c.np, nrows_pad, **f64)
-        check(lib().bo_post_kxt_rows(c.kind, _p(Xc), B, q, d, _p(c.lengthscale), _p(c.Xt_scaled),
-                                     c.n, c.outputscale, _p(Xq), _p(Kt), st), "post_kxt_rows")
+    Xqs, Kts = _kxt_rows_members(caches, Xc, nrows_pad)
+    for c, Xq, Kt in zip(caches, Xqs, Kts):
         Sp = torch.empty(nparts, nrows_pad // 16, 16, 16, **f64)
         mp = torch.empty(nparts, nrows_pad, **f64)
         Rt = torch.empty(nC * 128, nrows_pad, **f64) if store_R else None
@@ -522,6 +520,33 @@ def post_partials_members(caches, X: torch.Tensor, store_R: bool = False) -> lis
     if TIMING_HOOK is not None:
         TIMING_HOOK("post_partials_end")
     return pps
+
+
+def _kxt_rows_members(caches, Xc: torch.Tensor, nrows_pad: int):
+    """Every member's padded rows and K*x^T from one X: one launch where the
+    members share the kernel kind (bo_post_kxt_rows_members), else one each."""
+    dev = _dev(Xc)
+    B, q, d = Xc.shape
+    f64 = dict(dtype=torch.float64, device=dev)
+    st = _stream(dev)
+    Xqs = [torch.empty(nrows_pad, DP, **f64) for _ in caches]
+    Kts = [torch.empty(c.np, nrows_pad, **f64) for c in caches]
+    nm = len(caches)
+    if nm <= 8 and all(c.kind == caches[0].kind for c in caches):
+        P = ctypes.c_void_p * nm
+        os_ = (ctypes.c_double * nm)(*[float(c.outputscale) for c in caches])
+        check(lib().bo_post_kxt_rows_members(nm, caches[0].kind, _p(Xc), B, q, d,
+                                             P(*[_p(c.lengthscale).value for c in caches]),
+                                             P(*[_p(c.Xt_scaled).value for c in caches]), os_,
+                                             caches[0].n, P(*[_p(t).value for t in Xqs]),
+                                             P(*[_p(t).value for t in Kts]), st),
+              "post_kxt_rows_members")
+    else:
+        for c, Xq, Kt in zip(caches, Xqs, Kts):
+            check(lib().bo_post_kxt_rows(c.kind, _p(Xc), B, q, d, _p(c.lengthscale),
+                                         _p(c.Xt_scaled), c.n, c.outputscale, _p(Xq), _p(Kt), st),
+                  "post_kxt_rows")
+    return Xqs, Kts
 
 
 # BO_POST_MEMBERS=0: one stream-K launch per member instead (A/B knob)
@@ -540,11 +565,8 @@ def _post_members_streamk(caches, X: torch.Tensor, store_R: bool, work_elems: in
     st = _stream(dev)
     Xc = X.contiguous()
     pps, ptrs = [], {k: [] for k in ("Kt", "U", "beta", "S", "m", "Rt")}
-    for c in caches:
-        Xq = torch.empty(nrows_pad, DP, **f64)
-        Kt = torch.empty(c.np, nrows_pad, **f64)
-        check(lib().bo_post_kxt_rows(c.kind, _p(Xc), B, q, d, _p(c.lengthscale), _p(c.Xt_scaled),
-                                     c.n, c.outputscale, _p(Xq), _p(Kt), st), "post_kxt_rows")
+    Xqs, Kts = _kxt_rows_members(caches, Xc, nrows_pad)
+    for c, Xq, Kt in zip(caches, Xqs, Kts):
         Sp = torch.empty(nC, nrows_pad // 16, 16, 16, **f64)
         mp = torch.empty(nC, nrows_pad, **f64)
         Rt = torch.empty(nC * 128, nrows_pad, **f64) if store_R else None

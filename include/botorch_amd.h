@@ -365,6 +365,13 @@ int bo_post_small_batched(int nm, const double* const* Kt, const double* const* 
  * bo_post_members_work: the shared workspace in doubles, -1 where the
  * one-model plan is not stream-K (one launch per model then). */
 int bo_post_members_work(int nm, int64_t B, int q, int64_t n, int64_t* work_elems);
+/* bo_post_kxt_rows for nm <= 8 models of one shape and kernel kind sharing X
+ * (lengthscale[m], Xt_scaled[m], outputscale[m] -> Xq[m], Kt[m]) in one
+ * launch. */
+int bo_post_kxt_rows_members(int nm, int kind, const double* X, int B, int q, int d,
+                             const double* const* lengthscale, const double* const* Xt_scaled,
+                             const double* outputscale, int64_t n, double* const* Xq,
+                             double* const* Kt, void* stream);
 int bo_post_partials_members(int nm, const double* const* Kt, const double* const* U,
                              const double* const* beta, double* const* Spart, double* const* mpart,
                              double* const* Rt, const double* Xq0, int64_t B, int q, int64_t n,

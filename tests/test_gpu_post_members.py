@@ -142,3 +142,24 @@ def test_qehvi_member_status_words(monkeypatch):
         acqf(X)
     seed.clear()
     acqf(X)
+
+
+def test_kxt_rows_members_bit_equal_to_per_member():
+    """bo_post_kxt_rows_members (one launch, grid z = model) writes exactly
+    what bo_post_kxt_rows writes per model: the rows and K*x^T."""
+    from botorch_amd import kernels
+    from botorch_amd._lib import check, lib
+    _, _, models = _models(1500)
+    caches = [mm.prediction_cache() for mm in models]
+    X = torch.rand(40, 5, 6, dtype=torch.float64, generator=torch.Generator().manual_seed(9)).to(DEV)
+    _, nrows_pad, _ = kernels.geometry(40, 5, 1500)
+    Xqs, Kts = kernels._kxt_rows_members(caches, X, nrows_pad)
+    st = kernels._stream(X.device)
+    for c, Xq, Kt in zip(caches, Xqs, Kts):
+        Xq1 = torch.empty_like(Xq)
+        Kt1 = torch.empty_like(Kt)
+        check(lib().bo_post_kxt_rows(c.kind, kernels._p(X), 40, 5, 6, kernels._p(c.lengthscale),
+                                     kernels._p(c.Xt_scaled), c.n, c.outputscale, kernels._p(Xq1),
+                                     kernels._p(Kt1), st), "post_kxt_rows")
+        assert torch.equal(Xq, Xq1)
+        assert torch.equal(Kt, Kt1)
