@@ -16,6 +16,7 @@
 #include "common.h"
 
 #include <atomic>
+#include <cstdlib>
 #include <mutex>
 
 // No multiply-add contraction: scipy's L-BFGS-B rounds every product and sum
@@ -313,6 +314,17 @@ extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int m
     // the attribute is per device: set it once for each device this process
     // launches the joint kernel on, and report a refusal here, not as a
     // launch failure later
+    // 16 waves past n = 8192 (C3's joint problem, n = 12288: 813 -> 695 us per
+    // launch, optimize_acqf 76.9 -> 72.8 ms; C2's n = 3072 is faster on 8,
+    // 205 against 244 us: its reductions' LDS rounds outweigh the wider
+    // vector loops); BO_LBFGSB_JOINT_W=8 / 16 forces either (A/B knob)
+    static const int wenv = [] {
+      const char* e = getenv("BO_LBFGSB_JOINT_W");
+      return e ? atoi(e) : 0;
+    }();
+    const bool w16 = wenv == 16 || (wenv != 8 && n > 8192);
+    const void* fn = w16 ? reinterpret_cast<const void*>(&lbfgsb_kernel<16>)
+                         : reinterpret_cast<const void*>(&lbfgsb_kernel<JOINT_W>);
     if (dyn > 64 * 1024) {
       int dev = 0;
       BO_HIP(hipGetDevice(&dev));
@@ -321,14 +333,17 @@ extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int m
       std::lock_guard<std::mutex> lock(mu);
       const uint64_t bit = dev < 64 ? (uint64_t(1) << dev) : 0;
       if (!bit || !(set_mask & bit)) {
-        BO_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&lbfgsb_kernel<JOINT_W>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+        BO_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)(sizeof(double) * JOINT_TB_LDS)));
         set_mask |= bit;
       }
     }
-    lbfgsb_kernel<JOINT_W><<<B, 64 * JOINT_W, dyn, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws,
-                                                                         wy, mat, ds, is, mode);
+    if (w16)
+      lbfgsb_kernel<16><<<B, 64 * 16, dyn, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws, wy, mat, ds,
+                                                                 is, mode);
+    else
+      lbfgsb_kernel<JOINT_W><<<B, 64 * JOINT_W, dyn, as_stream(stream)>>>(P, xt, ft, gt, v, iv, ws,
+                                                                           wy, mat, ds, is, mode);
   }
   BO_LAUNCH_CHECK();
   return BO_OK;
