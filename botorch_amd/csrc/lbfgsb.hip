@@ -329,13 +329,13 @@ extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int m
       int dev = 0;
       BO_HIP(hipGetDevice(&dev));
       static std::mutex mu;
-      static uint64_t set_mask = 0;
+      static uint64_t set_mask[2] = {0, 0};  // per kernel variant (8 / 16 waves)
       std::lock_guard<std::mutex> lock(mu);
       const uint64_t bit = dev < 64 ? (uint64_t(1) << dev) : 0;
-      if (!bit || !(set_mask & bit)) {
+      if (!bit || !(set_mask[w16] & bit)) {
         BO_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)(sizeof(double) * JOINT_TB_LDS)));
-        set_mask |= bit;
+        set_mask[w16] |= bit;
       }
     }
     if (w16)
