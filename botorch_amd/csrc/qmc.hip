@@ -316,6 +316,24 @@ __device__ __forceinline__ void ladder_factor(int lane, int q, const double (&Si
   }
 }
 
+// A ModelListGP's members finalised in one launch (bo_qmc_finalize_members,
+// root-only mode): member blockIdx.y's rows, partials, scalars and outputs
+// replace the kernel's own arguments.
+constexpr int QMC_MAXM = 8;
+struct QmcMembers {
+  const double* Xq[QMC_MAXM];
+  const double* Spart[QMC_MAXM];
+  const double* mpart[QMC_MAXM];
+  double outputscale[QMC_MAXM], constant[QMC_MAXM], ymean[QMC_MAXM], ystd[QMC_MAXM];
+  double* mean_out[QMC_MAXM];
+  double* L_out[QMC_MAXM];
+  int* info_out[QMC_MAXM];
+  double* jitter_out[QMC_MAXM];
+  double* status_out[QMC_MAXM];
+  int* status_count[QMC_MAXM];
+  int nm;  // 0: the kernel's own arguments
+};
+
 template <int KIND, int MODE>
 __global__ __launch_bounds__(THREADS) void qmc_kernel(
     int q, int Qp, const double* __restrict__ Xq, const double* __restrict__ Spart,
@@ -326,7 +344,23 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     double* __restrict__ L_out, int* __restrict__ info_out, double* __restrict__ jitter_out,
     const double* __restrict__ Tm, int r, int64_t ldT, const double* __restrict__ F,
     int64_t ldF, LogRedParams lp, int sym, double* __restrict__ status_out,
-    int* __restrict__ status_count) {
+    int* __restrict__ status_count, QmcMembers qm = QmcMembers{}) {
+  if (qm.nm > 0) {
+    const int m = blockIdx.y;
+    Xq = qm.Xq[m];
+    Spart = qm.Spart[m];
+    mpart = qm.mpart[m];
+    outputscale = qm.outputscale[m];
+    constant = qm.constant[m];
+    ymean = qm.ymean[m];
+    ystd = qm.ystd[m];
+    mean_out = qm.mean_out[m];
+    L_out = qm.L_out[m];
+    info_out = qm.info_out[m];
+    jitter_out = qm.jitter_out[m];
+    status_out = qm.status_out[m];
+    status_count = qm.status_count[m];
+  }
   // qNEI with the cached baseline root (utils/low_rank.py:85-173): Tm (r x ldT)
   // holds bl_chol^T = L_rr^{-1} Sigma'(X_base, X) per padded test row and F
   // (S x ldF) the samples' baseline term Z_base T; then
@@ -674,6 +708,66 @@ extern "C" int bo_qmc_finalize_ext(int kind, int mode, int B, int q, const doubl
   hipStream_t st = as_stream(stream);
   if (kind == BO_RBF) launch_qmc<BO_RBF>(mode, B, a, st);
   else launch_qmc<BO_MATERN52>(mode, B, a, st);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+// The root-only finalisation (BO_QMC_CHOL: mean + jittered q x q Cholesky) of
+// nm <= 8 models of one shape and kernel kind in ONE launch (grid B x nm):
+// per member its rows, partials (nparts as bo_qmc_finalize_ext), scalars,
+// outputs and optional fused-status words.
+extern "C" int bo_qmc_finalize_members(int nm, int kind, int B, int q, const double* const* Xq,
+                                       const double* const* Spart, const double* const* mpart,
+                                       int64_t n, const double* outputscale, const double* constant,
+                                       const double* ymean, const double* ystd, int max_tries,
+                                       double jitter0, double* const* mean_out,
+                                       double* const* L_out, int* const* info_out,
+                                       double* const* jitter_out, int nparts,
+                                       double* const* status_out, int* const* status_count,
+                                       void* stream) {
+  BO_CHECK_ARG(nm >= 1 && nm <= QMC_MAXM, "bo_qmc_finalize_members: %d models (1..%d)", nm, QMC_MAXM);
+  BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
+  BO_CHECK_ARG(nparts >= 0, "bo_qmc_finalize_members: nparts %d", nparts);
+  BO_CHECK_ARG(Xq && Spart && mpart && outputscale && constant && ymean && ystd && mean_out && L_out &&
+                   info_out && jitter_out,
+               "bo_qmc_finalize_members: null pointer array");
+  if (B == 0) return BO_OK;
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  if (nparts > 0) nC = nparts;
+  QmcMembers qm{};
+  qm.nm = nm;
+  for (int m = 0; m < nm; ++m) {
+    BO_CHECK_ARG(Xq[m] && Spart[m] && mpart[m] && mean_out[m] && L_out[m] && info_out[m] && jitter_out[m],
+                 "bo_qmc_finalize_members: null buffer");
+    BO_CHECK_ARG(!status_out || (status_out[m] && status_count && status_count[m]),
+                 "bo_qmc_finalize_members: status words need their counters");
+    qm.Xq[m] = Xq[m];
+    qm.Spart[m] = Spart[m];
+    qm.mpart[m] = mpart[m];
+    qm.outputscale[m] = outputscale[m];
+    qm.constant[m] = constant[m];
+    qm.ymean[m] = ymean[m];
+    qm.ystd[m] = ystd[m];
+    qm.mean_out[m] = mean_out[m];
+    qm.L_out[m] = L_out[m];
+    qm.info_out[m] = info_out[m];
+    qm.jitter_out[m] = jitter_out[m];
+    qm.status_out[m] = status_out ? status_out[m] : nullptr;
+    qm.status_count[m] = status_out ? status_count[m] : nullptr;
+  }
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((unsigned)B, (unsigned)nm);
+#define BO_QMC_M(KIND)                                                                            \
+  qmc_kernel<KIND, QMC_CHOL><<<grid, THREADS, 0, st>>>(                                           \
+      q, Qp, Xq[0], Spart[0], mpart[0], nC, nrows_pad, outputscale[0], constant[0], ymean[0],     \
+      ystd[0], nullptr, 0, 0.0, nullptr, max_tries, jitter0, nullptr, mean_out[0], nullptr,       \
+      L_out[0], info_out[0], jitter_out[0], nullptr, 0, 0, nullptr, 0, LogRedParams{1.0, 1.0, 1}, \
+      0, qm.status_out[0], qm.status_count[0], qm)
+  if (kind == BO_RBF) BO_QMC_M(BO_RBF);
+  else BO_QMC_M(BO_MATERN52);
+#undef BO_QMC_M
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

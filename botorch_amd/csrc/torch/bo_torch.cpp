@@ -772,32 +772,31 @@ std::vector<at::Tensor> qehvi_members_eager(
   }
   double* mean = w + o_mean;
   double* Lq = w + o_L;
-  for (int m = 0; m < M; ++m) {
-    BoQmcFinalizeArgs fa{};
-    fa.struct_size = sizeof(fa);
-    fa.abi_version = BO_ABI_VERSION;
-    fa.kind = int(kind);
-    fa.mode = BO_QMC_CHOL;
-    fa.B = B;
-    fa.q = q;
-    fa.Xq = Xq_p[m];
-    fa.Spart = S_p[m];
-    fa.mpart = m_p[m];
-    fa.n = n;
-    fa.outputscale = outputscale[m];
-    fa.constant = constant[m];
-    fa.ymean = ymean[m];
-    fa.ystd = ystd[m];
-    fa.max_tries = 6;   // botorch/__init__.py:47 (cholesky_max_tries)
-    fa.jitter0 = 1e-8;  // [G] cholesky_jitter, double
-    fa.mean_out = mean + int64_t(m) * B * q;
-    fa.L_out = Lq + int64_t(m) * B * q * q;
-    fa.info_out = reinterpret_cast<int*>(w + o_info) + int64_t(m) * B;
-    fa.jitter_out = w + o_jit + int64_t(m) * B;
-    fa.nparts = nsmall;
-    fa.status_out = ms.dev + 2 * m;
-    fa.status_count = ms.count + m;
-    ck(bo_qmc_finalize_v(&fa, st), "qmc_finalize");
+  {  // every member's finalisation in one launch (grid B x M)
+    const double* xq_c[8];
+    const double* sp_c[8];
+    const double* mp_c[8];
+    double* mo[8];
+    double* lo_[8];
+    int* io[8];
+    double* jo[8];
+    double* so[8];
+    int* co[8];
+    for (int m = 0; m < M; ++m) {
+      xq_c[m] = Xq_p[m];
+      sp_c[m] = S_p[m];
+      mp_c[m] = m_p[m];
+      mo[m] = mean + int64_t(m) * B * q;
+      lo_[m] = Lq + int64_t(m) * B * q * q;
+      io[m] = reinterpret_cast<int*>(w + o_info) + int64_t(m) * B;
+      jo[m] = w + o_jit + int64_t(m) * B;
+      so[m] = ms.dev + 2 * m;
+      co[m] = ms.count + m;
+    }
+    // max_tries 6: botorch/__init__.py:47 (cholesky_max_tries); jitter 1e-8: [G] cholesky_jitter
+    ck(bo_qmc_finalize_members(M, int(kind), B, q, xq_c, sp_c, mp_c, n, outputscale.data(),
+                               constant.data(), ymean.data(), ystd.data(), 6, 1e-8, mo, lo_, io, jo,
+                               nsmall, so, co, st), "qmc_finalize_members");
   }
   BoQehviArgs qa{};
   qa.struct_size = sizeof(qa);

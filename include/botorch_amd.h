@@ -168,6 +168,18 @@ int bo_ladder_status(const int* info, const double* jitter, int64_t B, double* o
  * stream sync without a status launch or copy (a ModelListGP's members in
  * the qEHVI forward).  bo_pinned_free releases it. */
 int bo_pinned_alloc(int64_t bytes, void** host, void** dev);
+/* bo_qmc_finalize_ext in BO_QMC_CHOL mode (mean + jittered q x q root) for
+ * nm <= 8 models of one shape and kernel kind in ONE launch: per member its
+ * rows Xq[m], partials Spart[m] / mpart[m] (nparts as bo_qmc_finalize_ext),
+ * scalars and outputs; status_out (optional, with status_count) per member as
+ * BoQmcFinalizeArgs.status_out.  A ModelListGP's members in the qEHVI forward. */
+int bo_qmc_finalize_members(int nm, int kind, int B, int q, const double* const* Xq,
+                            const double* const* Spart, const double* const* mpart, int64_t n,
+                            const double* outputscale, const double* constant, const double* ymean,
+                            const double* ystd, int max_tries, double jitter0,
+                            double* const* mean_out, double* const* L_out, int* const* info_out,
+                            double* const* jitter_out, int nparts, double* const* status_out,
+                            int* const* status_count, void* stream);
 int bo_pinned_free(void* host);
 
 /* Pareto masks of S point sets (Y: S x n x m, m <= 8; out: S x n bytes, 1 =

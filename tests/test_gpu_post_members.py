@@ -163,3 +163,52 @@ def test_kxt_rows_members_bit_equal_to_per_member():
                                      kernels._p(Kt1), st), "post_kxt_rows")
         assert torch.equal(Xq, Xq1)
         assert torch.equal(Kt, Kt1)
+
+
+def test_qmc_finalize_members_bit_equal_to_per_member():
+    """bo_qmc_finalize_members (one launch, grid B x models, root-only mode)
+    writes exactly what bo_qmc_finalize does per member: means, q x q roots,
+    ladder info and jitter, and the fused status words."""
+    import ctypes
+    from botorch_amd import _lib, kernels
+    from botorch_amd._lib import check, lib
+    _, _, models = _models(1500)
+    caches = [mm.prediction_cache() for mm in models]
+    X = torch.rand(40, 5, 6, dtype=torch.float64, generator=torch.Generator().manual_seed(4)).to(DEV)
+    X[7, 1] = X[7, 0]  # one t-batch needs the jitter ladder
+    pps = kernels.post_partials_members(caches, X)
+    stats = [mm.outcome_stats() for mm in models]
+    refs = []
+    for c, pp, (ym, ys) in zip(caches, pps, stats):
+        refs.append(kernels.qmc_finalize(c, pp, _lib.QMC_CHOL, ym, ys, want_mean=True, want_cov=False,
+                                         want_L=True))
+    M, B, q = len(models), 40, 5
+    f64 = dict(dtype=torch.float64, device=DEV)
+    mean = torch.empty(M, B, q, **f64)
+    L = torch.empty(M, B, q, q, **f64)
+    info = torch.empty(M, B, dtype=torch.int32, device=DEV)
+    jit = torch.empty(M, B, **f64)
+    status = torch.zeros(M, 2, **f64)
+    count = torch.zeros(M, dtype=torch.int32, device=DEV)
+    P = ctypes.c_void_p * M
+    D = ctypes.c_double * M
+    nparts = int(pps[0].Spart.shape[0]) if pps[0].Spart.shape[0] != pps[0].nC else 0
+    check(lib().bo_qmc_finalize_members(
+        M, caches[0].kind, B, q, P(*[p.Xq.data_ptr() for p in pps]),
+        P(*[p.Spart.data_ptr() for p in pps]), P(*[p.mpart.data_ptr() for p in pps]), caches[0].n,
+        D(*[c.outputscale for c in caches]), D(*[c.constant for c in caches]),
+        D(*[s[0] for s in stats]), D(*[s[1] for s in stats]), kernels.CHOLESKY_MAX_TRIES,
+        kernels.CHOLESKY_JITTER_F64, P(*[mean[m].data_ptr() for m in range(M)]),
+        P(*[L[m].data_ptr() for m in range(M)]), P(*[info[m].data_ptr() for m in range(M)]),
+        P(*[jit[m].data_ptr() for m in range(M)]), nparts,
+        P(*[status[m].data_ptr() for m in range(M)]),
+        P(*[count[m:].data_ptr() for m in range(M)]), kernels._stream(X.device)),
+        "qmc_finalize_members")
+    for m, r in enumerate(refs):
+        assert torch.equal(mean[m], r["mean"])
+        assert torch.equal(L[m], r["L"])
+        assert torch.equal(info[m], r["info"])
+        assert torch.equal(jit[m], r["jitter"])
+        assert float(status[m, 0]) == float(r["info"].max())
+        assert float(status[m, 1]) == float(r["jitter"].max())
+    assert float(jit.max()) > 0  # the repeated point did take the ladder
