@@ -895,8 +895,11 @@ class qLogNoisyExpectedImprovement(qNoisyExpectedImprovement):
 def _qehvi_members_eager(acqf, X3: torch.Tensor):
     """Forward-only qEHVI through ONE native call (bo::qehvi_members_eager:
     every member's rows, K*x^T, posterior partials, finalisation and the
-    qEHVI launch, issued from C++), then one stream sync and the members'
-    ladder outcomes from pinned words, raised / warned in member order.
+    qEHVI launch, issued from C++).  The members' ladder outcomes are
+    deferred as the eager qEI's (a ring of pinned slots: the previous calls'
+    outcomes are acted on here, kernels.check_ladder_status waits for all);
+    with BO_SYNC_LADDER=1, one stream sync and the members' outcomes raised /
+    warned in member order.
     None where it does not apply (graph capture; members of unequal shape or
     kernel; more than 8 members): the caller takes _FusedQEHVI."""
     dev = X3.device
@@ -925,10 +928,16 @@ def _qehvi_members_eager(acqf, X3: torch.Tensor):
     q = X3.shape[-2]
     Z = acqf._ensure_sampler().base_samples_2d(q * len(models), dev)
     lo, hi = acqf._cells(dev)
+    defer = not kernels.SYNC_LADDER
     acq, status = _lib.torch_ops().qehvi_members_eager(
-        X3.contiguous(), *args[1:], Z, lo, hi, kernels.kxt_cap(dev))
-    kernels._stream_sync(dev)
-    kernels.raise_status_words(status.tolist(), "qEHVI posterior root")
+        X3.contiguous(), *args[1:], Z, lo, hi, kernels.kxt_cap(dev), defer)
+    if defer:
+        # as the eager qEI: the previous calls' outcomes, this one's pending
+        # (kernels.check_ladder_status / the optimisers' end-of-loop poll)
+        kernels.ladder_prev_outcome(status, idx, "qEHVI posterior root")
+    else:
+        kernels._stream_sync(dev)
+        kernels.raise_status_words(status.tolist(), "qEHVI posterior root")
     return acq
 
 

@@ -58,11 +58,16 @@ void check_f64(const at::Tensor& t, const char* name) {
 // host keeps issuing while the GPU runs (a failed root is reported within
 // NSLOT calls, or at bo::ladder_poll, which waits for all of them).
 constexpr int NSLOT = 4;
+constexpr int SLOT_MEMBERS = 8;       // a ModelListGP's members (qehvi_members_eager)
+constexpr int SLOT_WORDS = 2 + 2 * SLOT_MEMBERS;
 struct Slot {
-  double* host = nullptr;   // pinned [info_max, jitter_max]
+  // pinned [info_max, jitter_max], then one such pair per ModelListGP member
+  // (bo::qehvi_members_eager folds each member's ladder into its own pair:
+  // one pair for all would race between the members' last workgroups)
+  double* host = nullptr;
   double* host_dev = nullptr;  // the same pinned words as a device pointer (zero-copy)
   double* dev = nullptr;    // device [info_max, jitter_max]
-  int* count = nullptr;     // arrival counter of the fused status (qmc_kernel re-zeroes it)
+  int* count = nullptr;     // arrival counters of the fused status (qmc_kernel re-zeroes them)
   hipEvent_t ev = nullptr;
   bool busy = false;
 };
@@ -77,13 +82,14 @@ DeviceLadder& ladder_for(int dev) {
   auto& L = g_ladder[dev];
   if (!L.slot[0].host) {
     for (auto& s : L.slot) {
-      hk(hipHostMalloc(reinterpret_cast<void**>(&s.host), 2 * sizeof(double),
+      hk(hipHostMalloc(reinterpret_cast<void**>(&s.host), SLOT_WORDS * sizeof(double),
                        hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+      for (int e = 0; e < SLOT_WORDS; ++e) s.host[e] = 0.0;
       hk(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.host_dev), s.host, 0),
          "hipHostGetDevicePointer");
       hk(hipMalloc(reinterpret_cast<void**>(&s.dev), 2 * sizeof(double)), "hipMalloc");
-      hk(hipMalloc(reinterpret_cast<void**>(&s.count), sizeof(int)), "hipMalloc");
-      hk(hipMemset(s.count, 0, sizeof(int)), "hipMemset");
+      hk(hipMalloc(reinterpret_cast<void**>(&s.count), (1 + SLOT_MEMBERS) * sizeof(int)), "hipMalloc");
+      hk(hipMemset(s.count, 0, (1 + SLOT_MEMBERS) * sizeof(int)), "hipMemset");
       hk(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
     }
   }
@@ -94,8 +100,10 @@ DeviceLadder& ladder_for(int dev) {
 void fold_front(DeviceLadder& L, double* o) {
   Slot& s = L.slot[L.pending.front()];
   o[0] = 1.0;
-  o[1] = std::max(o[1], s.host[0]);
-  o[2] = std::max(o[2], s.host[1]);
+  for (int e = 0; e < SLOT_WORDS; e += 2) {  // the call's own pair and its members'
+    o[1] = std::max(o[1], s.host[e]);
+    o[2] = std::max(o[2], s.host[e + 1]);
+  }
   s.busy = false;
   L.pending.pop_front();
 }
@@ -131,8 +139,7 @@ int free_slot(DeviceLadder& L, at::Tensor& prev) {
   for (int i = 0; i < NSLOT; ++i)
     if (!L.slot[i].busy) {
       // qmc_kernel folds its status into the words it finds (sticky max)
-      L.slot[i].host[0] = 0.0;
-      L.slot[i].host[1] = 0.0;
+      for (int e = 0; e < SLOT_WORDS; ++e) L.slot[i].host[e] = 0.0;
       return i;
     }
   TORCH_CHECK(false, "botorch_amd: no free ladder-status slot");
@@ -641,7 +648,8 @@ std::vector<at::Tensor> qehvi_members_eager(
     const at::Tensor& X, at::TensorList Xt_scaled, at::TensorList U, at::TensorList beta,
     at::TensorList lengthscale, at::ArrayRef<double> outputscale, at::ArrayRef<double> constant,
     at::ArrayRef<double> ymean, at::ArrayRef<double> ystd, int64_t kind, int64_t n,
-    const at::Tensor& Z, const at::Tensor& cell_lo, const at::Tensor& cell_hi, int64_t kxt_cap) {
+    const at::Tensor& Z, const at::Tensor& cell_lo, const at::Tensor& cell_hi, int64_t kxt_cap,
+    bool defer_ladder) {
   check_f64(X, "X");
   check_f64(Z, "Z");
   check_f64(cell_lo, "cell_lo");
@@ -670,10 +678,32 @@ std::vector<at::Tensor> qehvi_members_eager(
   void* st = c10::hip::getCurrentHIPStream(dev).stream();
   auto f64 = X.options().dtype(at::kDouble);
   auto acq = at::empty({B}, f64);
-  std::lock_guard<std::mutex> lk(g_member_mu);
-  MemberStatus& ms = member_status(dev);
-  for (int e = 0; e < 2 * M; ++e) ms.host[e] = 0.0;
-  auto status = at::from_blob(ms.host, {M, 2}, at::TensorOptions().dtype(at::kDouble));
+  // ladder outcomes: deferred (the ring of pinned slots, as qmc_acq_eager:
+  // this call's members fold into one slot's member pairs, the finished
+  // calls' statuses come back as [has, info_max, jitter_max]) or, with
+  // defer_ladder off, the member pairs of per-device words the caller reads
+  // after a stream sync ([M, 2]: per member, in member order)
+  std::unique_lock<std::mutex> lk_ring(g_ladder_mu, std::defer_lock);
+  std::unique_lock<std::mutex> lk_mem(g_member_mu, std::defer_lock);
+  double* words_dev = nullptr;
+  int* counts = nullptr;
+  at::Tensor status;
+  DeviceLadder* Ld = nullptr;
+  int mine = -1;
+  if (defer_ladder) {
+    lk_ring.lock();
+    Ld = &ladder_for(dev);
+    mine = free_slot(*Ld, status);
+    words_dev = Ld->slot[mine].host_dev + 2;
+    counts = Ld->slot[mine].count + 1;
+  } else {
+    lk_mem.lock();
+    MemberStatus& ms = member_status(dev);
+    for (int e = 0; e < 2 * M; ++e) ms.host[e] = 0.0;
+    status = at::from_blob(ms.host, {M, 2}, at::TensorOptions().dtype(at::kDouble));
+    words_dev = ms.dev;
+    counts = ms.count;
+  }
   if (B == 0) return {acq, status};
 
   int Qp = 0, nrows = 0, nC = 0;
@@ -790,8 +820,8 @@ std::vector<at::Tensor> qehvi_members_eager(
       lo_[m] = Lq + int64_t(m) * B * q * q;
       io[m] = reinterpret_cast<int*>(w + o_info) + int64_t(m) * B;
       jo[m] = w + o_jit + int64_t(m) * B;
-      so[m] = ms.dev + 2 * m;
-      co[m] = ms.count + m;
+      so[m] = words_dev + 2 * m;
+      co[m] = counts + m;
     }
     // max_tries 6: botorch/__init__.py:47 (cholesky_max_tries); jitter 1e-8: [G] cholesky_jitter
     ck(bo_qmc_finalize_members(M, int(kind), B, q, xq_c, sp_c, mp_c, n, outputscale.data(),
@@ -815,6 +845,7 @@ std::vector<at::Tensor> qehvi_members_eager(
   qa.work = w + o_qw;
   qa.work_elems = 8 * int64_t(B);
   ck(bo_qehvi_v(&qa, st), "qehvi");
+  if (defer_ladder) publish_slot(*Ld, mine, st, true);
   return {acq, status};
 }
 
@@ -823,7 +854,8 @@ std::vector<at::Tensor> qehvi_members_eager(
 TORCH_LIBRARY_FRAGMENT(bo, m) {
   m.def("qehvi_members_eager(Tensor X, Tensor[] Xt_scaled, Tensor[] U, Tensor[] beta, "
         "Tensor[] lengthscale, float[] outputscale, float[] constant, float[] ymean, float[] ystd, "
-        "int kind, int n, Tensor Z, Tensor cell_lo, Tensor cell_hi, int kxt_cap) -> Tensor[]");
+        "int kind, int n, Tensor Z, Tensor cell_lo, Tensor cell_hi, int kxt_cap, "
+        "bool defer_ladder=False) -> Tensor[]");
   m.def("qmc_acq_native(Tensor X, Tensor Xt_scaled, Tensor U, Tensor Linv, Tensor beta, "
         "Tensor lengthscale, Tensor Z, Tensor? best_f_s, int kind, int mode, int n, "
         "float outputscale, float constant, float ymean, float ystd, float best_f, bool fat, "

@@ -111,13 +111,17 @@ def test_qehvi_member_status_words(monkeypatch):
     with warnings.catch_warnings():
         warnings.simplefilter("error", NumericalWarning)
         acqf(X)  # clean: no warning, no error (the native forward-only call)
+        kernels.check_ladder_status(X.device)  # its deferred outcome: clean
         acqf(X.clone().requires_grad_(True))  # the autograd path
     # a t-batch with a repeated point: its q x q posterior covariance is
-    # singular, the ladder adds the first jitter (psd_safe_cholesky's warning)
+    # singular, the ladder adds the first jitter (psd_safe_cholesky's
+    # warning); the native call's outcome is deferred (as the eager qEI's) to
+    # the next call or the end-of-loop poll
     Xd = X.clone()
     Xd[3, 1] = Xd[3, 0]
     with pytest.warns(NumericalWarning, match="1.0e-08"):
         v_native = acqf(Xd)
+        kernels.check_ladder_status(X.device)
     with pytest.warns(NumericalWarning, match="1.0e-08"):
         v_grad = acqf(Xd.clone().requires_grad_(True)).detach()
     torch.testing.assert_close(v_native, v_grad, rtol=1e-12, atol=1e-14)
