@@ -838,6 +838,9 @@ __global__ void prepare_rows_kernel(const double* __restrict__ X, int B, int q, 
 // summed in LDS in wave order (deterministic), then wave (t, h) runs the
 // epilogue of tile t, row half h.
 constexpr int SMU = 32;  // test rows and training columns per unit tile
+#ifndef SMALL_DEPTH
+#define SMALL_DEPTH 2  // k-steps of operands in flight per wave (A/B: -DSMALL_DEPTH=3)
+#endif
 
 __device__ __forceinline__ void small_load(const double* __restrict__ U, int64_t ldu,
                                            const double* __restrict__ Kt, int64_t ldk, int kb,
@@ -864,6 +867,35 @@ __device__ __forceinline__ void small_tile(const double* __restrict__ U, int64_t
   int s = first;
   if (s < nsteps) small_load(U, ldu, Kt, ldk, PK * s, c0, r0, lane, a0, b0);
   if (s + 4 < nsteps) small_load(U, ldu, Kt, ldk, PK * (s + 4), c0, r0, lane, a1, b1);
+#if SMALL_DEPTH >= 3
+  // a third step of operands in flight (BO A/B: SMALL_DEPTH)
+  double a2[4][2], b2[4][2];
+  if (s + 8 < nsteps) small_load(U, ldu, Kt, ldk, PK * (s + 8), c0, r0, lane, a2, b2);
+  for (; s < nsteps; s += 4) {
+    double a3[4][2], b3[4][2];
+    const bool more = s + 12 < nsteps;
+    if (more) small_load(U, ldu, Kt, ldk, PK * (s + 12), c0, r0, lane, a3, b3);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int hc = 0; hc < 2; ++hc)
+#pragma unroll
+        for (int hr = 0; hr < 2; ++hr) acc[hc][hr] = mfma_f64(a0[ks][hc], b0[ks][hr], acc[hc][hr]);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        a0[ks][h] = a1[ks][h];
+        b0[ks][h] = b1[ks][h];
+        a1[ks][h] = a2[ks][h];
+        b1[ks][h] = b2[ks][h];
+        if (more) {
+          a2[ks][h] = a3[ks][h];
+          b2[ks][h] = b3[ks][h];
+        }
+      }
+  }
+#else
   for (; s < nsteps; s += 4) {
     double a2[4][2], b2[4][2];
     const bool more = s + 8 < nsteps;
@@ -886,6 +918,7 @@ __device__ __forceinline__ void small_tile(const double* __restrict__ U, int64_t
         }
       }
   }
+#endif
 }
 
 // One launch serves up to 8 models of one shape (the members of a
