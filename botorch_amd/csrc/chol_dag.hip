@@ -1888,7 +1888,10 @@ std::vector<int4> build_tasks_batched(int T, int nb, bool ainv = false) {
   // -> 0.797-0.805 ms), take 2 / 4 rows; batches of n = 4096 keep 8 / 8 (with
   // 2 / 4: 4 x 4096 5.38 -> 5.69 ms; profiles/r03/cholesky/ab_ch_batched_small.log)
   // (BO_CHOL_CH / BO_CHOL_CHB override the one-matrix chunk rows: an A/B knob,
-  // read once, 1..16)
+  // read once, 1..16).  Round 5 (with the 2-row diagonal-tile first chunk):
+  // batched chunks of 3 rows, n = 4096 1.603-1.616 -> 1.598-1.602 ms, 3 x
+  // 2048 0.759-0.764 -> 0.751-0.752 ms; 6 rows 1.655-1.663 / 0.825 ms
+  // (tools/sweep_chol.sh)
   static const int ch1 = [] {
     const char* e = getenv("BO_CHOL_CH");
     const int v = e ? atoi(e) : 2;
@@ -1896,8 +1899,8 @@ std::vector<int4> build_tasks_batched(int T, int nb, bool ainv = false) {
   }();
   static const int chb1 = [] {
     const char* e = getenv("BO_CHOL_CHB");
-    const int v = e ? atoi(e) : 4;
-    return v >= 1 && v <= 16 ? v : 4;
+    const int v = e ? atoi(e) : 3;
+    return v >= 1 && v <= 16 ? v : 3;
   }();
   const std::vector<int4> one =
       (nb == 1 || T <= 32) ? build_tasks(T, ch1, chb1, ainv) : build_tasks(T, CH, CHB, ainv);
