@@ -22,6 +22,8 @@
 // kernel issued one VALU instruction per ~25 cycles per wave, PMC r03).
 #include "common.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 
 namespace {
@@ -408,7 +410,7 @@ extern "C" int bo_qehvi(int B, int q, int m, const double* mean, const double* L
 }
 
 // work (>= 2 B doubles, optional): the samples of each t-batch split over H =
-// min(8, 256 / B, work_elems / B) workgroups when B leaves CUs idle.
+// min(8, 1024 / B, work_elems / B) workgroups when B leaves CUs idle.
 extern "C" int bo_qehvi_ext(int B, int q, int m, const double* mean, const double* L,
                             const double* Z, int S, const double* cell_lo, const double* cell_hi,
                             int K, int64_t cell_stride, const double* F, int64_t ldF, int64_t sF,
@@ -422,8 +424,17 @@ extern "C" int bo_qehvi_ext(int B, int q, int m, const double* mean, const doubl
   const QehviExt ex{cell_stride, F, ldF, sF, Qp};
   const bool cl = cell_stride == 0 && (int64_t)K * m <= LDS_CELL_DOUBLES / 2;
   int H = 1;
+  // Sample split toward ~1024 workgroups (4 per CU): C4 (B = 128, H = 8) step
+  // 0.395 -> 0.380-0.383 ms against a 256-workgroup target (one per CU; 512:
+  // 0.386-0.391; tools/ab_qehvi_wg.sh) -- more resident waves hide the
+  // inclusion-exclusion's latency.  BO_QEHVI_WG overrides (A/B knob).
+  static const int target = [] {
+    const char* e = std::getenv("BO_QEHVI_WG");
+    const int v = e ? std::atoi(e) : 1024;
+    return v >= 1 && v <= 4096 ? v : 1024;
+  }();
   if (work != nullptr && work_elems >= 2 * (int64_t)B) {
-    H = (int)std::min<int64_t>(std::min(8, std::max(1, 256 / B)), work_elems / B);
+    H = (int)std::min<int64_t>(std::min(8, std::max(1, target / B)), work_elems / B);
     H = std::max(1, std::min(H, S));
   }
   const unsigned grid = (unsigned)((int64_t)B * H);
