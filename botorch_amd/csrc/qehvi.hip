@@ -496,8 +496,14 @@ extern "C" int bo_qehvi_backward_ext(int B, int q, int m, const double* mean, co
   const QehviExt ex{cell_stride, F, ldF, sF, Qp};
   const int64_t nent = (int64_t)m * q * (q + 3) / 2;
   int H = 1;
+  // BO_QEHVI_BWD_WG: target workgroups of the backward's sample split (A/B knob)
+  static const int target = [] {
+    const char* e = std::getenv("BO_QEHVI_BWD_WG");
+    const int v = e ? std::atoi(e) : 256;
+    return v >= 1 && v <= 4096 ? v : 256;
+  }();
   if (work != nullptr && work_elems >= 2 * (int64_t)B * nent) {
-    H = (int)std::min<int64_t>(std::min(8, std::max(1, 256 / B)), work_elems / ((int64_t)B * nent));
+    H = (int)std::min<int64_t>(std::min(8, std::max(1, target / B)), work_elems / ((int64_t)B * nent));
     H = std::max(1, std::min(H, S));
   }
   const unsigned grid = (unsigned)((int64_t)B * H);
