@@ -23,6 +23,9 @@
 // XCDs, so block b runs on XCD b % 8; tile t = (b % 8) * per_xcd + b / 8 gives
 // each XCD a contiguous run of tiles that share A row panels in its own L2.
 #include "common.h"
+
+#include <algorithm>
+#include <cstdlib>
 #include "gemm.h"
 
 namespace {
@@ -117,7 +120,7 @@ __global__ __launch_bounds__(256, MINB) void gemm_f64_kernel(
     int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
     int64_t sA, const double* __restrict__ B, int64_t ldb, int64_t sB, double beta,
     double* __restrict__ C, int64_t ldc, int64_t sC, int flags, TileMap tm, int vecA,
-    int vecB) {
+    int vecB, int ksplit = 1, double* __restrict__ work = nullptr) {
   constexpr int TM = BM / 32;  // MFMA tiles per wave along m (2 x 2 waves)
   constexpr int TN = BN / 32;
   __shared__ __attribute__((aligned(16))) double As[2][BK][BM + PAD];
@@ -147,7 +150,14 @@ __global__ __launch_bounds__(256, MINB) void gemm_f64_kernel(
   if (flags & BO_GEMM_A_UPPER) kbeg = max(kbeg, m0);       // op(A)[m][k] = 0 for k < m
   if (flags & BO_GEMM_B_LOWER) kbeg = max(kbeg, n0);       // op(B)[k][n] = 0 for k < n
   kbeg = (kbeg / BK) * BK;
-  const int nsteps = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  int nsteps = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (ksplit > 1) {  // split-k: chunk blockIdx.z of the k-steps (partials to work)
+    const int per = (nsteps + ksplit - 1) / ksplit;
+    const int s0 = min(nsteps, (int)blockIdx.z * per);
+    const int s1 = min(nsteps, s0 + per);
+    kbeg += s0 * BK;
+    nsteps = s1 - s0;
+  }
 
   v4d acc[TM][TN];
 #pragma unroll
@@ -195,6 +205,20 @@ __global__ __launch_bounds__(256, MINB) void gemm_f64_kernel(
     __syncthreads();
   }
 
+  if (ksplit > 1) {  // the chunk's raw partial (every element: empty chunks write zeros)
+    double* W = work + ((int64_t)blockIdx.z * gridDim.y + bz) * (int64_t)M * N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gm = m0 + wm + i * 16 + mfma_row(lane, r);
+          const int gn = n0 + wn + j * 16 + mfma_col(lane);
+          if (gm < M && gn < N) W[(int64_t)gm * N + gn] = acc[i][j][r];
+        }
+    return;
+  }
   // Epilogue.  The beta * C reads of one 16-row strip are all issued before
   // any of its stores (a load after a store to the same array cannot be
   // hoisted by the compiler, which would otherwise serialise one HBM round
@@ -226,11 +250,28 @@ __global__ __launch_bounds__(256, MINB) void gemm_f64_kernel(
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// C = alpha * (sum of the ksplit chunk partials, in chunk order) + beta * C.
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(int M, int N, int batch, int ksplit,
+                                                                 const double* __restrict__ work,
+                                                                 double alpha, double beta,
+                                                                 double* __restrict__ C, int64_t ldc,
+                                                                 int64_t sC) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t mn = (int64_t)M * N;
+  if (e >= mn * batch) return;
+  const int64_t z = e / mn, r = e - z * mn;
+  const int m = (int)(r / N), n = (int)(r - (int64_t)m * N);
+  double acc = 0.0;
+  for (int s = 0; s < ksplit; ++s) acc += work[((int64_t)s * batch + z) * mn + r];
+  double* c = C + z * sC + (int64_t)m * ldc + n;
+  *c = beta != 0.0 ? fma(beta, *c, alpha * acc) : alpha * acc;
+}
+
 template <int BM, int BN, int MINB>
 int launch_gemm(bool ta, bool tb, int M, int N, int K, double alpha, const double* A,
                 int64_t lda, int64_t sA, const double* B, int64_t ldb, int64_t sB,
                 double beta, double* C, int64_t ldc, int64_t sC, int batch, int flags,
-                hipStream_t st) {
+                hipStream_t st, int ksplit = 1) {
   TileMap tm;
   const int tilesM = (int)ceil_div(M, BM);
   tm.tilesN = (int)ceil_div(N, BN);
@@ -254,16 +295,28 @@ int launch_gemm(bool ta, bool tb, int M, int N, int K, double alpha, const doubl
   // even batch stride
   const int vecA = aligned16(A) && lda % 2 == 0 && (batch == 1 || sA % 2 == 0);
   const int vecB = aligned16(B) && ldb % 2 == 0 && (batch == 1 || sB % 2 == 0);
-  dim3 grid((unsigned)(8 * tm.per_xcd), (unsigned)batch);
+  double* work = nullptr;
+  if (ksplit > 1)
+    BO_HIP(hipMallocAsync(reinterpret_cast<void**>(&work),
+                          sizeof(double) * (size_t)ksplit * batch * M * N, st));
+  dim3 grid((unsigned)(8 * tm.per_xcd), (unsigned)batch, (unsigned)ksplit);
 #define BO_GEMM_GO(TA_, TB_)                                                                 \
   gemm_f64_kernel<BM, BN, TA_, TB_, MINB><<<grid, 256, 0, st>>>(                            \
-      M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, flags, tm, vecA, vecB)
+      M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, flags, tm, vecA, vecB,      \
+      ksplit, work)
   if (ta && tb) BO_GEMM_GO(true, true);
   else if (ta) BO_GEMM_GO(true, false);
   else if (tb) BO_GEMM_GO(false, true);
   else BO_GEMM_GO(false, false);
 #undef BO_GEMM_GO
   BO_LAUNCH_CHECK();
+  if (ksplit > 1) {
+    const int64_t tot = (int64_t)batch * M * N;
+    gemm_splitk_reduce_kernel<<<(unsigned)ceil_div(tot, 256), 256, 0, st>>>(M, N, batch, ksplit, work,
+                                                                         alpha, beta, C, ldc, sC);
+    BO_LAUNCH_CHECK();
+    BO_HIP(hipFreeAsync(work, st));
+  }
   return BO_OK;
 }
 
@@ -343,6 +396,19 @@ int bo_gemm_f64_impl(int ta, int tb, int M, int N, int K, double alpha, const do
   if (tiles128 >= 512 && !(tri && K > 1024))
     return launch_gemm<128, 128, 1>(ta, tb, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc,
                                     sC, batch, flags, st);
+  // Split-k where the 64 x 64 grid leaves most CUs idle on a long k-range
+  // (qNEHVI's cached-root cross term at C4: P_b R^T, 248 x 1024 x 2048 --
+  // 64 tiles, 160 us unsplit): chunk partials in a stream-ordered workspace,
+  // summed in chunk order (deterministic) by one reduction launch.
+  // BO_GEMM_SPLITK=0 keeps one pass (A/B knob).
+  static const bool splitk_on = [] {
+    const char* e = std::getenv("BO_GEMM_SPLITK");
+    return !(e && e[0] == '0');
+  }();
+  const int64_t tiles64 = ceil_div(M, 64) * ceil_div(N, 64) * (int64_t)batch;
+  int ksplit = 1;
+  if (splitk_on && !(flags & BO_GEMM_LOWER_C) && tiles64 < 256 && K >= 1024)
+    ksplit = (int)std::min<int64_t>(std::min<int64_t>(8, std::max<int64_t>(1, 512 / tiles64)), K / 256);
   return launch_gemm<64, 64, 2>(ta, tb, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
-                                batch, flags, st);
+                                batch, flags, st, ksplit);
 }
