@@ -457,7 +457,11 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     for (int j = 0; j < nsplit; ++j) acc += psum[j * E + tid];
     double v = s2 * (kxx - acc);
     if (Tm != nullptr) {
+      // T^T T over the r baseline rows: unrolled so eight rows' loads are in
+      // flight per wait (one L2 round trip per row had made this loop most of
+      // qNEHVI's finalisation, 68 us at C4); the FMA chain keeps its order
       double tt = 0.0;
+#pragma unroll 8
       for (int j = 0; j < r; ++j) tt = fma(Tm[j * ldT + row0 + a], Tm[j * ldT + row0 + c], tt);
       v -= tt;
     }
