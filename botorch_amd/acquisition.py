@@ -1145,11 +1145,21 @@ class _FusedQNEHVI(torch.autograd.Function):
         means, Ls, Fs, saved, status = [], [], [], [], []
         pp = None
         keys = prime_prediction_caches(models)
+        caches = [mm.prediction_cache(key=key) for mm, key in zip(models, keys)]
+        # where the one-model plan splits k (C4), the cross term cannot ride in
+        # the posterior pass and R^T is stored anyway: then every member's
+        # partials + R^T in one launch (post_partials_members)
+        B, q_, _ = X3.shape
+        c0 = caches[0]
+        pps = None
+        if (1 < len(models) <= 8 and kernels.split_plan(B, q_, c0.n)[0] != 0
+                and all(c.n == c0.n and c.np == c0.np and c.d == c0.d for c in caches)):
+            pps = kernels.post_partials_members(caches, X3.detach(), store_R=True)
         for t, mm in enumerate(models):
-            cache = mm.prediction_cache(key=keys[t])
+            cache = caches[t]
             ymean, ystd = mm.outcome_stats()
-            pp = kernels.post_partials(cache, X3.detach(), store_R=need_grad,
-                                       cross=acqf._roots[t].Q_b)
+            pp = pps[t] if pps is not None else kernels.post_partials(
+                cache, X3.detach(), store_R=need_grad, cross=acqf._roots[t].Q_b)
             T, F = acqf._roots[t].forward(cache, pp, ystd)
             out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
                                        want_cov=False, want_L=True, T=T, F=F)
