@@ -465,6 +465,7 @@ static int gp_cache_build_impl(int kind, const double* Xt, int64_t n, int d,
   int64_t we = 0;
   bo_gemv_lt_work(n, &we);
   double* work = nullptr;
+  keep_pool_warm();
   BO_HIP(hipMallocAsync(reinterpret_cast<void**>(&work), sizeof(double) * we, st));
   s = bo_gemv_lt(Linv, np, n, beta, 0.0, alpha, work, stream);
   BO_HIP(hipFreeAsync(work, st));

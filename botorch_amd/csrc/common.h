@@ -9,6 +9,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stdint.h>
 
 #include <cmath>
@@ -104,3 +106,21 @@ void bo_set_error(const char* fmt, ...);
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Stream-ordered scratch (hipMallocAsync) comes from the device's default
+// pool; with its release threshold at 0 every synchronisation hands the
+// memory back and the next allocation goes to the driver again.  Once per
+// device the pool keeps what it has.
+inline void keep_pool_warm() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+  static std::atomic<uint64_t> done{0};
+  const uint64_t bit = uint64_t(1) << dev;
+  if (done.load() & bit) return;
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+    uint64_t thr = ~uint64_t(0);
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+  }
+  done.fetch_or(bit);
+}

@@ -25,6 +25,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include "gemm.h"
 
@@ -250,6 +251,7 @@ __global__ __launch_bounds__(256, MINB) void gemm_f64_kernel(
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+
 // C = alpha * (sum of the ksplit chunk partials, in chunk order) + beta * C.
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(int M, int N, int batch, int ksplit,
                                                                  const double* __restrict__ work,
@@ -296,9 +298,11 @@ int launch_gemm(bool ta, bool tb, int M, int N, int K, double alpha, const doubl
   const int vecA = aligned16(A) && lda % 2 == 0 && (batch == 1 || sA % 2 == 0);
   const int vecB = aligned16(B) && ldb % 2 == 0 && (batch == 1 || sB % 2 == 0);
   double* work = nullptr;
-  if (ksplit > 1)
+  if (ksplit > 1) {
+    keep_pool_warm();
     BO_HIP(hipMallocAsync(reinterpret_cast<void**>(&work),
                           sizeof(double) * (size_t)ksplit * batch * M * N, st));
+  }
   dim3 grid((unsigned)(8 * tm.per_xcd), (unsigned)batch, (unsigned)ksplit);
 #define BO_GEMM_GO(TA_, TB_)                                                                 \
   gemm_f64_kernel<BM, BN, TA_, TB_, MINB><<<grid, 256, 0, st>>>(                            \
@@ -407,8 +411,16 @@ int bo_gemm_f64_impl(int ta, int tb, int M, int N, int K, double alpha, const do
   }();
   const int64_t tiles64 = ceil_div(M, 64) * ceil_div(N, 64) * (int64_t)batch;
   int ksplit = 1;
-  if (splitk_on && !(flags & BO_GEMM_LOWER_C) && tiles64 < 256 && K >= 1024)
-    ksplit = (int)std::min<int64_t>(std::min<int64_t>(8, std::max<int64_t>(1, 512 / tiles64)), K / 256);
+  // (BO_GEMM_SPLITK_KMIN: the shortest k-range split, default 1024; chunks
+  // of >= KMIN / 4)
+  static const int kmin = [] {
+    const char* e = std::getenv("BO_GEMM_SPLITK_KMIN");
+    const int v = e ? std::atoi(e) : 1024;
+    return v >= 128 ? v : 1024;
+  }();
+  if (splitk_on && !(flags & BO_GEMM_LOWER_C) && tiles64 < 256 && K >= kmin)
+    ksplit = (int)std::min<int64_t>(std::min<int64_t>(8, std::max<int64_t>(1, 512 / tiles64)),
+                                    K / (kmin / 4));
   return launch_gemm<64, 64, 2>(ta, tb, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
                                 batch, flags, st, ksplit);
 }
