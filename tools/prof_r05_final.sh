@@ -7,7 +7,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r05final
+O=gpurun_out/${OUT:-r05final}
 mkdir -p $O
 if [ "${SKIP_SUITE:-0}" != 1 ]; then
   bash tools/gpu_run.sh test smoke || exit $?
