@@ -533,16 +533,19 @@ class _CachedBaselineRoot:
                 self.Xb_scaled[:, : cache.d] = X_baseline / cache.lengthscale
                 self.fused_ready = True
 
-    def forward(self, cache, pp, ystd):
+    def forward(self, cache, pp, ystd, F_out=None):
+        """T and F (F written into F_out when given: the stacked qEHVI input)."""
         s2 = ystd * ystd
-        ones = torch.ones(kernels.DP, dtype=torch.float64, device=pp.Xq.device)
+        ones = self.__dict__.get("_ones")
+        if ones is None or ones.device != pp.Xq.device:
+            ones = self._ones = torch.ones(kernels.DP, dtype=torch.float64, device=pp.Xq.device)
         Kbx = kernels.covar_matrix(self.Xb_scaled, pp.Xq, ones, cache.kind, cache.outputscale)
         T = kernels.gemm(self.Linv, Kbx, alpha=s2, flags=_lib.GEMM_A_LOWER)
         if pp.Cx is not None:   # P_b R^T = Q_b K*x^T, fused into the posterior pass
             T.add_(pp.Cx, alpha=-s2)
         else:
             T = kernels.gemm(self.P_b, pp.Rt, alpha=-s2, beta=1.0, C=T)
-        F = kernels.gemm(self.Z_base, T)
+        F = kernels.gemm(self.Z_base, T, C=F_out)
         return T, F
 
     def backward(self, cache, pp, W, dmean, dcov, dF, T, ystd, dX=None):
@@ -1142,7 +1145,7 @@ class _FusedQNEHVI(torch.autograd.Function):
         models = acqf.model.models
         need_grad = ctx.needs_input_grad[0]
         q = X3.shape[-2]
-        means, Ls, Fs, saved, status = [], [], [], [], []
+        saved, status = [], []
         pp = None
         keys = prime_prediction_caches(models)
         caches = [mm.prediction_cache(key=key) for mm, key in zip(models, keys)]
@@ -1155,25 +1158,38 @@ class _FusedQNEHVI(torch.autograd.Function):
         if (1 < len(models) <= 8 and kernels.split_plan(B, q_, c0.n)[0] != 0
                 and all(c.n == c0.n and c.np == c0.np and c.d == c0.d for c in caches)):
             pps = kernels.post_partials_members(caches, X3.detach(), store_R=True)
+        # the members' means, roots and baseline terms written straight into
+        # the stacked qEHVI inputs; outside graph capture their ladder
+        # outcomes folded into pinned words (as qEHVI's forward)
+        f64 = dict(dtype=torch.float64, device=X3.device)
+        M = len(models)
+        mean = torch.empty(M, B, q_, **f64)
+        L = torch.empty(M, B, q_, q_, **f64)
+        F = None
+        idx = kernels._dev_index(X3.device)
+        ps = kernels.pinned_status(X3.device) if (idx not in kernels._CAPTURE and M <= 8) else None
+        words = ps.arm(M) if ps is not None else [None] * M
         for t, mm in enumerate(models):
             cache = caches[t]
             ymean, ystd = mm.outcome_stats()
             pp = pps[t] if pps is not None else kernels.post_partials(
                 cache, X3.detach(), store_R=need_grad, cross=acqf._roots[t].Q_b)
-            T, F = acqf._roots[t].forward(cache, pp, ystd)
+            if F is None:
+                F = torch.empty(M, acqf._roots[t].Z_base.shape[0], pp.nrows_pad, **f64)
+            T, Ft = acqf._roots[t].forward(cache, pp, ystd, F_out=F[t])
             out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
-                                       want_cov=False, want_L=True, T=T, F=F)
+                                       want_cov=False, want_L=True, T=T, F=Ft, mean_out=mean[t],
+                                       L_out=L[t], status=words[t])
             status.append((out["info"], out["jitter"]))
-            means.append(out["mean"])
-            Ls.append(out["L"])
-            Fs.append(F)
             if need_grad:
                 saved.append((cache, pp, ystd, T, kernels.w_matrix(cache, pp)))
         Zq = acqf._base_samples_q(q, X3.device)
         lo, hi = acqf._cells
-        mean, L, F = torch.stack(means), torch.stack(Ls), torch.stack(Fs)
         acq = kernels.qehvi(mean, L, Zq, lo, hi, F=F, Qp=pp.Qp)
-        kernels.raise_not_psd_many(status, "qNEHVI posterior root")  # one read (as qEHVI)
+        if ps is not None:
+            kernels.raise_not_psd_members(ps, M, X3.device, "qNEHVI posterior root")
+        else:
+            kernels.raise_not_psd_many(status, "qNEHVI posterior root")  # one read (as qEHVI)
         if need_grad:
             ctx.acqf, ctx.saved, ctx.mean, ctx.L, ctx.F, ctx.Zq, ctx.Qp = (
                 acqf, saved, mean, L, F, Zq, pp.Qp)

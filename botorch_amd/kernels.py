@@ -104,7 +104,11 @@ def gemm(A, B, transA=False, transB=False, alpha=1.0, beta=0.0, C=None, flags=0)
     N = B3.shape[1] if transB else B3.shape[2]
     batch = A3.shape[0]
     if C is None:
-        C3 = torch.zeros(batch, M, N, dtype=torch.float64, device=dev)
+        # every element is written when beta = 0 (no fill launch); a lower-
+        # triangular result leaves the upper part to the zeros
+        alloc = torch.zeros if flags & _lib.GEMM_LOWER_C else torch.empty
+        C3 = alloc(batch, M, N, dtype=torch.float64, device=dev)
+        beta = 0.0
     else:
         C3 = C if batched else C.unsqueeze(0)
     check(lib().bo_gemm_f64(int(transA), int(transB), M, N, K, alpha, _p(A3), A3.shape[2],
