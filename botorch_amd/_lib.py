@@ -91,7 +91,8 @@ _SIGNATURES = {
     "bo_pinned_alloc": (c_int, [c_int64, POINTER(c_void_p), POINTER(c_void_p)]),
     "bo_pinned_free": (c_int, [c_void_p]),
     "bo_qmc_finalize_members": (c_int, [c_int, c_int, c_int, c_int, _P, _P, _P, c_int64, _P, _P, _P,
-                                        _P, c_int, c_double, _P, _P, _P, _P, c_int, _P, _P, _P]),
+                                        _P, c_int, c_double, _P, _P, _P, _P, c_int, _P, _P, _P,
+                                        c_int, c_int64, _P, c_int64, _P]),
     "bo_post_kxt_rows_members": (c_int, [c_int, c_int, _P, c_int, c_int, c_int, _P, _P, _P, c_int64,
                                          _P, _P, _P]),
     "bo_post_members_work": (c_int, [c_int, c_int64, c_int, c_int64, POINTER(c_int64)]),

@@ -1169,20 +1169,33 @@ class _FusedQNEHVI(torch.autograd.Function):
         idx = kernels._dev_index(X3.device)
         ps = kernels.pinned_status(X3.device) if (idx not in kernels._CAPTURE and M <= 8) else None
         words = ps.arm(M) if ps is not None else [None] * M
+        stats, Ts, pp_list = [], [], []
         for t, mm in enumerate(models):
             cache = caches[t]
             ymean, ystd = mm.outcome_stats()
+            stats.append((ymean, ystd))
             pp = pps[t] if pps is not None else kernels.post_partials(
                 cache, X3.detach(), store_R=need_grad, cross=acqf._roots[t].Q_b)
+            pp_list.append(pp)
             if F is None:
                 F = torch.empty(M, acqf._roots[t].Z_base.shape[0], pp.nrows_pad, **f64)
-            T, Ft = acqf._roots[t].forward(cache, pp, ystd, F_out=F[t])
-            out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
-                                       want_cov=False, want_L=True, T=T, F=Ft, mean_out=mean[t],
-                                       L_out=L[t], status=words[t])
-            status.append((out["info"], out["jitter"]))
+            T, _ = acqf._roots[t].forward(cache, pp, ystd, F_out=F[t])
+            Ts.append(T)
             if need_grad:
                 saved.append((cache, pp, ystd, T, kernels.w_matrix(cache, pp)))
+        same_parts = all(p_.Spart.shape == pp_list[0].Spart.shape for p_ in pp_list)
+        if M <= 8 and same_parts and all(c.kind == caches[0].kind for c in caches):
+            # every member's finalisation in one launch
+            info, jit = kernels.qmc_finalize_members(
+                caches, pp_list, stats, mean, L, status=words if ps is not None else None,
+                Ts=Ts, F=F)
+            status = [(info[t], jit[t]) for t in range(M)]
+        else:
+            for t in range(M):
+                out = kernels.qmc_finalize(caches[t], pp_list[t], _lib.QMC_CHOL, *stats[t],
+                                           want_mean=True, want_cov=False, want_L=True, T=Ts[t],
+                                           F=F[t], mean_out=mean[t], L_out=L[t], status=words[t])
+                status.append((out["info"], out["jitter"]))
         Zq = acqf._base_samples_q(q, X3.device)
         lo, hi = acqf._cells
         acq = kernels.qehvi(mean, L, Zq, lo, hi, F=F, Qp=pp.Qp)

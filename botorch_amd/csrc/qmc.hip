@@ -331,6 +331,8 @@ struct QmcMembers {
   double* jitter_out[QMC_MAXM];
   double* status_out[QMC_MAXM];
   int* status_count[QMC_MAXM];
+  const double* Tm[QMC_MAXM];  // cached-root qNEHVI: per member T (r x ldT) and F (S x ldF)
+  const double* F[QMC_MAXM];
   int nm;  // 0: the kernel's own arguments
 };
 
@@ -360,6 +362,8 @@ __global__ __launch_bounds__(THREADS) void qmc_kernel(
     jitter_out = qm.jitter_out[m];
     status_out = qm.status_out[m];
     status_count = qm.status_count[m];
+    Tm = qm.Tm[m];
+    F = qm.F[m];
   }
   // qNEI with the cached baseline root (utils/low_rank.py:85-173): Tm (r x ldT)
   // holds bl_chol^T = L_rr^{-1} Sigma'(X_base, X) per padded test row and F
@@ -728,7 +732,8 @@ extern "C" int bo_qmc_finalize_members(int nm, int kind, int B, int q, const dou
                                        double* const* L_out, int* const* info_out,
                                        double* const* jitter_out, int nparts,
                                        double* const* status_out, int* const* status_count,
-                                       void* stream) {
+                                       const double* const* Tm, int r, int64_t ldT,
+                                       const double* const* F, int64_t ldF, void* stream) {
   BO_CHECK_ARG(nm >= 1 && nm <= QMC_MAXM, "bo_qmc_finalize_members: %d models (1..%d)", nm, QMC_MAXM);
   BO_CHECK_ARG(kind == BO_RBF || kind == BO_MATERN52, "bad kernel kind %d", kind);
   BO_CHECK_ARG(nparts >= 0, "bo_qmc_finalize_members: nparts %d", nparts);
@@ -760,6 +765,10 @@ extern "C" int bo_qmc_finalize_members(int nm, int kind, int B, int q, const dou
     qm.jitter_out[m] = jitter_out[m];
     qm.status_out[m] = status_out ? status_out[m] : nullptr;
     qm.status_count[m] = status_out ? status_count[m] : nullptr;
+    BO_CHECK_ARG((Tm == nullptr) == (F == nullptr) && (Tm == nullptr || (r > 0 && Tm[m] && F[m])),
+                 "bo_qmc_finalize_members: cached-root members need T and F (r > 0)");
+    qm.Tm[m] = Tm ? Tm[m] : nullptr;
+    qm.F[m] = F ? F[m] : nullptr;
   }
   hipStream_t st = as_stream(stream);
   const dim3 grid((unsigned)B, (unsigned)nm);
@@ -767,8 +776,8 @@ extern "C" int bo_qmc_finalize_members(int nm, int kind, int B, int q, const dou
   qmc_kernel<KIND, QMC_CHOL><<<grid, THREADS, 0, st>>>(                                           \
       q, Qp, Xq[0], Spart[0], mpart[0], nC, nrows_pad, outputscale[0], constant[0], ymean[0],     \
       ystd[0], nullptr, 0, 0.0, nullptr, max_tries, jitter0, nullptr, mean_out[0], nullptr,       \
-      L_out[0], info_out[0], jitter_out[0], nullptr, 0, 0, nullptr, 0, LogRedParams{1.0, 1.0, 1}, \
-      0, qm.status_out[0], qm.status_count[0], qm)
+      L_out[0], info_out[0], jitter_out[0], qm.Tm[0], Tm ? r : 0, ldT, qm.F[0], ldF,               \
+      LogRedParams{1.0, 1.0, 1}, 0, qm.status_out[0], qm.status_count[0], qm)
   if (kind == BO_RBF) BO_QMC_M(BO_RBF);
   else BO_QMC_M(BO_MATERN52);
 #undef BO_QMC_M

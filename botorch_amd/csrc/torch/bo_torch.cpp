@@ -826,7 +826,8 @@ std::vector<at::Tensor> qehvi_members_eager(
     // max_tries 6: botorch/__init__.py:47 (cholesky_max_tries); jitter 1e-8: [G] cholesky_jitter
     ck(bo_qmc_finalize_members(M, int(kind), B, q, xq_c, sp_c, mp_c, n, outputscale.data(),
                                constant.data(), ymean.data(), ystd.data(), 6, 1e-8, mo, lo_, io, jo,
-                               nsmall, so, co, st), "qmc_finalize_members");
+                               nsmall, so, co, nullptr, 0, 0, nullptr, 0, st),
+       "qmc_finalize_members");
   }
   BoQehviArgs qa{};
   qa.struct_size = sizeof(qa);

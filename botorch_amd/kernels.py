@@ -737,6 +737,41 @@ def qmc_finalize(cache: GPCache, pp: PostPartials, mode: int, ymean: float, ystd
     return dict(acq=acq, mean=mean, cov=cov, L=L, info=info, jitter=jit)
 
 
+def qmc_finalize_members(caches, pps, stats, mean: torch.Tensor, L: torch.Tensor, status=None,
+                         Ts=None, F: Optional[torch.Tensor] = None):
+    """Root-only finalisation (QMC_CHOL: mean + jittered q x q root) of a
+    ModelListGP's members in ONE launch (bo_qmc_finalize_members): member t's
+    mean / root into mean[t] / L[t] (M x B x q / M x B x q x q, contiguous);
+    ``status``: per member (status_out, status_count) pointers
+    (pinned_status().arm); ``Ts`` / ``F``: the cached-root qNEHVI terms (T_t
+    r x nrows_pad, F[t] S x nrows_pad).  Returns (info, jitter), M x B."""
+    M = len(caches)
+    c0, p0 = caches[0], pps[0]
+    B, q = p0.B, p0.q
+    dev = mean.device
+    info = torch.empty(M, B, dtype=torch.int32, device=dev)
+    jit = torch.empty(M, B, dtype=torch.float64, device=dev)
+    P = ctypes.c_void_p * M
+    D = ctypes.c_double * M
+    nparts = int(p0.Spart.shape[0]) if p0.Spart.shape[0] != p0.nC else 0
+    st_out = P(*[w[0] for w in status]) if status is not None else None
+    st_cnt = P(*[w[1] for w in status]) if status is not None else None
+    Tp = P(*[t.data_ptr() for t in Ts]) if Ts is not None else None
+    Fp = P(*[F[t].data_ptr() for t in range(M)]) if F is not None else None
+    r = int(Ts[0].shape[0]) if Ts is not None else 0
+    ldT = int(Ts[0].shape[1]) if Ts is not None else 0
+    ldF = int(F.shape[2]) if F is not None else 0
+    check(lib().bo_qmc_finalize_members(
+        M, c0.kind, B, q, P(*[p.Xq.data_ptr() for p in pps]), P(*[p.Spart.data_ptr() for p in pps]),
+        P(*[p.mpart.data_ptr() for p in pps]), c0.n, D(*[float(c.outputscale) for c in caches]),
+        D(*[float(c.constant) for c in caches]), D(*[float(sv[0]) for sv in stats]),
+        D(*[float(sv[1]) for sv in stats]), CHOLESKY_MAX_TRIES, CHOLESKY_JITTER_F64,
+        P(*[mean[t].data_ptr() for t in range(M)]), P(*[L[t].data_ptr() for t in range(M)]),
+        P(*[info[t].data_ptr() for t in range(M)]), P(*[jit[t].data_ptr() for t in range(M)]),
+        nparts, st_out, st_cnt, Tp, r, ldT, Fp, ldF, _stream(dev)), "qmc_finalize_members")
+    return info, jit
+
+
 def sobol_engine_state(dim: int, seed: int):
     """Scrambled direction numbers + digital shift of torch's SobolEngine
     (the engine the reference's NormalQMCEngine wraps, sampling/qmc.py:56)."""

@@ -172,14 +172,17 @@ int bo_pinned_alloc(int64_t bytes, void** host, void** dev);
  * nm <= 8 models of one shape and kernel kind in ONE launch: per member its
  * rows Xq[m], partials Spart[m] / mpart[m] (nparts as bo_qmc_finalize_ext),
  * scalars and outputs; status_out (optional, with status_count) per member as
- * BoQmcFinalizeArgs.status_out.  A ModelListGP's members in the qEHVI forward. */
+ * BoQmcFinalizeArgs.status_out; Tm / F (optional, with r, ldT, ldF): each
+ * member's cached-root qNEHVI terms as BoQmcFinalizeArgs.Tm / F.  A
+ * ModelListGP's members in the qEHVI / qNEHVI forward. */
 int bo_qmc_finalize_members(int nm, int kind, int B, int q, const double* const* Xq,
                             const double* const* Spart, const double* const* mpart, int64_t n,
                             const double* outputscale, const double* constant, const double* ymean,
                             const double* ystd, int max_tries, double jitter0,
                             double* const* mean_out, double* const* L_out, int* const* info_out,
                             double* const* jitter_out, int nparts, double* const* status_out,
-                            int* const* status_count, void* stream);
+                            int* const* status_count, const double* const* Tm, int r,
+                            int64_t ldT, const double* const* F, int64_t ldF, void* stream);
 int bo_pinned_free(void* host);
 
 /* Pareto masks of S point sets (Y: S x n x m, m <= 8; out: S x n bytes, 1 =

@@ -206,7 +206,8 @@ def test_qmc_finalize_members_bit_equal_to_per_member():
         P(*[L[m].data_ptr() for m in range(M)]), P(*[info[m].data_ptr() for m in range(M)]),
         P(*[jit[m].data_ptr() for m in range(M)]), nparts,
         P(*[status[m].data_ptr() for m in range(M)]),
-        P(*[count[m:].data_ptr() for m in range(M)]), kernels._stream(X.device)),
+        P(*[count[m:].data_ptr() for m in range(M)]), None, 0, 0, None, 0,
+        kernels._stream(X.device)),
         "qmc_finalize_members")
     for m, r in enumerate(refs):
         assert torch.equal(mean[m], r["mean"])
