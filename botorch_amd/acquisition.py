@@ -975,14 +975,22 @@ class _FusedQEHVI(torch.autograd.Function):
         ps = kernels.pinned_status(X3.device) if (idx not in kernels._CAPTURE and
                                                   len(models) <= 8) else None
         words = ps.arm(len(models)) if ps is not None else [None] * len(models)
-        for t, (mm, cache, pp) in enumerate(zip(models, caches, pps)):
-            ymean, ystd = mm.outcome_stats()
-            out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, ymean, ystd, want_mean=True,
-                                       want_cov=False, want_L=True, mean_out=mean[t], L_out=L[t],
-                                       status=words[t])
-            status.append((out["info"], out["jitter"]))
-            if need_grad:
-                saved.append((cache, pp, ystd, kernels.w_matrix(cache, pp)))
+        stats = [mm.outcome_stats() for mm in models]
+        if (len(models) <= 8 and all(p_.Spart.shape == pps[0].Spart.shape for p_ in pps)
+                and all(c.kind == caches[0].kind for c in caches)):
+            # every member's finalisation in one launch
+            info, jit = kernels.qmc_finalize_members(caches, pps, stats, mean, L,
+                                                     status=words if ps is not None else None)
+            status = [(info[t], jit[t]) for t in range(len(models))]
+        else:
+            for t, (cache, pp) in enumerate(zip(caches, pps)):
+                out = kernels.qmc_finalize(cache, pp, _lib.QMC_CHOL, *stats[t], want_mean=True,
+                                           want_cov=False, want_L=True, mean_out=mean[t],
+                                           L_out=L[t], status=words[t])
+                status.append((out["info"], out["jitter"]))
+        if need_grad:
+            for t, (cache, pp) in enumerate(zip(caches, pps)):
+                saved.append((cache, pp, stats[t][1], kernels.w_matrix(cache, pp)))
         sampler = acqf._ensure_sampler()
         Z = sampler.base_samples_2d(q * len(models), X3.device)
         lo, hi = acqf._cells(X3.device)
