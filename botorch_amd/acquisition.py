@@ -1175,7 +1175,12 @@ class _FusedQNEHVI(torch.autograd.Function):
         L = torch.empty(M, B, q_, q_, **f64)
         F = None
         idx = kernels._dev_index(X3.device)
-        ps = kernels.pinned_status(X3.device) if (idx not in kernels._CAPTURE and M <= 8) else None
+        # forward-only calls defer the ladder outcome (the eager qEI's ring:
+        # no stream sync per call); the gradient path reads it at once
+        # through pinned words
+        defer = not need_grad and not kernels.SYNC_LADDER and idx not in kernels._CAPTURE
+        ps = (kernels.pinned_status(X3.device)
+              if (not defer and idx not in kernels._CAPTURE and M <= 8) else None)
         words = ps.arm(M) if ps is not None else [None] * M
         stats, Ts, pp_list = [], [], []
         for t, mm in enumerate(models):
@@ -1207,7 +1212,11 @@ class _FusedQNEHVI(torch.autograd.Function):
         Zq = acqf._base_samples_q(q, X3.device)
         lo, hi = acqf._cells
         acq = kernels.qehvi(mean, L, Zq, lo, hi, F=F, Qp=pp.Qp)
-        if ps is not None:
+        if defer:
+            kernels.raise_not_psd_deferred(torch.cat([i_.reshape(-1) for i_, _ in status]),
+                                           torch.cat([j_.reshape(-1) for _, j_ in status]),
+                                           "qNEHVI posterior root")
+        elif ps is not None:
             kernels.raise_not_psd_members(ps, M, X3.device, "qNEHVI posterior root")
         else:
             kernels.raise_not_psd_many(status, "qNEHVI posterior root")  # one read (as qEHVI)
