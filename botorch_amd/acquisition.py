@@ -1182,20 +1182,31 @@ class _FusedQNEHVI(torch.autograd.Function):
         ps = (kernels.pinned_status(X3.device)
               if (not defer and idx not in kernels._CAPTURE and M <= 8) else None)
         words = ps.arm(M) if ps is not None else [None] * M
-        stats, Ts, pp_list = [], [], []
-        for t, mm in enumerate(models):
-            cache = caches[t]
-            ymean, ystd = mm.outcome_stats()
-            stats.append((ymean, ystd))
-            pp = pps[t] if pps is not None else kernels.post_partials(
-                cache, X3.detach(), store_R=need_grad, cross=acqf._roots[t].Q_b)
-            pp_list.append(pp)
-            if F is None:
-                F = torch.empty(M, acqf._roots[t].Z_base.shape[0], pp.nrows_pad, **f64)
-            T, _ = acqf._roots[t].forward(cache, pp, ystd, F_out=F[t])
-            Ts.append(T)
+        stats = [mm.outcome_stats() for mm in models]
+        batched = pps is not None and _roots_batched(acqf, caches, pps, stats)
+        if batched:
+            # every member's T and F in three batched GEMMs over the members
+            Ts, F = _roots_forward_batched(acqf, caches, pps, stats)
+            pp_list = list(pps)
             if need_grad:
-                saved.append((cache, pp, ystd, T, kernels.w_matrix(cache, pp)))
+                for t in range(M):
+                    saved.append((caches[t], pps[t], stats[t][1], Ts[t],
+                                  kernels.w_matrix(caches[t], pps[t])))
+        else:
+            Ts, pp_list = [], []
+            for t, mm in enumerate(models):
+                cache = caches[t]
+                ystd = stats[t][1]
+                pp = pps[t] if pps is not None else kernels.post_partials(
+                    cache, X3.detach(), store_R=need_grad, cross=acqf._roots[t].Q_b)
+                pp_list.append(pp)
+                if F is None:
+                    F = torch.empty(M, acqf._roots[t].Z_base.shape[0], pp.nrows_pad, **f64)
+                T, _ = acqf._roots[t].forward(cache, pp, ystd, F_out=F[t])
+                Ts.append(T)
+                if need_grad:
+                    saved.append((cache, pp, ystd, T, kernels.w_matrix(cache, pp)))
+        pp = pp_list[-1]
         same_parts = all(p_.Spart.shape == pp_list[0].Spart.shape for p_ in pp_list)
         if M <= 8 and same_parts and all(c.kind == caches[0].kind for c in caches):
             # every member's finalisation in one launch
@@ -1236,6 +1247,51 @@ class _FusedQNEHVI(torch.autograd.Function):
             dX = ctx.acqf._roots[t].backward(cache, pp, W, dmean[t], dcov, dF[t].contiguous(), T,
                                              ystd, dX=dX)
         return dX, None
+
+
+def _roots_batched(acqf, caches, pps, stats) -> bool:
+    """Whether the members' cached-root terms can go as batched GEMMs: R^T
+    stacked by the members' route, equal baseline sizes and sample counts."""
+    roots = acqf._roots
+    if any(p_.Rt is None or p_.Cx is not None for p_ in pps):
+        return False
+    r0, S0 = roots[0].Linv.shape[0], roots[0].Z_base.shape[0]
+    if any(rt.Linv.shape[0] != r0 or rt.Z_base.shape[0] != S0 for rt in roots):
+        return False
+    base = pps[0].Rt
+    step = base.numel()
+    return all(p_.Rt.data_ptr() == base.data_ptr() + 8 * step * t and p_.Rt.is_contiguous()
+               for t, p_ in enumerate(pps))
+
+
+def _roots_forward_batched(acqf, caches, pps, stats):
+    """_CachedBaselineRoot.forward for all members at once: T_t = s_t^2
+    (L_rr,t^-1 K(X_b, X)_t - P_b,t R_t^T), F_t = Z_base,t T_t as three batched
+    GEMMs over the members (the s_t^2 folded into stacked copies of L_rr^-1
+    and P_b, rebuilt when the outcome scales change)."""
+    roots = acqf._roots
+    M = len(roots)
+    p0 = pps[0]
+    dev = p0.Xq.device
+    key = (tuple(float(s_[1]) for s_ in stats), str(dev))
+    stk = acqf.__dict__.get("_root_stack")
+    if stk is None or stk[0] != key:
+        s2 = [float(s_[1]) ** 2 for s_ in stats]
+        stk = (key, torch.stack([rt.Linv * s2[t] for t, rt in enumerate(roots)]).contiguous(),
+               torch.stack([rt.P_b * s2[t] for t, rt in enumerate(roots)]).contiguous(),
+               torch.stack([rt.Z_base for rt in roots]).contiguous(),
+               torch.ones(kernels.DP, dtype=torch.float64, device=dev))
+        acqf.__dict__["_root_stack"] = stk
+    _, Linv_s, Pb_s, Zb, ones = stk
+    r = Linv_s.shape[1]
+    Kbx = torch.empty(M, r, p0.nrows_pad, dtype=torch.float64, device=dev)
+    for t, (rt, c, p_) in enumerate(zip(roots, caches, pps)):
+        kernels.covar_matrix(rt.Xb_scaled, p_.Xq, ones, c.kind, c.outputscale, out=Kbx[t])
+    T = kernels.gemm(Linv_s, Kbx, flags=_lib.GEMM_A_LOWER)
+    Rt_all = p0.Rt.as_strided((M,) + tuple(p0.Rt.shape), (p0.Rt.numel(),) + tuple(p0.Rt.stride()))
+    T = kernels.gemm(Pb_s, Rt_all, alpha=-1.0, beta=1.0, C=T)
+    F = kernels.gemm(Zb, T)
+    return [T[t] for t in range(M)], F
 
 
 class _QEHVIFromRoots(torch.autograd.Function):

@@ -127,11 +127,13 @@ def gemm_strided(M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, alpha=1.0, 
     return C
 
 
-def covar_matrix(X1, X2, lengthscale, kind=_lib.RBF, outputscale=1.0, diag_add=0.0):
+def covar_matrix(X1, X2, lengthscale, kind=_lib.RBF, outputscale=1.0, diag_add=0.0, out=None):
     dev = _dev(X1, X2, lengthscale)
     n1, d = X1.shape
     n2 = X2.shape[0]
-    K = torch.empty(n1, n2, dtype=torch.float64, device=dev)
+    K = out if out is not None else torch.empty(n1, n2, dtype=torch.float64, device=dev)
+    if tuple(K.shape) != (n1, n2) or not K.is_contiguous():
+        raise ValueError("covar_matrix: out must be a contiguous n1 x n2 fp64 tensor")
     check(lib().bo_covar_matrix(kind, _p(X1.contiguous()), n1, _p(X2.contiguous()), n2, d,
                                 _p(lengthscale.contiguous()), outputscale, diag_add, 0, _p(K),
                                 n2, n1, n2, _stream(dev)), "covar_matrix")
@@ -508,10 +510,11 @@ def post_partials_members(caches, X: torch.Tensor, store_R: bool = False) -> lis
     Xc = X.contiguous()
     pps, ptrs = [], {k: [] for k in ("Kt", "U", "beta", "S", "m", "Rt")}
     Xqs, Kts = _kxt_rows_members(caches, Xc, nrows_pad)
-    for c, Xq, Kt in zip(caches, Xqs, Kts):
+    Rt_all = torch.empty(len(caches), nC * 128, nrows_pad, **f64) if store_R else None
+    for m_, (c, Xq, Kt) in enumerate(zip(caches, Xqs, Kts)):
         Sp = torch.empty(nparts, nrows_pad // 16, 16, 16, **f64)
         mp = torch.empty(nparts, nrows_pad, **f64)
-        Rt = torch.empty(nC * 128, nrows_pad, **f64) if store_R else None
+        Rt = Rt_all[m_] if store_R else None
         pps.append(PostPartials(B, q, Qp, nrows_pad, nC, Xq, Sp, mp, Rt))
         for k, t in (("Kt", Kt), ("U", c.U), ("beta", c.beta), ("S", Sp), ("m", mp), ("Rt", Rt)):
             ptrs[k].append(_p(t).value if t is not None else None)
@@ -570,10 +573,13 @@ def _post_members_streamk(caches, X: torch.Tensor, store_R: bool, work_elems: in
     Xc = X.contiguous()
     pps, ptrs = [], {k: [] for k in ("Kt", "U", "beta", "S", "m", "Rt")}
     Xqs, Kts = _kxt_rows_members(caches, Xc, nrows_pad)
-    for c, Xq, Kt in zip(caches, Xqs, Kts):
+    # the members' R^T stacked (M x np x nrows_pad): slices per member, and
+    # batched GEMMs over all members read it as one operand (qNEHVI)
+    Rt_all = torch.empty(len(caches), nC * 128, nrows_pad, **f64) if store_R else None
+    for m_, (c, Xq, Kt) in enumerate(zip(caches, Xqs, Kts)):
         Sp = torch.empty(nC, nrows_pad // 16, 16, 16, **f64)
         mp = torch.empty(nC, nrows_pad, **f64)
-        Rt = torch.empty(nC * 128, nrows_pad, **f64) if store_R else None
+        Rt = Rt_all[m_] if store_R else None
         pps.append(PostPartials(B, q, Qp, nrows_pad, nC, Xq, Sp, mp, Rt))
         for k, t in (("Kt", Kt), ("U", c.U), ("beta", c.beta), ("S", Sp), ("m", mp), ("Rt", Rt)):
             ptrs[k].append(_p(t).value if t is not None else None)

@@ -241,3 +241,47 @@ def test_qnehvi_without_cached_root(m, q):
     torch.testing.assert_close(gx, go, rtol=1e-5, atol=1e-8)
     torch.testing.assert_close(v, vc, rtol=1e-6, atol=1e-9)
     torch.testing.assert_close(gx, gc, rtol=1e-4, atol=1e-7)
+
+
+def test_qnehvi_members_batched_roots_match_per_member(monkeypatch):
+    """At a size whose one-model plan splits k (n = 1024: the members' route
+    stores R^T stacked), the members' cached-root terms go as batched GEMMs
+    over the members (acquisition._roots_forward_batched); values and
+    gradients equal the per-member route (s^2 folded into the operands:
+    rounding only)."""
+    import torch
+    from botorch_amd import acquisition, kernels
+    from botorch_amd.acquisition import qNoisyExpectedHypervolumeImprovement
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    X, Y, model, _, _ = _setup(3, n=1024, r=40, seed=3)
+    assert kernels.split_plan(32, 4, 1024)[0] != 0  # stream-K: the members' route applies
+    acqf = qNoisyExpectedHypervolumeImprovement(model, [-1.1] * 3, X[:40].to(DEV),
+                                                sampler=SobolQMCNormalSampler(torch.Size([64]), seed=0),
+                                                prune_baseline=False)
+    Xc = torch.rand(32, 4, 6, dtype=torch.float64, generator=torch.Generator().manual_seed(1)).to(DEV)
+    calls = []
+    orig = acquisition._roots_forward_batched
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(acquisition, "_roots_forward_batched", spy)
+
+    def run():
+        Xg = Xc.clone().requires_grad_(True)
+        v = acqf(Xg)
+        (g,) = torch.autograd.grad(v.sum(), Xg)
+        with torch.no_grad():
+            v2 = acqf(Xc)
+        kernels.check_ladder_status(DEV)
+        return v.detach().cpu(), g.cpu(), v2.cpu()
+
+    v1, g1, w1 = run()
+    assert calls, "the batched roots route did not run"
+    monkeypatch.setattr(acquisition, "_roots_batched", lambda *a, **k: False)
+    v0, g0, w0 = run()
+    assert (v0 > 0).sum() > 5
+    torch.testing.assert_close(v1, v0, rtol=1e-10, atol=1e-13)
+    torch.testing.assert_close(w1, w0, rtol=1e-10, atol=1e-13)
+    torch.testing.assert_close(g1, g0, rtol=1e-8, atol=1e-11)
