@@ -35,4 +35,14 @@ with torch.no_grad():
         v = acqf(Xd)
     torch.cuda.synchronize()
     ms = 1e3 * (time.perf_counter() - t0) / steps
-print("done", float(v.sum()), "r", int(acqf.X_baseline.shape[0]), "ms_per_call", round(ms, 4))
+Xg = Xd.clone().requires_grad_(True)
+for _ in range(2):
+    (gx,) = torch.autograd.grad(acqf(Xg).sum(), Xg)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(steps // 2):
+    (gx,) = torch.autograd.grad(acqf(Xg).sum(), Xg)
+torch.cuda.synchronize()
+ms_fb = 1e3 * (time.perf_counter() - t0) / (steps // 2)
+print("done", float(v.sum()), "r", int(acqf.X_baseline.shape[0]), "ms_per_call", round(ms, 4),
+      "fwd_bwd_ms", round(ms_fb, 4), "grad_abs", float(gx.abs().sum()))
