@@ -841,6 +841,9 @@ constexpr int SMU = 32;  // test rows and training columns per unit tile
 #ifndef SMALL_DEPTH
 #define SMALL_DEPTH 2  // k-steps of operands in flight per wave (A/B: -DSMALL_DEPTH=3)
 #endif
+#ifndef SMALL_PAIRED
+#define SMALL_PAIRED 1  // both tiles of a pair over their common k-range (A/B: 0)
+#endif
 
 __device__ __forceinline__ void small_load(const double* __restrict__ U, int64_t ldu,
                                            const double* __restrict__ Kt, int64_t ldk, int kb,
@@ -921,6 +924,67 @@ __device__ __forceinline__ void small_tile(const double* __restrict__ U, int64_t
 #endif
 }
 
+// Both tiles of a pair together over their common k-range (round 5): the
+// K*x^T operand (rows k, the unit's 32 test rows) is the same for both
+// column tiles there, so it is loaded once for the two tiles' 8 MFMAs per
+// 4-deep step -- half the K*x^T traffic of the common range and 8
+// independent accumulator chains per wave instead of 4.  Steps s of the
+// common range go to wave s % 4 (first = wave), each tile's own sum in
+// k order.  Tile B's remaining steps follow in small_tile.
+__device__ __forceinline__ void small_load2(const double* __restrict__ U, int64_t ldu,
+                                            const double* __restrict__ Kt, int64_t ldk, int kb,
+                                            int cA, int cB, int r0, int lane, double (&aA)[4][2],
+                                            double (&aB)[4][2], double (&b)[4][2]) {
+  const int kr = lane >> 4, cl = lane & 15;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int64_t k = kb + 4 * ks + kr;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      aA[ks][h] = U[k * ldu + cA + 16 * h + cl];
+      aB[ks][h] = U[k * ldu + cB + 16 * h + cl];
+      b[ks][h] = Kt[k * ldk + r0 + 16 * h + cl];
+    }
+  }
+}
+
+__device__ __forceinline__ void small_pair(const double* __restrict__ U, int64_t ldu,
+                                           const double* __restrict__ Kt, int64_t ldk, int cA, int cB,
+                                           int r0, int nsteps, int first, int lane,
+                                           v4d (&accA)[2][2], v4d (&accB)[2][2]) {
+  double aA0[4][2], aB0[4][2], b0[4][2], aA1[4][2], aB1[4][2], b1[4][2];
+  int s = first;
+  if (s < nsteps) small_load2(U, ldu, Kt, ldk, PK * s, cA, cB, r0, lane, aA0, aB0, b0);
+  if (s + 4 < nsteps) small_load2(U, ldu, Kt, ldk, PK * (s + 4), cA, cB, r0, lane, aA1, aB1, b1);
+  for (; s < nsteps; s += 4) {
+    double aA2[4][2], aB2[4][2], b2[4][2];
+    const bool more = s + 8 < nsteps;
+    if (more) small_load2(U, ldu, Kt, ldk, PK * (s + 8), cA, cB, r0, lane, aA2, aB2, b2);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int hc = 0; hc < 2; ++hc)
+#pragma unroll
+        for (int hr = 0; hr < 2; ++hr) {
+          accA[hc][hr] = mfma_f64(aA0[ks][hc], b0[ks][hr], accA[hc][hr]);
+          accB[hc][hr] = mfma_f64(aB0[ks][hc], b0[ks][hr], accB[hc][hr]);
+        }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        aA0[ks][h] = aA1[ks][h];
+        aB0[ks][h] = aB1[ks][h];
+        b0[ks][h] = b1[ks][h];
+        if (more) {
+          aA1[ks][h] = aA2[ks][h];
+          aB1[ks][h] = aB2[ks][h];
+          b1[ks][h] = b2[ks][h];
+        }
+      }
+  }
+}
+
 // One launch serves up to 8 models of one shape (the members of a
 // ModelListGP: C4's three outputs): block b -> member b / units, unit b % units.
 constexpr int SMALL_MAXM = 8;
@@ -966,8 +1030,18 @@ __global__ __launch_bounds__(256, 2) void post_small_kernel(const SmallArgs a) {
   // tile t: k in [0, 32 (ct + 1)), 2 (ct + 1) steps of 16; the second tile's
   // steps are dealt from the wave after the one that took the first's last step
   const int sA = 2 * (ctA + 1), sB = 2 * (ctB + 1);
+#if SMALL_PAIRED
+  // the common k-range of both tiles (sA <= sB: ctA < ctB), then tile B's rest
+  small_pair(U, ldu, Kt, ldk, SMU * ctA, SMU * ctB, r0, sA, wave, lane, acc[0], acc[1]);
+  if (sB > sA) {
+    // tile B's steps sA.. continue the round robin: step s on wave s % 4
+    const int firstB = sA + ((wave - sA % 4 + 4) % 4);
+    small_tile(U, ldu, Kt, ldk, SMU * ctB, r0, sB, firstB, lane, acc[1]);
+  }
+#else
   small_tile(U, ldu, Kt, ldk, SMU * ctA, r0, sA, wave, lane, acc[0]);
   small_tile(U, ldu, Kt, ldk, SMU * ctB, r0, sB, (wave - sA % 4 + 4) % 4, lane, acc[1]);
+#endif
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
