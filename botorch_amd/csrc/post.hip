@@ -844,6 +844,10 @@ constexpr int SMU = 32;  // test rows and training columns per unit tile
 #ifndef SMALL_PAIRED
 #define SMALL_PAIRED 1  // both tiles of a pair over their common k-range (A/B: 0)
 #endif
+#ifndef SMALL_WAVES
+#define SMALL_WAVES 4  // waves per unit, taking the k-steps in turn (A/B: 8)
+#endif
+constexpr int SMW = SMALL_WAVES;
 
 __device__ __forceinline__ void small_load(const double* __restrict__ U, int64_t ldu,
                                            const double* __restrict__ Kt, int64_t ldk, int kb,
@@ -869,15 +873,15 @@ __device__ __forceinline__ void small_tile(const double* __restrict__ U, int64_t
   double a0[4][2], b0[4][2], a1[4][2], b1[4][2];
   int s = first;
   if (s < nsteps) small_load(U, ldu, Kt, ldk, PK * s, c0, r0, lane, a0, b0);
-  if (s + 4 < nsteps) small_load(U, ldu, Kt, ldk, PK * (s + 4), c0, r0, lane, a1, b1);
+  if (s + SMW < nsteps) small_load(U, ldu, Kt, ldk, PK * (s + SMW), c0, r0, lane, a1, b1);
 #if SMALL_DEPTH >= 3
   // a third step of operands in flight (BO A/B: SMALL_DEPTH)
   double a2[4][2], b2[4][2];
-  if (s + 8 < nsteps) small_load(U, ldu, Kt, ldk, PK * (s + 8), c0, r0, lane, a2, b2);
-  for (; s < nsteps; s += 4) {
+  if (s + 2 * SMW < nsteps) small_load(U, ldu, Kt, ldk, PK * (s + 2 * SMW), c0, r0, lane, a2, b2);
+  for (; s < nsteps; s += SMW) {
     double a3[4][2], b3[4][2];
-    const bool more = s + 12 < nsteps;
-    if (more) small_load(U, ldu, Kt, ldk, PK * (s + 12), c0, r0, lane, a3, b3);
+    const bool more = s + 3 * SMW < nsteps;
+    if (more) small_load(U, ldu, Kt, ldk, PK * (s + 3 * SMW), c0, r0, lane, a3, b3);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
@@ -899,10 +903,10 @@ __device__ __forceinline__ void small_tile(const double* __restrict__ U, int64_t
       }
   }
 #else
-  for (; s < nsteps; s += 4) {
+  for (; s < nsteps; s += SMW) {
     double a2[4][2], b2[4][2];
-    const bool more = s + 8 < nsteps;
-    if (more) small_load(U, ldu, Kt, ldk, PK * (s + 8), c0, r0, lane, a2, b2);
+    const bool more = s + 2 * SMW < nsteps;
+    if (more) small_load(U, ldu, Kt, ldk, PK * (s + 2 * SMW), c0, r0, lane, a2, b2);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
@@ -955,11 +959,11 @@ __device__ __forceinline__ void small_pair(const double* __restrict__ U, int64_t
   double aA0[4][2], aB0[4][2], b0[4][2], aA1[4][2], aB1[4][2], b1[4][2];
   int s = first;
   if (s < nsteps) small_load2(U, ldu, Kt, ldk, PK * s, cA, cB, r0, lane, aA0, aB0, b0);
-  if (s + 4 < nsteps) small_load2(U, ldu, Kt, ldk, PK * (s + 4), cA, cB, r0, lane, aA1, aB1, b1);
-  for (; s < nsteps; s += 4) {
+  if (s + SMW < nsteps) small_load2(U, ldu, Kt, ldk, PK * (s + SMW), cA, cB, r0, lane, aA1, aB1, b1);
+  for (; s < nsteps; s += SMW) {
     double aA2[4][2], aB2[4][2], b2[4][2];
-    const bool more = s + 8 < nsteps;
-    if (more) small_load2(U, ldu, Kt, ldk, PK * (s + 8), cA, cB, r0, lane, aA2, aB2, b2);
+    const bool more = s + 2 * SMW < nsteps;
+    if (more) small_load2(U, ldu, Kt, ldk, PK * (s + 2 * SMW), cA, cB, r0, lane, aA2, aB2, b2);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
@@ -1002,9 +1006,12 @@ struct SmallArgs {
   int n, nct, units;
 };
 
-__global__ __launch_bounds__(256, 2) void post_small_kernel(const SmallArgs a) {
-  // [source wave][tile][hc][hr][register][lane]: 64 KB
-  __shared__ __attribute__((aligned(16))) double red[4][2][2][2][4][64];
+// SMW waves per unit (round 5: 8, two per SIMD -- with one, half of every
+// wave's cycles waited on its operand loads at C2, SQ_WAIT_INST_ANY /
+// SQ_WAVE_CYCLES = 0.52, MFMA busy 0.27; tools/pmc_small.sh)
+__global__ __launch_bounds__(64 * SMW, 8 / SMW) void post_small_kernel(const SmallArgs a) {
+  // [source wave][tile][hc][hr][register][lane]: 16 KB per wave
+  __shared__ __attribute__((aligned(16))) double red[SMW][2][2][2][4][64];
   const int npair = a.nct >> 1;
   const int mem = blockIdx.x / a.units;
   const int unit = blockIdx.x - mem * a.units;
@@ -1035,12 +1042,12 @@ __global__ __launch_bounds__(256, 2) void post_small_kernel(const SmallArgs a) {
   small_pair(U, ldu, Kt, ldk, SMU * ctA, SMU * ctB, r0, sA, wave, lane, acc[0], acc[1]);
   if (sB > sA) {
     // tile B's steps sA.. continue the round robin: step s on wave s % 4
-    const int firstB = sA + ((wave - sA % 4 + 4) % 4);
+    const int firstB = sA + ((wave - sA % SMW + SMW) % SMW);
     small_tile(U, ldu, Kt, ldk, SMU * ctB, r0, sB, firstB, lane, acc[1]);
   }
 #else
   small_tile(U, ldu, Kt, ldk, SMU * ctA, r0, sA, wave, lane, acc[0]);
-  small_tile(U, ldu, Kt, ldk, SMU * ctB, r0, sB, (wave - sA % 4 + 4) % 4, lane, acc[1]);
+  small_tile(U, ldu, Kt, ldk, SMU * ctB, r0, sB, (wave - sA % SMW + SMW) % SMW, lane, acc[1]);
 #endif
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -1051,21 +1058,22 @@ __global__ __launch_bounds__(256, 2) void post_small_kernel(const SmallArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) red[wave][t][hc][hr][r][lane] = acc[t][hc][hr][r];
   __syncthreads();
-  // wave (t, hr): the unit's R^T block of tile t, row half hr, summed in wave order
-  const int t = wave >> 1, hr = wave & 1;
+  // wave (t, hr) < 4: the unit's R^T block of tile t, row half hr, summed in
+  // wave order (waves 4.. only meet the barriers)
+  const bool role = wave < 4;
+  const int t = (wave >> 1) & 1, hr = wave & 1;
   double v[2][4];
 #pragma unroll
   for (int hc = 0; hc < 2; ++hc)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       double x = red[0][t][hc][hr][r][lane];
-      x += red[1][t][hc][hr][r][lane];
-      x += red[2][t][hc][hr][r][lane];
-      x += red[3][t][hc][hr][r][lane];
+#pragma unroll
+      for (int w = 1; w < SMW; ++w) x += red[w][t][hc][hr][r][lane];
       v[hc][r] = x;
     }
   const int c0 = SMU * (t ? ctB : ctA);
-  if (M.Rt != nullptr) {  // row-major R^T: 16 lanes = one 128-B row segment
+  if (role && M.Rt != nullptr) {  // row-major R^T: 16 lanes = one 128-B row segment
 #pragma unroll
     for (int hc = 0; hc < 2; ++hc)
 #pragma unroll
@@ -1088,13 +1096,13 @@ __global__ __launch_bounds__(256, 2) void post_small_kernel(const SmallArgs a) {
   __syncthreads();  // every wave's reads of red done
   double* xP = &red[0][0][0][0][0][0];  // tile 1's blocks handed to tile 0's waves
   double* xm = xP + 2 * 4 * 64;
-  if (t == 1) {
+  if (role && t == 1) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) xP[(hr * 4 + r) * 64 + lane] = P[r];
     xm[hr * 64 + lane] = m;
   }
   __syncthreads();
-  if (t == 0) {
+  if (role && t == 0) {
     const int nrows16 = (int)(ldk >> 4);
     const int row16 = (r0 >> 4) + hr;
     double* sp = M.Spart + ((int64_t)p * nrows16 + row16) * 256;
@@ -1445,7 +1453,7 @@ int bo_post_small_batched(int nm, const double* const* Kt, const double* const* 
   a.n = (int)n;
   a.nct = (int)(np / SMU);
   a.units = (int)(ceil_div(B * Qp, SMU) * (a.nct / 2));
-  post_small_kernel<<<(unsigned)(a.units * nm), 256, 0, as_stream(stream)>>>(a);
+  post_small_kernel<<<(unsigned)(a.units * nm), 64 * SMW, 0, as_stream(stream)>>>(a);
   BO_LAUNCH_CHECK();
   return BO_OK;
 }
