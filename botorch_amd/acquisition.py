@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import copy
 import math
+import os
 import warnings
 from typing import Callable, List, Optional, Union
 
@@ -1234,6 +1235,7 @@ class _FusedQNEHVI(torch.autograd.Function):
         if need_grad:
             ctx.acqf, ctx.saved, ctx.mean, ctx.L, ctx.F, ctx.Zq, ctx.Qp = (
                 acqf, saved, mean, L, F, Zq, pp.Qp)
+            ctx.batched = batched
         return acq
 
     @staticmethod
@@ -1242,11 +1244,53 @@ class _FusedQNEHVI(torch.autograd.Function):
         dmean, dL, dF = kernels.qehvi_backward(ctx.mean, ctx.L, ctx.Zq, lo, hi, dacq, F=ctx.F,
                                                Qp=ctx.Qp)
         dX = None
+        if ctx.batched and _BWD_BATCHED:
+            return _roots_backward_batched(ctx, dmean, dL, dF), None
         for t, (cache, pp, ystd, T, W) in enumerate(ctx.saved):
             dcov = kernels.chol_backward(ctx.L[t], dL[t])
             dX = ctx.acqf._roots[t].backward(cache, pp, W, dmean[t], dcov, dF[t].contiguous(), T,
                                              ystd, dX=dX)
         return dX, None
+
+
+# BO_QNEHVI_BWD_BATCHED=0: the per-member backward on the batched forward (A/B)
+_BWD_BATCHED = os.environ.get("BO_QNEHVI_BWD_BATCHED", "1") != "0"
+
+
+def _roots_backward_batched(ctx, dmean, dL, dF):
+    """_CachedBaselineRoot.backward for all members at once (the forward's
+    batched route): dT = Z_base^T dF and the dK*x / dK(X_b, X) GEMMs batched
+    over the members (s^2 folded into the stacked operands), the per-t-batch
+    dT -= T G and the two post_backward passes per member."""
+    acqf = ctx.acqf
+    roots = acqf._roots
+    M = len(roots)
+    _, Linv_s, _, Zb, _ = acqf.__dict__["_root_stack"]
+    Qb_s = acqf.__dict__.get("_root_stack_qb")
+    key = acqf.__dict__["_root_stack"][0]
+    if Qb_s is None or Qb_s[0] != key:
+        s2 = [float(sv) ** 2 for sv in key[0]]
+        Qb_s = (key, torch.stack([rt.Q_b * (-s2[t]) for t, rt in enumerate(roots)]).contiguous())
+        acqf.__dict__["_root_stack_qb"] = Qb_s
+    Qb_s = Qb_s[1]
+    dT = kernels.gemm(Zb, dF.contiguous(), transA=True)                 # M x r x N
+    r = dT.shape[1]
+    dcovs = []
+    for t, (cache, pp, ystd, T, W) in enumerate(ctx.saved):
+        dcov = kernels.chol_backward(ctx.L[t], dL[t])
+        dcovs.append(dcov)
+        G = (dcov + dcov.mT).contiguous()
+        q, Qp, nrows, B = pp.q, pp.Qp, pp.nrows_pad, pp.B
+        kernels.gemm_strided(r, q, q, T, nrows, Qp, G, q, q * q, dT[t], nrows, Qp, B,
+                             alpha=-1.0, beta=1.0)                      # dT_b -= T_b G_b
+    E = kernels.gemm(dT, Qb_s, transA=True)                             # M x N x np
+    dKbx = kernels.gemm(Linv_s, dT, transA=True, flags=_lib.GEMM_A_UPPER)  # M x r x N
+    dX = None
+    for t, (cache, pp, ystd, T, W) in enumerate(ctx.saved):
+        dX = kernels.post_backward(cache, pp, W, dmean[t], dcovs[t], ystd, E=E[t], dX=dX)
+        dX = kernels.post_backward(cache, pp, None, None, None, ystd, E=dKbx[t].mT.contiguous(),
+                                   Xt_scaled=roots[t].Xb_scaled, n=r, dX=dX)
+    return dX
 
 
 def _roots_batched(acqf, caches, pps, stats) -> bool:
