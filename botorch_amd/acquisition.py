@@ -1284,11 +1284,12 @@ def _roots_backward_batched(ctx, dmean, dL, dF):
         kernels.gemm_strided(r, q, q, T, nrows, Qp, G, q, q * q, dT[t], nrows, Qp, B,
                              alpha=-1.0, beta=1.0)                      # dT_b -= T_b G_b
     E = kernels.gemm(dT, Qb_s, transA=True)                             # M x N x np
-    dKbx = kernels.gemm(Linv_s, dT, transA=True, flags=_lib.GEMM_A_UPPER)  # M x r x N
+    # (s^2 L_rr^-T dT)^T = dT^T (s^2 L_rr^-1): already in post_backward's layout
+    dKbxT = kernels.gemm(dT, Linv_s, transA=True, flags=_lib.GEMM_B_LOWER)  # M x N x r
     dX = None
     for t, (cache, pp, ystd, T, W) in enumerate(ctx.saved):
         dX = kernels.post_backward(cache, pp, W, dmean[t], dcovs[t], ystd, E=E[t], dX=dX)
-        dX = kernels.post_backward(cache, pp, None, None, None, ystd, E=dKbx[t].mT.contiguous(),
+        dX = kernels.post_backward(cache, pp, None, None, None, ystd, E=dKbxT[t],
                                    Xt_scaled=roots[t].Xb_scaled, n=r, dX=dX)
     return dX
 
