@@ -76,6 +76,8 @@ _SIGNATURES = {
     "bo_ainv_work": (c_int, [c_int64, POINTER(c_int64)]),
     "bo_post_w_work": (c_int, [c_int, c_int, c_int64, POINTER(c_int), POINTER(c_int64)]),
     "bo_post_w_split": (c_int, [_P, c_int64, _P, c_int, c_int, c_int64, _P, _P, _P]),
+    "bo_post_w_members_work": (c_int, [c_int, c_int, c_int, c_int64, POINTER(c_int64)]),
+    "bo_post_w_split_members": (c_int, [c_int, _P, c_int64, _P, c_int, c_int, c_int64, _P, _P, _P]),
     "bo_post_w_dx_work": (c_int, [c_int, c_int, c_int64, POINTER(c_int64)]),
     "bo_post_w_dx": (c_int, [c_int, _P, c_int64, _P, c_int, c_int, c_int, c_int64, _P, _P, _P, _P,
                              _P, _P, c_double, c_double, _P, _P, _P]),

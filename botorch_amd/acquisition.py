@@ -1190,9 +1190,9 @@ class _FusedQNEHVI(torch.autograd.Function):
             Ts, F = _roots_forward_batched(acqf, caches, pps, stats)
             pp_list = list(pps)
             if need_grad:
+                Ws = kernels.w_matrix_members(caches, pps)
                 for t in range(M):
-                    saved.append((caches[t], pps[t], stats[t][1], Ts[t],
-                                  kernels.w_matrix(caches[t], pps[t])))
+                    saved.append((caches[t], pps[t], stats[t][1], Ts[t], Ws[t]))
         else:
             Ts, pp_list = [], []
             for t, mm in enumerate(models):

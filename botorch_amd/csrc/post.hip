@@ -1996,6 +1996,67 @@ int bo_post_w_split(const double* Linv, int64_t ldl, const double* Rt, int B, in
   return BO_OK;
 }
 
+// W^T = L^{-T} R^T of nm models of one shape in ONE stream-K launch (+ one
+// reduction launch): the members' (m, row tile) lanes share the slots as in
+// bo_post_partials_members.  *work_elems = the shared workspace in doubles, or
+// -1 where the one-model W plan is not stream-K (then one call per model).
+int bo_post_w_members_work(int nm, int B, int q, int64_t n, int64_t* work_elems) {
+  BO_CHECK_ARG(nm >= 1 && nm <= POST_MAXM, "bo_post_w_members_work: %d models (1..%d)", nm, POST_MAXM);
+  int kc = 0;
+  int64_t we = 0;
+  int s = bo_post_w_work(B, q, n, &kc, &we);
+  if (s) return s;
+  *work_elems = -1;
+  int Qp, nrows_pad, nC;
+  s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  if (kc != -1 || nrows_pad == 0) return BO_OK;
+  *work_elems = (int64_t)plan_chunks(nC, nrows_pad / PI, (int)n, -1, kSlots, PLAN_LOWER, nm) * PI * PC;
+  return BO_OK;
+}
+
+int bo_post_w_split_members(int nm, const double* const* Linv, int64_t ldl, const double* const* Rt,
+                            int B, int q, int64_t n, double* const* Wt, double* work, void* stream) {
+  BO_CHECK_ARG(nm >= 1 && nm <= POST_MAXM, "bo_post_w_split_members: %d models (1..%d)", nm, POST_MAXM);
+  BO_CHECK_ARG(Linv && Rt && Wt, "bo_post_w_split_members: null pointer");
+  BO_CHECK_ARG(ldl % 2 == 0 && ldl >= ceil_div(n, PC) * PC, "L^{-1} leading dim %lld too small",
+               (long long)ldl);
+  if (B == 0) return BO_OK;
+  int Qp, nrows_pad, nC;
+  int s = bo_post_geometry(B, q, n, &Qp, &nrows_pad, &nC);
+  if (s) return s;
+  const int nI = nrows_pad / PI;
+  if (nI == 0) return BO_OK;
+  int64_t we = 0;
+  s = bo_post_w_members_work(nm, B, q, n, &we);
+  if (s) return s;
+  BO_CHECK_ARG(we >= 0, "bo_post_w_split_members: the one-model W plan is not stream-K here");
+  BO_CHECK_ARG(we == 0 || work != nullptr, "bo_post_w_split_members: workspace of %lld doubles needed",
+               (long long)we);
+  PostMembers pm{};
+  pm.nm = nm;
+  for (int m = 0; m < nm; ++m) {
+    BO_CHECK_ARG(Linv[m] && Rt[m] && Wt[m], "bo_post_w_split_members: null buffer");
+    pm.U[m] = Linv[m];
+    pm.Kt[m] = Rt[m];
+    pm.Rt[m] = Wt[m];  // beta / Spart / mpart stay null, as in bo_post_w_split
+  }
+  DevPlan* plan = nullptr;
+  s = device_plan(nC, nI, (int)n, -1, &plan, PLAN_LOWER, nm);
+  if (s) return s;
+  hipStream_t st = as_stream(stream);
+  post_partials_kernel<BO_RBF, 1, true, false, true, true><<<(unsigned)plan->W, 256, 0, st>>>(
+      Rt[0], 0, Rt[0], (int)n, Linv[0], ldl, nullptr, 0.0, nC, nI, nullptr, nullptr, Wt[0], plan->segs,
+      plan->wg_off, work, nullptr, 0, 0, nullptr, Rt[0], 0, FusedDx{}, 0, pm);
+  BO_LAUNCH_CHECK();
+  if (plan->nred > 0) {
+    post_splitk_reduce_kernel<<<(unsigned)(plan->nred * (PI / 16)), 256, 0, st>>>(
+        work, plan->red, (int)n, nI, nullptr, nullptr, nullptr, Wt[0], pm);
+    BO_LAUNCH_CHECK();
+  }
+  return BO_OK;
+}
+
 // A^{-1} = L^{-T} L^{-1} (lower tiles: Ainv[r][c] for tile row >= tile column)
 // from L^{-1} (np x np, ld = np, identity pad): the posterior kernel's lower
 // k-range MFMA tiles with L^{-1} as both operands, under a stream-K plan (the

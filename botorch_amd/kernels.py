@@ -860,6 +860,36 @@ def w_matrix(cache: GPCache, pp: PostPartials, post_w: Optional[bool] = None) ->
     return WMat(W, False)
 
 
+# BO_W_MEMBERS=0: w_matrix per member in w_matrix_members (A/B)
+W_MEMBERS = os.environ.get("BO_W_MEMBERS", "1") != "0"
+
+
+def w_matrix_members(caches, pps) -> list:
+    """w_matrix of every member (a ModelListGP's, one shape): where the
+    one-model plan is stream-K, all members' W^T = L^{-T} R^T in ONE
+    member-batched launch + one reduction (bo_post_w_split_members), else
+    per member."""
+    nm = len(caches)
+    p0, c0 = pps[0], caches[0]
+    same = all(c.n == c0.n and c.np == c0.np for c in caches) and all(
+        p_.Rt is not None and p_.Rt.dim() == 2 and p_.Rt.is_contiguous() and p_.B == p0.B
+        and p_.q == p0.q for p_ in pps)
+    we = ctypes.c_int64(-1)
+    if W_MEMBERS and 1 < nm <= 8 and same:
+        check(lib().bo_post_w_members_work(nm, p0.B, p0.q, c0.n, ctypes.byref(we)), "post_w_members_work")
+    if we.value < 0:
+        return [w_matrix(c, p_) for c, p_ in zip(caches, pps)]
+    dev = p0.Rt.device
+    Wt = torch.empty(nm, c0.np, p0.nrows_pad, dtype=torch.float64, device=dev)
+    work = torch.empty(max(1, we.value), dtype=torch.float64, device=dev)
+    arr = lambda ts: (ctypes.c_void_p * nm)(*[_p(t).value for t in ts])  # noqa: E731
+    check(lib().bo_post_w_split_members(nm, arr([c.Linv for c in caches]), c0.np,
+                                        arr([p_.Rt for p_ in pps]), p0.B, p0.q, c0.n,
+                                        arr([Wt[m] for m in range(nm)]), _p(work), _stream(dev)),
+          "post_w_split_members")
+    return [WMat(Wt[m], True) for m in range(nm)]
+
+
 def post_w_dx(cache: GPCache, pp: PostPartials, dmean: torch.Tensor, dcov: torch.Tensor,
               ystd: float) -> Optional[torch.Tensor]:
     """dX of the posterior moments' cotangents with W = R L^{-1} reduced into

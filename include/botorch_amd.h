@@ -317,6 +317,13 @@ int bo_post_w(const double* Linv, int64_t ldl, const double* Rt, int B, int q, i
 int bo_post_w_work(int B, int q, int64_t n, int* kc_len, int64_t* work_elems);
 int bo_post_w_split(const double* Linv, int64_t ldl, const double* Rt, int B, int q, int64_t n,
                     double* Wt, double* work, void* stream);
+/* The same W^T of nm <= 8 models of one shape (a ModelListGP's members:
+ * Linv[m], Rt[m], Wt[m]) in one stream-K launch + one reduction.
+ * bo_post_w_members_work: the shared workspace in doubles, or -1 where the
+ * one-model plan is not stream-K (then bo_post_w_split per model). */
+int bo_post_w_members_work(int nm, int B, int q, int64_t n, int64_t* work_elems);
+int bo_post_w_split_members(int nm, const double* const* Linv, int64_t ldl, const double* const* Rt,
+                            int B, int q, int64_t n, double* const* Wt, double* work, void* stream);
 
 /* The posterior backward without W: dX (B x q x d) of the posterior moments'
  * cotangents (dmean B x q, dcov B x q x q, standardised by ystd as in

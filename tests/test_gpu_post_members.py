@@ -217,3 +217,27 @@ def test_qmc_finalize_members_bit_equal_to_per_member():
         assert float(status[m, 0]) == float(r["info"].max())
         assert float(status[m, 1]) == float(r["jitter"].max())
     assert float(jit.max()) > 0  # the repeated point did take the ladder
+
+
+@pytest.mark.parametrize("n,B,q", [(2048, 128, 8),    # C4
+                                   (1500, 40, 5)])    # ragged n, odd q
+def test_w_matrix_members_matches_per_member(n, B, q):
+    """bo_post_w_split_members (all members' W^T = L^{-T} R^T in one
+    stream-K launch) against w_matrix per member; the members' plan cuts the
+    k-sums at other positions (1e-12 relative, 1e-11 absolute)."""
+    from botorch_amd import kernels
+    from botorch_amd._lib import check, lib
+    _, _, models = _models(n)
+    nm = len(models)
+    we = ctypes.c_int64()
+    check(lib().bo_post_w_members_work(nm, B, q, n, ctypes.byref(we)), "post_w_members_work")
+    if we.value < 0:
+        pytest.skip("one-model W plan not stream-K at this shape")
+    caches = [mm.prediction_cache() for mm in models]
+    X = torch.rand(B, q, 6, dtype=torch.float64, generator=torch.Generator().manual_seed(9)).to(DEV)
+    pps = [kernels.post_partials(c, X, store_R=True, small=False) for c in caches]
+    Ws = kernels.w_matrix_members(caches, pps)
+    for c, pp, W in zip(caches, pps, Ws):
+        ref = kernels.w_matrix(c, pp)
+        assert W.kmajor == ref.kmajor and W.t.shape == ref.t.shape
+        torch.testing.assert_close(W.t, ref.t, rtol=1e-12, atol=1e-11)
