@@ -990,8 +990,9 @@ class _FusedQEHVI(torch.autograd.Function):
                                            L_out=L[t], status=words[t])
                 status.append((out["info"], out["jitter"]))
         if need_grad:
+            Ws = kernels.w_matrix_members(caches, pps)   # one launch where stream-K
             for t, (cache, pp) in enumerate(zip(caches, pps)):
-                saved.append((cache, pp, stats[t][1], kernels.w_matrix(cache, pp)))
+                saved.append((cache, pp, stats[t][1], Ws[t]))
         sampler = acqf._ensure_sampler()
         Z = sampler.base_samples_2d(q * len(models), X3.device)
         lo, hi = acqf._cells(X3.device)
