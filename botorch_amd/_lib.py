@@ -240,6 +240,7 @@ for _name, _cls in (("bo_post_partials_v", PostPartialsArgs), ("bo_qmc_finalize_
                     ("bo_lbfgs_step_v", LbfgsStepArgs), ("bo_lbfgsb_step_v", LbfgsbArgs)):
     _SIGNATURES[_name] = (c_int, [POINTER(_cls), _P])
 _SIGNATURES["bo_struct_size"] = (c_int64, [ctypes.c_char_p])
+_SIGNATURES["bo_post_backward_jobs"] = (c_int, [c_int, POINTER(POINTER(PostBackwardArgs)), _P, _P])
 ARG_RECORDS = {"BoPostPartialsArgs": PostPartialsArgs, "BoQmcFinalizeArgs": QmcFinalizeArgs,
                "BoQmcBackwardArgs": QmcBackwardArgs, "BoPostBackwardArgs": PostBackwardArgs,
                "BoQehviArgs": QehviArgs, "BoLbfgsStepArgs": LbfgsStepArgs,

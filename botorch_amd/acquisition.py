@@ -1256,6 +1256,8 @@ class _FusedQNEHVI(torch.autograd.Function):
 
 # BO_QNEHVI_BWD_BATCHED=0: the per-member backward on the batched forward (A/B)
 _BWD_BATCHED = os.environ.get("BO_QNEHVI_BWD_BATCHED", "1") != "0"
+# BO_PB_JOBS=0: the members' post_backward passes one launch each (A/B)
+_PB_JOBS = os.environ.get("BO_PB_JOBS", "1") != "0"
 
 
 def _roots_backward_batched(ctx, dmean, dL, dF):
@@ -1287,6 +1289,15 @@ def _roots_backward_batched(ctx, dmean, dL, dF):
     E = kernels.gemm(dT, Qb_s, transA=True)                             # M x N x np
     # (s^2 L_rr^-T dT)^T = dT^T (s^2 L_rr^-1): already in post_backward's layout
     dKbxT = kernels.gemm(dT, Linv_s, transA=True, flags=_lib.GEMM_B_LOWER)  # M x N x r
+    if _PB_JOBS and 2 * M <= 16:
+        # every member's training and baseline passes in one launch
+        jobs = []
+        for t, (cache, pp, ystd, T, W) in enumerate(ctx.saved):
+            jobs.append(dict(cache=cache, pp=pp, W=W, dmean=dmean[t], dcov=dcovs[t], ystd=ystd,
+                             E=E[t]))
+            jobs.append(dict(cache=cache, pp=pp, ystd=ystd, E=dKbxT[t],
+                             Xt_scaled=roots[t].Xb_scaled, n=r))
+        return kernels.post_backward_jobs(jobs)
     dX = None
     for t, (cache, pp, ystd, T, W) in enumerate(ctx.saved):
         dX = kernels.post_backward(cache, pp, W, dmean[t], dcovs[t], ystd, E=E[t], dX=dX)

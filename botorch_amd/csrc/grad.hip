@@ -345,8 +345,8 @@ static_assert(THREADS == QMAX * QMAX, "post_backward: one G entry per thread");
 // the lane evaluates dk/dx for its 4 (row, point) pairs.  The waves stride over
 // the 16-point blocks; per-row sums are combined by shuffles and LDS.
 template <int KIND, int ND>
-__global__ __launch_bounds__(THREADS) void post_backward_kernel(
-    int q, int Qp, const double* __restrict__ Xq, const double* __restrict__ Xt, int n,
+__device__ __forceinline__ void post_backward_body(
+    int b, int q, int Qp, const double* __restrict__ Xq, const double* __restrict__ Xt, int n,
     const double* __restrict__ W, int64_t ldw, const double* __restrict__ alpha,
     const double* __restrict__ dmean, const double* __restrict__ dcov,
     const double* __restrict__ E, int64_t lde,
@@ -357,7 +357,6 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
   __shared__ double xs[QMAX][DP];
   __shared__ double red[THREADS / 64][QMAX][DP + 1];
 
-  const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int row0 = b * Qp;
   const double s2 = ystd * ystd;
@@ -465,6 +464,42 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
     double* o = dX + ((int64_t)b * q + a) * d + t;
     *o = accumulate ? *o + s / ls[t] : s / ls[t];
   }
+}
+
+template <int KIND, int ND>
+__global__ __launch_bounds__(THREADS) void post_backward_kernel(
+    int q, int Qp, const double* __restrict__ Xq, const double* __restrict__ Xt, int n,
+    const double* __restrict__ W, int64_t ldw, const double* __restrict__ alpha,
+    const double* __restrict__ dmean, const double* __restrict__ dcov,
+    const double* __restrict__ E, int64_t lde,
+    const double* __restrict__ ls, double outputscale, double ystd, int d, int accumulate,
+    double* __restrict__ dX, int wkm) {
+  post_backward_body<KIND, ND>(blockIdx.x, q, Qp, Xq, Xt, n, W, ldw, alpha, dmean, dcov, E, lde, ls,
+                               outputscale, ystd, d, accumulate, dX, wkm);
+}
+
+// Several posterior backward passes of one (B, q, d, kind) in ONE launch
+// (bo_post_backward_jobs: a ModelListGP's members, each with its training and
+// baseline passes): grid (B, jobs), job j's dX written to its own slice (no
+// accumulation across workgroups; the caller sums the slices).  One pass
+// alone is B = 128 workgroups on 256 CUs.
+constexpr int PB_MAXJ = 16;
+struct PBJob {
+  const double *Xq, *Xt, *W, *alpha, *dmean, *dcov, *E, *ls;
+  double* dX;
+  int64_t ldw, lde;
+  double outputscale, ystd;
+  int n, wkm;
+};
+struct PBJobs {
+  PBJob j[PB_MAXJ];
+};
+
+template <int KIND, int ND>
+__global__ __launch_bounds__(THREADS) void post_backward_jobs_kernel(int q, int Qp, int d, PBJobs jb) {
+  const PBJob& J = jb.j[blockIdx.y];
+  post_backward_body<KIND, ND>(blockIdx.x, q, Qp, J.Xq, J.Xt, J.n, J.W, J.ldw, J.alpha, J.dmean,
+                               J.dcov, J.E, J.lde, J.ls, J.outputscale, J.ystd, d, 0, J.dX, J.wkm);
 }
 
 // Generic-d kernel-matrix gradient: dX[i][t] (+)= sum_k dK[i][k] d k(x_i, y_k) / d x_it
@@ -609,6 +644,40 @@ extern "C" int bo_post_backward(int kind, int B, int q, int d, const double* Xq,
     if (d == 6) BO_PB(BO_MATERN52, 6); else BO_PB(BO_MATERN52, 8);
   }
 #undef BO_PB
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
+
+extern "C" int bo_post_backward_jobs(int njobs, const BoPostBackwardArgs* const* jobs, double* dX_parts,
+                                     void* stream) {
+  BO_CHECK_ARG(njobs >= 1 && njobs <= PB_MAXJ, "bo_post_backward_jobs: %d jobs (1..%d)", njobs, PB_MAXJ);
+  BO_CHECK_ARG(jobs && dX_parts, "bo_post_backward_jobs: null pointer");
+  const BoPostBackwardArgs* a0 = jobs[0];
+  BO_CHECK_ARG(a0 && a0->q >= 1 && a0->q <= QMAX && a0->d >= 1 && a0->d <= DP, "bo_post_backward_jobs: bad q/d");
+  const int B = a0->B, q = a0->q, d = a0->d, kind = a0->kind;
+  PBJobs jb{};
+  for (int j = 0; j < njobs; ++j) {
+    const BoPostBackwardArgs* a = jobs[j];
+    BO_CHECK_ARG(a && a->B == B && a->q == q && a->d == d && a->kind == kind,
+                 "bo_post_backward_jobs: job %d differs in B/q/d/kind", j);
+    BO_CHECK_ARG(a->Xq && a->Xt_scaled && a->lengthscale && a->n >= 0,
+                 "bo_post_backward_jobs: job %d lacks inputs", j);
+    jb.j[j] = PBJob{a->Xq, a->Xt_scaled, a->W, a->alpha, a->dmean, a->dcov, a->E, a->lengthscale,
+                    dX_parts + (int64_t)j * B * q * d, a->ldw, a->lde, a->outputscale, a->ystd,
+                    (int)a->n, a->w_kmajor};
+  }
+  if (B == 0) return BO_OK;
+  int Qp = 1;
+  while (Qp < q) Qp *= 2;
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((unsigned)B, (unsigned)njobs);
+#define BO_PBJ(KIND, ND) post_backward_jobs_kernel<KIND, ND><<<grid, THREADS, 0, st>>>(q, Qp, d, jb)
+  if (kind == BO_RBF) {
+    if (d == 6) BO_PBJ(BO_RBF, 6); else BO_PBJ(BO_RBF, 8);
+  } else {
+    if (d == 6) BO_PBJ(BO_MATERN52, 6); else BO_PBJ(BO_MATERN52, 8);
+  }
+#undef BO_PBJ
   BO_LAUNCH_CHECK();
   return BO_OK;
 }

@@ -973,6 +973,40 @@ def post_backward(cache: GPCache, pp: PostPartials, W: Optional[WMat],
     return dX
 
 
+def post_backward_jobs(jobs: list) -> torch.Tensor:
+    """Several post_backward passes of one (B, q, d, kind) -- each job a dict
+    of post_backward's arguments (cache, pp, W, dmean, dcov, ystd, E,
+    Xt_scaled, n) -- in ONE launch (bo_post_backward_jobs, grid B x jobs),
+    every job's dX into its own slice; returns their sum (B x q x d)."""
+    nj = len(jobs)
+    c0, p0 = jobs[0]["cache"], jobs[0]["pp"]
+    dev = p0.Xq.device
+    parts = torch.empty(nj, p0.B, p0.q, c0.d, dtype=torch.float64, device=dev)
+    recs, keep = [], []
+    cont = lambda t: t.contiguous() if t is not None else None  # noqa: E731
+    for j in jobs:
+        cache, pp = j["cache"], j["pp"]
+        W = j.get("W")
+        if isinstance(W, torch.Tensor):
+            W = WMat(W, False)
+        kmajor = W is not None and W.kmajor
+        Wt = cont(W.t) if W is not None else None
+        E, dmean, dcov = cont(j.get("E")), cont(j.get("dmean")), cont(j.get("dcov"))
+        other = j.get("Xt_scaled") is not None
+        keep += [Wt, E, dmean, dcov]
+        recs.append(_lib.PostBackwardArgs(
+            kind=cache.kind, B=pp.B, q=pp.q, d=cache.d, Xq=pp.Xq,
+            Xt_scaled=j["Xt_scaled"] if other else cache.Xt_scaled,
+            n=j["n"] if other else cache.n, W=Wt, ldw=Wt.shape[1] if Wt is not None else 0,
+            alpha=None if other else cache.alpha, dmean=dmean, dcov=dcov, E=E,
+            lde=E.shape[1] if E is not None else 0, lengthscale=cache.lengthscale,
+            outputscale=cache.outputscale, ystd=float(j["ystd"]), accumulate=0,
+            w_kmajor=int(kmajor), dX=parts))
+    arr = (ctypes.POINTER(_lib.PostBackwardArgs) * nj)(*[ctypes.pointer(r) for r in recs])
+    check(lib().bo_post_backward_jobs(nj, arr, _p(parts), _stream(dev)), "post_backward_jobs")
+    return parts.sum(0)
+
+
 # Deferred ladder status (forward-only fused acquisitions): the status of call t
 # is copied to pinned host memory behind an event and checked at call t + 1, at
 # the driver's own synchronisation points (gen_candidates_scipy's loss.item(),

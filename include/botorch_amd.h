@@ -749,6 +749,12 @@ typedef struct BoPostBackwardArgs { /* bo_post_backward */
   double* dX;
 } BoPostBackwardArgs;
 int bo_post_backward_v(const BoPostBackwardArgs* a, void* stream);
+/* njobs <= 16 posterior backward passes of one (B, q, d, kind) in one launch
+ * (a ModelListGP's members, each with its training and baseline passes):
+ * job j's dX (its dX / accumulate fields ignored) is written to dX_parts + j B q d;
+ * the caller sums the slices. */
+int bo_post_backward_jobs(int njobs, const BoPostBackwardArgs* const* jobs, double* dX_parts,
+                          void* stream);
 
 typedef struct BoQehviArgs { /* bo_qehvi and bo_qehvi_backward (d* fields: backward only) */
   BO_STRUCT_HEADER;

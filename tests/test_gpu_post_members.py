@@ -241,3 +241,34 @@ def test_w_matrix_members_matches_per_member(n, B, q):
         ref = kernels.w_matrix(c, pp)
         assert W.kmajor == ref.kmajor and W.t.shape == ref.t.shape
         torch.testing.assert_close(W.t, ref.t, rtol=1e-12, atol=1e-11)
+
+
+def test_post_backward_jobs_matches_sequential_passes():
+    """bo_post_backward_jobs (the members' training + baseline passes in one
+    launch, per-job dX slices summed) against post_backward accumulated pass by
+    pass (the same per-pass sums, added in another order: 1e-12)."""
+    from botorch_amd import kernels
+    n, B, q, r = 1500, 40, 5, 37
+    _, _, models = _models(n)
+    caches = [mm.prediction_cache() for mm in models]
+    g = torch.Generator().manual_seed(11)
+    X = torch.rand(B, q, 6, dtype=torch.float64, generator=g).to(DEV)
+    jobs = []
+    for c in caches:
+        pp = kernels.post_partials(c, X, store_R=True, small=False)
+        W = kernels.w_matrix(c, pp)
+        dmean = torch.randn(B, q, dtype=torch.float64, generator=g).to(DEV)
+        dcov = torch.randn(B, q, q, dtype=torch.float64, generator=g).to(DEV)
+        E = torch.randn(pp.nrows_pad, c.np, dtype=torch.float64, generator=g).to(DEV)
+        Xb = torch.zeros(r, kernels.DP, dtype=torch.float64)
+        Xb[:, :6] = torch.rand(r, 6, dtype=torch.float64, generator=g)
+        Eb = torch.randn(pp.nrows_pad, r, dtype=torch.float64, generator=g).to(DEV)
+        jobs.append(dict(cache=c, pp=pp, W=W, dmean=dmean, dcov=dcov, ystd=0.7, E=E))
+        jobs.append(dict(cache=c, pp=pp, ystd=0.7, E=Eb, Xt_scaled=Xb.to(DEV), n=r))
+    got = kernels.post_backward_jobs(jobs)
+    ref = None
+    for j in jobs:
+        ref = kernels.post_backward(j["cache"], j["pp"], j.get("W"), j.get("dmean"), j.get("dcov"),
+                                    j["ystd"], E=j["E"], Xt_scaled=j.get("Xt_scaled"), n=j.get("n"),
+                                    dX=ref)
+    torch.testing.assert_close(got, ref, rtol=1e-12, atol=1e-12)
