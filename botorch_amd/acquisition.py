@@ -1015,7 +1015,15 @@ class _FusedQEHVI(torch.autograd.Function):
         lo, hi = ctx.cells
         dmean, dL = kernels.qehvi_backward(ctx.mean, ctx.L, ctx.Z, lo, hi, dacq)
         dX = None
-        for t, (cache, pp, ystd, W) in enumerate(ctx.saved):
+        sv = ctx.saved
+        if (_PB_JOBS and 1 < len(sv) <= 16 and all(
+                c.kind == sv[0][0].kind and c.d == sv[0][0].d for c, _, _, _ in sv)):
+            # every member's posterior backward pass in one launch
+            return kernels.post_backward_jobs([
+                dict(cache=cache, pp=pp, W=W, dmean=dmean[t], ystd=ystd,
+                     dcov=kernels.chol_backward(ctx.L[t], dL[t]))
+                for t, (cache, pp, ystd, W) in enumerate(sv)]), None
+        for t, (cache, pp, ystd, W) in enumerate(sv):
             dcov = kernels.chol_backward(ctx.L[t], dL[t])
             dX = kernels.post_backward(cache, pp, W, dmean[t], dcov, ystd, dX=dX)
         return dX, None
