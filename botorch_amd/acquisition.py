@@ -1018,10 +1018,12 @@ class _FusedQEHVI(torch.autograd.Function):
         sv = ctx.saved
         if (_PB_JOBS and 1 < len(sv) <= 16 and all(
                 c.kind == sv[0][0].kind and c.d == sv[0][0].d for c, _, _, _ in sv)):
-            # every member's posterior backward pass in one launch
+            # every member's Cholesky backward, then posterior backward pass, in one launch each
+            q_ = ctx.L.shape[-1]
+            dcovs = kernels.chol_backward(ctx.L.reshape(-1, q_, q_),
+                                          dL.reshape(-1, q_, q_)).reshape(ctx.L.shape)
             return kernels.post_backward_jobs([
-                dict(cache=cache, pp=pp, W=W, dmean=dmean[t], ystd=ystd,
-                     dcov=kernels.chol_backward(ctx.L[t], dL[t]))
+                dict(cache=cache, pp=pp, W=W, dmean=dmean[t], ystd=ystd, dcov=dcovs[t])
                 for t, (cache, pp, ystd, W) in enumerate(sv)]), None
         for t, (cache, pp, ystd, W) in enumerate(sv):
             dcov = kernels.chol_backward(ctx.L[t], dL[t])
@@ -1286,10 +1288,11 @@ def _roots_backward_batched(ctx, dmean, dL, dF):
     Qb_s = Qb_s[1]
     dT = kernels.gemm(Zb, dF.contiguous(), transA=True)                 # M x r x N
     r = dT.shape[1]
-    dcovs = []
+    q_ = ctx.L.shape[-1]
+    dcovs = kernels.chol_backward(ctx.L.reshape(-1, q_, q_), dL.reshape(-1, q_, q_)).reshape(
+        ctx.L.shape)                                                    # all members, one launch
     for t, (cache, pp, ystd, T, W) in enumerate(ctx.saved):
-        dcov = kernels.chol_backward(ctx.L[t], dL[t])
-        dcovs.append(dcov)
+        dcov = dcovs[t]
         G = (dcov + dcov.mT).contiguous()
         q, Qp, nrows, B = pp.q, pp.Qp, pp.nrows_pad, pp.B
         kernels.gemm_strided(r, q, q, T, nrows, Qp, G, q, q * q, dT[t], nrows, Qp, B,
