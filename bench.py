@@ -210,15 +210,27 @@ def cpu_baseline(Xtr, Ytr, Xc, best_f, budget_s=20.0):
     }
 
 
-def _gpu_time(fn, steps=5, warmup=1):
+def _gpu_time(fn, steps=5, warmup=2, reps=3):
+    """Seconds per call of ``fn``: HIP events on torch's current stream (the
+    stream every op here launches on) around ``steps`` back-to-back calls,
+    after ``warmup`` untimed calls; the median of ``reps`` such runs.  A call
+    that waits on the host in between still shows as idle device time between
+    the events, so host-bound calls are timed as they run."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        fn()
-    torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / steps
+    ts = []
+    for _ in range(reps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(steps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e-3 / steps)
+    ts.sort()
+    return ts[len(ts) // 2]
 
 
 def _cpu_time(fn, budget_s=4.0, max_runs=5):
@@ -231,6 +243,63 @@ def _cpu_time(fn, budget_s=4.0, max_runs=5):
         times.append(time.perf_counter() - t0)
     times.sort()
     return times[len(times) // 2], len(times)
+
+
+def _check_qnehvi(acqf, Xd, X, Y, models, ref_point, S, k=4):
+    """Outside the timed region: the timed qNEHVI forward (and dX) at k spread
+    t-batches against the CPU restatement (oracle.QNEHVIOracle, the checker) on
+    the same pruned baseline and per-sample cells -- values by the per-sample
+    cell inclusion-exclusion (rtol 1e-7) and by exact hypervolume differences
+    on two of them (north_star's 1e-2), dX by autograd through the oracle
+    (rtol 1e-5).  Where the timed Sobol t-batches improve on too few samples,
+    t-batches scattered around the Pareto set are checked as well."""
+    from oracle.acquisition import QNEHVIOracle
+    from oracle.gp import ExactGPOracle, GPHyper
+    f64 = torch.float64
+    orcs = [ExactGPOracle(X, Y[:, t:t + 1], GPHyper(torch.full((6,), 0.6, dtype=f64), 1e-3, 0.0))
+            for t in range(Y.shape[-1])]
+    orc = QNEHVIOracle(orcs, acqf.X_baseline.cpu(), ref_point.tolist(), S, seed=0)
+    base_err = float((acqf.baseline_samples - orc.Y_base).abs().max())
+    lo, hi = acqf.cell_lower_bounds.cpu(), acqf.cell_upper_bounds.cpu()
+    g = torch.Generator().manual_seed(4)
+    from botorch_amd.multi_objective import is_non_dominated
+    P = X[is_non_dominated(Y)]
+    b, q = Xd.shape[0], Xd.shape[1]
+    pick = torch.randint(0, P.shape[0], (b, q), generator=g)
+    Xn = (P[pick] + 0.05 * torch.randn(b, q, X.shape[-1], generator=g, dtype=f64)).clamp(0, 1)
+    res = {"baseline_samples_max_abs_err": base_err, "rtol_cells": 1e-7, "rtol_exact": 1e-2,
+           "rtol_grad": 1e-5}
+    worst_v, worst_g, worst_x, checked = 0.0, 0.0, 0.0, []
+    for tag, Xs in (("timed", Xd.detach().cpu()), ("near_pareto", Xn)):
+        Xg = Xs.to(Xd.device).requires_grad_(True)
+        v = acqf(Xg)
+        (gd,) = torch.autograd.grad(v.sum(), Xg)
+        v, gd = v.detach().cpu(), gd.cpu()
+        nz = (v != 0).nonzero().flatten()
+        res[f"{tag}_nonzero"] = int(nz.numel())
+        if nz.numel() < k:
+            continue
+        idx = nz[torch.linspace(0, nz.numel() - 1, k).round().long()]
+        for i in idx.tolist():
+            Xo = Xs[i:i + 1].clone().requires_grad_(True)
+            rv = orc.value_cells(Xo, lo, hi)
+            (go,) = torch.autograd.grad(rv.sum(), Xo)
+            worst_v = max(worst_v, float(((v[i] - rv.detach()[0]).abs() / rv.detach().abs()[0])))
+            worst_g = max(worst_g, float(((gd[i] - go[0]).abs() / go[0].abs().clamp_min(1e-8)).max()))
+            ok = torch.allclose(v[i:i + 1], rv.detach(), rtol=1e-7, atol=1e-10) and \
+                torch.allclose(gd[i:i + 1], go, rtol=1e-5, atol=1e-8)
+            if not ok:
+                raise SystemExit(f"bench: C4 qNEHVI disagrees with the oracle at t-batch {i} ({tag})")
+        ex = orc.value_exact(Xs[idx[:2]])
+        worst_x = max(worst_x, float(((v[idx[:2]] - ex).abs() / ex.abs()).max()))
+        if not torch.allclose(v[idx[:2]], ex, rtol=1e-2, atol=1e-6):
+            raise SystemExit(f"bench: C4 qNEHVI disagrees with the exact hypervolumes ({tag})")
+        checked += [f"{tag}:{i}" for i in idx.tolist()]
+    if not checked:
+        raise SystemExit("bench: C4 qNEHVI check degenerate (no non-zero values)")
+    res.update(t_batches=checked, max_rel_err_cells=worst_v, max_rel_err_grad=worst_g,
+               max_rel_err_exact_hv=worst_x)
+    return res
 
 
 def other_configs(dev, cpu=True):
@@ -526,6 +595,8 @@ def other_configs(dev, cpu=True):
                         "cells_per_sample_max": int(acqf.cell_lower_bounds.shape[1]),
                         "init_ms": init_ms, "gpu_evals_per_s": q * S * b / t, "gpu_ms": 1e3 * t,
                         "fwd_bwd_ms": 1e3 * tfb}
+    if cpu:
+        out["C4_qNEHVI"]["check"] = _check_qnehvi(acqf, Xd, X, Y, models, ref_point, S)
 
     # C5: SAAS (M=16 prior draws), d=50, n=256, qEI q=4, S=256, b=64
     d, n, M, q, S, b = 50, 256, 16, 4, 256, 64

@@ -1341,7 +1341,10 @@ def _roots_forward_batched(acqf, caches, pps, stats):
     M = len(roots)
     p0 = pps[0]
     dev = p0.Xq.device
-    key = (tuple(float(s_[1]) for s_ in stats), str(dev))
+    # keyed by the roots too (their identity and baseline size), not only by
+    # the outcome scales: _set_cell_bounds rebuilds the roots
+    key = (tuple(float(s_[1]) for s_ in stats), str(dev),
+           tuple((id(rt), rt.Linv.data_ptr(), rt.Linv.shape[0]) for rt in roots))
     stk = acqf.__dict__.get("_root_stack")
     if stk is None or stk[0] != key:
         s2 = [float(s_[1]) ** 2 for s_ in stats]
@@ -1506,6 +1509,11 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
         Zb = kernels.sobol_normal(r * m, S, sampler.seed, Xb.device).view(S, r, m)
         self._roots = [_CachedBaselineRoot(mm, Xb, Zb[:, :, t].contiguous())
                        for t, mm in enumerate(models)]
+        # the members' stacked root operands (_roots_forward_batched /
+        # _roots_backward_batched) belong to the previous roots: a baseline
+        # that grew by pending points has a different r
+        self.__dict__.pop("_root_stack", None)
+        self.__dict__.pop("_root_stack_qb", None)
         if not all(rt.fused_ready for rt in self._roots):
             raise UnsupportedError(f"qNEHVI here needs d <= {kernels.DP}")
         Y = torch.stack([rt.samples for rt in self._roots], dim=-1).cpu()  # S x r x m

@@ -345,6 +345,76 @@ def sample_points_around_best(acq_function, n_discrete_points, sigma, bounds, be
 SOBOL_MAXDIM = 21201  # torch.quasirandom.SobolEngine.MAXDIM
 
 
+def check_init_inputs(bounds, options, equality_constraints=None, generator=None) -> None:
+    """The argument checks of gen_batch_initial_conditions (initializers.py:
+    305-330)."""
+    from .exceptions import UnsupportedError
+    if bounds.isinf().any():
+        raise NotImplementedError("Currently only finite values in `bounds` are supported for "
+                                  "generating initial conditions for optimization.")
+    sample_around_best = (options or {}).get("sample_around_best", False)
+    if sample_around_best and equality_constraints:
+        raise UnsupportedError("Option 'sample_around_best' is not supported when equality"
+                               "constraints are present.")
+    if sample_around_best and generator:
+        raise UnsupportedError("Option 'sample_around_best' is not supported when custom "
+                               "generator is be used.")
+
+
+def raw_designs_use_global_rng(options, seed, generator=None, constrained=False) -> bool:
+    """Whether raw_designs may draw from the global torch generator (so that
+    replicas of it on several ranks could differ): points around the
+    incumbents, a caller's generator, an unseeded draw, or the polytope chain
+    (its d = 1 directions are random signs from the global generator)."""
+    return bool((options or {}).get("sample_around_best", False)) or generator is not None \
+        or seed is None or bool(constrained)
+
+
+def raw_designs(acq_function, bounds, q, n, seed, options, fixed_features=None,
+                inequality_constraints=None, equality_constraints=None, generator=None,
+                fixed_X_fantasies=None) -> torch.Tensor:
+    """The n raw q-batch designs of one round of gen_batch_initial_conditions
+    (initializers.py:350-410): ``generator(n, q, seed)``, or polytope q-batches
+    under linear constraints, or the Sobol draw (uniform past
+    SobolEngine.MAXDIM); joined by points around the incumbents
+    (``sample_around_best``), features fixed, ``fixed_X_fantasies`` appended."""
+    options = options or {}
+    d = bounds.shape[-1]
+    if generator is not None:
+        X_rnd = generator(n, q, seed)
+    elif inequality_constraints or equality_constraints:
+        from .constraints import sample_q_batches_from_polytope
+        X_rnd = sample_q_batches_from_polytope(
+            n=n, q=q, bounds=bounds, n_burnin=options.get("n_burnin", 10000),
+            n_thinning=options.get("n_thinning", 32), seed=seed,
+            equality_constraints=equality_constraints,
+            inequality_constraints=inequality_constraints)
+    elif d * q <= SOBOL_MAXDIM:
+        X_rnd = draw_raw_samples(bounds, n, q, seed)
+    else:
+        b_cpu = bounds.cpu()
+        with manual_seed(seed):
+            u = torch.rand(n, q, d, dtype=bounds.dtype)
+        X_rnd = b_cpu[0] + (b_cpu[1] - b_cpu[0]) * u
+    if options.get("sample_around_best", False):
+        X_best = sample_points_around_best(
+            acq_function, n_discrete_points=n * q,
+            sigma=options.get("sample_around_best_sigma", 1e-3), bounds=bounds,
+            subset_sigma=options.get("sample_around_best_subset_sigma", 1e-1),
+            prob_perturb=options.get("sample_around_best_prob_perturb"))
+        if X_best is not None:
+            X_rnd = torch.cat([X_rnd, X_best.view(n, q, d).to(X_rnd)], dim=0)
+    X_rnd = fix_features(X_rnd, fixed_features)
+    if fixed_X_fantasies is not None:
+        if fixed_X_fantasies.shape[-1] != X_rnd.shape[-1]:
+            raise ValueError("`fixed_X_fantasies` and `bounds` must both have the same "
+                             f"trailing dimension `d`, but have {fixed_X_fantasies.shape[-1]} "
+                             f"and {X_rnd.shape[-1]}, respectively.")
+        fx = fixed_X_fantasies.to(X_rnd)
+        X_rnd = torch.cat([X_rnd, fx.unsqueeze(0).expand(X_rnd.shape[0], *fx.shape)], dim=-2)
+    return X_rnd
+
+
 def gen_batch_initial_conditions(acq_function, bounds, q, num_restarts, raw_samples,
                                  fixed_features=None, options=None, inequality_constraints=None,
                                  equality_constraints=None, generator=None, fixed_X_fantasies=None):
@@ -362,56 +432,16 @@ def gen_batch_initial_conditions(acq_function, bounds, q, num_restarts, raw_samp
     designs are q-batches of the hit-and-run chain over the feasible polytope
     (constraints.sample_q_batches_from_polytope, initializers.py:365-375; the
     chain's steps in native host code), evaluated on the device the same way."""
-    from .exceptions import UnsupportedError
-    if bounds.isinf().any():
-        raise NotImplementedError("Currently only finite values in `bounds` are supported for "
-                                  "generating initial conditions for optimization.")
     options = options or {}
-    sample_around_best = options.get("sample_around_best", False)
-    if sample_around_best and equality_constraints:
-        raise UnsupportedError("Option 'sample_around_best' is not supported when equality"
-                               "constraints are present.")
-    if sample_around_best and generator:
-        raise UnsupportedError("Option 'sample_around_best' is not supported when custom "
-                               "generator is be used.")
+    check_init_inputs(bounds, options, equality_constraints, generator)
     seed, batch_limit, init_func, init_kwargs = init_options(acq_function, bounds, options)
     q = 1 if q is None else q
-    d = bounds.shape[-1]
     factor, max_factor = 1, 5
     while factor < max_factor:
         n = raw_samples * factor
-        if generator is not None:
-            X_rnd = generator(n, q, seed)
-        elif inequality_constraints or equality_constraints:
-            from .constraints import sample_q_batches_from_polytope
-            X_rnd = sample_q_batches_from_polytope(
-                n=n, q=q, bounds=bounds, n_burnin=options.get("n_burnin", 10000),
-                n_thinning=options.get("n_thinning", 32), seed=seed,
-                equality_constraints=equality_constraints,
-                inequality_constraints=inequality_constraints)
-        elif d * q <= SOBOL_MAXDIM:
-            X_rnd = draw_raw_samples(bounds, n, q, seed)
-        else:
-            b_cpu = bounds.cpu()
-            with manual_seed(seed):
-                u = torch.rand(n, q, d, dtype=bounds.dtype)
-            X_rnd = b_cpu[0] + (b_cpu[1] - b_cpu[0]) * u
-        if sample_around_best:
-            X_best = sample_points_around_best(
-                acq_function, n_discrete_points=n * q,
-                sigma=options.get("sample_around_best_sigma", 1e-3), bounds=bounds,
-                subset_sigma=options.get("sample_around_best_subset_sigma", 1e-1),
-                prob_perturb=options.get("sample_around_best_prob_perturb"))
-            if X_best is not None:
-                X_rnd = torch.cat([X_rnd, X_best.view(n, q, d).to(X_rnd)], dim=0)
-        X_rnd = fix_features(X_rnd, fixed_features)
-        if fixed_X_fantasies is not None:
-            if fixed_X_fantasies.shape[-1] != X_rnd.shape[-1]:
-                raise ValueError("`fixed_X_fantasies` and `bounds` must both have the same "
-                                 f"trailing dimension `d`, but have {fixed_X_fantasies.shape[-1]} "
-                                 f"and {X_rnd.shape[-1]}, respectively.")
-            fx = fixed_X_fantasies.to(X_rnd)
-            X_rnd = torch.cat([X_rnd, fx.unsqueeze(0).expand(X_rnd.shape[0], *fx.shape)], dim=-2)
+        X_rnd = raw_designs(acq_function, bounds, q, n, seed, options, fixed_features,
+                            inequality_constraints, equality_constraints, generator,
+                            fixed_X_fantasies)
         Y_rnd = evaluate_raw_samples(acq_function, X_rnd.to(bounds.device), batch_limit)
         idx, warned = select_initial_indices(init_func, Y_rnd, num_restarts, init_kwargs)
         ics = X_rnd[idx.to(X_rnd.device)].to(device=bounds.device)
@@ -1051,6 +1081,26 @@ def optimize_acqf(acq_function, bounds, q, num_restarts, raw_samples=None, optio
     constraints raise UnsupportedError (out of scope); every other argument has
     the reference's meaning.  ``return_full_tree`` only matters for one-shot
     acquisitions, which are not on this path."""
+    return optimize_acqf_driver(
+        _optimize_acqf_batch, acq_function, bounds, q, num_restarts, raw_samples, options,
+        inequality_constraints, equality_constraints, nonlinear_inequality_constraints,
+        fixed_features, post_processing_func, batch_initial_conditions, return_best_only,
+        gen_candidates, sequential, ic_generator=ic_generator, timeout_sec=timeout_sec,
+        return_full_tree=return_full_tree,
+        retry_on_optimization_warning=retry_on_optimization_warning, **ic_gen_kwargs)
+
+
+def optimize_acqf_driver(batch_fn, acq_function, bounds, q, num_restarts, raw_samples=None,
+                         options=None, inequality_constraints=None, equality_constraints=None,
+                         nonlinear_inequality_constraints=None, fixed_features=None,
+                         post_processing_func=None, batch_initial_conditions=None,
+                         return_best_only=True, gen_candidates=None, sequential=False, *,
+                         ic_generator=None, timeout_sec=None, return_full_tree=False,
+                         retry_on_optimization_warning=True, **ic_gen_kwargs):
+    """optimize_acqf's control flow (optimize.py:397-564) around the joint
+    batch problem ``batch_fn`` (_optimize_acqf_batch here, its restart-sharded
+    twin in distributed.py): input validation, the all-fixed shortcut, the
+    sequential greedy loop over q."""
     from .exceptions import UnsupportedError
     _reject_constraints(None, None, nonlinear_inequality_constraints, "optimize_acqf")
     gen_candidates = gen_candidates or gen_candidates_scipy
@@ -1072,7 +1122,7 @@ def optimize_acqf(acq_function, bounds, q, num_restarts, raw_samples=None, optio
                 ic_gen_kwargs=ic_gen_kwargs, inequality_constraints=inequality_constraints,
                 equality_constraints=equality_constraints)
     if not (sequential and q > 1):
-        return _optimize_acqf_batch(**args)
+        return batch_fn(**args)
     # _validate_sequential_inputs (optimize.py:162-199), then q greedy picks
     for group, kind in ((inequality_constraints, "inequality"), (equality_constraints, "equality")):
         if any(len(c[0].shape) > 1 for c in group or []):
@@ -1091,7 +1141,7 @@ def optimize_acqf(acq_function, bounds, q, num_restarts, raw_samples=None, optio
     base_pending = acq_function.X_pending
     picks, values = [], []
     for _ in range(q):
-        c, v = _optimize_acqf_batch(**args)
+        c, v = batch_fn(**args)
         picks.append(c)
         values.append(v)
         cands = torch.cat(picks, dim=-2)

@@ -277,3 +277,146 @@ def test_c3_gradient_fused_route_matches_oracle(c3, b, acq):
     torch.testing.assert_close(v[idx], ref.detach(), rtol=1e-6, atol=1e-10)
     assert go.abs().amax(dim=(1, 2)).min() > 0
     torch.testing.assert_close(gd[idx], go, rtol=1e-5, atol=1e-8)
+
+
+def _c4_models(golden):
+    X = torch.from_numpy(golden["dtlz2_X"])
+    Y = torch.from_numpy(golden["dtlz2_Y"])
+    assert X.shape == (2048, 6)
+    return X, Y, [_stgp(X, Y[:, t:t + 1], 0.6, 1e-3) for t in range(3)]
+
+
+def _spy_member_routes(monkeypatch):
+    """Counts of the ModelListGP gradient routes taken: the members' W in one
+    launch (kernels.w_matrix_members -> bo_post_w_split_members), the per-member
+    W (kernels.w_matrix), and the members' posterior backward passes in one
+    launch (kernels.post_backward_jobs)."""
+    from botorch_amd import kernels
+    calls = {"w_members": 0, "w_single": 0, "pb_jobs": 0}
+
+    def spy(name, key):
+        orig = getattr(kernels, name)
+
+        def f(*a, **k):
+            calls[key] += 1
+            return orig(*a, **k)
+        monkeypatch.setattr(kernels, name, f)
+    spy("w_matrix_members", "w_members")
+    spy("w_matrix", "w_single")
+    spy("post_backward_jobs", "pb_jobs")
+    return calls
+
+
+def test_c4_qehvi_gradient_member_routes_match_oracle(golden, monkeypatch):
+    """C4 forward + backward at the config size (ModelListGP(3), n = 2048,
+    q = 8, S = 128, b = 128) through the round-5 member-batched gradient routes
+    -- the members' W = R L^-1 in one stream-K launch (bo_post_w_split_members,
+    asserted: no per-member W) and the members' posterior backward passes in
+    one launch (bo_post_backward_jobs, asserted) -- dX at 8 spread t-batches
+    with non-zero values against torch.autograd through the oracle's qEHVI on
+    the reference's 294 cells (multi_objective/monte_carlo.py:230-322,
+    generation/gen.py:194-222), rtol 1e-5."""
+    from botorch_amd import kernels
+    from botorch_amd.acquisition import qExpectedHypervolumeImprovement
+    from botorch_amd.models import ModelListGP
+    from botorch_amd.multi_objective import FastNondominatedPartitioning
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import qehvi
+    from oracle.sampling import base_samples_multi_output
+    torch.set_num_threads(16)
+    X, Y, pairs = _c4_models(golden)
+    ref_point = torch.full((3,), -1.1, dtype=torch.float64)
+    part = FastNondominatedPartitioning(ref_point, Y)
+    S, q, b = 128, 8, 128
+    acqf = qExpectedHypervolumeImprovement(ModelListGP(*[p[0] for p in pairs]), ref_point.tolist(), part,
+                                           sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
+    g = torch.Generator().manual_seed(2)
+    P = X[torch.from_numpy(golden["dtlz2_pareto_mask"])]
+    pick = torch.randint(0, P.shape[0], (b, q), generator=g)
+    Xn = (P[pick] + 0.05 * torch.randn(b, q, 6, generator=g, dtype=torch.float64)).clamp(0, 1)
+    calls = _spy_member_routes(monkeypatch)
+    Xd = Xn.to(DEV).requires_grad_(True)
+    v = acqf(Xd)
+    (gd,) = torch.autograd.grad(v.sum(), Xd)
+    kernels.check_ladder_status(DEV)
+    assert calls["w_members"] >= 1 and calls["w_single"] == 0, \
+        f"the members' W did not go as one launch: {calls}"
+    assert calls["pb_jobs"] >= 1, f"the members' posterior backward was not one launch: {calls}"
+    v, gd = v.detach().cpu(), gd.cpu()
+    assert torch.isfinite(gd).all()
+    idx = _spread_nonzero(v, 8)
+    cl = torch.from_numpy(golden["dtlz2_cells_lower"])
+    cu = torch.from_numpy(golden["dtlz2_cells_upper"])
+    Zm = base_samples_multi_output(S, q, 3, 0)
+    orcs = [p[1] for p in pairs]
+    for i in idx.tolist():   # one t-batch at a time: the oracle's subset x cell tensors are large
+        Xo = Xn[i:i + 1].clone().requires_grad_(True)
+        ref = qehvi(orcs, Xo, Zm, cl, cu)
+        (go,) = torch.autograd.grad(ref.sum(), Xo)
+        torch.testing.assert_close(v[i:i + 1], ref.detach(), rtol=1e-7, atol=1e-10)
+        assert go.abs().max() > 0
+        torch.testing.assert_close(gd[i:i + 1], go, rtol=1e-5, atol=1e-8)
+
+
+def test_c4_qnehvi_config_size_matches_oracle(golden, monkeypatch):
+    """qNEHVI (section 8(f) rank 4) at the C4 shape: ModelListGP(3) on the
+    reference's DTLZ2 draw (n = 2048), X_baseline = the training inputs pruned
+    on the device (prune_baseline=True), S = 128 per-sample box decompositions,
+    q = 8, b = 128 through the cached baseline roots and the member-batched
+    routes (asserted).  Against QNEHVIOracle on the kept baseline: the baseline
+    samples, the values of 4 spread t-batches by exact hypervolume differences
+    (north_star's 1e-2 and the observed 1e-7), and value + dX through the
+    per-sample cells (rtol 1e-7 / 1e-5) -- multi_objective/monte_carlo.py:
+    325-468, utils/multi_objective/hypervolume.py:507-835."""
+    from botorch_amd import kernels
+    from botorch_amd.acquisition import qNoisyExpectedHypervolumeImprovement
+    from botorch_amd.models import ModelListGP
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from oracle.acquisition import QNEHVIOracle
+    torch.set_num_threads(16)
+    X, Y, pairs = _c4_models(golden)
+    ref_point = [-1.1] * 3
+    S, q, b = 128, 8, 128
+    torch.manual_seed(0)
+    acqf = qNoisyExpectedHypervolumeImprovement(ModelListGP(*[p[0] for p in pairs]), ref_point,
+                                                X.to(DEV), prune_baseline=True,
+                                                sampler=SobolQMCNormalSampler(torch.Size([S]), seed=0))
+    Xb = acqf.X_baseline.cpu()
+    r = Xb.shape[0]
+    assert 100 < r < 2048, f"pruned baseline size {r}"
+    orc = QNEHVIOracle([p[1] for p in pairs], Xb, ref_point, S, seed=0)
+    torch.testing.assert_close(acqf.baseline_samples, orc.Y_base, rtol=1e-8, atol=1e-10)
+    g = torch.Generator().manual_seed(4)
+    P = X[torch.from_numpy(golden["dtlz2_pareto_mask"])]
+    pick = torch.randint(0, P.shape[0], (b, q), generator=g)
+    Xn = (P[pick] + 0.05 * torch.randn(b, q, 6, generator=g, dtype=torch.float64)).clamp(0, 1)
+    calls = _spy_member_routes(monkeypatch)
+    from botorch_amd import acquisition
+    orig_rf = acquisition._roots_forward_batched
+
+    def spy_rf(*a, **k):
+        calls["roots_batched"] = calls.get("roots_batched", 0) + 1
+        return orig_rf(*a, **k)
+    monkeypatch.setattr(acquisition, "_roots_forward_batched", spy_rf)
+    Xd = Xn.to(DEV).requires_grad_(True)
+    v = acqf(Xd)
+    (gd,) = torch.autograd.grad(v.sum(), Xd)
+    assert calls.get("roots_batched", 0) >= 1, f"the members' batched roots did not run: {calls}"
+    with torch.no_grad():
+        v_fwd = acqf(Xn.to(DEV)).cpu()
+    kernels.check_ladder_status(DEV)
+    assert calls["w_single"] == 0 and calls["w_members"] >= 1, calls
+    v, gd = v.detach().cpu(), gd.cpu()
+    torch.testing.assert_close(v_fwd, v, rtol=1e-10, atol=1e-13)
+    idx = _spread_nonzero(v, 4)
+    ref_exact = orc.value_exact(Xn[idx[:2]])
+    torch.testing.assert_close(v[idx[:2]], ref_exact, rtol=1e-2, atol=1e-6)   # north_star MC bar
+    torch.testing.assert_close(v[idx[:2]], ref_exact, rtol=1e-7, atol=1e-10)
+    lo, hi = acqf.cell_lower_bounds.cpu(), acqf.cell_upper_bounds.cpu()
+    for i in idx.tolist():
+        Xo = Xn[i:i + 1].clone().requires_grad_(True)
+        rv = orc.value_cells(Xo, lo, hi)
+        (go,) = torch.autograd.grad(rv.sum(), Xo)
+        torch.testing.assert_close(v[i:i + 1], rv.detach(), rtol=1e-7, atol=1e-10)
+        assert go.abs().max() > 0
+        torch.testing.assert_close(gd[i:i + 1], go, rtol=1e-5, atol=1e-8)

@@ -285,3 +285,42 @@ def test_qnehvi_members_batched_roots_match_per_member(monkeypatch):
     torch.testing.assert_close(v1, v0, rtol=1e-10, atol=1e-13)
     torch.testing.assert_close(w1, w0, rtol=1e-10, atol=1e-13)
     torch.testing.assert_close(g1, g0, rtol=1e-8, atol=1e-11)
+
+
+def test_qnehvi_batched_roots_rebuilt_after_pending_join(monkeypatch):
+    """The members' stacked root operands (_roots_forward_batched's L_rr^-1 /
+    P_b / Z_base stacks, the backward's Q_b stack) belong to the roots they were
+    built from: after set_X_pending grows the baseline past max_iep (the roots
+    rebuilt with a larger r, hypervolume.py:795-820) the batched route must
+    rebuild them.  On the n = 1024 batched route: values and gradients after
+    the join equal a fresh acquisition on [X_baseline; X_pending]."""
+    from botorch_amd import acquisition, kernels
+    X, Y, model, _, _ = _setup(3, n=1024, r=40, seed=3)
+    assert kernels.split_plan(32, 4, 1024)[0] != 0
+    calls = []
+    orig = acquisition._roots_forward_batched
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(acquisition, "_roots_forward_batched", spy)
+    acqf = _qnehvi(model, X[:40], 32, 0, 3)
+    Xc = torch.rand(32, 4, 6, dtype=torch.float64, generator=torch.Generator().manual_seed(1))
+    _value_and_grad(acqf, Xc)              # builds the stacks for r = 40
+    assert calls
+    Xp = X[600:603]
+    acqf.set_X_pending(Xp.to(DEV))         # 3 > max_iep = 0: joins the baseline
+    assert acqf.X_baseline.shape[0] == 43 and acqf.X_pending is None
+    n0 = len(calls)
+    v, g = _value_and_grad(acqf, Xc)
+    with torch.no_grad():
+        w = acqf(Xc.to(DEV)).cpu()
+    assert len(calls) > n0, "the batched roots route did not run after the join"
+    fresh = _qnehvi(model, torch.cat([X[:40], Xp]), 32, 0, 3)
+    v0, g0 = _value_and_grad(fresh, Xc)
+    kernels.check_ladder_status(DEV)
+    assert (v0 > 0).sum() > 5
+    torch.testing.assert_close(v, v0, rtol=0, atol=0)
+    torch.testing.assert_close(w, v0, rtol=1e-12, atol=1e-14)
+    torch.testing.assert_close(g, g0, rtol=0, atol=0)
