@@ -184,7 +184,7 @@ def _fused_mc(X3: torch.Tensor, acqf, mode: int, best_f: float, best_f_s, Z: tor
             kernels.quad_ainv(cache, X3.shape[0], X3.shape[1]), cache.alpha,
             cap[0] if cap else None, cap[1] if cap else None)
         if cap:
-            kernels._CAPTURE[idx] = ("native", type(acqf).__name__)
+            kernels.record_capture_status(idx, None, type(acqf).__name__)
         else:
             kernels.ladder_prev_outcome(prev, idx, type(acqf).__name__)
         return acq

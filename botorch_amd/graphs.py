@@ -69,6 +69,10 @@ class GraphedAcquisition:
         # a status reduction, a device max and a pinned copy are captured too
         self._host = _lib.torch_ops().pinned_status() if not with_grad else \
             torch.zeros(2, dtype=torch.float64).pin_memory()
+        # a device-side status of another route beside the native one (a body
+        # mixing both) lands in a pinned pair of its own (kernels.
+        # record_capture_status), never over the native route's words
+        self._host2 = torch.zeros(2, dtype=torch.float64).pin_memory()
         counter = torch.zeros(1, dtype=torch.int32, device=self.dev)
         with kernels.capturing(self.dev) as cap:
             if not with_grad:
@@ -79,8 +83,9 @@ class GraphedAcquisition:
                     st = kernels._CAPTURE.get(cap.idx)
                     if st is not None and st[0] != "native":
                         # the replay's status: sticky max, then to the host
-                        torch.maximum(self._sticky, st[0], out=self._sticky)
-                        self._host.copy_(self._sticky, non_blocking=True)
+                        mixed = st[0] == "native+"
+                        torch.maximum(self._sticky, st[2] if mixed else st[0], out=self._sticky)
+                        (self._host2 if mixed else self._host).copy_(self._sticky, non_blocking=True)
             finally:
                 kernels._CAPTURE_STATUS.pop(cap.idx, None)
         self._counter = counter
@@ -109,7 +114,8 @@ class GraphedAcquisition:
     def _act(self) -> None:
         """The replays' status published to the host so far (sticky max):
         raise / warn, and re-arm the device maximum after a warning."""
-        info_max, jitter_max = float(self._host[0]), float(self._host[1])
+        info_max = max(float(self._host[0]), float(self._host2[0]))
+        jitter_max = max(float(self._host[1]), float(self._host2[1]))
         if info_max > 0 or jitter_max > 0:
             # re-armed before acting: a warning is given once per jittered
             # stretch, and a NotPSDError reports only the replays up to now
@@ -117,6 +123,7 @@ class GraphedAcquisition:
             # later replay that factors cleanly must not raise again)
             self._sticky.zero_()
             self._host.zero_()
+            self._host2.zero_()
             kernels._ladder_outcome(info_max, jitter_max, self._what)
 
     def check_status(self) -> None:

@@ -1101,8 +1101,35 @@ def _capture_status(info: torch.Tensor, jitter: torch.Tensor, what: str) -> bool
     if info.numel():
         check(lib().bo_ladder_status(_p(info.contiguous()), _p(jitter.contiguous()), info.numel(),
                                      _p(packed), _stream(dev)), "ladder_status")
-    _CAPTURE[idx] = (packed, what)
+    record_capture_status(idx, packed, what)
     return True
+
+
+def record_capture_status(idx: int, packed, what: str) -> None:
+    """Record one route's ladder status in the running capture, merging with
+    what earlier routes of the same body recorded: device statuses combine by
+    a captured max; a device status beside the native route (whose
+    finalisation folds into the graph's pinned words) is kept as
+    ("native+", what, packed) so the graph copies it to a second pinned pair
+    -- neither kind ever overwrites the other.  ``packed`` None: the native
+    route."""
+    prev = _CAPTURE.get(idx)
+    if packed is None:                                   # the native route
+        if prev is None or prev[0] == "native":
+            _CAPTURE[idx] = ("native", what)
+        elif prev[0] == "native+":
+            pass
+        else:                                            # a device status came first
+            _CAPTURE[idx] = ("native+", what, prev[0])
+        return
+    if prev is None:
+        _CAPTURE[idx] = (packed, what)
+    elif prev[0] == "native":
+        _CAPTURE[idx] = ("native+", prev[1], packed)
+    elif prev[0] == "native+":
+        _CAPTURE[idx] = ("native+", prev[1], torch.maximum(prev[2], packed))
+    else:
+        _CAPTURE[idx] = (torch.maximum(prev[0], packed), prev[1])
 
 
 def raise_not_psd_deferred(info: torch.Tensor, jitter: torch.Tensor, what: str) -> None:

@@ -222,3 +222,40 @@ def test_quad_plan_geometries(monkeypatch):
     assert pairs(64, 8, 1024) == 0
     monkeypatch.setenv("BO_POST_QUAD", "1")
     assert pairs(512, 16, 4096) == chunks(64)
+
+
+def test_capture_status_merge_never_overwrites():
+    """kernels.record_capture_status: inside one graph capture, the native
+    route (its finalisation folds the ladder status into the graph's pinned
+    words) and any device-side status of another route are both kept --
+    device statuses combine by max, a device status beside the native route
+    becomes ("native+", what, packed) in either order (graphs.py copies it to
+    a second pinned pair)."""
+    from botorch_amd import kernels
+    idx = 7
+    t = lambda a, b: torch.tensor([a, b], dtype=torch.float64)  # noqa: E731
+    try:
+        for order in ("native_first", "device_first"):
+            kernels._CAPTURE[idx] = None
+            if order == "native_first":
+                kernels.record_capture_status(idx, None, "qEI")
+                kernels.record_capture_status(idx, t(0.0, 1e-8), "qEHVI")
+                kernels.record_capture_status(idx, t(2.0, 0.0), "qEHVI")
+            else:
+                kernels.record_capture_status(idx, t(0.0, 1e-8), "qEHVI")
+                kernels.record_capture_status(idx, None, "qEI")
+                kernels.record_capture_status(idx, t(2.0, 0.0), "qEHVI")
+                kernels.record_capture_status(idx, None, "qEI")
+            st = kernels._CAPTURE[idx]
+            assert st[0] == "native+"
+            assert torch.equal(st[2], t(2.0, 1e-8))
+        kernels._CAPTURE[idx] = None
+        kernels.record_capture_status(idx, t(1.0, 0.0), "a")
+        kernels.record_capture_status(idx, t(0.0, 1e-6), "b")
+        assert torch.equal(kernels._CAPTURE[idx][0], t(1.0, 1e-6))
+        kernels._CAPTURE[idx] = None
+        kernels.record_capture_status(idx, None, "qEI")
+        kernels.record_capture_status(idx, None, "qEI")
+        assert kernels._CAPTURE[idx] == ("native", "qEI")
+    finally:
+        kernels._CAPTURE.pop(idx, None)

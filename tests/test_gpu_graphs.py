@@ -113,3 +113,58 @@ def test_graphed_forward_status_without_stalls():
             ga(good)
         ga.check_status()
         assert sum(issubclass(w.category, NumericalWarning) for w in ws) == n_warn
+
+
+def test_graphed_mixed_routes_keep_both_statuses():
+    """A forward-only capture whose body mixes a route that records a device
+    ladder status (qEHVI's members, _FusedQEHVI under capture) with the native
+    fused qEI (its finalisation folds into the graph's pinned words): the
+    device status is kept beside the native one (kernels.
+    record_capture_status, a second pinned pair), so a jittered qEHVI root in
+    a replay still reaches the caller as NumericalWarning, and the replay
+    equals the eager body."""
+    import warnings
+    from botorch_amd import kernels
+    from botorch_amd.acquisition import qExpectedHypervolumeImprovement, qExpectedImprovement
+    from botorch_amd.exceptions import NumericalWarning
+    from botorch_amd.graphs import GraphedAcquisition
+    from botorch_amd.models import ModelListGP
+    from botorch_amd.multi_objective import FastNondominatedPartitioning
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from tests.test_gpu_acquisition import _setup
+    members = []
+    for _ in range(2):   # noiseless members: duplicated training rows give singular roots
+        X, Y, mm, _ = _setup(n=64, noise=1e-4)
+        mm.likelihood.noise = torch.tensor([1e-12], dtype=torch.float64)
+        members.append(mm.eval())
+    Ym = torch.cat([Y, 0.5 * Y], dim=-1)
+    ref_point = Ym.min(dim=0).values - 0.1
+    part = FastNondominatedPartitioning(ref_point, Ym)
+    qehvi = qExpectedHypervolumeImprovement(ModelListGP(*members), ref_point.tolist(), part,
+                                            sampler=SobolQMCNormalSampler(torch.Size([16]), seed=0))
+    m2, Y2 = _model(256, seed=6)   # noisy: clean roots everywhere
+    qei = qExpectedImprovement(m2, Y2.max().item() - 0.2,
+                               sampler=SobolQMCNormalSampler(torch.Size([32]), seed=0))
+
+    class Mixed(torch.nn.Module):
+        def forward(self, X):   # the device-status route first, then the native one
+            return qehvi(X) + qei(X)
+
+    body = Mixed()
+    bad = X[:3].unsqueeze(1).repeat(1, 2, 1).to(DEV)
+    good = torch.rand(3, 2, 6, dtype=torch.float64).to(DEV)
+    kernels.check_ladder_status()
+    ga = GraphedAcquisition(body, good)
+    with warnings.catch_warnings(record=True) as ws:
+        warnings.simplefilter("always")
+        for Xc in (good,):
+            with torch.no_grad():
+                ref = body(Xc)
+            kernels.check_ladder_status()
+            assert torch.equal(ga(Xc).clone(), ref)
+        ga.check_status()
+        assert not any(issubclass(w.category, NumericalWarning) for w in ws)
+        ga(bad)
+        ga.check_status()
+        assert any(issubclass(w.category, NumericalWarning) for w in ws), \
+            "the qEHVI root's jitter was dropped by the mixed capture"
