@@ -283,6 +283,21 @@ __device__ __forceinline__ void publish(const Ctx& c, u32* f, u32 val) {
   if (c.tid == 0) __hip_atomic_store(f, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The same, but waiting only for the stores issued BEFORE the wave's `younger`
+// most recent vector-memory instructions (loads, stores and atomics count
+// together, in issue order): the prefetch loads issued after a tile's stores
+// stay in flight.  `younger` must not exceed the instructions really issued
+// after those stores (fewer is safe, only slower); wave-uniform.
+__device__ __forceinline__ void publish_after(const Ctx& c, u32* f, u32 val, int younger) {
+  younger = __builtin_amdgcn_readfirstlane(younger);  // (uniform: scalar branches)
+  if (younger >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (younger >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (younger >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (c.tid == 0) __hip_atomic_store(f, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Thread 0 polls until f1 >= t1 and f2 >= t2 (bounded: timeout -> abort word);
 // the workgroup then proceeds together.  Returns false when aborted.
 __device__ __forceinline__ bool wait2(const Ctx& c, const u32* f1, u32 t1, const u32* f2, u32 t2,
@@ -1172,11 +1187,31 @@ __device__ bool batched_update2(const Ctx& c, const Flags& f, int kb, int nk, in
                                                       c.wn + 16 * b + mfma_col(c.lane)));
   };
   bool ok = true;
+  // Deferred publish (round 6): a row's C tile is stored at its last step and
+  // its flag published at the END of the next step, draining only those
+  // stores (publish_after: the loads issued after them -- the next operands --
+  // stay in flight).  A full vmcnt(0) drain right after the stores waited for
+  // the write-through stores and the in-flight prefetch together, every row.
+  // The chunk's first row publishes at once (it may be the diagonal tile the
+  // chain waits on), and nothing blocks while a row is unpublished.
+  u32* pending = nullptr;
+  u32 pend_val = 0;
+  int pend_younger = 0;  // vector-memory instructions issued after its stores
+  // this thread's vector-memory instructions per issue_c / issue_a
+  const int n_c = (KIND == 2 && v0 == 0u) ? 0 : 16;
+  const int n_a = 8;
+  auto flush = [&]() {
+    if (pending) {
+      publish(c, pending, pend_val);
+      pending = nullptr;
+    }
+  };
   // one stream element in register slot S (the other slot: O)
   auto step = [&](int e, double2 (&pvS)[8], double2 (&pvO)[8]) {
     const int r = e / nk, g = e - r * nk, i = i0 + r;
     if (g == 0) {
       if (issued <= e) {  // not prefetched: wait for the row, then its C and two operands
+        flush();  // never block while holding an unpublished row (a waiter could need it)
         if (!wait2(c, f.at(f.fL, i, ke - 1), 1u, f.at(fC, i, j), v0, f.abortw, s_ok, wsum)) {
           ok = false;
           return;
@@ -1228,13 +1263,28 @@ __device__ bool batched_update2(const Ctx& c, const Flags& f, int kb, int nk, in
         if (g2 == 0) issue_c(i2);
         if (own(i2)) issue_a(pvS, i2, kb + g2);
         issued = e2 + 1;
+        pend_younger += (g2 == 0 ? n_c : 0) + (own(i2) ? n_a : 0);
       }
     }
     acc_mma_nt(c, acc, own(i) ? X0 : XB(g), XB(g), sgn);
-    __syncthreads();  // X0 free for the next element's operand
+    if (pending) {  // the previous row: its stores had this step's MFMAs to land
+      publish_after(c, pending, pend_val, pend_younger);
+      pending = nullptr;
+    } else {
+      __syncthreads();  // X0 free for the next element's operand
+    }
     if (g == nk - 1) {
       acc_store(c, acc, rc, i, j);
-      publish(c, f.at(fC, i, j), v1);
+      if (i == i0 || e + 1 >= E) {
+        publish(c, f.at(fC, i, j), v1);
+      } else {
+        // (compiler order: no later load may be hoisted above these stores,
+        // or publish_after's count would not cover them)
+        asm volatile("" ::: "memory");
+        pending = f.at(fC, i, j);
+        pend_val = v1;
+        pend_younger = 0;
+      }
     }
   };
   for (int e = 0; e < E; e += 2) {
@@ -1245,6 +1295,7 @@ __device__ bool batched_update2(const Ctx& c, const Flags& f, int kb, int nk, in
       if (!ok) return false;
     }
   }
+  flush();
   return true;
 }
 
@@ -2088,7 +2139,8 @@ extern "C" int bo_chol_dag_tasks_ainv(int T, int* out, int cap) {
 
 extern "C" int bo_chol_dag_tasks(int T, int* out, int cap) {
   if (T < 1) return 0;
-  const std::vector<int4> v = build_tasks(T);
+  // the queue one matrix's launch runs (bo_chol_dag: build_tasks_batched)
+  const std::vector<int4> v = build_tasks_batched(T, 1);
   const int n = (int)v.size();
   for (int t = 0; t < n && t < cap; ++t) {
     out[4 * t] = v[t].x;
