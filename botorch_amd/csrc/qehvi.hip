@@ -82,7 +82,9 @@ __global__ __launch_bounds__(NT) void qehvi_kernel(
   const int sbeg = (int)((int64_t)S * h / H), send = (int)((int64_t)S * (h + 1) / H);
   const int tid = threadIdx.x;
   const int per_sample = q * M;
-  const int chunk = LDS_SAMPLES_DOUBLES / per_sample;
+  // a chunk's samples, then their per-objective maxima over the points
+  const int chunk = LDS_SAMPLES_DOUBLES / (per_sample + M);
+  double* const fmx = f + chunk * per_sample;
   if constexpr (CELLS_LDS) {
     for (int e = tid; e < K * M; e += NT) {
       cells[e] = lo[e];
@@ -98,21 +100,31 @@ __global__ __launch_bounds__(NT) void qehvi_kernel(
       f[e] = sample_value<M>(B, b, q, (e / M) % q, e % M, s0 + s, mean, L, Z, ex);
     }
     __syncthreads();
+    for (int e = tid; e < ns * M; e += NT) {
+      const double* fs = f + (e / M) * per_sample + e % M;
+      double mx = fs[0];
+      for (int p = 1; p < q; ++p) mx = fmax(mx, fs[p * M]);
+      fmx[e] = mx;
+    }
+    __syncthreads();
     for (int e = tid; e < ns * K; e += NT) {
       const int s = e / K;
       const int k = e % K;
       double l[M], u[M];
       const int64_t co = (int64_t)(s0 + s) * ex.cstride + (int64_t)k * M;
+      // a point is active in the cell only if it exceeds the lower corner in
+      // every objective, so no point is unless each objective's maximum over
+      // the points does: such pairs contribute exactly zero (skipped; at C4
+      // over 90% of the (sample, cell) pairs have no active point)
+      bool any = true;
 #pragma unroll
       for (int t = 0; t < M; ++t) {
-        if constexpr (CELLS_LDS) {
-          l[t] = cells[k * M + t];
-          u[t] = cells[LDS_CELL_DOUBLES / 2 + k * M + t];
-        } else {
-          l[t] = lo[co + t];
-          u[t] = hi[co + t];
-        }
+        l[t] = CELLS_LDS ? cells[k * M + t] : lo[co + t];
+        any = any && (fmx[s * M + t] > l[t]);
       }
+      if (!any) continue;
+#pragma unroll
+      for (int t = 0; t < M; ++t) u[t] = CELLS_LDS ? cells[LDS_CELL_DOUBLES / 2 + k * M + t] : hi[co + t];
       const double* fs = f + s * per_sample;
       double a[QMAX][M];
       unsigned act = 0;
@@ -191,7 +203,9 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
   const int sbeg = (int)((int64_t)S * h / H), send = (int)((int64_t)S * (h + 1) / H);
   const int tid = threadIdx.x;
   const int per_sample = q * M;
-  const int chunk = CH / per_sample;
+  // a chunk's samples (then their per-objective maxima over the points in f)
+  const int chunk = CH / (per_sample + M);
+  double* const fmx = f + chunk * per_sample;
   const double g = dacq[b] / (double)S;
   // entries owned by this thread: (t, p, j) with j <= p (j == p + 1 -> dmean)
   const int nent = M * q * (q + 3) / 2;
@@ -202,6 +216,13 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
     for (int e = tid; e < ns * per_sample; e += NT) {
       const int s = e / per_sample;
       f[e] = sample_value<M>(B, b, q, (e / M) % q, e % M, s0 + s, mean, L, Z, ex);
+    }
+    __syncthreads();
+    for (int e = tid; e < ns * M; e += NT) {
+      const double* fs = f + (e / M) * per_sample + e % M;
+      double mx = fs[0];
+      for (int p = 1; p < q; ++p) mx = fmax(mx, fs[p * M]);
+      fmx[e] = mx;
     }
     __syncthreads();
     // GROUP consecutive lanes share one sample: lane g of the group takes the
@@ -217,11 +238,15 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
       for (int k = tid % GROUP; k < K; k += GROUP) {
         double l[M], u[M];
         const int64_t co = (int64_t)(s0 + s) * ex.cstride + (int64_t)k * M;
+        bool any = true;  // as the forward: no active point -> no gradient
 #pragma unroll
         for (int t = 0; t < M; ++t) {
           l[t] = lo[co + t];
-          u[t] = hi[co + t];
+          any = any && (fmx[s * M + t] > l[t]);
         }
+        if (!any) continue;
+#pragma unroll
+        for (int t = 0; t < M; ++t) u[t] = hi[co + t];
         double a[QMAX][M];
         unsigned act = 0;
 #pragma unroll
