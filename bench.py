@@ -628,7 +628,7 @@ def other_configs(dev, cpu=True):
     return out
 
 
-def time_cholesky(Xtr, dev, reps=10, shapes=((3, 2048), (4, 4096), (8, 4096))):
+def time_cholesky(Xtr, dev, reps=10, shapes=((3, 2048), (4, 4096), (8, 4096)), ainv=True):
     """Standalone n x n Cholesky + triangular inverse (bo_cholesky_inverse, the
     persistent task DAG) on the C3 kernel matrix ("standalone
     n x n Cholesky ms and MFMA %"): HIP events on the launch stream around the
@@ -668,6 +668,8 @@ def time_cholesky(Xtr, dev, reps=10, shapes=((3, 2048), (4, 4096), (8, 4096))):
     out = {"n": n, "ms": ms, "flops": fl, "tflops": fl / (ms * 1e-3) / 1e12,
            "frac_of_spec": fl / (ms * 1e-3) / 1e12 / 78.6,
            "note": "factor + inverse, one persistent task-DAG launch, input in HBM"}
+    if not ainv and not shapes:  # the single launch alone (tools/chol_only.py single)
+        return out
     # the MLL closure's launch: factor + inverse + A^{-1} = L^{-T} L^{-1} (n^3/3
     # more) in one DAG (bo_cholesky_inverse_ainv), against the two launches
     # (DAG, then bo_ainv) it replaces
