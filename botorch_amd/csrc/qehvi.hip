@@ -64,7 +64,9 @@ __device__ __forceinline__ double sample_value(int B, int b, int q, int p, int t
 // LDS once, so the (sample, cell) loop reads only LDS
 constexpr int LDS_CELL_DOUBLES = 2048;  // K * M <= 1024 (C4: 294 x 3)
 
-template <int M, int NT = FWD_THREADS, bool CELLS_LDS = false>
+// QB: the q bucket (4, 8 or QMAX) the per-point arrays are sized for -- the
+// backward's a / gacc arrays at QMAX spilled to scratch (300-400 B per lane).
+template <int M, int NT = FWD_THREADS, bool CELLS_LDS = false, int QB = QMAX>
 __global__ __launch_bounds__(NT) void qehvi_kernel(
     int B, int q, const double* __restrict__ mean, const double* __restrict__ L,
     const double* __restrict__ Z, int S, const double* __restrict__ lo,
@@ -126,10 +128,10 @@ __global__ __launch_bounds__(NT) void qehvi_kernel(
 #pragma unroll
       for (int t = 0; t < M; ++t) u[t] = CELLS_LDS ? cells[LDS_CELL_DOUBLES / 2 + k * M + t] : hi[co + t];
       const double* fs = f + s * per_sample;
-      double a[QMAX][M];
+      double a[QB][M];
       unsigned act = 0;
 #pragma unroll
-      for (int p = 0; p < QMAX; ++p) {
+      for (int p = 0; p < QB; ++p) {
         bool ok = p < q;
 #pragma unroll
         for (int t = 0; t < M; ++t) {
@@ -145,7 +147,7 @@ __global__ __launch_bounds__(NT) void qehvi_kernel(
 #pragma unroll
         for (int t = 0; t < M; ++t) mn[t] = INFINITY;
 #pragma unroll
-        for (int p = 0; p < QMAX; ++p)
+        for (int p = 0; p < QB; ++p)
           if (sub & (1u << p))
 #pragma unroll
             for (int t = 0; t < M; ++t) mn[t] = fmin(mn[t], a[p][t]);
@@ -185,7 +187,7 @@ __global__ __launch_bounds__(64) void qehvi_part_reduce_kernel(const double* __r
 // clamped-at-lower term is zero with zero gradient).  df[s] is summed by one
 // 16-lane group over the cells in a fixed order (no atomics), then dmean_t[p] = sum_s df[s][p][t] and
 // dL_t[p][j] = sum_s df[s][p][t] Z[s][j m + t] (j <= p), scaled by dacq / S.
-template <int M, int NT = BWD_THREADS>
+template <int M, int NT = BWD_THREADS, int QB = QMAX>
 __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
     int B, int q, const double* __restrict__ mean, const double* __restrict__ L,
     const double* __restrict__ Z, int S, const double* __restrict__ lo,
@@ -230,9 +232,9 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
     // fixed butterfly, so df (and every gradient) is bitwise reproducible
     for (int s = tid / GROUP; s < ns; s += NT / GROUP) {
       const double* fs = f + s * per_sample;
-      double gacc[QMAX][M];
+      double gacc[QB][M];
 #pragma unroll
-      for (int p = 0; p < QMAX; ++p)
+      for (int p = 0; p < QB; ++p)
 #pragma unroll
         for (int t = 0; t < M; ++t) gacc[p][t] = 0.0;
       for (int k = tid % GROUP; k < K; k += GROUP) {
@@ -247,10 +249,10 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
         if (!any) continue;
 #pragma unroll
         for (int t = 0; t < M; ++t) u[t] = hi[co + t];
-        double a[QMAX][M];
+        double a[QB][M];
         unsigned act = 0;
 #pragma unroll
-        for (int p = 0; p < QMAX; ++p) {
+        for (int p = 0; p < QB; ++p) {
           bool ok = p < q;
 #pragma unroll
           for (int t = 0; t < M; ++t) {
@@ -269,7 +271,7 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
             am[t] = 0;
           }
 #pragma unroll
-          for (int p = 0; p < QMAX; ++p)
+          for (int p = 0; p < QB; ++p)
             if (sub & (1u << p))
 #pragma unroll
               for (int t = 0; t < M; ++t)
@@ -286,13 +288,13 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
               if (t2 != t) o *= mn[t2];
             // the min reaches f only where f < u (else the upper bound is active)
 #pragma unroll
-            for (int p = 0; p < QMAX; ++p)
+            for (int p = 0; p < QB; ++p)
               if (p == am[t] && fs[p * M + t] < u[t]) gacc[p][t] += o;
           }
         }
       }
 #pragma unroll
-      for (int p = 0; p < QMAX; ++p) {
+      for (int p = 0; p < QB; ++p) {
         if (p >= q) break;
 #pragma unroll
         for (int t = 0; t < M; ++t) {
@@ -463,20 +465,29 @@ extern "C" int bo_qehvi_ext(int B, int q, int m, const double* mean, const doubl
     H = std::max(1, std::min(H, S));
   }
   const unsigned grid = (unsigned)((int64_t)B * H);
-#define BO_QF(MM)                                                                              \
+#define BO_QF(MM, QQ)                                                                          \
   if (cl)                                                                                      \
-    qehvi_kernel<MM, FWD_THREADS, true><<<grid, FWD_THREADS, 0, st>>>(                         \
+    qehvi_kernel<MM, FWD_THREADS, true, QQ><<<grid, FWD_THREADS, 0, st>>>(                     \
         B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, acq, H, work);                           \
   else                                                                                         \
-    qehvi_kernel<MM><<<grid, FWD_THREADS, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, \
-                                                   acq, H, work)
-  if (m == 2) {
-    BO_QF(2);
-  } else if (m == 3) {
-    BO_QF(3);
-  } else {
-    BO_QF(4);
+    qehvi_kernel<MM, FWD_THREADS, false, QQ><<<grid, FWD_THREADS, 0, st>>>(                    \
+        B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, acq, H, work)
+#define BO_QFM(MM)          \
+  if (q <= 4) {             \
+    BO_QF(MM, 4);           \
+  } else if (q <= 8) {      \
+    BO_QF(MM, 8);           \
+  } else {                  \
+    BO_QF(MM, QMAX);        \
   }
+  if (m == 2) {
+    BO_QFM(2);
+  } else if (m == 3) {
+    BO_QFM(3);
+  } else {
+    BO_QFM(4);
+  }
+#undef BO_QFM
 #undef BO_QF
   BO_LAUNCH_CHECK();
   if (H > 1) {
@@ -532,10 +543,23 @@ extern "C" int bo_qehvi_backward_ext(int B, int q, int m, const double* mean, co
     H = std::max(1, std::min(H, S));
   }
   const unsigned grid = (unsigned)((int64_t)B * H);
-#define BO_QB(MM, NT) qehvi_backward_kernel<MM, NT><<<grid, NT, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, dacq, dmean, dL, dF, H, work)
-  if (m == 2) BO_QB(2, BWD_THREADS);
-  else if (m == 3) BO_QB(3, BWD_THREADS);
-  else BO_QB(4, 256);  // m = 4 needs 256 VGPRs: 4 waves per workgroup
+#define BO_QB(MM, NT, QQ) qehvi_backward_kernel<MM, NT, QQ><<<grid, NT, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, dacq, dmean, dL, dF, H, work)
+#define BO_QBM(MM, NT)        \
+  if (q <= 4) {               \
+    BO_QB(MM, NT, 4);         \
+  } else if (q <= 8) {        \
+    BO_QB(MM, NT, 8);         \
+  } else {                    \
+    BO_QB(MM, NT, QMAX);      \
+  }
+  if (m == 2) {
+    BO_QBM(2, BWD_THREADS);
+  } else if (m == 3) {
+    BO_QBM(3, BWD_THREADS);
+  } else {
+    BO_QBM(4, 256);  // m = 4 needs 256 VGPRs: 4 waves per workgroup
+  }
+#undef BO_QBM
 #undef BO_QB
   BO_LAUNCH_CHECK();
   if (H > 1) {
