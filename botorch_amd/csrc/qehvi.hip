@@ -187,7 +187,10 @@ __global__ __launch_bounds__(64) void qehvi_part_reduce_kernel(const double* __r
 // clamped-at-lower term is zero with zero gradient).  df[s] is summed by one
 // 16-lane group over the cells in a fixed order (no atomics), then dmean_t[p] = sum_s df[s][p][t] and
 // dL_t[p][j] = sum_s df[s][p][t] Z[s][j m + t] (j <= p), scaled by dacq / S.
-template <int M, int NT = BWD_THREADS, int QB = QMAX>
+// CELLS_LDS (shared cells, K m <= LDS_CELL_DOUBLES / 2): the cells staged in
+// LDS once; the chunk's base samples are staged in LDS always (read by the
+// sample values and again by the dmean / dL sums).
+template <int M, int NT = BWD_THREADS, int QB = QMAX, bool CELLS_LDS = false>
 __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
     int B, int q, const double* __restrict__ mean, const double* __restrict__ L,
     const double* __restrict__ Z, int S, const double* __restrict__ lo,
@@ -200,6 +203,8 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
   constexpr int CH = LDS_SAMPLES_DOUBLES / 2;
   __shared__ double f[CH];
   __shared__ double df[CH];
+  __shared__ double zc[CH];  // the chunk's base samples, Z[s0 + s][.]
+  __shared__ double cells[CELLS_LDS ? LDS_CELL_DOUBLES : 1];
   const int b = blockIdx.x / H;
   const int h = blockIdx.x - b * H;
   const int sbeg = (int)((int64_t)S * h / H), send = (int)((int64_t)S * (h + 1) / H);
@@ -212,12 +217,26 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
   // entries owned by this thread: (t, p, j) with j <= p (j == p + 1 -> dmean)
   const int nent = M * q * (q + 3) / 2;
   double accv[2] = {0.0, 0.0};
+  if constexpr (CELLS_LDS) {
+    for (int e = tid; e < K * M; e += NT) {
+      cells[e] = lo[e];
+      cells[LDS_CELL_DOUBLES / 2 + e] = hi[e];
+    }
+  }
   for (int s0 = sbeg; s0 < send; s0 += chunk) {
     const int ns = min(chunk, send - s0);
     __syncthreads();
+    for (int e = tid; e < ns * per_sample; e += NT) zc[e] = Z[(int64_t)s0 * per_sample + e];
+    __syncthreads();
     for (int e = tid; e < ns * per_sample; e += NT) {
-      const int s = e / per_sample;
-      f[e] = sample_value<M>(B, b, q, (e / M) % q, e % M, s0 + s, mean, L, Z, ex);
+      // sample_value with the base samples from LDS (the same sum, in order)
+      const int s = e / per_sample, p = (e / M) % q, t = e % M;
+      const double* Lt = L + (((int64_t)t * B + b) * q + p) * q;
+      const double* zs = zc + s * per_sample;
+      double v = mean[((int64_t)t * B + b) * q + p];
+      if (ex.F) v += ex.F[t * ex.sF + (int64_t)(s0 + s) * ex.ldF + (int64_t)b * ex.Qp + p];
+      for (int j = 0; j <= p; ++j) v = fma(Lt[j], zs[j * M + t], v);
+      f[e] = v;
     }
     __syncthreads();
     for (int e = tid; e < ns * M; e += NT) {
@@ -243,12 +262,12 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
         bool any = true;  // as the forward: no active point -> no gradient
 #pragma unroll
         for (int t = 0; t < M; ++t) {
-          l[t] = lo[co + t];
+          l[t] = CELLS_LDS ? cells[k * M + t] : lo[co + t];
           any = any && (fmx[s * M + t] > l[t]);
         }
         if (!any) continue;
 #pragma unroll
-        for (int t = 0; t < M; ++t) u[t] = hi[co + t];
+        for (int t = 0; t < M; ++t) u[t] = CELLS_LDS ? cells[LDS_CELL_DOUBLES / 2 + k * M + t] : hi[co + t];
         double a[QB][M];
         unsigned act = 0;
 #pragma unroll
@@ -327,7 +346,7 @@ __global__ __launch_bounds__(NT) void qehvi_backward_kernel(
       double acc = 0.0;
       for (int s = 0; s < ns; ++s) {
         const double d = df[s * per_sample + p * M + t];
-        acc = fma(d, (j <= p) ? Z[(int64_t)(s0 + s) * q * M + j * M + t] : 1.0, acc);
+        acc = fma(d, (j <= p) ? zc[s * per_sample + j * M + t] : 1.0, acc);
       }
       accv[w] += acc;
     }
@@ -543,7 +562,14 @@ extern "C" int bo_qehvi_backward_ext(int B, int q, int m, const double* mean, co
     H = std::max(1, std::min(H, S));
   }
   const unsigned grid = (unsigned)((int64_t)B * H);
-#define BO_QB(MM, NT, QQ) qehvi_backward_kernel<MM, NT, QQ><<<grid, NT, 0, st>>>(B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, dacq, dmean, dL, dF, H, work)
+  const bool cl = cell_stride == 0 && (int64_t)K * m <= LDS_CELL_DOUBLES / 2;
+#define BO_QB(MM, NT, QQ)                                                                      \
+  if (cl)                                                                                      \
+    qehvi_backward_kernel<MM, NT, QQ, true><<<grid, NT, 0, st>>>(                              \
+        B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, dacq, dmean, dL, dF, H, work);           \
+  else                                                                                         \
+    qehvi_backward_kernel<MM, NT, QQ, false><<<grid, NT, 0, st>>>(                             \
+        B, q, mean, L, Z, S, cell_lo, cell_hi, K, ex, dacq, dmean, dL, dF, H, work)
 #define BO_QBM(MM, NT)        \
   if (q <= 4) {               \
     BO_QB(MM, NT, 4);         \
