@@ -164,6 +164,15 @@ struct PostMembers {
   int nm;  // 0: the kernel's own pointer arguments
 };
 
+// The next k-step's U rows are stored to the other LDS stage on every step,
+// the last one included (its rows are the current step's, the stage is not
+// read again before the next segment's prologue rewrites it behind a
+// barrier): with the store behind `if (more)` the compiler sank the U loads
+// into that branch, after the step's MFMAs, and every step waited the full
+// load latency before its store.
+#ifndef BO_USTORE_ALWAYS
+#define BO_USTORE_ALWAYS 1
+#endif
 template <int KIND, int ND, bool SPLIT, bool CROSS, bool PRE = false, bool LOWERK = false,
           bool FUSEDX = false>
 __global__ __launch_bounds__(256, 2) void post_partials_kernel(
@@ -417,7 +426,7 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
         kv[2 * ks + 1] = BO_KVAL(knext + kh * 8 + 2 * ks + 1);                      \
       }                                                                              \
     }                                                                                \
-    if (more) BO_STORE(cur ^ 1);                                                     \
+    if (BO_USTORE_ALWAYS || more) BO_STORE(cur ^ 1);                                 \
     if (PRE) {                                                                       \
       _Pragma("unroll") for (int it = 0; it < 2; ++it)                              \
         _Pragma("unroll") for (int ks = 0; ks < 4; ++ks) bc[it][ks] = bn[it][ks];   \
