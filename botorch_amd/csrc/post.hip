@@ -170,6 +170,9 @@ struct PostMembers {
 // barrier): with the store behind `if (more)` the compiler sank the U loads
 // into that branch, after the step's MFMAs, and every step waited the full
 // load latency before its store.
+#ifndef BO_POST_PAIRED_REV
+#define BO_POST_PAIRED_REV 1
+#endif
 #ifndef BO_USTORE_ALWAYS
 #define BO_USTORE_ALWAYS 1
 #endif
@@ -305,6 +308,18 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   const int c0 = ci * PC;
   const int i0 = ii * PI;
   const int nsteps = (kend - kbeg + PK - 1) / PK;
+  // Paired schedule: every workgroup's long + short k-ranges add up to the
+  // same count, so a super-tile's 64 workgroups stay in step (and share each
+  // k-slice of K*x^T and U in the XCD's L2) only if both tiles walk relative to
+  // the common end of the ranges: k = 0 for the upper ranges [0, kend) -- the
+  // long tile ascending, the short one descending and ending at k = 0 at the
+  // same moment in every workgroup -- and k = n for the lower (LOWERK) ranges.
+  // Ascending short tiles started 8 k-steps apart per column offset and re-read
+  // K*x^T from HBM about once per column tile.  Only the summation order
+  // differs between the walks.
+  const bool rev = BO_POST_PAIRED_REV && !SPLIT && grouped == 2 && ((sidx == 1) != LOWERK);
+  const int kfirst = rev ? kbeg + (nsteps - 1) * PK : kbeg;
+  const int kdir = rev ? -PK : PK;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -389,13 +404,13 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
     _Pragma("unroll") for (int ks = 0; ks < 4; ++ks)                              \
       DST[it][ks] = FUSEDX ? ktb[((int64_t)((K0) >> 4) * (nI * (PI / 16)) + it) * 256 + ks * 64] \
                            : ktw[(int64_t)((K0) + 4 * ks) * (nI * PI) + it * 16];
-  BO_LOAD_U(kbeg);
+  BO_LOAD_U(kfirst);
   if (PRE) {
-    BO_LOAD_B(kbeg, bc);
+    BO_LOAD_B(kfirst, bc);
   } else {
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk)
-      kv[kk] = BO_KVAL(kbeg + kh * 8 + kk);
+      kv[kk] = BO_KVAL(kfirst + kh * 8 + kk);
   }
   BO_STORE(0);
   __syncthreads();
@@ -406,7 +421,7 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   {                                                                                  \
     const int cur = t & 1;                                                           \
     const bool more = t + 1 < nsteps;                                                \
-    const int knext = kbeg + (more ? (t + 1) * PK : t * PK);                         \
+    const int knext = kfirst + (more ? t + 1 : t) * kdir;                            \
     XLOAD                                                                            \
     BO_LOAD_U(knext);                                                                \
     if (PRE) { BO_LOAD_B(knext, bn); }                                               \
@@ -435,12 +450,16 @@ __global__ __launch_bounds__(256, 2) void post_partials_kernel(
   }
   int t = 0;
   if (cross) {
+    // the cross term's steps are those with k >= c0: the last ones ascending,
+    // the first ones on a reversed walk
     const int tc = min(nsteps, c0 / PK);
-    for (; t < tc; ++t) BO_KSTEP(, )
-    for (; t < nsteps; ++t)
-      BO_KSTEP(BO_LOAD_Q(kbeg + t * PK),
+    const int t0 = rev ? 0 : tc, t1 = rev ? nsteps - tc : nsteps;
+    for (; t < t0; ++t) BO_KSTEP(, )
+    for (; t < t1; ++t)
+      BO_KSTEP(BO_LOAD_Q(kfirst + t * kdir),
                accx[0] = mfma_f64(qa[ks], b[0], accx[0]);
                accx[1] = mfma_f64(qa[ks], b[1], accx[1]);)
+    for (; t < nsteps; ++t) BO_KSTEP(, )
   } else {
     for (; t < nsteps; ++t) BO_KSTEP(, )
   }

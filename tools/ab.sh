@@ -31,5 +31,24 @@ for r in $(seq 1 ${R:-2}); do
     echo "$VAR=$v round $r: $(tail -1 $O/${v}_$r.log | cut -c1-160)"
   done
 done
+# PMC=1: one FETCH_SIZE / WRITE_SIZE pass per variant (PMC_CMD, default the
+# measured command), summarised per variant by tools/pmc_summary.py
+if [ "${PMC:-0}" = 1 ]; then
+  export TMPDIR=/tmp
+  if [ -n "$PMC_CMD" ]; then PC=($PMC_CMD); else PC=("$@"); fi
+  for v in $VALS; do
+    for c in FETCH_SIZE WRITE_SIZE; do
+      if [ "$VAR" = LIB ]; then
+        cp ab_libs/lib$v.so botorch_amd/libbotorch_amd.so
+        timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc_${v}_$c -o run -- "${PC[@]}" > $O/pmc_${v}_$c.log 2>&1 || exit 1
+      else
+        env $VAR=$v timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc_${v}_$c -o run -- "${PC[@]}" > $O/pmc_${v}_$c.log 2>&1 || exit 1
+      fi
+    done
+    python3 tools/pmc_summary.py $O/pmc_$v.json $O/pmc_${v}_FETCH_SIZE $O/pmc_${v}_WRITE_SIZE > $O/pmc_$v.txt 2>&1 || exit 1
+    find $O/pmc_${v}_* -name 'run_counter_collection.csv' -size +2M -delete
+    echo "PMC $v: $(head -c 600 $O/pmc_$v.txt)"
+  done
+fi
 [ "$VAR" = LIB ] && cp ab_libs/libCUR.so botorch_amd/libbotorch_amd.so
 exit 0

@@ -16,7 +16,7 @@ from botorch_amd.sampling import SobolQMCNormalSampler  # noqa: E402
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 b = int(sys.argv[2]) if len(sys.argv) > 2 else bench.RESTARTS
 dev = torch.device("cuda", 0)
-Xtr, Ytr, Xc = bench.build_problem(dev, bench.RESTARTS)
+Xtr, Ytr, Xc = bench.build_problem(dev, max(b, bench.RESTARTS))
 m = SingleTaskGP(Xtr.to(dev), Ytr.to(dev))
 m.covar_module.lengthscale = torch.full((1, bench.D), bench.LENGTHSCALE, dtype=torch.float64)
 m.likelihood.noise = torch.tensor([bench.NOISE], dtype=torch.float64)
