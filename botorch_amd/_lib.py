@@ -124,6 +124,8 @@ _SIGNATURES = {
     "bo_lbfgsb_layout": (c_int, [_P]),
     "bo_lbfgsb_set_profile": (c_int, [_P, c_int]),
     "bo_lbfgsb_set_staging": (c_int, [c_int]),
+    "bo_lbfgsb_set_grid": (c_int, [c_int]),
+    "bo_lbfgsb_grid_launches": (c_int64, []),
     "bo_nd_partition_host": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, POINTER(c_int64), _P,
                                      _P, c_int]),
     "bo_nd_partition_alpha_host": (c_int, [_P, c_int64, c_int64, c_int, _P, c_double, c_int64,

@@ -278,6 +278,21 @@ extern "C" int bo_lbfgsb_set_staging(int on) {
   return BO_OK;
 }
 
+// The grid-wide kernel of a single wide restart (lbfgsb_grid.hip).
+bool lbfgsb_grid_fits(int n, int m);
+int lbfgsb_grid_launch(const bolb::Problem& P, double* xt, const double* ft, const double* gt,
+                       double* v, int* iv, double* ws, double* wy, double* mat, double* ds, int* is,
+                       void* stream);
+// 0: a single restart of at least GRID_MIN_N variables runs on the grid
+// kernel (where it fits); 1: every single restart that fits does; -1: never
+static std::atomic<int> g_lbfgsb_grid{0};
+constexpr int GRID_MIN_N = 2048;
+extern "C" int bo_lbfgsb_set_grid(int mode) {
+  BO_CHECK_ARG(mode >= -1 && mode <= 1, "bo_lbfgsb_set_grid: mode %d (-1, 0 or 1)", mode);
+  g_lbfgsb_grid.store(mode);
+  return BO_OK;
+}
+
 extern "C" int bo_lbfgsb_layout(int* out) {
   out[0] = bolb::V_COUNT;
   out[1] = bolb::IV_COUNT;
@@ -300,6 +315,10 @@ extern "C" int bo_lbfgsb_step(int B, int n, int m, int maxls, int maxiter, int m
   // profile only launches the buffer can hold (B x PROF_SLOTS clocks)
   unsigned long long* prof = lbfgsb_profile_for(B);
   bolb::Problem P{n, m, maxls, maxiter, maxfun, ftol, pgtol, lower, upper, prof};
+  // the joint problem (one restart of b q d variables) over the chip
+  const int gmode = g_lbfgsb_grid.load();
+  if (B == 1 && gmode >= 0 && (gmode == 1 || n >= GRID_MIN_N) && lbfgsb_grid_fits(n, m))
+    return lbfgsb_grid_launch(P, xt, ft, gt, v, iv, ws, wy, mat, ds, is, stream);
   const size_t bytes = staged_bytes(n, m);
   const int staged = bytes <= STAGE_LIMIT && !g_lbfgsb_unstaged.load();
   // one wave per restart; a restart wider than the wave's working set (the

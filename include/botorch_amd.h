@@ -607,6 +607,15 @@ int bo_lbfgsb_set_profile(unsigned long long* prof, int capacity);
 /* Timing aid: 0 keeps every restart's working set in HBM; 1 (default) stages it
  * in LDS for each launch when it fits (8 (10 + 2m) n + 8 n bytes <= ~40 KB). */
 int bo_lbfgsb_set_staging(int on);
+/* Route of a single restart (B == 1, the joint problem of
+ * gen_candidates_device(joint=True)): 0 (default) runs n >= 2048 on the
+ * grid-wide kernel (one workgroup per 256 variables, the S / Y ring in LDS;
+ * n <= 16384 and maxcor small enough for its LDS), 1 every single restart
+ * that fits, -1 never (the one-workgroup kernel).  Same state layout. */
+int bo_lbfgsb_set_grid(int mode);
+/* Number of grid-wide L-BFGS-B launches this process has made (tests assert
+ * the route). */
+int64_t bo_lbfgsb_grid_launches(void);
 
 /* HOST function (plain host pointers; no GPU involved): exact non-dominated
  * box decompositions of S point sets Y (S x n x m, maximisation) w.r.t. ref (m),

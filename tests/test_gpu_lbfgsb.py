@@ -279,3 +279,146 @@ def test_gen_candidates_device_joint_equals_scipy(b):
     torch.testing.assert_close(cd, cs, atol=1e-6, rtol=0)
     torch.testing.assert_close(vd, vs, atol=1e-10, rtol=1e-7)
     assert float(vs.max()) > 0
+
+
+# ---- the grid-wide kernel of a single restart (csrc/lbfgsb_grid.hip) --------
+class _grid:
+    """bo_lbfgsb_set_grid(mode) for the block; asserts the grid route ran
+    (mode 1) or did not (mode -1)."""
+
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        from botorch_amd._lib import lib
+        lib().bo_lbfgsb_set_grid(self.mode)
+        self.before = lib().bo_lbfgsb_grid_launches()
+        return self
+
+    def __exit__(self, *exc):
+        from botorch_amd._lib import lib
+        self.launches = lib().bo_lbfgsb_grid_launches() - self.before
+        lib().bo_lbfgsb_set_grid(0)
+        if exc[0] is None and self.mode != 0:
+            assert (self.launches > 0) == (self.mode == 1), (self.mode, self.launches)
+
+
+@pytest.mark.parametrize("q", [50, 200, 300, 700])
+def test_grid_kernel_trial_points_equal_scipy(q):
+    """The grid route (one workgroup per 256 variables: n = 300 / 1200 / 1800 /
+    4200 on 2 / 5 / 8 / 17 workgroups) on one Hartmann q-batch: scipy's trial
+    points in scipy's order (the opening 25), its final value."""
+    n = 6 * q
+    x0 = np.random.default_rng(q).uniform(0, 1, n)
+    lo, hi = np.zeros(n), np.ones(n)
+    fg = _hartmann_batch(q)
+    with _grid(1):
+        trials, x, f, status, nit = _drive([fg], x0[None], lo, hi, maxiter=60)
+    sp, res = scipy_trials(fg, x0, list(zip(lo, hi)), maxiter=60)
+    k = min(25, len(sp))
+    assert len(trials[0]) >= k
+    for i in range(k):
+        np.testing.assert_allclose(trials[0][i], sp[i], atol=1e-9, rtol=0, err_msg=f"trial {i}")
+    np.testing.assert_allclose(f[0], res.fun, rtol=1e-7, atol=1e-9)
+
+
+def test_grid_kernel_long_runs_equal_scipy():
+    """The grid route on one workgroup: the box Rosenbrock run (active upper
+    bounds, history wrap-around, 44 evaluations), the unconstrained branch and
+    fixed variables -- whole runs equal scipy's."""
+    from tests.test_lbfgsb_cpu import _quad
+    rng = np.random.default_rng(0)
+    n = 10
+    x0 = rng.uniform(-1, 1, n)
+    lo, hi = np.full(n, -1.5), np.full(n, 0.8)
+    with _grid(1):
+        trials, x, f, status, nit = _drive([_rosen], x0[None], lo, hi)
+    sp, res = scipy_trials(_rosen, x0, list(zip(lo, hi)))
+    assert len(trials[0]) == len(sp) and nit[0] == res.nit and status[0] == 2
+    for a, b in zip(sp, trials[0]):
+        np.testing.assert_allclose(b, a, atol=1e-9, rtol=0)
+    np.testing.assert_allclose(x[0], res.x, atol=1e-10, rtol=0)
+    inf = np.full(10, np.inf)
+    x0 = rng.uniform(-1, 1, 10)
+    with _grid(1):
+        trials, x, f, status, nit = _drive([_rosen], x0[None], -inf, inf)
+    sp, res = scipy_trials(_rosen, x0, None)
+    assert len(trials[0]) == len(sp) and nit[0] == res.nit
+    for a, b in zip(sp[:50], trials[0][:50]):
+        np.testing.assert_allclose(b, a, atol=1e-9, rtol=0)
+    rng = np.random.default_rng(11)
+    M = rng.standard_normal((n, n))
+    A = M @ M.T + np.eye(n)
+    bb = rng.standard_normal(n) * 4
+    lo = np.array([0.3, 0.3, 0, 0, -np.inf, -np.inf, 0, -1, -np.inf, 0.5])
+    hi = np.array([0.3, 0.3, 1, 1, np.inf, 0.0, np.inf, 1, np.inf, 0.5])
+    x0 = np.clip(rng.uniform(-0.5, 0.5, n), lo, hi)
+    fg = _quad(A, bb)
+    with _grid(1):
+        trials, x, f, status, nit = _drive([fg], x0[None], lo, hi)
+    sp, res = scipy_trials(fg, x0, list(zip(lo, hi)))
+    assert len(trials[0]) == len(sp) and nit[0] == res.nit
+    np.testing.assert_allclose(x[0], res.x, atol=1e-10, rtol=0)
+    assert x[0][0] == 0.3 and x[0][1] == 0.3 and x[0][9] == 0.5
+
+
+def test_grid_kernel_maxcor_and_wide_multi_round_cauchy():
+    """maxcor 3 and 17 (ring wrap-around, the LDS limit) on a 2-workgroup
+    problem whose first Cauchy search walks many breakpoints (a linear
+    objective pushing every variable to a bound: more than one round of
+    published breakpoints), trial points and values equal scipy's."""
+    n = 400
+    rng = np.random.default_rng(5)
+    c = rng.standard_normal(n)
+    D = np.abs(rng.standard_normal(n)) * 0.05
+
+    def fg(x):
+        return float(c @ x + 0.5 * np.sum(D * x * x) + 0.25 * np.sum(x ** 4)), c + D * x + x ** 3
+
+    x0 = rng.uniform(-0.5, 0.5, n)
+    lo, hi = np.full(n, -0.6), np.full(n, 0.6)
+    for m in (3, 17):
+        with _grid(1):
+            trials, x, f, status, nit = _drive([fg], x0[None], lo, hi, m=m, maxiter=80)
+        sp, res = scipy_trials(fg, x0, list(zip(lo, hi)), maxcor=m, maxiter=80)
+        k = min(30, len(sp))
+        assert len(trials[0]) >= k
+        for i in range(k):
+            np.testing.assert_allclose(trials[0][i], sp[i], atol=1e-9, rtol=0,
+                                       err_msg=f"m={m} trial {i}")
+        np.testing.assert_allclose(f[0], res.fun, rtol=1e-9, atol=1e-10)
+
+
+@pytest.mark.parametrize("b,mode", [(32, 1), (64, 0)])
+def test_gen_candidates_device_joint_grid_equals_scipy(b, mode):
+    """joint=True on the grid route: b = 32 forced (1536 variables, 6
+    workgroups), b = 64 by default (3072 >= 2048: 12 workgroups) -- the
+    candidates and values of gen_candidates_scipy on the same initial
+    conditions."""
+    from botorch_amd.acquisition import qExpectedImprovement
+    from botorch_amd.models import SingleTaskGP
+    from botorch_amd.optim import (gen_batch_initial_conditions, gen_candidates_device,
+                                   gen_candidates_scipy)
+    from botorch_amd.sampling import SobolQMCNormalSampler
+    from botorch_amd.test_functions import Hartmann
+    from botorch_amd.utils_sampling import draw_sobol_samples
+    box = torch.stack([torch.zeros(6), torch.ones(6)]).to(torch.float64)
+    X = draw_sobol_samples(box, 1024, 1, seed=0).squeeze(1)
+    Y = Hartmann(negate=True)(X).unsqueeze(-1)
+    m = SingleTaskGP(X.to(DEV), Y.to(DEV))
+    m.covar_module.lengthscale = torch.full((1, 6), 0.5016, dtype=torch.float64)
+    m.likelihood.noise = torch.tensor([6.737947e-3], dtype=torch.float64)
+    m.eval()
+    acqf = qExpectedImprovement(m, float(Y.max()) - 0.3,
+                                sampler=SobolQMCNormalSampler(torch.Size([256]), seed=0))
+    bounds = box.to(DEV)
+    ics = gen_batch_initial_conditions(acqf, bounds, q=8, num_restarts=b, raw_samples=4 * b,
+                                       options={"seed": 3})
+    opts = {"maxiter": 100}
+    cs, vs = gen_candidates_scipy(ics, acqf, bounds[0], bounds[1], options=opts)
+    with _grid(1 if mode == 1 else 0) as gr:
+        cd, vd = gen_candidates_device(ics, acqf, bounds[0], bounds[1],
+                                       options={**opts, "joint": True})
+    assert gr.launches == gen_candidates_device.last_evals
+    torch.testing.assert_close(cd, cs, atol=1e-6, rtol=0)
+    torch.testing.assert_close(vd, vs, atol=1e-10, rtol=1e-7)
