@@ -52,6 +52,18 @@
 #define BO_HD __device__ __attribute__((always_inline))
 #include "lbfgsb_core.h"
 
+// BO_GRID_SUBPROF (development builds): the profile slots time sub-phases
+// instead -- 0 load + first exchange, 1 Cauchy pass + exchange, 2 bmv + M,
+// 3 breakpoint selection + exchange, 4 merge + walk, 5 formk products +
+// exchange, 6 LEL^T + cmprlb + subsm, 7 update, line-search start, stores.
+#ifdef BO_GRID_SUBPROF
+#define SUBTICK(p) tick(p)
+#define PHTICK(p)
+#else
+#define SUBTICK(p)
+#define PHTICK(p) tick(p)
+#endif
+
 namespace {
 
 using namespace bolb;
@@ -131,6 +143,126 @@ BO_HD void wave_argmin(double& v, int& i) {
       i = oi;
     }
   }
+}
+
+// ---- the 2m x 2m algebra on one wave (lane = row or column index) -----------
+// lbfgsb_core.h runs these on one lane, where every step waits on an LDS
+// round trip and many on an fp64 division: ~10 us per bmv, ~5-10 per dpofa
+// at col = 10.  Here they are column- / row-parallel over the wave's lanes
+// (col <= MMAX, 2 col <= 40 < 64): the same operations on the same values,
+// in another summation order (the triangular solves and the Cholesky update
+// right-looking); results are uniform or land in LDS.  Wave 0 only; the
+// caller's barrier publishes them.
+BO_HD double readlane_d(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), l);
+  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// upper Cholesky A = R^T R of the n x n leading block (column-major, ld) in
+// place, LINPACK dpofa's result: 0 or the failing column + 1 (uniform)
+BO_HD int dpofa_w(double* a, int ld, int n, int lane) {
+  for (int k = 0; k < n; ++k) {
+    const double d = a[k + k * ld];
+    if (d <= 0.0) return k + 1;
+    const double r = sqrt(d);
+    double akj = 0.0;
+    if (lane > k && lane < n) akj = a[k + lane * ld] / r;
+    __builtin_amdgcn_wave_barrier();
+    if (lane == k) a[k + k * ld] = r;
+    if (lane > k && lane < n) a[k + lane * ld] = akj;
+    __builtin_amdgcn_wave_barrier();
+    if (lane > k && lane < n)  // a[i][j] -= R[k][i] R[k][j], k < i <= j (lane j)
+      for (int i = k + 1; i <= lane; ++i) a[i + lane * ld] -= a[k + i * ld] * akj;
+    __builtin_amdgcn_wave_barrier();
+  }
+  return 0;
+}
+// first zero on T's diagonal + 1, or 0 (uniform)
+BO_HD int zero_diag_w(const double* t, int ld, int n, int lane) {
+  const unsigned long long z = __ballot(lane < n && t[lane + lane * ld] == 0.0);
+  return z ? __builtin_ffsll((long long)z) : 0;
+}
+// T^T x = b (T upper; dtrsl job 11), b in LDS, overwritten by x
+BO_HD int dtrsl_t_w(const double* t, int ld, int n, double* b, int lane) {
+  const int info = zero_diag_w(t, ld, n, lane);
+  if (info) return info;
+  double bj = lane < n ? b[lane] : 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double xi = readlane_d(bj / t[i + i * ld], i);
+    if (lane == i) bj = xi;
+    if (lane > i && lane < n) bj -= t[i + lane * ld] * xi;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < n) b[lane] = bj;
+  __builtin_amdgcn_wave_barrier();
+  return 0;
+}
+// T x = b (T upper; dtrsl job 01)
+BO_HD int dtrsl_n_w(const double* t, int ld, int n, double* b, int lane) {
+  const int info = zero_diag_w(t, ld, n, lane);
+  if (info) return info;
+  double bj = lane < n ? b[lane] : 0.0;
+  for (int j = n - 1; j >= 0; --j) {
+    const double xj = readlane_d(bj / t[j + j * ld], j);
+    if (lane == j) bj = xj;
+    if (lane < j) bj -= t[lane + j * ld] * xj;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < n) b[lane] = bj;
+  __builtin_amdgcn_wave_barrier();
+  return 0;
+}
+// bmv: p = M v for the 2col x 2col middle matrix (lbfgsb_core.h bmv; lane i
+// does row i's sums in the serial order, the two solves are dtrsl_*_w)
+BO_HD int bmv_w(const double* sy, const double* wt, int col, const double* v, double* p, int lane) {
+  if (col == 0) return 0;
+  if (lane < col) {
+    if (lane == 0) {
+      p[col] = v[col];
+    } else {
+      double sum = 0.0;
+      for (int k = 0; k < lane; ++k) sum += sy[lane + k * MMAX] * v[k] / sy[k + k * MMAX];
+      p[col + lane] = v[col + lane] + sum;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  int info = dtrsl_t_w(wt, MMAX, col, p + col, lane);
+  if (info) return info;
+  if (lane < col) p[lane] = v[lane] / sqrt(sy[lane + lane * MMAX]);
+  __builtin_amdgcn_wave_barrier();
+  info = dtrsl_n_w(wt, MMAX, col, p + col, lane);
+  if (info) return info;
+  if (lane < col) {
+    const double sii = sy[lane + lane * MMAX];
+    double pi = -p[lane] / sqrt(sii);
+    double sum = 0.0;
+    for (int k = lane + 1; k < col; ++k) sum += sy[k + lane * MMAX] * p[col + k] / sii;
+    p[lane] = pi + sum;
+  }
+  __builtin_amdgcn_wave_barrier();
+  return 0;
+}
+// formt: WT = chol(theta SS + L D^-1 L^T), entries (i, j), i <= j, over the lanes
+BO_HD int formt_w(double* wt, const double* sy, const double* ss, int col, double theta, int lane) {
+  const int np = col * (col + 1) / 2;
+  for (int e = lane; e < np; e += 64) {
+    int i = 0, q = e;  // e -> (i, j), i <= j, row-major over i
+    while (q >= col - i) {
+      q -= col - i;
+      ++i;
+    }
+    const int j = i + q;
+    if (i == 0) {
+      wt[0 + j * MMAX] = theta * ss[0 + j * MMAX];
+    } else {
+      double ddum = 0.0;
+      for (int k = 0; k < i; ++k) ddum += sy[i + k * MMAX] * sy[j + k * MMAX] / sy[k + k * MMAX];
+      wt[i + j * MMAX] = ddum + theta * ss[i + j * MMAX];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  return dpofa_w(wt, MMAX, col, lane) ? -3 : 0;
 }
 
 struct CauchyState {  // the breakpoint walk's scalars, handed from wave 0 to the workgroup
@@ -476,6 +608,7 @@ struct GStep {
         mode = 0;
       });
     if (!greduce(4 + 2 * col, 1u << 3)) return 0;
+    SUBTICK(1);
     f1 = red[0];
     const int nbrk = (int)red[1];
     const int nfr = (int)red[2];
@@ -492,17 +625,16 @@ struct GStep {
       __syncthreads();
       return 0;
     }
-    if (tid == 0) {
-      for (int j = 0; j < 2 * col; ++j) S.c[j] = 0.0;
-      double f2 = -theta * f1;
-      int info = 0;
-      if (col > 0) {
-        info = bmv(S.sy, S.wt, col, S.p, S.v);
-        if (!info)
+    if (wave == 0) {
+      if (lane < 2 * col) S.c[lane] = 0.0;
+      const int info = col > 0 ? bmv_w(S.sy, S.wt, col, S.p, S.v, lane) : 0;
+      if (lane == 0) {
+        double f2 = -theta * f1;
+        if (col > 0 && !info)
           for (int j = 0; j < 2 * col; ++j) f2 -= S.v[j] * S.p[j];
+        S.t0 = f2;
+        S.k0 = info;
       }
-      S.t0 = f2;
-      S.k0 = info;
     }
     __syncthreads();
     if (S.k0) return S.k0;
@@ -527,6 +659,7 @@ struct GStep {
         bmv(S.sy, S.wt, col, e, Mx + lane * M2);
       }
       __syncthreads();
+      SUBTICK(2);
       const int PW = 3 + 2 * col;
       while (!cs->done) {
         if (!breakpoint_round(col, theta, nbrk, bnded, f2_org, PW, Mx)) return 0;
@@ -608,6 +741,7 @@ struct GStep {
       __syncthreads();
     }
     if (!publish_meet(rec, HW + KB * PW)) return false;
+    SUBTICK(3);
     // (2) the headers of all workgroups
     double* hdr = red + R_HDR;
     gather(hdr, 0, HW);
@@ -734,6 +868,15 @@ struct GStep {
         break;
       }
       if (!done && final_list) done = 1;  // no breakpoint left
+      // profiling launches (tools/prof_lbfgsb_joint.py): the freev slot, idle
+      // on this route, counts the breakpoints walked (x 100 ticks), the store
+      // slot the rounds
+#ifndef BO_GRID_SUBPROF
+      if (prof && lane == 0) {
+        prof[2] += 100ull * (unsigned long long)M;
+        prof[7] += 100ull;
+      }
+#endif
       if (li) {
         S.p[lane] = p;
         S.c[lane] = c;
@@ -750,6 +893,7 @@ struct GStep {
       }
     }
     __syncthreads();
+    SUBTICK(4);
     return true;
   }
 
@@ -837,6 +981,7 @@ struct GStep {
     if (tid == 0) red[0] = (double)nfl;
     __syncthreads();
     if (!greduce(1 + ntri)) return 0;
+    SUBTICK(5);
     const int nfree = (int)red[0];
     if (tid == 0) S.i[I_NFREE] = nfree;
     if (nfree == 0) {
@@ -866,7 +1011,10 @@ struct GStep {
     // LEL^T (lbfgsb_core.h formk): the upper-left Cholesky, the col right-hand
     // columns' solves and the lower-right block's products over the threads,
     // then the lower-right Cholesky
-    if (tid == 0) S.k0 = dpofa(S.wn, M2, col) ? -1 : 0;
+    if (wave == 0) {
+      const int f = dpofa_w(S.wn, M2, col, lane);
+      if (lane == 0) S.k0 = f ? -1 : 0;
+    }
     __syncthreads();
     if (S.k0 == 0) {
       for (int js = col + tid; js < 2 * col; js += GT) dtrsl_t(S.wn, M2, col, S.wn + js * M2);
@@ -885,7 +1033,10 @@ struct GStep {
         S.wn[is + js * M2] += s;
       }
       __syncthreads();
-      if (tid == 0 && dpofa(S.wn + col + col * M2, M2, col)) S.k0 = -2;
+      if (wave == 0) {
+        const int f = dpofa_w(S.wn + col + col * M2, M2, col, lane);
+        if (lane == 0 && f) S.k0 = -2;
+      }
     }
     __syncthreads();
     return S.k0;
@@ -901,7 +1052,10 @@ struct GStep {
       __syncthreads();
       return 0;
     }
-    if (tid == 0) S.k0 = bmv(S.sy, S.wt, col, S.c, S.v) ? -8 : 0;
+    if (wave == 0) {
+      const int f = bmv_w(S.sy, S.wt, col, S.c, S.v, lane);
+      if (lane == 0) S.k0 = f ? -8 : 0;
+    }
     __syncthreads();
     if (S.k0) return S.k0;
     if (own() && is_free(tid)) {
@@ -928,17 +1082,19 @@ struct GStep {
       mode = 1;
     });
     if (!greduce(2 * col)) return 0;
-    if (tid == 0) {
-      for (int j = 0; j < col; ++j) {
-        S.wv[j] = red[j];
-        S.wv[col + j] = theta * red[col + j];
+    if (wave == 0) {
+      if (lane < col) {
+        S.wv[lane] = red[lane];
+        S.wv[col + lane] = theta * red[col + lane];
       }
-      int info = dtrsl_t(S.wn, M2, 2 * col, S.wv);
+      __builtin_amdgcn_wave_barrier();
+      int info = dtrsl_t_w(S.wn, M2, 2 * col, S.wv, lane);
       if (!info) {
-        for (int i = 0; i < col; ++i) S.wv[i] = -S.wv[i];
-        info = dtrsl_n(S.wn, M2, 2 * col, S.wv);
+        if (lane < col) S.wv[lane] = -S.wv[lane];
+        __builtin_amdgcn_wave_barrier();
+        info = dtrsl_n_w(S.wn, M2, 2 * col, S.wv, lane);
       }
-      S.k0 = info;
+      if (lane == 0) S.k0 = info;
     }
     __syncthreads();
     if (S.k0) return S.k0;
@@ -1034,26 +1190,26 @@ struct GStep {
         if (tid == 0) S.i[I_NFREE] = n;
         __syncthreads();
       } else {
-        tick(6);
+        PHTICK(6);
         const int info = cauchy();
-        tick(1);
+        PHTICK(1);
         if (aborted) return;
         if (info) {
           refresh();
           continue;
         }
-        tick(2);
+        PHTICK(2);
       }
       if (S.i[I_COL] != 0) {
         bool skip = false;
         int info = formk(skip);
-        tick(3);
+        PHTICK(3);
         if (aborted) return;
         if (!info && !skip) {
           info = cmprlb(unconstrained);
-          tick(4);
+          PHTICK(4);
           if (!info) info = subsm();
-          tick(5);
+          PHTICK(5);
           if (aborted) return;
         }
         if (info) {
@@ -1061,6 +1217,7 @@ struct GStep {
           continue;
         }
       }
+      SUBTICK(6);
       // lnsrlb (first entry): |d|^2, the largest feasible step, g.d in one exchange
       const int k = tid;
       double sm = BIG, dtdp = 0.0, gdp = 0.0;
@@ -1125,6 +1282,7 @@ struct GStep {
       }
       __syncthreads();
       write_trial();
+      SUBTICK(7);
       return;
     }
     stop(ST_ABNORMAL);  // not reached: a refreshed memory cannot fail again
@@ -1132,6 +1290,7 @@ struct GStep {
 
   // ---- matupd + formt after an accepted step ----
   BO_HD void update() {
+    SUBTICK(7);
     double* r = V(L_R);
     double* dd = V(L_D);
     const int k = tid;
@@ -1189,18 +1348,24 @@ struct GStep {
       }
     });
     if (!greduce(1 + 2 * (col - 1))) return;
-    if (tid == 0) {
-      S.d[D_THETA] = red[0] / dr;
-      for (int j = 0; j < col - 1; ++j) {
-        S.sy[(col - 1) + j * MMAX] = red[1 + j];
-        S.ss[j + (col - 1) * MMAX] = red[col + j];
+    if (wave == 0) {
+      const double theta = red[0] / dr;
+      if (lane < col - 1) {
+        S.sy[(col - 1) + lane * MMAX] = red[1 + lane];
+        S.ss[lane + (col - 1) * MMAX] = red[col + lane];
       }
-      const double dtd = S.d[D_DTD];
-      S.ss[(col - 1) + (col - 1) * MMAX] = (stp == 1.0) ? dtd : stp * stp * dtd;
-      S.sy[(col - 1) + (col - 1) * MMAX] = dr;
-      S.k0 = formt(S.wt, S.sy, S.ss, col, S.d[D_THETA]);
+      if (lane == 0) {
+        S.d[D_THETA] = theta;
+        const double dtd = S.d[D_DTD];
+        S.ss[(col - 1) + (col - 1) * MMAX] = (stp == 1.0) ? dtd : stp * stp * dtd;
+        S.sy[(col - 1) + (col - 1) * MMAX] = dr;
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int f = formt_w(S.wt, S.sy, S.ss, col, theta, lane);
+      if (lane == 0) S.k0 = f;
     }
     __syncthreads();
+    SUBTICK(7);
     if (S.k0) refresh();
   }
 
@@ -1265,7 +1430,8 @@ struct GStep {
       cnstnd = red[1] > 0.0;
       boxed = red[2] > 0.0;
       const double gdv = red[3], sbv = red[4];
-      tick(0);
+      PHTICK(0);
+      SUBTICK(0);
       if (phase == PH_START) {
         if (tid == 0) {
           for (int j = 0; j < DSLOTS; ++j) S.d[j] = 0.0;
@@ -1341,7 +1507,7 @@ struct GStep {
       }
     }
     __syncthreads();
-    tick(6);
+    PHTICK(6);
     if (tid == 0) *sflag = (aborted || ld_u32(gm.cnt + 2)) ? 1 : 0;
     __syncthreads();
     if (*sflag) {  // the grid did not meet: keep the iterate, report an error
@@ -1375,7 +1541,8 @@ struct GStep {
         R.mat[2 * MMAX * MMAX + j] = S.wt[j];
       }
     }
-    tick(7);
+    PHTICK(7);
+    SUBTICK(7);
   }
 };
 

@@ -3,8 +3,9 @@
 ONE restart of n = b q d on a 4-wave workgroup) inside C2 / C3 optimize_acqf,
 next to the per-restart run and scipy: where one bo_lbfgsb_step launch spends
 its time (us per launch; load, cauchy, freev, formk, cmprlb, subsm, line
-search + update, store), and the number of breakpoints the Cauchy search
-walked is not counted -- the cauchy phase's share says whether it matters."""
+search + update, store).  On the grid route (n >= 2048) the freev column is
+the number of Cauchy breakpoints walked per launch and the store column adds
+the breakpoint rounds per launch to its ~1 us."""
 import os
 import sys
 import time
