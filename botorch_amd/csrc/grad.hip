@@ -14,6 +14,8 @@
 // The model caches carry no gradient (detach_test_caches, botorch/models/
 // utils/assorted.py:286-298), so nothing flows to L^{-1} or alpha.
 #include "common.h"
+
+#include <algorithm>
 #include "logred.h"
 
 namespace {
@@ -336,7 +338,8 @@ __global__ __launch_bounds__(THREADS) void qmc_log_backward_kernel(
 
 static_assert(THREADS == QMAX * QMAX, "post_backward: one G entry per thread");
 
-// dX for one t-batch per workgroup.  The G W term is a (16 x 16) x (16 x 16k)
+// dX for one t-batch per workgroup (training points [kb, ke): all of them, or
+// one split of several -- see post_backward_kernel).  The G W term is a (16 x 16) x (16 x 16k)
 // product per block of 16 training points, so each wave runs it on the matrix
 // cores: A = G[a][j] (fixed for the kernel, in registers), B = W[j][k] (the
 // t-batch's 16 W rows, 128-B row segments, each element read once), and the
@@ -351,7 +354,8 @@ __device__ __forceinline__ void post_backward_body(
     const double* __restrict__ dmean, const double* __restrict__ dcov,
     const double* __restrict__ E, int64_t lde,
     const double* __restrict__ ls, double outputscale, double ystd, int d, int accumulate,
-    double* __restrict__ dX, int wkm) {
+    double* __restrict__ dX, int wkm, int kb = 0, int ke = -1, double* __restrict__ part = nullptr) {
+  if (ke < 0) ke = n;
   __shared__ double G[QMAX][QMAX + 1];
   __shared__ double dmu[QMAX];
   __shared__ double xs[QMAX][DP];
@@ -392,7 +396,7 @@ __device__ __forceinline__ void post_backward_body(
   // second one's points past n are masked like any ragged block
   auto block = [&](int k0) {
     const int k = k0 + kc;
-    const bool kv = k < n;
+    const bool kv = k < ke;
     v4d c = v4d_zero();
     if (W) {
 #pragma unroll
@@ -425,7 +429,7 @@ __device__ __forceinline__ void post_backward_body(
     }
   };
   constexpr int KSTRIDE = 16 * (THREADS / 64);
-  for (int k0 = wave * 16; k0 < n; k0 += 2 * KSTRIDE) {  // wave-uniform trip count
+  for (int k0 = kb + wave * 16; k0 < ke; k0 += 2 * KSTRIDE) {  // wave-uniform trip count
     block(k0);
     block(k0 + KSTRIDE);
   }
@@ -448,8 +452,8 @@ __device__ __forceinline__ void post_backward_body(
 #pragma unroll
     for (int w = 0; w < THREADS / 64; ++w) s += red[w][a][t];
     // K** terms: Sigma*[a][c] = K**(a, c) - ..., d K** = d Sigma* (c != a; the
-    // diagonal is the constant outputscale).
-    if (dcov) {
+    // diagonal is the constant outputscale) -- once, in the first split.
+    if (dcov && kb == 0) {
       for (int c = 0; c < q; ++c) {
         if (c == a) continue;
         double d2 = 0.0;
@@ -461,11 +465,20 @@ __device__ __forceinline__ void post_backward_body(
         s = fma(G[a][c] * dkernel_factor<KIND>(d2, outputscale), xs[a][t] - xs[c][t], s);
       }
     }
-    double* o = dX + ((int64_t)b * q + a) * d + t;
-    *o = accumulate ? *o + s / ls[t] : s / ls[t];
+    if (part) {  // one split's unscaled sum (post_backward_reduce_kernel finishes it)
+      part[((int64_t)b * q + a) * d + t] = s;
+    } else {
+      double* o = dX + ((int64_t)b * q + a) * d + t;
+      *o = accumulate ? *o + s / ls[t] : s / ls[t];
+    }
   }
 }
 
+// grid (B, NS): with NS > 1 workgroup (b, s) takes the training points
+// [s chunk, (s + 1) chunk) of t-batch b and writes its unscaled sums to
+// part + s B q d; post_backward_reduce_kernel adds the NS splits in order.  A
+// few t-batches (the tail of a compacted optimiser run: B = 2) otherwise left
+// B workgroups walking all n points on a 256-CU chip (120 us at n = 4096).
 template <int KIND, int ND>
 __global__ __launch_bounds__(THREADS) void post_backward_kernel(
     int q, int Qp, const double* __restrict__ Xq, const double* __restrict__ Xt, int n,
@@ -473,9 +486,25 @@ __global__ __launch_bounds__(THREADS) void post_backward_kernel(
     const double* __restrict__ dmean, const double* __restrict__ dcov,
     const double* __restrict__ E, int64_t lde,
     const double* __restrict__ ls, double outputscale, double ystd, int d, int accumulate,
-    double* __restrict__ dX, int wkm) {
+    double* __restrict__ dX, int wkm, int chunk, double* __restrict__ part) {
+  const int kb = blockIdx.y * chunk;
+  const int ke = min(n, kb + chunk);
   post_backward_body<KIND, ND>(blockIdx.x, q, Qp, Xq, Xt, n, W, ldw, alpha, dmean, dcov, E, lde, ls,
-                               outputscale, ystd, d, accumulate, dX, wkm);
+                               outputscale, ystd, d, accumulate, dX, wkm, kb, ke,
+                               part ? part + (int64_t)blockIdx.y * gridDim.x * q * d : nullptr);
+}
+
+// dX (+)= (sum over the NS splits, in split order) / lengthscale
+__global__ __launch_bounds__(256) void post_backward_reduce_kernel(int ns, int64_t total, int d,
+                                                                    const double* __restrict__ part,
+                                                                    const double* __restrict__ ls,
+                                                                    int accumulate, double* __restrict__ dX) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  double s = part[e];
+  for (int j = 1; j < ns; ++j) s += part[(int64_t)j * total + e];
+  const double v = s / ls[e % d];
+  dX[e] = accumulate ? dX[e] + v : v;
 }
 
 // Several posterior backward passes of one (B, q, d, kind) in ONE launch
@@ -633,11 +662,26 @@ extern "C" int bo_post_backward(int kind, int B, int q, int d, const double* Xq,
   int Qp = 1;
   while (Qp < q) Qp *= 2;
   hipStream_t st = as_stream(stream);
-#define BO_PB(KIND, ND)                                                                      \
-  post_backward_kernel<KIND, ND><<<B, THREADS, 0, st>>>(q, Qp, Xq, Xt_scaled, (int)n, W, ldw, \
-                                                        alpha, dmean, dcov, E, lde,           \
-                                                        lengthscale, outputscale, ystd, d,    \
-                                                        accumulate, dX, w_kmajor)
+  // splits of >= 128 training points (one trip of the body's loop) until B NS
+  // reaches ~256 workgroups; NS = 1 (B >= 256, or n <= 128) is the one-pass
+  // kernel as before, bit for bit
+  const int nchunks = (int)std::max<int64_t>(1, ceil_div(n, 128));
+  const int ns = (int)std::min<int64_t>(nchunks, std::max<int64_t>(1, ceil_div(256, B)));
+  const int chunk = (int)(ceil_div(nchunks, ns) * 128);
+  const int ns_used = std::max(1, (int)ceil_div(n, chunk));
+  double* part = nullptr;
+  if (ns_used > 1) {
+    keep_pool_warm();
+    BO_HIP(hipMallocAsync(reinterpret_cast<void**>(&part),
+                          sizeof(double) * (size_t)ns_used * B * q * d, st));
+  }
+  const dim3 grid((unsigned)B, (unsigned)ns_used);
+#define BO_PB(KIND, ND)                                                                        \
+  post_backward_kernel<KIND, ND><<<grid, THREADS, 0, st>>>(q, Qp, Xq, Xt_scaled, (int)n, W, ldw, \
+                                                           alpha, dmean, dcov, E, lde,           \
+                                                           lengthscale, outputscale, ystd, d,    \
+                                                           accumulate, dX, w_kmajor,             \
+                                                           ns_used > 1 ? chunk : (int)n, part)
   if (kind == BO_RBF) {
     if (d == 6) BO_PB(BO_RBF, 6); else BO_PB(BO_RBF, 8);
   } else {
@@ -645,6 +689,13 @@ extern "C" int bo_post_backward(int kind, int B, int q, int d, const double* Xq,
   }
 #undef BO_PB
   BO_LAUNCH_CHECK();
+  if (part) {
+    const int64_t total = (int64_t)B * q * d;
+    post_backward_reduce_kernel<<<(unsigned)ceil_div(total, 256), 256, 0, st>>>(
+        ns_used, total, d, part, lengthscale, accumulate, dX);
+    BO_LAUNCH_CHECK();
+    BO_HIP(hipFreeAsync(part, st));
+  }
   return BO_OK;
 }
 
