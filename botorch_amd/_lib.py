@@ -117,6 +117,7 @@ _SIGNATURES = {
                                c_int, c_int, _P, _P]),
     "bo_mc_reduce": (c_int, [c_int, c_int, c_int, _P, c_double, _P, _P, _P]),
     "bo_sobol_normal": (c_int, [_P, _P, c_int, c_int64, c_int64, c_int, _P, _P]),
+    "bo_sobol_scramble": (c_int, [c_int, _P, _P, _P, _P, _P]),
     "bo_lbfgs_step": (c_int, [c_int, c_int, c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, _P, _P, _P, _P, c_double, c_double, c_double, c_double, _P]),
     "bo_lbfgsb_step": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_double, c_double, _P,

@@ -135,7 +135,57 @@ __global__ void sobol_box_kernel(const int64_t* __restrict__ state,
   out[idx] = __dadd_rn(lower[t], __dmul_rn(range[t], u));
 }
 
+// Owen-type scramble of the direction numbers, as SobolEngine(scramble=True)
+// applies it at construction (torch/quasirandom.py _scramble +
+// torch._sobol_engine_scramble_): with L_d the random lower-triangular 30 x 30
+// bit matrix of dimension d (unit diagonal) and row p packed MSB-first
+// (bit 29 - k = L_d[p][k]),
+//   state[d][j] bit (29 - p) = parity(L_d[p] & state0[d][j]),
+//   shift[d] = sum_k s[d][k] 2^k.
+// `bits` holds the engine's two randint draws in order: the dim x 30 shift bits,
+// then the dim x 30 x 30 matrix bits (taken below/on the diagonal only).  One
+// workgroup scrambles SDIM dimensions: the packed rows go through LDS.
+constexpr int SDIM = 8;
+
+__global__ void __launch_bounds__(256) sobol_scramble_kernel(
+    int dim, const int64_t* __restrict__ state0, const uint8_t* __restrict__ bits,
+    int64_t* __restrict__ state, int64_t* __restrict__ shift) {
+  __shared__ unsigned rows[SDIM][MAXBIT];
+  const int t = threadIdx.x;
+  const int dl = t / MAXBIT, r = t % MAXBIT;
+  const int d = blockIdx.x * SDIM + dl;
+  const bool live = t < SDIM * MAXBIT && d < dim;
+  if (live) {
+    const uint8_t* row = bits + (int64_t)dim * MAXBIT + ((int64_t)d * MAXBIT + r) * MAXBIT;
+    unsigned packed = 1u << (MAXBIT - 1 - r);
+    for (int k = 0; k < r; ++k) packed |= (unsigned)(row[k] & 1) << (MAXBIT - 1 - k);
+    rows[dl][r] = packed;
+  }
+  __syncthreads();
+  if (!live) return;
+  const unsigned v = (unsigned)state0[(int64_t)d * MAXBIT + r];
+  unsigned out = 0;
+#pragma unroll
+  for (int p = 0; p < MAXBIT; ++p) out |= (unsigned)(__popc(rows[dl][p] & v) & 1) << (MAXBIT - 1 - p);
+  state[(int64_t)d * MAXBIT + r] = (int64_t)out;
+  if (r == 0) {
+    int64_t s = 0;
+    const uint8_t* sb = bits + (int64_t)d * MAXBIT;
+    for (int k = 0; k < MAXBIT; ++k) s |= (int64_t)(sb[k] & 1) << k;
+    shift[d] = s;
+  }
+}
+
 }  // namespace
+
+extern "C" int bo_sobol_scramble(int dim, const int64_t* state0, const uint8_t* bits,
+                                 int64_t* state, int64_t* shift, void* stream) {
+  BO_CHECK_ARG(dim > 0, "bo_sobol_scramble: bad dimension %d", dim);
+  sobol_scramble_kernel<<<(unsigned)ceil_div(dim, SDIM), 256, 0, as_stream(stream)>>>(
+      dim, state0, bits, state, shift);
+  BO_LAUNCH_CHECK();
+  return BO_OK;
+}
 
 extern "C" int bo_sobol_box(const int64_t* state, const int64_t* shift, int dim, int64_t n,
                             int64_t skip, int first_f32, const double* lower, const double* range,

@@ -778,17 +778,63 @@ def qmc_finalize_members(caches, pps, stats, mean: torch.Tensor, L: torch.Tensor
     return info, jit
 
 
-def sobol_engine_state(dim: int, seed: int):
+SOBOL_MAXBIT = 30  # torch.quasirandom.SobolEngine.MAXBIT
+
+
+@functools.lru_cache(maxsize=16)
+def _sobol_state0(dim: int, device: torch.device) -> torch.Tensor:
+    """Unscrambled direction numbers (dim x 30) on the device, once per dim."""
+    st = torch.zeros(dim, SOBOL_MAXBIT, dtype=torch.long)
+    torch._sobol_engine_initialize_state_(st, dim)
+    return st.to(device)
+
+
+def sobol_engine_state(dim: int, seed: Optional[int], device=None):
     """Scrambled direction numbers + digital shift of torch's SobolEngine
-    (the engine the reference's NormalQMCEngine wraps, sampling/qmc.py:56)."""
-    eng = SobolEngine(dimension=dim, scramble=True, seed=seed)
-    return eng.sobolstate.clone(), eng.shift.clone()
+    (the engine the reference's NormalQMCEngine wraps, sampling/qmc.py:56).
+
+    On a ROCm device the state is built there (bo_sobol_scramble): the
+    engine's own two draws from its seeded CPU generator -- shift bits, then the
+    lower-triangular matrix bits, drawn as uint8 (the same stream as the int64
+    draws) into one pinned buffer -- go over in one copy, and the scramble,
+    the engine's 30 x 30 bit-matrix products per dimension, runs in one launch
+    with the unscrambled direction numbers cached on the device.  Bit-identical
+    to SobolEngine(dim, scramble=True, seed) (tests/test_gpu_ops.py); the
+    engine itself spends ~30 ms of host time at dim 4096 (the baseline pruning
+    of every qNEI / qNEHVI construction)."""
+    if device is None or torch.device(device).type != "cuda":
+        eng = SobolEngine(dimension=dim, scramble=True, seed=seed)
+        return eng.sobolstate.clone(), eng.shift.clone()
+    if not 1 <= dim <= SobolEngine.MAXDIM:
+        raise ValueError(f"Supported range of dimensionality for SobolEngine is "
+                         f"[1, {SobolEngine.MAXDIM}]")
+    dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator()
+    if seed is not None:
+        g.manual_seed(seed)
+    else:
+        g.seed()
+    nb = dim * SOBOL_MAXBIT
+    host = torch.empty(nb * (1 + SOBOL_MAXBIT), dtype=torch.uint8, pin_memory=True)
+    torch.randint(2, (dim, SOBOL_MAXBIT), generator=g, dtype=torch.uint8,
+                  out=host[:nb].view(dim, SOBOL_MAXBIT))
+    torch.randint(2, (dim, SOBOL_MAXBIT, SOBOL_MAXBIT), generator=g, dtype=torch.uint8,
+                  out=host[nb:].view(dim, SOBOL_MAXBIT, SOBOL_MAXBIT))
+    bits = host.to(dev, non_blocking=True)
+    state0 = _sobol_state0(dim, dev)
+    state = torch.empty(dim, SOBOL_MAXBIT, dtype=torch.long, device=dev)
+    shift = torch.empty(dim, dtype=torch.long, device=dev)
+    check(lib().bo_sobol_scramble(dim, _p(state0), _p(bits), _p(state), _p(shift), _stream(dev)),
+          "sobol_scramble")
+    return state, shift
 
 
 def sobol_normal(dim: int, n: int, seed: int, device, skip: int = 0) -> torch.Tensor:
     """n x dim scrambled-Sobol N(0,1) samples generated on the device."""
     from . import ops  # noqa: F401  (torch.ops.bo registration)
-    state, shift = sobol_engine_state(dim, seed)
+    state, shift = sobol_engine_state(dim, seed, device)
     first_f32 = torch.get_default_dtype() == torch.float32
     return torch.ops.bo.sobol_normal(state.to(device), shift.to(device), n, skip, first_f32)
 
@@ -798,8 +844,7 @@ def sobol_box(bounds: torch.Tensor, n: int, q: int, seed: Optional[int]) -> torc
     device), bit-identical to draw_sobol_samples (botorch/utils/sampling.py:66-105)."""
     dev = bounds.device
     d = bounds.shape[-1]
-    state, shift = sobol_engine_state(q * d, seed)
-    state, shift = state.to(dev), shift.to(dev)  # keep alive across the launch
+    state, shift = sobol_engine_state(q * d, seed, dev)  # kept alive across the launch
     lower = bounds[0].to(torch.float64).contiguous()
     rng = (bounds[1] - bounds[0]).to(torch.float64).contiguous()
     out = torch.empty(n, q, d, dtype=torch.float64, device=dev)

@@ -562,6 +562,16 @@ int bo_mc_reduce(int S, int B, int q, const double* samples, double best_f,
 int bo_sobol_normal(const int64_t* state, const int64_t* shift, int dim, int64_t n,
                     int64_t skip, int first_f32, double* out, void* stream);
 
+/* The scrambled engine state itself: state (dim x 30) and shift (dim) of
+ * SobolEngine(dim, scramble=True, seed) from state0 (dim x 30, the unscrambled
+ * direction numbers, torch._sobol_engine_initialize_state_) and bits (uint8,
+ * 0/1): the engine's two draws from its seeded generator, in order -- dim x 30
+ * shift bits, then dim x 30 x 30 matrix bits.  Replaces SobolEngine._scramble
+ * (torch/quasirandom.py; torch._sobol_engine_scramble_), which the reference's
+ * samplers run at every construction (sampling/qmc.py:56). */
+int bo_sobol_scramble(int dim, const int64_t* state0, const uint8_t* bits, int64_t* state,
+                      int64_t* shift, void* stream);
+
 /* One function evaluation of the device-resident multi-start projected L-BFGS
  * (replaces scipy L-BFGS-B in gen_candidates_scipy, botorch/generation/gen.py:
  * 194-267).  B restarts of dimension n, history m (<= 32).  The caller fills

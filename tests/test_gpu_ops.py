@@ -31,7 +31,7 @@ def _check(op, args, grad=False):
 
 
 def test_opcheck_sobol_and_cache():
-    from botorch_amd import kernels
+    from botorch_amd import kernels, ops  # noqa: F401  (registers torch.ops.bo)
     state, shift = kernels.sobol_engine_state(5, 3)
     _check(torch.ops.bo.sobol_normal.default, (state.to(DEV), shift.to(DEV), 64, 0, False))
     m, X, Y = _model()
@@ -40,6 +40,28 @@ def test_opcheck_sobol_and_cache():
                                            1e-3, 0.0, 0))
     _check(torch.ops.bo.mll.default, (c.Xt, m.train_targets.contiguous(), c.lengthscale, 1e-3, 0.0,
                                       1.0, 0))
+
+
+@pytest.mark.parametrize("dim,seed", [(1, 0), (5, 3), (30, 1234), (96, 7), (1000, 2**31 - 1),
+                                      (4096, 99), (21201, 5)])
+def test_sobol_scramble_equals_sobol_engine(dim, seed):
+    """bo_sobol_scramble's state and shift are SobolEngine(dim, scramble=True,
+    seed)'s, bit for bit, up to the engine's largest dimension."""
+    from torch.quasirandom import SobolEngine
+    from botorch_amd import kernels
+    state, shift = kernels.sobol_engine_state(dim, seed, DEV)
+    assert state.device.type == "cuda" and shift.device.type == "cuda"
+    eng = SobolEngine(dimension=dim, scramble=True, seed=seed)
+    assert torch.equal(state.cpu(), eng.sobolstate)
+    assert torch.equal(shift.cpu(), eng.shift)
+
+
+def test_sobol_scramble_dimension_range():
+    from botorch_amd import kernels
+    with pytest.raises(ValueError, match="dimensionality"):
+        kernels.sobol_engine_state(21202, 0, DEV)
+    s1, _ = kernels.sobol_engine_state(8, None, DEV)  # unseeded: a fresh generator seed
+    assert s1.shape == (8, 30)
 
 
 def test_opcheck_chol_jitter():
