@@ -10,7 +10,8 @@ def _host(Y, maximize, dedup):
     return torch.stack([is_non_dominated(y, maximize=maximize, deduplicate=dedup) for y in Y])
 
 
-@pytest.mark.parametrize("S,n,m", [(3, 50, 2), (4, 300, 3), (2, 2100, 3), (5, 17, 8)])
+@pytest.mark.parametrize("S,n,m", [(3, 50, 2), (4, 300, 3), (2, 2100, 3), (5, 17, 8), (3, 700, 1),
+                                   (2, 513, 4), (3, 257, 5), (2, 300, 6), (2, 129, 7)])
 @pytest.mark.parametrize("maximize", [True, False])
 @pytest.mark.parametrize("dedup", [True, False])
 def test_pareto_mask_matches_host(S, n, m, maximize, dedup):
