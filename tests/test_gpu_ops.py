@@ -60,8 +60,29 @@ def test_sobol_scramble_dimension_range():
     from botorch_amd import kernels
     with pytest.raises(ValueError, match="dimensionality"):
         kernels.sobol_engine_state(21202, 0, DEV)
-    s1, _ = kernels.sobol_engine_state(8, None, DEV)  # unseeded: a fresh generator seed
-    assert s1.shape == (8, 30)
+
+
+@pytest.mark.parametrize("dim", [1, 8, 6144])
+def test_sobol_scramble_unseeded_is_a_scrambled_net(dim):
+    """seed=None draws the scramble bits on the device: the state is still a
+    scrambled Sobol sequence -- in every dimension the first 2^k points fall
+    one in each interval [i 2^-k, (i + 1) 2^-k) -- and two draws differ."""
+    import numpy as np
+    from botorch_amd import kernels
+    s1, sh1 = kernels.sobol_engine_state(dim, None, DEV)
+    s2, _ = kernels.sobol_engine_state(dim, None, DEV)
+    assert s1.shape == (dim, 30) and sh1.shape == (dim,)
+    assert dim == 1 or not torch.equal(s1, s2)
+    st, sh = s1.cpu().numpy(), sh1.cpu().numpy()
+    assert (st >= 0).all() and (st < 2**30).all() and (sh >= 0).all() and (sh < 2**30).all()
+    k = 10
+    idx = np.arange(2**k)
+    gray = idx ^ (idx >> 1)
+    for j in range(0, dim, max(1, dim // 64)):
+        u = np.full(2**k, sh[j], dtype=np.int64)
+        for b in range(k):
+            u ^= np.where((gray >> b) & 1, st[j, b], 0)
+        assert np.array_equal(np.sort(u >> (30 - k)), idx)
 
 
 def test_opcheck_chol_jitter():
