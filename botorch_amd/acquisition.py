@@ -971,17 +971,24 @@ class _FusedQEHVI(torch.autograd.Function):
         mean = torch.empty(len(models), X3.shape[0], q, **f64)
         L = torch.empty(len(models), X3.shape[0], q, q, **f64)
         # outside graph capture the finalisation launches fold their ladder
-        # outcomes straight into pinned words (no status launches or copy)
+        # outcomes straight into pinned words (no status launches or copy); on
+        # the gradient path those words are read at the end of the backward
+        # (kernels._LadderRing), else once behind the qEHVI launch
         idx = kernels._dev_index(X3.device)
-        ps = kernels.pinned_status(X3.device) if (idx not in kernels._CAPTURE and
-                                                  len(models) <= 8) else None
-        words = ps.arm(len(models)) if ps is not None else [None] * len(models)
+        pinned = idx not in kernels._CAPTURE and len(models) <= 8
+        ring = (kernels.ladder_ring(X3.device) if pinned and need_grad and not kernels.SYNC_LADDER
+                else None)
+        ps = kernels.pinned_status(X3.device) if pinned and ring is None else None
+        if ring is not None:
+            token, words = ring.take(len(models), "qEHVI posterior root")
+        else:
+            words = ps.arm(len(models)) if ps is not None else [None] * len(models)
         stats = [mm.outcome_stats() for mm in models]
         if (len(models) <= 8 and all(p_.Spart.shape == pps[0].Spart.shape for p_ in pps)
                 and all(c.kind == caches[0].kind for c in caches)):
             # every member's finalisation in one launch
             info, jit = kernels.qmc_finalize_members(caches, pps, stats, mean, L,
-                                                     status=words if ps is not None else None)
+                                                     status=words if pinned else None)
             status = [(info[t], jit[t]) for t in range(len(models))]
         else:
             for t, (cache, pp) in enumerate(zip(caches, pps)):
@@ -1002,7 +1009,11 @@ class _FusedQEHVI(torch.autograd.Function):
         # the members' ladders checked once, behind the qEHVI launch (one host
         # read per forward instead of one per member, each of which drained
         # the queue: ~40 us of idle device between members at C4)
-        if ps is not None:
+        ctx.ladder = None
+        if ring is not None:
+            ring.record(token)
+            ctx.ladder = (ring, token)
+        elif ps is not None:
             kernels.raise_not_psd_members(ps, len(models), X3.device, "qEHVI posterior root")
         else:
             kernels.raise_not_psd_many(status, "qEHVI posterior root")
@@ -1022,13 +1033,24 @@ class _FusedQEHVI(torch.autograd.Function):
             q_ = ctx.L.shape[-1]
             dcovs = kernels.chol_backward(ctx.L.reshape(-1, q_, q_),
                                           dL.reshape(-1, q_, q_)).reshape(ctx.L.shape)
-            return kernels.post_backward_jobs([
+            dX = kernels.post_backward_jobs([
                 dict(cache=cache, pp=pp, W=W, dmean=dmean[t], ystd=ystd, dcov=dcovs[t])
-                for t, (cache, pp, ystd, W) in enumerate(sv)]), None
-        for t, (cache, pp, ystd, W) in enumerate(sv):
-            dcov = kernels.chol_backward(ctx.L[t], dL[t])
-            dX = kernels.post_backward(cache, pp, W, dmean[t], dcov, ystd, dX=dX)
+                for t, (cache, pp, ystd, W) in enumerate(sv)])
+        else:
+            for t, (cache, pp, ystd, W) in enumerate(sv):
+                dcov = kernels.chol_backward(ctx.L[t], dL[t])
+                dX = kernels.post_backward(cache, pp, W, dmean[t], dcov, ystd, dX=dX)
+        _settle_ladder(ctx)
         return dX, None
+
+
+def _settle_ladder(ctx) -> None:
+    """The forward's deferred ladder outcome (kernels._LadderRing), read once
+    the backward's launches are queued behind it."""
+    lad = getattr(ctx, "ladder", None)
+    if lad is not None:
+        ctx.ladder = None
+        lad[0].settle(lad[1])
 
 
 class IdentityMCMultiOutputObjective(MCObjective):
@@ -1188,12 +1210,16 @@ class _FusedQNEHVI(torch.autograd.Function):
         F = None
         idx = kernels._dev_index(X3.device)
         # forward-only calls defer the ladder outcome (the eager qEI's ring:
-        # no stream sync per call); the gradient path reads it at once
-        # through pinned words
+        # no stream sync per call); the gradient path folds it into pinned
+        # words read at the end of the backward (kernels._LadderRing)
         defer = not need_grad and not kernels.SYNC_LADDER and idx not in kernels._CAPTURE
-        ps = (kernels.pinned_status(X3.device)
-              if (not defer and idx not in kernels._CAPTURE and M <= 8) else None)
-        words = ps.arm(M) if ps is not None else [None] * M
+        pinned = not defer and idx not in kernels._CAPTURE and M <= 8
+        ring = kernels.ladder_ring(X3.device) if pinned and not kernels.SYNC_LADDER else None
+        ps = kernels.pinned_status(X3.device) if pinned and ring is None else None
+        if ring is not None:
+            token, words = ring.take(M, "qNEHVI posterior root")
+        else:
+            words = ps.arm(M) if ps is not None else [None] * M
         stats = [mm.outcome_stats() for mm in models]
         batched = pps is not None and _roots_batched(acqf, caches, pps, stats)
         if batched:
@@ -1223,7 +1249,7 @@ class _FusedQNEHVI(torch.autograd.Function):
         if M <= 8 and same_parts and all(c.kind == caches[0].kind for c in caches):
             # every member's finalisation in one launch
             info, jit = kernels.qmc_finalize_members(
-                caches, pp_list, stats, mean, L, status=words if ps is not None else None,
+                caches, pp_list, stats, mean, L, status=words if pinned else None,
                 Ts=Ts, F=F)
             status = [(info[t], jit[t]) for t in range(M)]
         else:
@@ -1235,10 +1261,14 @@ class _FusedQNEHVI(torch.autograd.Function):
         Zq = acqf._base_samples_q(q, X3.device)
         lo, hi = acqf._cells
         acq = kernels.qehvi(mean, L, Zq, lo, hi, F=F, Qp=pp.Qp)
+        ctx.ladder = None
         if defer:
             kernels.raise_not_psd_deferred(torch.cat([i_.reshape(-1) for i_, _ in status]),
                                            torch.cat([j_.reshape(-1) for _, j_ in status]),
                                            "qNEHVI posterior root")
+        elif ring is not None:
+            ring.record(token)
+            ctx.ladder = (ring, token)
         elif ps is not None:
             kernels.raise_not_psd_members(ps, M, X3.device, "qNEHVI posterior root")
         else:
@@ -1256,11 +1286,13 @@ class _FusedQNEHVI(torch.autograd.Function):
                                                Qp=ctx.Qp)
         dX = None
         if ctx.batched and _BWD_BATCHED:
-            return _roots_backward_batched(ctx, dmean, dL, dF), None
-        for t, (cache, pp, ystd, T, W) in enumerate(ctx.saved):
-            dcov = kernels.chol_backward(ctx.L[t], dL[t])
-            dX = ctx.acqf._roots[t].backward(cache, pp, W, dmean[t], dcov, dF[t].contiguous(), T,
-                                             ystd, dX=dX)
+            dX = _roots_backward_batched(ctx, dmean, dL, dF)
+        else:
+            for t, (cache, pp, ystd, T, W) in enumerate(ctx.saved):
+                dcov = kernels.chol_backward(ctx.L[t], dL[t])
+                dX = ctx.acqf._roots[t].backward(cache, pp, W, dmean[t], dcov, dF[t].contiguous(),
+                                                 T, ystd, dX=dX)
+        _settle_ladder(ctx)
         return dX, None
 
 

@@ -1097,6 +1097,10 @@ def check_ladder_status(device=None) -> None:
         what = _LADDER_WHAT.pop(idx, "acquisition")
         if has:
             _ladder_outcome(info_max, jitter_max, what)
+    # the gradient path's outcomes whose backward has not run (_LadderRing)
+    for idx in (list(_RINGS) if device is None else [_dev_index(device)]):
+        if idx in _RINGS:
+            _RINGS[idx].settle_all()
 
 
 def _ladder_outcome(info_max: float, jitter_max: float, what: str) -> None:
@@ -1226,6 +1230,72 @@ def pinned_status(dev) -> "_PinnedStatus":
     if idx not in _PINNED:
         _PINNED[idx] = _PinnedStatus(torch.device("cuda", idx))
     return _PINNED[idx]
+
+
+class _LadderRing:
+    """Per device: a few _PinnedStatus blocks for the gradient path of the
+    ModelListGP acquisitions (qEHVI / qNEHVI).  A forward takes a block, its
+    finalisation launch folds the members' ladder outcomes into it, and an
+    event is recorded behind the forward; the outcome is read at the end of the
+    backward (``settle``: waits for that event only, once the backward's
+    launches are queued) -- not in the forward, whose stream drain kept the
+    device idle while the host issued the backward (C4 forward + backward
+    0.92-1.07 -> 0.84 ms).  A forward whose backward never runs is read when
+    its block comes round again (one ring behind) or at check_ladder_status,
+    as the eager qEI's deferred status is.  Outcomes raise / warn in member
+    order, as raise_not_psd_members."""
+
+    N = 4
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.blocks = [_PinnedStatus(dev) for _ in range(self.N)]
+        self.events = [torch.cuda.Event() for _ in range(self.N)]
+        self.pending = [None] * self.N  # (generation, members, what)
+        self.next = 0
+        self.gen = 0
+
+    def take(self, m: int, what: str):
+        """(token, per-member (status_out, status_count) pointers) of a block."""
+        i = self.next
+        self.next = (i + 1) % self.N
+        if self.pending[i] is not None:
+            self._settle_slot(i)
+        self.gen += 1
+        self.pending[i] = (self.gen, m, what)
+        return (i, self.gen), self.blocks[i].arm(m)
+
+    def record(self, token) -> None:
+        self.events[token[0]].record(torch.cuda.current_stream(self.dev))
+
+    def settle(self, token) -> None:
+        i, g = token
+        p = self.pending[i]
+        if p is not None and p[0] == g:
+            self._settle_slot(i)
+
+    def settle_all(self) -> None:
+        for k in range(self.N):  # oldest first
+            i = (self.next + k) % self.N
+            if self.pending[i] is not None:
+                self._settle_slot(i)
+
+    def _settle_slot(self, i: int) -> None:
+        _, m, what = self.pending[i]
+        self.pending[i] = None
+        self.events[i].synchronize()
+        w = self.blocks[i].words
+        raise_status_words([(w[2 * t], w[2 * t + 1]) for t in range(m)], what)
+
+
+_RINGS = {}
+
+
+def ladder_ring(dev) -> "_LadderRing":
+    idx = _dev_index(dev)
+    if idx not in _RINGS:
+        _RINGS[idx] = _LadderRing(torch.device("cuda", idx))
+    return _RINGS[idx]
 
 
 def raise_not_psd_members(ps: "_PinnedStatus", m: int, dev, what: str) -> None:

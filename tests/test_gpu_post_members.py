@@ -122,9 +122,19 @@ def test_qehvi_member_status_words(monkeypatch):
     with pytest.warns(NumericalWarning, match="1.0e-08"):
         v_native = acqf(Xd)
         kernels.check_ladder_status(X.device)
+    # the gradient path: the outcome is read at the end of the backward
+    # (kernels._LadderRing) -- within the forward + backward call -- or, for a
+    # forward whose backward never runs, at check_ladder_status
+    Xg = Xd.clone().requires_grad_(True)
     with pytest.warns(NumericalWarning, match="1.0e-08"):
-        v_grad = acqf(Xd.clone().requires_grad_(True)).detach()
-    torch.testing.assert_close(v_native, v_grad, rtol=1e-12, atol=1e-14)
+        v_grad = acqf(Xg)
+        torch.autograd.grad(v_grad.sum(), Xg)
+    torch.testing.assert_close(v_native, v_grad.detach(), rtol=1e-12, atol=1e-14)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", NumericalWarning)
+        acqf(Xd.clone().requires_grad_(True))  # not read in the forward
+    with pytest.warns(NumericalWarning, match="1.0e-08"):
+        kernels.check_ladder_status(X.device)
     # seeded words (the autograd path's pinned status pairs)
     X = X.clone().requires_grad_(True)
     orig = kernels._PinnedStatus.arm
@@ -139,13 +149,19 @@ def test_qehvi_member_status_words(monkeypatch):
     monkeypatch.setattr(kernels._PinnedStatus, "arm", arm)
     seed.update({3: 1e-6})  # member 1 added jitter
     with pytest.warns(NumericalWarning, match="1.0e-06"):
-        acqf(X)
+        torch.autograd.grad(acqf(X).sum(), X)
     seed.clear()
     seed.update({4: 1.0})  # member 2 failed
     with pytest.raises(NotPSDError):
+        torch.autograd.grad(acqf(X).sum(), X)
+    with pytest.raises(NotPSDError):  # a forward alone: at the poll
         acqf(X)
+        kernels.check_ladder_status(X.device)
     seed.clear()
-    acqf(X)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", NumericalWarning)
+        torch.autograd.grad(acqf(X).sum(), X)
+        kernels.check_ladder_status(X.device)
 
 
 def test_kxt_rows_members_bit_equal_to_per_member():
