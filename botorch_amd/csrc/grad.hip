@@ -24,6 +24,9 @@ constexpr int QMAX = 16;
 constexpr int DP = 8;
 constexpr int THREADS = 256;
 constexpr int SMAX = 256;  // samples staged in LDS per pass (winner masks + base samples)
+// row stride of the staged base samples: a lane per sample reads its own row,
+// and a 16-double (128 B) stride put the wave's 64 rows on two bank groups
+constexpr int ZST = QMAX + 1;
 
 enum { MODE_QEI = 1, MODE_QNEI = 2, MODE_QLOGEI = 4, MODE_QLOGNEI = 5 };
 
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
   __shared__ double mu[QMAX];
   __shared__ unsigned short win[SMAX];
   __shared__ double wgt[SMAX];
-  __shared__ double Zs[SMAX * QMAX];   // the chunk's base samples (shared by every t-batch)
+  __shared__ double Zs[SMAX * ZST];    // the chunk's base samples (shared by every t-batch)
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -189,11 +192,14 @@ __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
   }
   for (int s0 = 0; s0 < S; s0 += SMAX) {
     const int ns = min(SMAX, S - s0);
-    for (int e = tid; e < ns * q; e += THREADS) Zs[(e / q) * QMAX + e % q] = Z[(int64_t)s0 * q + e];
+    for (int e = tid; e < ns * q; e += THREADS) Zs[(e / q) * ZST + e % q] = Z[(int64_t)s0 * q + e];
     // Pass 1: the winning (maximal, non-clamped) q-index set per sample.
     __syncthreads();  // Zs
     for (int s = tid; s < ns; s += THREADS) {
-      const double* z = Zs + s * QMAX;
+      const double* z = Zs + s * ZST;
+      double zr[QMAX];  // the sample's row once, in registers
+#pragma unroll
+      for (int j = 0; j < QMAX; ++j) zr[j] = j < q ? z[j] : 0.0;
       const double bf = (MODE == MODE_QNEI) ? best_f_s[s0 + s] : best_f;
       double v[QMAX];
       double m = 0.0;
@@ -203,7 +209,8 @@ __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
         if (a < q) {
           double f = mu[a];
           if (MODE == MODE_QNEI) f += Fs[a];
-          for (int j = 0; j <= a; ++j) f = fma(L[a][j], z[j], f);
+#pragma unroll
+          for (int j = 0; j <= a; ++j) f = fma(L[a][j], zr[j], f);
           v[a] = f - bf;
           m = fmax(m, fmax(v[a], 0.0));
         }
@@ -233,7 +240,7 @@ __global__ __launch_bounds__(THREADS) void qmc_backward_kernel(
 #pragma unroll 8
       for (int s = 0; s < ns; ++s) {
         const double w = (win[s] >> ta & 1u) ? wgt[s] : 0.0;
-        dl_acc = fma(w, Zs[s * QMAX + tj], dl_acc);
+        dl_acc = fma(w, Zs[s * ZST + tj], dl_acc);
         dmu_acc += w;
       }
     }
@@ -268,7 +275,7 @@ __global__ __launch_bounds__(THREADS) void qmc_log_backward_kernel(
   __shared__ double Tm[QMAX][QMAX + 1];
   __shared__ double mu[QMAX];
   __shared__ double w[SL][QMAX + 1];
-  __shared__ double Zs[SL * QMAX];
+  __shared__ double Zs[SL * ZST];
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -289,10 +296,13 @@ __global__ __launch_bounds__(THREADS) void qmc_log_backward_kernel(
   }
   for (int s0 = 0; s0 < S; s0 += SL) {
     const int ns = min(SL, S - s0);
-    for (int e = tid; e < ns * q; e += THREADS) Zs[(e / q) * QMAX + e % q] = Z[(int64_t)s0 * q + e];
+    for (int e = tid; e < ns * q; e += THREADS) Zs[(e / q) * ZST + e % q] = Z[(int64_t)s0 * q + e];
     __syncthreads();
     for (int s = tid; s < ns; s += THREADS) {
-      const double* z = Zs + s * QMAX;
+      const double* z = Zs + s * ZST;
+      double zr[QMAX];
+#pragma unroll
+      for (int j = 0; j < QMAX; ++j) zr[j] = j < q ? z[j] : 0.0;
       const double bf = PERSAMPLE ? best_f_s[s0 + s] : best_f;
       const double* Fs = PERSAMPLE ? F + (int64_t)(s0 + s) * ldF + (int64_t)b * Qp : nullptr;
       double li[QMAX], dli[QMAX], gq[QMAX];
@@ -303,7 +313,8 @@ __global__ __launch_bounds__(THREADS) void qmc_log_backward_kernel(
         if (a < q) {
           double f = mu[a];
           if (PERSAMPLE) f += Fs[a];
-          for (int j = 0; j <= a; ++j) f = fma(L[a][j], z[j], f);
+#pragma unroll
+          for (int j = 0; j <= a; ++j) f = fma(L[a][j], zr[j], f);
           li[a] = log_soft_relu(f - bf, lp, &dli[a]);
         }
       }
@@ -323,7 +334,7 @@ __global__ __launch_bounds__(THREADS) void qmc_log_backward_kernel(
 #pragma unroll 8
       for (int s = 0; s < ns; ++s) {
         const double v = w[s][ta];
-        dl_acc = fma(v, Zs[s * QMAX + tj], dl_acc);
+        dl_acc = fma(v, Zs[s * ZST + tj], dl_acc);
         dmu_acc += v;
       }
     }

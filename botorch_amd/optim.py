@@ -734,6 +734,16 @@ def _eval_flops(acquisition_function, B: int, q: int):
     return total
 
 
+def _fused_qei(acquisition_function, X: torch.Tensor) -> bool:
+    """The evaluation runs the fused qEI / qLogEI forward and backward (two
+    native calls, acquisition._fused_mc)."""
+    from .acquisition import qExpectedImprovement
+    acq = acquisition_function
+    while hasattr(acq, "acq_func"):  # FixedFeatureAcquisitionFunction
+        acq = acq.acq_func
+    return isinstance(acq, qExpectedImprovement) and bool(acq._fused_eligible(X))
+
+
 def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds=None,
                           upper_bounds=None, inequality_constraints=None,
                           equality_constraints=None, nonlinear_inequality_constraints=None,
@@ -758,9 +768,11 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
     One evaluation = one batched forward + backward of the acquisition at all
     trial points + one step launch; iterates, gradients and histories never
     leave HBM and the host reads the status vector every ``check_every``
-    evaluations.  ``use_graph`` (default True): the evaluation is captured once
-    as a HIP graph and replayed (botorch_amd.graphs) where the acquisition
-    allows capture.  ``compact`` (L-BFGS-B; True, False or "auto", the
+    evaluations.  ``use_graph`` (True, False or "auto", the default): the
+    evaluation is captured once as a HIP graph and replayed
+    (botorch_amd.graphs) where the acquisition allows capture; "auto" keeps
+    the fused qEI / qLogEI evaluation eager (a replay saves it no host work and
+    is slower on the device).  ``compact`` (L-BFGS-B; True, False or "auto", the
     default): at a status read where at most half of the batch is still
     running (and at least ``compact_min`` restarts have stopped), the running
     restarts continue as a smaller batch (their states gathered; the graph
@@ -831,9 +843,16 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
           else torch.full((st.n,), math.inf, dtype=torch.float64, device=X0.device))
     stream = kernels._stream(X0.device)
     # one evaluation (forward + backward at all trial points) as a HIP graph
-    # replay where the acquisition allows capture (the fused qEI / qLogEI
-    # paths); the eager autograd evaluation otherwise
-    use_graph = bool(options.get("use_graph", True))
+    # replay where the acquisition allows capture; the eager autograd
+    # evaluation otherwise.  "auto" (default): eager for the fused qEI /
+    # qLogEI evaluation -- one native call per forward and per backward, so a
+    # replay saves no host work: measured inside optimize_acqf, C2 eager 6.6
+    # against 7.0 ms with the capture, and at C3 a replay is slower than the
+    # eager call (0.29 against 0.27 ms at b = 2, 1.49 against 1.38 ms at
+    # b = 128; tools/c2_opt_graph.py, tools/capture_cost.py) -- and a
+    # captured graph for the other routes
+    ug = options.get("use_graph", "auto")
+    use_graph = not _fused_qei(acquisition_function, X0) if ug == "auto" else bool(ug)
     compact = options.get("compact", "auto") if lbfgsb and not joint else False
     compact_min = int(options.get("compact_min", 8))
     # after a shrink the evaluation graph is re-captured only once the smaller

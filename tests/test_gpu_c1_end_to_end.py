@@ -202,6 +202,7 @@ def test_fixed_features_on_device(gen):
     with warnings.catch_warnings(record=True) as ws:
         warnings.simplefilter("always")
         c, v = optimize_acqf(acqf, bounds, q=2, num_restarts=6, raw_samples=64,
+                             options={"use_graph": True} if gen == "device" else None,
                              fixed_features={1: 0.25, 4: 0.5}, gen_candidates=g)
     assert not any("Graph is empty" in str(w.message) for w in ws)
     assert torch.all(c[:, 1] == 0.25) and torch.all(c[:, 4] == 0.5)

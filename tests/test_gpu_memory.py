@@ -87,7 +87,7 @@ def test_gen_candidates_device_graphed_memory_and_no_stream_warning():
     hi = torch.ones(6, dtype=torch.float64, device=DEV)
     with warnings.catch_warnings(record=True) as ws:
         warnings.simplefilter("always")
-        c, v = gen_candidates_device(ics, acqf, lo, hi, options={"maxiter": 30})
+        c, v = gen_candidates_device(ics, acqf, lo, hi, options={"maxiter": 30, "use_graph": True})
         assert gen_candidates_device.last_graphed_evals > 0, gen_candidates_device.last_graph_error
         del c, v
         torch.cuda.synchronize()
@@ -98,7 +98,8 @@ def test_gen_candidates_device_graphed_memory_and_no_stream_warning():
             gen_candidates_device.last_state = None
             seen = [torch.cuda.memory_allocated()]
             for _ in range(4):
-                c, v = gen_candidates_device(ics, acqf, lo, hi, options={"maxiter": 30})
+                c, v = gen_candidates_device(ics, acqf, lo, hi,
+                                             options={"maxiter": 30, "use_graph": True})
                 assert gen_candidates_device.last_graphed_evals > 0
                 del c, v
                 gen_candidates_device.last_state = None
