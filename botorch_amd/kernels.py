@@ -779,6 +779,16 @@ def qmc_finalize_members(caches, pps, stats, mean: torch.Tensor, L: torch.Tensor
 
 
 SOBOL_MAXBIT = 30  # torch.quasirandom.SobolEngine.MAXBIT
+_UNSEEDED = {}
+
+
+def _unseeded_generator(dev: torch.device) -> torch.Generator:
+    """A device generator per device, seeded non-deterministically once."""
+    if dev not in _UNSEEDED:
+        g = torch.Generator(device=dev)
+        g.seed()
+        _UNSEEDED[dev] = g
+    return _UNSEEDED[dev]
 
 
 @functools.lru_cache(maxsize=16)
@@ -816,9 +826,12 @@ def sobol_engine_state(dim: int, seed: Optional[int], device=None):
     if seed is None:
         # unseeded, the engine scrambles from a freshly seeded generator
         # (g.seed()): any source of independent fair bits is the same draw in
-        # distribution, so they come from the device generator (no host draw,
-        # no copy: ~5 ms at the dim 6144 of the C4 baseline pruning)
-        bits = torch.randint(2, (nb * (1 + SOBOL_MAXBIT),), dtype=torch.uint8, device=dev)
+        # distribution, so they come from a device generator (no host draw,
+        # no copy: ~5 ms at the dim 6144 of the C4 baseline pruning) -- a
+        # private one, seeded from the OS like g.seed(), so the caller's global
+        # CUDA random stream is left where it was, as the reference leaves it
+        bits = torch.randint(2, (nb * (1 + SOBOL_MAXBIT),), dtype=torch.uint8, device=dev,
+                             generator=_unseeded_generator(dev))
     else:
         g = torch.Generator()
         g.manual_seed(seed)

@@ -69,8 +69,10 @@ def test_sobol_scramble_unseeded_is_a_scrambled_net(dim):
     one in each interval [i 2^-k, (i + 1) 2^-k) -- and two draws differ."""
     import numpy as np
     from botorch_amd import kernels
+    rng = torch.cuda.get_rng_state()
     s1, sh1 = kernels.sobol_engine_state(dim, None, DEV)
     s2, _ = kernels.sobol_engine_state(dim, None, DEV)
+    assert torch.equal(torch.cuda.get_rng_state(), rng)  # the global CUDA stream untouched
     assert s1.shape == (dim, 30) and sh1.shape == (dim,)
     assert dim == 1 or not torch.equal(s1, s2)
     st, sh = s1.cpu().numpy(), sh1.cpu().numpy()
