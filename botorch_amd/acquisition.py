@@ -1141,9 +1141,12 @@ def prune_inferior_points_multi_objective(model, X, ref_point, objective=None, c
     n, m = X.shape[-2], len(models)
     with torch.no_grad():
         # joint samples of the independent outputs: Sobol dimension n m,
-        # point-major / output-minor base samples (get_sampler on the MTMVN)
+        # point-major / output-minor base samples (get_sampler on the MTMVN),
+        # seeded as the reference's sampler seeds itself from the global
+        # generator (sampling/base.py: torch.randint(0, 1000000, (1,)))
         if n * m <= 21201:
-            Z = kernels.sobol_normal(n * m, num_samples, None, X.device).view(num_samples, n, m)
+            seed = int(torch.randint(0, 1000000, (1,)).item())
+            Z = kernels.sobol_normal(n * m, num_samples, seed, X.device).view(num_samples, n, m)
         else:
             Z = torch.randn(num_samples, n, m, dtype=torch.float64, device=X.device)
         cols = []

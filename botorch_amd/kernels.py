@@ -779,16 +779,6 @@ def qmc_finalize_members(caches, pps, stats, mean: torch.Tensor, L: torch.Tensor
 
 
 SOBOL_MAXBIT = 30  # torch.quasirandom.SobolEngine.MAXBIT
-_UNSEEDED = {}
-
-
-def _unseeded_generator(dev: torch.device) -> torch.Generator:
-    """A device generator per device, seeded non-deterministically once."""
-    if dev not in _UNSEEDED:
-        g = torch.Generator(device=dev)
-        g.seed()
-        _UNSEEDED[dev] = g
-    return _UNSEEDED[dev]
 
 
 @functools.lru_cache(maxsize=16)
@@ -811,8 +801,8 @@ def sobol_engine_state(dim: int, seed: Optional[int], device=None):
     with the unscrambled direction numbers cached on the device.  Bit-identical
     to SobolEngine(dim, scramble=True, seed) (tests/test_gpu_ops.py); the
     engine itself spends ~30 ms of host time at dim 4096 (the baseline pruning
-    of every qNEI / qNEHVI construction).  seed=None: the bits come from the
-    device generator (see below)."""
+    of every qNEI / qNEHVI construction).  seed=None: the global CPU
+    generator's draws, as the engine's."""
     if device is None or torch.device(device).type != "cuda":
         eng = SobolEngine(dimension=dim, scramble=True, seed=seed)
         return eng.sobolstate.clone(), eng.shift.clone()
@@ -823,24 +813,19 @@ def sobol_engine_state(dim: int, seed: Optional[int], device=None):
     if dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
     nb = dim * SOBOL_MAXBIT
-    if seed is None:
-        # unseeded, the engine scrambles from a freshly seeded generator
-        # (g.seed()): any source of independent fair bits is the same draw in
-        # distribution, so they come from a device generator (no host draw,
-        # no copy: ~5 ms at the dim 6144 of the C4 baseline pruning) -- a
-        # private one, seeded from the OS like g.seed(), so the caller's global
-        # CUDA random stream is left where it was, as the reference leaves it
-        bits = torch.randint(2, (nb * (1 + SOBOL_MAXBIT),), dtype=torch.uint8, device=dev,
-                             generator=_unseeded_generator(dev))
-    else:
+    # unseeded, the engine draws from torch's global CPU generator (as
+    # SobolEngine._scramble does with seed=None): the same stream, consumed
+    # by the same amount, so later global draws see the reference's state
+    g = None
+    if seed is not None:
         g = torch.Generator()
         g.manual_seed(seed)
-        host = torch.empty(nb * (1 + SOBOL_MAXBIT), dtype=torch.uint8, pin_memory=True)
-        torch.randint(2, (dim, SOBOL_MAXBIT), generator=g, dtype=torch.uint8,
-                      out=host[:nb].view(dim, SOBOL_MAXBIT))
-        torch.randint(2, (dim, SOBOL_MAXBIT, SOBOL_MAXBIT), generator=g, dtype=torch.uint8,
-                      out=host[nb:].view(dim, SOBOL_MAXBIT, SOBOL_MAXBIT))
-        bits = host.to(dev, non_blocking=True)
+    host = torch.empty(nb * (1 + SOBOL_MAXBIT), dtype=torch.uint8, pin_memory=True)
+    torch.randint(2, (dim, SOBOL_MAXBIT), generator=g, dtype=torch.uint8,
+                  out=host[:nb].view(dim, SOBOL_MAXBIT))
+    torch.randint(2, (dim, SOBOL_MAXBIT, SOBOL_MAXBIT), generator=g, dtype=torch.uint8,
+                  out=host[nb:].view(dim, SOBOL_MAXBIT, SOBOL_MAXBIT))
+    bits = host.to(dev, non_blocking=True)
     state0 = _sobol_state0(dim, dev)
     state = torch.empty(dim, SOBOL_MAXBIT, dtype=torch.long, device=dev)
     shift = torch.empty(dim, dtype=torch.long, device=dev)

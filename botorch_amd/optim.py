@@ -972,8 +972,17 @@ def gen_candidates_device(initial_conditions, acquisition_function, lower_bounds
         shapeX = X0.shape
     cands = st.x.view(shapeX).to(initial_conditions.dtype)
     cands = columnwise_clamp(cands, lower_bounds, upper_bounds)
-    with torch.no_grad():
-        acq = acquisition_function(cands)
+    # every restart converged (status 1 / 2): each x is an accepted iterate,
+    # inside the box, and the state holds its objective f = -acq(x) from the
+    # evaluation that accepted it -- the values gen_candidates_scipy computes
+    # by evaluating the candidates once more (gen.py:292-296), without that
+    # forward (C3: 0.71 ms at b = 128).  Joint runs (f is the batch sum) and
+    # any other stop evaluate the candidates.
+    if lbfgsb and not joint and bool(((st.status == 1) | (st.status == 2)).all()):
+        acq = (-st.f).to(cands.dtype).reshape(shapeX[:-2])
+    else:
+        with torch.no_grad():
+            acq = acquisition_function(cands)
     if lbfgsb:
         bad = (st.status == 3) | (st.status == 6)
         if bool(bad.any()):

@@ -123,6 +123,24 @@ def test_gen_candidates_device_b1_equals_scipy():
         torch.testing.assert_close(vd, vs, atol=1e-10, rtol=1e-8)
 
 
+@pytest.mark.parametrize("opts", [{}, {"compact": True, "compact_min": 1}, {"maxiter": 2}])
+def test_gen_candidates_device_values_are_the_candidates_values(opts):
+    """Converged restarts return -f from their L-BFGS-B state instead of a
+    final forward: equal to the acquisition at the returned candidates (also
+    after compaction, whose evaluations sum in another order); a run that
+    stops on maxiter evaluates the candidates."""
+    from botorch_amd.optim import gen_candidates_device
+    acqf, bounds, ics = _qei_setup()
+    cd, vd = gen_candidates_device(ics, acqf, bounds[0], bounds[1], options=opts)
+    st = gen_candidates_device.last_state
+    converged = set(st.status.cpu().tolist()) <= {1, 2}
+    assert converged == ("maxiter" not in opts)
+    with torch.no_grad():
+        ve = acqf(cd)
+    assert vd.shape == ve.shape and vd.dtype == ve.dtype
+    torch.testing.assert_close(vd, ve, rtol=1e-10, atol=1e-13)
+
+
 def test_gen_candidates_device_restarts_equal_scipy_per_restart():
     from botorch_amd.optim import gen_candidates_device, gen_candidates_scipy
     acqf, bounds, ics = _qei_setup()

@@ -64,15 +64,22 @@ def test_sobol_scramble_dimension_range():
 
 @pytest.mark.parametrize("dim", [1, 8, 6144])
 def test_sobol_scramble_unseeded_is_a_scrambled_net(dim):
-    """seed=None draws the scramble bits on the device: the state is still a
-    scrambled Sobol sequence -- in every dimension the first 2^k points fall
-    one in each interval [i 2^-k, (i + 1) 2^-k) -- and two draws differ."""
+    """seed=None: the engine's draws from the global CPU generator -- the
+    state equals SobolEngine(dim, scramble=True) after the same manual_seed,
+    and the global stream is left where the engine leaves it -- and the state
+    is a scrambled Sobol sequence: in every dimension the first 2^k points
+    fall one in each interval [i 2^-k, (i + 1) 2^-k); two draws differ."""
     import numpy as np
+    from torch.quasirandom import SobolEngine
     from botorch_amd import kernels
-    rng = torch.cuda.get_rng_state()
+    torch.manual_seed(123)
     s1, sh1 = kernels.sobol_engine_state(dim, None, DEV)
+    after = torch.rand(3)
+    torch.manual_seed(123)
+    eng = SobolEngine(dimension=dim, scramble=True)
+    assert torch.equal(s1.cpu(), eng.sobolstate) and torch.equal(sh1.cpu(), eng.shift)
+    assert torch.equal(torch.rand(3), after)
     s2, _ = kernels.sobol_engine_state(dim, None, DEV)
-    assert torch.equal(torch.cuda.get_rng_state(), rng)  # the global CUDA stream untouched
     assert s1.shape == (dim, 30) and sh1.shape == (dim,)
     assert dim == 1 or not torch.equal(s1, s2)
     st, sh = s1.cpu().numpy(), sh1.cpu().numpy()
