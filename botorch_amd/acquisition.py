@@ -1488,7 +1488,12 @@ class qNoisyExpectedHypervolumeImprovement(qExpectedHypervolumeImprovement):
         self._X_baseline = X_baseline
         self._X_baseline_and_pending = X_baseline
         self._partitioned = False
-        self.register_buffer("_prev_nehvi", torch.tensor(0.0, dtype=torch.float64))
+        # on the baseline's device, as the reference's tkwargs buffer
+        # (hypervolume.py:619-622): a host scalar here made every forward's
+        # ``+ prev_nehvi`` a pageable copy that drained the stream (C4
+        # qNEHVI forward + backward: ~150 us of idle device per call)
+        self.register_buffer("_prev_nehvi", torch.tensor(0.0, dtype=torch.float64,
+                                                         device=X_baseline.device))
         if X_pending is not None:
             self.set_X_pending(X_pending)
         # hypervolume.py:643-644: the first decomposition, unless set_X_pending
