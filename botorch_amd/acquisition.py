@@ -210,6 +210,21 @@ def _fused_mc(X3: torch.Tensor, acqf, mode: int, best_f: float, best_f_s, Z: tor
     kernels.raise_not_psd_deferred(info, jit, type(acqf).__name__)
     return acq
 
+def _host_scalar(module, name: str) -> float:
+    """float(module.<name>) read once per value: a best_f on the device (the
+    usual ``best_f=train_Y.max()``) would otherwise be a device-to-host read,
+    i.e. a stream drain, in every forward.  Keyed on the tensor's storage and
+    version counter, so an in-place change or a new tensor is read again."""
+    t = getattr(module, name)
+    key = (t.data_ptr(), t._version, t.device)
+    cache = module.__dict__.setdefault("_host_scalars", {})
+    hit = cache.get(name)
+    if hit is None or hit[0] != key:
+        hit = (key, float(t))
+        cache[name] = hit
+    return hit[1]
+
+
 def _ensemble_mean(model, acq: torch.Tensor) -> torch.Tensor:
     """Average over the MCMC batch of ensemble models (utils/transforms.py:289-293)."""
     return acq.mean(dim=-1) if getattr(model, "_is_ensemble", False) else acq
@@ -238,7 +253,7 @@ class qExpectedImprovement(MCAcquisitionFunction):
         if self._fused_eligible(X) and self.best_f.numel() == 1:
             sampler = self._ensure_sampler()
             Z = sampler.base_samples_2d(q, X.device)
-            acq = _fused_mc(X3, self, _lib.QMC_QEI, float(self.best_f), None, Z)
+            acq = _fused_mc(X3, self, _lib.QMC_QEI, _host_scalar(self, "best_f"), None, Z)
             return acq.reshape(batch)
         if (getattr(self.model, "_is_fully_bayesian", False) and X.is_cuda and not self._log
                 and type(self.objective) is IdentityMCObjective and self.posterior_transform is None
@@ -246,7 +261,7 @@ class qExpectedImprovement(MCAcquisitionFunction):
                 and self.best_f.numel() == 1 and q <= FUSED_QMAX):
             sampler = self._ensure_sampler()
             Z = sampler.base_samples_2d(q, X.device)
-            return _SaasQEI.apply(X3, self, float(self.best_f), Z).reshape(batch)
+            return _SaasQEI.apply(X3, self, _host_scalar(self, "best_f"), Z).reshape(batch)
         return self._generic_forward(X)
 
 
@@ -857,8 +872,8 @@ class qLogExpectedImprovement(qExpectedImprovement):
         if self._fused_eligible(X) and self.best_f.numel() == 1:
             sampler = self._ensure_sampler()
             Z = sampler.base_samples_2d(q, X.device)
-            acq = _fused_mc(X.reshape(-1, q, d), self, _lib.QMC_QLOGEI, float(self.best_f),
-                                 None, Z)
+            acq = _fused_mc(X.reshape(-1, q, d), self, _lib.QMC_QLOGEI,
+                            _host_scalar(self, "best_f"), None, Z)
             return acq.reshape(batch)
         return self._generic_forward(X)
 
