@@ -141,6 +141,26 @@ def test_gen_candidates_device_values_are_the_candidates_values(opts):
     torch.testing.assert_close(vd, ve, rtol=1e-10, atol=1e-13)
 
 
+def test_gen_candidates_device_early_checks_same_result():
+    """The early status reads (after evaluations 1 and 2 where the batch can
+    shrink) move the shrink earlier, not the result: the same candidates and
+    values as reading every 4 evaluations, to the rounding of the smaller
+    batch's evaluation order."""
+    from botorch_amd.optim import gen_candidates_device
+    acqf, bounds, ics = _qei_setup()
+    opts = {"compact": True, "compact_min": 1}
+    c1, v1 = gen_candidates_device(ics, acqf, bounds[0], bounds[1], options=opts)
+    s1 = list(gen_candidates_device.last_shrinks)
+    c0, v0 = gen_candidates_device(ics, acqf, bounds[0], bounds[1],
+                                   options={**opts, "early_checks": False})
+    s0 = list(gen_candidates_device.last_shrinks)
+    assert all(e % 4 == 0 for e, _ in s0)
+    if s1:
+        assert s1[0][0] <= (s0[0][0] if s0 else 4)
+    torch.testing.assert_close(c1, c0, atol=1e-9, rtol=0)
+    torch.testing.assert_close(v1, v0, atol=1e-12, rtol=1e-9)
+
+
 def test_gen_candidates_device_restarts_equal_scipy_per_restart():
     from botorch_amd.optim import gen_candidates_device, gen_candidates_scipy
     acqf, bounds, ics = _qei_setup()
