@@ -213,16 +213,16 @@ def _fused_mc(X3: torch.Tensor, acqf, mode: int, best_f: float, best_f_s, Z: tor
 def _host_scalar(module, name: str) -> float:
     """float(module.<name>) read once per value: a best_f on the device (the
     usual ``best_f=train_Y.max()``) would otherwise be a device-to-host read,
-    i.e. a stream drain, in every forward.  Keyed on the tensor's storage and
-    version counter, so an in-place change or a new tensor is read again."""
+    i.e. a stream drain, in every forward.  The cache holds the tensor itself
+    (so a replacement can never reuse its identity) and its version counter:
+    a new tensor or an in-place change is read again."""
     t = getattr(module, name)
-    key = (t.data_ptr(), t._version, t.device)
     cache = module.__dict__.setdefault("_host_scalars", {})
     hit = cache.get(name)
-    if hit is None or hit[0] != key:
-        hit = (key, float(t))
+    if hit is None or hit[0] is not t or hit[1] != t._version:
+        hit = (t, t._version, float(t))
         cache[name] = hit
-    return hit[1]
+    return hit[2]
 
 
 def _ensemble_mean(model, acq: torch.Tensor) -> torch.Tensor:
