@@ -66,6 +66,36 @@ def prune_inferior_points(model: ExactGPOracle, X, num_samples=2048, seed=0, max
     return X[idcs]
 
 
+def prune_inferior_points_multi_objective(models, X, ref_point, num_samples=2048, seed=0,
+                                          max_frac=1.0):
+    """acquisition/multi_objective/utils.py:77-161 (unconstrained, identity
+    objective; the sampler seed -- the reference's SobolQMCNormalSampler draws
+    it with torch.randint(0, 1000000, (1,)) -- made explicit): joint samples of
+    the independent outputs from the point-major / output-minor base samples
+    (Sobol dim n m), a point kept when it is Pareto-optimal (pareto.py:16-64,
+    deduplicate=False) and better than ref_point in every objective in any
+    sample."""
+    from .sampling import base_samples_multi_output
+    n, m = X.shape[-2], len(models)
+    Z = base_samples_multi_output(num_samples, n, m, seed)  # S x m x n
+    cols = []
+    for t, mod in enumerate(models):
+        mean, cov = mod.posterior(X)
+        cols.append(mc_samples(mean, cov, Z[:, t]))  # S x n
+    obj = torch.stack(cols, dim=-1)  # S x n x m
+    # dominated[s, a] = some b with obj[s, b] >= obj[s, a] everywhere and > somewhere
+    Ya, Yb = obj.unsqueeze(-2), obj.unsqueeze(-3)  # [s, a, 1, m], [s, 1, b, m]
+    dominates = (Yb >= Ya).all(dim=-1) & (Yb > Ya).any(dim=-1)  # [s, a, b]
+    mask = ~dominates.any(dim=-1) & (obj > torch.as_tensor(ref_point, dtype=obj.dtype)).all(dim=-1)
+    probs = mask.to(obj.dtype).mean(dim=0)
+    idcs = probs.nonzero().view(-1)
+    max_points = math.ceil(max_frac * n)
+    if idcs.shape[0] > max_points:
+        _, order = torch.sort(probs, descending=True)
+        idcs = order[:max_points]
+    return X[idcs]
+
+
 class QNEIOracle:
     """qNoisyExpectedImprovement with cache_root=True (acquisition/monte_carlo.py:
     441-625, cached_cholesky.py:94-186, utils/low_rank.py:85-173,
