@@ -98,6 +98,23 @@ def test_device_sobol_box_matches_reference(golden, n, q, d, seed):
                                draw_sobol_samples(b2, n, q, seed=seed), rtol=0, atol=0)
 
 
+def test_device_sobol_box_unseeded_matches_reference():
+    """seed=None (gen_batch_initial_conditions without options['seed']): the
+    device raw designs equal draw_sobol_samples(seed=None), whose engine draws
+    its scramble from the global CPU generator, under the same manual_seed,
+    and leave that generator where the reference leaves it."""
+    from oracle.sampling import draw_sobol_samples as oracle_draw
+    from botorch_amd import kernels
+    lo, hi = torch.full((6,), -1.0, dtype=torch.float64), torch.full((6,), 2.0, dtype=torch.float64)
+    torch.manual_seed(11)
+    x = kernels.sobol_box(torch.stack([lo, hi]).to(DEV), 40, 4, None).cpu()
+    after = torch.rand(2)
+    torch.manual_seed(11)
+    ref = oracle_draw(lo, hi, 40, 4, None)
+    assert torch.equal(torch.rand(2), after)
+    torch.testing.assert_close(x, ref, rtol=0, atol=0)
+
+
 def test_gen_batch_initial_conditions_on_device():
     """Raw designs, their forward-only values and the Boltzmann selection stay
     on the device; the picks are raw designs and include the best one."""
